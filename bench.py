@@ -1,0 +1,211 @@
+"""bench.py -- SWASA dE cost evaluation throughput on MI355X.
+
+Metric (BASELINE.json): Mpixel*evals/s of the SWASA dE cost at 4096x4096, K=256.
+A "step" is one SWASA iteration of the native search (IM:497-568): neighbour
+generation for P palettes, evaluation of the P candidate costs on the GPU
+(palette prep + exact grid, argmin, S-CIELAB stencil + dE76, fixed-order fp64
+reduction), the RCCL all-reduce of the partial costs when N > 1, and the
+acceptance step.  value = W*H*P*steps / max-over-ranks wall time (strong
+scaling: the 4096^2 image is row-block sharded over the N GPUs).
+
+Run: python bench.py [--gpus N] [--steps K] [--warmup W]; N > 1 under
+torch.distributed.run (one process per GPU; RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*).
+"""
+
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_PEAK_TFLOPS = 157.3    # vector FP32 spec
+
+
+def synthetic_planes(w, h, seed=1):
+    """SplitMix64 u8 per channel -> u8/255.0f; same as oracle.synthetic_image."""
+    with np.errstate(over="ignore"):
+        i = np.arange(1, w * h + 1, dtype=np.uint64)
+        z = np.uint64(seed) + i * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    s = np.float32(255.0)
+    return [((z >> np.uint64(8 * c)) & np.uint64(0xFF)).astype(np.float32) / s for c in range(3)]
+
+
+def cpu_baseline(args):
+    """Oracle (C restatement, 'port') on this host's cores over a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import c_oracle  # checker/baseline only
+    import oracle as o
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    w = h = args.cpu_size
+    R, G, B = o.synthetic_image(w, h, seed=1)
+    rgba = o.inline_rgba(R, G, B)
+    f = o.design_filters()
+    lab = c_oracle.srgb_to_scielab(R, G, B, f, w)
+    evals = 0
+    t0 = time.perf_counter()
+    while True:
+        pal = o.synthetic_palette(args.K, 2 + evals)
+        c_oracle.eval_palette(rgba, lab, pal, f, w, nthreads=threads)
+        evals += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds or evals >= 64:
+            break
+    return {"value": w * h * evals / el / 1e6, "unit": "Mpixel*evals/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{w}x{h} image, K={args.K}, {evals} candidate evaluations "
+                      f"(C restatement oracle/hq_oracle.c, {threads} threads, {el:.1f} s)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--size", type=int, default=4096)
+    ap.add_argument("--K", type=int, default=256)
+    ap.add_argument("--population", type=int, default=4)
+    ap.add_argument("--grid", type=int, default=64)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-size", type=int, default=1024)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("gloo")  # control plane only; data path is libhq's RCCL comm
+
+    import hybridquantization_amd as hq
+    from hybridquantization_amd import _lib
+
+    lib = hq.load()
+    W = H = args.size
+    m = hq.ImageManipulation(hq.deltaETypes.CIE76, device=local)
+    if not m.getOpenCLAvailable():
+        raise RuntimeError("bench.py: libhq could not open the GPU")
+    sp = hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
+    m.setOption("grid", args.grid)
+    R, G, B = synthetic_planes(W, H, seed=args.seed)
+    r0 = rank * H // world
+    r1 = (rank + 1) * H // world
+    _lib.check(lib.hq_set_image_planar_shard(m.ctx, _lib.fptr(R), _lib.fptr(G), _lib.fptr(B), W, H,
+                                             _lib.fptr(sp.illuminant), r0, r1), m.ctx)
+    del R, G, B
+    if world > 1:
+        import torch
+
+        uid = torch.zeros(128, dtype=torch.uint8)
+        if rank == 0:
+            uid = torch.frombuffer(bytearray(hq.ImageManipulation.commUniqueId()), dtype=torch.uint8)
+        dist.broadcast(uid, 0)
+        m.initComm(world, rank, bytes(uid.numpy().tobytes()))
+
+    sw = hq.SWASA(population=args.population, imax=10 ** 9, seed=args.seed)
+    params = sw.params()
+    search = C.c_void_p()
+    _lib.check(lib.hq_search_create(m.ctx, C.byref(params), args.K, sw.seed, C.byref(search)), m.ctx)
+    ran = C.c_int()
+    _lib.check(lib.hq_search_run(search, args.warmup, C.byref(ran)), m.ctx)
+
+    def sync_all():
+        if world > 1:
+            import torch
+
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    lib.hq_profile_reset(m.ctx)
+    lib.hq_profile_enable(m.ctx, 1)
+    sync_all()
+    t0 = time.perf_counter()
+    _lib.check(lib.hq_search_run(search, args.steps, C.byref(ran)), m.ctx)
+    sync_all()
+    elapsed = time.perf_counter() - t0
+    lib.hq_profile_enable(m.ctx, 0)
+    if world > 1:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    prof = {}
+    for k in ("grid", "assign", "cost", "finalize"):
+        ms = C.c_double()
+        n = C.c_int64()
+        lib.hq_profile_get(m.ctx, k.encode(), C.byref(ms), C.byref(n))
+        prof[k] = (ms.value / max(n.value, 1), n.value)
+    best = np.zeros(4 * args.K, np.float32)
+    berr = C.c_double()
+    it = C.c_int()
+    lib.hq_search_best(search, _lib.fptr(best), C.byref(berr), C.byref(it))
+    lib.hq_search_destroy(search)
+
+    P = args.population
+    n_own = W * (r1 - r0)
+    value = W * H * P * args.steps / elapsed / 1e6
+    # Dominant kernel: cost_tile (S-CIELAB stencil + Lab + dE).  Algorithmic
+    # bytes per launch = LabRef fp32x3 once per pixel + the u8 index image of
+    # each of the P palettes (DESIGN.md "Roofline accounting").
+    cost_ms = prof["cost"][0]
+    alg_bytes = n_own * (12 + P)
+    achieved = alg_bytes / (cost_ms * 1e-3) / 1e9 if cost_ms > 0 else 0.0
+    # whole-evaluation view: the metric's 24 B/px-eval HBM roofline
+    eval_roof_mpx = HBM_PEAK_GBS * 1e9 / 24.0 / 1e6 * args.gpus
+    out = {
+        "metric": "Mpixel*evals/s (SWASA dE cost) at 4096x4096 K=256",
+        "value": round(value, 2),
+        "unit": "Mpixel*evals/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (SplitMix64 u8 RGB image, java.util.Random-seeded SWASA palettes)",
+        "config": {"workload": f"SWASA search iteration, {W}x{H} RGB image, K={args.K}, "
+                               f"population P={P} palettes per step (BASELINE config 3)",
+                   "image": f"{W}x{H}", "K": args.K, "population": P,
+                   "parallelism": f"row-block x{world} + RCCL all-reduce" if world > 1 else "1 GPU",
+                   "argmin_grid": args.grid},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "cost_tile_kernel", "kernel_avg_ms": round(cost_ms, 4),
+                     "alg_bytes_per_launch": alg_bytes},
+        "metric_hbm_roofline_frac": round(value / eval_roof_mpx, 4),
+        "kernel_avg_ms": {k: round(v[0], 4) for k, v in prof.items()},
+        "best_error": berr.value,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args)
+    m.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,118 @@
+// hq_internal.h -- structs shared by the HIP kernels (hq_kernels.hip) and the
+// host runtime (hq_runtime.hip).  Not part of the public ABI (include/hq.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hq {
+
+constexpr int kMaxK = 256;        // u8 palette indices (K <= 256 on this path)
+constexpr int kMaxTaps = 255;     // generic path limit (2*half+1)
+constexpr int kNumFilt = 7;       // separable filter pairs of the S-CIELAB stencil
+constexpr int kL1Cap = 31;        // level-1 candidate list capacity (32-B entry)
+constexpr int kL2Cap = 15;        // level-2 candidate list capacity (16-B entry)
+constexpr uint8_t kOverflow = 255;
+
+// The 7 separable (vertical, horizontal) filter pairs of the candidate stencil,
+// CL:234-306 restated: channel 0 = k1.x (x) k1.x + k2.x (x) k2.x + |k3| (x) k3,
+// channel 1 = k1.y (x) k1.y + k2.y (x) k2.y, channel 2 = k1.z (x) k1.z + k2.z (x) k2.z
+// (vertical kernel first).  Filter f feeds opponent channel kFiltChan[f].
+__host__ __device__ constexpr int filt_chan(int f) { return f < 3 ? 0 : (f < 5 ? 1 : 2); }
+
+template <int T>
+struct TapTable {
+    float v[kNumFilt][T];  // vertical taps per filter
+    float h[kNumFilt][T];  // horizontal taps per filter
+};
+
+// Geometry of one (possibly sharded) image on a device.
+struct Geom {
+    int W, H;        // full image
+    int r0, r1;      // owned rows [r0, r1)
+    int e0, e1;      // extended rows held on device [e0, e1) (owned +- half, clipped)
+    int lab_pitch;   // floats per row of the planar LabRef (multiple of 4)
+    int64_t n_ext;   // W * (e1 - e0)
+    int64_t idx_pitch;  // bytes per palette in the index buffer (>= n_ext, multiple of 256)
+};
+
+struct PaletteArgs {
+    const float4* pal_in;   // [P][K] host-uploaded palettes
+    float4* pal;            // [P][256] sanitised colours (.w = 0)
+    float4* opp;            // [P][256] opponent colour of each palette entry (CL:194-198)
+    uint8_t* dup;           // [P][256] 1 if an identical colour exists at a lower index
+    int* pflags;            // [P] bit0: non-finite colour present -> exhaustive argmin
+    int K;
+};
+
+struct GridArgs {
+    const float4* pal;
+    const uint8_t* dup;
+    const int* pflags;
+    uint8_t* lvl1;          // [P][G1^3][32]
+    uint8_t* lvl2;          // [P][G2^3][16]
+    int K;
+    int G1;                 // level-1 resolution (G2 / 4)
+    int64_t lvl1_pitch, lvl2_pitch;  // bytes per palette
+};
+
+struct AssignArgs {
+    const float* R;         // planar, n_ext floats (extended rows)
+    const float* G;
+    const float* B;
+    const float4* pal;      // [P][256]
+    const int* pflags;
+    const uint8_t* lvl1;
+    const uint8_t* lvl2;
+    uint8_t* idx;           // [P][idx_pitch]
+    uint32_t* used_mask;    // [P][nblocks][8]
+    int64_t n_ext;
+    int64_t idx_pitch;
+    int64_t lvl1_pitch, lvl2_pitch;
+    int K;
+    int G2;                 // 0 = exhaustive
+    int nblocks;            // blocks per palette
+};
+
+struct CostArgs {
+    const uint8_t* idx;     // [P][idx_pitch]
+    const float4* opp;      // [P][256]
+    const float* labL;      // planar LabRef, owned rows, pitch lab_pitch
+    const float* labA;
+    const float* labB;
+    double* partial;        // [P][ntiles]
+    Geom g;
+    int K;
+    int tiles_x;
+    int ntiles;
+    float inv_illum[3];
+};
+
+struct FinalizeArgs {
+    const double* partial;  // [P][ntiles]
+    const uint32_t* used_mask;  // [P][nblocks][8]
+    double* out;            // [P][1+K]
+    int ntiles;
+    int nblocks;
+    int K;
+};
+
+// Generic two-pass path (any half-width), one palette per launch.
+struct GenArgs {
+    const uint8_t* idx;      // palette's index image (extended rows)
+    const float4* opp;       // palette's opponent table [256]
+    const float* k1;         // [T][4]
+    const float* k2;         // [T][4]
+    const float* k3;         // [T]
+    const float* absk3;      // [T]
+    float* t;                // [7][n_ext] horizontal results (t1.xyz, t2.xyz, t3)
+    const float* labL;
+    const float* labA;
+    const float* labB;
+    double* partial;         // [nblocks]
+    Geom g;
+    int half;
+    float inv_illum[3];
+};
+
+}  // namespace hq

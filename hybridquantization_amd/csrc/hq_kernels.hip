@@ -1,0 +1,865 @@
+// hq_kernels.hip -- gfx950 kernels of the SWASA dE cost evaluator.
+//
+// Hot path for one population of P candidate palettes (IM:620-727 restated):
+//   prep_palette   : opponent colour per palette entry (CL:194-198), exact
+//                    duplicate flags, non-finite guard.
+//   build_grid     : exact two-level candidate lists for the argmin (grid over
+//                    the RGB cube, bounds in fp64), per palette.
+//   assign         : per-pixel palette index (CL:179-193 argmin, bit-exact) +
+//                    used-colour bitmask (CL:193); u8 index image in HBM.
+//   cost_tile      : S-CIELAB stencil of the quantized image (CL:234-306,
+//                    vertical pass first), Opp->Lab (CL:124-145), dE76 vs the
+//                    precomputed LabRef (CL:201-209), fp64 per-tile partials.
+//   finalize       : deterministic fixed-order fp64 reduction (IM:736-768) and
+//                    used-flag OR (-> penalty SW:74-82 on the host).
+// Setup / once-per-search kernels: LabRef (CL:79-116, CL:2-74, CL:124-145),
+// final quantize (CL:147-170), CIEDE error image (CL:201-231).
+//
+// Numerical contract of the argmin (frozen, see oracle/oracle.py header):
+// d2 = ((dx*dx + dy*dy) + dz*dz) in fp32 with no contraction, ranking by
+// sqrtf(d2) (correctly rounded), strict '<' in ascending palette order.
+#include "hq_internal.h"
+
+#include <math.h>
+
+namespace hq {
+
+// ----------------------------------------------------------------------------
+// Colour constants (CL:77, CL:110, CL:118, CL:171; CL:120-123)
+// ----------------------------------------------------------------------------
+__constant__ float c_RGB2XYZ[9] = {0.4124564f, 0.3575761f, 0.1804375f, 0.2126729f, 0.7151522f,
+                                   0.0721750f, 0.0193339f, 0.1191920f, 0.9503041f};
+__constant__ float c_XYZ2Opp[9] = {0.2787336f,  0.7218031f, -0.1065520f, -0.4487736f, 0.2898056f,
+                                   -0.0771569f, 0.0859513f, -0.5899859f, 0.5011089f};
+__constant__ float c_Opp2XYZ[9] = {0.624045f, -1.87044f, -0.155304f, 1.36606f, 0.931563f,
+                                   0.433903f, 1.5013f,   1.41761f,  2.53307f};
+__constant__ float c_RGB2Opp[9] = {0.266413f,  0.603167f, 0.00113333f, -0.124957f, 0.0375879f,
+                                   -0.133381f, -0.0803345f, -0.331467f, 0.449132f};
+
+#define LAB_DELTA3 (216.0f / 24389.0f)
+#define LAB_KAPPA (24389.0f / 27.0f)
+
+__device__ __forceinline__ float dot3(float x, float y, float z, const float* m) {
+    return (x * m[0] + y * m[1]) + z * m[2];
+}
+
+__device__ __forceinline__ float srgb_lin(float x) {  // CL:85-87, CL:194-196
+    return x <= 0.04045f ? x / 12.92f : powf((x + 0.055f) / 1.055f, 2.4f);
+}
+
+__device__ __forceinline__ float lab_f(float t) {  // CL:137
+    return t > LAB_DELTA3 ? cbrtf(t) : fmaf(LAB_KAPPA, t, 16.0f) * (1.0f / 116.0f);
+}
+
+// CL:124-145 Opp2LAB with reciprocal illuminant (hot path; fp32 tolerance).
+__device__ __forceinline__ float3 opp2lab_fast(float o0, float o1, float o2, float ix, float iy,
+                                               float iz) {
+    const float X = dot3(o0, o1, o2, c_Opp2XYZ + 0);
+    const float Y = dot3(o0, o1, o2, c_Opp2XYZ + 3);
+    const float Z = dot3(o0, o1, o2, c_Opp2XYZ + 6);
+    const float fx = lab_f(X * ix), fy = lab_f(Y * iy), fz = lab_f(Z * iz);
+    return make_float3(116.0f * fy - 16.0f, 500.0f * (fx - fy), 200.0f * (fy - fz));
+}
+
+// CL:124-145 with true division (setup paths: LabRef, quantize/error image).
+__device__ __forceinline__ float3 opp2lab_ref(float o0, float o1, float o2, const float* illum) {
+    const float X = dot3(o0, o1, o2, c_Opp2XYZ + 0);
+    const float Y = dot3(o0, o1, o2, c_Opp2XYZ + 3);
+    const float Z = dot3(o0, o1, o2, c_Opp2XYZ + 6);
+    const float fx = lab_f(X / illum[0]), fy = lab_f(Y / illum[1]), fz = lab_f(Z / illum[2]);
+    return make_float3(116.0f * fy - 16.0f, 500.0f * (fx - fy), 200.0f * (fy - fz));
+}
+
+// CL:201-231: dE76 (distance) or dE94.
+template <int DE>
+__device__ __forceinline__ float delta_e(float L1, float a1, float b1, float L2, float a2,
+                                         float b2) {
+    if constexpr (DE == 0) {
+        const float dl = L1 - L2, da = a1 - a2, db = b1 - b2;
+        return sqrtf((dl * dl + da * da) + db * db);
+    } else {
+        const float dL = L1 - L2;
+        const float c1 = sqrtf(fmaf(a1, a1, b1 * b1));
+        const float dC = c1 - sqrtf(fmaf(a2, a2, b2 * b2));
+        const float da = a1 - a2, db = b1 - b2;
+        const float dH = sqrtf(fmaf(da, da, db * db) - dC * dC);
+        const float sc = 1.0f + 0.045f * c1, sh = 1.0f + 0.015f * c1;
+        return sqrtf(fmaf(dL, dL, fmaf(dC / sc, dC / sc, (dH / sh) * (dH / sh))));
+    }
+}
+
+// CL:256-263 reflection; clamped so garbage coordinates of partial tiles stay
+// in bounds (their results are masked).
+__device__ __forceinline__ int reflect_clamp(int j, int n) {
+    if (j < 0) j = -j - 1;
+    if (j >= n) j = 2 * n - j - 1;
+    return min(max(j, 0), n - 1);
+}
+
+__device__ __forceinline__ int reflect_only(int j, int n) {
+    if (j < 0) return -j - 1;
+    if (j >= n) return 2 * n - j - 1;
+    return j;
+}
+
+// Exact argmin distance: no contraction (__f*_rn are never fused).
+__device__ __forceinline__ float dist2(float r, float g, float b, float4 c) {
+    const float dx = __fsub_rn(r, c.x), dy = __fsub_rn(g, c.y), dz = __fsub_rn(b, c.z);
+    return __fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz));
+}
+
+template <typename V>
+__device__ __forceinline__ V wave_sum(V v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    return v;
+}
+
+// ----------------------------------------------------------------------------
+// prep_palette: grid (P), block 256.
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void prep_palette_kernel(PaletteArgs a) {
+    const int p = blockIdx.x, k = threadIdx.x;
+    __shared__ float4 s[kMaxK];
+    __shared__ int s_nonfinite;
+    if (k == 0) s_nonfinite = 0;
+    __syncthreads();
+    float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (k < a.K) {
+        c = a.pal_in[(int64_t)p * a.K + k];
+        c.w = 0.f;  // SW:49: palettes carry .w = 0
+        s[k] = c;
+        if (!(isfinite(c.x) && isfinite(c.y) && isfinite(c.z))) atomicOr(&s_nonfinite, 1);
+    }
+    __syncthreads();
+    if (k < a.K) {
+        uint8_t dup = 0;
+        for (int j = 0; j < k; ++j) {
+            const float4 o = s[j];
+            if (o.x == c.x && o.y == c.y && o.z == c.z) { dup = 1; break; }
+        }
+        const float lr = srgb_lin(c.x), lg = srgb_lin(c.y), lb = srgb_lin(c.z);
+        const float4 opp = make_float4(dot3(lr, lg, lb, c_RGB2Opp + 0),
+                                       dot3(lr, lg, lb, c_RGB2Opp + 3),
+                                       dot3(lr, lg, lb, c_RGB2Opp + 6), 0.f);
+        a.pal[(int64_t)p * kMaxK + k] = c;
+        a.opp[(int64_t)p * kMaxK + k] = opp;
+        a.dup[(int64_t)p * kMaxK + k] = dup;
+    }
+    if (k == 0) a.pflags[p] = s_nonfinite;
+}
+
+// ----------------------------------------------------------------------------
+// build_grid: grid (G1^3, P), block 256.  One workgroup per level-1 cell; it
+// also writes the 64 level-2 children (G2 = 4*G1).
+//
+// Exactness: for a closed box B and any pixel p in B, the reference winner k*
+// satisfies dmin2(B,k*) <= T(B)*(1+~1.1e-6) with T(B) = min_j dmax2(B,j) (fp32
+// rounding of d2 and the sqrt collapse bounded by ~18 ulp); candidates keep
+// dmin2 <= T*(1+1e-5).  Children lists are subsets of the parent list, and
+// the child's T is attained inside it, so level 2 needs only the parent list.
+// Entries: byte0 = count (255 = overflow), then ascending indices.
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ double ax_min2(double c, double lo, double hi) {
+    const double d = fmax(fmax(lo - c, c - hi), 0.0);
+    return d * d;
+}
+__device__ __forceinline__ double ax_max2(double c, double lo, double hi) {
+    const double d = fmax(c - lo, hi - c);
+    return d * d;
+}
+
+#define HQ_CAND_MARGIN (1.0 + 1e-5)
+
+__global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
+    const int p = blockIdx.y, cell = blockIdx.x, tid = threadIdx.x;
+    const int G1 = a.G1, G2 = 4 * G1;
+    const int ci = cell / (G1 * G1), cj = (cell / G1) % G1, ck = cell % G1;
+    __shared__ float4 s_col[kMaxK];
+    __shared__ uint8_t s_list[kMaxK];
+    __shared__ double s_min[4];
+    __shared__ int s_wcount[4];
+
+    const bool exh = a.pflags[p] != 0;
+    const float4* pal = a.pal + (int64_t)p * kMaxK;
+    bool valid = false;
+    float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (tid < a.K) {
+        c = pal[tid];
+        valid = !exh && a.dup[(int64_t)p * kMaxK + tid] == 0;
+    }
+    s_col[tid] = c;
+    const double inv1 = 1.0 / G1;
+    const double lo0 = ci * inv1, hi0 = (ci + 1) * inv1;
+    const double lo1 = cj * inv1, hi1 = (cj + 1) * inv1;
+    const double lo2 = ck * inv1, hi2 = (ck + 1) * inv1;
+    double dmin2 = INFINITY, dmax2 = INFINITY;
+    if (valid) {
+        dmin2 = ax_min2(c.x, lo0, hi0) + ax_min2(c.y, lo1, hi1) + ax_min2(c.z, lo2, hi2);
+        dmax2 = ax_max2(c.x, lo0, hi0) + ax_max2(c.y, lo1, hi1) + ax_max2(c.z, lo2, hi2);
+    }
+    double m = dmax2;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmin(m, __shfl_xor(m, off, 64));
+    const int wave = tid >> 6, lane = tid & 63;
+    if (lane == 0) s_min[wave] = m;
+    __syncthreads();
+    const double T1 = fmin(fmin(s_min[0], s_min[1]), fmin(s_min[2], s_min[3]));
+    const bool cand = valid && dmin2 <= T1 * HQ_CAND_MARGIN;
+    const uint64_t bal = __ballot(cand);
+    if (lane == 0) s_wcount[wave] = __popcll(bal);
+    __syncthreads();
+    int base = 0;
+    for (int w = 0; w < wave; ++w) base += s_wcount[w];
+    const int total = s_wcount[0] + s_wcount[1] + s_wcount[2] + s_wcount[3];
+    if (cand) s_list[base + __popcll(bal & ((1ull << lane) - 1ull))] = (uint8_t)tid;
+    __syncthreads();
+
+    uint8_t* l1 = a.lvl1 + (int64_t)p * a.lvl1_pitch + (int64_t)cell * 32;
+    const bool ovf1 = exh || total > kL1Cap;
+    if (tid < 32) {
+        uint8_t v;
+        if (tid == 0) v = ovf1 ? kOverflow : (uint8_t)total;
+        else v = (!ovf1 && tid - 1 < total) ? s_list[tid - 1] : 0;
+        l1[tid] = v;
+    }
+    if (tid < 64) {
+        const int ci2 = ci * 4 + (tid >> 4), cj2 = cj * 4 + ((tid >> 2) & 3), ck2 = ck * 4 + (tid & 3);
+        const double inv2 = 1.0 / G2;
+        const double l0 = ci2 * inv2, h0 = (ci2 + 1) * inv2;
+        const double l1b = cj2 * inv2, h1 = (cj2 + 1) * inv2;
+        const double l2 = ck2 * inv2, h2 = (ck2 + 1) * inv2;
+        uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+        int n = 0;
+        if (!exh) {
+            double T2 = INFINITY;
+            for (int i = 0; i < total; ++i) {
+                const float4 cc = s_col[s_list[i]];
+                T2 = fmin(T2, ax_max2(cc.x, l0, h0) + ax_max2(cc.y, l1b, h1) + ax_max2(cc.z, l2, h2));
+            }
+            const double thr = T2 * HQ_CAND_MARGIN;
+            for (int i = 0; i < total; ++i) {
+                const int k = s_list[i];
+                const float4 cc = s_col[k];
+                const double d = ax_min2(cc.x, l0, h0) + ax_min2(cc.y, l1b, h1) + ax_min2(cc.z, l2, h2);
+                if (d <= thr) {
+                    const int pos = n + 1;  // byte position in the entry
+                    const uint32_t v = (uint32_t)k << (8 * (pos & 3));
+                    if (pos < 4) w0 |= v;
+                    else if (pos < 8) w1 |= v;
+                    else if (pos < 12) w2 |= v;
+                    else if (pos < 16) w3 |= v;
+                    ++n;
+                }
+            }
+        }
+        if (exh || n > kL2Cap) { w0 = kOverflow; w1 = w2 = w3 = 0; }
+        else w0 |= (uint32_t)n;
+        uint8_t* l2e = a.lvl2 + (int64_t)p * a.lvl2_pitch +
+                       ((int64_t)(ci2 * G2 + cj2) * G2 + ck2) * 16;
+        *reinterpret_cast<uint4*>(l2e) = make_uint4(w0, w1, w2, w3);
+    }
+}
+
+// ----------------------------------------------------------------------------
+// assign: grid (nblocks, P), block 256, dynamic LDS = K*REP*16 bytes.
+// Palette replicated REP times in LDS; lane l reads copy (l % REP) so that a
+// ds_read_b128 16-lane group never hits one bank position twice (REP = 16).
+// ----------------------------------------------------------------------------
+template <int REP>
+__device__ __forceinline__ int argmin_pixel(float r, float g, float b, const float4* s_pal,
+                                            int copy, const uint8_t* lvl1p, const uint8_t* lvl2p,
+                                            int G2, bool exh_pal, int K) {
+    const bool inside = r >= 0.f && r <= 1.f && g >= 0.f && g <= 1.f && b >= 0.f && b <= 1.f;
+    uint4 L0 = make_uint4(0, 0, 0, 0), L1 = make_uint4(0, 0, 0, 0);
+    int cnt = 0;
+    bool exh = exh_pal || !inside;
+    if (!exh) {
+        const int G1 = G2 >> 2;
+        const int ir = min((int)(r * (float)G2), G2 - 1);
+        const int ig = min((int)(g * (float)G2), G2 - 1);
+        const int ib = min((int)(b * (float)G2), G2 - 1);
+        L0 = *reinterpret_cast<const uint4*>(lvl2p + ((int64_t)(ir * G2 + ig) * G2 + ib) * 16);
+        cnt = L0.x & 0xff;
+        if (cnt == kOverflow) {
+            const uint4* e = reinterpret_cast<const uint4*>(
+                lvl1p + ((int64_t)((ir >> 2) * G1 + (ig >> 2)) * G1 + (ib >> 2)) * 32);
+            L0 = e[0];
+            L1 = e[1];
+            cnt = L0.x & 0xff;
+            if (cnt == kOverflow) { exh = true; cnt = 0; }
+        }
+    }
+    int bi = (L0.x >> 8) & 0xff;  // first candidate (lowest index)
+    if (__any(cnt > 1)) {
+        float best2 = dist2(r, g, b, s_pal[bi * REP + copy]);
+        const uint32_t words[8] = {L0.x, L0.y, L0.z, L0.w, L1.x, L1.y, L1.z, L1.w};
+#pragma unroll
+        for (int i = 1; i < kL1Cap; ++i) {
+            if (!__any(i < cnt)) break;
+            const int k = (words[(i + 1) >> 2] >> (8 * ((i + 1) & 3))) & 0xff;
+            const float d2 = dist2(r, g, b, s_pal[k * REP + copy]);
+            bool lt = (i < cnt) && d2 < best2;
+            // sqrtf may map d2 < best2 onto equal distances (CL:186 compares
+            // distance()); resolve near-ties exactly, keeping the lower index.
+            if (lt && d2 >= best2 * 0.99999905f) lt = sqrtf(d2) < sqrtf(best2);
+            best2 = lt ? d2 : best2;
+            bi = lt ? k : bi;
+        }
+    }
+    if (exh) {  // reference loop verbatim (CL:179-192); rare
+        float best = sqrtf(dist2(r, g, b, s_pal[copy]));
+        bi = 0;
+        for (int k = 1; k < K; ++k) {
+            const float d = sqrtf(dist2(r, g, b, s_pal[k * REP + copy]));
+            if (d < best) { best = d; bi = k; }
+        }
+    }
+    return bi;
+}
+
+template <int REP>
+__global__ __launch_bounds__(256) void assign_kernel(AssignArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float4 s_pal[];
+    __shared__ uint32_t s_used[8];
+    const int p = blockIdx.y, tid = threadIdx.x;
+    const float4* pal = a.pal + (int64_t)p * kMaxK;
+    for (int e = tid; e < a.K * REP; e += 256) s_pal[e] = pal[e / REP];
+    if (tid < 8) s_used[tid] = 0;
+    __syncthreads();
+    const bool exh_pal = a.pflags[p] != 0 || a.G2 == 0;
+    const int copy = tid & (REP - 1);
+    const uint8_t* lvl1p = a.lvl1 + (int64_t)p * a.lvl1_pitch;
+    const uint8_t* lvl2p = a.lvl2 + (int64_t)p * a.lvl2_pitch;
+    uint8_t* idx = a.idx + (int64_t)p * a.idx_pitch;
+    const int64_t stride = (int64_t)a.nblocks * 256 * 4;
+    for (int64_t q = ((int64_t)blockIdx.x * 256 + tid) * 4; q < a.n_ext; q += stride) {
+        const float4 r4 = *reinterpret_cast<const float4*>(a.R + q);
+        const float4 g4 = *reinterpret_cast<const float4*>(a.G + q);
+        const float4 b4 = *reinterpret_cast<const float4*>(a.B + q);
+        const float rr[4] = {r4.x, r4.y, r4.z, r4.w};
+        const float gg[4] = {g4.x, g4.y, g4.z, g4.w};
+        const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
+        uint32_t packed = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int k = argmin_pixel<REP>(rr[j], gg[j], bb[j], s_pal, copy, lvl1p, lvl2p, a.G2,
+                                            exh_pal, a.K);
+            packed |= (uint32_t)k << (8 * j);
+            if (q + j < a.n_ext) {
+                const uint32_t bit = 1u << (k & 31);
+                if (!(s_used[k >> 5] & bit)) atomicOr(&s_used[k >> 5], bit);
+            }
+        }
+        *reinterpret_cast<uint32_t*>(idx + q) = packed;
+    }
+    __syncthreads();
+    if (tid < 8) a.used_mask[((int64_t)p * a.nblocks + blockIdx.x) * 8 + tid] = s_used[tid];
+}
+
+// ----------------------------------------------------------------------------
+// cost_tile: grid (ntiles, P), block 256.  One workgroup = one TW x TH output
+// tile; region = (TH + 2*HALF) rows x RW cols of indices (RW = TW + 2*HALF).
+// Vertical pass first on all RW region columns (separable filters commute),
+// then horizontal pass on the TW output columns, Opp->Lab, dE, fp64 partial.
+// ----------------------------------------------------------------------------
+template <int HALF>
+struct CostTaps {
+    float v[kNumFilt][2 * HALF + 1];
+    float h[kNumFilt][2 * HALF + 1];
+};
+
+template <int HALF, int RW, int TH, int RV, int DE>
+__global__ __launch_bounds__(256, 2) void cost_tile_kernel(CostArgs a, CostTaps<HALF> taps) {
+    constexpr int T = 2 * HALF + 1;
+    constexpr int TW = RW - 2 * HALF;
+    constexpr int RH = TH + 2 * HALF;
+    constexpr int NIN = RV + 2 * HALF;
+    constexpr int NRUN = TW / 4;
+    static_assert(RW * (TH / RV) == 256, "one V item per thread");
+    static_assert(TW % 4 == 0, "4-wide H runs");
+    __shared__ __attribute__((aligned(16))) float s_v[kNumFilt * TH * RW];
+    __shared__ __attribute__((aligned(16))) float4 s_opp[kMaxK];
+    __shared__ uint8_t s_idx[RH * RW];
+    __shared__ double s_red[4];
+
+    const int p = blockIdx.y, tile = blockIdx.x, tid = threadIdx.x;
+    const Geom& g = a.g;
+    const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
+    const int x0 = tx * TW, y0 = g.r0 + ty * TH;
+    const uint8_t* idx = a.idx + (int64_t)p * g.idx_pitch;
+
+    for (int k = tid; k < a.K; k += 256) s_opp[k] = a.opp[(int64_t)p * kMaxK + k];
+    for (int e = tid; e < RH * RW; e += 256) {
+        const int i = e / RW, j = e % RW;
+        int gy = reflect_clamp(y0 - HALF + i, g.H);
+        gy = min(max(gy, g.e0), g.e1 - 1);
+        const int gx = reflect_clamp(x0 - HALF + j, g.W);
+        s_idx[e] = idx[(int64_t)(gy - g.e0) * g.W + gx];
+    }
+    __syncthreads();
+
+    // ---- vertical pass: thread = (region column c, rows [RV*gr, RV*gr+RV)) ----
+    {
+        const int c = tid % RW, gr = tid / RW;
+        float o0[NIN], o1[NIN], o2[NIN];
+#pragma unroll
+        for (int r = 0; r < NIN; ++r) {
+            const float4 v = s_opp[s_idx[(gr * RV + r) * RW + c]];
+            o0[r] = v.x; o1[r] = v.y; o2[r] = v.z;
+        }
+#pragma unroll
+        for (int f = 0; f < kNumFilt; ++f) {
+            const float* o = filt_chan(f) == 0 ? o0 : (filt_chan(f) == 1 ? o1 : o2);
+            float acc[RV];
+#pragma unroll
+            for (int y = 0; y < RV; ++y) acc[y] = 0.f;
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                const float k = taps.v[f][t];
+#pragma unroll
+                for (int y = 0; y < RV; ++y) acc[y] = fmaf(o[y + t], k, acc[y]);
+            }
+#pragma unroll
+            for (int y = 0; y < RV; ++y) s_v[(f * TH + gr * RV + y) * RW + c] = acc[y];
+        }
+    }
+    __syncthreads();
+
+    // ---- horizontal pass + Lab + dE: item = (row y, 4-column run j) ----
+    double sum = 0.0;
+    for (int item = tid; item < TH * NRUN; item += 256) {
+        const int y = item / NRUN, j = item % NRUN;
+        float acc0[4] = {0.f, 0.f, 0.f, 0.f}, acc1[4] = {0.f, 0.f, 0.f, 0.f},
+              acc2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int f = 0; f < kNumFilt; ++f) {
+            float in[4 + 2 * HALF + 3];
+            const float4* src = reinterpret_cast<const float4*>(&s_v[(f * TH + y) * RW + 4 * j]);
+#pragma unroll
+            for (int q = 0; q < (4 + 2 * HALF + 3) / 4; ++q) {
+                const float4 v = src[q];
+                in[4 * q] = v.x; in[4 * q + 1] = v.y; in[4 * q + 2] = v.z; in[4 * q + 3] = v.w;
+            }
+            float* acc = filt_chan(f) == 0 ? acc0 : (filt_chan(f) == 1 ? acc1 : acc2);
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                const float k = taps.h[f][t];
+#pragma unroll
+                for (int xo = 0; xo < 4; ++xo) acc[xo] = fmaf(in[xo + t], k, acc[xo]);
+            }
+        }
+        const int gy = y0 + y, gx0 = x0 + 4 * j;
+        if (gy < g.r1 && gx0 < g.W) {
+            const int64_t off = (int64_t)(gy - g.r0) * g.lab_pitch + gx0;
+            const float4 L4 = *reinterpret_cast<const float4*>(a.labL + off);
+            const float4 A4 = *reinterpret_cast<const float4*>(a.labA + off);
+            const float4 B4 = *reinterpret_cast<const float4*>(a.labB + off);
+            const float Ls[4] = {L4.x, L4.y, L4.z, L4.w};
+            const float As[4] = {A4.x, A4.y, A4.z, A4.w};
+            const float Bs[4] = {B4.x, B4.y, B4.z, B4.w};
+            float part = 0.f;
+#pragma unroll
+            for (int xo = 0; xo < 4; ++xo) {
+                const float3 lab = opp2lab_fast(acc0[xo], acc1[xo], acc2[xo], a.inv_illum[0],
+                                                a.inv_illum[1], a.inv_illum[2]);
+                const float e = delta_e<DE>(Ls[xo], As[xo], Bs[xo], lab.x, lab.y, lab.z);
+                part += (gx0 + xo < g.W) ? e : 0.f;
+            }
+            sum += (double)part;
+        }
+    }
+    sum = wave_sum(sum);
+    if ((tid & 63) == 0) s_red[tid >> 6] = sum;
+    __syncthreads();
+    if (tid == 0)
+        a.partial[(int64_t)p * a.ntiles + tile] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+}
+
+// ----------------------------------------------------------------------------
+// Generic two-pass path (any half-width): the reference's Temp/End structure
+// (CL:234-306) with the horizontal results in HBM.  Used when the filters are
+// not the default 21 taps, and as an independent cross-check of cost_tile.
+// ----------------------------------------------------------------------------
+
+
+__global__ __launch_bounds__(256) void gen_hpass_kernel(GenArgs a) {
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (q >= a.g.n_ext) return;
+    const int ly = (int)(q / a.g.W), x = (int)(q % a.g.W);
+    const uint8_t* row = a.idx + (int64_t)ly * a.g.W;
+    float t1x = 0, t1y = 0, t1z = 0, t2x = 0, t2y = 0, t2z = 0, t3 = 0;
+    for (int i = -a.half, t = 0; i <= a.half; ++i, ++t) {  // CL:254-267
+        const float4 in = a.opp[row[reflect_only(x + i, a.g.W)]];
+        t1x = fmaf(in.x, a.k1[4 * t + 0], t1x);
+        t1y = fmaf(in.y, a.k1[4 * t + 1], t1y);
+        t1z = fmaf(in.z, a.k1[4 * t + 2], t1z);
+        t2x = fmaf(in.x, a.k2[4 * t + 0], t2x);
+        t2y = fmaf(in.y, a.k2[4 * t + 1], t2y);
+        t2z = fmaf(in.z, a.k2[4 * t + 2], t2z);
+        t3 = fmaf(in.x, a.k3[t], t3);
+    }
+    const int64_t n = a.g.n_ext;
+    a.t[q] = t1x; a.t[n + q] = t1y; a.t[2 * n + q] = t1z;
+    a.t[3 * n + q] = t2x; a.t[4 * n + q] = t2y; a.t[5 * n + q] = t2z;
+    a.t[6 * n + q] = t3;
+}
+
+template <int DE>
+__global__ __launch_bounds__(256) void gen_vpass_kernel(GenArgs a) {
+    __shared__ double s_red[4];
+    const int own_w = a.g.W;
+    const int64_t n_own = (int64_t)own_w * (a.g.r1 - a.g.r0);
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    double e = 0.0;
+    if (q < n_own) {
+        const int y = a.g.r0 + (int)(q / own_w), x = (int)(q % own_w);
+        const int64_t n = a.g.n_ext;
+        float ox = 0, oy = 0, oz = 0;
+        for (int i = -a.half, t = 0; i <= a.half; ++i, ++t) {  // CL:292-304
+            const int64_t s = (int64_t)(reflect_only(y + i, a.g.H) - a.g.e0) * a.g.W + x;
+            ox = fmaf(a.t[s], a.k1[4 * t + 0], fmaf(a.t[3 * n + s], a.k2[4 * t + 0], ox));
+            oy = fmaf(a.t[n + s], a.k1[4 * t + 1], fmaf(a.t[4 * n + s], a.k2[4 * t + 1], oy));
+            oz = fmaf(a.t[2 * n + s], a.k1[4 * t + 2], fmaf(a.t[5 * n + s], a.k2[4 * t + 2], oz));
+            ox = fmaf(a.t[6 * n + s], a.absk3[t], ox);
+        }
+        const float3 lab = opp2lab_fast(ox, oy, oz, a.inv_illum[0], a.inv_illum[1], a.inv_illum[2]);
+        const int64_t off = (int64_t)(y - a.g.r0) * a.g.lab_pitch + x;
+        e = (double)delta_e<DE>(a.labL[off], a.labA[off], a.labB[off], lab.x, lab.y, lab.z);
+    }
+    e = wave_sum(e);
+    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = e;
+    __syncthreads();
+    if (threadIdx.x == 0) a.partial[blockIdx.x] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+}
+
+// ----------------------------------------------------------------------------
+// finalize: grid (P), block 256.  Fixed-order fp64 sum of the tile partials
+// and OR of the per-block used masks -> out[p] = {sum, used[0..K-1]}.
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void finalize_kernel(FinalizeArgs a) {
+    const int p = blockIdx.x, tid = threadIdx.x;
+    __shared__ double s_red[4];
+    __shared__ uint32_t s_mask[256];
+    double s = 0.0;
+    for (int t = tid; t < a.ntiles; t += 256) s += a.partial[(int64_t)p * a.ntiles + t];
+    s = wave_sum(s);
+    if ((tid & 63) == 0) s_red[tid >> 6] = s;
+    // used: thread = (word w = tid & 7, block slice tid >> 3)
+    uint32_t m = 0;
+    const int w = tid & 7;
+    for (int b = tid >> 3; b < a.nblocks; b += 32) m |= a.used_mask[((int64_t)p * a.nblocks + b) * 8 + w];
+    s_mask[tid] = m;
+    __syncthreads();
+    double* out = a.out + (int64_t)p * (1 + a.K);
+    if (tid == 0) out[0] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+    if (tid < 8) {
+        uint32_t acc = 0;
+        for (int i = tid; i < 256; i += 8) acc |= s_mask[i];
+        s_mask[tid] = acc;  // slots 0..7 are only read after the barrier below
+    }
+    __syncthreads();
+    for (int k = tid; k < a.K; k += 256) out[1 + k] = (s_mask[k >> 5] >> (k & 31)) & 1u ? 1.0 : 0.0;
+}
+
+// ----------------------------------------------------------------------------
+// LabRef (setup, once per search): IM:100-153 + IM:285-370 on the device.
+// ----------------------------------------------------------------------------
+// planar R,G,B -> Opp float4 (CL:79-90 then CL:111-116)
+__global__ __launch_bounds__(256) void labref_opp_kernel(const float* R, const float* G,
+                                                         const float* B, float4* opp, int64_t n) {
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (q >= n) return;
+    const float lr = srgb_lin(R[q]), lg = srgb_lin(G[q]), lb = srgb_lin(B[q]);
+    const float X = dot3(lr, lg, lb, c_RGB2XYZ + 0);
+    const float Y = dot3(lr, lg, lb, c_RGB2XYZ + 3);
+    const float Z = dot3(lr, lg, lb, c_RGB2XYZ + 6);
+    opp[q] = make_float4(dot3(X, Y, Z, c_XYZ2Opp + 0), dot3(X, Y, Z, c_XYZ2Opp + 3),
+                         dot3(X, Y, Z, c_XYZ2Opp + 6), 0.f);
+}
+
+// inline XYZ float4 -> Opp float4 (CL:111-116), for hq_xyz_to_scielab
+__global__ __launch_bounds__(256) void xyz_to_opp_kernel(const float4* xyz, float4* opp, int64_t n) {
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (q >= n) return;
+    const float4 v = xyz[q];
+    opp[q] = make_float4(dot3(v.x, v.y, v.z, c_XYZ2Opp + 0), dot3(v.x, v.y, v.z, c_XYZ2Opp + 3),
+                         dot3(v.x, v.y, v.z, c_XYZ2Opp + 6), 0.f);
+}
+
+// planar R,G,B -> inline XYZ float4 (CL:79-90), for hq_rgb_to_xyz
+__global__ __launch_bounds__(256) void rgb_to_xyz_kernel(const float* R, const float* G,
+                                                         const float* B, float4* xyz, int64_t n) {
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (q >= n) return;
+    const float lr = srgb_lin(R[q]), lg = srgb_lin(G[q]), lb = srgb_lin(B[q]);
+    xyz[q] = make_float4(dot3(lr, lg, lb, c_RGB2XYZ + 0), dot3(lr, lg, lb, c_RGB2XYZ + 3),
+                         dot3(lr, lg, lb, c_RGB2XYZ + 6), 0.f);
+}
+
+// Horizontal 1-D pass of convolve4Channels / convolve1Channel (CL:2-74) on the
+// extended rows: out = sum_t fma(in[refl], k[t], acc), chans 3 (.xyz) or 1 (.x).
+__global__ __launch_bounds__(256) void labref_hconv_kernel(const float4* in, float4* out,
+                                                           const float* k, int half, int chans,
+                                                           int W, int64_t n) {
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (q >= n) return;
+    const int ly = (int)(q / W), x = (int)(q % W);
+    const float4* row = in + (int64_t)ly * W;
+    float ax = 0.f, ay = 0.f, az = 0.f;
+    for (int i = -half, t = 0; i <= half; ++i, ++t) {
+        const float4 v = row[reflect_only(x + i, W)];
+        ax = fmaf(v.x, k[4 * t + 0], ax);
+        if (chans == 3) {
+            ay = fmaf(v.y, k[4 * t + 1], ay);
+            az = fmaf(v.z, k[4 * t + 2], az);
+        }
+    }
+    out[q] = make_float4(ax, ay, az, 0.f);
+}
+
+// Vertical pass over the owned rows reading the extended rows; update = 1
+// accumulates into conv like the `update` flag of CL:30-36 / CL:67-73.
+__global__ __launch_bounds__(256) void labref_vconv_kernel(const float4* in, float4* conv,
+                                                           const float* k, int half, int chans,
+                                                           int update, Geom g) {
+    const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (q >= n_own) return;
+    const int y = g.r0 + (int)(q / g.W), x = (int)(q % g.W);
+    float ax = 0.f, ay = 0.f, az = 0.f;
+    for (int i = -half, t = 0; i <= half; ++i, ++t) {
+        const float4 v = in[(int64_t)(reflect_only(y + i, g.H) - g.e0) * g.W + x];
+        ax = fmaf(v.x, k[4 * t + 0], ax);
+        if (chans == 3) {
+            ay = fmaf(v.y, k[4 * t + 1], ay);
+            az = fmaf(v.z, k[4 * t + 2], az);
+        }
+    }
+    float4 o = conv[q];
+    if (update) {
+        o.x += ax;
+        if (chans == 3) { o.y += ay; o.z += az; }
+    } else {
+        o.x = ax;
+        if (chans == 3) { o.y = ay; o.z = az; }
+    }
+    conv[q] = o;
+}
+
+// conv (Opp) -> Lab (CL:124-145, true division) -> planar L,A,B (pitch) and
+// optional inline float4 copy.
+__global__ __launch_bounds__(256) void labref_lab_kernel(const float4* conv, float* L, float* A,
+                                                         float* B, float4* inline4, int W,
+                                                         int64_t n, int pitch, float ilx,
+                                                         float ily, float ilz) {
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (q >= n) return;
+    const float4 o = conv[q];
+    const float il[3] = {ilx, ily, ilz};
+    const float3 lab = opp2lab_ref(o.x, o.y, o.z, il);
+    if (L) {
+        const int64_t off = (q / W) * pitch + (q % W);
+        L[off] = lab.x; A[off] = lab.y; B[off] = lab.z;
+    }
+    if (inline4) inline4[q] = make_float4(lab.x, lab.y, lab.z, 0.f);
+}
+
+// inline float4 Lab (owned rows) -> planar with pitch
+__global__ __launch_bounds__(256) void lab_to_planar_kernel(const float4* lab4, float* L, float* A,
+                                                            float* B, int W, int64_t n, int pitch) {
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (q >= n) return;
+    const float4 v = lab4[q];
+    const int64_t off = (q / W) * pitch + (q % W);
+    L[off] = v.x; A[off] = v.y; B[off] = v.z;
+}
+
+// ----------------------------------------------------------------------------
+// Final quantize (CL:147-170): exhaustive argmin, any K, chosen colour out.
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void quantize_kernel(const float4* in, const float4* colors,
+                                                       int K, int* used, float4* out, int64_t n) {
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (q >= n) return;
+    const float4 px = in[q];
+    float4 bc = colors[0];
+    float best = sqrtf(dist2(px.x, px.y, px.z, bc));
+    int bi = 0;
+    for (int i = 1; i < K; ++i) {
+        const float4 c = colors[i];
+        const float d = sqrtf(dist2(px.x, px.y, px.z, c));
+        if (d < best) { best = d; bc = c; bi = i; }
+    }
+    out[q] = bc;
+    if (used[bi] == 0) atomicOr(&used[bi], 1);
+}
+
+// CIEDE (CL:201-231) + error image of IM:886-893, fp64 block partials.
+template <int DE>
+__global__ __launch_bounds__(256) void error_image_kernel(const float4* orig, const float4* quant,
+                                                          float4* err_img, double* partial,
+                                                          int64_t n) {
+    __shared__ double s_red[4];
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    double v = 0.0;
+    if (q < n) {
+        const float4 a = orig[q], b = quant[q];
+        const float e = delta_e<DE>(a.x, a.y, a.z, b.x, b.y, b.z);
+        const float im = ((255.f - e) * (255.f - e)) / (255.f * 255.f);
+        if (err_img) err_img[q] = make_float4(im, im, im, 0.f);
+        v = e;
+    }
+    v = wave_sum(v);
+    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) partial[blockIdx.x] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+}
+
+// ----------------------------------------------------------------------------
+// Launchers (host side of this translation unit)
+// ----------------------------------------------------------------------------
+static inline unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }
+
+hipError_t launch_prep_palette(const PaletteArgs& a, int P, hipStream_t s) {
+    hipLaunchKernelGGL(prep_palette_kernel, dim3(P), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_build_grid(const GridArgs& a, int P, hipStream_t s) {
+    hipLaunchKernelGGL(build_grid_kernel, dim3(a.G1 * a.G1 * a.G1, P), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_assign(const AssignArgs& a, int P, hipStream_t s) {
+    constexpr int REP = 16;
+    const size_t lds = (size_t)a.K * REP * sizeof(float4);
+    static bool attr_set = false;  // allow > 64 KiB of dynamic LDS (160 KiB per CU on gfx950)
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)assign_kernel<REP>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)(kMaxK * REP * sizeof(float4)));
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(assign_kernel<REP>, dim3(a.nblocks, P), dim3(256), lds, s, a);
+    return hipGetLastError();
+}
+
+static void make_taps10(const float* k1, const float* k2, const float* k3, const float* absk3,
+                        CostTaps<10>& t) {
+    for (int i = 0; i < 21; ++i) {
+        // f: 0 k1.x, 1 k2.x, 2 k3 (|k3| vertical), 3 k1.y, 4 k2.y, 5 k1.z, 6 k2.z
+        t.v[0][i] = k1[4 * i + 0]; t.h[0][i] = k1[4 * i + 0];
+        t.v[1][i] = k2[4 * i + 0]; t.h[1][i] = k2[4 * i + 0];
+        t.v[2][i] = absk3[i];      t.h[2][i] = k3[i];
+        t.v[3][i] = k1[4 * i + 1]; t.h[3][i] = k1[4 * i + 1];
+        t.v[4][i] = k2[4 * i + 1]; t.h[4][i] = k2[4 * i + 1];
+        t.v[5][i] = k1[4 * i + 2]; t.h[5][i] = k1[4 * i + 2];
+        t.v[6][i] = k2[4 * i + 2]; t.h[6][i] = k2[4 * i + 2];
+    }
+}
+
+// Tile geometry of the fast path (HALF = 10): RW = 128 region columns,
+// TW = 108 output columns, TH = 16 output rows, RV = 8 rows per V item.
+constexpr int kFastHalf = 10, kFastRW = 128, kFastTH = 16, kFastRV = 8;
+constexpr int kFastTW = kFastRW - 2 * kFastHalf;
+
+void fast_tile_dims(int W, int own_rows, int* tiles_x, int* ntiles) {
+    *tiles_x = (W + kFastTW - 1) / kFastTW;
+    *ntiles = *tiles_x * ((own_rows + kFastTH - 1) / kFastTH);
+}
+
+hipError_t launch_cost_fast(const CostArgs& a, int P, const float* k1, const float* k2,
+                            const float* k3, const float* absk3, int de, hipStream_t s) {
+    CostTaps<10> t;
+    make_taps10(k1, k2, k3, absk3, t);
+    if (de == 0)
+        hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, kFastTH, kFastRV, 0>),
+                           dim3(a.ntiles, P), dim3(256), 0, s, a, t);
+    else
+        hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, kFastTH, kFastRV, 1>),
+                           dim3(a.ntiles, P), dim3(256), 0, s, a, t);
+    return hipGetLastError();
+}
+
+hipError_t launch_cost_generic(const GenArgs& a, int de, hipStream_t s) {
+    hipLaunchKernelGGL(gen_hpass_kernel, dim3(blocks_for(a.g.n_ext)), dim3(256), 0, s, a);
+    const int64_t n_own = (int64_t)a.g.W * (a.g.r1 - a.g.r0);
+    if (de == 0)
+        hipLaunchKernelGGL(gen_vpass_kernel<0>, dim3(blocks_for(n_own)), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(gen_vpass_kernel<1>, dim3(blocks_for(n_own)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_finalize(const FinalizeArgs& a, int P, hipStream_t s) {
+    hipLaunchKernelGGL(finalize_kernel, dim3(P), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_labref_opp(const float* R, const float* G, const float* B, float4* opp,
+                             int64_t n, hipStream_t s) {
+    hipLaunchKernelGGL(labref_opp_kernel, dim3(blocks_for(n)), dim3(256), 0, s, R, G, B, opp, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_xyz_to_opp(const float4* xyz, float4* opp, int64_t n, hipStream_t s) {
+    hipLaunchKernelGGL(xyz_to_opp_kernel, dim3(blocks_for(n)), dim3(256), 0, s, xyz, opp, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_rgb_to_xyz(const float* R, const float* G, const float* B, float4* xyz,
+                             int64_t n, hipStream_t s) {
+    hipLaunchKernelGGL(rgb_to_xyz_kernel, dim3(blocks_for(n)), dim3(256), 0, s, R, G, B, xyz, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_labref_hconv(const float4* in, float4* out, const float* k, int half,
+                               int chans, int W, int64_t n, hipStream_t s) {
+    hipLaunchKernelGGL(labref_hconv_kernel, dim3(blocks_for(n)), dim3(256), 0, s, in, out, k,
+                       half, chans, W, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_labref_vconv(const float4* in, float4* conv, const float* k, int half,
+                               int chans, int update, const Geom& g, hipStream_t s) {
+    const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
+    hipLaunchKernelGGL(labref_vconv_kernel, dim3(blocks_for(n_own)), dim3(256), 0, s, in, conv,
+                       k, half, chans, update, g);
+    return hipGetLastError();
+}
+
+hipError_t launch_labref_lab(const float4* conv, float* L, float* A, float* B, float4* inline4,
+                             int W, int64_t n, int pitch, const float* illum, hipStream_t s) {
+    hipLaunchKernelGGL(labref_lab_kernel, dim3(blocks_for(n)), dim3(256), 0, s, conv, L, A, B,
+                       inline4, W, n, pitch, illum[0], illum[1], illum[2]);
+    return hipGetLastError();
+}
+
+hipError_t launch_lab_to_planar(const float4* lab4, float* L, float* A, float* B, int W,
+                                int64_t n, int pitch, hipStream_t s) {
+    hipLaunchKernelGGL(lab_to_planar_kernel, dim3(blocks_for(n)), dim3(256), 0, s, lab4, L, A, B,
+                       W, n, pitch);
+    return hipGetLastError();
+}
+
+hipError_t launch_quantize(const float4* in, const float4* colors, int K, int* used, float4* out,
+                           int64_t n, hipStream_t s) {
+    hipLaunchKernelGGL(quantize_kernel, dim3(blocks_for(n)), dim3(256), 0, s, in, colors, K,
+                       used, out, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_error_image(const float4* orig, const float4* quant, float4* err_img,
+                              double* partial, int64_t n, int de, hipStream_t s) {
+    if (de == 0)
+        hipLaunchKernelGGL(error_image_kernel<0>, dim3(blocks_for(n)), dim3(256), 0, s, orig,
+                           quant, err_img, partial, n);
+    else
+        hipLaunchKernelGGL(error_image_kernel<1>, dim3(blocks_for(n)), dim3(256), 0, s, orig,
+                           quant, err_img, partial, n);
+    return hipGetLastError();
+}
+
+}  // namespace hq

@@ -1,0 +1,842 @@
+// hq_runtime.hip -- libhq host runtime: the C ABI of include/hq.h.
+//
+// One hq_ctx = one GPU, one HIP stream (the reference's single in-order queue,
+// IM:58-59), the device-resident image of IM:450-478 (planar RGB of the owned
+// rows +- halo, planar LabRef of the owned rows), per-population work buffers,
+// and optionally an RCCL communicator for row-block sharding.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "hq_internal.h"
+#include "hq_swasa.h"
+
+namespace hq {
+// launchers from hq_kernels.hip
+hipError_t launch_prep_palette(const PaletteArgs&, int P, hipStream_t);
+hipError_t launch_build_grid(const GridArgs&, int P, hipStream_t);
+hipError_t launch_assign(const AssignArgs&, int P, hipStream_t);
+void fast_tile_dims(int W, int own_rows, int* tiles_x, int* ntiles);
+hipError_t launch_cost_fast(const CostArgs&, int P, const float* k1, const float* k2,
+                            const float* k3, const float* absk3, int de, hipStream_t);
+
+hipError_t launch_cost_generic(const GenArgs&, int de, hipStream_t);
+hipError_t launch_finalize(const FinalizeArgs&, int P, hipStream_t);
+hipError_t launch_labref_opp(const float*, const float*, const float*, float4*, int64_t, hipStream_t);
+hipError_t launch_xyz_to_opp(const float4*, float4*, int64_t, hipStream_t);
+hipError_t launch_rgb_to_xyz(const float*, const float*, const float*, float4*, int64_t, hipStream_t);
+hipError_t launch_labref_hconv(const float4*, float4*, const float*, int, int, int, int64_t, hipStream_t);
+hipError_t launch_labref_vconv(const float4*, float4*, const float*, int, int, int, const Geom&, hipStream_t);
+hipError_t launch_labref_lab(const float4*, float*, float*, float*, float4*, int, int64_t, int,
+                             const float*, hipStream_t);
+hipError_t launch_lab_to_planar(const float4*, float*, float*, float*, int, int64_t, int, hipStream_t);
+hipError_t launch_quantize(const float4*, const float4*, int, int*, float4*, int64_t, hipStream_t);
+hipError_t launch_error_image(const float4*, const float4*, float4*, double*, int64_t, int, hipStream_t);
+}  // namespace hq
+
+using namespace hq;
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= bytes) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipMalloc(&p, n);
+        if (e == hipSuccess) bytes = n;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <typename T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+struct ProfSlot {
+    double ms = 0.0;
+    int64_t launches = 0;
+};
+
+}  // namespace
+
+struct hq_ctx {
+    int device = 0;
+    int de_type = HQ_DE_CIE76;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    // filters (IM:800-841)
+    int taps = 0, half = 0;
+    std::vector<float> k1, k2, k3, absk3;
+    DevBuf d_k1, d_k2, d_k3, d_absk3;
+
+    // image
+    bool have_image = false;
+    Geom g{};
+    float illum[3] = {0.95047f, 1.0f, 1.0883f};
+    DevBuf d_R, d_G, d_B;          // planar, extended rows (n_ext, padded to 4)
+    DevBuf d_labL, d_labA, d_labB;  // planar LabRef, owned rows, lab_pitch
+
+    // population work buffers
+    int P_cap = 0, K_cur = 0;
+    DevBuf d_pal_in, d_pal, d_opp, d_dup, d_pflags, d_lvl1, d_lvl2, d_idx, d_used_mask,
+        d_partial, d_out, d_gen_t;
+    float* h_pal = nullptr;   // pinned [P][K][4]
+    double* h_out = nullptr;  // pinned [P][1+K]
+    size_t h_pal_bytes = 0, h_out_bytes = 0;
+    int last_P = 0;
+
+    // options
+    int G2 = 64;           // argmin grid resolution (0 = exhaustive)
+    int cost_variant = 0;  // 0 fast tiled, 1 generic
+    int assign_blocks_per_cu = 8;
+
+    // comm
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+
+    // profiling
+    bool prof = false;
+    ProfSlot prof_assign, prof_cost, prof_grid, prof_finalize;
+    hipEvent_t ev[6] = {};
+    int num_cu = 256;
+};
+
+struct hq_search {
+    hq_ctx* ctx;
+    SearchDriver* driver;
+    int K;
+};
+
+namespace {
+
+int fail(hq_ctx* c, int code, const char* fmt, ...) {
+    if (c) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        c->err = buf;
+    }
+    return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                                      \
+    do {                                                                                        \
+        hipError_t _e = (expr);                                                                 \
+        if (_e != hipSuccess)                                                                   \
+            return fail((ctx), _e == hipErrorOutOfMemory ? HQ_ERR_NOMEM : HQ_ERR_DEVICE,        \
+                        "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, __LINE__); \
+    } while (0)
+
+#define NCCL_TRY(ctx, expr)                                                                     \
+    do {                                                                                        \
+        ncclResult_t _r = (expr);                                                               \
+        if (_r != ncclSuccess)                                                                  \
+            return fail((ctx), HQ_ERR_COMM, "%s failed: %s", #expr, ncclGetErrorString(_r));    \
+    } while (0)
+
+inline int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+
+int bind(hq_ctx* c) {
+    HIP_TRY(c, hipSetDevice(c->device));
+    return HQ_OK;
+}
+
+// Geometry of the shard [r0, r1) of a (W x H) image with halo `half`.
+Geom make_geom(int W, int H, int r0, int r1, int half) {
+    Geom g{};
+    g.W = W;
+    g.H = H;
+    g.r0 = r0;
+    g.r1 = r1;
+    g.e0 = std::max(0, r0 - half);
+    g.e1 = std::min(H, r1 + half);
+    g.lab_pitch = (int)round_up(W, 4);
+    g.n_ext = (int64_t)W * (g.e1 - g.e0);
+    g.idx_pitch = round_up(g.n_ext + 4, 256);
+    return g;
+}
+
+int ensure_pinned(hq_ctx* c, size_t pal_bytes, size_t out_bytes) {
+    if (pal_bytes > c->h_pal_bytes) {
+        if (c->h_pal) (void)hipHostFree(c->h_pal);
+        c->h_pal = nullptr;
+        HIP_TRY(c, hipHostMalloc((void**)&c->h_pal, pal_bytes, hipHostMallocDefault));
+        c->h_pal_bytes = pal_bytes;
+    }
+    if (out_bytes > c->h_out_bytes) {
+        if (c->h_out) (void)hipHostFree(c->h_out);
+        c->h_out = nullptr;
+        HIP_TRY(c, hipHostMalloc((void**)&c->h_out, out_bytes, hipHostMallocDefault));
+        c->h_out_bytes = out_bytes;
+    }
+    return HQ_OK;
+}
+
+// Upload one plane of the extended rows from a full-image host source with
+// stride `sstride` floats between pixels and channel offset `ch`.
+void gather_rows(const float* src, int sstride, int ch, const Geom& g, std::vector<float>& dst) {
+    dst.assign((size_t)round_up(g.n_ext, 4), 0.0f);
+    const int64_t base = (int64_t)g.e0 * g.W;
+    for (int64_t i = 0; i < g.n_ext; ++i) dst[i] = src[(base + i) * sstride + ch];
+}
+
+int compute_labref_device(hq_ctx* c) {
+    // IM:100 RGBtoXYZ + IM:285-370 XYZtoScielab on the extended rows.
+    const Geom& g = c->g;
+    const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
+    DevBuf opp, tmp, conv, k3v, ak3v;
+    HIP_TRY(c, opp.ensure(sizeof(float4) * g.n_ext));
+    HIP_TRY(c, tmp.ensure(sizeof(float4) * g.n_ext));
+    HIP_TRY(c, conv.ensure(sizeof(float4) * std::max<int64_t>(n_own, 1)));
+    std::vector<float> k3h(4 * c->taps, 0.f), ak3h(4 * c->taps, 0.f);
+    for (int t = 0; t < c->taps; ++t) { k3h[4 * t] = c->k3[t]; ak3h[4 * t] = c->absk3[t]; }
+    HIP_TRY(c, k3v.ensure(sizeof(float) * k3h.size()));
+    HIP_TRY(c, ak3v.ensure(sizeof(float) * ak3h.size()));
+    HIP_TRY(c, hipMemcpyAsync(k3v.p, k3h.data(), sizeof(float) * k3h.size(), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(ak3v.p, ak3h.data(), sizeof(float) * ak3h.size(), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, launch_labref_opp(c->d_R.as<float>(), c->d_G.as<float>(), c->d_B.as<float>(),
+                                 opp.as<float4>(), g.n_ext, c->stream));
+    // IM:319-346 filter by filter: H then V (update for filters 2 and 3)
+    const float* hk[3] = {c->d_k1.as<float>(), c->d_k2.as<float>(), k3v.as<float>()};
+    const float* vk[3] = {c->d_k1.as<float>(), c->d_k2.as<float>(), ak3v.as<float>()};
+    for (int f = 0; f < 3; ++f) {
+        const int chans = f < 2 ? 3 : 1;
+        HIP_TRY(c, launch_labref_hconv(opp.as<float4>(), tmp.as<float4>(), hk[f], c->half, chans,
+                                       g.W, g.n_ext, c->stream));
+        HIP_TRY(c, launch_labref_vconv(tmp.as<float4>(), conv.as<float4>(), vk[f], c->half, chans,
+                                       f > 0, g, c->stream));
+    }
+    HIP_TRY(c, launch_labref_lab(conv.as<float4>(), c->d_labL.as<float>(), c->d_labA.as<float>(),
+                                 c->d_labB.as<float>(), nullptr, g.W, n_own, g.lab_pitch, c->illum,
+                                 c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    opp.release(); tmp.release(); conv.release(); k3v.release(); ak3v.release();
+    return HQ_OK;
+}
+
+int set_image_common(hq_ctx* c, const std::vector<float>& R, const std::vector<float>& G,
+                     const std::vector<float>& B, const float* lab4_full, const float* illum) {
+    const Geom& g = c->g;
+    const size_t plane = sizeof(float) * (size_t)round_up(g.n_ext, 4);
+    HIP_TRY(c, c->d_R.ensure(plane));
+    HIP_TRY(c, c->d_G.ensure(plane));
+    HIP_TRY(c, c->d_B.ensure(plane));
+    HIP_TRY(c, hipMemcpyAsync(c->d_R.p, R.data(), plane, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->d_G.p, G.data(), plane, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->d_B.p, B.data(), plane, hipMemcpyHostToDevice, c->stream));
+    if (illum) std::memcpy(c->illum, illum, sizeof c->illum);
+    const int own = g.r1 - g.r0;
+    const size_t lplane = sizeof(float) * (size_t)g.lab_pitch * std::max(own, 1);
+    HIP_TRY(c, c->d_labL.ensure(lplane));
+    HIP_TRY(c, c->d_labA.ensure(lplane));
+    HIP_TRY(c, c->d_labB.ensure(lplane));
+    HIP_TRY(c, hipMemsetAsync(c->d_labL.p, 0, lplane, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->d_labA.p, 0, lplane, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->d_labB.p, 0, lplane, c->stream));
+    if (lab4_full) {
+        const int64_t n_own = (int64_t)g.W * own;
+        DevBuf tmp;
+        HIP_TRY(c, tmp.ensure(sizeof(float4) * n_own));
+        HIP_TRY(c, hipMemcpyAsync(tmp.p, lab4_full + (int64_t)g.r0 * g.W * 4, sizeof(float4) * n_own,
+                                  hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(c, launch_lab_to_planar(tmp.as<float4>(), c->d_labL.as<float>(), c->d_labA.as<float>(),
+                                        c->d_labB.as<float>(), g.W, n_own, g.lab_pitch, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        tmp.release();
+    } else {
+        int rc = compute_labref_device(c);
+        if (rc) return rc;
+    }
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->have_image = true;
+    return HQ_OK;
+}
+
+int check_geom_args(hq_ctx* c, int w, int h, int r0, int r1) {
+    if (!c->taps) return fail(c, HQ_ERR_STATE, "filters not set (call hq_set_filters first)");
+    if (w < c->half || h < c->half || w < 1 || h < 1)
+        return fail(c, HQ_ERR_ARG, "image %dx%d smaller than the stencil half-width %d", w, h, c->half);
+    if (r0 < 0 || r1 > h || r0 >= r1) return fail(c, HQ_ERR_ARG, "bad row range [%d,%d)", r0, r1);
+    return HQ_OK;
+}
+
+// Ensure population buffers for P palettes of K colours.
+int ensure_population(hq_ctx* c, int P, int K) {
+    const Geom& g = c->g;
+    const int G2 = c->G2 > 0 ? c->G2 : 4;
+    const int G1 = G2 / 4;
+    const int64_t l1p = round_up((int64_t)G1 * G1 * G1 * 32, 256);
+    const int64_t l2p = round_up((int64_t)G2 * G2 * G2 * 16, 256);
+    int tiles_x, ntiles;
+    fast_tile_dims(g.W, g.r1 - g.r0, &tiles_x, &ntiles);
+    const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
+    const int64_t gen_blocks = (n_own + 255) / 256;
+    const int64_t nparts = std::max<int64_t>(ntiles, gen_blocks);
+    const int nblocks = c->num_cu * c->assign_blocks_per_cu;
+    HIP_TRY(c, c->d_pal_in.ensure(sizeof(float4) * (size_t)P * K));
+    HIP_TRY(c, c->d_pal.ensure(sizeof(float4) * (size_t)P * kMaxK));
+    HIP_TRY(c, c->d_opp.ensure(sizeof(float4) * (size_t)P * kMaxK));
+    HIP_TRY(c, c->d_dup.ensure((size_t)P * kMaxK));
+    HIP_TRY(c, c->d_pflags.ensure(sizeof(int) * (size_t)P));
+    HIP_TRY(c, c->d_lvl1.ensure((size_t)P * l1p));
+    HIP_TRY(c, c->d_lvl2.ensure((size_t)P * l2p));
+    HIP_TRY(c, c->d_idx.ensure((size_t)P * g.idx_pitch));
+    HIP_TRY(c, c->d_used_mask.ensure(sizeof(uint32_t) * 8 * (size_t)P * nblocks));
+    HIP_TRY(c, c->d_partial.ensure(sizeof(double) * (size_t)P * nparts));
+    HIP_TRY(c, c->d_out.ensure(sizeof(double) * (size_t)P * (1 + K)));
+    return ensure_pinned(c, sizeof(float) * 4 * (size_t)P * K, sizeof(double) * (size_t)P * (1 + K));
+}
+
+void prof_add(hq_ctx* c, ProfSlot& s, hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, a, b) == hipSuccess) {
+        s.ms += ms;
+        s.launches += 1;
+    }
+}
+
+// Enqueue the whole evaluation of the P palettes already in h_pal; results
+// (partial sums + used flags) land in d_out; all-reduced if a comm is set.
+int enqueue_eval(hq_ctx* c, int P, int K) {
+    const Geom& g = c->g;
+    hipStream_t s = c->stream;
+    const int G2 = c->G2 > 0 ? c->G2 : 4;
+    const int G1 = G2 / 4;
+    const int64_t l1p = round_up((int64_t)G1 * G1 * G1 * 32, 256);
+    const int64_t l2p = round_up((int64_t)G2 * G2 * G2 * 16, 256);
+    const int nblocks = c->num_cu * c->assign_blocks_per_cu;
+    HIP_TRY(c, hipMemcpyAsync(c->d_pal_in.p, c->h_pal, sizeof(float) * 4 * (size_t)P * K,
+                              hipMemcpyHostToDevice, s));
+    if (c->prof) HIP_TRY(c, hipEventRecord(c->ev[0], s));
+    PaletteArgs pa{c->d_pal_in.as<float4>(), c->d_pal.as<float4>(), c->d_opp.as<float4>(),
+                   c->d_dup.as<uint8_t>(), c->d_pflags.as<int>(), K};
+    HIP_TRY(c, launch_prep_palette(pa, P, s));
+    if (c->G2 > 0) {
+        GridArgs ga{c->d_pal.as<float4>(), c->d_dup.as<uint8_t>(), c->d_pflags.as<int>(),
+                    c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(), K, G1, l1p, l2p};
+        HIP_TRY(c, launch_build_grid(ga, P, s));
+    }
+    if (c->prof) HIP_TRY(c, hipEventRecord(c->ev[1], s));
+    AssignArgs aa{c->d_R.as<float>(), c->d_G.as<float>(), c->d_B.as<float>(), c->d_pal.as<float4>(),
+                  c->d_pflags.as<int>(), c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(),
+                  c->d_idx.as<uint8_t>(), c->d_used_mask.as<uint32_t>(), g.n_ext, g.idx_pitch,
+                  l1p, l2p, K, c->G2, nblocks};
+    HIP_TRY(c, launch_assign(aa, P, s));
+    if (c->prof) HIP_TRY(c, hipEventRecord(c->ev[2], s));
+    int tiles_x, ntiles;
+    fast_tile_dims(g.W, g.r1 - g.r0, &tiles_x, &ntiles);
+    const float inv[3] = {1.0f / c->illum[0], 1.0f / c->illum[1], 1.0f / c->illum[2]};
+    int nparts;
+    const bool fast = c->cost_variant == 0 && c->half == 10;
+    if (fast) {
+        CostArgs ca{};
+        ca.idx = c->d_idx.as<uint8_t>();
+        ca.opp = c->d_opp.as<float4>();
+        ca.labL = c->d_labL.as<float>();
+        ca.labA = c->d_labA.as<float>();
+        ca.labB = c->d_labB.as<float>();
+        ca.partial = c->d_partial.as<double>();
+        ca.g = g;
+        ca.K = K;
+        ca.tiles_x = tiles_x;
+        ca.ntiles = ntiles;
+        std::memcpy(ca.inv_illum, inv, sizeof inv);
+        HIP_TRY(c, launch_cost_fast(ca, P, c->k1.data(), c->k2.data(), c->k3.data(),
+                                    c->absk3.data(), c->de_type, s));
+        nparts = ntiles;
+    } else {
+        HIP_TRY(c, c->d_gen_t.ensure(sizeof(float) * 7 * (size_t)g.n_ext));
+        const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
+        nparts = (int)((n_own + 255) / 256);
+        for (int p = 0; p < P; ++p) {
+            GenArgs ga{};
+            ga.idx = c->d_idx.as<uint8_t>() + (int64_t)p * g.idx_pitch;
+            ga.opp = c->d_opp.as<float4>() + (int64_t)p * kMaxK;
+            ga.k1 = c->d_k1.as<float>();
+            ga.k2 = c->d_k2.as<float>();
+            ga.k3 = c->d_k3.as<float>();
+            ga.absk3 = c->d_absk3.as<float>();
+            ga.t = c->d_gen_t.as<float>();
+            ga.labL = c->d_labL.as<float>();
+            ga.labA = c->d_labA.as<float>();
+            ga.labB = c->d_labB.as<float>();
+            ga.partial = c->d_partial.as<double>() + (int64_t)p * nparts;
+            ga.g = g;
+            ga.half = c->half;
+            std::memcpy(ga.inv_illum, inv, sizeof inv);
+            HIP_TRY(c, launch_cost_generic(ga, c->de_type, s));
+        }
+    }
+    if (c->prof) HIP_TRY(c, hipEventRecord(c->ev[3], s));
+    FinalizeArgs fa{c->d_partial.as<double>(), c->d_used_mask.as<uint32_t>(), c->d_out.as<double>(),
+                    nparts, nblocks, K};
+    HIP_TRY(c, launch_finalize(fa, P, s));
+    if (c->prof) HIP_TRY(c, hipEventRecord(c->ev[4], s));
+    if (c->comm && c->nranks > 1) {
+        NCCL_TRY(c, ncclAllReduce(c->d_out.p, c->d_out.p, (size_t)P * (1 + K), ncclFloat64, ncclSum,
+                                  c->comm, s));
+    }
+    HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out.p, sizeof(double) * (size_t)P * (1 + K),
+                              hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    if (c->prof) {
+        prof_add(c, c->prof_grid, c->ev[0], c->ev[1]);
+        prof_add(c, c->prof_assign, c->ev[1], c->ev[2]);
+        prof_add(c, c->prof_cost, c->ev[2], c->ev[3]);
+        prof_add(c, c->prof_finalize, c->ev[3], c->ev[4]);
+    }
+    c->last_P = P;
+    c->K_cur = K;
+    return HQ_OK;
+}
+
+int check_eval_args(hq_ctx* c, const float* palettes, int P, int K) {
+    if (!c) return HQ_ERR_ARG;
+    if (!c->have_image) return fail(c, HQ_ERR_STATE, "no image set (hq_set_image)");
+    if (!palettes || P < 1 || K < 1) return fail(c, HQ_ERR_ARG, "bad palettes / P=%d / K=%d", P, K);
+    if (K > kMaxK)
+        return fail(c, HQ_ERR_UNSUPPORTED, "K=%d > %d: the u8 index path supports K <= 256", K, kMaxK);
+    if (c->de_type == HQ_DE_CIEDE2000)
+        return fail(c, HQ_ERR_UNSUPPORTED, "CIEDE2000 is unimplemented in the reference (CL:227-230)");
+    return HQ_OK;
+}
+
+int eval_partial_into_hout(hq_ctx* c, const float* palettes, int P, int K) {
+    int rc = check_eval_args(c, palettes, P, K);
+    if (rc) return rc;
+    if ((rc = bind(c))) return rc;
+    if ((rc = ensure_population(c, P, K))) return rc;
+    std::memcpy(c->h_pal, palettes, sizeof(float) * 4 * (size_t)P * K);
+    return enqueue_eval(c, P, K);
+}
+
+}  // namespace
+
+// ============================================================================
+// C ABI
+// ============================================================================
+extern "C" {
+
+int hq_version(void) { return HQ_VERSION; }
+
+const char* hq_status_string(int s) {
+    switch (s) {
+        case HQ_OK: return "ok";
+        case HQ_ERR_ARG: return "invalid argument";
+        case HQ_ERR_DEVICE: return "device error";
+        case HQ_ERR_STATE: return "invalid state";
+        case HQ_ERR_UNSUPPORTED: return "unsupported";
+        case HQ_ERR_COMM: return "communication error";
+        case HQ_ERR_NOMEM: return "out of memory";
+        default: return "unknown status";
+    }
+}
+
+int hq_device_count(int* count) {
+    if (!count) return HQ_ERR_ARG;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return HQ_OK;
+}
+
+int hq_create(int device, int delta_e_type, hq_ctx** out) {
+    if (!out) return HQ_ERR_ARG;
+    *out = nullptr;
+    if (delta_e_type < HQ_DE_CIE76 || delta_e_type > HQ_DE_CIEDE2000) return HQ_ERR_ARG;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device < 0 || device >= n)
+        return HQ_ERR_DEVICE;
+    hq_ctx* c = new hq_ctx();
+    c->device = device;
+    c->de_type = delta_e_type;
+    if (hipSetDevice(device) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return HQ_ERR_DEVICE;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        c->num_cu = prop.multiProcessorCount;
+    for (auto& e : c->ev) (void)hipEventCreate(&e);
+    *out = c;
+    return HQ_OK;
+}
+
+void hq_destroy(hq_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    for (DevBuf* b : {&c->d_k1, &c->d_k2, &c->d_k3, &c->d_absk3, &c->d_R, &c->d_G, &c->d_B,
+                      &c->d_labL, &c->d_labA, &c->d_labB, &c->d_pal_in, &c->d_pal, &c->d_opp,
+                      &c->d_dup, &c->d_pflags, &c->d_lvl1, &c->d_lvl2, &c->d_idx,
+                      &c->d_used_mask, &c->d_partial, &c->d_out, &c->d_gen_t})
+        b->release();
+    if (c->h_pal) (void)hipHostFree(c->h_pal);
+    if (c->h_out) (void)hipHostFree(c->h_out);
+    for (auto& e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* hq_last_error(const hq_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int hq_set_filters(hq_ctx* c, int taps, const float* k1, const float* k2, const float* k3,
+                   const float* absk3) {
+    if (!c) return HQ_ERR_ARG;
+    if (taps < 1 || taps > kMaxTaps || !k1 || !k2 || !k3 || !absk3)
+        return fail(c, HQ_ERR_ARG, "bad filters (taps=%d)", taps);
+    int rc = bind(c);
+    if (rc) return rc;
+    c->taps = taps;
+    c->half = (taps * 4) / 8;  // IM:408 filters4[0].length/8
+    if (2 * c->half + 1 != taps)
+        return fail(c, HQ_ERR_UNSUPPORTED, "even tap count %d (the reference assumes odd)", taps);
+    c->k1.assign(k1, k1 + 4 * taps);
+    c->k2.assign(k2, k2 + 4 * taps);
+    c->k3.assign(k3, k3 + taps);
+    c->absk3.assign(absk3, absk3 + taps);
+    HIP_TRY(c, c->d_k1.ensure(sizeof(float) * 4 * taps));
+    HIP_TRY(c, c->d_k2.ensure(sizeof(float) * 4 * taps));
+    HIP_TRY(c, c->d_k3.ensure(sizeof(float) * taps));
+    HIP_TRY(c, c->d_absk3.ensure(sizeof(float) * taps));
+    HIP_TRY(c, hipMemcpy(c->d_k1.p, k1, sizeof(float) * 4 * taps, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(c->d_k2.p, k2, sizeof(float) * 4 * taps, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(c->d_k3.p, k3, sizeof(float) * taps, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(c->d_absk3.p, absk3, sizeof(float) * taps, hipMemcpyHostToDevice));
+    c->have_image = false;  // halo depends on the filters
+    return HQ_OK;
+}
+
+int hq_set_image_shard(hq_ctx* c, const float* rgba4, const float* lab4, int w, int h,
+                       const float* illum, int row_begin, int row_end) {
+    if (!c) return HQ_ERR_ARG;
+    if (!rgba4) return fail(c, HQ_ERR_ARG, "null image");
+    int rc = check_geom_args(c, w, h, row_begin, row_end);
+    if (rc) return rc;
+    if ((rc = bind(c))) return rc;
+    c->g = make_geom(w, h, row_begin, row_end, c->half);
+    std::vector<float> R, G, B;
+    gather_rows(rgba4, 4, 0, c->g, R);
+    gather_rows(rgba4, 4, 1, c->g, G);
+    gather_rows(rgba4, 4, 2, c->g, B);
+    return set_image_common(c, R, G, B, lab4, illum);
+}
+
+int hq_set_image(hq_ctx* c, const float* rgba4, const float* lab4, int w, int h,
+                 const float* illum) {
+    return hq_set_image_shard(c, rgba4, lab4, w, h, illum, 0, h);
+}
+
+int hq_set_image_planar_shard(hq_ctx* c, const float* R, const float* G, const float* B, int w,
+                              int h, const float* illum, int row_begin, int row_end) {
+    if (!c) return HQ_ERR_ARG;
+    if (!R || !G || !B) return fail(c, HQ_ERR_ARG, "null plane");
+    int rc = check_geom_args(c, w, h, row_begin, row_end);
+    if (rc) return rc;
+    if ((rc = bind(c))) return rc;
+    c->g = make_geom(w, h, row_begin, row_end, c->half);
+    std::vector<float> r, g, b;
+    gather_rows(R, 1, 0, c->g, r);
+    gather_rows(G, 1, 0, c->g, g);
+    gather_rows(B, 1, 0, c->g, b);
+    return set_image_common(c, r, g, b, nullptr, illum);
+}
+
+int hq_get_labref(hq_ctx* c, float* lab4) {
+    if (!c || !lab4) return HQ_ERR_ARG;
+    if (!c->have_image) return fail(c, HQ_ERR_STATE, "no image set");
+    int rc = bind(c);
+    if (rc) return rc;
+    const Geom& g = c->g;
+    const int own = g.r1 - g.r0;
+    std::vector<float> L((size_t)g.lab_pitch * own), A(L.size()), B(L.size());
+    HIP_TRY(c, hipMemcpy(L.data(), c->d_labL.p, sizeof(float) * L.size(), hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(A.data(), c->d_labA.p, sizeof(float) * A.size(), hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(B.data(), c->d_labB.p, sizeof(float) * B.size(), hipMemcpyDeviceToHost));
+    for (int y = 0; y < own; ++y)
+        for (int x = 0; x < g.W; ++x) {
+            const size_t s = (size_t)y * g.lab_pitch + x, d = 4 * ((size_t)y * g.W + x);
+            lab4[d] = L[s]; lab4[d + 1] = A[s]; lab4[d + 2] = B[s]; lab4[d + 3] = 0.f;
+        }
+    return HQ_OK;
+}
+
+int hq_eval_population_partial(hq_ctx* c, const float* palettes, int P, int K, double* partial) {
+    if (!partial) return fail(c, HQ_ERR_ARG, "null output");
+    int rc = eval_partial_into_hout(c, palettes, P, K);
+    if (rc) return rc;
+    std::memcpy(partial, c->h_out, sizeof(double) * (size_t)P * (1 + K));
+    return HQ_OK;
+}
+
+int hq_eval_population(hq_ctx* c, const float* palettes, int P, int K, float delta,
+                       double* costs, int32_t* used) {
+    if (!costs) return fail(c, HQ_ERR_ARG, "null output");
+    int rc = eval_partial_into_hout(c, palettes, P, K);
+    if (rc) return rc;
+    // IM:712: averageArray(error) + computePenalty(used).  After an all-reduce
+    // the used entries count the ranks using colour k; unused <=> 0.
+    const bool full = c->g.r0 == 0 && c->g.r1 == c->g.H;
+    if (!full && !(c->comm && c->nranks > 1))
+        return fail(c, HQ_ERR_STATE, "sharded context without a communicator: use "
+                                     "hq_eval_population_partial");
+    const double n_total = (double)c->g.W * (double)c->g.H;
+    for (int p = 0; p < P; ++p) {
+        const double* o = c->h_out + (size_t)p * (1 + K);
+        double penalty = 0.0;
+        for (int k = 0; k < K; ++k) {
+            const bool u = o[1 + k] != 0.0;
+            if (!u) penalty += delta;
+            if (used) used[(size_t)p * K + k] = u ? 1 : 0;
+        }
+        costs[p] = o[0] / n_total + penalty;
+    }
+    return HQ_OK;
+}
+
+int hq_get_indices(hq_ctx* c, int p, uint8_t* idx) {
+    if (!c || !idx) return HQ_ERR_ARG;
+    if (p < 0 || p >= c->last_P) return fail(c, HQ_ERR_ARG, "palette %d not in last population", p);
+    int rc = bind(c);
+    if (rc) return rc;
+    const Geom& g = c->g;
+    const int64_t off = (int64_t)(g.r0 - g.e0) * g.W;
+    const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
+    HIP_TRY(c, hipMemcpy(idx, c->d_idx.as<uint8_t>() + (int64_t)p * g.idx_pitch + off, n_own,
+                         hipMemcpyDeviceToHost));
+    return HQ_OK;
+}
+
+int hq_rgb_to_xyz(hq_ctx* c, const float* R, const float* G, const float* B, int64_t n,
+                  float* xyz4) {
+    if (!c || !R || !G || !B || !xyz4 || n < 1) return HQ_ERR_ARG;
+    int rc = bind(c);
+    if (rc) return rc;
+    DevBuf dr, dg, db, dx;
+    HIP_TRY(c, dr.ensure(sizeof(float) * n));
+    HIP_TRY(c, dg.ensure(sizeof(float) * n));
+    HIP_TRY(c, db.ensure(sizeof(float) * n));
+    HIP_TRY(c, dx.ensure(sizeof(float4) * n));
+    HIP_TRY(c, hipMemcpyAsync(dr.p, R, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(dg.p, G, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(db.p, B, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, launch_rgb_to_xyz(dr.as<float>(), dg.as<float>(), db.as<float>(), dx.as<float4>(), n,
+                                 c->stream));
+    HIP_TRY(c, hipMemcpyAsync(xyz4, dx.p, sizeof(float4) * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return HQ_OK;
+}
+
+int hq_xyz_to_scielab(hq_ctx* c, const float* xyz4, int w, int h, const float* illum,
+                      float* lab4) {
+    if (!c || !xyz4 || !lab4) return HQ_ERR_ARG;
+    int rc = check_geom_args(c, w, h, 0, h);
+    if (rc) return rc;
+    if ((rc = bind(c))) return rc;
+    const Geom g = make_geom(w, h, 0, h, c->half);
+    const int64_t n = (int64_t)w * h;
+    DevBuf dxyz, opp, tmp, conv, k3v, ak3v;
+    HIP_TRY(c, dxyz.ensure(sizeof(float4) * n));
+    HIP_TRY(c, opp.ensure(sizeof(float4) * n));
+    HIP_TRY(c, tmp.ensure(sizeof(float4) * n));
+    HIP_TRY(c, conv.ensure(sizeof(float4) * n));
+    std::vector<float> k3h(4 * c->taps, 0.f), ak3h(4 * c->taps, 0.f);
+    for (int t = 0; t < c->taps; ++t) { k3h[4 * t] = c->k3[t]; ak3h[4 * t] = c->absk3[t]; }
+    HIP_TRY(c, k3v.ensure(sizeof(float) * k3h.size()));
+    HIP_TRY(c, ak3v.ensure(sizeof(float) * ak3h.size()));
+    HIP_TRY(c, hipMemcpyAsync(k3v.p, k3h.data(), sizeof(float) * k3h.size(), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(ak3v.p, ak3h.data(), sizeof(float) * ak3h.size(), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(dxyz.p, xyz4, sizeof(float4) * n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, launch_xyz_to_opp(dxyz.as<float4>(), opp.as<float4>(), n, c->stream));
+    const float* hk[3] = {c->d_k1.as<float>(), c->d_k2.as<float>(), k3v.as<float>()};
+    const float* vk[3] = {c->d_k1.as<float>(), c->d_k2.as<float>(), ak3v.as<float>()};
+    for (int f = 0; f < 3; ++f) {
+        const int chans = f < 2 ? 3 : 1;
+        HIP_TRY(c, launch_labref_hconv(opp.as<float4>(), tmp.as<float4>(), hk[f], c->half, chans,
+                                       w, n, c->stream));
+        HIP_TRY(c, launch_labref_vconv(tmp.as<float4>(), conv.as<float4>(), vk[f], c->half, chans,
+                                       f > 0, g, c->stream));
+    }
+    const float* il = illum ? illum : c->illum;
+    HIP_TRY(c, launch_labref_lab(conv.as<float4>(), nullptr, nullptr, nullptr, dxyz.as<float4>(), w,
+                                 n, 0, il, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(lab4, dxyz.p, sizeof(float4) * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return HQ_OK;
+}
+
+int hq_quantize(hq_ctx* c, const float* rgba4, int64_t n, const float* colors, int K, float* out4,
+                int32_t* used) {
+    if (!c || !rgba4 || !colors || !out4 || n < 1 || K < 1) return HQ_ERR_ARG;
+    int rc = bind(c);
+    if (rc) return rc;
+    DevBuf din, dcol, dused, dout;
+    HIP_TRY(c, din.ensure(sizeof(float4) * n));
+    HIP_TRY(c, dcol.ensure(sizeof(float4) * K));
+    HIP_TRY(c, dused.ensure(sizeof(int) * K));
+    HIP_TRY(c, dout.ensure(sizeof(float4) * n));
+    HIP_TRY(c, hipMemcpyAsync(din.p, rgba4, sizeof(float4) * n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(dcol.p, colors, sizeof(float4) * K, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemsetAsync(dused.p, 0, sizeof(int) * K, c->stream));
+    HIP_TRY(c, launch_quantize(din.as<float4>(), dcol.as<float4>(), K, dused.as<int>(),
+                               dout.as<float4>(), n, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(out4, dout.p, sizeof(float4) * n, hipMemcpyDeviceToHost, c->stream));
+    if (used)
+        HIP_TRY(c, hipMemcpyAsync(used, dused.p, sizeof(int) * K, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return HQ_OK;
+}
+
+int hq_compute_error(hq_ctx* c, const float* orig4, const float* quant4, int64_t n,
+                     float* err_img4, double* mean) {
+    if (!c || !orig4 || !quant4 || n < 1 || !mean) return HQ_ERR_ARG;
+    if (c->de_type == HQ_DE_CIEDE2000)
+        return fail(c, HQ_ERR_UNSUPPORTED, "CIEDE2000 is unimplemented in the reference (CL:227-230)");
+    int rc = bind(c);
+    if (rc) return rc;
+    const int64_t nb = (n + 255) / 256;
+    DevBuf da, db, de, dp;
+    HIP_TRY(c, da.ensure(sizeof(float4) * n));
+    HIP_TRY(c, db.ensure(sizeof(float4) * n));
+    if (err_img4) HIP_TRY(c, de.ensure(sizeof(float4) * n));
+    HIP_TRY(c, dp.ensure(sizeof(double) * nb));
+    HIP_TRY(c, hipMemcpyAsync(da.p, orig4, sizeof(float4) * n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(db.p, quant4, sizeof(float4) * n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, launch_error_image(da.as<float4>(), db.as<float4>(), err_img4 ? de.as<float4>() : nullptr,
+                                  dp.as<double>(), n, c->de_type, c->stream));
+    std::vector<double> parts(nb);
+    HIP_TRY(c, hipMemcpyAsync(parts.data(), dp.p, sizeof(double) * nb, hipMemcpyDeviceToHost, c->stream));
+    if (err_img4)
+        HIP_TRY(c, hipMemcpyAsync(err_img4, de.p, sizeof(float4) * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    double s = 0.0;
+    for (double v : parts) s += v;
+    *mean = s / (double)n;  // IM:893
+    return HQ_OK;
+}
+
+int hq_comm_unique_id(unsigned char id[128]) {
+    if (!id) return HQ_ERR_ARG;
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return HQ_ERR_COMM;
+    std::memcpy(id, &u, 128);
+    return HQ_OK;
+}
+
+int hq_comm_init(hq_ctx* c, int nranks, int rank, const unsigned char id[128]) {
+    if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return HQ_ERR_ARG;
+    int rc = bind(c);
+    if (rc) return rc;
+    if (c->comm) { (void)ncclCommDestroy(c->comm); c->comm = nullptr; }
+    ncclUniqueId u;
+    std::memcpy(&u, id, 128);
+    NCCL_TRY(c, ncclCommInitRank(&c->comm, nranks, u, rank));
+    c->nranks = nranks;
+    c->rank = rank;
+    return HQ_OK;
+}
+
+int hq_search_create(hq_ctx* c, const hq_swasa_params* params, int K, uint64_t seed,
+                     hq_search** out) {
+    if (!c || !params || !out) return HQ_ERR_ARG;
+    *out = nullptr;
+    if (params->population < 1 || params->imax < 1 || params->iTc < 1 || K < 1)
+        return fail(c, HQ_ERR_ARG, "bad SWASA parameters");
+    const float delta = params->delta;
+    auto eval = [c, delta](const float* pal, int P, int KK, double* costs) {
+        return hq_eval_population(c, pal, P, KK, delta, costs, nullptr);
+    };
+    hq_search* s = new hq_search{c, new SearchDriver(*params, K, seed, eval), K};
+    int rc = s->driver->start();
+    if (rc) {
+        delete s->driver;
+        delete s;
+        return rc;
+    }
+    *out = s;
+    return HQ_OK;
+}
+
+int hq_search_run(hq_search* s, int iterations, int* ran) {
+    if (!s || iterations < 0) return HQ_ERR_ARG;
+    return s->driver->run(iterations, ran, nullptr);
+}
+
+int hq_search_best(const hq_search* s, float* colors, double* best_error, int* iteration) {
+    if (!s) return HQ_ERR_ARG;
+    if (colors) std::copy(s->driver->best_colors().begin(), s->driver->best_colors().end(), colors);
+    if (best_error) *best_error = s->driver->best_error();
+    if (iteration) *iteration = s->driver->iteration();
+    return HQ_OK;
+}
+
+void hq_search_destroy(hq_search* s) {
+    if (!s) return;
+    delete s->driver;
+    delete s;
+}
+
+int hq_profile_enable(hq_ctx* c, int on) {
+    if (!c) return HQ_ERR_ARG;
+    c->prof = on != 0;
+    return HQ_OK;
+}
+
+int hq_profile_reset(hq_ctx* c) {
+    if (!c) return HQ_ERR_ARG;
+    c->prof_assign = c->prof_cost = c->prof_grid = c->prof_finalize = ProfSlot{};
+    return HQ_OK;
+}
+
+int hq_profile_get(hq_ctx* c, const char* kernel, double* total_ms, int64_t* launches) {
+    if (!c || !kernel) return HQ_ERR_ARG;
+    const ProfSlot* s = nullptr;
+    if (!std::strcmp(kernel, "assign")) s = &c->prof_assign;
+    else if (!std::strcmp(kernel, "cost")) s = &c->prof_cost;
+    else if (!std::strcmp(kernel, "grid")) s = &c->prof_grid;
+    else if (!std::strcmp(kernel, "finalize")) s = &c->prof_finalize;
+    else return fail(c, HQ_ERR_ARG, "unknown kernel '%s'", kernel);
+    if (total_ms) *total_ms = s->ms;
+    if (launches) *launches = s->launches;
+    return HQ_OK;
+}
+
+int hq_set_option(hq_ctx* c, const char* name, int value) {
+    if (!c || !name) return HQ_ERR_ARG;
+    if (!std::strcmp(name, "grid")) {
+        if (value != 0 && value != 16 && value != 32 && value != 64)
+            return fail(c, HQ_ERR_ARG, "grid must be 0, 16, 32 or 64");
+        c->G2 = value;
+    } else if (!std::strcmp(name, "cost_variant")) {
+        if (value != 0 && value != 1) return fail(c, HQ_ERR_ARG, "cost_variant must be 0 or 1");
+        c->cost_variant = value;
+    } else if (!std::strcmp(name, "assign_blocks_per_cu")) {
+        if (value < 1 || value > 64) return fail(c, HQ_ERR_ARG, "assign_blocks_per_cu in [1,64]");
+        c->assign_blocks_per_cu = value;
+    } else {
+        return fail(c, HQ_ERR_ARG, "unknown option '%s'", name);
+    }
+    return HQ_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,347 @@
+/*
+ * hq_oracle.c -- CPU oracle for the SWASA dE cost path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Plain-C restatement of the reference's per-candidate cost (SURVEY.md section 0,
+ * steps a-h) and of the original-image S-CIELAB (LabRef) precompute.  It is the
+ * checker for the HIP path and the "port" CPU baseline timed by bench.py; only
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load it.  The
+ * product library (hybridquantization_amd/csrc) never links it.
+ *
+ * PARITY STATUS: parity unpinned -- the reference ships no tests/golden vectors
+ * and cannot run here (no JVM/JavaCL, no OpenCL device); see oracle/oracle.py.
+ *
+ * Build: oracle/Makefile  (gcc -O2 -ffp-contract=off: no fma contraction, so the
+ * argmin distance is exactly ((dx*dx + dy*dy) + dz*dz) in fp32; explicit fmaf()
+ * where the reference's OpenCL calls fma()).
+ *
+ * Citations (reference tree src/plugins/dbrasseur/hybridquantization/):
+ *   CL = OptimizedConvolution.cl, IM = ImageManipulation.java, SW = SWASA.java
+ */
+#include <math.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* CL:77, CL:110, CL:118, CL:171 */
+static const float RGB2XYZm[3][3] = {{0.4124564f, 0.3575761f, 0.1804375f},
+                                     {0.2126729f, 0.7151522f, 0.0721750f},
+                                     {0.0193339f, 0.1191920f, 0.9503041f}};
+static const float XYZ2Oppm[3][3] = {{0.2787336f, 0.7218031f, -0.1065520f},
+                                     {-0.4487736f, 0.2898056f, -0.0771569f},
+                                     {0.0859513f, -0.5899859f, 0.5011089f}};
+static const float Opp2XYZm[3][3] = {{0.624045f, -1.87044f, -0.155304f},
+                                     {1.36606f, 0.931563f, 0.433903f},
+                                     {1.5013f, 1.41761f, 2.53307f}};
+static const float RGB2Oppm[3][3] = {{0.266413f, 0.603167f, 0.00113333f},
+                                     {-0.124957f, 0.0375879f, -0.133381f},
+                                     {-0.0803345f, -0.331467f, 0.449132f}};
+
+static inline float dot3(const float *v, const float *m) {
+    return (v[0] * m[0] + v[1] * m[1]) + v[2] * m[2];
+}
+
+/* CL:85-87, CL:194-196 */
+static inline float srgb_lin(float x) {
+    return x <= 0.04045f ? x / 12.92f : powf((x + 0.055f) / 1.055f, 2.4f);
+}
+
+/* CL:137 / CL:140 / CL:143 */
+static inline float lab_f(float t) {
+    const float d3 = 216.0f / 24389.0f, kappa = 24389.0f / 27.0f;
+    return t > d3 ? cbrtf(t) : fmaf(kappa, t, 16.0f) / 116.0f;
+}
+
+/* CL:124-145 Opp2LAB on one pixel. */
+static inline void opp2lab(const float *o, const float *illum, float *lab) {
+    float X = dot3(o, Opp2XYZm[0]), Y = dot3(o, Opp2XYZm[1]), Z = dot3(o, Opp2XYZm[2]);
+    float fx = lab_f(X / illum[0]), fy = lab_f(Y / illum[1]), fz = lab_f(Z / illum[2]);
+    lab[0] = 116.0f * fy - 16.0f;
+    lab[1] = 500.0f * (fx - fy);
+    lab[2] = 200.0f * (fy - fz);
+    lab[3] = 0.0f;
+}
+
+/* CL:256-263 reflection (valid for n >= half). */
+static inline int reflect(int j, int n) {
+    if (j < 0) return -j - 1;
+    if (j >= n) return 2 * n - j - 1;
+    return j;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Thread pool helper: run fn(arg, lo, hi) over [0, n) split in nthreads.    */
+/* ------------------------------------------------------------------------ */
+typedef void (*range_fn)(void *arg, int lo, int hi);
+typedef struct { range_fn fn; void *arg; int lo, hi; } job_t;
+static void *job_main(void *p) { job_t *j = (job_t *)p; j->fn(j->arg, j->lo, j->hi); return NULL; }
+
+static void parallel_for(int n, int nthreads, range_fn fn, void *arg) {
+    if (nthreads <= 1 || n < 2 * nthreads) { fn(arg, 0, n); return; }
+    pthread_t th[256];
+    job_t jobs[256];
+    if (nthreads > 256) nthreads = 256;
+    for (int t = 0; t < nthreads; ++t) {
+        jobs[t].fn = fn; jobs[t].arg = arg;
+        jobs[t].lo = (int)((long long)n * t / nthreads);
+        jobs[t].hi = (int)((long long)n * (t + 1) / nthreads);
+        pthread_create(&th[t], NULL, job_main, &jobs[t]);
+    }
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+}
+
+/* ------------------------------------------------------------------------ */
+/* (a,b) argmin: CL:179-193.  d = sqrtf(((dx*dx + dy*dy) + dz*dz)), strict <. */
+/* ------------------------------------------------------------------------ */
+static inline int argmin_px(const float *p, const float *pal4, int K) {
+    float dx = p[0] - pal4[0], dy = p[1] - pal4[1], dz = p[2] - pal4[2];
+    float best = sqrtf((dx * dx + dy * dy) + dz * dz);
+    int bi = 0;
+    for (int k = 1; k < K; ++k) {
+        const float *c = pal4 + 4 * k;
+        dx = p[0] - c[0]; dy = p[1] - c[1]; dz = p[2] - c[2];
+        float d = sqrtf((dx * dx + dy * dy) + dz * dz);
+        if (d < best) { best = d; bi = k; }
+    }
+    return bi;
+}
+
+int hqo_assign(const float *rgb4, long long n, const float *pal4, int K, int32_t *idx,
+               int32_t *used) {
+    if (used) memset(used, 0, sizeof(int32_t) * (size_t)K);
+    for (long long i = 0; i < n; ++i) {
+        int k = argmin_px(rgb4 + 4 * i, pal4, K);
+        if (idx) idx[i] = k;
+        if (used) used[k] = 1;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Candidate cost: steps a-h.                                                */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    const float *rgb4, *lab4, *pal4, *k1, *k2, *k3, *absk3, *illum;
+    int w, h, K, half;
+    int32_t *idx;        /* [N] */
+    float *opp;          /* [N][3] */
+    float *t1, *t2;      /* [N][3] horizontal results (row-major) */
+    float *t3;           /* [N] */
+    float *err;          /* [N] */
+    int32_t *used_tls;   /* [nthreads][K] (only for assign) */
+    int nthreads;
+} eval_ctx;
+
+typedef struct { eval_ctx *c; int tid; } assign_arg;
+
+static void assign_rows(void *a, int lo, int hi) {
+    eval_ctx *c = (eval_ctx *)a;
+    float opp_pal[256 * 3];
+    float *op = opp_pal;
+    float *heap = NULL;
+    if (c->K > 256) { heap = (float *)malloc(sizeof(float) * 3 * (size_t)c->K); op = heap; }
+    for (int k = 0; k < c->K; ++k) {            /* CL:194-198 */
+        const float *col = c->pal4 + 4 * k;
+        float lin[3] = {srgb_lin(col[0]), srgb_lin(col[1]), srgb_lin(col[2])};
+        for (int i = 0; i < 3; ++i) op[3 * k + i] = dot3(lin, RGB2Oppm[i]);
+    }
+    for (int y = lo; y < hi; ++y) {
+        for (int x = 0; x < c->w; ++x) {
+            long long p = (long long)y * c->w + x;
+            int k = argmin_px(c->rgb4 + 4 * p, c->pal4, c->K);
+            c->idx[p] = k;
+            c->opp[3 * p + 0] = op[3 * k + 0];
+            c->opp[3 * p + 1] = op[3 * k + 1];
+            c->opp[3 * p + 2] = op[3 * k + 2];
+        }
+    }
+    free(heap);
+}
+
+/* CL:234-272 computeScielabKernelsTemp: horizontal, per-tap sequential fma. */
+static void hpass_rows(void *a, int lo, int hi) {
+    eval_ctx *c = (eval_ctx *)a;
+    const int w = c->w, half = c->half;
+    for (int y = lo; y < hi; ++y) {
+        const float *row = c->opp + 3LL * y * w;
+        for (int x = 0; x < w; ++x) {
+            float a1[3] = {0, 0, 0}, a2[3] = {0, 0, 0}, a3 = 0.0f;
+            for (int i = -half, t = 0; i <= half; ++i, ++t) {
+                const float *in = row + 3 * reflect(x + i, w);
+                for (int ch = 0; ch < 3; ++ch) {
+                    a1[ch] = fmaf(in[ch], c->k1[4 * t + ch], a1[ch]);
+                    a2[ch] = fmaf(in[ch], c->k2[4 * t + ch], a2[ch]);
+                }
+                a3 = fmaf(in[0], c->k3[t], a3);
+            }
+            long long p = (long long)y * w + x;
+            memcpy(c->t1 + 3 * p, a1, sizeof a1);
+            memcpy(c->t2 + 3 * p, a2, sizeof a2);
+            c->t3[p] = a3;
+        }
+    }
+}
+
+/* CL:274-306 computeScielabKernelsEnd (vertical) + CL:124-145 + CL:201-209. */
+static void vpass_rows(void *a, int lo, int hi) {
+    eval_ctx *c = (eval_ctx *)a;
+    const int w = c->w, h = c->h, half = c->half;
+    for (int y = lo; y < hi; ++y) {
+        for (int x = 0; x < w; ++x) {
+            float o[3] = {0, 0, 0};
+            for (int i = -half, t = 0; i <= half; ++i, ++t) {
+                long long q = (long long)reflect(y + i, h) * w + x;
+                for (int ch = 0; ch < 3; ++ch)
+                    o[ch] = fmaf(c->t1[3 * q + ch], c->k1[4 * t + ch],
+                                 fmaf(c->t2[3 * q + ch], c->k2[4 * t + ch], o[ch]));
+                o[0] = fmaf(c->t3[q], c->absk3[t], o[0]);
+            }
+            float lab[4];
+            opp2lab(o, c->illum, lab);
+            long long p = (long long)y * w + x;
+            const float *r = c->lab4 + 4 * p;
+            float dl = r[0] - lab[0], da = r[1] - lab[1], db = r[2] - lab[2];
+            c->err[p] = sqrtf((dl * dl + da * da) + db * db);
+        }
+    }
+}
+
+/* IM:741-768 sumArray: recursive halving to `depth`, sequential double leaves. */
+static double sum_array(const float *a, long long s, long long e, int depth) {
+    if (e <= s) return 0.0;
+    if (depth <= 0) {
+        double sum = 0.0;
+        for (long long i = s; i < e; ++i) sum += (double)a[i];
+        return sum;
+    }
+    long long m = (s + e) / 2;
+    return sum_array(a, s, m, depth - 1) + sum_array(a, m, e, depth - 1);
+}
+
+/*
+ * One candidate evaluation (IM:647-712).  rgb4/lab4/pal4 are float4 inline
+ * arrays (.w = 0).  Outputs (all optional except cost): idx[N], used[K], err[N].
+ * cost = sum(err)/N + delta * #unused, summed like IM:736-768 with `depth`.
+ * Also returns the raw fp64 error sum in *err_sum (optional).
+ */
+int hqo_eval(const float *rgb4, const float *lab4, int w, int h, const float *pal4, int K,
+             const float *k1, const float *k2, const float *k3, const float *absk3, int half,
+             const float *illum, float delta, int depth, int nthreads, int32_t *idx_out,
+             int32_t *used_out, float *err_out, double *err_sum, double *cost) {
+    if (w < half || h < half || K < 1) return -1;
+    long long n = (long long)w * h;
+    eval_ctx c;
+    memset(&c, 0, sizeof c);
+    c.rgb4 = rgb4; c.lab4 = lab4; c.pal4 = pal4; c.k1 = k1; c.k2 = k2; c.k3 = k3;
+    c.absk3 = absk3; c.illum = illum; c.w = w; c.h = h; c.K = K; c.half = half;
+    c.nthreads = nthreads;
+    c.idx = idx_out ? idx_out : (int32_t *)malloc(sizeof(int32_t) * n);
+    c.opp = (float *)malloc(sizeof(float) * 3 * n);
+    c.t1 = (float *)malloc(sizeof(float) * 3 * n);
+    c.t2 = (float *)malloc(sizeof(float) * 3 * n);
+    c.t3 = (float *)malloc(sizeof(float) * n);
+    c.err = err_out ? err_out : (float *)malloc(sizeof(float) * n);
+    if (!c.idx || !c.opp || !c.t1 || !c.t2 || !c.t3 || !c.err) return -2;
+
+    parallel_for(h, nthreads, assign_rows, &c);
+    parallel_for(h, nthreads, hpass_rows, &c);
+    parallel_for(h, nthreads, vpass_rows, &c);
+
+    int32_t *used = used_out ? used_out : (int32_t *)calloc((size_t)K, sizeof(int32_t));
+    memset(used, 0, sizeof(int32_t) * (size_t)K);
+    for (long long i = 0; i < n; ++i) used[c.idx[i]] = 1;   /* CL:193 */
+    int unused = 0;
+    for (int k = 0; k < K; ++k) unused += used[k] == 0;
+    double s = sum_array(c.err, 0, n, depth);
+    if (err_sum) *err_sum = s;
+    *cost = s / (double)n + (double)delta * unused;           /* SW:74-82, IM:712 */
+
+    if (!used_out) free(used);
+    if (!idx_out) free(c.idx);
+    if (!err_out) free(c.err);
+    free(c.opp); free(c.t1); free(c.t2); free(c.t3);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* LabRef: RGB2XYZ (CL:79-90) then XYZtoScielab (IM:285-370).                */
+/* ------------------------------------------------------------------------ */
+int hqo_rgb_to_xyz(const float *R, const float *G, const float *B, long long n, float *xyz4) {
+    for (long long i = 0; i < n; ++i) {
+        float rgb[3] = {srgb_lin(R[i]), srgb_lin(G[i]), srgb_lin(B[i])};
+        for (int c = 0; c < 3; ++c) xyz4[4 * i + c] = dot3(rgb, RGB2XYZm[c]);
+        xyz4[4 * i + 3] = 0.0f;
+    }
+    return 0;
+}
+
+/* One 1-D pass of convolve4Channels / convolve1Channel (CL:2-74) along rows of
+ * a (rows x n) array of float3, with the filter k[T][4]; chans = 3 or 1 (.x). */
+static void conv_rows(const float *in, float *out, int rows, int n, const float *k, int half,
+                      int chans, int update) {
+    for (int r = 0; r < rows; ++r)
+        for (int j = 0; j < n; ++j) {
+            float acc[3] = {0, 0, 0};
+            for (int i = -half, t = 0; i <= half; ++i, ++t) {
+                const float *p = in + 3LL * ((long long)r * n + reflect(j + i, n));
+                for (int c = 0; c < chans; ++c) acc[c] = fmaf(p[c], k[4 * t + c], acc[c]);
+            }
+            float *o = out + 3LL * ((long long)r * n + j);
+            for (int c = 0; c < chans; ++c) o[c] = update ? o[c] + acc[c] : acc[c];
+        }
+}
+
+/* transpose (rows x n) float3 -> (n x rows) */
+static void transpose3(const float *in, float *out, int rows, int n) {
+    for (int r = 0; r < rows; ++r)
+        for (int j = 0; j < n; ++j)
+            for (int c = 0; c < 3; ++c) out[3LL * ((long long)j * rows + r) + c] = in[3LL * ((long long)r * n + j) + c];
+}
+
+int hqo_xyz_to_scielab(const float *xyz4, int w, int h, const float *k1, const float *k2,
+                       const float *k3, const float *absk3, int half, const float *illum,
+                       float *lab4) {
+    if (w < half || h < half) return -1;
+    long long n = (long long)w * h;
+    int T = 2 * half + 1;
+    float *opp = (float *)malloc(sizeof(float) * 3 * n);
+    float *tmp = (float *)malloc(sizeof(float) * 3 * n);
+    float *tmpT = (float *)malloc(sizeof(float) * 3 * n);
+    float *convT = (float *)calloc((size_t)(3 * n), sizeof(float));
+    float *conv = (float *)malloc(sizeof(float) * 3 * n);
+    float *k3v = (float *)calloc((size_t)(4 * T), sizeof(float));
+    float *ak3v = (float *)calloc((size_t)(4 * T), sizeof(float));
+    if (!opp || !tmp || !tmpT || !convT || !conv || !k3v || !ak3v) return -2;
+    for (int t = 0; t < T; ++t) { k3v[4 * t] = k3[t]; ak3v[4 * t] = absk3[t]; }
+    for (long long i = 0; i < n; ++i)                       /* CL:111-116 */
+        for (int c = 0; c < 3; ++c) opp[3 * i + c] = dot3(xyz4 + 4 * i, XYZ2Oppm[c]);
+    /* IM:319-346: per filter, horizontal along rows then vertical along columns
+     * (the OpenCL kernels transpose on store; we transpose explicitly).        */
+    const float *hk[3] = {k1, k2, k3v}, *vk[3] = {k1, k2, ak3v};
+    for (int f = 0; f < 3; ++f) {
+        int chans = f < 2 ? 3 : 1;
+        conv_rows(opp, tmp, h, w, hk[f], half, chans, 0);
+        transpose3(tmp, tmpT, h, w);                         /* now (w x h) */
+        conv_rows(tmpT, convT, w, h, vk[f], half, chans, f > 0);
+    }
+    transpose3(convT, conv, w, h);
+    for (long long i = 0; i < n; ++i) opp2lab(conv + 3 * i, illum, lab4 + 4 * i);
+    free(opp); free(tmp); free(tmpT); free(convT); free(conv); free(k3v); free(ak3v);
+    return 0;
+}
+
+/* CL:201-209 CIEDE(-DCIE76) + IM:886-893 (computeError's host loop). */
+double hqo_compute_error(const float *orig4, const float *quant4, long long n, float *err_img4) {
+    double error = 0.0;
+    for (long long i = 0; i < n; ++i) {
+        const float *a = orig4 + 4 * i, *b = quant4 + 4 * i;
+        float dl = a[0] - b[0], da = a[1] - b[1], db = a[2] - b[2];
+        float e = sqrtf((dl * dl + da * da) + db * db);
+        if (err_img4) {
+            float v = ((255 - e) * (255 - e)) / (255 * 255);
+            err_img4[4 * i] = err_img4[4 * i + 1] = err_img4[4 * i + 2] = v;
+        }
+        error += e;
+    }
+    return error / (double)n;
+}

@@ -1,0 +1,34 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libhq on the GPU)")
+
+
+def _gpu_available() -> bool:
+    try:
+        import hybridquantization_amd as hq
+
+        import ctypes
+
+        n = ctypes.c_int(0)
+        hq.load().hq_device_count(ctypes.byref(n))
+        return n.value > 0
+    except OSError:
+        return False
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    """Skip-free guard: a gpu-marked test run without a device is an error."""
+    if not _gpu_available():
+        pytest.fail("gpu test requested but no HIP device / libhq.so")
+    return 0

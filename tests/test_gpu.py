@@ -1,0 +1,281 @@
+"""GPU parity tests: libhq (HIP, gfx950) vs the CPU oracle, through the C ABI.
+
+Bar: palette indices and used flags bit-exact; costs within 1e-4 relative
+(the north-star tolerance; we assert tighter where the oracle is fast);
+LabRef within 2e-4 absolute on Lab values in [-128, 100].
+"""
+
+import os
+
+import numpy as np
+import pytest
+
+import c_oracle
+import hybridquantization_amd as hq
+import oracle as o
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+COST_RTOL = 1e-4  # north-star tolerance on the summed dE cost
+
+
+@pytest.fixture(scope="module")
+def filt():
+    return o.design_filters()
+
+
+@pytest.fixture()
+def ip(gpu):
+    m = hq.ImageManipulation(hq.deltaETypes.CIE76, device=gpu)
+    assert m.getOpenCLAvailable()
+    sp = hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
+    m.illum = sp.illuminant
+    yield m
+    m.close()
+
+
+def load_case(name):
+    g = np.load(os.path.join(GOLD, f"{name}.npz"))
+    img = g["rgb_u8"].astype(np.float32) / np.float32(255)
+    return g, img[:, 0].copy(), img[:, 1].copy(), img[:, 2].copy()
+
+
+# ---------------------------------------------------------------------------
+# LabRef / colour conversions (IM:100, IM:285)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ["case_64x48_k16", "case_97x53_k64"])
+def test_labref_on_device_matches_oracle(ip, name):
+    g, R, G, B = load_case(name)
+    w = int(g["w"])
+    ip.setImage(o.inline_rgba(R, G, B).reshape(-1), None, w, ip.illum)
+    lab = ip.getLabRef().reshape(-1, 4)
+    np.testing.assert_allclose(lab, g["lab"], atol=2e-4)
+
+
+def test_rgb_to_xyz_and_xyz_to_scielab(ip, filt):
+    g, R, G, B = load_case("case_97x53_k64")
+    w = int(g["w"])
+    xyz = ip.RGBtoXYZ(R, G, B).reshape(-1, 4)
+    np.testing.assert_allclose(xyz, o.rgb_to_xyz(R, G, B), rtol=1e-5, atol=1e-7)
+    lab = ip.XYZtoScielab(xyz.reshape(-1), None, None, w, filt.illum).reshape(-1, 4)
+    np.testing.assert_allclose(lab, g["lab"], atol=2e-4)
+
+
+def test_labref_256_checksum(ip):
+    g, R, G, B = load_case("case_256_k16")
+    ip.setImage(o.inline_rgba(R, G, B).reshape(-1), None, 256, ip.illum)
+    lab = ip.getLabRef().reshape(-1, 4)
+    np.testing.assert_allclose(np.abs(lab[:, :3].astype(np.float64)).sum(0), g["lab_checksum"],
+                               rtol=1e-6)
+    np.testing.assert_allclose(lab[:512], g["lab_rows"], atol=2e-4)
+
+
+# ---------------------------------------------------------------------------
+# Candidate evaluation (IM:620-727): golden fixtures
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("grid", [64, 32, 16, 0])
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("name", ["case_64x48_k16", "case_97x53_k64"])
+def test_eval_golden(ip, name, grid, variant):
+    g, R, G, B = load_case(name)
+    w = int(g["w"])
+    ip.setOption("grid", grid)
+    ip.setOption("cost_variant", variant)
+    ip.setImage(o.inline_rgba(R, G, B).reshape(-1), g["lab"].reshape(-1), w, ip.illum)
+    pals = g["palettes"]
+    costs, used = ip.computeQuantizationErrorPopulation(pals.reshape(len(pals), -1), 2.0,
+                                                        return_used=True)
+    np.testing.assert_allclose(costs, g["costs"], rtol=1e-6)
+    np.testing.assert_array_equal(used, g["used"])
+    for p in range(len(pals)):
+        np.testing.assert_array_equal(ip.getIndices(p), g["idx"][p])
+
+
+def test_eval_config1_256_k16(ip):
+    g, R, G, B = load_case("case_256_k16")
+    ip.setImage(o.inline_rgba(R, G, B).reshape(-1), None, 256, ip.illum)  # device LabRef
+    costs, used = ip.computeQuantizationErrorPopulation(g["palettes"].reshape(4, -1), 2.0,
+                                                        return_used=True)
+    np.testing.assert_allclose(costs, g["costs"], rtol=1e-5)
+    np.testing.assert_array_equal(used, g["used"])
+    np.testing.assert_array_equal(ip.getIndices(0), g["idx0"])
+
+
+def test_eval_config2_1024_k64(ip, filt):
+    w = h = 1024
+    R, G, B = o.synthetic_image(w, h, seed=1)
+    rgba = o.inline_rgba(R, G, B)
+    ip.setImage(rgba.reshape(-1), None, w, ip.illum)
+    lab_dev = ip.getLabRef().reshape(-1, 4)
+    lab = c_oracle.srgb_to_scielab(R, G, B, filt, w)
+    np.testing.assert_allclose(lab_dev, lab, atol=2e-4)
+    pal = o.synthetic_palette(64, 2)
+    cost = ip.computeQuantizationErrorPopulation([pal.reshape(-1)], 2.0)[0]
+    ref, parts = c_oracle.eval_palette(rgba, lab, pal, filt, w, nthreads=8, return_parts=True)
+    np.testing.assert_array_equal(ip.getIndices(0), parts["idx"].astype(np.uint8))
+    assert abs(cost - ref) <= COST_RTOL * abs(ref) * 0.1
+
+
+# ---------------------------------------------------------------------------
+# argmin edge cases (CL:179-193), bit-exact
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("grid", [64, 32, 16, 0])
+def test_assign_edge_cases(ip, grid):
+    g = np.load(os.path.join(GOLD, "edge_assign.npz"))
+    px = g["px"]  # 4096 pixels -> 64 x 64 image, values partly outside [0, 1]
+    ip.setOption("grid", grid)
+    ip.setImage(px.reshape(-1), np.zeros_like(px).reshape(-1), 64, ip.illum)
+    for name in ("dup", "clamped", "k1", "k256", "ties"):
+        pal = g[f"pal_{name}"]
+        ip.computeQuantizationErrorPopulation([pal.reshape(-1)], 2.0)
+        np.testing.assert_array_equal(ip.getIndices(0), g[f"idx_{name}"], err_msg=name)
+
+
+@pytest.mark.parametrize("K", [1, 2, 7, 64, 255, 256])
+def test_assign_random_and_near_ties(ip, K):
+    rng = np.random.default_rng(K)
+    w = h = 128
+    px = np.zeros((w * h, 4), np.float32)
+    px[:, :3] = (rng.integers(0, 256, (w * h, 3)) / 255.0).astype(np.float32)
+    pal = o.synthetic_palette(K, 40 + K)
+    if K > 4:
+        # near-duplicates 1 ulp apart and exact duplicates: stress sqrt-collapse ties
+        pal[K // 2, :3] = np.nextafter(pal[0, :3], np.float32(1))
+        pal[K // 3, :3] = pal[1, :3]
+        pal[K - 1, :3] = px[5, :3]
+    ip.setImage(px.reshape(-1), np.zeros_like(px).reshape(-1), w, ip.illum)
+    ref_idx, ref_used = c_oracle.assign(px, pal)
+    for grid in (64, 16, 0):
+        ip.setOption("grid", grid)
+        _, used = ip.computeQuantizationErrorPopulation([pal.reshape(-1)], 2.0, return_used=True)
+        np.testing.assert_array_equal(ip.getIndices(0), ref_idx.astype(np.uint8))
+        np.testing.assert_array_equal(used[0], ref_used)
+
+
+def test_nonfinite_palette_falls_back_exactly(ip):
+    w = h = 32
+    px = np.zeros((w * h, 4), np.float32)
+    px[:, :3] = np.random.default_rng(3).random((w * h, 3), dtype=np.float32)
+    pal = o.synthetic_palette(16, 5)
+    pal[3, 1] = np.nan
+    pal[7, 0] = np.inf
+    ip.setImage(px.reshape(-1), np.zeros_like(px).reshape(-1), w, ip.illum)
+    ip.computeQuantizationErrorPopulation([pal.reshape(-1)], 2.0)
+    ref_idx, _ = c_oracle.assign(px, pal)
+    np.testing.assert_array_equal(ip.getIndices(0), ref_idx.astype(np.uint8))
+
+
+# ---------------------------------------------------------------------------
+# Row-block sharding: shards' partials add up to the full image
+# ---------------------------------------------------------------------------
+def test_row_block_shards_sum_to_full(gpu, filt):
+    w, h, K, P = 96, 90, 32, 3
+    R, G, B = o.synthetic_image(w, h, seed=4)
+    rgba = o.inline_rgba(R, G, B).reshape(-1)
+    pals = np.stack([o.synthetic_palette(K, 60 + p) for p in range(P)]).reshape(P, -1)
+    full = hq.ImageManipulation(device=gpu)
+    hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, full)
+    full.setImage(rgba, None, w, filt.illum)
+    lib = hq.load()
+    ref = np.zeros(P * (1 + K))
+    lib.hq_eval_population_partial(full.ctx, hq._lib.fptr(pals), P, K, hq._lib.dptr(ref))
+    for nshards in (2, 3, 7):
+        bounds = np.linspace(0, h, nshards + 1).astype(int)
+        acc = np.zeros(P * (1 + K))
+        for r0, r1 in zip(bounds[:-1], bounds[1:]):
+            sh = hq.ImageManipulation(device=gpu)
+            hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, sh)
+            sh.setImage(rgba, None, w, filt.illum, row_begin=r0, row_end=r1)
+            part = np.zeros(P * (1 + K))
+            hq._lib.check(lib.hq_eval_population_partial(sh.ctx, hq._lib.fptr(pals), P, K,
+                                                         hq._lib.dptr(part)), sh.ctx)
+            acc += part
+            sh.close()
+        acc = acc.reshape(P, 1 + K)
+        refp = ref.reshape(P, 1 + K)
+        np.testing.assert_allclose(acc[:, 0], refp[:, 0], rtol=1e-6)
+        np.testing.assert_array_equal(acc[:, 1:] > 0, refp[:, 1:] > 0)
+    full.close()
+
+
+# ---------------------------------------------------------------------------
+# Final quantize (IM:770) and error image (IM:858)
+# ---------------------------------------------------------------------------
+def test_quantize_matches_oracle(ip):
+    g, R, G, B = load_case("case_97x53_k64")
+    rgba = o.inline_rgba(R, G, B)
+    pal = g["palettes"][0]
+    q = ip.quantize(rgba.reshape(-1), pal.reshape(-1)).reshape(-1, 4)
+    ref, idx, used = o.quantize(rgba[:, :3], pal)
+    np.testing.assert_array_equal(q, ref)
+    np.testing.assert_array_equal(ip.lastUsedColors, used)
+
+
+@pytest.mark.parametrize("de", [hq.deltaETypes.CIE76, hq.deltaETypes.CIE94])
+def test_compute_error_matches_oracle(gpu, de):
+    g, R, G, B = load_case("case_97x53_k64")
+    m = hq.ImageManipulation(de, device=gpu)
+    rng = np.random.default_rng(0)
+    other = (g["lab"] + rng.normal(0, 2, g["lab"].shape)).astype(np.float32)
+    other[:, 3] = 0
+    img = np.zeros(g["lab"].size, np.float32)
+    mean = m.computeError(g["lab"].reshape(-1), other.reshape(-1), img)
+    e = o.ciede76(g["lab"], other) if de == hq.deltaETypes.CIE76 else o.ciede94(g["lab"], other)
+    assert abs(mean - float(np.mean(e.astype(np.float64)))) < 1e-5 * float(np.mean(e))
+    np.testing.assert_allclose(img.reshape(-1, 4)[:, 0],
+                               ((255 - e) * (255 - e) / (255 * 255)).astype(np.float32), rtol=1e-5)
+    m.close()
+
+
+# ---------------------------------------------------------------------------
+# SA search on the GPU (IM:383-591) vs the same native driver on oracle costs
+# ---------------------------------------------------------------------------
+def test_search_matches_host_driver_on_oracle_costs(ip, filt):
+    w, h, K = 48, 40, 8
+    R, G, B = o.synthetic_image(w, h, seed=8)
+    rgba = o.inline_rgba(R, G, B)
+    lab = c_oracle.srgb_to_scielab(R, G, B, filt, w)
+    ip.setImage(rgba.reshape(-1), lab.reshape(-1), w, filt.illum)
+    sw = hq.SWASA(population=3, imax=40, seed=77, t0=0.5)
+    best = ip.findBestQuantization(rgba.reshape(-1), lab.reshape(-1), w, K, sw, None, None,
+                                   filt.illum)
+    gpu_err = ip.bestError
+
+    def ev(ps):
+        return [c_oracle.eval_palette(rgba, lab, p, filt, w) for p in ps]
+
+    hbest, herr, _ = hq.SWASA(population=3, imax=40, seed=77, t0=0.5).search_host(K, ev)
+    # identical decisions unless an acceptance test lands within fp32 noise
+    assert abs(gpu_err - herr) <= 1e-5 * abs(herr)
+    np.testing.assert_array_equal(best, hbest)
+
+
+# ---------------------------------------------------------------------------
+# Full-size properties (4096^2, K = 256): determinism, grid == exhaustive,
+# fast == generic, shards == full.
+# ---------------------------------------------------------------------------
+def test_full_size_properties(gpu, filt):
+    w = h = 4096
+    K = 256
+    R, G, B = o.synthetic_image(w, h, seed=1)
+    m = hq.ImageManipulation(device=gpu)
+    hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
+    lib = hq.load()
+    hq._lib.check(lib.hq_set_image_planar_shard(m.ctx, hq._lib.fptr(R), hq._lib.fptr(G),
+                                                hq._lib.fptr(B), w, h, hq._lib.fptr(filt.illum),
+                                                0, h), m.ctx)
+    m.w, m.h = w, h
+    pals = np.stack([o.synthetic_palette(K, 2 + p) for p in range(2)]).reshape(2, -1)
+    c1 = m.computeQuantizationErrorPopulation(pals, 2.0)
+    idx1 = m.getIndices(1)
+    c2 = m.computeQuantizationErrorPopulation(pals, 2.0)
+    np.testing.assert_array_equal(c1, c2)  # deterministic reduction
+    m.setOption("grid", 0)
+    c3 = m.computeQuantizationErrorPopulation(pals, 2.0)
+    np.testing.assert_array_equal(m.getIndices(1), idx1)  # pruned == exhaustive argmin
+    np.testing.assert_array_equal(c3, c1)
+    m.setOption("cost_variant", 1)
+    c4 = m.computeQuantizationErrorPopulation(pals, 2.0)
+    np.testing.assert_allclose(c4, c1, rtol=1e-6)  # tiled == generic two-pass
+    assert np.all(np.isfinite(c1)) and np.all(c1 > 0)
+    m.close()

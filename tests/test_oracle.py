@@ -1,0 +1,166 @@
+"""CPU tests of the oracle: constants, golden fixtures, known answers, and the
+agreement of the two independent restatements (numpy and C).
+
+Parity status: the reference ships no vectors, so the fixtures
+are oracle-generated (tests/golden/make_golden.py) -- "parity unpinned" except
+for the java.util.Random known answers.
+"""
+
+import json
+import os
+
+import numpy as np
+import pytest
+
+import c_oracle
+import oracle as o
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_reference_constants_self_consistent():
+    # RGB2Oppm (CL:171) is XYZ2Oppm (CL:110) . RGB2XYZm (CL:77) rounded to ~6 digits
+    prod = o.XYZ2OPPM.astype(np.float64) @ o.RGB2XYZM.astype(np.float64)
+    np.testing.assert_allclose(o.RGB2OPPM, prod, rtol=2e-5, atol=2e-6)
+    # Opp2XYZm (CL:118) is the inverse of XYZ2Oppm to ~6 significant digits
+    inv = np.linalg.inv(o.XYZ2OPPM.astype(np.float64))
+    np.testing.assert_allclose(o.OPP2XYZM, inv, rtol=5e-5, atol=5e-5)
+    # D65 of SP:20 (note Z = 1.0883, not 1.08883)
+    assert o.D65.tolist() == [np.float32(0.95047), np.float32(1.0), np.float32(1.0883)]
+
+
+def test_default_filter_design():
+    f = o.design_filters()
+    assert o.samp_per_deg(72, 45.0) == (242, 11)
+    assert f.taps == 21 and f.half == 10  # IM:408 halfSize
+    # k3 is negative (weight -0.117686) and absk3 = |k3|
+    assert (f.k3 < 0).all() and np.array_equal(f.absk3, -f.k3)
+    assert (f.k1[:, 3] == 0).all() and (f.k2[:, 3] == 0).all()
+
+
+@pytest.mark.parametrize("dpi,vd,wp", [(72, 45.0, "D65"), (72, 45.0, "D50"), (96, 60.0, "D65"),
+                                       (150, 30.0, "D65")])
+def test_filters_golden(dpi, vd, wp):
+    g = np.load(os.path.join(GOLD, "filters.npz"))
+    f = o.design_filters(dpi, vd, wp)
+    tag = f"{dpi}_{int(vd)}_{wp}"
+    for name in ("k1", "k2", "k3", "absk3", "illum"):
+        np.testing.assert_array_equal(getattr(f, name), g[f"{name}_{tag}"])
+
+
+def test_java_random_known_answers():
+    with open(os.path.join(GOLD, "kat_java_random.json")) as fh:
+        kat = json.load(fh)
+    assert o.JavaRandom(42).next(32) == kat["seed42_nextInt"]
+    assert o.JavaRandom(0).next(32) == kat["seed0_nextInt"]
+    assert o.JavaRandom(42).next_double() == kat["seed42_nextDouble"]
+    r = o.JavaRandom(1234)
+    assert [float(r.next_float()) for _ in range(8)] == kat["seed1234_nextFloat_x8"]
+
+
+def test_reflect_index_matches_cl():
+    idx = o.reflect_index(12, 10)
+    assert idx[0, 0] == 9 and idx[0, 9] == 0 and idx[0, 10] == 0   # -10 -> 9, -1 -> 0
+    assert idx[11, 20] == 2   # 21 -> 2*12-21-1
+    with pytest.raises(ValueError):
+        o.reflect_index(9, 10)
+
+
+@pytest.mark.parametrize("name", ["case_64x48_k16", "case_97x53_k64"])
+def test_golden_case_numpy_and_c(name):
+    g = np.load(os.path.join(GOLD, f"{name}.npz"))
+    w = int(g["w"])
+    f = o.design_filters()
+    img = g["rgb_u8"].astype(np.float32) / np.float32(255)
+    R, G, B = img[:, 0].copy(), img[:, 1].copy(), img[:, 2].copy()
+    rgba = o.inline_rgba(R, G, B)
+    lab_c = c_oracle.srgb_to_scielab(R, G, B, f, w)
+    np.testing.assert_allclose(lab_c, g["lab"], atol=2e-4)
+    for p in range(g["palettes"].shape[0]):
+        cc, parts = c_oracle.eval_palette(rgba, g["lab"], g["palettes"][p], f, w, return_parts=True)
+        np.testing.assert_array_equal(parts["idx"], g["idx"][p])
+        np.testing.assert_array_equal(parts["used"], g["used"][p])
+        assert abs(cc - g["costs"][p]) <= 1e-6 * abs(g["costs"][p])
+
+
+def test_golden_256_config1():
+    g = np.load(os.path.join(GOLD, "case_256_k16.npz"))
+    w = int(g["w"])
+    f = o.design_filters()
+    img = g["rgb_u8"].astype(np.float32) / np.float32(255)
+    R, G, B = img[:, 0].copy(), img[:, 1].copy(), img[:, 2].copy()
+    lab = c_oracle.srgb_to_scielab(R, G, B, f, w)
+    np.testing.assert_allclose(np.abs(lab[:, :3].astype(np.float64)).sum(0), g["lab_checksum"],
+                               rtol=1e-6)
+    rgba = o.inline_rgba(R, G, B)
+    for p in range(4):
+        cc, parts = c_oracle.eval_palette(rgba, lab, g["palettes"][p], f, w, return_parts=True)
+        if p == 0:
+            np.testing.assert_array_equal(parts["idx"], g["idx0"])
+        assert abs(cc - g["costs"][p]) <= 1e-5 * abs(g["costs"][p])
+
+
+def test_edge_assign_golden():
+    g = np.load(os.path.join(GOLD, "edge_assign.npz"))
+    for name in ("dup", "clamped", "k1", "k256", "ties"):
+        idx, _ = c_oracle.assign(g["px"], g[f"pal_{name}"])
+        np.testing.assert_array_equal(idx, g[f"idx_{name}"])
+
+
+def test_duplicates_lowest_index_wins():
+    pal = np.zeros((4, 4), np.float32)
+    pal[:, :3] = [[0.2, 0.2, 0.2], [0.7, 0.7, 0.7], [0.2, 0.2, 0.2], [0.7, 0.7, 0.7]]
+    px = np.array([[0.21, 0.2, 0.2], [0.69, 0.7, 0.7]], np.float32)
+    idx, used = o.assign(px, pal)
+    assert idx.tolist() == [0, 1] and used.tolist() == [1, 1, 0, 0]
+
+
+def test_perfect_palette_cost_is_small_not_zero():
+    # LabRef and the candidate path use different matrices/orders
+    w, h = 32, 24
+    f = o.design_filters()
+    rng = np.random.default_rng(0)
+    cols = rng.integers(0, 256, (6, 3)).astype(np.float32) / np.float32(255)
+    sel = rng.integers(0, 6, w * h)
+    R, G, B = cols[sel, 0], cols[sel, 1], cols[sel, 2]
+    lab = c_oracle.srgb_to_scielab(R, G, B, f, w)
+    pal = np.zeros((6, 4), np.float32)
+    pal[:, :3] = cols
+    c = c_oracle.eval_palette(o.inline_rgba(R, G, B), lab, pal, f, w)
+    assert 0 < c < 5e-3
+
+
+def test_unused_penalty():
+    w, h = 16, 16
+    f = o.design_filters()
+    R = np.full(w * h, 0.5, np.float32)
+    lab = c_oracle.srgb_to_scielab(R, R, R, f, w)
+    pal = o.synthetic_palette(8, 3)
+    c, parts = c_oracle.eval_palette(o.inline_rgba(R, R, R), lab, pal, f, w, delta=2.0,
+                                     return_parts=True)
+    assert parts["used"].sum() == 1
+    # constant image -> constant quantized image -> uniform dE
+    e = parts["err"]
+    assert np.ptp(e) < 1e-3 * max(e.max(), 1e-6) + 1e-5
+    assert abs(c - (parts["err_sum"] / (w * h) + 2.0 * 7)) < 1e-9
+
+
+def test_sum_array_tree_matches_sequential():
+    a = np.random.default_rng(1).random(10001).astype(np.float32)
+    s4 = o.sum_array(a, 4)
+    assert abs(s4 - float(np.sum(a.astype(np.float64)))) < 1e-9
+    assert o.default_depth(8) == 4 and o.default_depth(16) == 5
+
+
+def test_swasa_trace_golden():
+    g = np.load(os.path.join(GOLD, "swasa_trace.npz"))
+
+    def cost(pal):
+        pal = np.asarray(pal, np.float32)[..., :3].astype(np.float64)
+        return float(np.sum((pal - 0.3) ** 2) + 0.01 * np.sum(np.sin(pal * 17)))
+
+    sw = o.Swasa(o.SwasaParams(population=4, imax=int(g["imax"])), int(g["seed"]))
+    tr = []
+    best, err = o.find_best_quantization(lambda ps: [cost(p) for p in ps], int(g["K"]), sw, trace=tr)
+    np.testing.assert_array_equal(np.array([[t[3]] + t[1] for t in tr]), g["trace"])
+    np.testing.assert_array_equal(best, g["best"])
