@@ -22,6 +22,8 @@
 
 #include <math.h>
 
+#include <algorithm>
+
 namespace hq {
 
 // ----------------------------------------------------------------------------
@@ -51,13 +53,23 @@ __device__ __forceinline__ float lab_f(float t) {  // CL:137
     return t > LAB_DELTA3 ? cbrtf(t) : fmaf(LAB_KAPPA, t, 16.0f) * (1.0f / 116.0f);
 }
 
+// Branch-free f(t) of CL:137 for the hot path: cube root by exp2(log2(t)/3)
+// refined with one Newton step (error ~1 ulp), linear segment selected.
+__device__ __forceinline__ float lab_f_fast(float t) {
+    const float tc = fmaxf(t, LAB_DELTA3);  // cbrt branch only used for t > delta^3 > 0
+    float y = __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(tc) * (1.0f / 3.0f));
+    y = fmaf(-(1.0f / 3.0f), fmaf(y * y, y, -tc) * __builtin_amdgcn_rcpf(y * y), y);
+    const float lin = fmaf(LAB_KAPPA, t, 16.0f) * (1.0f / 116.0f);
+    return t > LAB_DELTA3 ? y : lin;
+}
+
 // CL:124-145 Opp2LAB with reciprocal illuminant (hot path; fp32 tolerance).
 __device__ __forceinline__ float3 opp2lab_fast(float o0, float o1, float o2, float ix, float iy,
                                                float iz) {
     const float X = dot3(o0, o1, o2, c_Opp2XYZ + 0);
     const float Y = dot3(o0, o1, o2, c_Opp2XYZ + 3);
     const float Z = dot3(o0, o1, o2, c_Opp2XYZ + 6);
-    const float fx = lab_f(X * ix), fy = lab_f(Y * iy), fz = lab_f(Z * iz);
+    const float fx = lab_f_fast(X * ix), fy = lab_f_fast(Y * iy), fz = lab_f_fast(Z * iz);
     return make_float3(116.0f * fy - 16.0f, 500.0f * (fx - fy), 200.0f * (fy - fz));
 }
 
@@ -102,11 +114,16 @@ __device__ __forceinline__ int reflect_only(int j, int n) {
     return j;
 }
 
-// Exact argmin distance: no contraction (__f*_rn are never fused).
+// Exact argmin distance ((dx*dx + dy*dy) + dz*dz), never fused: hipcc's default
+// -ffp-contract=fast would otherwise turn it into FMAs (and differently at
+// different call sites), breaking bit-exactness against the oracle.
 __device__ __forceinline__ float dist2(float r, float g, float b, float4 c) {
-    const float dx = __fsub_rn(r, c.x), dy = __fsub_rn(g, c.y), dz = __fsub_rn(b, c.z);
-    return __fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz));
+#pragma clang fp contract(off)
+    const float dx = r - c.x, dy = g - c.y, dz = b - c.z;
+    return (dx * dx + dy * dy) + dz * dz;
 }
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <typename V>
 __device__ __forceinline__ V wave_sum(V v) {
@@ -133,11 +150,17 @@ __global__ __launch_bounds__(256) void prep_palette_kernel(PaletteArgs a) {
     }
     __syncthreads();
     if (k < a.K) {
-        uint8_t dup = 0;
-        for (int j = 0; j < k; ++j) {
+        // exact duplicate at a lower index?  8 independent LDS reads per step
+        // (a serial dependent loop here was latency-bound at ~30 us).
+        // Uniform trip count (every lane scans all K entries, broadcast reads)
+        // so the loads pipeline; only the comparison is predicated on j < k.
+        bool dupb = false;
+#pragma unroll 8
+        for (int j = 0; j < a.K; ++j) {
             const float4 o = s[j];
-            if (o.x == c.x && o.y == c.y && o.z == c.z) { dup = 1; break; }
+            dupb |= (j < k) & (o.x == c.x) & (o.y == c.y) & (o.z == c.z);
         }
+        const uint8_t dup = dupb ? 1 : 0;
         const float lr = srgb_lin(c.x), lg = srgb_lin(c.y), lb = srgb_lin(c.z);
         const float4 opp = make_float4(dot3(lr, lg, lb, c_RGB2Opp + 0),
                                        dot3(lr, lg, lb, c_RGB2Opp + 3),
@@ -266,29 +289,38 @@ __global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
 // Palette replicated REP times in LDS; lane l reads copy (l % REP) so that a
 // ds_read_b128 16-lane group never hits one bank position twice (REP = 16).
 // ----------------------------------------------------------------------------
-template <int REP>
-__device__ __forceinline__ int argmin_pixel(float r, float g, float b, const float4* s_pal,
-                                            int copy, const uint8_t* lvl1p, const uint8_t* lvl2p,
-                                            int G2, bool exh_pal, int K) {
+// Level-2 entry lookup: returns false (exhaustive) for pixels outside [0,1]^3
+// or NaN, and for palettes flagged non-finite.
+__device__ __forceinline__ bool lvl2_lookup(float r, float g, float b, const uint8_t* lvl2p,
+                                            int G2, bool exh_pal, uint4& e) {
     const bool inside = r >= 0.f && r <= 1.f && g >= 0.f && g <= 1.f && b >= 0.f && b <= 1.f;
-    uint4 L0 = make_uint4(0, 0, 0, 0), L1 = make_uint4(0, 0, 0, 0);
-    int cnt = 0;
-    bool exh = exh_pal || !inside;
-    if (!exh) {
+    e = make_uint4(0, 0, 0, 0);
+    if (exh_pal || !inside) return false;
+    const int ir = min((int)(r * (float)G2), G2 - 1);
+    const int ig = min((int)(g * (float)G2), G2 - 1);
+    const int ib = min((int)(b * (float)G2), G2 - 1);
+    e = *reinterpret_cast<const uint4*>(lvl2p + ((int64_t)(ir * G2 + ig) * G2 + ib) * 16);
+    return true;
+}
+
+template <int REP>
+__device__ __forceinline__ int argmin_from_entry(float r, float g, float b, uint4 L0, bool listed,
+                                                 const float4* s_pal, int copy,
+                                                 const uint8_t* lvl1p, int G2, int K) {
+    uint4 L1 = make_uint4(0, 0, 0, 0);
+    int cnt = listed ? (int)(L0.x & 0xff) : 0;
+    bool exh = !listed;
+    if (cnt == kOverflow) {  // level-2 overflow: the parent's level-1 list (rare)
         const int G1 = G2 >> 2;
-        const int ir = min((int)(r * (float)G2), G2 - 1);
-        const int ig = min((int)(g * (float)G2), G2 - 1);
-        const int ib = min((int)(b * (float)G2), G2 - 1);
-        L0 = *reinterpret_cast<const uint4*>(lvl2p + ((int64_t)(ir * G2 + ig) * G2 + ib) * 16);
+        const int ir = min((int)(r * (float)G2), G2 - 1) >> 2;
+        const int ig = min((int)(g * (float)G2), G2 - 1) >> 2;
+        const int ib = min((int)(b * (float)G2), G2 - 1) >> 2;
+        const uint4* e = reinterpret_cast<const uint4*>(
+            lvl1p + ((int64_t)(ir * G1 + ig) * G1 + ib) * 32);
+        L0 = e[0];
+        L1 = e[1];
         cnt = L0.x & 0xff;
-        if (cnt == kOverflow) {
-            const uint4* e = reinterpret_cast<const uint4*>(
-                lvl1p + ((int64_t)((ir >> 2) * G1 + (ig >> 2)) * G1 + (ib >> 2)) * 32);
-            L0 = e[0];
-            L1 = e[1];
-            cnt = L0.x & 0xff;
-            if (cnt == kOverflow) { exh = true; cnt = 0; }
-        }
+        if (cnt == kOverflow) { exh = true; cnt = 0; }
     }
     int bi = (L0.x >> 8) & 0xff;  // first candidate (lowest index)
     if (__any(cnt > 1)) {
@@ -337,14 +369,21 @@ __global__ __launch_bounds__(256) void assign_kernel(AssignArgs a) {
         const float4 r4 = *reinterpret_cast<const float4*>(a.R + q);
         const float4 g4 = *reinterpret_cast<const float4*>(a.G + q);
         const float4 b4 = *reinterpret_cast<const float4*>(a.B + q);
-        const float rr[4] = {r4.x, r4.y, r4.z, r4.w};
-        const float gg[4] = {g4.x, g4.y, g4.z, g4.w};
-        const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
+        // all four table loads in flight before any candidate loop
+        uint4 e0, e1, e2, e3;
+        const bool l0 = lvl2_lookup(r4.x, g4.x, b4.x, lvl2p, a.G2, exh_pal, e0);
+        const bool l1 = lvl2_lookup(r4.y, g4.y, b4.y, lvl2p, a.G2, exh_pal, e1);
+        const bool l2 = lvl2_lookup(r4.z, g4.z, b4.z, lvl2p, a.G2, exh_pal, e2);
+        const bool l3 = lvl2_lookup(r4.w, g4.w, b4.w, lvl2p, a.G2, exh_pal, e3);
         uint32_t packed = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int k = argmin_pixel<REP>(rr[j], gg[j], bb[j], s_pal, copy, lvl1p, lvl2p, a.G2,
-                                            exh_pal, a.K);
+#pragma unroll 1
+        for (int j = 0; j < 4; ++j) {  // not unrolled: one copy of the candidate loop
+            const float r = j == 0 ? r4.x : (j == 1 ? r4.y : (j == 2 ? r4.z : r4.w));
+            const float gv = j == 0 ? g4.x : (j == 1 ? g4.y : (j == 2 ? g4.z : g4.w));
+            const float b = j == 0 ? b4.x : (j == 1 ? b4.y : (j == 2 ? b4.z : b4.w));
+            const uint4 e = j == 0 ? e0 : (j == 1 ? e1 : (j == 2 ? e2 : e3));
+            const bool li = j == 0 ? l0 : (j == 1 ? l1 : (j == 2 ? l2 : l3));
+            const int k = argmin_from_entry<REP>(r, gv, b, e, li, s_pal, copy, lvl1p, a.G2, a.K);
             packed |= (uint32_t)k << (8 * j);
             if (q + j < a.n_ext) {
                 const uint32_t bit = 1u << (k & 31);
@@ -369,19 +408,82 @@ struct CostTaps {
     float h[kNumFilt][2 * HALF + 1];
 };
 
-template <int HALF, int RW, int TH, int RV, int DE>
-__global__ __launch_bounds__(256, 2) void cost_tile_kernel(CostArgs a, CostTaps<HALF> taps) {
+// Vertical pass of filters [f0, f1) of one opponent channel: RV outputs per
+// thread from RV + 2*HALF gathered inputs; results to s_v[f][row][col].
+template <int HALF, int RV, int TH, int RW>
+__device__ __forceinline__ void vpass_filters(const float (&o)[RV + 2 * HALF],
+                                              const CostTaps<HALF>& taps, int f0, int f1,
+                                              float* out) {
     constexpr int T = 2 * HALF + 1;
+#pragma unroll 1
+    for (int f = f0; f < f1; ++f) {
+        float acc[RV];
+#pragma unroll
+        for (int y = 0; y < RV; ++y) acc[y] = 0.f;
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const float k = taps.v[f][t];
+#pragma unroll
+            for (int y = 0; y < RV; ++y) acc[y] = fmaf(o[y + t], k, acc[y]);
+        }
+#pragma unroll
+        for (int y = 0; y < RV; ++y) out[(f * TH + y) * RW] = acc[y];
+    }
+}
+
+// Horizontal pass of filters [f0, f1) of one channel for a 4-column run:
+// 4 + 2*HALF inputs per filter read as ds_read_b128 from s_v.
+template <int HALF, int TH, int RW>
+__device__ __forceinline__ void hpass_filters(const float4* src, const CostTaps<HALF>& taps,
+                                              int f0, int f1, float (&acc)[4]) {
+    constexpr int T = 2 * HALF + 1;
+    constexpr int NQ = (4 + 2 * HALF + 3) / 4;
+#pragma unroll
+    for (int xo = 0; xo < 4; ++xo) acc[xo] = 0.f;
+    static_assert(NQ == 6, "the asm barrier below names six vectors");
+#pragma unroll 1
+    for (int f = f0; f < f1; ++f) {
+        float in[4 * NQ];
+        const f32x4* row = reinterpret_cast<const f32x4*>(src + (f * TH * RW) / 4);
+        f32x4 v0 = row[0], v1 = row[1], v2 = row[2], v3 = row[3], v4 = row[4], v5 = row[5];
+        // One opaque barrier over all six loads: keeps them whole ds_read_b128
+        // (scalar reads re-paired at odd offsets were 4-way conflicted) and lets
+        // all six be in flight before a single wait.
+        asm volatile("" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+v"(v4), "+v"(v5));
+        const f32x4 vv[NQ] = {v0, v1, v2, v3, v4, v5};
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            in[4 * q] = vv[q].x; in[4 * q + 1] = vv[q].y; in[4 * q + 2] = vv[q].z;
+            in[4 * q + 3] = vv[q].w;
+        }
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const float k = taps.h[f][t];
+#pragma unroll
+            for (int xo = 0; xo < 4; ++xo) acc[xo] = fmaf(in[xo + t], k, acc[xo]);
+        }
+    }
+}
+
+template <int HALF, int RW, int TH, int RV, int DE, int OCC>
+__global__ __launch_bounds__(256, OCC) void cost_tile_kernel(CostArgs a, CostTaps<HALF> taps) {
     constexpr int TW = RW - 2 * HALF;
     constexpr int RH = TH + 2 * HALF;
     constexpr int NIN = RV + 2 * HALF;
     constexpr int NRUN = TW / 4;
     static_assert(RW * (TH / RV) == 256, "one V item per thread");
     static_assert(TW % 4 == 0, "4-wide H runs");
-    __shared__ __attribute__((aligned(16))) float s_v[kNumFilt * TH * RW];
-    __shared__ __attribute__((aligned(16))) float4 s_opp[kMaxK];
-    __shared__ uint8_t s_idx[RH * RW];
+    static_assert(TH * 32 <= 512, "at most two H rounds");
+    // s_v is float4-typed so the H-pass reads stay ds_read_b128 (a float-typed
+    // array let the compiler split them into 4-way-conflicted ds_read2_b32).
+    __shared__ float4 s_v4[kNumFilt * TH * RW / 4];
+    // opponent table replicated OPP_REP times; lane l reads copy (l % OPP_REP),
+    // spreading the random-index gathers over more bank positions.
+    constexpr int OPP_REP = 4;
+    __shared__ float4 s_opp[kMaxK * OPP_REP];
+    __shared__ __attribute__((aligned(16))) uint8_t s_idx[RH * RW];
     __shared__ double s_red[4];
+    float* s_v = reinterpret_cast<float*>(s_v4);
 
     const int p = blockIdx.y, tile = blockIdx.x, tid = threadIdx.x;
     const Geom& g = a.g;
@@ -389,66 +491,69 @@ __global__ __launch_bounds__(256, 2) void cost_tile_kernel(CostArgs a, CostTaps<
     const int x0 = tx * TW, y0 = g.r0 + ty * TH;
     const uint8_t* idx = a.idx + (int64_t)p * g.idx_pitch;
 
-    for (int k = tid; k < a.K; k += 256) s_opp[k] = a.opp[(int64_t)p * kMaxK + k];
-    for (int e = tid; e < RH * RW; e += 256) {
-        const int i = e / RW, j = e % RW;
-        int gy = reflect_clamp(y0 - HALF + i, g.H);
-        gy = min(max(gy, g.e0), g.e1 - 1);
-        const int gx = reflect_clamp(x0 - HALF + j, g.W);
-        s_idx[e] = idx[(int64_t)(gy - g.e0) * g.W + gx];
+    for (int e = tid; e < a.K * OPP_REP; e += 256)
+        s_opp[e] = a.opp[(int64_t)p * kMaxK + e / OPP_REP];
+    if (x0 - HALF >= 0 && x0 + TW + HALF <= g.W) {
+        // interior columns: each region row is RW contiguous bytes; aligned dword
+        // loads + alignbyte funnel shift (rows reflect vertically only)
+        constexpr int DW = RW / 4;
+        for (int e = tid; e < RH * DW; e += 256) {
+            const int i = e / DW, k = e % DW;
+            int gy = reflect_clamp(y0 - HALF + i, g.H);
+            gy = min(max(gy, g.e0), g.e1 - 1);
+            const int64_t base = (int64_t)(gy - g.e0) * g.W + (x0 - HALF);
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(idx + (base & ~(int64_t)3)) + k;
+            const uint32_t lo = src[0], hi = src[1];
+            reinterpret_cast<uint32_t*>(s_idx)[e] =
+                __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(base & 3));
+        }
+    } else {
+        for (int e = tid; e < RH * RW; e += 256) {
+            const int i = e / RW, j = e % RW;
+            int gy = reflect_clamp(y0 - HALF + i, g.H);
+            gy = min(max(gy, g.e0), g.e1 - 1);
+            const int gx = reflect_clamp(x0 - HALF + j, g.W);
+            s_idx[e] = idx[(int64_t)(gy - g.e0) * g.W + gx];
+        }
     }
     __syncthreads();
 
     // ---- vertical pass: thread = (region column c, rows [RV*gr, RV*gr+RV)) ----
+    // The filter loops are not unrolled so only one filter's 21 taps are live in
+    // SGPRs at a time (all 294 taps at once spill into VGPR lanes).
     {
         const int c = tid % RW, gr = tid / RW;
+        const int copy = tid & (OPP_REP - 1);
         float o0[NIN], o1[NIN], o2[NIN];
+        float wsum = 0.f;  // .w (= 0) is consumed so the gather stays one ds_read_b128
 #pragma unroll
         for (int r = 0; r < NIN; ++r) {
-            const float4 v = s_opp[s_idx[(gr * RV + r) * RW + c]];
+            const float4 v = s_opp[s_idx[(gr * RV + r) * RW + c] * OPP_REP + copy];
             o0[r] = v.x; o1[r] = v.y; o2[r] = v.z;
+            wsum += v.w;
         }
-#pragma unroll
-        for (int f = 0; f < kNumFilt; ++f) {
-            const float* o = filt_chan(f) == 0 ? o0 : (filt_chan(f) == 1 ? o1 : o2);
-            float acc[RV];
-#pragma unroll
-            for (int y = 0; y < RV; ++y) acc[y] = 0.f;
-#pragma unroll
-            for (int t = 0; t < T; ++t) {
-                const float k = taps.v[f][t];
-#pragma unroll
-                for (int y = 0; y < RV; ++y) acc[y] = fmaf(o[y + t], k, acc[y]);
-            }
-#pragma unroll
-            for (int y = 0; y < RV; ++y) s_v[(f * TH + gr * RV + y) * RW + c] = acc[y];
-        }
+        o0[0] += wsum;  // wsum == 0 exactly (prep_palette writes .w = 0)
+        float* out = s_v + (gr * RV) * RW + c;
+        vpass_filters<HALF, RV, TH, RW>(o0, taps, 0, 3, out);
+        vpass_filters<HALF, RV, TH, RW>(o1, taps, 3, 5, out);
+        vpass_filters<HALF, RV, TH, RW>(o2, taps, 5, 7, out);
     }
     __syncthreads();
 
     // ---- horizontal pass + Lab + dE: item = (row y, 4-column run j) ----
     double sum = 0.0;
-    for (int item = tid; item < TH * NRUN; item += 256) {
-        const int y = item / NRUN, j = item % NRUN;
-        float acc0[4] = {0.f, 0.f, 0.f, 0.f}, acc1[4] = {0.f, 0.f, 0.f, 0.f},
-              acc2[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int f = 0; f < kNumFilt; ++f) {
-            float in[4 + 2 * HALF + 3];
-            const float4* src = reinterpret_cast<const float4*>(&s_v[(f * TH + y) * RW + 4 * j]);
-#pragma unroll
-            for (int q = 0; q < (4 + 2 * HALF + 3) / 4; ++q) {
-                const float4 v = src[q];
-                in[4 * q] = v.x; in[4 * q + 1] = v.y; in[4 * q + 2] = v.z; in[4 * q + 3] = v.w;
-            }
-            float* acc = filt_chan(f) == 0 ? acc0 : (filt_chan(f) == 1 ? acc1 : acc2);
-#pragma unroll
-            for (int t = 0; t < T; ++t) {
-                const float k = taps.h[f][t];
-#pragma unroll
-                for (int xo = 0; xo < 4; ++xo) acc[xo] = fmaf(in[xo + t], k, acc[xo]);
-            }
-        }
+    // 32 run slots per row (NRUN used): a ds_read_b128 16-lane group then
+    // covers 16 distinct bank positions of one row (27 runs per row wrapped
+    // lanes into the next row's bank 0).
+    static_assert(NRUN <= 32, "runs per row");
+    for (int item = tid; item < TH * 32; item += 256) {
+        const int y = item >> 5, j = item & 31;
+        if (j >= NRUN) continue;
+        const float4* src = &s_v4[(y * RW) / 4 + j];
+        float acc0[4], acc1[4], acc2[4];
+        hpass_filters<HALF, TH, RW>(src, taps, 0, 3, acc0);
+        hpass_filters<HALF, TH, RW>(src, taps, 3, 5, acc1);
+        hpass_filters<HALF, TH, RW>(src, taps, 5, 7, acc2);
         const int gy = y0 + y, gx0 = x0 + 4 * j;
         if (gy < g.r1 && gx0 < g.W) {
             const int64_t off = (int64_t)(gy - g.r0) * g.lab_pitch + gx0;
@@ -474,6 +579,204 @@ __global__ __launch_bounds__(256, 2) void cost_tile_kernel(CostArgs a, CostTaps<
     __syncthreads();
     if (tid == 0)
         a.partial[(int64_t)p * a.ntiles + tile] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+}
+
+// ----------------------------------------------------------------------------
+// cost_persist: the same tile computation as cost_tile, as a persistent,
+// software-pipelined kernel.  Grid = a multiple of 8 workgroups (2 per CU);
+// workgroup w walks work items it = w', w' + G, ... where w' is an XCD-aware
+// relabelling (consecutive w' share an XCD) and it = tile * P + p, so the P
+// palettes of one tile read its LabRef through one L2.  While item i is
+// computed, item i+1's index rows (interior tiles), opponent table and LabRef
+// are already in flight into registers.
+// ----------------------------------------------------------------------------
+template <int HALF, int RW, int TH>
+struct CostPrefetch {
+    static constexpr int RH = TH + 2 * HALF;
+    static constexpr int DW = RW / 4;
+    static constexpr int NLD = (RH * DW + 255) / 256;
+    uint32_t lo[NLD], hi[NLD], sh[NLD];
+    float4 opp;
+    float4 lab[2][3];
+    bool interior;
+};
+
+template <int HALF, int RW, int TH>
+__device__ __forceinline__ void cost_prefetch(const CostArgs& a, int P, int it, int nitems, int tid,
+                                              CostPrefetch<HALF, RW, TH>& pf) {
+    using PF = CostPrefetch<HALF, RW, TH>;
+    constexpr int TW = RW - 2 * HALF;
+    constexpr int NRUN = TW / 4;
+    if (it >= nitems) return;
+    const Geom& g = a.g;
+    const int tile = it / P, p = it - tile * P;
+    const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
+    const int x0 = tx * TW, y0 = g.r0 + ty * TH;
+    const uint8_t* idx = a.idx + (int64_t)p * g.idx_pitch;
+    pf.interior = x0 - HALF >= 0 && x0 + TW + HALF <= g.W;
+    if (pf.interior) {
+#pragma unroll
+        for (int u = 0; u < PF::NLD; ++u) {
+            const int e = tid + 256 * u;
+            pf.lo[u] = pf.hi[u] = pf.sh[u] = 0;
+            if (e < PF::RH * PF::DW) {
+                const int i = e / PF::DW, k = e % PF::DW;
+                int gy = reflect_clamp(y0 - HALF + i, g.H);
+                gy = min(max(gy, g.e0), g.e1 - 1);
+                const int64_t base = (int64_t)(gy - g.e0) * g.W + (x0 - HALF);
+                const uint32_t* src =
+                    reinterpret_cast<const uint32_t*>(idx + (base & ~(int64_t)3)) + k;
+                pf.lo[u] = src[0];
+                pf.hi[u] = src[1];
+                pf.sh[u] = (uint32_t)(base & 3);
+            }
+        }
+    }
+    pf.opp = tid < a.K ? a.opp[(int64_t)p * kMaxK + tid] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const int item = tid + 256 * r;
+        const int y = item >> 5, j = item & 31;
+        const int gy = y0 + y, gx0 = x0 + 4 * j;
+        if (item < TH * 32 && j < NRUN && gy < g.r1 && gx0 < g.W) {
+            const int64_t off = (int64_t)(gy - g.r0) * g.lab_pitch + gx0;
+            pf.lab[r][0] = *reinterpret_cast<const float4*>(a.labL + off);
+            pf.lab[r][1] = *reinterpret_cast<const float4*>(a.labA + off);
+            pf.lab[r][2] = *reinterpret_cast<const float4*>(a.labB + off);
+        } else {
+            pf.lab[r][0] = pf.lab[r][1] = pf.lab[r][2] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+}
+
+template <int HALF, int RW, int TH, int RV, int DE>
+__global__ __launch_bounds__(256, 2) void cost_persist_kernel(CostArgs a, CostTaps<HALF> taps,
+                                                               int P, int nitems) {
+    using PF = CostPrefetch<HALF, RW, TH>;
+    constexpr int TW = RW - 2 * HALF;
+    constexpr int RH = TH + 2 * HALF;
+    constexpr int NIN = RV + 2 * HALF;
+    constexpr int NRUN = TW / 4;
+    constexpr int OPP_REP = 4;
+    static_assert(RW * (TH / RV) == 256, "one V item per thread");
+    static_assert(TW % 4 == 0 && NRUN <= 32 && TH * 32 <= 512, "H items");
+    __shared__ float4 s_v4[kNumFilt * TH * RW / 4];
+    __shared__ float4 s_opp[kMaxK * OPP_REP];
+    __shared__ __attribute__((aligned(16))) uint8_t s_idx[RH * RW];
+    __shared__ double s_red[2][4];
+    float* s_v = reinterpret_cast<float*>(s_v4);
+
+    const int tid = threadIdx.x;
+    const int G = gridDim.x;  // multiple of 8
+    const int lw = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+    const Geom& g = a.g;
+
+    PF pf;
+    cost_prefetch<HALF, RW, TH>(a, P, lw, nitems, tid, pf);
+    int prev_item = -1, parity = 0;
+    for (int it = lw; it < nitems; it += G) {
+        const int tile = it / P, p = it - tile * P;
+        const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
+        const int x0 = tx * TW, y0 = g.r0 + ty * TH;
+
+        // ---- stage item `it` into LDS (s_idx / s_opp are free: the previous
+        //      V-pass finished at the mid barrier; the H-pass does not read them)
+        if (pf.interior) {
+#pragma unroll
+            for (int u = 0; u < PF::NLD; ++u) {
+                const int e = tid + 256 * u;
+                if (e < RH * PF::DW)
+                    reinterpret_cast<uint32_t*>(s_idx)[e] =
+                        __builtin_amdgcn_alignbyte(pf.hi[u], pf.lo[u], pf.sh[u]);
+            }
+        } else {  // edge tile: reflected byte gathers (no prefetch)
+            const uint8_t* idx = a.idx + (int64_t)p * g.idx_pitch;
+            for (int e = tid; e < RH * RW; e += 256) {
+                const int i = e / RW, j = e % RW;
+                int gy = reflect_clamp(y0 - HALF + i, g.H);
+                gy = min(max(gy, g.e0), g.e1 - 1);
+                const int gx = reflect_clamp(x0 - HALF + j, g.W);
+                s_idx[e] = idx[(int64_t)(gy - g.e0) * g.W + gx];
+            }
+        }
+        if (tid < a.K) {
+#pragma unroll
+            for (int c = 0; c < OPP_REP; ++c) s_opp[tid * OPP_REP + c] = pf.opp;
+        }
+        float4 lab[2][3];
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) lab[r][q] = pf.lab[r][q];
+        __syncthreads();
+        // partial of the previous item (its wave sums are in s_red[parity ^ 1])
+        if (tid == 0 && prev_item >= 0) {
+            const double* r = s_red[parity ^ 1];
+            const int pt = prev_item / P, pp = prev_item - pt * P;
+            a.partial[(int64_t)pp * a.ntiles + pt] = (r[0] + r[1]) + (r[2] + r[3]);
+        }
+        // ---- next item's loads go in flight now
+        cost_prefetch<HALF, RW, TH>(a, P, it + G, nitems, tid, pf);
+
+        // ---- vertical pass
+        {
+            const int c = tid % RW, gr = tid / RW;
+            const int copy = tid & (OPP_REP - 1);
+            float o0[NIN], o1[NIN], o2[NIN];
+            float wsum = 0.f;
+#pragma unroll
+            for (int r = 0; r < NIN; ++r) {
+                const float4 v = s_opp[s_idx[(gr * RV + r) * RW + c] * OPP_REP + copy];
+                o0[r] = v.x; o1[r] = v.y; o2[r] = v.z;
+                wsum += v.w;
+            }
+            o0[0] += wsum;  // == 0: keeps the gather one ds_read_b128
+            float* out = s_v + (gr * RV) * RW + c;
+            vpass_filters<HALF, RV, TH, RW>(o0, taps, 0, 3, out);
+            vpass_filters<HALF, RV, TH, RW>(o1, taps, 3, 5, out);
+            vpass_filters<HALF, RV, TH, RW>(o2, taps, 5, 7, out);
+        }
+        __syncthreads();
+
+        // ---- horizontal pass + Lab + dE
+        double sum = 0.0;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int item = tid + 256 * r;
+            const int y = item >> 5, j = item & 31;
+            if (item >= TH * 32 || j >= NRUN) continue;
+            const float4* src = &s_v4[(y * RW) / 4 + j];
+            float acc0[4], acc1[4], acc2[4];
+            hpass_filters<HALF, TH, RW>(src, taps, 0, 3, acc0);
+            hpass_filters<HALF, TH, RW>(src, taps, 3, 5, acc1);
+            hpass_filters<HALF, TH, RW>(src, taps, 5, 7, acc2);
+            const int gy = y0 + y, gx0 = x0 + 4 * j;
+            if (gy < g.r1 && gx0 < g.W) {
+                const float Ls[4] = {lab[r][0].x, lab[r][0].y, lab[r][0].z, lab[r][0].w};
+                const float As[4] = {lab[r][1].x, lab[r][1].y, lab[r][1].z, lab[r][1].w};
+                const float Bs[4] = {lab[r][2].x, lab[r][2].y, lab[r][2].z, lab[r][2].w};
+                float part = 0.f;
+#pragma unroll
+                for (int xo = 0; xo < 4; ++xo) {
+                    const float3 l = opp2lab_fast(acc0[xo], acc1[xo], acc2[xo], a.inv_illum[0],
+                                                  a.inv_illum[1], a.inv_illum[2]);
+                    const float e = delta_e<DE>(Ls[xo], As[xo], Bs[xo], l.x, l.y, l.z);
+                    part += (gx0 + xo < g.W) ? e : 0.f;
+                }
+                sum += (double)part;
+            }
+        }
+        sum = wave_sum(sum);
+        if ((tid & 63) == 0) s_red[parity][tid >> 6] = sum;
+        prev_item = it;
+        parity ^= 1;
+    }
+    __syncthreads();
+    if (tid == 0 && prev_item >= 0) {
+        const double* r = s_red[parity ^ 1];
+        const int pt = prev_item / P, pp = prev_item - pt * P;
+        a.partial[(int64_t)pp * a.ntiles + pt] = (r[0] + r[1]) + (r[2] + r[3]);
+    }
 }
 
 // ----------------------------------------------------------------------------
@@ -541,14 +844,30 @@ __global__ __launch_bounds__(256) void finalize_kernel(FinalizeArgs a) {
     const int p = blockIdx.x, tid = threadIdx.x;
     __shared__ double s_red[4];
     __shared__ uint32_t s_mask[256];
-    double s = 0.0;
-    for (int t = tid; t < a.ntiles; t += 256) s += a.partial[(int64_t)p * a.ntiles + t];
+    // 8 independent partial sums per thread (fixed order) for memory-level parallelism
+    const double* part = a.partial + (int64_t)p * a.ntiles;
+    double s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int t0 = 0; t0 < a.ntiles; t0 += 256 * 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int t = t0 + u * 256 + tid;
+            s8[u] += t < a.ntiles ? part[t] : 0.0;
+        }
+    }
+    double s = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
     s = wave_sum(s);
     if ((tid & 63) == 0) s_red[tid >> 6] = s;
     // used: thread = (word w = tid & 7, block slice tid >> 3)
     uint32_t m = 0;
     const int w = tid & 7;
-    for (int b = tid >> 3; b < a.nblocks; b += 32) m |= a.used_mask[((int64_t)p * a.nblocks + b) * 8 + w];
+    const uint32_t* um = a.used_mask + (int64_t)p * a.nblocks * 8;
+    for (int b0 = tid >> 3; b0 < a.nblocks; b0 += 32 * 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int b = b0 + 32 * u;
+            m |= b < a.nblocks ? um[b * 8 + w] : 0u;
+        }
+    }
     s_mask[tid] = m;
     __syncthreads();
     double* out = a.out + (int64_t)p * (1 + a.K);
@@ -731,8 +1050,8 @@ hipError_t launch_build_grid(const GridArgs& a, int P, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_assign(const AssignArgs& a, int P, hipStream_t s) {
-    constexpr int REP = 16;
+template <int REP>
+static hipError_t launch_assign_rep(const AssignArgs& a, int P, hipStream_t s) {
     const size_t lds = (size_t)a.K * REP * sizeof(float4);
     static bool attr_set = false;  // allow > 64 KiB of dynamic LDS (160 KiB per CU on gfx950)
     if (!attr_set) {
@@ -744,6 +1063,13 @@ hipError_t launch_assign(const AssignArgs& a, int P, hipStream_t s) {
     }
     hipLaunchKernelGGL(assign_kernel<REP>, dim3(a.nblocks, P), dim3(256), lds, s, a);
     return hipGetLastError();
+}
+
+// rep: LDS replication of the palette (1, 4 or 16); lane l reads copy l % rep.
+hipError_t launch_assign(const AssignArgs& a, int P, int rep, hipStream_t s) {
+    if (rep == 16) return launch_assign_rep<16>(a, P, s);
+    if (rep == 1) return launch_assign_rep<1>(a, P, s);
+    return launch_assign_rep<4>(a, P, s);
 }
 
 static void make_taps10(const float* k1, const float* k2, const float* k3, const float* absk3,
@@ -765,21 +1091,45 @@ static void make_taps10(const float* k1, const float* k2, const float* k3, const
 constexpr int kFastHalf = 10, kFastRW = 128, kFastTH = 16, kFastRV = 8;
 constexpr int kFastTW = kFastRW - 2 * kFastHalf;
 
-void fast_tile_dims(int W, int own_rows, int* tiles_x, int* ntiles) {
+// tile rows of the fast path: 16 (RV 8, 2 WG/CU) or 8 (RV 4, 3 WG/CU)
+int fast_tile_rows(int tile_cfg) { return tile_cfg == 1 ? 8 : kFastTH; }
+
+void fast_tile_dims(int W, int own_rows, int tile_cfg, int* tiles_x, int* ntiles) {
+    const int th = fast_tile_rows(tile_cfg);
     *tiles_x = (W + kFastTW - 1) / kFastTW;
-    *ntiles = *tiles_x * ((own_rows + kFastTH - 1) / kFastTH);
+    *ntiles = *tiles_x * ((own_rows + th - 1) / th);
+}
+
+template <int TH, int RV, int OCC>
+static void launch_tile_cfg(const CostArgs& a, int P, const CostTaps<10>& t, int de,
+                            hipStream_t s) {
+    if (de == 0)
+        hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, 0, OCC>),
+                           dim3(a.ntiles, P), dim3(256), 0, s, a, t);
+    else
+        hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, 1, OCC>),
+                           dim3(a.ntiles, P), dim3(256), 0, s, a, t);
 }
 
 hipError_t launch_cost_fast(const CostArgs& a, int P, const float* k1, const float* k2,
-                            const float* k3, const float* absk3, int de, hipStream_t s) {
+                            const float* k3, const float* absk3, int de, int persistent,
+                            int tile_cfg, int num_cu, hipStream_t s) {
     CostTaps<10> t;
     make_taps10(k1, k2, k3, absk3, t);
-    if (de == 0)
-        hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, kFastTH, kFastRV, 0>),
-                           dim3(a.ntiles, P), dim3(256), 0, s, a, t);
-    else
-        hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, kFastTH, kFastRV, 1>),
-                           dim3(a.ntiles, P), dim3(256), 0, s, a, t);
+    if (persistent && tile_cfg == 0) {  // the persistent kernel exists for 16-row tiles
+        const int nitems = a.ntiles * P;
+        int G = std::min(2 * num_cu, nitems);
+        G = std::max(8, (G + 7) / 8 * 8);  // the XCD relabelling needs a multiple of 8
+        if (de == 0)
+            hipLaunchKernelGGL((cost_persist_kernel<kFastHalf, kFastRW, kFastTH, kFastRV, 0>),
+                               dim3(G), dim3(256), 0, s, a, t, P, nitems);
+        else
+            hipLaunchKernelGGL((cost_persist_kernel<kFastHalf, kFastRW, kFastTH, kFastRV, 1>),
+                               dim3(G), dim3(256), 0, s, a, t, P, nitems);
+        return hipGetLastError();
+    }
+    if (tile_cfg == 1) launch_tile_cfg<8, 4, 3>(a, P, t, de, s);
+    else launch_tile_cfg<kFastTH, kFastRV, 2>(a, P, t, de, s);
     return hipGetLastError();
 }
 

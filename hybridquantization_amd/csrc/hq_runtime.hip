@@ -21,10 +21,11 @@ namespace hq {
 // launchers from hq_kernels.hip
 hipError_t launch_prep_palette(const PaletteArgs&, int P, hipStream_t);
 hipError_t launch_build_grid(const GridArgs&, int P, hipStream_t);
-hipError_t launch_assign(const AssignArgs&, int P, hipStream_t);
-void fast_tile_dims(int W, int own_rows, int* tiles_x, int* ntiles);
+hipError_t launch_assign(const AssignArgs&, int P, int rep, hipStream_t);
+void fast_tile_dims(int W, int own_rows, int tile_cfg, int* tiles_x, int* ntiles);
 hipError_t launch_cost_fast(const CostArgs&, int P, const float* k1, const float* k2,
-                            const float* k3, const float* absk3, int de, hipStream_t);
+                            const float* k3, const float* absk3, int de, int persistent,
+                            int tile_cfg, int num_cu, hipStream_t);
 
 hipError_t launch_cost_generic(const GenArgs&, int de, hipStream_t);
 hipError_t launch_finalize(const FinalizeArgs&, int P, hipStream_t);
@@ -103,6 +104,8 @@ struct hq_ctx {
     int G2 = 64;           // argmin grid resolution (0 = exhaustive)
     int cost_variant = 0;  // 0 fast tiled, 1 generic
     int assign_blocks_per_cu = 8;
+    int assign_rep = 4;    // palette replication in the assign kernel's LDS
+    int tile_cfg = 0;      // cost tile: 0 = 16 rows (2 WG/CU), 1 = 8 rows (3 WG/CU)
 
     // comm
     ncclComm_t comm = nullptr;
@@ -284,7 +287,7 @@ int ensure_population(hq_ctx* c, int P, int K) {
     const int64_t l1p = round_up((int64_t)G1 * G1 * G1 * 32, 256);
     const int64_t l2p = round_up((int64_t)G2 * G2 * G2 * 16, 256);
     int tiles_x, ntiles;
-    fast_tile_dims(g.W, g.r1 - g.r0, &tiles_x, &ntiles);
+    fast_tile_dims(g.W, g.r1 - g.r0, c->tile_cfg, &tiles_x, &ntiles);
     const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
     const int64_t gen_blocks = (n_own + 255) / 256;
     const int64_t nparts = std::max<int64_t>(ntiles, gen_blocks);
@@ -337,13 +340,13 @@ int enqueue_eval(hq_ctx* c, int P, int K) {
                   c->d_pflags.as<int>(), c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(),
                   c->d_idx.as<uint8_t>(), c->d_used_mask.as<uint32_t>(), g.n_ext, g.idx_pitch,
                   l1p, l2p, K, c->G2, nblocks};
-    HIP_TRY(c, launch_assign(aa, P, s));
+    HIP_TRY(c, launch_assign(aa, P, c->assign_rep, s));
     if (c->prof) HIP_TRY(c, hipEventRecord(c->ev[2], s));
     int tiles_x, ntiles;
-    fast_tile_dims(g.W, g.r1 - g.r0, &tiles_x, &ntiles);
+    fast_tile_dims(g.W, g.r1 - g.r0, c->tile_cfg, &tiles_x, &ntiles);
     const float inv[3] = {1.0f / c->illum[0], 1.0f / c->illum[1], 1.0f / c->illum[2]};
     int nparts;
-    const bool fast = c->cost_variant == 0 && c->half == 10;
+    const bool fast = c->cost_variant != 1 && c->half == 10;
     if (fast) {
         CostArgs ca{};
         ca.idx = c->d_idx.as<uint8_t>();
@@ -358,7 +361,8 @@ int enqueue_eval(hq_ctx* c, int P, int K) {
         ca.ntiles = ntiles;
         std::memcpy(ca.inv_illum, inv, sizeof inv);
         HIP_TRY(c, launch_cost_fast(ca, P, c->k1.data(), c->k2.data(), c->k3.data(),
-                                    c->absk3.data(), c->de_type, s));
+                                    c->absk3.data(), c->de_type, c->cost_variant == 0,
+                                    c->tile_cfg, c->num_cu, s));
         nparts = ntiles;
     } else {
         HIP_TRY(c, c->d_gen_t.ensure(sizeof(float) * 7 * (size_t)g.n_ext));
@@ -828,8 +832,14 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
             return fail(c, HQ_ERR_ARG, "grid must be 0, 16, 32 or 64");
         c->G2 = value;
     } else if (!std::strcmp(name, "cost_variant")) {
-        if (value != 0 && value != 1) return fail(c, HQ_ERR_ARG, "cost_variant must be 0 or 1");
+        if (value < 0 || value > 2) return fail(c, HQ_ERR_ARG, "cost_variant must be 0, 1 or 2");
         c->cost_variant = value;
+    } else if (!std::strcmp(name, "cost_tile")) {
+        if (value != 0 && value != 1) return fail(c, HQ_ERR_ARG, "cost_tile in {0,1}");
+        c->tile_cfg = value;
+    } else if (!std::strcmp(name, "assign_rep")) {
+        if (value != 1 && value != 4 && value != 16) return fail(c, HQ_ERR_ARG, "assign_rep in {1,4,16}");
+        c->assign_rep = value;
     } else if (!std::strcmp(name, "assign_blocks_per_cu")) {
         if (value < 1 || value > 64) return fail(c, HQ_ERR_ARG, "assign_blocks_per_cu in [1,64]");
         c->assign_blocks_per_cu = value;

@@ -178,9 +178,11 @@ int hq_profile_enable(hq_ctx *ctx, int on);
 int hq_profile_get(hq_ctx *ctx, const char *kernel, double *total_ms, int64_t *launches);
 int hq_profile_reset(hq_ctx *ctx);
 
-/* Tuning knobs (testing / benchmarking): grid resolution of the exact argmin
- * pruning (G2 in {0 = exhaustive, 16, 32, 64}), and cost-kernel variant
- * (0 = tiled fast path, 1 = generic two-pass path). */
+/* Tuning knobs (testing / benchmarking): "grid" = resolution G2 of the exact
+ * argmin pruning (0 = exhaustive, 16, 32, 64); "cost_variant" = 0 persistent
+ * pipelined tiles (default), 1 generic two-pass path, 2 one-tile-per-workgroup;
+ * "assign_rep" = palette replication in LDS (1, 4, 16);
+ * "assign_blocks_per_cu". */
 int hq_set_option(hq_ctx *ctx, const char *name, int value);
 
 #ifdef __cplusplus

@@ -1,0 +1,71 @@
+"""Profiling driver: repeated population evaluations at a given size (for rocprofv3).
+
+python scripts/profile_eval.py [--size 4096] [--K 256] [--P 4] [--evals 10] [--grid 64]
+Prints per-kernel HIP-event averages and the end-to-end eval time.
+"""
+
+import argparse
+import ctypes as C
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import hybridquantization_amd as hq  # noqa: E402
+from hybridquantization_amd import _lib  # noqa: E402
+from bench import synthetic_planes  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=int, default=4096)
+    ap.add_argument("--K", type=int, default=256)
+    ap.add_argument("--P", type=int, default=4)
+    ap.add_argument("--evals", type=int, default=10)
+    ap.add_argument("--grid", type=int, default=64)
+    ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--tile", type=int, default=0)
+    ap.add_argument("--rep", type=int, default=4)
+    args = ap.parse_args()
+    lib = hq.load()
+    m = hq.ImageManipulation(device=0)
+    sp = hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
+    m.setOption("grid", args.grid)
+    m.setOption("cost_variant", args.variant)
+    m.setOption("cost_tile", args.tile)
+    m.setOption("assign_rep", args.rep)
+    W = H = args.size
+    R, G, B = synthetic_planes(W, H, 1)
+    _lib.check(lib.hq_set_image_planar_shard(m.ctx, _lib.fptr(R), _lib.fptr(G), _lib.fptr(B), W, H,
+                                             _lib.fptr(sp.illuminant), 0, H), m.ctx)
+    rng = np.random.default_rng(0)
+    pals = np.zeros((args.P, args.K, 4), np.float32)
+    pals[..., :3] = rng.random((args.P, args.K, 3), dtype=np.float32)
+    costs = np.zeros(args.P)
+    flat = pals.reshape(-1)
+    lib.hq_eval_population(m.ctx, _lib.fptr(flat), args.P, args.K, 2.0, _lib.dptr(costs), None)
+    lib.hq_profile_enable(m.ctx, 1)
+    t0 = time.perf_counter()
+    for _ in range(args.evals):
+        _lib.check(lib.hq_eval_population(m.ctx, _lib.fptr(flat), args.P, args.K, 2.0,
+                                          _lib.dptr(costs), None), m.ctx)
+    el = time.perf_counter() - t0
+    out = []
+    for k in ("grid", "assign", "cost", "finalize"):
+        ms = C.c_double()
+        n = C.c_int64()
+        lib.hq_profile_get(m.ctx, k.encode(), C.byref(ms), C.byref(n))
+        out.append(f"{k}={ms.value / max(n.value, 1):.4f}ms")
+    print(f"size={W} K={args.K} P={args.P} grid={args.grid} variant={args.variant} tile={args.tile} rep={args.rep}: "
+          f"{el / args.evals * 1e3:.3f} ms/eval-population, "
+          f"{W * H * args.P * args.evals / el / 1e6:.1f} Mpx*evals/s  ", " ".join(out),
+          "costs", costs.tolist())
+    m.close()
+
+
+if __name__ == "__main__":
+    main()
