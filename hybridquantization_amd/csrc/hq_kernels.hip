@@ -23,6 +23,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <cmath>
 
 namespace hq {
 
@@ -396,6 +397,7 @@ __global__ __launch_bounds__(256) void assign_kernel(AssignArgs a) {
     if (tid < 8) a.used_mask[((int64_t)p * a.nblocks + blockIdx.x) * 8 + tid] = s_used[tid];
 }
 
+
 // ----------------------------------------------------------------------------
 // cost_tile: grid (ntiles, P), block 256.  One workgroup = one TW x TH output
 // tile; region = (TH + 2*HALF) rows x RW cols of indices (RW = TW + 2*HALF).
@@ -410,18 +412,19 @@ struct CostTaps {
 
 // Vertical pass of filters [f0, f1) of one opponent channel: RV outputs per
 // thread from RV + 2*HALF gathered inputs; results to s_v[f][row][col].
-template <int HALF, int RV, int TH, int RW>
+// Taps [TLO, THI] only (the default filter set's narrow k1 filters have |taps|
+// below 1e-9 of their peak outside a short window; see trim_window()).
+template <int HALF, int RV, int TH, int RW, int TLO = 0, int THI = 2 * HALF>
 __device__ __forceinline__ void vpass_filters(const float (&o)[RV + 2 * HALF],
                                               const CostTaps<HALF>& taps, int f0, int f1,
                                               float* out) {
-    constexpr int T = 2 * HALF + 1;
 #pragma unroll 1
     for (int f = f0; f < f1; ++f) {
         float acc[RV];
 #pragma unroll
         for (int y = 0; y < RV; ++y) acc[y] = 0.f;
 #pragma unroll
-        for (int t = 0; t < T; ++t) {
+        for (int t = TLO; t <= THI; ++t) {
             const float k = taps.v[f][t];
 #pragma unroll
             for (int y = 0; y < RV; ++y) acc[y] = fmaf(o[y + t], k, acc[y]);
@@ -433,13 +436,11 @@ __device__ __forceinline__ void vpass_filters(const float (&o)[RV + 2 * HALF],
 
 // Horizontal pass of filters [f0, f1) of one channel for a 4-column run:
 // 4 + 2*HALF inputs per filter read as ds_read_b128 from s_v.
-template <int HALF, int TH, int RW>
+// Accumulates filters [f0, f1) into acc (caller zeroes it); taps [TLO, THI].
+template <int HALF, int TH, int RW, int TLO = 0, int THI = 2 * HALF>
 __device__ __forceinline__ void hpass_filters(const float4* src, const CostTaps<HALF>& taps,
                                               int f0, int f1, float (&acc)[4]) {
-    constexpr int T = 2 * HALF + 1;
     constexpr int NQ = (4 + 2 * HALF + 3) / 4;
-#pragma unroll
-    for (int xo = 0; xo < 4; ++xo) acc[xo] = 0.f;
     static_assert(NQ == 6, "the asm barrier below names six vectors");
 #pragma unroll 1
     for (int f = f0; f < f1; ++f) {
@@ -457,7 +458,7 @@ __device__ __forceinline__ void hpass_filters(const float4* src, const CostTaps<
             in[4 * q + 3] = vv[q].w;
         }
 #pragma unroll
-        for (int t = 0; t < T; ++t) {
+        for (int t = TLO; t <= THI; ++t) {
             const float k = taps.h[f][t];
 #pragma unroll
             for (int xo = 0; xo < 4; ++xo) acc[xo] = fmaf(in[xo + t], k, acc[xo]);
@@ -465,7 +466,52 @@ __device__ __forceinline__ void hpass_filters(const float4* src, const CostTaps<
     }
 }
 
-template <int HALF, int RW, int TH, int RV, int DE, int OCC>
+// The seven filters of both passes.  TRIM: the narrow k1.x / k1.y / k1.z filters
+// (f = 0, 3, 5) run over their significant-tap windows kTrimLo/Hi only
+// (|taps| outside are below 1e-9 of the filter's peak for the default filter
+// set; see trim_window_ok()).  Per-filter loops keep one filter's 21 taps live
+// in SGPRs (interleaving a channel's filters needs 63 and spills to VGPR lanes).
+constexpr int kTrimLo[3] = {7, 6, 5}, kTrimHi[3] = {13, 14, 15};
+
+template <int HALF, int RV, int TH, int RW, bool TRIM>
+__device__ __forceinline__ void vpass_all(const float (&o0)[RV + 2 * HALF],
+                                          const float (&o1)[RV + 2 * HALF],
+                                          const float (&o2)[RV + 2 * HALF],
+                                          const CostTaps<HALF>& taps, float* out) {
+    if constexpr (TRIM) {
+        vpass_filters<HALF, RV, TH, RW, kTrimLo[0], kTrimHi[0]>(o0, taps, 0, 1, out);
+        vpass_filters<HALF, RV, TH, RW>(o0, taps, 1, 3, out);
+        vpass_filters<HALF, RV, TH, RW, kTrimLo[1], kTrimHi[1]>(o1, taps, 3, 4, out);
+        vpass_filters<HALF, RV, TH, RW>(o1, taps, 4, 5, out);
+        vpass_filters<HALF, RV, TH, RW, kTrimLo[2], kTrimHi[2]>(o2, taps, 5, 6, out);
+        vpass_filters<HALF, RV, TH, RW>(o2, taps, 6, 7, out);
+    } else {
+        vpass_filters<HALF, RV, TH, RW>(o0, taps, 0, 3, out);
+        vpass_filters<HALF, RV, TH, RW>(o1, taps, 3, 5, out);
+        vpass_filters<HALF, RV, TH, RW>(o2, taps, 5, 7, out);
+    }
+}
+
+template <int HALF, int TH, int RW, bool TRIM>
+__device__ __forceinline__ void hpass_all(const float4* src, const CostTaps<HALF>& taps,
+                                          float (&acc0)[4], float (&acc1)[4], float (&acc2)[4]) {
+#pragma unroll
+    for (int xo = 0; xo < 4; ++xo) acc0[xo] = acc1[xo] = acc2[xo] = 0.f;
+    if constexpr (TRIM) {
+        hpass_filters<HALF, TH, RW, kTrimLo[0], kTrimHi[0]>(src, taps, 0, 1, acc0);
+        hpass_filters<HALF, TH, RW>(src, taps, 1, 3, acc0);
+        hpass_filters<HALF, TH, RW, kTrimLo[1], kTrimHi[1]>(src, taps, 3, 4, acc1);
+        hpass_filters<HALF, TH, RW>(src, taps, 4, 5, acc1);
+        hpass_filters<HALF, TH, RW, kTrimLo[2], kTrimHi[2]>(src, taps, 5, 6, acc2);
+        hpass_filters<HALF, TH, RW>(src, taps, 6, 7, acc2);
+    } else {
+        hpass_filters<HALF, TH, RW>(src, taps, 0, 3, acc0);
+        hpass_filters<HALF, TH, RW>(src, taps, 3, 5, acc1);
+        hpass_filters<HALF, TH, RW>(src, taps, 5, 7, acc2);
+    }
+}
+
+template <int HALF, int RW, int TH, int RV, int DE, int OCC, bool TRIM>
 __global__ __launch_bounds__(256, OCC) void cost_tile_kernel(CostArgs a, CostTaps<HALF> taps) {
     constexpr int TW = RW - 2 * HALF;
     constexpr int RH = TH + 2 * HALF;
@@ -534,9 +580,7 @@ __global__ __launch_bounds__(256, OCC) void cost_tile_kernel(CostArgs a, CostTap
         }
         o0[0] += wsum;  // wsum == 0 exactly (prep_palette writes .w = 0)
         float* out = s_v + (gr * RV) * RW + c;
-        vpass_filters<HALF, RV, TH, RW>(o0, taps, 0, 3, out);
-        vpass_filters<HALF, RV, TH, RW>(o1, taps, 3, 5, out);
-        vpass_filters<HALF, RV, TH, RW>(o2, taps, 5, 7, out);
+        vpass_all<HALF, RV, TH, RW, TRIM>(o0, o1, o2, taps, out);
     }
     __syncthreads();
 
@@ -551,9 +595,7 @@ __global__ __launch_bounds__(256, OCC) void cost_tile_kernel(CostArgs a, CostTap
         if (j >= NRUN) continue;
         const float4* src = &s_v4[(y * RW) / 4 + j];
         float acc0[4], acc1[4], acc2[4];
-        hpass_filters<HALF, TH, RW>(src, taps, 0, 3, acc0);
-        hpass_filters<HALF, TH, RW>(src, taps, 3, 5, acc1);
-        hpass_filters<HALF, TH, RW>(src, taps, 5, 7, acc2);
+        hpass_all<HALF, TH, RW, TRIM>(src, taps, acc0, acc1, acc2);
         const int gy = y0 + y, gx0 = x0 + 4 * j;
         if (gy < g.r1 && gx0 < g.W) {
             const int64_t off = (int64_t)(gy - g.r0) * g.lab_pitch + gx0;
@@ -649,7 +691,7 @@ __device__ __forceinline__ void cost_prefetch(const CostArgs& a, int P, int it, 
     }
 }
 
-template <int HALF, int RW, int TH, int RV, int DE>
+template <int HALF, int RW, int TH, int RV, int DE, bool TRIM>
 __global__ __launch_bounds__(256, 2) void cost_persist_kernel(CostArgs a, CostTaps<HALF> taps,
                                                                int P, int nitems) {
     using PF = CostPrefetch<HALF, RW, TH>;
@@ -732,9 +774,7 @@ __global__ __launch_bounds__(256, 2) void cost_persist_kernel(CostArgs a, CostTa
             }
             o0[0] += wsum;  // == 0: keeps the gather one ds_read_b128
             float* out = s_v + (gr * RV) * RW + c;
-            vpass_filters<HALF, RV, TH, RW>(o0, taps, 0, 3, out);
-            vpass_filters<HALF, RV, TH, RW>(o1, taps, 3, 5, out);
-            vpass_filters<HALF, RV, TH, RW>(o2, taps, 5, 7, out);
+            vpass_all<HALF, RV, TH, RW, TRIM>(o0, o1, o2, taps, out);
         }
         __syncthreads();
 
@@ -747,9 +787,7 @@ __global__ __launch_bounds__(256, 2) void cost_persist_kernel(CostArgs a, CostTa
             if (item >= TH * 32 || j >= NRUN) continue;
             const float4* src = &s_v4[(y * RW) / 4 + j];
             float acc0[4], acc1[4], acc2[4];
-            hpass_filters<HALF, TH, RW>(src, taps, 0, 3, acc0);
-            hpass_filters<HALF, TH, RW>(src, taps, 3, 5, acc1);
-            hpass_filters<HALF, TH, RW>(src, taps, 5, 7, acc2);
+            hpass_all<HALF, TH, RW, TRIM>(src, taps, acc0, acc1, acc2);
             const int gy = y0 + y, gx0 = x0 + 4 * j;
             if (gy < g.r1 && gx0 < g.W) {
                 const float Ls[4] = {lab[r][0].x, lab[r][0].y, lab[r][0].z, lab[r][0].w};
@@ -1100,36 +1138,62 @@ void fast_tile_dims(int W, int own_rows, int tile_cfg, int* tiles_x, int* ntiles
     *ntiles = *tiles_x * ((own_rows + th - 1) / th);
 }
 
-template <int TH, int RV, int OCC>
+template <int TH, int RV, int OCC, bool TRIM>
 static void launch_tile_cfg(const CostArgs& a, int P, const CostTaps<10>& t, int de,
                             hipStream_t s) {
     if (de == 0)
-        hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, 0, OCC>),
+        hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, 0, OCC, TRIM>),
                            dim3(a.ntiles, P), dim3(256), 0, s, a, t);
     else
-        hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, 1, OCC>),
+        hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, 1, OCC, TRIM>),
                            dim3(a.ntiles, P), dim3(256), 0, s, a, t);
+}
+
+template <bool TRIM>
+static void launch_persist(const CostArgs& a, int P, const CostTaps<10>& t, int de, int G,
+                           int nitems, hipStream_t s) {
+    if (de == 0)
+        hipLaunchKernelGGL((cost_persist_kernel<kFastHalf, kFastRW, kFastTH, kFastRV, 0, TRIM>),
+                           dim3(G), dim3(256), 0, s, a, t, P, nitems);
+    else
+        hipLaunchKernelGGL((cost_persist_kernel<kFastHalf, kFastRW, kFastTH, kFastRV, 1, TRIM>),
+                           dim3(G), dim3(256), 0, s, a, t, P, nitems);
+}
+
+// True when every tap of the narrow filters outside the trim window is below
+// 1e-9 of that filter's peak (products that far under fp32 rounding).
+bool trim_window_ok(const float* k1) {
+    const int ch[3] = {0, 1, 2};
+    for (int i = 0; i < 3; ++i) {
+        float peak = 0.f;
+        for (int t = 0; t < 21; ++t) peak = std::max(peak, std::fabs(k1[4 * t + ch[i]]));
+        for (int t = 0; t < 21; ++t)
+            if ((t < kTrimLo[i] || t > kTrimHi[i]) && std::fabs(k1[4 * t + ch[i]]) > 1e-9f * peak)
+                return false;
+    }
+    return true;
 }
 
 hipError_t launch_cost_fast(const CostArgs& a, int P, const float* k1, const float* k2,
                             const float* k3, const float* absk3, int de, int persistent,
-                            int tile_cfg, int num_cu, hipStream_t s) {
+                            int tile_cfg, int num_cu, bool trim, hipStream_t s) {
     CostTaps<10> t;
     make_taps10(k1, k2, k3, absk3, t);
     if (persistent && tile_cfg == 0) {  // the persistent kernel exists for 16-row tiles
         const int nitems = a.ntiles * P;
         int G = std::min(2 * num_cu, nitems);
         G = std::max(8, (G + 7) / 8 * 8);  // the XCD relabelling needs a multiple of 8
-        if (de == 0)
-            hipLaunchKernelGGL((cost_persist_kernel<kFastHalf, kFastRW, kFastTH, kFastRV, 0>),
-                               dim3(G), dim3(256), 0, s, a, t, P, nitems);
-        else
-            hipLaunchKernelGGL((cost_persist_kernel<kFastHalf, kFastRW, kFastTH, kFastRV, 1>),
-                               dim3(G), dim3(256), 0, s, a, t, P, nitems);
+        if (trim) launch_persist<true>(a, P, t, de, G, nitems, s);
+        else launch_persist<false>(a, P, t, de, G, nitems, s);
         return hipGetLastError();
     }
-    if (tile_cfg == 1) launch_tile_cfg<8, 4, 3>(a, P, t, de, s);
-    else launch_tile_cfg<kFastTH, kFastRV, 2>(a, P, t, de, s);
+    if (tile_cfg == 1) {
+        if (trim) launch_tile_cfg<8, 4, 3, true>(a, P, t, de, s);
+        else launch_tile_cfg<8, 4, 3, false>(a, P, t, de, s);
+    } else {
+        if (trim) launch_tile_cfg<kFastTH, kFastRV, 2, true>(a, P, t, de, s);
+        else launch_tile_cfg<kFastTH, kFastRV, 2, false>(a, P, t, de, s);
+    }
     return hipGetLastError();
 }
 

@@ -25,7 +25,8 @@ hipError_t launch_assign(const AssignArgs&, int P, int rep, hipStream_t);
 void fast_tile_dims(int W, int own_rows, int tile_cfg, int* tiles_x, int* ntiles);
 hipError_t launch_cost_fast(const CostArgs&, int P, const float* k1, const float* k2,
                             const float* k3, const float* absk3, int de, int persistent,
-                            int tile_cfg, int num_cu, hipStream_t);
+                            int tile_cfg, int num_cu, bool trim, hipStream_t);
+bool trim_window_ok(const float* k1);
 
 hipError_t launch_cost_generic(const GenArgs&, int de, hipStream_t);
 hipError_t launch_finalize(const FinalizeArgs&, int P, hipStream_t);
@@ -102,10 +103,12 @@ struct hq_ctx {
 
     // options
     int G2 = 64;           // argmin grid resolution (0 = exhaustive)
-    int cost_variant = 0;  // 0 fast tiled, 1 generic
+    int cost_variant = 0;  // 0 tiled (default), 1 generic two-pass, 2 persistent tiled
     int assign_blocks_per_cu = 8;
     int assign_rep = 4;    // palette replication in the assign kernel's LDS
-    int tile_cfg = 0;      // cost tile: 0 = 16 rows (2 WG/CU), 1 = 8 rows (3 WG/CU)
+    int tile_cfg = 1;      // cost tile: 0 = 16 rows (2 WG/CU), 1 = 8 rows (3 WG/CU)
+    int trim = 1;          // skip taps < 1e-9 of the peak of the narrow k1 filters
+    bool trim_ok = false;  // set by hq_set_filters (default 21-tap filter set)
 
     // comm
     ncclComm_t comm = nullptr;
@@ -361,8 +364,8 @@ int enqueue_eval(hq_ctx* c, int P, int K) {
         ca.ntiles = ntiles;
         std::memcpy(ca.inv_illum, inv, sizeof inv);
         HIP_TRY(c, launch_cost_fast(ca, P, c->k1.data(), c->k2.data(), c->k3.data(),
-                                    c->absk3.data(), c->de_type, c->cost_variant == 0,
-                                    c->tile_cfg, c->num_cu, s));
+                                    c->absk3.data(), c->de_type, c->cost_variant == 2,
+                                    c->tile_cfg, c->num_cu, c->trim && c->trim_ok, s));
         nparts = ntiles;
     } else {
         HIP_TRY(c, c->d_gen_t.ensure(sizeof(float) * 7 * (size_t)g.n_ext));
@@ -526,6 +529,7 @@ int hq_set_filters(hq_ctx* c, int taps, const float* k1, const float* k2, const 
     HIP_TRY(c, hipMemcpy(c->d_k2.p, k2, sizeof(float) * 4 * taps, hipMemcpyHostToDevice));
     HIP_TRY(c, hipMemcpy(c->d_k3.p, k3, sizeof(float) * taps, hipMemcpyHostToDevice));
     HIP_TRY(c, hipMemcpy(c->d_absk3.p, absk3, sizeof(float) * taps, hipMemcpyHostToDevice));
+    c->trim_ok = taps == 21 && trim_window_ok(k1);
     c->have_image = false;  // halo depends on the filters
     return HQ_OK;
 }
@@ -834,6 +838,8 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
     } else if (!std::strcmp(name, "cost_variant")) {
         if (value < 0 || value > 2) return fail(c, HQ_ERR_ARG, "cost_variant must be 0, 1 or 2");
         c->cost_variant = value;
+    } else if (!std::strcmp(name, "trim")) {
+        c->trim = value != 0;
     } else if (!std::strcmp(name, "cost_tile")) {
         if (value != 0 && value != 1) return fail(c, HQ_ERR_ARG, "cost_tile in {0,1}");
         c->tile_cfg = value;

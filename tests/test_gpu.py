@@ -74,7 +74,7 @@ def test_labref_256_checksum(ip):
 # Candidate evaluation (IM:620-727): golden fixtures
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("grid", [64, 32, 16, 0])
-@pytest.mark.parametrize("variant", [0, 1, 2, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("name", ["case_64x48_k16", "case_97x53_k64"])
 def test_eval_golden(ip, name, grid, variant):
     g, R, G, B = load_case(name)
@@ -282,5 +282,9 @@ def test_full_size_properties(gpu, filt):
         m.setOption("cost_tile", tile)
         c4 = m.computeQuantizationErrorPopulation(pals, 2.0)
         np.testing.assert_allclose(c4, c1, rtol=1e-6)  # persistent == generic == per-tile
+    m.setOption("cost_variant", 0)
+    m.setOption("trim", 0)  # all 21 taps of the narrow filters
+    c5 = m.computeQuantizationErrorPopulation(pals, 2.0)
+    np.testing.assert_allclose(c5, c1, rtol=1e-7)
     assert np.all(np.isfinite(c1)) and np.all(c1 > 0)
     m.close()
