@@ -414,6 +414,39 @@ def candidate_scielab(idx, palette4, filt: Filters, w: int, h: int):
     return opp_to_lab(conv4.reshape(h * w, 4), filt.illum)
 
 
+def shard_partial(rgb3, lab_ref4, palette4, filt: Filters, w: int, h: int, r0: int, r1: int):
+    """Row-block shard of the candidate cost: uses only RGB rows
+    [r0-half, r1+half) clipped to the image (halo re-quantised locally, reflection
+    only at true edges) and LabRef rows [r0, r1).  Returns (fp64 dE sum over the
+    owned rows, used flags of the extended rows)."""
+    half = filt.half
+    e0, e1 = max(0, r0 - half), min(h, r1 + half)
+    ext = np.asarray(rgb3, f32).reshape(h, w, 3)[e0:e1].reshape(-1, 3)
+    idx, used = assign(ext, palette4)
+    opp = palette_opp(palette4)[idx].reshape(e1 - e0, w, 4)[..., :3]
+    hidx = reflect_index(w, half)
+    T = 2 * half + 1
+    t1 = np.zeros((e1 - e0, w, 3), f32)
+    t2 = np.zeros((e1 - e0, w, 3), f32)
+    t3 = np.zeros((e1 - e0, w), f32)
+    for t in range(T):
+        src = opp[:, hidx[:, t], :]
+        t1 = fma32(src, filt.k1[t, :3], t1)
+        t2 = fma32(src, filt.k2[t, :3], t2)
+        t3 = fma32(src[..., 0], filt.k3[t], t3)
+    vidx = reflect_index(h, half)[r0:r1] - e0
+    out = np.zeros((r1 - r0, w, 3), f32)
+    for t in range(T):
+        r = vidx[:, t]
+        out = fma32(t1[r], filt.k1[t, :3], fma32(t2[r], filt.k2[t, :3], out))
+        out[..., 0] = fma32(t3[r], filt.absk3[t], out[..., 0])
+    conv4 = np.zeros((r1 - r0, w, 4), f32)
+    conv4[..., :3] = out
+    lab = opp_to_lab(conv4.reshape(-1, 4), filt.illum)
+    err = ciede76(np.asarray(lab_ref4, f32).reshape(h, w, 4)[r0:r1].reshape(-1, 4), lab)
+    return float(np.sum(err.astype(np.float64))), used
+
+
 def sum_array(arr, depth: int) -> float:
     """IM:741-768: recursive halving to ``depth``, sequential fp64 leaf sums."""
     def rec(s, e, d):

@@ -1,0 +1,89 @@
+"""Multi-process (gloo, world size 2) test of the row-block sharded evaluation
+ on CPU: each rank evaluates its shard with halo rows through the
+oracle's shard restatement, partials are all-reduced, and the result must equal
+the single-process full-image cost.  This is the same decomposition libhq's
+hq_eval_population_partial + RCCL all-reduce performs on the GPUs."""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import c_oracle
+import oracle as o
+
+W, H, K, P = 40, 37, 12, 2
+
+
+def _inputs():
+    f = o.design_filters()
+    R, G, B = o.synthetic_image(W, H, seed=21)
+    rgb3 = np.stack([R, G, B], axis=1)
+    lab = c_oracle.srgb_to_scielab(R, G, B, f, W)
+    pals = [o.synthetic_palette(K, 70 + p) for p in range(P)]
+    return f, rgb3, lab, pals
+
+
+def _worker(rank, world, port, out):
+    import torch
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    f, rgb3, lab, pals = _inputs()
+    r0, r1 = rank * H // world, (rank + 1) * H // world
+    part = torch.zeros(P, 1 + K, dtype=torch.float64)
+    for p, pal in enumerate(pals):
+        s, used = o.shard_partial(rgb3, lab, pal, f, W, H, r0, r1)
+        part[p, 0] = s
+        part[p, 1:] = torch.from_numpy(used.astype(np.float64))
+    dist.all_reduce(part)  # the single exchange step of the sharded path
+    if rank == 0:
+        out.put(part.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world", [2])
+def test_row_block_shards_allreduce_matches_full(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    red = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    f, rgb3, lab, pals = _inputs()
+    rgba = o.inline_rgba(rgb3[:, 0], rgb3[:, 1], rgb3[:, 2])
+    for p, pal in enumerate(pals):
+        cost, parts = c_oracle.eval_palette(rgba, lab, pal, f, W, return_parts=True)
+        full_sum = parts["err_sum"]
+        assert abs(red[p, 0] - full_sum) <= 1e-6 * abs(full_sum)  # numpy vs C oracle
+        np.testing.assert_array_equal(red[p, 1:] > 0, parts["used"] > 0)
+        # cost assembled like hq_eval_population: mean + delta * #unused
+        c = red[p, 0] / (W * H) + 2.0 * np.count_nonzero(red[p, 1:] == 0)
+        assert abs(c - cost) <= 1e-6 * abs(cost)
+
+
+def test_shard_partial_single_process_identity():
+    f, rgb3, lab, pals = _inputs()
+    rgba = o.inline_rgba(rgb3[:, 0], rgb3[:, 1], rgb3[:, 2])
+    for pal in pals:
+        _, parts = c_oracle.eval_palette(rgba, lab, pal, f, W, return_parts=True)
+        acc = 0.0
+        bounds = [0, 5, 11, 30, H]  # ragged shards, some thinner than the halo
+        for r0, r1 in zip(bounds[:-1], bounds[1:]):
+            acc += o.shard_partial(rgb3, lab, pal, f, W, H, r0, r1)[0]
+        assert abs(acc - parts["err_sum"]) <= 1e-6 * parts["err_sum"]
