@@ -77,7 +77,7 @@ def main():
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--K", type=int, default=256)
     ap.add_argument("--population", type=int, default=4)
-    ap.add_argument("--grid", type=int, default=64)
+    ap.add_argument("--grid", type=int, default=32)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-size", type=int, default=1024)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)

@@ -136,6 +136,17 @@ __device__ __forceinline__ V wave_sum(V v) {
 // ----------------------------------------------------------------------------
 // prep_palette: grid (P), block 256.
 // ----------------------------------------------------------------------------
+// XCD-aware relabelling of a 1-D grid of N workgroups.  Workgroups are placed
+// round-robin over the 8 XCDs (b % 8), so XCD x is given the contiguous work
+// range starting at x*(N/8) + min(x, N%8): neighbouring work items (the P
+// palettes of one tile or pixel block, adjacent tiles) then meet in one L2 and
+// LabRef / RGB reach HBM once instead of once per palette.  Bijective for any N;
+// placement only affects speed, never results.
+__device__ __forceinline__ int xcd_remap(int b, int N) {
+    const int q = N >> 3, r = N & 7, x = b & 7, s = b >> 3;
+    return x * q + min(x, r) + s;
+}
+
 __global__ __launch_bounds__(256) void prep_palette_kernel(PaletteArgs a) {
     const int p = blockIdx.x, k = threadIdx.x;
     __shared__ float4 s[kMaxK];
@@ -304,6 +315,28 @@ __device__ __forceinline__ bool lvl2_lookup(float r, float g, float b, const uin
     return true;
 }
 
+// Reference loop verbatim (CL:179-192) over a candidate list or all K colours.
+template <int REP>
+__device__ __noinline__ int argmin_exact_slow(float r, float g, float b, uint4 L0, uint4 L1,
+                                              int cnt, bool all, const float4* s_pal, int copy,
+                                              int K) {
+    const uint32_t words[8] = {L0.x, L0.y, L0.z, L0.w, L1.x, L1.y, L1.z, L1.w};
+    const int n = all ? K : cnt;
+    int bi = all ? 0 : (int)((words[0] >> 8) & 0xff);
+    float best = sqrtf(dist2(r, g, b, s_pal[bi * REP + copy]));
+    for (int i = 1; i < n; ++i) {
+        const int k = all ? i : (int)((words[(i + 1) >> 2] >> (8 * ((i + 1) & 3))) & 0xff);
+        const float d = sqrtf(dist2(r, g, b, s_pal[k * REP + copy]));
+        if (d < best) { best = d; bi = k; }
+    }
+    return bi;
+}
+
+// Exact argmin (CL:179-193 semantics) over the pixel's candidate list.
+// Candidates are ranked by d2; the reference ranks by sqrtf(d2), which can map
+// two different d2 onto one distance, and then keeps the lower index.  Equal
+// sqrtf values imply |d2a - d2b| < 2^-22 * d2, so lanes that ever compare two
+// d2 within 1e-6 relative are re-resolved with the reference loop (rare).
 template <int REP>
 __device__ __forceinline__ int argmin_from_entry(float r, float g, float b, uint4 L0, bool listed,
                                                  const float4* s_pal, int copy,
@@ -324,6 +357,7 @@ __device__ __forceinline__ int argmin_from_entry(float r, float g, float b, uint
         if (cnt == kOverflow) { exh = true; cnt = 0; }
     }
     int bi = (L0.x >> 8) & 0xff;  // first candidate (lowest index)
+    bool near = false;
     if (__any(cnt > 1)) {
         float best2 = dist2(r, g, b, s_pal[bi * REP + copy]);
         const uint32_t words[8] = {L0.x, L0.y, L0.z, L0.w, L1.x, L1.y, L1.z, L1.w};
@@ -331,31 +365,35 @@ __device__ __forceinline__ int argmin_from_entry(float r, float g, float b, uint
         for (int i = 1; i < kL1Cap; ++i) {
             if (!__any(i < cnt)) break;
             const int k = (words[(i + 1) >> 2] >> (8 * ((i + 1) & 3))) & 0xff;
-            const float d2 = dist2(r, g, b, s_pal[k * REP + copy]);
-            bool lt = (i < cnt) && d2 < best2;
-            // sqrtf may map d2 < best2 onto equal distances (CL:186 compares
-            // distance()); resolve near-ties exactly, keeping the lower index.
-            if (lt && d2 >= best2 * 0.99999905f) lt = sqrtf(d2) < sqrtf(best2);
+            const float4 c = s_pal[k * REP + copy];
+            asm volatile("" ::"v"(c.w));  // keep .w: one ds_read_b128 (16-lane groups), not b96
+            const float d2 = dist2(r, g, b, c);
+            const bool act = i < cnt;
+            near |= act && fabsf(d2 - best2) <= best2 * 1e-6f;
+            const bool lt = act && d2 < best2;
             best2 = lt ? d2 : best2;
             bi = lt ? k : bi;
         }
     }
-    if (exh) {  // reference loop verbatim (CL:179-192); rare
-        float best = sqrtf(dist2(r, g, b, s_pal[copy]));
-        bi = 0;
-        for (int k = 1; k < K; ++k) {
-            const float d = sqrtf(dist2(r, g, b, s_pal[k * REP + copy]));
-            if (d < best) { best = d; bi = k; }
-        }
+    if (__any(exh || near)) {
+        if (exh || near) bi = argmin_exact_slow<REP>(r, g, b, L0, L1, cnt, exh, s_pal, copy, K);
     }
     return bi;
 }
 
+// assign: grid (nblocks * P), block 256, dynamic LDS = K*REP*16 B.  Thread t of
+// a chunk handles pixels q0 + (t/64)*64*PPT + (t%64) + 64*j, j < PPT, so every
+// pixel load and index store is coalesced across the wave; the next pixel's
+// RGB and level-2 entry are loaded while the current one is resolved.
 template <int REP>
-__global__ __launch_bounds__(256) void assign_kernel(AssignArgs a) {
+__global__ __launch_bounds__(256) void assign_kernel(AssignArgs a, int P) {
+    constexpr int PPT = 8;
     extern __shared__ __attribute__((aligned(16))) float4 s_pal[];
     __shared__ uint32_t s_used[8];
-    const int p = blockIdx.y, tid = threadIdx.x;
+    // 1-D grid of nblocks * P: work item w = blk * P + p, so the P palettes of
+    // one pixel block run side by side on one XCD and share its RGB reads in L2.
+    const int w = xcd_remap(blockIdx.x, a.nblocks * P);
+    const int p = w % P, blk = w / P, tid = threadIdx.x;
     const float4* pal = a.pal + (int64_t)p * kMaxK;
     for (int e = tid; e < a.K * REP; e += 256) s_pal[e] = pal[e / REP];
     if (tid < 8) s_used[tid] = 0;
@@ -365,41 +403,114 @@ __global__ __launch_bounds__(256) void assign_kernel(AssignArgs a) {
     const uint8_t* lvl1p = a.lvl1 + (int64_t)p * a.lvl1_pitch;
     const uint8_t* lvl2p = a.lvl2 + (int64_t)p * a.lvl2_pitch;
     uint8_t* idx = a.idx + (int64_t)p * a.idx_pitch;
-    const int64_t stride = (int64_t)a.nblocks * 256 * 4;
-    for (int64_t q = ((int64_t)blockIdx.x * 256 + tid) * 4; q < a.n_ext; q += stride) {
-        const float4 r4 = *reinterpret_cast<const float4*>(a.R + q);
-        const float4 g4 = *reinterpret_cast<const float4*>(a.G + q);
-        const float4 b4 = *reinterpret_cast<const float4*>(a.B + q);
-        // all four table loads in flight before any candidate loop
-        uint4 e0, e1, e2, e3;
-        const bool l0 = lvl2_lookup(r4.x, g4.x, b4.x, lvl2p, a.G2, exh_pal, e0);
-        const bool l1 = lvl2_lookup(r4.y, g4.y, b4.y, lvl2p, a.G2, exh_pal, e1);
-        const bool l2 = lvl2_lookup(r4.z, g4.z, b4.z, lvl2p, a.G2, exh_pal, e2);
-        const bool l3 = lvl2_lookup(r4.w, g4.w, b4.w, lvl2p, a.G2, exh_pal, e3);
-        uint32_t packed = 0;
+    const int64_t chunk = 256 * PPT;
+    const int64_t lane_off = (int64_t)(tid >> 6) * 64 * PPT + (tid & 63);
+    for (int64_t q0 = (int64_t)blk * chunk; q0 < a.n_ext; q0 += (int64_t)a.nblocks * chunk) {
+        int64_t q = q0 + lane_off;
+        bool in = q < a.n_ext;
+        float r = in ? a.R[q] : 0.f, gv = in ? a.G[q] : 0.f, b = in ? a.B[q] : 0.f;
+        uint4 e;
+        bool li = lvl2_lookup(r, gv, b, lvl2p, a.G2, exh_pal, e);
 #pragma unroll 1
-        for (int j = 0; j < 4; ++j) {  // not unrolled: one copy of the candidate loop
-            const float r = j == 0 ? r4.x : (j == 1 ? r4.y : (j == 2 ? r4.z : r4.w));
-            const float gv = j == 0 ? g4.x : (j == 1 ? g4.y : (j == 2 ? g4.z : g4.w));
-            const float b = j == 0 ? b4.x : (j == 1 ? b4.y : (j == 2 ? b4.z : b4.w));
-            const uint4 e = j == 0 ? e0 : (j == 1 ? e1 : (j == 2 ? e2 : e3));
-            const bool li = j == 0 ? l0 : (j == 1 ? l1 : (j == 2 ? l2 : l3));
+        for (int j = 0; j < PPT; ++j) {
+            // prefetch pixel j+1
+            const int64_t qn = q + 64;
+            const bool inn = j + 1 < PPT && qn < a.n_ext;
+            const float rn = inn ? a.R[qn] : 0.f, gn = inn ? a.G[qn] : 0.f,
+                        bn = inn ? a.B[qn] : 0.f;
+            uint4 en;
+            const bool lin = lvl2_lookup(rn, gn, bn, lvl2p, a.G2, exh_pal || !inn, en);
             const int k = argmin_from_entry<REP>(r, gv, b, e, li, s_pal, copy, lvl1p, a.G2, a.K);
-            packed |= (uint32_t)k << (8 * j);
-            if (q + j < a.n_ext) {
+            if (in) {
+                idx[q] = (uint8_t)k;
                 const uint32_t bit = 1u << (k & 31);
                 if (!(s_used[k >> 5] & bit)) atomicOr(&s_used[k >> 5], bit);
             }
+            q = qn; in = inn; r = rn; gv = gn; b = bn; e = en; li = lin;
         }
-        *reinterpret_cast<uint32_t*>(idx + q) = packed;
     }
     __syncthreads();
-    if (tid < 8) a.used_mask[((int64_t)p * a.nblocks + blockIdx.x) * 8 + tid] = s_used[tid];
+    if (tid < 8) a.used_mask[((int64_t)p * a.nblocks + blk) * 8 + tid] = s_used[tid];
 }
 
+// assign_multi: grid (nblocks, ceil(P/PG)), dynamic LDS = PG*K*REP*16 B.  One
+// pass over the pixels serves PG palettes: each pixel's RGB is read once, its
+// cell index computed once, and the PG level-2 entries loaded together
+// (512 KiB tables at G2 = 32 stay L2-resident), then resolved palette by palette.
+template <int REP, int PG>
+__global__ __launch_bounds__(256) void assign_multi_kernel(AssignArgs a, int P) {
+    constexpr int PPT = 8;
+    extern __shared__ __attribute__((aligned(16))) float4 s_pal[];
+    __shared__ uint32_t s_used[PG][8];
+    const int tid = threadIdx.x;
+    const int p0 = blockIdx.y * PG;
+    const int ng = min(PG, P - p0);
+    for (int e = tid; e < ng * a.K * REP; e += 256) {
+        const int pp = e / (a.K * REP), r = e - pp * a.K * REP;
+        s_pal[e] = a.pal[(int64_t)(p0 + pp) * kMaxK + r / REP];
+    }
+    if (tid < 8 * PG) s_used[tid >> 3][tid & 7] = 0;
+    __syncthreads();
+    const int copy = tid & (REP - 1);
+    bool exh_pal[PG];
+    const uint8_t* lvl2p[PG];
+#pragma unroll
+    for (int pp = 0; pp < PG; ++pp) {
+        const int pq = min(p0 + pp, P - 1);
+        exh_pal[pp] = a.pflags[pq] != 0 || a.G2 == 0;
+        lvl2p[pp] = a.lvl2 + (int64_t)pq * a.lvl2_pitch;
+    }
+    const int64_t chunk = 256 * PPT;
+    const int64_t lane_off = (int64_t)(tid >> 6) * 64 * PPT + (tid & 63);
+    const int G2 = a.G2 > 0 ? a.G2 : 4;
+    for (int64_t q0 = (int64_t)blockIdx.x * chunk; q0 < a.n_ext; q0 += (int64_t)a.nblocks * chunk) {
+        int64_t q = q0 + lane_off;
+        bool in = q < a.n_ext;
+        float r = in ? a.R[q] : 0.f, gv = in ? a.G[q] : 0.f, b = in ? a.B[q] : 0.f;
+#pragma unroll 1
+        for (int j = 0; j < PPT; ++j) {
+            const int64_t qn = q + 64;
+            const bool inn = j + 1 < PPT && qn < a.n_ext;
+            const float rn = inn ? a.R[qn] : 0.f, gn = inn ? a.G[qn] : 0.f,
+                        bn = inn ? a.B[qn] : 0.f;
+            // one cell index, PG table loads in flight
+            const bool inside = r >= 0.f && r <= 1.f && gv >= 0.f && gv <= 1.f && b >= 0.f && b <= 1.f;
+            const int64_t cell = ((int64_t)(min((int)(r * (float)G2), G2 - 1) * G2 +
+                                            min((int)(gv * (float)G2), G2 - 1)) * G2 +
+                                  min((int)(b * (float)G2), G2 - 1)) * 16;
+            uint4 e[PG];
+            bool li[PG];
+#pragma unroll
+            for (int pp = 0; pp < PG; ++pp) {
+                li[pp] = inside && !exh_pal[pp] && pp < ng;
+                e[pp] = li[pp] ? *reinterpret_cast<const uint4*>(lvl2p[pp] + cell)
+                               : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int pp = 0; pp < PG; ++pp) {
+                if (pp >= ng) break;
+                const int pq = p0 + pp;
+                const int k = argmin_from_entry<REP>(r, gv, b, e[pp], li[pp],
+                                                     s_pal + pp * a.K * REP, copy,
+                                                     a.lvl1 + (int64_t)pq * a.lvl1_pitch, G2,
+                                                     a.K);
+                if (in) {
+                    a.idx[(int64_t)pq * a.idx_pitch + q] = (uint8_t)k;
+                    const uint32_t bit = 1u << (k & 31);
+                    if (!(s_used[pp][k >> 5] & bit)) atomicOr(&s_used[pp][k >> 5], bit);
+                }
+            }
+            q = qn; in = inn; r = rn; gv = gn; b = bn;
+        }
+    }
+    __syncthreads();
+    if (tid < 8 * ng)
+        a.used_mask[((int64_t)(p0 + (tid >> 3)) * a.nblocks + blockIdx.x) * 8 + (tid & 7)] =
+            s_used[tid >> 3][tid & 7];
+}
 
 // ----------------------------------------------------------------------------
-// cost_tile: grid (ntiles, P), block 256.  One workgroup = one TW x TH output
+// cost_tile: grid (ntiles * P), block 256.  One workgroup = one TW x TH output
 // tile; region = (TH + 2*HALF) rows x RW cols of indices (RW = TW + 2*HALF).
 // Vertical pass first on all RW region columns (separable filters commute),
 // then horizontal pass on the TW output columns, Opp->Lab, dE, fp64 partial.
@@ -512,14 +623,15 @@ __device__ __forceinline__ void hpass_all(const float4* src, const CostTaps<HALF
 }
 
 template <int HALF, int RW, int TH, int RV, int DE, int OCC, bool TRIM>
-__global__ __launch_bounds__(256, OCC) void cost_tile_kernel(CostArgs a, CostTaps<HALF> taps) {
+__global__ __launch_bounds__(256, OCC) void cost_tile_kernel(CostArgs a, CostTaps<HALF> taps,
+                                                            int P_) {
     constexpr int TW = RW - 2 * HALF;
     constexpr int RH = TH + 2 * HALF;
     constexpr int NIN = RV + 2 * HALF;
     constexpr int NRUN = TW / 4;
     static_assert(RW * (TH / RV) == 256, "one V item per thread");
     static_assert(TW % 4 == 0, "4-wide H runs");
-    static_assert(TH * 32 <= 512, "at most two H rounds");
+    static_assert(TH * 32 % 256 == 0 && TH * 32 <= 512, "one or two H items per thread");
     // s_v is float4-typed so the H-pass reads stay ds_read_b128 (a float-typed
     // array let the compiler split them into 4-way-conflicted ds_read2_b32).
     __shared__ float4 s_v4[kNumFilt * TH * RW / 4];
@@ -531,11 +643,31 @@ __global__ __launch_bounds__(256, OCC) void cost_tile_kernel(CostArgs a, CostTap
     __shared__ double s_red[4];
     float* s_v = reinterpret_cast<float*>(s_v4);
 
-    const int p = blockIdx.y, tile = blockIdx.x, tid = threadIdx.x;
+    // 1-D grid of ntiles * P: work item w = tile * P + p, so the P palettes of a
+    // tile run side by side on one XCD and read its LabRef from L2 after the first.
+    const int w = xcd_remap(blockIdx.x, a.ntiles * P_);
+    const int p = w % P_, tile = w / P_, tid = threadIdx.x;
     const Geom& g = a.g;
     const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
     const int x0 = tx * TW, y0 = g.r0 + ty * TH;
     const uint8_t* idx = a.idx + (int64_t)p * g.idx_pitch;
+
+    // LabRef of this thread's H items, loaded first so the HBM latency overlaps
+    // the index fill and the V pass instead of stalling the H pass.
+    constexpr int NH = TH * 32 / 256;
+    float4 labL[NH], labA[NH], labB[NH];
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        const int item = tid + 256 * h, y = item >> 5, j = item & 31;
+        const int gy = y0 + y, gx0 = x0 + 4 * j;
+        labL[h] = labA[h] = labB[h] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (j < NRUN && gy < g.r1 && gx0 < g.W) {
+            const int64_t off = (int64_t)(gy - g.r0) * g.lab_pitch + gx0;
+            labL[h] = *reinterpret_cast<const float4*>(a.labL + off);
+            labA[h] = *reinterpret_cast<const float4*>(a.labA + off);
+            labB[h] = *reinterpret_cast<const float4*>(a.labB + off);
+        }
+    }
 
     for (int e = tid; e < a.K * OPP_REP; e += 256)
         s_opp[e] = a.opp[(int64_t)p * kMaxK + e / OPP_REP];
@@ -590,18 +722,16 @@ __global__ __launch_bounds__(256, OCC) void cost_tile_kernel(CostArgs a, CostTap
     // covers 16 distinct bank positions of one row (27 runs per row wrapped
     // lanes into the next row's bank 0).
     static_assert(NRUN <= 32, "runs per row");
-    for (int item = tid; item < TH * 32; item += 256) {
-        const int y = item >> 5, j = item & 31;
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        const int item = tid + 256 * h, y = item >> 5, j = item & 31;
         if (j >= NRUN) continue;
         const float4* src = &s_v4[(y * RW) / 4 + j];
         float acc0[4], acc1[4], acc2[4];
         hpass_all<HALF, TH, RW, TRIM>(src, taps, acc0, acc1, acc2);
         const int gy = y0 + y, gx0 = x0 + 4 * j;
         if (gy < g.r1 && gx0 < g.W) {
-            const int64_t off = (int64_t)(gy - g.r0) * g.lab_pitch + gx0;
-            const float4 L4 = *reinterpret_cast<const float4*>(a.labL + off);
-            const float4 A4 = *reinterpret_cast<const float4*>(a.labA + off);
-            const float4 B4 = *reinterpret_cast<const float4*>(a.labB + off);
+            const float4 L4 = labL[h], A4 = labA[h], B4 = labB[h];
             const float Ls[4] = {L4.x, L4.y, L4.z, L4.w};
             const float As[4] = {A4.x, A4.y, A4.z, A4.w};
             const float Bs[4] = {B4.x, B4.y, B4.z, B4.w};
@@ -1099,12 +1229,35 @@ static hipError_t launch_assign_rep(const AssignArgs& a, int P, hipStream_t s) {
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    hipLaunchKernelGGL(assign_kernel<REP>, dim3(a.nblocks, P), dim3(256), lds, s, a);
+    hipLaunchKernelGGL(assign_kernel<REP>, dim3(a.nblocks * P), dim3(256), lds, s, a, P);
+    return hipGetLastError();
+}
+
+template <int REP, int PG>
+static hipError_t launch_assign_multi(const AssignArgs& a, int P, hipStream_t s) {
+    const size_t lds = (size_t)PG * a.K * REP * sizeof(float4);
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)assign_multi_kernel<REP, PG>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)(PG * kMaxK * REP * sizeof(float4)));
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((assign_multi_kernel<REP, PG>), dim3(a.nblocks, (P + PG - 1) / PG),
+                       dim3(256), lds, s, a, P);
     return hipGetLastError();
 }
 
 // rep: LDS replication of the palette (1, 4 or 16); lane l reads copy l % rep.
-hipError_t launch_assign(const AssignArgs& a, int P, int rep, hipStream_t s) {
+// group > 1: one pixel pass serves `group` palettes (assign_multi_kernel).
+hipError_t launch_assign(const AssignArgs& a, int P, int rep, int group, hipStream_t s) {
+    if (group == 4) {
+        if (rep == 1) return launch_assign_multi<1, 4>(a, P, s);
+        if (rep == 2) return launch_assign_multi<2, 4>(a, P, s);
+        return launch_assign_multi<4, 4>(a, P, s);
+    }
+    if (group == 2) return launch_assign_multi<4, 2>(a, P, s);
     if (rep == 16) return launch_assign_rep<16>(a, P, s);
     if (rep == 1) return launch_assign_rep<1>(a, P, s);
     return launch_assign_rep<4>(a, P, s);
@@ -1143,10 +1296,10 @@ static void launch_tile_cfg(const CostArgs& a, int P, const CostTaps<10>& t, int
                             hipStream_t s) {
     if (de == 0)
         hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, 0, OCC, TRIM>),
-                           dim3(a.ntiles, P), dim3(256), 0, s, a, t);
+                           dim3(a.ntiles * P), dim3(256), 0, s, a, t, P);
     else
         hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, 1, OCC, TRIM>),
-                           dim3(a.ntiles, P), dim3(256), 0, s, a, t);
+                           dim3(a.ntiles * P), dim3(256), 0, s, a, t, P);
 }
 
 template <bool TRIM>

@@ -21,7 +21,7 @@ namespace hq {
 // launchers from hq_kernels.hip
 hipError_t launch_prep_palette(const PaletteArgs&, int P, hipStream_t);
 hipError_t launch_build_grid(const GridArgs&, int P, hipStream_t);
-hipError_t launch_assign(const AssignArgs&, int P, int rep, hipStream_t);
+hipError_t launch_assign(const AssignArgs&, int P, int rep, int group, hipStream_t);
 void fast_tile_dims(int W, int own_rows, int tile_cfg, int* tiles_x, int* ntiles);
 hipError_t launch_cost_fast(const CostArgs&, int P, const float* k1, const float* k2,
                             const float* k3, const float* absk3, int de, int persistent,
@@ -102,10 +102,11 @@ struct hq_ctx {
     int last_P = 0;
 
     // options
-    int G2 = 64;           // argmin grid resolution (0 = exhaustive)
+    int G2 = 32;           // argmin grid resolution (0 = exhaustive)
     int cost_variant = 0;  // 0 tiled (default), 1 generic two-pass, 2 persistent tiled
     int assign_blocks_per_cu = 8;
-    int assign_rep = 4;    // palette replication in the assign kernel's LDS
+    int assign_rep = 1;    // palette replication in the assign kernel's LDS
+    int assign_group = 1;  // palettes per pixel pass in the assign kernel (1, 2, 4)
     int tile_cfg = 1;      // cost tile: 0 = 16 rows (2 WG/CU), 1 = 8 rows (3 WG/CU)
     int trim = 1;          // skip taps < 1e-9 of the peak of the narrow k1 filters
     bool trim_ok = false;  // set by hq_set_filters (default 21-tap filter set)
@@ -343,7 +344,7 @@ int enqueue_eval(hq_ctx* c, int P, int K) {
                   c->d_pflags.as<int>(), c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(),
                   c->d_idx.as<uint8_t>(), c->d_used_mask.as<uint32_t>(), g.n_ext, g.idx_pitch,
                   l1p, l2p, K, c->G2, nblocks};
-    HIP_TRY(c, launch_assign(aa, P, c->assign_rep, s));
+    HIP_TRY(c, launch_assign(aa, P, c->assign_rep, c->assign_group, s));
     if (c->prof) HIP_TRY(c, hipEventRecord(c->ev[2], s));
     int tiles_x, ntiles;
     fast_tile_dims(g.W, g.r1 - g.r0, c->tile_cfg, &tiles_x, &ntiles);
@@ -843,8 +844,12 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
     } else if (!std::strcmp(name, "cost_tile")) {
         if (value != 0 && value != 1) return fail(c, HQ_ERR_ARG, "cost_tile in {0,1}");
         c->tile_cfg = value;
+    } else if (!std::strcmp(name, "assign_group")) {
+        if (value != 1 && value != 2 && value != 4) return fail(c, HQ_ERR_ARG, "assign_group in {1,2,4}");
+        c->assign_group = value;
     } else if (!std::strcmp(name, "assign_rep")) {
-        if (value != 1 && value != 4 && value != 16) return fail(c, HQ_ERR_ARG, "assign_rep in {1,4,16}");
+        if (value != 1 && value != 2 && value != 4 && value != 16)
+            return fail(c, HQ_ERR_ARG, "assign_rep in {1,2,4,16}");
         c->assign_rep = value;
     } else if (!std::strcmp(name, "assign_blocks_per_cu")) {
         if (value < 1 || value > 64) return fail(c, HQ_ERR_ARG, "assign_blocks_per_cu in [1,64]");

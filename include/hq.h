@@ -179,14 +179,15 @@ int hq_profile_get(hq_ctx *ctx, const char *kernel, double *total_ms, int64_t *l
 int hq_profile_reset(hq_ctx *ctx);
 
 /* Tuning knobs (testing / benchmarking; defaults are the measured best):
- *   "grid"         argmin pruning resolution G2: 0 = exhaustive, 16, 32, 64 (default 64)
+ *   "grid"         argmin pruning resolution G2: 0 = exhaustive, 16, 32 (default), 64
  *   "cost_variant" 0 = one tile per workgroup (default), 1 = generic two-pass
  *                  path (any filter length), 2 = persistent pipelined tiles
  *   "cost_tile"    0 = 16-row tiles (2 WG/CU), 1 = 8-row tiles (3 WG/CU, default)
  *   "trim"         1 = skip the narrow k1 filters' taps below 1e-9 of their peak
  *                  (default; only when the filters allow it), 0 = all taps
- *   "assign_rep"   palette replication in the assign kernel's LDS: 1, 4 (default), 16
- *   "assign_blocks_per_cu" */
+ *   "assign_rep"   palette replication in the assign kernel's LDS: 1 (default), 2, 4, 16
+ *   "assign_group" palettes evaluated per pixel pass in the assign kernel: 1 (default), 2, 4
+ *   "assign_blocks_per_cu" workgroups per CU of the assign grid (default 8) */
 int hq_set_option(hq_ctx *ctx, const char *name, int value);
 
 #ifdef __cplusplus

@@ -26,11 +26,12 @@ def main():
     ap.add_argument("--K", type=int, default=256)
     ap.add_argument("--P", type=int, default=4)
     ap.add_argument("--evals", type=int, default=10)
-    ap.add_argument("--grid", type=int, default=64)
+    ap.add_argument("--grid", type=int, default=32)
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--tile", type=int, default=1)
-    ap.add_argument("--rep", type=int, default=4)
+    ap.add_argument("--rep", type=int, default=1)
     ap.add_argument("--trim", type=int, default=1)
+    ap.add_argument("--group", type=int, default=1)
     args = ap.parse_args()
     lib = hq.load()
     m = hq.ImageManipulation(device=0)
@@ -40,6 +41,7 @@ def main():
     m.setOption("cost_tile", args.tile)
     m.setOption("assign_rep", args.rep)
     m.setOption("trim", args.trim)
+    m.setOption("assign_group", args.group)
     W = H = args.size
     R, G, B = synthetic_planes(W, H, 1)
     _lib.check(lib.hq_set_image_planar_shard(m.ctx, _lib.fptr(R), _lib.fptr(G), _lib.fptr(B), W, H,
@@ -62,7 +64,7 @@ def main():
         n = C.c_int64()
         lib.hq_profile_get(m.ctx, k.encode(), C.byref(ms), C.byref(n))
         out.append(f"{k}={ms.value / max(n.value, 1):.4f}ms")
-    print(f"size={W} K={args.K} P={args.P} grid={args.grid} variant={args.variant} tile={args.tile} rep={args.rep} trim={args.trim}: "
+    print(f"size={W} K={args.K} P={args.P} grid={args.grid} variant={args.variant} tile={args.tile} rep={args.rep} trim={args.trim} group={args.group}: "
           f"{el / args.evals * 1e3:.3f} ms/eval-population, "
           f"{W * H * args.P * args.evals / el / 1e6:.1f} Mpx*evals/s  ", " ".join(out),
           "costs", costs.tolist())

@@ -147,11 +147,18 @@ def test_assign_random_and_near_ties(ip, K):
         pal[K - 1, :3] = px[5, :3]
     ip.setImage(px.reshape(-1), np.zeros_like(px).reshape(-1), w, ip.illum)
     ref_idx, ref_used = c_oracle.assign(px, pal)
-    for grid in (64, 16, 0):
+    for grid, group, rep in ((64, 1, 4), (32, 4, 4), (32, 2, 4), (32, 4, 1), (16, 4, 2), (0, 1, 16)):
         ip.setOption("grid", grid)
-        _, used = ip.computeQuantizationErrorPopulation([pal.reshape(-1)], 2.0, return_used=True)
+        ip.setOption("assign_group", group)
+        ip.setOption("assign_rep", rep)
+        pals = [pal.reshape(-1), pal[::-1].copy().reshape(-1), pal.reshape(-1)]
+        _, used = ip.computeQuantizationErrorPopulation(pals, 2.0, return_used=True)
         np.testing.assert_array_equal(ip.getIndices(0), ref_idx.astype(np.uint8))
+        np.testing.assert_array_equal(ip.getIndices(2), ref_idx.astype(np.uint8))
         np.testing.assert_array_equal(used[0], ref_used)
+        rev_idx, rev_used = c_oracle.assign(px, pal[::-1].copy())
+        np.testing.assert_array_equal(ip.getIndices(1), rev_idx.astype(np.uint8))
+        np.testing.assert_array_equal(used[1], rev_used)
 
 
 def test_nonfinite_palette_falls_back_exactly(ip):
