@@ -42,6 +42,22 @@ def synthetic_planes(w, h, seed=1):
     return [((z >> np.uint64(8 * c)) & np.uint64(0xFF)).astype(np.float32) / s for c in range(3)]
 
 
+def measured_traffic(size, K, P, grid, world):
+    """HBM bytes per cost_tile launch from the committed PMC passes (or None)."""
+    path = os.path.join(ROOT, "profiles", "r01_hbm_traffic.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    c = d.get("config", {})
+    if world != 1 or (c.get("size"), c.get("K"), c.get("P"), c.get("grid")) != (size, K, P, grid):
+        return None
+    for name, v in d.get("kernels", {}).items():
+        if "cost_tile_kernel" in name:
+            return int(v["traffic_bytes"])
+    return None
+
+
 def cpu_baseline(args):
     """Oracle (C restatement, 'port') on this host's cores over a bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -164,13 +180,17 @@ def main():
     P = args.population
     n_own = W * (r1 - r0)
     value = W * H * P * args.steps / elapsed / 1e6
-    # Dominant kernel: cost_tile (S-CIELAB stencil + Lab + dE).  Algorithmic
-    # bytes per launch = LabRef fp32x3 once per pixel + the u8 index image of
-    # each of the P palettes (DESIGN.md "Roofline accounting").
+    # Dominant kernel: cost_tile (S-CIELAB stencil + Opp->Lab + dE76).  With P > 1
+    # palettes per launch its HBM bytes (LabRef once + P index images) amortise
+    # and FP32 VALU bounds it: algorithmic flops per pixel-eval =
+    # the reference's stencil, 7 separable filters x 2 passes x 21 taps x 2 flops
+    # = 588, + Opp->Lab / dE76 ~ 40 (DESIGN.md "Roofline accounting").
     cost_ms = prof["cost"][0]
+    alg_flops = n_own * P * (588 + 40)
+    achieved_tf = alg_flops / (cost_ms * 1e-3) / 1e12 if cost_ms > 0 else 0.0
     alg_bytes = n_own * (12 + P)
-    achieved = alg_bytes / (cost_ms * 1e-3) / 1e9 if cost_ms > 0 else 0.0
-    # whole-evaluation view: the metric's 24 B/px-eval HBM roofline
+    traffic = measured_traffic(W, args.K, P, args.grid, world)
+    # whole-evaluation view: the metric's 24 B/px-eval HBM-read roofline
     eval_roof_mpx = HBM_PEAK_GBS * 1e9 / 24.0 / 1e6 * args.gpus
     out = {
         "metric": "Mpixel*evals/s (SWASA dE cost) at 4096x4096 K=256",
@@ -190,10 +210,15 @@ def main():
                    "image": f"{W}x{H}", "K": args.K, "population": P,
                    "parallelism": f"row-block x{world} + RCCL all-reduce" if world > 1 else "1 GPU",
                    "argmin_grid": args.grid},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+        "roofline": {"bound": "valu", "achieved": round(achieved_tf, 2), "peak": FP32_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4),
+                     "traffic": traffic,
                      "kernel": "cost_tile_kernel", "kernel_avg_ms": round(cost_ms, 4),
-                     "alg_bytes_per_launch": alg_bytes},
+                     "alg_flops_per_launch": alg_flops, "alg_bytes_per_launch": alg_bytes,
+                     "hbm_GBs_alg": round(alg_bytes / (cost_ms * 1e-3) / 1e9, 1) if cost_ms > 0 else 0.0,
+                     "note": "f32 VALU kernel; peak = MI355X FP32 vector (= FP32 MFMA) 157.3 TFLOP/s; "
+                             "traffic = HBM bytes/launch from the committed rocprofv3 FETCH_SIZE(x2)+WRITE_SIZE "
+                             "passes (profiles/r01_hbm_traffic.json) when their config matches"},
         "metric_hbm_roofline_frac": round(value / eval_roof_mpx, 4),
         "kernel_avg_ms": {k: round(v[0], 4) for k, v in prof.items()},
         "best_error": berr.value,

@@ -85,7 +85,7 @@ struct CostArgs {
     int K;
     int tiles_x;
     int ntiles;
-    float inv_illum[3];
+    float m_lab[9];  // Opp->XYZ rows divided by the illuminant (CL:124-131), opp2xyz_over_illum()
 };
 
 struct FinalizeArgs {
@@ -112,7 +112,7 @@ struct GenArgs {
     double* partial;         // [nblocks]
     Geom g;
     int half;
-    float inv_illum[3];
+    float m_lab[9];  // Opp->XYZ rows divided by the illuminant (CL:124-131), opp2xyz_over_illum()
 };
 
 }  // namespace hq

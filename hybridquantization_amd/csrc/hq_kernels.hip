@@ -34,8 +34,9 @@ __constant__ float c_RGB2XYZ[9] = {0.4124564f, 0.3575761f, 0.1804375f, 0.2126729
                                    0.0721750f, 0.0193339f, 0.1191920f, 0.9503041f};
 __constant__ float c_XYZ2Opp[9] = {0.2787336f,  0.7218031f, -0.1065520f, -0.4487736f, 0.2898056f,
                                    -0.0771569f, 0.0859513f, -0.5899859f, 0.5011089f};
-__constant__ float c_Opp2XYZ[9] = {0.624045f, -1.87044f, -0.155304f, 1.36606f, 0.931563f,
-                                   0.433903f, 1.5013f,   1.41761f,  2.53307f};
+#define HQ_OPP2XYZ {0.624045f, -1.87044f, -0.155304f, 1.36606f, 0.931563f, \
+                   0.433903f, 1.5013f,   1.41761f,  2.53307f}
+__constant__ float c_Opp2XYZ[9] = HQ_OPP2XYZ;
 __constant__ float c_RGB2Opp[9] = {0.266413f,  0.603167f, 0.00113333f, -0.124957f, 0.0375879f,
                                    -0.133381f, -0.0803345f, -0.331467f, 0.449132f};
 
@@ -54,23 +55,23 @@ __device__ __forceinline__ float lab_f(float t) {  // CL:137
     return t > LAB_DELTA3 ? cbrtf(t) : fmaf(LAB_KAPPA, t, 16.0f) * (1.0f / 116.0f);
 }
 
-// Branch-free f(t) of CL:137 for the hot path: cube root by exp2(log2(t)/3)
-// refined with one Newton step (error ~1 ulp), linear segment selected.
+// Branch-free f(t) of CL:137 for the hot path: cube root as exp2(log2(t)/3)
+// (v_log_f32 / v_exp_f32, about 3 ulp; no Newton step -- the cost tolerance is
+// 1e-4 relative and this moves the mean dE by ~1e-7), linear segment selected.
 __device__ __forceinline__ float lab_f_fast(float t) {
     const float tc = fmaxf(t, LAB_DELTA3);  // cbrt branch only used for t > delta^3 > 0
-    float y = __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(tc) * (1.0f / 3.0f));
-    y = fmaf(-(1.0f / 3.0f), fmaf(y * y, y, -tc) * __builtin_amdgcn_rcpf(y * y), y);
+    const float y = __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(tc) * (1.0f / 3.0f));
     const float lin = fmaf(LAB_KAPPA, t, 16.0f) * (1.0f / 116.0f);
     return t > LAB_DELTA3 ? y : lin;
 }
 
-// CL:124-145 Opp2LAB with reciprocal illuminant (hot path; fp32 tolerance).
-__device__ __forceinline__ float3 opp2lab_fast(float o0, float o1, float o2, float ix, float iy,
-                                               float iz) {
-    const float X = dot3(o0, o1, o2, c_Opp2XYZ + 0);
-    const float Y = dot3(o0, o1, o2, c_Opp2XYZ + 3);
-    const float Z = dot3(o0, o1, o2, c_Opp2XYZ + 6);
-    const float fx = lab_f_fast(X * ix), fy = lab_f_fast(Y * iy), fz = lab_f_fast(Z * iz);
+// CL:124-145 Opp2LAB for the hot path: m = Opp->XYZ with row r divided by the
+// illuminant's component r (opp2xyz_over_illum), so X/Xn etc. come out of the
+// 3x3 product directly.
+__device__ __forceinline__ float3 opp2lab_fast(float o0, float o1, float o2, const float* m) {
+    const float fx = lab_f_fast(dot3(o0, o1, o2, m + 0));
+    const float fy = lab_f_fast(dot3(o0, o1, o2, m + 3));
+    const float fz = lab_f_fast(dot3(o0, o1, o2, m + 6));
     return make_float3(116.0f * fy - 16.0f, 500.0f * (fx - fy), 200.0f * (fy - fz));
 }
 
@@ -622,23 +623,68 @@ __device__ __forceinline__ void hpass_all(const float4* src, const CostTaps<HALF
     }
 }
 
-template <int HALF, int RW, int TH, int RV, int DE, int OCC, bool TRIM>
+// V pass split by channel group (VSPLIT): threads [0, RW) own channel 0
+// (filters 0-2) of region column c, threads [RW, 2*RW) channels 1 and 2
+// (filters 3-6), each over all TH rows.  The gathers are then ds_read_b32 /
+// ds_read_b64 from per-group tables (2 LDS cycles per wave-instruction against
+// 4 for the float4 table) and every gathered row feeds TH outputs instead of RV.
+template <int HALF, int TH, int RW, bool TRIM>
+__device__ __forceinline__ void vpass_split(const uint8_t* s_idx, const float* s_oppA,
+                                            const float2* s_oppB, const CostTaps<HALF>& taps,
+                                            float* s_v, int tid) {
+    constexpr int NIN = TH + 2 * HALF;
+    const int c = tid % RW;
+    float* out = s_v + c;
+    if (tid < RW) {
+        float o0[NIN];
+#pragma unroll
+        for (int r = 0; r < NIN; ++r) o0[r] = s_oppA[s_idx[r * RW + c]];
+        if constexpr (TRIM) {
+            vpass_filters<HALF, TH, TH, RW, kTrimLo[0], kTrimHi[0]>(o0, taps, 0, 1, out);
+            vpass_filters<HALF, TH, TH, RW>(o0, taps, 1, 3, out);
+        } else {
+            vpass_filters<HALF, TH, TH, RW>(o0, taps, 0, 3, out);
+        }
+    } else {
+        float o1[NIN], o2[NIN];
+#pragma unroll
+        for (int r = 0; r < NIN; ++r) {
+            const float2 v = s_oppB[s_idx[r * RW + c]];
+            o1[r] = v.x; o2[r] = v.y;
+        }
+        if constexpr (TRIM) {
+            vpass_filters<HALF, TH, TH, RW, kTrimLo[1], kTrimHi[1]>(o1, taps, 3, 4, out);
+            vpass_filters<HALF, TH, TH, RW>(o1, taps, 4, 5, out);
+            vpass_filters<HALF, TH, TH, RW, kTrimLo[2], kTrimHi[2]>(o2, taps, 5, 6, out);
+            vpass_filters<HALF, TH, TH, RW>(o2, taps, 6, 7, out);
+        } else {
+            vpass_filters<HALF, TH, TH, RW>(o1, taps, 3, 5, out);
+            vpass_filters<HALF, TH, TH, RW>(o2, taps, 5, 7, out);
+        }
+    }
+}
+
+template <int HALF, int RW, int TH, int RV, int DE, int OCC, bool TRIM, bool VSPLIT>
 __global__ __launch_bounds__(256, OCC) void cost_tile_kernel(CostArgs a, CostTaps<HALF> taps,
                                                             int P_) {
     constexpr int TW = RW - 2 * HALF;
     constexpr int RH = TH + 2 * HALF;
     constexpr int NIN = RV + 2 * HALF;
     constexpr int NRUN = TW / 4;
-    static_assert(RW * (TH / RV) == 256, "one V item per thread");
+    static_assert(VSPLIT ? (RV == TH && 2 * RW == 256) : RW * (TH / RV) == 256,
+                  "one V item per thread");
     static_assert(TW % 4 == 0, "4-wide H runs");
     static_assert(TH * 32 % 256 == 0 && TH * 32 <= 512, "one or two H items per thread");
     // s_v is float4-typed so the H-pass reads stay ds_read_b128 (a float-typed
     // array let the compiler split them into 4-way-conflicted ds_read2_b32).
     __shared__ float4 s_v4[kNumFilt * TH * RW / 4];
-    // opponent table replicated OPP_REP times; lane l reads copy (l % OPP_REP),
-    // spreading the random-index gathers over more bank positions.
-    constexpr int OPP_REP = 4;
-    __shared__ float4 s_opp[kMaxK * OPP_REP];
+    // opponent table, one copy: replicating it to spread the random gathers over
+    // more banks (OPP_REP 2, 4) measured slower -- the LDS it costs is worth
+    // more as a fourth workgroup per CU (36 KiB per workgroup at TH = 8).
+    constexpr int OPP_REP = 1;
+    __shared__ float4 s_opp[VSPLIT ? 1 : kMaxK * OPP_REP];
+    __shared__ float s_oppA[VSPLIT ? kMaxK : 1];    // VSPLIT: opponent channel 0
+    __shared__ float2 s_oppB[VSPLIT ? kMaxK : 1];   // VSPLIT: opponent channels 1, 2
     __shared__ __attribute__((aligned(16))) uint8_t s_idx[RH * RW];
     __shared__ double s_red[4];
     float* s_v = reinterpret_cast<float*>(s_v4);
@@ -669,8 +715,16 @@ __global__ __launch_bounds__(256, OCC) void cost_tile_kernel(CostArgs a, CostTap
         }
     }
 
-    for (int e = tid; e < a.K * OPP_REP; e += 256)
-        s_opp[e] = a.opp[(int64_t)p * kMaxK + e / OPP_REP];
+    if constexpr (VSPLIT) {
+        for (int e = tid; e < a.K; e += 256) {
+            const float4 v = a.opp[(int64_t)p * kMaxK + e];
+            s_oppA[e] = v.x;
+            s_oppB[e] = make_float2(v.y, v.z);
+        }
+    } else {
+        for (int e = tid; e < a.K * OPP_REP; e += 256)
+            s_opp[e] = a.opp[(int64_t)p * kMaxK + e / OPP_REP];
+    }
     if (x0 - HALF >= 0 && x0 + TW + HALF <= g.W) {
         // interior columns: each region row is RW contiguous bytes; aligned dword
         // loads + alignbyte funnel shift (rows reflect vertically only)
@@ -699,7 +753,9 @@ __global__ __launch_bounds__(256, OCC) void cost_tile_kernel(CostArgs a, CostTap
     // ---- vertical pass: thread = (region column c, rows [RV*gr, RV*gr+RV)) ----
     // The filter loops are not unrolled so only one filter's 21 taps are live in
     // SGPRs at a time (all 294 taps at once spill into VGPR lanes).
-    {
+    if constexpr (VSPLIT) {
+        vpass_split<HALF, TH, RW, TRIM>(s_idx, s_oppA, s_oppB, taps, s_v, tid);
+    } else {
         const int c = tid % RW, gr = tid / RW;
         const int copy = tid & (OPP_REP - 1);
         float o0[NIN], o1[NIN], o2[NIN];
@@ -738,8 +794,7 @@ __global__ __launch_bounds__(256, OCC) void cost_tile_kernel(CostArgs a, CostTap
             float part = 0.f;
 #pragma unroll
             for (int xo = 0; xo < 4; ++xo) {
-                const float3 lab = opp2lab_fast(acc0[xo], acc1[xo], acc2[xo], a.inv_illum[0],
-                                                a.inv_illum[1], a.inv_illum[2]);
+                const float3 lab = opp2lab_fast(acc0[xo], acc1[xo], acc2[xo], a.m_lab);
                 const float e = delta_e<DE>(Ls[xo], As[xo], Bs[xo], lab.x, lab.y, lab.z);
                 part += (gx0 + xo < g.W) ? e : 0.f;
             }
@@ -926,8 +981,7 @@ __global__ __launch_bounds__(256, 2) void cost_persist_kernel(CostArgs a, CostTa
                 float part = 0.f;
 #pragma unroll
                 for (int xo = 0; xo < 4; ++xo) {
-                    const float3 l = opp2lab_fast(acc0[xo], acc1[xo], acc2[xo], a.inv_illum[0],
-                                                  a.inv_illum[1], a.inv_illum[2]);
+                    const float3 l = opp2lab_fast(acc0[xo], acc1[xo], acc2[xo], a.m_lab);
                     const float e = delta_e<DE>(Ls[xo], As[xo], Bs[xo], l.x, l.y, l.z);
                     part += (gx0 + xo < g.W) ? e : 0.f;
                 }
@@ -994,7 +1048,7 @@ __global__ __launch_bounds__(256) void gen_vpass_kernel(GenArgs a) {
             oz = fmaf(a.t[2 * n + s], a.k1[4 * t + 2], fmaf(a.t[5 * n + s], a.k2[4 * t + 2], oz));
             ox = fmaf(a.t[6 * n + s], a.absk3[t], ox);
         }
-        const float3 lab = opp2lab_fast(ox, oy, oz, a.inv_illum[0], a.inv_illum[1], a.inv_illum[2]);
+        const float3 lab = opp2lab_fast(ox, oy, oz, a.m_lab);
         const int64_t off = (int64_t)(y - a.g.r0) * a.g.lab_pitch + x;
         e = (double)delta_e<DE>(a.labL[off], a.labA[off], a.labB[off], lab.x, lab.y, lab.z);
     }
@@ -1208,6 +1262,11 @@ __global__ __launch_bounds__(256) void error_image_kernel(const float4* orig, co
 // ----------------------------------------------------------------------------
 static inline unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }
 
+void opp2xyz_over_illum(const float inv_illum[3], float m[9]) {
+    static const float opp2xyz[9] = HQ_OPP2XYZ;
+    for (int i = 0; i < 9; ++i) m[i] = opp2xyz[i] * inv_illum[i / 3];
+}
+
 hipError_t launch_prep_palette(const PaletteArgs& a, int P, hipStream_t s) {
     hipLaunchKernelGGL(prep_palette_kernel, dim3(P), dim3(256), 0, s, a);
     return hipGetLastError();
@@ -1282,8 +1341,9 @@ static void make_taps10(const float* k1, const float* k2, const float* k3, const
 constexpr int kFastHalf = 10, kFastRW = 128, kFastTH = 16, kFastRV = 8;
 constexpr int kFastTW = kFastRW - 2 * kFastHalf;
 
-// tile rows of the fast path: 16 (RV 8, 2 WG/CU) or 8 (RV 4, 3 WG/CU)
-int fast_tile_rows(int tile_cfg) { return tile_cfg == 1 ? 8 : kFastTH; }
+// tile rows of the fast path: cfg 0 = 16 (RV 8, 2 WG/CU); cfg 1 = 8 with the V
+// pass split by channel group (4 WG/CU); cfg 2 = 8 (RV 4, 4 WG/CU)
+int fast_tile_rows(int tile_cfg) { return tile_cfg == 0 ? kFastTH : 8; }
 
 void fast_tile_dims(int W, int own_rows, int tile_cfg, int* tiles_x, int* ntiles) {
     const int th = fast_tile_rows(tile_cfg);
@@ -1291,14 +1351,14 @@ void fast_tile_dims(int W, int own_rows, int tile_cfg, int* tiles_x, int* ntiles
     *ntiles = *tiles_x * ((own_rows + th - 1) / th);
 }
 
-template <int TH, int RV, int OCC, bool TRIM>
+template <int TH, int RV, int OCC, bool TRIM, bool VSPLIT>
 static void launch_tile_cfg(const CostArgs& a, int P, const CostTaps<10>& t, int de,
                             hipStream_t s) {
     if (de == 0)
-        hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, 0, OCC, TRIM>),
+        hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, 0, OCC, TRIM, VSPLIT>),
                            dim3(a.ntiles * P), dim3(256), 0, s, a, t, P);
     else
-        hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, 1, OCC, TRIM>),
+        hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, 1, OCC, TRIM, VSPLIT>),
                            dim3(a.ntiles * P), dim3(256), 0, s, a, t, P);
 }
 
@@ -1341,11 +1401,14 @@ hipError_t launch_cost_fast(const CostArgs& a, int P, const float* k1, const flo
         return hipGetLastError();
     }
     if (tile_cfg == 1) {
-        if (trim) launch_tile_cfg<8, 4, 3, true>(a, P, t, de, s);
-        else launch_tile_cfg<8, 4, 3, false>(a, P, t, de, s);
+        if (trim) launch_tile_cfg<8, 8, 4, true, true>(a, P, t, de, s);
+        else launch_tile_cfg<8, 8, 4, false, true>(a, P, t, de, s);
+    } else if (tile_cfg == 2) {
+        if (trim) launch_tile_cfg<8, 4, 4, true, false>(a, P, t, de, s);
+        else launch_tile_cfg<8, 4, 4, false, false>(a, P, t, de, s);
     } else {
-        if (trim) launch_tile_cfg<kFastTH, kFastRV, 2, true>(a, P, t, de, s);
-        else launch_tile_cfg<kFastTH, kFastRV, 2, false>(a, P, t, de, s);
+        if (trim) launch_tile_cfg<kFastTH, kFastRV, 2, true, false>(a, P, t, de, s);
+        else launch_tile_cfg<kFastTH, kFastRV, 2, false, false>(a, P, t, de, s);
     }
     return hipGetLastError();
 }

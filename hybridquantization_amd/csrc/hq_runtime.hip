@@ -23,6 +23,7 @@ hipError_t launch_prep_palette(const PaletteArgs&, int P, hipStream_t);
 hipError_t launch_build_grid(const GridArgs&, int P, hipStream_t);
 hipError_t launch_assign(const AssignArgs&, int P, int rep, int group, hipStream_t);
 void fast_tile_dims(int W, int own_rows, int tile_cfg, int* tiles_x, int* ntiles);
+void opp2xyz_over_illum(const float inv_illum[3], float m[9]);
 hipError_t launch_cost_fast(const CostArgs&, int P, const float* k1, const float* k2,
                             const float* k3, const float* absk3, int de, int persistent,
                             int tile_cfg, int num_cu, bool trim, hipStream_t);
@@ -107,7 +108,7 @@ struct hq_ctx {
     int assign_blocks_per_cu = 8;
     int assign_rep = 1;    // palette replication in the assign kernel's LDS
     int assign_group = 1;  // palettes per pixel pass in the assign kernel (1, 2, 4)
-    int tile_cfg = 1;      // cost tile: 0 = 16 rows (2 WG/CU), 1 = 8 rows (3 WG/CU)
+    int tile_cfg = 2;      // cost tile: 0 = 16 rows, 1 = 8 rows + split V pass, 2 = 8 rows
     int trim = 1;          // skip taps < 1e-9 of the peak of the narrow k1 filters
     bool trim_ok = false;  // set by hq_set_filters (default 21-tap filter set)
 
@@ -363,7 +364,7 @@ int enqueue_eval(hq_ctx* c, int P, int K) {
         ca.K = K;
         ca.tiles_x = tiles_x;
         ca.ntiles = ntiles;
-        std::memcpy(ca.inv_illum, inv, sizeof inv);
+        opp2xyz_over_illum(inv, ca.m_lab);
         HIP_TRY(c, launch_cost_fast(ca, P, c->k1.data(), c->k2.data(), c->k3.data(),
                                     c->absk3.data(), c->de_type, c->cost_variant == 2,
                                     c->tile_cfg, c->num_cu, c->trim && c->trim_ok, s));
@@ -387,7 +388,7 @@ int enqueue_eval(hq_ctx* c, int P, int K) {
             ga.partial = c->d_partial.as<double>() + (int64_t)p * nparts;
             ga.g = g;
             ga.half = c->half;
-            std::memcpy(ga.inv_illum, inv, sizeof inv);
+            opp2xyz_over_illum(inv, ga.m_lab);
             HIP_TRY(c, launch_cost_generic(ga, c->de_type, s));
         }
     }
@@ -842,7 +843,7 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
     } else if (!std::strcmp(name, "trim")) {
         c->trim = value != 0;
     } else if (!std::strcmp(name, "cost_tile")) {
-        if (value != 0 && value != 1) return fail(c, HQ_ERR_ARG, "cost_tile in {0,1}");
+        if (value < 0 || value > 2) return fail(c, HQ_ERR_ARG, "cost_tile in {0,1,2}");
         c->tile_cfg = value;
     } else if (!std::strcmp(name, "assign_group")) {
         if (value != 1 && value != 2 && value != 4) return fail(c, HQ_ERR_ARG, "assign_group in {1,2,4}");

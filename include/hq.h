@@ -182,7 +182,9 @@ int hq_profile_reset(hq_ctx *ctx);
  *   "grid"         argmin pruning resolution G2: 0 = exhaustive, 16, 32 (default), 64
  *   "cost_variant" 0 = one tile per workgroup (default), 1 = generic two-pass
  *                  path (any filter length), 2 = persistent pipelined tiles
- *   "cost_tile"    0 = 16-row tiles (2 WG/CU), 1 = 8-row tiles (3 WG/CU, default)
+ *   "cost_tile"    0 = 16-row tiles (2 WG/CU); 1 = 8-row tiles with the vertical pass
+ *                  split by opponent-channel group (4 WG/CU); 2 = 8-row tiles, 4-row
+ *                  vertical items (4 WG/CU, default)
  *   "trim"         1 = skip the narrow k1 filters' taps below 1e-9 of their peak
  *                  (default; only when the filters allow it), 0 = all taps
  *   "assign_rep"   palette replication in the assign kernel's LDS: 1 (default), 2, 4, 16

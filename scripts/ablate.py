@@ -1,0 +1,93 @@
+"""Ablation builds of the cost kernel (timing experiments only; results are wrong).
+
+    python scripts/ablate.py            # writes build_exp/libhq_<name>.so
+    python scripts/profile_eval.py --lib build_exp/libhq_novfma.so
+
+Each variant is hq_kernels.hip with one part of cost_tile_kernel removed by a
+string patch on a copy (the product source is never modified); the delta
+against "base" is that part's share of the kernel time (DESIGN.md
+"Performance log").
+"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "hybridquantization_amd", "csrc")
+OUT = os.path.join(ROOT, "build_exp")
+
+PATCHES = {
+    "base": [],
+    # vertical taps -> one multiply
+    "novfma": [("            for (int y = 0; y < RV; ++y) acc[y] = fmaf(o[y + t], k, acc[y]);",
+                "            for (int y = 0; y < RV; ++y) if (t == THI) acc[y] = o[y + t] * k;")],
+    # horizontal taps -> one multiply
+    "nohfma": [("            for (int xo = 0; xo < 4; ++xo) acc[xo] = fmaf(in[xo + t], k, acc[xo]);",
+                "            for (int xo = 0; xo < 4; ++xo) if (t == THI) acc[xo] += in[xo + t] * k;")],
+    # gather without the index dependency (same number of LDS reads)
+    "nogather": [("            const float4 v = s_opp[s_idx[(gr * RV + r) * RW + c] * OPP_REP + copy];",
+                  "            const float4 v = s_opp[((c + r) & 255) * OPP_REP + copy];")],
+    # no Opp->Lab / dE
+    "nolab": [("                const float3 lab = opp2lab_fast(acc0[xo], acc1[xo], acc2[xo], a.inv_illum[0],\n"
+               "                                                a.inv_illum[1], a.inv_illum[2]);\n"
+               "                const float e = delta_e<DE>(Ls[xo], As[xo], Bs[xo], lab.x, lab.y, lab.z);",
+               "                const float e = acc0[xo] + acc1[xo] + acc2[xo] + Ls[xo] + As[xo] + Bs[xo];")],
+    # index rows not loaded from HBM (synthetic bytes)
+    "noidxload": [("            const uint32_t lo = src[0], hi = src[1];",
+                   "            const uint32_t lo = (uint32_t)(e + (int)(intptr_t)src) * 2654435761u, hi = lo ^ 0x5bd1e995u;")],
+    # opponent table not loaded (synthetic)
+    "nooppload": [("        s_opp[e] = a.opp[(int64_t)p * kMaxK + e / OPP_REP];",
+                   "        s_opp[e] = make_float4(e * 1e-3f, p * 1e-3f, 0.5f, 0.f);")],
+    # LabRef not loaded
+    "nolabload": [("            labL[h] = *reinterpret_cast<const float4*>(a.labL + off);\n"
+                   "            labA[h] = *reinterpret_cast<const float4*>(a.labA + off);\n"
+                   "            labB[h] = *reinterpret_cast<const float4*>(a.labB + off);",
+                   "            labL[h] = make_float4(off * 1e-9f, 1.f, 2.f, 3.f);")],
+    # gather address uniform over the wave (LDS broadcast: no bank conflicts)
+    "gatherbcast": [("            const float4 v = s_opp[s_idx[(gr * RV + r) * RW + c] * OPP_REP + copy];",
+                     "            const float4 v = s_opp[((gr * RV + r) & 255) * OPP_REP + copy];")],
+    # H reads at a wave-uniform address (broadcast)
+    "hreadbcast": [("        const float4* src = &s_v4[(y * RW) / 4 + j];\n        float acc0[4], acc1[4], acc2[4];\n        hpass_all<HALF, TH, RW, TRIM>(src, taps, acc0, acc1, acc2);\n        const int gy = y0 + y, gx0 = x0 + 4 * j;\n        if (gy < g.r1 && gx0 < g.W) {\n            const float4 L4",
+                    "        const float4* src = &s_v4[(tid >> 6) * 8];\n        float acc0[4], acc1[4], acc2[4];\n        hpass_all<HALF, TH, RW, TRIM>(src, taps, acc0, acc1, acc2);\n        const int gy = y0 + y, gx0 = x0 + 4 * j;\n        if (gy < g.r1 && gx0 < g.W) {\n            const float4 L4")],
+}
+# H pass with separate accumulators for even and odd taps (4 independent chains)
+PATCHES["hsplit"] = [(
+    "            for (int xo = 0; xo < 4; ++xo) acc[xo] = fmaf(in[xo + t], k, acc[xo]);",
+    "            for (int xo = 0; xo < 4; ++xo) { if (t & 1) acc2[xo] = fmaf(in[xo + t], k, acc2[xo]); else acc[xo] = fmaf(in[xo + t], k, acc[xo]); }"),
+    ("        float in[4 * NQ];\n", "        float in[4 * NQ];\n        float acc2[4] = {0.f, 0.f, 0.f, 0.f};\n"),
+    ("            for (int xo = 0; xo < 4; ++xo) { if (t & 1) acc2[xo] = fmaf(in[xo + t], k, acc2[xo]); else acc[xo] = fmaf(in[xo + t], k, acc[xo]); }\n        }\n",
+     "            for (int xo = 0; xo < 4; ++xo) { if (t & 1) acc2[xo] = fmaf(in[xo + t], k, acc2[xo]); else acc[xo] = fmaf(in[xo + t], k, acc[xo]); }\n        }\n#pragma unroll\n        for (int xo = 0; xo < 4; ++xo) acc[xo] += acc2[xo];\n")]
+# extra compiler flags per variant
+FLAGS = {"noslp": ["-fno-slp-vectorize"], "noslp_hsplit": ["-fno-slp-vectorize"]}
+PATCHES["noslp"] = []
+PATCHES["noslp_hsplit"] = PATCHES["hsplit"]
+PATCHES["skeleton"] = PATCHES["novfma"] + PATCHES["nohfma"] + PATCHES["nolab"]
+PATCHES["skeleton_bcast"] = PATCHES["skeleton"] + PATCHES["gatherbcast"]
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    src = open(os.path.join(CSRC, "hq_kernels.hip")).read()
+    names = sys.argv[1:] or list(PATCHES)
+    for name in names:
+        s = src
+        for old, new in PATCHES[name]:
+            if old not in s:
+                sys.exit(f"{name}: patch anchor not found")
+            s = s.replace(old, new)
+        path = os.path.join(OUT, f"hq_kernels_{name}.hip")
+        open(path, "w").write(s)
+        obj = os.path.join(OUT, f"hq_kernels_{name}.o")
+        flags = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-I/opt/rocm/include",
+                 "-I" + CSRC, "-munsafe-fp-atomics", *FLAGS.get(name, [])]
+        subprocess.check_call(["/opt/rocm/bin/hipcc", *flags, "-c", path, "-o", obj])
+        so = os.path.join(OUT, f"libhq_{name}.so")
+        subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", obj,
+                               os.path.join(CSRC, "hq_runtime.o"), os.path.join(CSRC, "hq_host.o"),
+                               "-shared", "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib",
+                               "-o", so])
+        print("built", so)
+
+
+if __name__ == "__main__":
+    main()

@@ -28,11 +28,14 @@ def main():
     ap.add_argument("--evals", type=int, default=10)
     ap.add_argument("--grid", type=int, default=32)
     ap.add_argument("--variant", type=int, default=0)
-    ap.add_argument("--tile", type=int, default=1)
+    ap.add_argument("--tile", type=int, default=2)
     ap.add_argument("--rep", type=int, default=1)
     ap.add_argument("--trim", type=int, default=1)
     ap.add_argument("--group", type=int, default=1)
+    ap.add_argument("--lib", default=None, help="alternative libhq build (scripts/ablate.py)")
     args = ap.parse_args()
+    if args.lib:
+        _lib.LIB_PATH = os.path.abspath(args.lib)
     lib = hq.load()
     m = hq.ImageManipulation(device=0)
     sp = hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
@@ -64,7 +67,7 @@ def main():
         n = C.c_int64()
         lib.hq_profile_get(m.ctx, k.encode(), C.byref(ms), C.byref(n))
         out.append(f"{k}={ms.value / max(n.value, 1):.4f}ms")
-    print(f"size={W} K={args.K} P={args.P} grid={args.grid} variant={args.variant} tile={args.tile} rep={args.rep} trim={args.trim} group={args.group}: "
+    print(f"{os.path.basename(args.lib or 'libhq.so')} size={W} K={args.K} P={args.P} grid={args.grid} variant={args.variant} tile={args.tile} rep={args.rep} trim={args.trim} group={args.group}: "
           f"{el / args.evals * 1e3:.3f} ms/eval-population, "
           f"{W * H * args.P * args.evals / el / 1e6:.1f} Mpx*evals/s  ", " ".join(out),
           "costs", costs.tolist())
