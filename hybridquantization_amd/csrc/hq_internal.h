@@ -10,6 +10,7 @@ namespace hq {
 constexpr int kMaxK = 256;        // u8 palette indices (K <= 256 on this path)
 constexpr int kMaxTaps = 255;     // generic path limit (2*half+1)
 constexpr int kNumFilt = 7;       // separable filter pairs of the S-CIELAB stencil
+constexpr int kCostPartsPerTile = 1;  // fp64 partials per cost tile (sizing; launch_cost_fast)
 constexpr int kL1Cap = 31;        // level-1 candidate list capacity (32-B entry)
 constexpr int kL2Cap = 15;        // level-2 candidate list capacity (16-B entry)
 constexpr uint8_t kOverflow = 255;
@@ -77,6 +78,8 @@ struct AssignArgs {
 struct CostArgs {
     const uint8_t* idx;     // [P][idx_pitch]
     const float4* opp;      // [P][256]
+    const uint4* vfrag;     // cost_tile 3: [7][hi, lo][64 lanes] f16x8 B fragments of the
+                            // vertical Toeplitz taps (build_vpass_fragments)
     const float* labL;      // planar LabRef, owned rows, pitch lab_pitch
     const float* labA;
     const float* labB;

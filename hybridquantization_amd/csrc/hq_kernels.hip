@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 
 namespace hq {
 
@@ -131,6 +132,28 @@ template <typename V>
 __device__ __forceinline__ V wave_sum(V v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    return v;
+}
+
+// Sum of a double over the wave with DPP moves only (no LDS round trips: the
+// __shfl_down tree above is 12 dependent ds_bpermute for an f64).  Fixed order:
+// row_shr 1, 2, 4, 8 leave each 16-lane row's sum in its lane 15; row_bcast 15
+// and 31 fold the rows into lane 63, which alone holds the total.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, ROW_MASK, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, ROW_MASK, 0xf, true);
+    return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+__device__ __forceinline__ double wave_sum_to_lane63(double v) {
+    v += dpp_f64<0x111, 0xf>(v);  // row_shr:1
+    v += dpp_f64<0x112, 0xf>(v);  // row_shr:2
+    v += dpp_f64<0x114, 0xf>(v);  // row_shr:4
+    v += dpp_f64<0x118, 0xf>(v);  // row_shr:8
+    v += dpp_f64<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
+    v += dpp_f64<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3
     return v;
 }
 
@@ -664,28 +687,110 @@ __device__ __forceinline__ void vpass_split(const uint8_t* s_idx, const float* s
     }
 }
 
-template <int HALF, int RW, int TH, int RV, int DE, int OCC, bool TRIM, bool VSPLIT>
+// ---- vertical pass on the matrix cores (cost_tile 3) -------------------------
+// The vertical pass of one filter over a 16-column block is a banded-Toeplitz
+// product V^T = X^T . T^T with X the block's TH + 2*HALF gathered input rows:
+// v_mfma_f32_16x16x32_f16 with A = X^T (16 columns x 32 input rows, rows past
+// the region zero-weighted), B = T^T (32 input rows x 16 output rows, the TH
+// valid ones carrying the taps) -- one K step.  fp32 accuracy from f16 operands:
+// x = hi + lo (both f16, x scaled by 2^14 so lo stays normal down to |x| ~ 1e-5)
+// and the products hi.hi + hi.lo + lo.hi (each exact in the f32 accumulator;
+// the dropped lo.lo is ~2^-22 relative).  Taps are split the same way on the
+// host, scaled by 2^16 (build_vpass_fragments); the 2^30 total scale is folded
+// into the horizontal taps, exactly (a power of two).
+// Lane l of the 16x16 result holds output row (l & 15) of four consecutive
+// columns 4(l >> 4) .. +3 -- one float4 into s_v[f][row][col], the layout the
+// horizontal pass already reads.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr float kVDataScale = 16384.0f;                   // 2^14
+constexpr float kVTapScale = 65536.0f;                    // 2^16
+constexpr float kVOutScale = 1.0f / (16384.0f * 65536.0f);  // 2^-30
+
+// (hi, lo) f16 split of x * 2^14 in one dword, hi in bits 0-15.
+__device__ __forceinline__ uint32_t split_f16(float x) {
+    const float xs = x * kVDataScale;
+    const _Float16 hi = (_Float16)xs;
+    const _Float16 lo = (_Float16)(xs - (float)hi);
+    return (uint32_t)__builtin_bit_cast(uint16_t, hi) |
+           ((uint32_t)__builtin_bit_cast(uint16_t, lo) << 16);
+}
+
+__device__ __forceinline__ uint32_t chan(const uint4& v, int c) {
+    return c == 0 ? v.x : (c == 1 ? v.y : v.z);
+}
+
+template <int HALF, int TH, int RW, int IDXP, int SVP>
+__device__ __forceinline__ void vpass_mfma(const uint8_t* s_idx, const uint4* s_opph,
+                                           const uint4 (&bf)[2 * kNumFilt], float* s_v, int tid) {
+    static_assert(TH + 2 * HALF <= 32 && TH <= 16, "one K = 32 step per output block");
+    static_assert(RW % 64 == 0, "whole 16-column blocks, the same number per wave");
+    constexpr int BPW = RW / 64;  // column blocks per wave
+    const int lane = tid & 63, wave = tid >> 6;
+    const int g = lane >> 4, n = lane & 15;
+#pragma unroll
+    for (int bi = 0; bi < BPW; ++bi) {
+        const int cb = wave * BPW + bi;
+        // A fragment rows: input rows 8g .. 8g+7 of column cb*16 + n
+        uint4 e[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) e[j] = s_opph[s_idx[(8 * g + j) * IDXP + cb * 16 + n]];
+        u32x4 ah[3], al[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const uint32_t w0 = chan(e[2 * m], c), w1 = chan(e[2 * m + 1], c);
+                ah[c][m] = __builtin_amdgcn_perm(w1, w0, 0x05040100u);  // hi halves
+                al[c][m] = __builtin_amdgcn_perm(w1, w0, 0x07060302u);  // lo halves
+            }
+        }
+#pragma unroll
+        for (int f = 0; f < kNumFilt; ++f) {
+            const int c = filt_chan(f);
+            const f16x8 a_hi = __builtin_bit_cast(f16x8, ah[c]);
+            const f16x8 a_lo = __builtin_bit_cast(f16x8, al[c]);
+            const f16x8 b_hi = __builtin_bit_cast(f16x8, bf[2 * f]);
+            const f16x8 b_lo = __builtin_bit_cast(f16x8, bf[2 * f + 1]);
+            f32x4 d = {0.f, 0.f, 0.f, 0.f};
+            d = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_lo, b_hi, d, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_hi, b_lo, d, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_hi, b_hi, d, 0, 0, 0);
+            if (n < TH) *reinterpret_cast<f32x4*>(s_v + (f * TH + n) * SVP + cb * 16 + 4 * g) = d;
+        }
+    }
+}
+
+// VMODE: 0 = V items of RV rows on VALU, 1 = V split by channel group (VALU),
+// 2 = V pass on the matrix cores (vpass_mfma).
+template <int HALF, int RW, int TH, int RV, int DE, int OCC, bool TRIM, int VMODE>
 __global__ __launch_bounds__(256, OCC) void cost_tile_kernel(CostArgs a, CostTaps<HALF> taps,
                                                             int P_) {
+    constexpr bool VSPLIT = VMODE == 1, VMFMA = VMODE == 2;
     constexpr int TW = RW - 2 * HALF;
     constexpr int RH = TH + 2 * HALF;
     constexpr int NIN = RV + 2 * HALF;
     constexpr int NRUN = TW / 4;
-    static_assert(VSPLIT ? (RV == TH && 2 * RW == 256) : RW * (TH / RV) == 256,
+    static_assert(VMFMA || (VSPLIT ? (RV == TH && 2 * RW == 256) : RW * (TH / RV) == 256),
                   "one V item per thread");
     static_assert(TW % 4 == 0, "4-wide H runs");
     static_assert(TH * 32 % 256 == 0 && TH * 32 <= 512, "one or two H items per thread");
     // s_v is float4-typed so the H-pass reads stay ds_read_b128 (a float-typed
     // array let the compiler split them into 4-way-conflicted ds_read2_b32).
-    __shared__ float4 s_v4[kNumFilt * TH * RW / 4];
+    // Row pitches of s_v (floats) and s_idx (bytes).  VMFMA pads both by 16 B:
+    // its float4 stores of 8 rows at once (and its index reads of 4 rows) would
+    // otherwise land on one bank set (8-way conflicts at a 512-B pitch).
+    constexpr int SVP = VMFMA ? RW + 4 : RW, IDXP = VMFMA ? RW + 4 : RW;
+    __shared__ float4 s_v4[kNumFilt * TH * SVP / 4];
     // opponent table, one copy: replicating it to spread the random gathers over
-    // more banks (OPP_REP 2, 4) measured slower -- the LDS it costs is worth
+    // more banks (2 or 4 copies) measured slower -- the LDS it costs is worth
     // more as a fourth workgroup per CU (36 KiB per workgroup at TH = 8).
-    constexpr int OPP_REP = 1;
-    __shared__ float4 s_opp[VSPLIT ? 1 : kMaxK * OPP_REP];
+    __shared__ float4 s_opp[VMODE == 0 ? kMaxK : 1];
     __shared__ float s_oppA[VSPLIT ? kMaxK : 1];    // VSPLIT: opponent channel 0
     __shared__ float2 s_oppB[VSPLIT ? kMaxK : 1];   // VSPLIT: opponent channels 1, 2
-    __shared__ __attribute__((aligned(16))) uint8_t s_idx[RH * RW];
+    __shared__ uint4 s_opph[VMFMA ? kMaxK : 1];     // VMFMA: split_f16 of channels 0-2
+    constexpr int IDX_ROWS = VMFMA ? 32 : RH;       // VMFMA reads a whole K = 32 step
+    __shared__ __attribute__((aligned(16))) uint8_t s_idx[IDX_ROWS * IDXP];
     __shared__ double s_red[4];
     float* s_v = reinterpret_cast<float*>(s_v4);
 
@@ -698,8 +803,87 @@ __global__ __launch_bounds__(256, OCC) void cost_tile_kernel(CostArgs a, CostTap
     const int x0 = tx * TW, y0 = g.r0 + ty * TH;
     const uint8_t* idx = a.idx + (int64_t)p * g.idx_pitch;
 
-    // LabRef of this thread's H items, loaded first so the HBM latency overlaps
-    // the index fill and the V pass instead of stalling the H pass.
+    // ---- prologue.  Every global load of the fill is issued before the first
+    // wait: vmcnt retires in order, so a load -> wait -> store loop pays one
+    // memory round trip per trip (4 for the interior index rows, 14 for the
+    // byte gathers of edge tiles) and waits for anything issued before it.
+    // LabRef is loaded after the fill, so it is in flight during the V pass.
+    constexpr int DW = RW / 4;
+    constexpr int NFD = (RH * DW + 255) / 256, NFB = (RH * RW + 255) / 256;
+    static_assert(kMaxK == 256, "one opponent-table entry per thread");
+    const bool interior = x0 - HALF >= 0 && x0 + TW + HALF <= g.W;
+    const float4 ov = tid < a.K ? a.opp[(int64_t)p * kMaxK + tid] : make_float4(0.f, 0.f, 0.f, 0.f);
+    uint4 bf[VMFMA ? 2 * kNumFilt : 1];  // Toeplitz B fragments, L2-resident
+    if constexpr (VMFMA) {
+#pragma unroll
+        for (int i = 0; i < 2 * kNumFilt; ++i) bf[i] = a.vfrag[i * 64 + (tid & 63)];
+    }
+    uint32_t flo[NFD], fhi[NFD], fsh[NFD], fb[NFB];
+    if (interior) {
+        // each region row is RW contiguous bytes: aligned dword pairs + alignbyte
+        // funnel shift (rows reflect vertically only)
+#pragma unroll
+        for (int q = 0; q < NFD; ++q) {
+            const int e = tid + 256 * q;
+            flo[q] = fhi[q] = fsh[q] = 0u;
+            if (e < RH * DW) {
+                const int i = e / DW, k = e % DW;
+                int gy = reflect_clamp(y0 - HALF + i, g.H);
+                gy = min(max(gy, g.e0), g.e1 - 1);
+                const int64_t base = (int64_t)(gy - g.e0) * g.W + (x0 - HALF);
+                const uint32_t* src =
+                    reinterpret_cast<const uint32_t*>(idx + (base & ~(int64_t)3)) + k;
+                flo[q] = src[0];
+                fhi[q] = src[1];
+                fsh[q] = (uint32_t)(base & 3);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < NFB; ++q) {
+            const int e = tid + 256 * q;
+            fb[q] = 0u;
+            if (e < RH * RW) {
+                const int i = e / RW, j = e % RW;
+                int gy = reflect_clamp(y0 - HALF + i, g.H);
+                gy = min(max(gy, g.e0), g.e1 - 1);
+                const int gx = reflect_clamp(x0 - HALF + j, g.W);
+                fb[q] = idx[(int64_t)(gy - g.e0) * g.W + gx];
+            }
+        }
+    }
+    // LDS writes (the first one waits for all the loads above)
+    if constexpr (VMFMA) {
+        // every entry finite: the padding rows of the K = 32 step gather too
+        s_opph[tid] = tid < a.K ? make_uint4(split_f16(ov.x), split_f16(ov.y), split_f16(ov.z), 0u)
+                                : make_uint4(0u, 0u, 0u, 0u);
+        for (int e = tid; e < (IDX_ROWS - RH) * IDXP / 4; e += 256)
+            reinterpret_cast<uint32_t*>(s_idx + RH * IDXP)[e] = 0u;
+    } else if constexpr (VSPLIT) {
+        if (tid < a.K) {
+            s_oppA[tid] = ov.x;
+            s_oppB[tid] = make_float2(ov.y, ov.z);
+        }
+    } else {
+        if (tid < a.K) s_opp[tid] = ov;
+    }
+    if (interior) {
+#pragma unroll
+        for (int q = 0; q < NFD; ++q) {
+            const int e = tid + 256 * q;
+            if (e < RH * DW)
+                reinterpret_cast<uint32_t*>(s_idx)[(e / DW) * (IDXP / 4) + e % DW] =
+                    __builtin_amdgcn_alignbyte(fhi[q], flo[q], fsh[q]);
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < NFB; ++q) {
+            const int e = tid + 256 * q;
+            if (e < RH * RW) s_idx[(e / RW) * IDXP + e % RW] = (uint8_t)fb[q];
+        }
+    }
+
+    // LabRef of this thread's H items
     constexpr int NH = TH * 32 / 256;
     float4 labL[NH], labA[NH], labB[NH];
 #pragma unroll
@@ -714,60 +898,27 @@ __global__ __launch_bounds__(256, OCC) void cost_tile_kernel(CostArgs a, CostTap
             labB[h] = *reinterpret_cast<const float4*>(a.labB + off);
         }
     }
-
-    if constexpr (VSPLIT) {
-        for (int e = tid; e < a.K; e += 256) {
-            const float4 v = a.opp[(int64_t)p * kMaxK + e];
-            s_oppA[e] = v.x;
-            s_oppB[e] = make_float2(v.y, v.z);
-        }
-    } else {
-        for (int e = tid; e < a.K * OPP_REP; e += 256)
-            s_opp[e] = a.opp[(int64_t)p * kMaxK + e / OPP_REP];
-    }
-    if (x0 - HALF >= 0 && x0 + TW + HALF <= g.W) {
-        // interior columns: each region row is RW contiguous bytes; aligned dword
-        // loads + alignbyte funnel shift (rows reflect vertically only)
-        constexpr int DW = RW / 4;
-        for (int e = tid; e < RH * DW; e += 256) {
-            const int i = e / DW, k = e % DW;
-            int gy = reflect_clamp(y0 - HALF + i, g.H);
-            gy = min(max(gy, g.e0), g.e1 - 1);
-            const int64_t base = (int64_t)(gy - g.e0) * g.W + (x0 - HALF);
-            const uint32_t* src = reinterpret_cast<const uint32_t*>(idx + (base & ~(int64_t)3)) + k;
-            const uint32_t lo = src[0], hi = src[1];
-            reinterpret_cast<uint32_t*>(s_idx)[e] =
-                __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(base & 3));
-        }
-    } else {
-        for (int e = tid; e < RH * RW; e += 256) {
-            const int i = e / RW, j = e % RW;
-            int gy = reflect_clamp(y0 - HALF + i, g.H);
-            gy = min(max(gy, g.e0), g.e1 - 1);
-            const int gx = reflect_clamp(x0 - HALF + j, g.W);
-            s_idx[e] = idx[(int64_t)(gy - g.e0) * g.W + gx];
-        }
-    }
     __syncthreads();
 
     // ---- vertical pass: thread = (region column c, rows [RV*gr, RV*gr+RV)) ----
     // The filter loops are not unrolled so only one filter's 21 taps are live in
     // SGPRs at a time (all 294 taps at once spill into VGPR lanes).
-    if constexpr (VSPLIT) {
+    if constexpr (VMFMA) {
+        vpass_mfma<HALF, TH, RW, IDXP, SVP>(s_idx, s_opph, bf, s_v, tid);
+    } else if constexpr (VSPLIT) {
         vpass_split<HALF, TH, RW, TRIM>(s_idx, s_oppA, s_oppB, taps, s_v, tid);
     } else {
         const int c = tid % RW, gr = tid / RW;
-        const int copy = tid & (OPP_REP - 1);
         float o0[NIN], o1[NIN], o2[NIN];
         float wsum = 0.f;  // .w (= 0) is consumed so the gather stays one ds_read_b128
 #pragma unroll
         for (int r = 0; r < NIN; ++r) {
-            const float4 v = s_opp[s_idx[(gr * RV + r) * RW + c] * OPP_REP + copy];
+            const float4 v = s_opp[s_idx[(gr * RV + r) * IDXP + c]];
             o0[r] = v.x; o1[r] = v.y; o2[r] = v.z;
             wsum += v.w;
         }
         o0[0] += wsum;  // wsum == 0 exactly (prep_palette writes .w = 0)
-        float* out = s_v + (gr * RV) * RW + c;
+        float* out = s_v + (gr * RV) * SVP + c;
         vpass_all<HALF, RV, TH, RW, TRIM>(o0, o1, o2, taps, out);
     }
     __syncthreads();
@@ -782,9 +933,9 @@ __global__ __launch_bounds__(256, OCC) void cost_tile_kernel(CostArgs a, CostTap
     for (int h = 0; h < NH; ++h) {
         const int item = tid + 256 * h, y = item >> 5, j = item & 31;
         if (j >= NRUN) continue;
-        const float4* src = &s_v4[(y * RW) / 4 + j];
+        const float4* src = &s_v4[(y * SVP) / 4 + j];
         float acc0[4], acc1[4], acc2[4];
-        hpass_all<HALF, TH, RW, TRIM>(src, taps, acc0, acc1, acc2);
+        hpass_all<HALF, TH, SVP, TRIM>(src, taps, acc0, acc1, acc2);
         const int gy = y0 + y, gx0 = x0 + 4 * j;
         if (gy < g.r1 && gx0 < g.W) {
             const float4 L4 = labL[h], A4 = labA[h], B4 = labB[h];
@@ -801,8 +952,8 @@ __global__ __launch_bounds__(256, OCC) void cost_tile_kernel(CostArgs a, CostTap
             sum += (double)part;
         }
     }
-    sum = wave_sum(sum);
-    if ((tid & 63) == 0) s_red[tid >> 6] = sum;
+    sum = wave_sum_to_lane63(sum);
+    if ((tid & 63) == 63) s_red[tid >> 6] = sum;
     __syncthreads();
     if (tid == 0)
         a.partial[(int64_t)p * a.ntiles + tile] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
@@ -1336,13 +1487,62 @@ static void make_taps10(const float* k1, const float* k2, const float* k3, const
     }
 }
 
+// f32 -> f16 bits, round to nearest even (host; finite inputs well inside the
+// f16 range after scaling, subnormal results included).
+static uint16_t host_f16(float x) {
+    uint32_t u;
+    std::memcpy(&u, &x, 4);
+    const uint32_t sign = (u >> 16) & 0x8000u;
+    const float ax = std::fabs(x);
+    if (ax < 5.9604645e-08f * 0.5f) return (uint16_t)sign;          // below half the smallest subnormal
+    if (ax < 6.1035156e-05f) {                                        // f16 subnormal: multiples of 2^-24
+        const float q = std::nearbyint(ax * 16777216.0f);             // round-half-even (default mode)
+        return (uint16_t)(sign | (uint32_t)q);
+    }
+    uint32_t a = u & 0x7fffffffu;
+    const uint32_t mant = a & 0x7fffffu;
+    int32_t e = (int32_t)(a >> 23) - 127 + 15;
+    uint32_t m = mant >> 13, rem = mant & 0x1fffu;
+    if (rem > 0x1000u || (rem == 0x1000u && (m & 1u))) {
+        if (++m == 0x400u) { m = 0; ++e; }
+    }
+    return (uint16_t)(sign | ((uint32_t)e << 10) | m);
+}
+
+static float host_f16_to_f32(uint16_t h) {
+    const uint32_t e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
+    const float v = e == 0 ? std::ldexp((float)m, -24) : std::ldexp((float)(m | 0x400u), (int)e - 25);
+    return (h & 0x8000u) ? -v : v;
+}
+
+// B fragments of v_mfma_f32_16x16x32_f16 for the matrix-core vertical pass
+// (vpass_mfma): lane l holds B[k = 8(l >> 4) + j][n = l & 15], j = 0..7, with
+// B[i][r] = v-tap (i - r) of the filter for output rows r < 8 and 0 <= i - r <= 20,
+// scaled by 2^16 and split into hi / lo f16.  out: [7][2][64][8] f16 bits.
+void build_vpass_fragments(const float* k1, const float* k2, const float* k3,
+                           const float* absk3, uint16_t* out) {
+    CostTaps<10> t;
+    make_taps10(k1, k2, k3, absk3, t);
+    for (int f = 0; f < kNumFilt; ++f)
+        for (int l = 0; l < 64; ++l)
+            for (int j = 0; j < 8; ++j) {
+                const int i = 8 * (l >> 4) + j, r = l & 15, d = i - r;
+                const float w = (r < 8 && d >= 0 && d <= 20) ? t.v[f][d] * kVTapScale : 0.f;
+                const uint16_t hi = host_f16(w);
+                const uint16_t lo = host_f16(w - host_f16_to_f32(hi));
+                out[((f * 2 + 0) * 64 + l) * 8 + j] = hi;
+                out[((f * 2 + 1) * 64 + l) * 8 + j] = lo;
+            }
+}
+
 // Tile geometry of the fast path (HALF = 10): RW = 128 region columns,
 // TW = 108 output columns, TH = 16 output rows, RV = 8 rows per V item.
 constexpr int kFastHalf = 10, kFastRW = 128, kFastTH = 16, kFastRV = 8;
 constexpr int kFastTW = kFastRW - 2 * kFastHalf;
 
 // tile rows of the fast path: cfg 0 = 16 (RV 8, 2 WG/CU); cfg 1 = 8 with the V
-// pass split by channel group (4 WG/CU); cfg 2 = 8 (RV 4, 4 WG/CU)
+// pass split by channel group (4 WG/CU); cfg 2 = 8 (RV 4, 4 WG/CU); cfg 3 = 8
+// with the V pass on the matrix cores
 int fast_tile_rows(int tile_cfg) { return tile_cfg == 0 ? kFastTH : 8; }
 
 void fast_tile_dims(int W, int own_rows, int tile_cfg, int* tiles_x, int* ntiles) {
@@ -1351,14 +1551,14 @@ void fast_tile_dims(int W, int own_rows, int tile_cfg, int* tiles_x, int* ntiles
     *ntiles = *tiles_x * ((own_rows + th - 1) / th);
 }
 
-template <int TH, int RV, int OCC, bool TRIM, bool VSPLIT>
+template <int TH, int RV, int OCC, bool TRIM, int VMODE>
 static void launch_tile_cfg(const CostArgs& a, int P, const CostTaps<10>& t, int de,
                             hipStream_t s) {
     if (de == 0)
-        hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, 0, OCC, TRIM, VSPLIT>),
+        hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, 0, OCC, TRIM, VMODE>),
                            dim3(a.ntiles * P), dim3(256), 0, s, a, t, P);
     else
-        hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, 1, OCC, TRIM, VSPLIT>),
+        hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, 1, OCC, TRIM, VMODE>),
                            dim3(a.ntiles * P), dim3(256), 0, s, a, t, P);
 }
 
@@ -1389,9 +1589,11 @@ bool trim_window_ok(const float* k1) {
 
 hipError_t launch_cost_fast(const CostArgs& a, int P, const float* k1, const float* k2,
                             const float* k3, const float* absk3, int de, int persistent,
-                            int tile_cfg, int num_cu, bool trim, hipStream_t s) {
+                            int tile_cfg, int num_cu, bool trim, int* parts_per_tile,
+                            hipStream_t s) {
     CostTaps<10> t;
     make_taps10(k1, k2, k3, absk3, t);
+    *parts_per_tile = 1;
     if (persistent && tile_cfg == 0) {  // the persistent kernel exists for 16-row tiles
         const int nitems = a.ntiles * P;
         int G = std::min(2 * num_cu, nitems);
@@ -1400,15 +1602,20 @@ hipError_t launch_cost_fast(const CostArgs& a, int P, const float* k1, const flo
         else launch_persist<false>(a, P, t, de, G, nitems, s);
         return hipGetLastError();
     }
-    if (tile_cfg == 1) {
-        if (trim) launch_tile_cfg<8, 8, 4, true, true>(a, P, t, de, s);
-        else launch_tile_cfg<8, 8, 4, false, true>(a, P, t, de, s);
+    if (tile_cfg == 3) {
+        for (int f = 0; f < kNumFilt; ++f)
+            for (int i = 0; i < 2 * kFastHalf + 1; ++i) t.h[f][i] *= kVOutScale;  // exact
+        if (trim) launch_tile_cfg<8, 8, 4, true, 2>(a, P, t, de, s);
+        else launch_tile_cfg<8, 8, 4, false, 2>(a, P, t, de, s);
+    } else if (tile_cfg == 1) {
+        if (trim) launch_tile_cfg<8, 8, 4, true, 1>(a, P, t, de, s);
+        else launch_tile_cfg<8, 8, 4, false, 1>(a, P, t, de, s);
     } else if (tile_cfg == 2) {
-        if (trim) launch_tile_cfg<8, 4, 4, true, false>(a, P, t, de, s);
-        else launch_tile_cfg<8, 4, 4, false, false>(a, P, t, de, s);
+        if (trim) launch_tile_cfg<8, 4, 4, true, 0>(a, P, t, de, s);
+        else launch_tile_cfg<8, 4, 4, false, 0>(a, P, t, de, s);
     } else {
-        if (trim) launch_tile_cfg<kFastTH, kFastRV, 2, true, false>(a, P, t, de, s);
-        else launch_tile_cfg<kFastTH, kFastRV, 2, false, false>(a, P, t, de, s);
+        if (trim) launch_tile_cfg<kFastTH, kFastRV, 2, true, 0>(a, P, t, de, s);
+        else launch_tile_cfg<kFastTH, kFastRV, 2, false, 0>(a, P, t, de, s);
     }
     return hipGetLastError();
 }

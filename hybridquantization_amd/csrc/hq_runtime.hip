@@ -24,9 +24,12 @@ hipError_t launch_build_grid(const GridArgs&, int P, hipStream_t);
 hipError_t launch_assign(const AssignArgs&, int P, int rep, int group, hipStream_t);
 void fast_tile_dims(int W, int own_rows, int tile_cfg, int* tiles_x, int* ntiles);
 void opp2xyz_over_illum(const float inv_illum[3], float m[9]);
+void build_vpass_fragments(const float* k1, const float* k2, const float* k3,
+                           const float* absk3, uint16_t* out);
 hipError_t launch_cost_fast(const CostArgs&, int P, const float* k1, const float* k2,
                             const float* k3, const float* absk3, int de, int persistent,
-                            int tile_cfg, int num_cu, bool trim, hipStream_t);
+                            int tile_cfg, int num_cu, bool trim, int* parts_per_tile,
+                            hipStream_t);
 bool trim_window_ok(const float* k1);
 
 hipError_t launch_cost_generic(const GenArgs&, int de, hipStream_t);
@@ -85,6 +88,7 @@ struct hq_ctx {
     int taps = 0, half = 0;
     std::vector<float> k1, k2, k3, absk3;
     DevBuf d_k1, d_k2, d_k3, d_absk3;
+    DevBuf d_vfrag;  // cost_tile 3: Toeplitz B fragments [7][2][64] x 16 B (21-tap filters)
 
     // image
     bool have_image = false;
@@ -108,7 +112,8 @@ struct hq_ctx {
     int assign_blocks_per_cu = 8;
     int assign_rep = 1;    // palette replication in the assign kernel's LDS
     int assign_group = 1;  // palettes per pixel pass in the assign kernel (1, 2, 4)
-    int tile_cfg = 2;      // cost tile: 0 = 16 rows, 1 = 8 rows + split V pass, 2 = 8 rows
+    int tile_cfg = 2;      // cost tile: 0 = 16 rows, 1 = 8 rows + split V pass, 2 = 8 rows,
+                           // 3 = 8 rows + V pass on the matrix cores
     int trim = 1;          // skip taps < 1e-9 of the peak of the narrow k1 filters
     bool trim_ok = false;  // set by hq_set_filters (default 21-tap filter set)
 
@@ -295,7 +300,7 @@ int ensure_population(hq_ctx* c, int P, int K) {
     fast_tile_dims(g.W, g.r1 - g.r0, c->tile_cfg, &tiles_x, &ntiles);
     const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
     const int64_t gen_blocks = (n_own + 255) / 256;
-    const int64_t nparts = std::max<int64_t>(ntiles, gen_blocks);
+    const int64_t nparts = std::max<int64_t>((int64_t)kCostPartsPerTile * ntiles, gen_blocks);
     const int nblocks = c->num_cu * c->assign_blocks_per_cu;
     HIP_TRY(c, c->d_pal_in.ensure(sizeof(float4) * (size_t)P * K));
     HIP_TRY(c, c->d_pal.ensure(sizeof(float4) * (size_t)P * kMaxK));
@@ -356,6 +361,7 @@ int enqueue_eval(hq_ctx* c, int P, int K) {
         CostArgs ca{};
         ca.idx = c->d_idx.as<uint8_t>();
         ca.opp = c->d_opp.as<float4>();
+        ca.vfrag = c->d_vfrag.as<uint4>();
         ca.labL = c->d_labL.as<float>();
         ca.labA = c->d_labA.as<float>();
         ca.labB = c->d_labB.as<float>();
@@ -365,10 +371,12 @@ int enqueue_eval(hq_ctx* c, int P, int K) {
         ca.tiles_x = tiles_x;
         ca.ntiles = ntiles;
         opp2xyz_over_illum(inv, ca.m_lab);
+        int parts_per_tile = 1;
         HIP_TRY(c, launch_cost_fast(ca, P, c->k1.data(), c->k2.data(), c->k3.data(),
                                     c->absk3.data(), c->de_type, c->cost_variant == 2,
-                                    c->tile_cfg, c->num_cu, c->trim && c->trim_ok, s));
-        nparts = ntiles;
+                                    c->tile_cfg, c->num_cu, c->trim && c->trim_ok,
+                                    &parts_per_tile, s));
+        nparts = parts_per_tile * ntiles;
     } else {
         HIP_TRY(c, c->d_gen_t.ensure(sizeof(float) * 7 * (size_t)g.n_ext));
         const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
@@ -496,7 +504,7 @@ void hq_destroy(hq_ctx* c) {
     for (DevBuf* b : {&c->d_k1, &c->d_k2, &c->d_k3, &c->d_absk3, &c->d_R, &c->d_G, &c->d_B,
                       &c->d_labL, &c->d_labA, &c->d_labB, &c->d_pal_in, &c->d_pal, &c->d_opp,
                       &c->d_dup, &c->d_pflags, &c->d_lvl1, &c->d_lvl2, &c->d_idx,
-                      &c->d_used_mask, &c->d_partial, &c->d_out, &c->d_gen_t})
+                      &c->d_used_mask, &c->d_partial, &c->d_out, &c->d_gen_t, &c->d_vfrag})
         b->release();
     if (c->h_pal) (void)hipHostFree(c->h_pal);
     if (c->h_out) (void)hipHostFree(c->h_out);
@@ -532,6 +540,13 @@ int hq_set_filters(hq_ctx* c, int taps, const float* k1, const float* k2, const 
     HIP_TRY(c, hipMemcpy(c->d_k3.p, k3, sizeof(float) * taps, hipMemcpyHostToDevice));
     HIP_TRY(c, hipMemcpy(c->d_absk3.p, absk3, sizeof(float) * taps, hipMemcpyHostToDevice));
     c->trim_ok = taps == 21 && trim_window_ok(k1);
+    if (taps == 21) {
+        std::vector<uint16_t> frag((size_t)kNumFilt * 2 * 64 * 8);
+        build_vpass_fragments(k1, k2, k3, absk3, frag.data());
+        HIP_TRY(c, c->d_vfrag.ensure(frag.size() * sizeof(uint16_t)));
+        HIP_TRY(c, hipMemcpy(c->d_vfrag.p, frag.data(), frag.size() * sizeof(uint16_t),
+                             hipMemcpyHostToDevice));
+    }
     c->have_image = false;  // halo depends on the filters
     return HQ_OK;
 }
@@ -843,7 +858,7 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
     } else if (!std::strcmp(name, "trim")) {
         c->trim = value != 0;
     } else if (!std::strcmp(name, "cost_tile")) {
-        if (value < 0 || value > 2) return fail(c, HQ_ERR_ARG, "cost_tile in {0,1,2}");
+        if (value < 0 || value > 3) return fail(c, HQ_ERR_ARG, "cost_tile in {0,1,2,3}");
         c->tile_cfg = value;
     } else if (!std::strcmp(name, "assign_group")) {
         if (value != 1 && value != 2 && value != 4) return fail(c, HQ_ERR_ARG, "assign_group in {1,2,4}");

@@ -61,6 +61,39 @@ PATCHES["hsplit"] = [(
 FLAGS = {"noslp": ["-fno-slp-vectorize"], "noslp_hsplit": ["-fno-slp-vectorize"]}
 PATCHES["noslp"] = []
 PATCHES["noslp_hsplit"] = PATCHES["hsplit"]
+# per-phase s_memtime stamps of cost_tile_kernel, summed over waves (hq_debug_phases)
+PHASES_DECL = ("// VMODE: 0 = V items of RV rows on VALU",
+               "__device__ unsigned long long g_phase[256 * 8];\n"
+               "#define HQ_STAMP(k) do { const unsigned long long _t = __builtin_amdgcn_s_memtime(); "
+               "if ((tid & 63) == 0) atomicAdd(&g_phase[(blockIdx.x & 255) * 8 + (k)], _t - _tp); _tp = _t; } while (0)\n"
+               "// VMODE: 0 = V items of RV rows on VALU")
+PATCHES["phases"] = [
+    PHASES_DECL,
+    ("    const int p = w % P_, tile = w / P_, tid = threadIdx.x;\n",
+     "    const int p = w % P_, tile = w / P_, tid = threadIdx.x;\n    unsigned long long _tp = __builtin_amdgcn_s_memtime();\n"),
+    ("    }\n    __syncthreads();\n\n    // ---- vertical pass:",
+     "    }\n    HQ_STAMP(0);\n    __syncthreads();\n    HQ_STAMP(1);\n\n    // ---- vertical pass:"),
+    ("    __syncthreads();\n\n    // ---- horizontal pass + Lab + dE",
+     "    HQ_STAMP(2);\n    __syncthreads();\n    HQ_STAMP(3);\n\n    // ---- horizontal pass + Lab + dE"),
+    ("    sum = wave_sum_to_lane63(sum);\n", "    HQ_STAMP(4);\n    sum = wave_sum_to_lane63(sum);\n"),
+    ("        a.partial[(int64_t)p * a.ntiles + tile] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);\n}\n\n// ----------------------------------------------------------------------------\n// cost_persist",
+     "        a.partial[(int64_t)p * a.ntiles + tile] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);\n    HQ_STAMP(5);\n    if ((tid & 63) == 0) atomicAdd(&g_phase[(blockIdx.x & 255) * 8 + 7], 1ull);\n}\n\n// ----------------------------------------------------------------------------\n// cost_persist"),
+]
+APPEND = {"phases": """
+extern "C" int hq_debug_phases(unsigned long long* out, int reset) {
+    static unsigned long long buf[256 * 8];
+    if (hipMemcpyFromSymbol(buf, HIP_SYMBOL(hq::g_phase), sizeof buf) != hipSuccess) return 1;
+    for (int k = 0; k < 8; ++k) {
+        out[k] = 0;
+        for (int i = 0; i < 256; ++i) out[k] += buf[i * 8 + k];
+    }
+    if (reset) {
+        for (auto& v : buf) v = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(hq::g_phase), buf, sizeof buf) != hipSuccess) return 1;
+    }
+    return 0;
+}
+"""}
 PATCHES["skeleton"] = PATCHES["novfma"] + PATCHES["nohfma"] + PATCHES["nolab"]
 PATCHES["skeleton_bcast"] = PATCHES["skeleton"] + PATCHES["gatherbcast"]
 
@@ -75,6 +108,7 @@ def main():
             if old not in s:
                 sys.exit(f"{name}: patch anchor not found")
             s = s.replace(old, new)
+        s += APPEND.get(name, "")
         path = os.path.join(OUT, f"hq_kernels_{name}.hip")
         open(path, "w").write(s)
         obj = os.path.join(OUT, f"hq_kernels_{name}.o")

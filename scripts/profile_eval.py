@@ -55,6 +55,10 @@ def main():
     costs = np.zeros(args.P)
     flat = pals.reshape(-1)
     lib.hq_eval_population(m.ctx, _lib.fptr(flat), args.P, args.K, 2.0, _lib.dptr(costs), None)
+    phases = getattr(lib, "hq_debug_phases", None) if args.lib else None
+    ph = (C.c_ulonglong * 8)()
+    if phases is not None:
+        phases(ph, 1)
     lib.hq_profile_enable(m.ctx, 1)
     t0 = time.perf_counter()
     for _ in range(args.evals):
@@ -71,6 +75,12 @@ def main():
           f"{el / args.evals * 1e3:.3f} ms/eval-population, "
           f"{W * H * args.P * args.evals / el / 1e6:.1f} Mpx*evals/s  ", " ".join(out),
           "costs", costs.tolist())
+    if phases is not None:
+        phases(ph, 0)
+        n = max(ph[7], 1)
+        names = ["prologue", "barrier1", "vpass", "barrier2", "hpass+lab", "reduce"]
+        print("per-wave cycles:", " ".join(f"{nm}={ph[i] / n:.0f}" for i, nm in enumerate(names)),
+              f"waves={ph[7]}")
     m.close()
 
 
