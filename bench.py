@@ -77,7 +77,7 @@ def cpu_baseline(args):
         c_oracle.eval_palette(rgba, lab, pal, f, w, nthreads=threads)
         evals += 1
         el = time.perf_counter() - t0
-        if el >= args.cpu_seconds or evals >= 64:
+        if el >= args.cpu_seconds or evals >= 4096:
             break
     return {"value": w * h * evals / el / 1e6, "unit": "Mpixel*evals/s", "cores": threads,
             "kind": "port",

@@ -80,6 +80,7 @@ struct CostArgs {
     const float4* opp;      // [P][256]
     const uint4* vfrag;     // cost_tile 3: [7][hi, lo][64 lanes] f16x8 B fragments of the
                             // vertical Toeplitz taps (build_vpass_fragments)
+    const void* taps;       // CostTaps<10> in device memory (build_fast_taps)
     const float* labL;      // planar LabRef, owned rows, pitch lab_pitch
     const float* labA;
     const float* labB;

@@ -457,6 +457,63 @@ __global__ __launch_bounds__(256) void assign_kernel(AssignArgs a, int P) {
     if (tid < 8) a.used_mask[((int64_t)p * a.nblocks + blk) * 8 + tid] = s_used[tid];
 }
 
+// assign_batch: the assign kernel with the memory round trips batched.  Per
+// chunk, each thread issues the RGB loads of all its PPT pixels, then the
+// level-2 entry loads of all of them (they need the RGB), then resolves the PPT
+// pixels from LDS: two round trips per PPT pixels.  (assign_kernel prefetches one
+// pixel ahead, but the next pixel's level-2 lookup waits for its RGB at once,
+// so each pixel there pays an HBM round trip of its own.)
+template <int REP, int PPT>
+__global__ __launch_bounds__(256) void assign_batch_kernel(AssignArgs a, int P) {
+    extern __shared__ __attribute__((aligned(16))) float4 s_pal[];
+    __shared__ uint32_t s_used[8];
+    // 1-D grid of nblocks * P: work item w = blk * P + p, so the P palettes of
+    // one pixel block run side by side on one XCD and share its RGB reads in L2.
+    const int w = xcd_remap(blockIdx.x, a.nblocks * P);
+    const int p = w % P, blk = w / P, tid = threadIdx.x;
+    const float4* pal = a.pal + (int64_t)p * kMaxK;
+    for (int e = tid; e < a.K * REP; e += 256) s_pal[e] = pal[e / REP];
+    if (tid < 8) s_used[tid] = 0;
+    __syncthreads();
+    const bool exh_pal = a.pflags[p] != 0 || a.G2 == 0;
+    const int copy = tid & (REP - 1);
+    const uint8_t* lvl1p = a.lvl1 + (int64_t)p * a.lvl1_pitch;
+    const uint8_t* lvl2p = a.lvl2 + (int64_t)p * a.lvl2_pitch;
+    uint8_t* idx = a.idx + (int64_t)p * a.idx_pitch;
+    const int64_t chunk = 256 * PPT;
+    const int64_t lane_off = (int64_t)(tid >> 6) * 64 * PPT + (tid & 63);
+    for (int64_t q0 = (int64_t)blk * chunk; q0 < a.n_ext; q0 += (int64_t)a.nblocks * chunk) {
+        const int64_t qb = q0 + lane_off;
+        float r[PPT], gv[PPT], b[PPT];
+#pragma unroll
+        for (int j = 0; j < PPT; ++j) {
+            const int64_t q = qb + 64 * j;
+            const bool in = q < a.n_ext;
+            r[j] = in ? a.R[q] : 0.f;
+            gv[j] = in ? a.G[q] : 0.f;
+            b[j] = in ? a.B[q] : 0.f;
+        }
+        uint4 e[PPT];
+        bool li[PPT];
+#pragma unroll
+        for (int j = 0; j < PPT; ++j)
+            li[j] = lvl2_lookup(r[j], gv[j], b[j], lvl2p, a.G2, exh_pal || qb + 64 * j >= a.n_ext, e[j]);
+#pragma unroll
+        for (int j = 0; j < PPT; ++j) {
+            const int64_t q = qb + 64 * j;
+            const int k = argmin_from_entry<REP>(r[j], gv[j], b[j], e[j], li[j], s_pal, copy, lvl1p,
+                                                 a.G2, a.K);
+            if (q < a.n_ext) {
+                idx[q] = (uint8_t)k;
+                const uint32_t bit = 1u << (k & 31);
+                if (!(s_used[k >> 5] & bit)) atomicOr(&s_used[k >> 5], bit);
+            }
+        }
+    }
+    __syncthreads();
+    if (tid < 8) a.used_mask[((int64_t)p * a.nblocks + blk) * 8 + tid] = s_used[tid];
+}
+
 // assign_multi: grid (nblocks, ceil(P/PG)), dynamic LDS = PG*K*REP*16 B.  One
 // pass over the pixels serves PG palettes: each pixel's RGB is read once, its
 // cell index computed once, and the PG level-2 entries loaded together
@@ -545,13 +602,20 @@ struct CostTaps {
     float h[kNumFilt][2 * HALF + 1];
 };
 
+// Taps are read through a constant-address-space pointer (uniform s_load per
+// filter).  The cost kernel launders it once per work item so the loads stay in
+// the item loop: hoisted out of the persistent loop, all 294 taps would be held
+// in registers (and spilled).
+template <int HALF>
+using TapsPtr = const __attribute__((address_space(4))) CostTaps<HALF>*;
+
 // Vertical pass of filters [f0, f1) of one opponent channel: RV outputs per
 // thread from RV + 2*HALF gathered inputs; results to s_v[f][row][col].
 // Taps [TLO, THI] only (the default filter set's narrow k1 filters have |taps|
 // below 1e-9 of their peak outside a short window; see trim_window()).
 template <int HALF, int RV, int TH, int RW, int TLO = 0, int THI = 2 * HALF>
 __device__ __forceinline__ void vpass_filters(const float (&o)[RV + 2 * HALF],
-                                              const CostTaps<HALF>& taps, int f0, int f1,
+                                              TapsPtr<HALF> taps, int f0, int f1,
                                               float* out) {
 #pragma unroll 1
     for (int f = f0; f < f1; ++f) {
@@ -560,7 +624,7 @@ __device__ __forceinline__ void vpass_filters(const float (&o)[RV + 2 * HALF],
         for (int y = 0; y < RV; ++y) acc[y] = 0.f;
 #pragma unroll
         for (int t = TLO; t <= THI; ++t) {
-            const float k = taps.v[f][t];
+            const float k = taps->v[f][t];
 #pragma unroll
             for (int y = 0; y < RV; ++y) acc[y] = fmaf(o[y + t], k, acc[y]);
         }
@@ -573,7 +637,7 @@ __device__ __forceinline__ void vpass_filters(const float (&o)[RV + 2 * HALF],
 // 4 + 2*HALF inputs per filter read as ds_read_b128 from s_v.
 // Accumulates filters [f0, f1) into acc (caller zeroes it); taps [TLO, THI].
 template <int HALF, int TH, int RW, int TLO = 0, int THI = 2 * HALF>
-__device__ __forceinline__ void hpass_filters(const float4* src, const CostTaps<HALF>& taps,
+__device__ __forceinline__ void hpass_filters(const float4* src, TapsPtr<HALF> taps,
                                               int f0, int f1, float (&acc)[4]) {
     constexpr int NQ = (4 + 2 * HALF + 3) / 4;
     static_assert(NQ == 6, "the asm barrier below names six vectors");
@@ -594,7 +658,7 @@ __device__ __forceinline__ void hpass_filters(const float4* src, const CostTaps<
         }
 #pragma unroll
         for (int t = TLO; t <= THI; ++t) {
-            const float k = taps.h[f][t];
+            const float k = taps->h[f][t];
 #pragma unroll
             for (int xo = 0; xo < 4; ++xo) acc[xo] = fmaf(in[xo + t], k, acc[xo]);
         }
@@ -612,7 +676,7 @@ template <int HALF, int RV, int TH, int RW, bool TRIM>
 __device__ __forceinline__ void vpass_all(const float (&o0)[RV + 2 * HALF],
                                           const float (&o1)[RV + 2 * HALF],
                                           const float (&o2)[RV + 2 * HALF],
-                                          const CostTaps<HALF>& taps, float* out) {
+                                          TapsPtr<HALF> taps, float* out) {
     if constexpr (TRIM) {
         vpass_filters<HALF, RV, TH, RW, kTrimLo[0], kTrimHi[0]>(o0, taps, 0, 1, out);
         vpass_filters<HALF, RV, TH, RW>(o0, taps, 1, 3, out);
@@ -628,7 +692,7 @@ __device__ __forceinline__ void vpass_all(const float (&o0)[RV + 2 * HALF],
 }
 
 template <int HALF, int TH, int RW, bool TRIM>
-__device__ __forceinline__ void hpass_all(const float4* src, const CostTaps<HALF>& taps,
+__device__ __forceinline__ void hpass_all(const float4* src, TapsPtr<HALF> taps,
                                           float (&acc0)[4], float (&acc1)[4], float (&acc2)[4]) {
 #pragma unroll
     for (int xo = 0; xo < 4; ++xo) acc0[xo] = acc1[xo] = acc2[xo] = 0.f;
@@ -653,7 +717,7 @@ __device__ __forceinline__ void hpass_all(const float4* src, const CostTaps<HALF
 // 4 for the float4 table) and every gathered row feeds TH outputs instead of RV.
 template <int HALF, int TH, int RW, bool TRIM>
 __device__ __forceinline__ void vpass_split(const uint8_t* s_idx, const float* s_oppA,
-                                            const float2* s_oppB, const CostTaps<HALF>& taps,
+                                            const float2* s_oppB, TapsPtr<HALF> taps,
                                             float* s_v, int tid) {
     constexpr int NIN = TH + 2 * HALF;
     const int c = tid % RW;
@@ -722,12 +786,15 @@ __device__ __forceinline__ uint32_t chan(const uint4& v, int c) {
 
 template <int HALF, int TH, int RW, int IDXP, int SVP>
 __device__ __forceinline__ void vpass_mfma(const uint8_t* s_idx, const uint4* s_opph,
-                                           const uint4 (&bf)[2 * kNumFilt], float* s_v, int tid) {
+                                           const uint4* vfrag, float* s_v, int tid) {
     static_assert(TH + 2 * HALF <= 32 && TH <= 16, "one K = 32 step per output block");
     static_assert(RW % 64 == 0, "whole 16-column blocks, the same number per wave");
     constexpr int BPW = RW / 64;  // column blocks per wave
     const int lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, n = lane & 15;
+    uint4 bf[2 * kNumFilt];  // Toeplitz B fragments (L2-resident), live only in this pass
+#pragma unroll
+    for (int i = 0; i < 2 * kNumFilt; ++i) bf[i] = vfrag[i * 64 + lane];
 #pragma unroll
     for (int bi = 0; bi < BPW; ++bi) {
         const int cb = wave * BPW + bi;
@@ -761,16 +828,151 @@ __device__ __forceinline__ void vpass_mfma(const uint8_t* s_idx, const uint4* s_
     }
 }
 
+// One work item of the cost pass: palette p over output tile `tile`.
+struct TileItem {
+    int p, tile, x0, y0;
+};
+
+template <int TW, int TH>
+__device__ __forceinline__ TileItem tile_item(const CostArgs& a, int w, int P) {
+    TileItem t;
+    t.p = w % P;
+    t.tile = w / P;
+    t.x0 = (t.tile % a.tiles_x) * TW;
+    t.y0 = a.g.r0 + (t.tile / a.tiles_x) * TH;
+    return t;
+}
+
+// The global loads that fill one item's LDS (index rows of its region, its
+// palette's opponent entry), held in registers between issue and commit.
+// Every load is issued before the first wait: vmcnt retires in order, so a
+// load -> wait -> store loop pays one memory round trip per trip (4 for the
+// interior index rows, 14 for the byte gathers of edge tiles).
+template <int HALF, int RW, int TH>
+struct TileFill {
+    static constexpr int TW = RW - 2 * HALF, RH = TH + 2 * HALF, DW = RW / 4;
+    static constexpr int NFD = (RH * DW + 255) / 256, NFB = (RH * RW + 255) / 256;
+    uint32_t lo[NFD], hi[NFD];  // interior tiles: aligned dword pairs of the index rows
+    float4 ov;
+    TileItem t;
+    bool interior;
+
+    // interior index-row dword pair q of this thread: LDS dword e, source offset
+    __device__ __forceinline__ static int row_base(const Geom& g, const TileItem& t, int i) {
+        int gy = reflect_clamp(t.y0 - HALF + i, g.H);
+        gy = min(max(gy, g.e0), g.e1 - 1);
+        // 32-bit offsets from the uniform palette base (the host keeps n_ext < 2^31):
+        // saddr + voffset loads, no 64-bit VGPR addresses
+        return (gy - g.e0) * g.W + (t.x0 - HALF);
+    }
+
+    // Issue the loads; interior tiles only (edge tiles -- the image's first and
+    // last tile columns -- gather bytes with reflection at commit time).
+    __device__ __forceinline__ void issue(const CostArgs& a, const TileItem& ti, int tid) {
+        static_assert(kMaxK == 256, "one opponent-table entry per thread");
+        const Geom& g = a.g;
+        t = ti;
+        const uint8_t* idx = a.idx + (int64_t)t.p * g.idx_pitch;
+        ov = tid < a.K ? a.opp[(int64_t)t.p * kMaxK + tid] : make_float4(0.f, 0.f, 0.f, 0.f);
+        interior = t.x0 - HALF >= 0 && t.x0 + TW + HALF <= g.W;
+        if (interior) {
+#pragma unroll
+            for (int q = 0; q < NFD; ++q) {
+                const int e = tid + 256 * q;
+                lo[q] = hi[q] = 0u;
+                if (e < RH * DW) {
+                    const int base = row_base(g, t, e / DW);
+                    const uint32_t* src =
+                        reinterpret_cast<const uint32_t*>(idx + (base & ~3)) + e % DW;
+                    lo[q] = src[0];
+                    hi[q] = src[1];
+                }
+            }
+        }
+    }
+
+    // index rows into s_idx (row pitch IDXP bytes); the first write waits for the loads
+    template <int IDXP>
+    __device__ __forceinline__ void commit_idx(const CostArgs& a, uint8_t* s_idx, int tid) const {
+        const Geom& g = a.g;
+        if (interior) {
+#pragma unroll
+            for (int q = 0; q < NFD; ++q) {
+                const int e = tid + 256 * q;
+                if (e < RH * DW)
+                    reinterpret_cast<uint32_t*>(s_idx)[(e / DW) * (IDXP / 4) + e % DW] =
+                        __builtin_amdgcn_alignbyte(hi[q], lo[q],
+                                                   (uint32_t)(row_base(g, t, e / DW) & 3));
+            }
+        } else {
+            const uint8_t* idx = a.idx + (int64_t)t.p * g.idx_pitch;
+            uint32_t b[NFB];
+#pragma unroll
+            for (int q = 0; q < NFB; ++q) {  // all loads first: one round trip
+                const int e = tid + 256 * q;
+                b[q] = 0u;
+                if (e < RH * RW) {
+                    const int i = e / RW, j = e % RW;
+                    int gy = reflect_clamp(t.y0 - HALF + i, g.H);
+                    gy = min(max(gy, g.e0), g.e1 - 1);
+                    const int gx = reflect_clamp(t.x0 - HALF + j, g.W);
+                    b[q] = idx[(gy - g.e0) * g.W + gx];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < NFB; ++q) {
+                const int e = tid + 256 * q;
+                if (e < RH * RW) s_idx[(e / RW) * IDXP + e % RW] = (uint8_t)b[q];
+            }
+        }
+    }
+};
+
+// LabRef of a thread's H items (NH = TH * 32 / 256 of them).
+template <int TW, int TH>
+struct TileLab {
+    static constexpr int NH = TH * 32 / 256, NRUN = TW / 4;
+    float4 L[NH], A[NH], B[NH];
+    __device__ __forceinline__ void issue(const CostArgs& a, const TileItem& t, int tid) {
+        const Geom& g = a.g;
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            const int item = tid + 256 * h, y = item >> 5, j = item & 31;
+            const int gy = t.y0 + y, gx0 = t.x0 + 4 * j;
+            L[h] = A[h] = B[h] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (j < NRUN && gy < g.r1 && gx0 < g.W) {
+                const int off = (gy - g.r0) * (int)g.lab_pitch + gx0;
+                L[h] = *reinterpret_cast<const float4*>(a.labL + off);
+                A[h] = *reinterpret_cast<const float4*>(a.labA + off);
+                B[h] = *reinterpret_cast<const float4*>(a.labB + off);
+            }
+        }
+    }
+};
+
+// cost_tile: one workgroup = one TW x TH output tile of one palette per work
+// item; region = (TH + 2*HALF) rows x RW columns of indices.  Vertical pass
+// first on all RW region columns (separable filters commute), then horizontal
+// pass on the TW output columns, Opp->Lab, dE, fp64 partial per item.
 // VMODE: 0 = V items of RV rows on VALU, 1 = V split by channel group (VALU),
 // 2 = V pass on the matrix cores (vpass_mfma).
-template <int HALF, int RW, int TH, int RV, int DE, int OCC, bool TRIM, int VMODE>
-__global__ __launch_bounds__(256, OCC) void cost_tile_kernel(CostArgs a, CostTaps<HALF> taps,
-                                                            int P_) {
+// PERSIST = false: 1-D grid of ntiles * P, one item per workgroup; item
+// w = tile * P + p, XCD-relabelled so the P palettes of a tile run side by side
+// on one XCD and read its LabRef from L2 after the first.
+// PERSIST = true: a grid of OCC workgroups per CU, each walking a contiguous
+// run of items (XCD-relabelled, so an XCD covers one region of the image) as a
+// software pipeline: the next item's index rows and opponent entry are loaded
+// during this item's horizontal pass and written to LDS after it, its LabRef
+// then loaded during the next vertical pass -- the memory round trip that
+// starts every item of the one-shot grid is off the critical path.
+template <int HALF, int RW, int TH, int RV, int DE, int OCC, bool TRIM, int VMODE, bool PERSIST>
+__global__ __launch_bounds__(256, OCC) void cost_tile_kernel(CostArgs a, int P_) {
     constexpr bool VSPLIT = VMODE == 1, VMFMA = VMODE == 2;
     constexpr int TW = RW - 2 * HALF;
     constexpr int RH = TH + 2 * HALF;
     constexpr int NIN = RV + 2 * HALF;
     constexpr int NRUN = TW / 4;
+    constexpr int NH = TH * 32 / 256;
     static_assert(VMFMA || (VSPLIT ? (RV == TH && 2 * RW == 256) : RW * (TH / RV) == 256),
                   "one V item per thread");
     static_assert(TW % 4 == 0, "4-wide H runs");
@@ -793,369 +995,146 @@ __global__ __launch_bounds__(256, OCC) void cost_tile_kernel(CostArgs a, CostTap
     __shared__ __attribute__((aligned(16))) uint8_t s_idx[IDX_ROWS * IDXP];
     __shared__ double s_red[4];
     float* s_v = reinterpret_cast<float*>(s_v4);
-
-    // 1-D grid of ntiles * P: work item w = tile * P + p, so the P palettes of a
-    // tile run side by side on one XCD and read its LabRef from L2 after the first.
-    const int w = xcd_remap(blockIdx.x, a.ntiles * P_);
-    const int p = w % P_, tile = w / P_, tid = threadIdx.x;
+    int tid = threadIdx.x;
     const Geom& g = a.g;
-    const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
-    const int x0 = tx * TW, y0 = g.r0 + ty * TH;
-    const uint8_t* idx = a.idx + (int64_t)p * g.idx_pitch;
 
-    // ---- prologue.  Every global load of the fill is issued before the first
-    // wait: vmcnt retires in order, so a load -> wait -> store loop pays one
-    // memory round trip per trip (4 for the interior index rows, 14 for the
-    // byte gathers of edge tiles) and waits for anything issued before it.
-    // LabRef is loaded after the fill, so it is in flight during the V pass.
-    constexpr int DW = RW / 4;
-    constexpr int NFD = (RH * DW + 255) / 256, NFB = (RH * RW + 255) / 256;
-    static_assert(kMaxK == 256, "one opponent-table entry per thread");
-    const bool interior = x0 - HALF >= 0 && x0 + TW + HALF <= g.W;
-    const float4 ov = tid < a.K ? a.opp[(int64_t)p * kMaxK + tid] : make_float4(0.f, 0.f, 0.f, 0.f);
-    uint4 bf[VMFMA ? 2 * kNumFilt : 1];  // Toeplitz B fragments, L2-resident
-    if constexpr (VMFMA) {
-#pragma unroll
-        for (int i = 0; i < 2 * kNumFilt; ++i) bf[i] = a.vfrag[i * 64 + (tid & 63)];
-    }
-    uint32_t flo[NFD], fhi[NFD], fsh[NFD], fb[NFB];
-    if (interior) {
-        // each region row is RW contiguous bytes: aligned dword pairs + alignbyte
-        // funnel shift (rows reflect vertically only)
-#pragma unroll
-        for (int q = 0; q < NFD; ++q) {
-            const int e = tid + 256 * q;
-            flo[q] = fhi[q] = fsh[q] = 0u;
-            if (e < RH * DW) {
-                const int i = e / DW, k = e % DW;
-                int gy = reflect_clamp(y0 - HALF + i, g.H);
-                gy = min(max(gy, g.e0), g.e1 - 1);
-                const int64_t base = (int64_t)(gy - g.e0) * g.W + (x0 - HALF);
-                const uint32_t* src =
-                    reinterpret_cast<const uint32_t*>(idx + (base & ~(int64_t)3)) + k;
-                flo[q] = src[0];
-                fhi[q] = src[1];
-                fsh[q] = (uint32_t)(base & 3);
-            }
-        }
+    const int N = a.ntiles * P_;
+    int it, it_end;
+    if constexpr (PERSIST) {
+        const int G = gridDim.x, b = xcd_remap(blockIdx.x, G);
+        it = (int)((int64_t)b * N / G);
+        it_end = (int)((int64_t)(b + 1) * N / G);
+        if (it >= it_end) return;  // uniform over the workgroup, before any barrier
     } else {
-#pragma unroll
-        for (int q = 0; q < NFB; ++q) {
-            const int e = tid + 256 * q;
-            fb[q] = 0u;
-            if (e < RH * RW) {
-                const int i = e / RW, j = e % RW;
-                int gy = reflect_clamp(y0 - HALF + i, g.H);
-                gy = min(max(gy, g.e0), g.e1 - 1);
-                const int gx = reflect_clamp(x0 - HALF + j, g.W);
-                fb[q] = idx[(int64_t)(gy - g.e0) * g.W + gx];
+        it = xcd_remap(blockIdx.x, N);
+        it_end = it + 1;
+    }
+
+    auto commit_table = [&](const float4& ov) {
+        if constexpr (VMFMA) {
+            // every entry finite: the padding rows of the K = 32 step gather too
+            s_opph[tid] = tid < a.K ? make_uint4(split_f16(ov.x), split_f16(ov.y), split_f16(ov.z), 0u)
+                                    : make_uint4(0u, 0u, 0u, 0u);
+        } else if constexpr (VSPLIT) {
+            if (tid < a.K) {
+                s_oppA[tid] = ov.x;
+                s_oppB[tid] = make_float2(ov.y, ov.z);
             }
-        }
-    }
-    // LDS writes (the first one waits for all the loads above)
-    if constexpr (VMFMA) {
-        // every entry finite: the padding rows of the K = 32 step gather too
-        s_opph[tid] = tid < a.K ? make_uint4(split_f16(ov.x), split_f16(ov.y), split_f16(ov.z), 0u)
-                                : make_uint4(0u, 0u, 0u, 0u);
-        for (int e = tid; e < (IDX_ROWS - RH) * IDXP / 4; e += 256)
-            reinterpret_cast<uint32_t*>(s_idx + RH * IDXP)[e] = 0u;
-    } else if constexpr (VSPLIT) {
-        if (tid < a.K) {
-            s_oppA[tid] = ov.x;
-            s_oppB[tid] = make_float2(ov.y, ov.z);
-        }
-    } else {
-        if (tid < a.K) s_opp[tid] = ov;
-    }
-    if (interior) {
-#pragma unroll
-        for (int q = 0; q < NFD; ++q) {
-            const int e = tid + 256 * q;
-            if (e < RH * DW)
-                reinterpret_cast<uint32_t*>(s_idx)[(e / DW) * (IDXP / 4) + e % DW] =
-                    __builtin_amdgcn_alignbyte(fhi[q], flo[q], fsh[q]);
-        }
-    } else {
-#pragma unroll
-        for (int q = 0; q < NFB; ++q) {
-            const int e = tid + 256 * q;
-            if (e < RH * RW) s_idx[(e / RW) * IDXP + e % RW] = (uint8_t)fb[q];
-        }
-    }
-
-    // LabRef of this thread's H items
-    constexpr int NH = TH * 32 / 256;
-    float4 labL[NH], labA[NH], labB[NH];
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-        const int item = tid + 256 * h, y = item >> 5, j = item & 31;
-        const int gy = y0 + y, gx0 = x0 + 4 * j;
-        labL[h] = labA[h] = labB[h] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (j < NRUN && gy < g.r1 && gx0 < g.W) {
-            const int64_t off = (int64_t)(gy - g.r0) * g.lab_pitch + gx0;
-            labL[h] = *reinterpret_cast<const float4*>(a.labL + off);
-            labA[h] = *reinterpret_cast<const float4*>(a.labA + off);
-            labB[h] = *reinterpret_cast<const float4*>(a.labB + off);
-        }
-    }
-    __syncthreads();
-
-    // ---- vertical pass: thread = (region column c, rows [RV*gr, RV*gr+RV)) ----
-    // The filter loops are not unrolled so only one filter's 21 taps are live in
-    // SGPRs at a time (all 294 taps at once spill into VGPR lanes).
-    if constexpr (VMFMA) {
-        vpass_mfma<HALF, TH, RW, IDXP, SVP>(s_idx, s_opph, bf, s_v, tid);
-    } else if constexpr (VSPLIT) {
-        vpass_split<HALF, TH, RW, TRIM>(s_idx, s_oppA, s_oppB, taps, s_v, tid);
-    } else {
-        const int c = tid % RW, gr = tid / RW;
-        float o0[NIN], o1[NIN], o2[NIN];
-        float wsum = 0.f;  // .w (= 0) is consumed so the gather stays one ds_read_b128
-#pragma unroll
-        for (int r = 0; r < NIN; ++r) {
-            const float4 v = s_opp[s_idx[(gr * RV + r) * IDXP + c]];
-            o0[r] = v.x; o1[r] = v.y; o2[r] = v.z;
-            wsum += v.w;
-        }
-        o0[0] += wsum;  // wsum == 0 exactly (prep_palette writes .w = 0)
-        float* out = s_v + (gr * RV) * SVP + c;
-        vpass_all<HALF, RV, TH, RW, TRIM>(o0, o1, o2, taps, out);
-    }
-    __syncthreads();
-
-    // ---- horizontal pass + Lab + dE: item = (row y, 4-column run j) ----
-    double sum = 0.0;
-    // 32 run slots per row (NRUN used): a ds_read_b128 16-lane group then
-    // covers 16 distinct bank positions of one row (27 runs per row wrapped
-    // lanes into the next row's bank 0).
-    static_assert(NRUN <= 32, "runs per row");
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-        const int item = tid + 256 * h, y = item >> 5, j = item & 31;
-        if (j >= NRUN) continue;
-        const float4* src = &s_v4[(y * SVP) / 4 + j];
-        float acc0[4], acc1[4], acc2[4];
-        hpass_all<HALF, TH, SVP, TRIM>(src, taps, acc0, acc1, acc2);
-        const int gy = y0 + y, gx0 = x0 + 4 * j;
-        if (gy < g.r1 && gx0 < g.W) {
-            const float4 L4 = labL[h], A4 = labA[h], B4 = labB[h];
-            const float Ls[4] = {L4.x, L4.y, L4.z, L4.w};
-            const float As[4] = {A4.x, A4.y, A4.z, A4.w};
-            const float Bs[4] = {B4.x, B4.y, B4.z, B4.w};
-            float part = 0.f;
-#pragma unroll
-            for (int xo = 0; xo < 4; ++xo) {
-                const float3 lab = opp2lab_fast(acc0[xo], acc1[xo], acc2[xo], a.m_lab);
-                const float e = delta_e<DE>(Ls[xo], As[xo], Bs[xo], lab.x, lab.y, lab.z);
-                part += (gx0 + xo < g.W) ? e : 0.f;
-            }
-            sum += (double)part;
-        }
-    }
-    sum = wave_sum_to_lane63(sum);
-    if ((tid & 63) == 63) s_red[tid >> 6] = sum;
-    __syncthreads();
-    if (tid == 0)
-        a.partial[(int64_t)p * a.ntiles + tile] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
-}
-
-// ----------------------------------------------------------------------------
-// cost_persist: the same tile computation as cost_tile, as a persistent,
-// software-pipelined kernel.  Grid = a multiple of 8 workgroups (2 per CU);
-// workgroup w walks work items it = w', w' + G, ... where w' is an XCD-aware
-// relabelling (consecutive w' share an XCD) and it = tile * P + p, so the P
-// palettes of one tile read its LabRef through one L2.  While item i is
-// computed, item i+1's index rows (interior tiles), opponent table and LabRef
-// are already in flight into registers.
-// ----------------------------------------------------------------------------
-template <int HALF, int RW, int TH>
-struct CostPrefetch {
-    static constexpr int RH = TH + 2 * HALF;
-    static constexpr int DW = RW / 4;
-    static constexpr int NLD = (RH * DW + 255) / 256;
-    uint32_t lo[NLD], hi[NLD], sh[NLD];
-    float4 opp;
-    float4 lab[2][3];
-    bool interior;
-};
-
-template <int HALF, int RW, int TH>
-__device__ __forceinline__ void cost_prefetch(const CostArgs& a, int P, int it, int nitems, int tid,
-                                              CostPrefetch<HALF, RW, TH>& pf) {
-    using PF = CostPrefetch<HALF, RW, TH>;
-    constexpr int TW = RW - 2 * HALF;
-    constexpr int NRUN = TW / 4;
-    if (it >= nitems) return;
-    const Geom& g = a.g;
-    const int tile = it / P, p = it - tile * P;
-    const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
-    const int x0 = tx * TW, y0 = g.r0 + ty * TH;
-    const uint8_t* idx = a.idx + (int64_t)p * g.idx_pitch;
-    pf.interior = x0 - HALF >= 0 && x0 + TW + HALF <= g.W;
-    if (pf.interior) {
-#pragma unroll
-        for (int u = 0; u < PF::NLD; ++u) {
-            const int e = tid + 256 * u;
-            pf.lo[u] = pf.hi[u] = pf.sh[u] = 0;
-            if (e < PF::RH * PF::DW) {
-                const int i = e / PF::DW, k = e % PF::DW;
-                int gy = reflect_clamp(y0 - HALF + i, g.H);
-                gy = min(max(gy, g.e0), g.e1 - 1);
-                const int64_t base = (int64_t)(gy - g.e0) * g.W + (x0 - HALF);
-                const uint32_t* src =
-                    reinterpret_cast<const uint32_t*>(idx + (base & ~(int64_t)3)) + k;
-                pf.lo[u] = src[0];
-                pf.hi[u] = src[1];
-                pf.sh[u] = (uint32_t)(base & 3);
-            }
-        }
-    }
-    pf.opp = tid < a.K ? a.opp[(int64_t)p * kMaxK + tid] : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-        const int item = tid + 256 * r;
-        const int y = item >> 5, j = item & 31;
-        const int gy = y0 + y, gx0 = x0 + 4 * j;
-        if (item < TH * 32 && j < NRUN && gy < g.r1 && gx0 < g.W) {
-            const int64_t off = (int64_t)(gy - g.r0) * g.lab_pitch + gx0;
-            pf.lab[r][0] = *reinterpret_cast<const float4*>(a.labL + off);
-            pf.lab[r][1] = *reinterpret_cast<const float4*>(a.labA + off);
-            pf.lab[r][2] = *reinterpret_cast<const float4*>(a.labB + off);
         } else {
-            pf.lab[r][0] = pf.lab[r][1] = pf.lab[r][2] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (tid < a.K) s_opp[tid] = ov;
         }
+    };
+
+    TileItem cur = tile_item<TW, TH>(a, it, P_);
+    TileFill<HALF, RW, TH> fill;
+    TileLab<TW, TH> lab;
+    fill.issue(a, cur, tid);
+    if constexpr (VMFMA) {
+        for (int e = tid; e < (IDX_ROWS - RH) * IDXP / 4; e += 256)
+            reinterpret_cast<uint32_t*>(s_idx + RH * IDXP)[e] = 0u;  // never rewritten
     }
-}
+    commit_table(fill.ov);
+    fill.template commit_idx<IDXP>(a, s_idx, tid);
+    lab.issue(a, cur, tid);  // in flight during the V pass
 
-template <int HALF, int RW, int TH, int RV, int DE, bool TRIM>
-__global__ __launch_bounds__(256, 2) void cost_persist_kernel(CostArgs a, CostTaps<HALF> taps,
-                                                               int P, int nitems) {
-    using PF = CostPrefetch<HALF, RW, TH>;
-    constexpr int TW = RW - 2 * HALF;
-    constexpr int RH = TH + 2 * HALF;
-    constexpr int NIN = RV + 2 * HALF;
-    constexpr int NRUN = TW / 4;
-    constexpr int OPP_REP = 4;
-    static_assert(RW * (TH / RV) == 256, "one V item per thread");
-    static_assert(TW % 4 == 0 && NRUN <= 32 && TH * 32 <= 512, "H items");
-    __shared__ float4 s_v4[kNumFilt * TH * RW / 4];
-    __shared__ float4 s_opp[kMaxK * OPP_REP];
-    __shared__ __attribute__((aligned(16))) uint8_t s_idx[RH * RW];
-    __shared__ double s_red[2][4];
-    float* s_v = reinterpret_cast<float*>(s_v4);
+    bool have_prev = false;
+    TileItem prev = cur;
+    for (;;) {
+        // Opaque per item: the taps pointer and the thread index.  Everything
+        // derived from them (tap loads, per-thread LDS / global offsets) stays in
+        // the item loop -- hoisted out of the persistent loop it would be held in
+        // registers across it and spilled.
+        TapsPtr<HALF> taps = (TapsPtr<HALF>)(uintptr_t)a.taps;  // flat -> constant: same address
+        asm volatile("" : "+s"(taps));
+        if constexpr (PERSIST) asm volatile("" : "+v"(tid));
+        __syncthreads();  // s_idx / table of `cur` written; s_v free; s_red of `prev` complete
+        if (PERSIST && have_prev && tid == 0)
+            a.partial[(int64_t)prev.p * a.ntiles + prev.tile] =
+                (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
 
-    const int tid = threadIdx.x;
-    const int G = gridDim.x;  // multiple of 8
-    const int lw = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
-    const Geom& g = a.g;
-
-    PF pf;
-    cost_prefetch<HALF, RW, TH>(a, P, lw, nitems, tid, pf);
-    int prev_item = -1, parity = 0;
-    for (int it = lw; it < nitems; it += G) {
-        const int tile = it / P, p = it - tile * P;
-        const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
-        const int x0 = tx * TW, y0 = g.r0 + ty * TH;
-
-        // ---- stage item `it` into LDS (s_idx / s_opp are free: the previous
-        //      V-pass finished at the mid barrier; the H-pass does not read them)
-        if (pf.interior) {
-#pragma unroll
-            for (int u = 0; u < PF::NLD; ++u) {
-                const int e = tid + 256 * u;
-                if (e < RH * PF::DW)
-                    reinterpret_cast<uint32_t*>(s_idx)[e] =
-                        __builtin_amdgcn_alignbyte(pf.hi[u], pf.lo[u], pf.sh[u]);
-            }
-        } else {  // edge tile: reflected byte gathers (no prefetch)
-            const uint8_t* idx = a.idx + (int64_t)p * g.idx_pitch;
-            for (int e = tid; e < RH * RW; e += 256) {
-                const int i = e / RW, j = e % RW;
-                int gy = reflect_clamp(y0 - HALF + i, g.H);
-                gy = min(max(gy, g.e0), g.e1 - 1);
-                const int gx = reflect_clamp(x0 - HALF + j, g.W);
-                s_idx[e] = idx[(int64_t)(gy - g.e0) * g.W + gx];
-            }
-        }
-        if (tid < a.K) {
-#pragma unroll
-            for (int c = 0; c < OPP_REP; ++c) s_opp[tid * OPP_REP + c] = pf.opp;
-        }
-        float4 lab[2][3];
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-#pragma unroll
-            for (int q = 0; q < 3; ++q) lab[r][q] = pf.lab[r][q];
-        __syncthreads();
-        // partial of the previous item (its wave sums are in s_red[parity ^ 1])
-        if (tid == 0 && prev_item >= 0) {
-            const double* r = s_red[parity ^ 1];
-            const int pt = prev_item / P, pp = prev_item - pt * P;
-            a.partial[(int64_t)pp * a.ntiles + pt] = (r[0] + r[1]) + (r[2] + r[3]);
-        }
-        // ---- next item's loads go in flight now
-        cost_prefetch<HALF, RW, TH>(a, P, it + G, nitems, tid, pf);
-
-        // ---- vertical pass
-        {
+        // ---- vertical pass ----
+        // The filter loops are not unrolled so only one filter's 21 taps are live
+        // in SGPRs at a time (all 294 taps at once spill into VGPR lanes).
+        if constexpr (VMFMA) {
+            vpass_mfma<HALF, TH, RW, IDXP, SVP>(s_idx, s_opph, a.vfrag, s_v, tid);
+        } else if constexpr (VSPLIT) {
+            vpass_split<HALF, TH, RW, TRIM>(s_idx, s_oppA, s_oppB, taps, s_v, tid);
+        } else {
+            // thread = (region column c, rows [RV*gr, RV*gr+RV))
             const int c = tid % RW, gr = tid / RW;
-            const int copy = tid & (OPP_REP - 1);
             float o0[NIN], o1[NIN], o2[NIN];
-            float wsum = 0.f;
+            float wsum = 0.f;  // .w (= 0) is consumed so the gather stays one ds_read_b128
 #pragma unroll
             for (int r = 0; r < NIN; ++r) {
-                const float4 v = s_opp[s_idx[(gr * RV + r) * RW + c] * OPP_REP + copy];
+                const float4 v = s_opp[s_idx[(gr * RV + r) * IDXP + c]];
                 o0[r] = v.x; o1[r] = v.y; o2[r] = v.z;
                 wsum += v.w;
             }
-            o0[0] += wsum;  // == 0: keeps the gather one ds_read_b128
-            float* out = s_v + (gr * RV) * RW + c;
+            o0[0] += wsum;  // wsum == 0 exactly (prep_palette writes .w = 0)
+            float* out = s_v + (gr * RV) * SVP + c;
             vpass_all<HALF, RV, TH, RW, TRIM>(o0, o1, o2, taps, out);
         }
-        __syncthreads();
+        const bool more = PERSIST && it + 1 < it_end;
+        TileItem next = cur;
+        if (more) {
+            next = tile_item<TW, TH>(a, it + 1, P_);
+            // scheduling fences keep the issue between the passes: interleaved into
+            // them, its addresses and destinations would be live across their peaks
+            __builtin_amdgcn_sched_barrier(0);
+            fill.issue(a, next, tid);  // in flight during the H pass
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        __syncthreads();  // s_v complete; s_idx / table free
 
-        // ---- horizontal pass + Lab + dE
+        // ---- horizontal pass + Lab + dE: item = (row y, 4-column run j) ----
         double sum = 0.0;
+        // 32 run slots per row (NRUN used): a ds_read_b128 16-lane group then
+        // covers 16 distinct bank positions of one row (27 runs per row wrapped
+        // lanes into the next row's bank 0).
+        static_assert(NRUN <= 32, "runs per row");
 #pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            const int item = tid + 256 * r;
-            const int y = item >> 5, j = item & 31;
-            if (item >= TH * 32 || j >= NRUN) continue;
-            const float4* src = &s_v4[(y * RW) / 4 + j];
+        for (int h = 0; h < NH; ++h) {
+            const int item = tid + 256 * h, y = item >> 5, j = item & 31;
+            if (j >= NRUN) continue;
+            const float4* src = &s_v4[(y * SVP) / 4 + j];
             float acc0[4], acc1[4], acc2[4];
-            hpass_all<HALF, TH, RW, TRIM>(src, taps, acc0, acc1, acc2);
-            const int gy = y0 + y, gx0 = x0 + 4 * j;
+            hpass_all<HALF, TH, SVP, TRIM>(src, taps, acc0, acc1, acc2);
+            const int gy = cur.y0 + y, gx0 = cur.x0 + 4 * j;
             if (gy < g.r1 && gx0 < g.W) {
-                const float Ls[4] = {lab[r][0].x, lab[r][0].y, lab[r][0].z, lab[r][0].w};
-                const float As[4] = {lab[r][1].x, lab[r][1].y, lab[r][1].z, lab[r][1].w};
-                const float Bs[4] = {lab[r][2].x, lab[r][2].y, lab[r][2].z, lab[r][2].w};
+                const float4 L4 = lab.L[h], A4 = lab.A[h], B4 = lab.B[h];
+                const float Ls[4] = {L4.x, L4.y, L4.z, L4.w};
+                const float As[4] = {A4.x, A4.y, A4.z, A4.w};
+                const float Bs[4] = {B4.x, B4.y, B4.z, B4.w};
                 float part = 0.f;
 #pragma unroll
                 for (int xo = 0; xo < 4; ++xo) {
-                    const float3 l = opp2lab_fast(acc0[xo], acc1[xo], acc2[xo], a.m_lab);
-                    const float e = delta_e<DE>(Ls[xo], As[xo], Bs[xo], l.x, l.y, l.z);
+                    const float3 l3 = opp2lab_fast(acc0[xo], acc1[xo], acc2[xo], a.m_lab);
+                    const float e = delta_e<DE>(Ls[xo], As[xo], Bs[xo], l3.x, l3.y, l3.z);
                     part += (gx0 + xo < g.W) ? e : 0.f;
                 }
                 sum += (double)part;
             }
         }
-        sum = wave_sum(sum);
-        if ((tid & 63) == 0) s_red[parity][tid >> 6] = sum;
-        prev_item = it;
-        parity ^= 1;
+        sum = wave_sum_to_lane63(sum);
+        if ((tid & 63) == 63) s_red[tid >> 6] = sum;
+        if (!more) break;
+        // next item: LDS fill (s_idx / table free since the barrier above), then
+        // its LabRef and fragments, in flight across the barrier and V pass
+        __builtin_amdgcn_sched_barrier(0);
+        commit_table(fill.ov);
+        fill.template commit_idx<IDXP>(a, s_idx, tid);
+        lab.issue(a, next, tid);
+        __builtin_amdgcn_sched_barrier(0);
+        prev = cur;
+        have_prev = true;
+        cur = next;
+        ++it;
     }
     __syncthreads();
-    if (tid == 0 && prev_item >= 0) {
-        const double* r = s_red[parity ^ 1];
-        const int pt = prev_item / P, pp = prev_item - pt * P;
-        a.partial[(int64_t)pp * a.ntiles + pt] = (r[0] + r[1]) + (r[2] + r[3]);
-    }
+    if (tid == 0)
+        a.partial[(int64_t)cur.p * a.ntiles + cur.tile] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
 }
 
-// ----------------------------------------------------------------------------
-// Generic two-pass path (any half-width): the reference's Temp/End structure
-// (CL:234-306) with the horizontal results in HBM.  Used when the filters are
-// not the default 21 taps, and as an independent cross-check of cost_tile.
 // ----------------------------------------------------------------------------
 
 
@@ -1459,9 +1438,20 @@ static hipError_t launch_assign_multi(const AssignArgs& a, int P, hipStream_t s)
     return hipGetLastError();
 }
 
+template <int PPT>
+static hipError_t launch_assign_batch(const AssignArgs& a, int P, hipStream_t s) {
+    const size_t lds = (size_t)a.K * sizeof(float4);
+    hipLaunchKernelGGL((assign_batch_kernel<1, PPT>), dim3(a.nblocks * P), dim3(256), lds, s, a, P);
+    return hipGetLastError();
+}
+
 // rep: LDS replication of the palette (1, 4 or 16); lane l reads copy l % rep.
 // group > 1: one pixel pass serves `group` palettes (assign_multi_kernel).
-hipError_t launch_assign(const AssignArgs& a, int P, int rep, int group, hipStream_t s) {
+// batch: 4 or 8 = assign_batch_kernel with that many pixels per round trip
+// (single palette copy), 0 = assign_kernel.
+hipError_t launch_assign(const AssignArgs& a, int P, int rep, int group, int batch, hipStream_t s) {
+    if (batch == 4) return launch_assign_batch<4>(a, P, s);
+    if (batch == 8) return launch_assign_batch<8>(a, P, s);
     if (group == 4) {
         if (rep == 1) return launch_assign_multi<1, 4>(a, P, s);
         if (rep == 2) return launch_assign_multi<2, 4>(a, P, s);
@@ -1551,26 +1541,27 @@ void fast_tile_dims(int W, int own_rows, int tile_cfg, int* tiles_x, int* ntiles
     *ntiles = *tiles_x * ((own_rows + th - 1) / th);
 }
 
+// Persistent grids run POCC workgroups per CU: the pipeline's extra live state
+// (next item's loads, loop-carried coordinates) does not fit the one-shot
+// kernel's 128-VGPR budget at OCC = 4.
 template <int TH, int RV, int OCC, bool TRIM, int VMODE>
-static void launch_tile_cfg(const CostArgs& a, int P, const CostTaps<10>& t, int de,
+static void launch_tile_cfg(const CostArgs& a, int P, int de, bool persistent, int num_cu,
                             hipStream_t s) {
-    if (de == 0)
-        hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, 0, OCC, TRIM, VMODE>),
-                           dim3(a.ntiles * P), dim3(256), 0, s, a, t, P);
-    else
-        hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, 1, OCC, TRIM, VMODE>),
-                           dim3(a.ntiles * P), dim3(256), 0, s, a, t, P);
-}
-
-template <bool TRIM>
-static void launch_persist(const CostArgs& a, int P, const CostTaps<10>& t, int de, int G,
-                           int nitems, hipStream_t s) {
-    if (de == 0)
-        hipLaunchKernelGGL((cost_persist_kernel<kFastHalf, kFastRW, kFastTH, kFastRV, 0, TRIM>),
-                           dim3(G), dim3(256), 0, s, a, t, P, nitems);
-    else
-        hipLaunchKernelGGL((cost_persist_kernel<kFastHalf, kFastRW, kFastTH, kFastRV, 1, TRIM>),
-                           dim3(G), dim3(256), 0, s, a, t, P, nitems);
+    constexpr int POCC = OCC > 3 ? 3 : OCC;
+    const int N = a.ntiles * P;
+    const unsigned grid = persistent ? (unsigned)std::min(POCC * num_cu, N) : (unsigned)N;
+#define HQ_TILE_LAUNCH(DEV, PERS)                                                              \
+    hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, DEV, PERS ? POCC : OCC, TRIM, \
+                                         VMODE, PERS>),                                        \
+                       dim3(grid), dim3(256), 0, s, a, P)
+    if (de == 0) {
+        if (persistent) HQ_TILE_LAUNCH(0, true);
+        else HQ_TILE_LAUNCH(0, false);
+    } else {
+        if (persistent) HQ_TILE_LAUNCH(1, true);
+        else HQ_TILE_LAUNCH(1, false);
+    }
+#undef HQ_TILE_LAUNCH
 }
 
 // True when every tap of the narrow filters outside the trim window is below
@@ -1587,35 +1578,39 @@ bool trim_window_ok(const float* k1) {
     return true;
 }
 
-hipError_t launch_cost_fast(const CostArgs& a, int P, const float* k1, const float* k2,
-                            const float* k3, const float* absk3, int de, int persistent,
-                            int tile_cfg, int num_cu, bool trim, int* parts_per_tile,
-                            hipStream_t s) {
-    CostTaps<10> t;
-    make_taps10(k1, k2, k3, absk3, t);
+size_t fast_taps_bytes() { return 2 * sizeof(CostTaps<10>); }
+
+// [0] the taps as designed, [1] the same with the horizontal taps scaled by
+// 2^-30 (exact) for the matrix-core vertical pass, whose outputs carry 2^30.
+void build_fast_taps(const float* k1, const float* k2, const float* k3, const float* absk3,
+                     void* out) {
+    CostTaps<10> t[2];
+    make_taps10(k1, k2, k3, absk3, t[0]);
+    t[1] = t[0];
+    for (int f = 0; f < kNumFilt; ++f)
+        for (int i = 0; i < 2 * kFastHalf + 1; ++i) t[1].h[f][i] *= kVOutScale;
+    std::memcpy(out, t, sizeof t);
+}
+
+// a.taps = the two CostTaps<10> of build_fast_taps
+hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, int persistent, int tile_cfg,
+                            int num_cu, bool trim, int* parts_per_tile, hipStream_t s) {
+    CostArgs a = a0;
+    if (tile_cfg == 3) a.taps = static_cast<const char*>(a0.taps) + sizeof(CostTaps<10>);
     *parts_per_tile = 1;
-    if (persistent && tile_cfg == 0) {  // the persistent kernel exists for 16-row tiles
-        const int nitems = a.ntiles * P;
-        int G = std::min(2 * num_cu, nitems);
-        G = std::max(8, (G + 7) / 8 * 8);  // the XCD relabelling needs a multiple of 8
-        if (trim) launch_persist<true>(a, P, t, de, G, nitems, s);
-        else launch_persist<false>(a, P, t, de, G, nitems, s);
-        return hipGetLastError();
-    }
+    const bool ps = persistent != 0;
     if (tile_cfg == 3) {
-        for (int f = 0; f < kNumFilt; ++f)
-            for (int i = 0; i < 2 * kFastHalf + 1; ++i) t.h[f][i] *= kVOutScale;  // exact
-        if (trim) launch_tile_cfg<8, 8, 4, true, 2>(a, P, t, de, s);
-        else launch_tile_cfg<8, 8, 4, false, 2>(a, P, t, de, s);
+        if (trim) launch_tile_cfg<8, 8, 4, true, 2>(a, P, de, ps, num_cu, s);
+        else launch_tile_cfg<8, 8, 4, false, 2>(a, P, de, ps, num_cu, s);
     } else if (tile_cfg == 1) {
-        if (trim) launch_tile_cfg<8, 8, 4, true, 1>(a, P, t, de, s);
-        else launch_tile_cfg<8, 8, 4, false, 1>(a, P, t, de, s);
+        if (trim) launch_tile_cfg<8, 8, 4, true, 1>(a, P, de, ps, num_cu, s);
+        else launch_tile_cfg<8, 8, 4, false, 1>(a, P, de, ps, num_cu, s);
     } else if (tile_cfg == 2) {
-        if (trim) launch_tile_cfg<8, 4, 4, true, 0>(a, P, t, de, s);
-        else launch_tile_cfg<8, 4, 4, false, 0>(a, P, t, de, s);
+        if (trim) launch_tile_cfg<8, 4, 4, true, 0>(a, P, de, ps, num_cu, s);
+        else launch_tile_cfg<8, 4, 4, false, 0>(a, P, de, ps, num_cu, s);
     } else {
-        if (trim) launch_tile_cfg<kFastTH, kFastRV, 2, true, 0>(a, P, t, de, s);
-        else launch_tile_cfg<kFastTH, kFastRV, 2, false, 0>(a, P, t, de, s);
+        if (trim) launch_tile_cfg<kFastTH, kFastRV, 2, true, 0>(a, P, de, ps, num_cu, s);
+        else launch_tile_cfg<kFastTH, kFastRV, 2, false, 0>(a, P, de, ps, num_cu, s);
     }
     return hipGetLastError();
 }

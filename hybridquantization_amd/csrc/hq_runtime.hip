@@ -21,15 +21,16 @@ namespace hq {
 // launchers from hq_kernels.hip
 hipError_t launch_prep_palette(const PaletteArgs&, int P, hipStream_t);
 hipError_t launch_build_grid(const GridArgs&, int P, hipStream_t);
-hipError_t launch_assign(const AssignArgs&, int P, int rep, int group, hipStream_t);
+hipError_t launch_assign(const AssignArgs&, int P, int rep, int group, int batch, hipStream_t);
 void fast_tile_dims(int W, int own_rows, int tile_cfg, int* tiles_x, int* ntiles);
 void opp2xyz_over_illum(const float inv_illum[3], float m[9]);
 void build_vpass_fragments(const float* k1, const float* k2, const float* k3,
                            const float* absk3, uint16_t* out);
-hipError_t launch_cost_fast(const CostArgs&, int P, const float* k1, const float* k2,
-                            const float* k3, const float* absk3, int de, int persistent,
-                            int tile_cfg, int num_cu, bool trim, int* parts_per_tile,
-                            hipStream_t);
+hipError_t launch_cost_fast(const CostArgs&, int P, int de, int persistent, int tile_cfg,
+                            int num_cu, bool trim, int* parts_per_tile, hipStream_t);
+size_t fast_taps_bytes();
+void build_fast_taps(const float* k1, const float* k2, const float* k3, const float* absk3,
+                     void* out);
 bool trim_window_ok(const float* k1);
 
 hipError_t launch_cost_generic(const GenArgs&, int de, hipStream_t);
@@ -89,6 +90,7 @@ struct hq_ctx {
     std::vector<float> k1, k2, k3, absk3;
     DevBuf d_k1, d_k2, d_k3, d_absk3;
     DevBuf d_vfrag;  // cost_tile 3: Toeplitz B fragments [7][2][64] x 16 B (21-tap filters)
+    DevBuf d_taps;   // fast path taps, build_fast_taps (21-tap filters)
 
     // image
     bool have_image = false;
@@ -112,6 +114,7 @@ struct hq_ctx {
     int assign_blocks_per_cu = 8;
     int assign_rep = 1;    // palette replication in the assign kernel's LDS
     int assign_group = 1;  // palettes per pixel pass in the assign kernel (1, 2, 4)
+    int assign_batch = 4;  // pixels per memory round trip (assign_batch_kernel: 4, 8; 0 = off)
     int tile_cfg = 2;      // cost tile: 0 = 16 rows, 1 = 8 rows + split V pass, 2 = 8 rows,
                            // 3 = 8 rows + V pass on the matrix cores
     int trim = 1;          // skip taps < 1e-9 of the peak of the narrow k1 filters
@@ -286,6 +289,10 @@ int check_geom_args(hq_ctx* c, int w, int h, int r0, int r1) {
     if (w < c->half || h < c->half || w < 1 || h < 1)
         return fail(c, HQ_ERR_ARG, "image %dx%d smaller than the stencil half-width %d", w, h, c->half);
     if (r0 < 0 || r1 > h || r0 >= r1) return fail(c, HQ_ERR_ARG, "bad row range [%d,%d)", r0, r1);
+    // the cost kernels address a shard's index image and LabRef with 32-bit offsets
+    if ((int64_t)(w + 4) * (int64_t)(r1 - r0 + 2 * c->half) >= (int64_t)INT32_MAX)
+        return fail(c, HQ_ERR_UNSUPPORTED, "shard of %d x %d pixels exceeds 2^31; use more row blocks",
+                    w, r1 - r0);
     return HQ_OK;
 }
 
@@ -350,7 +357,7 @@ int enqueue_eval(hq_ctx* c, int P, int K) {
                   c->d_pflags.as<int>(), c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(),
                   c->d_idx.as<uint8_t>(), c->d_used_mask.as<uint32_t>(), g.n_ext, g.idx_pitch,
                   l1p, l2p, K, c->G2, nblocks};
-    HIP_TRY(c, launch_assign(aa, P, c->assign_rep, c->assign_group, s));
+    HIP_TRY(c, launch_assign(aa, P, c->assign_rep, c->assign_group, c->assign_batch, s));
     if (c->prof) HIP_TRY(c, hipEventRecord(c->ev[2], s));
     int tiles_x, ntiles;
     fast_tile_dims(g.W, g.r1 - g.r0, c->tile_cfg, &tiles_x, &ntiles);
@@ -372,10 +379,9 @@ int enqueue_eval(hq_ctx* c, int P, int K) {
         ca.ntiles = ntiles;
         opp2xyz_over_illum(inv, ca.m_lab);
         int parts_per_tile = 1;
-        HIP_TRY(c, launch_cost_fast(ca, P, c->k1.data(), c->k2.data(), c->k3.data(),
-                                    c->absk3.data(), c->de_type, c->cost_variant == 2,
-                                    c->tile_cfg, c->num_cu, c->trim && c->trim_ok,
-                                    &parts_per_tile, s));
+        ca.taps = c->d_taps.p;
+        HIP_TRY(c, launch_cost_fast(ca, P, c->de_type, c->cost_variant == 2, c->tile_cfg,
+                                    c->num_cu, c->trim && c->trim_ok, &parts_per_tile, s));
         nparts = parts_per_tile * ntiles;
     } else {
         HIP_TRY(c, c->d_gen_t.ensure(sizeof(float) * 7 * (size_t)g.n_ext));
@@ -504,7 +510,8 @@ void hq_destroy(hq_ctx* c) {
     for (DevBuf* b : {&c->d_k1, &c->d_k2, &c->d_k3, &c->d_absk3, &c->d_R, &c->d_G, &c->d_B,
                       &c->d_labL, &c->d_labA, &c->d_labB, &c->d_pal_in, &c->d_pal, &c->d_opp,
                       &c->d_dup, &c->d_pflags, &c->d_lvl1, &c->d_lvl2, &c->d_idx,
-                      &c->d_used_mask, &c->d_partial, &c->d_out, &c->d_gen_t, &c->d_vfrag})
+                      &c->d_used_mask, &c->d_partial, &c->d_out, &c->d_gen_t, &c->d_vfrag,
+                      &c->d_taps})
         b->release();
     if (c->h_pal) (void)hipHostFree(c->h_pal);
     if (c->h_out) (void)hipHostFree(c->h_out);
@@ -546,6 +553,10 @@ int hq_set_filters(hq_ctx* c, int taps, const float* k1, const float* k2, const 
         HIP_TRY(c, c->d_vfrag.ensure(frag.size() * sizeof(uint16_t)));
         HIP_TRY(c, hipMemcpy(c->d_vfrag.p, frag.data(), frag.size() * sizeof(uint16_t),
                              hipMemcpyHostToDevice));
+        std::vector<char> tb(fast_taps_bytes());
+        build_fast_taps(k1, k2, k3, absk3, tb.data());
+        HIP_TRY(c, c->d_taps.ensure(tb.size()));
+        HIP_TRY(c, hipMemcpy(c->d_taps.p, tb.data(), tb.size(), hipMemcpyHostToDevice));
     }
     c->have_image = false;  // halo depends on the filters
     return HQ_OK;
@@ -863,6 +874,9 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
     } else if (!std::strcmp(name, "assign_group")) {
         if (value != 1 && value != 2 && value != 4) return fail(c, HQ_ERR_ARG, "assign_group in {1,2,4}");
         c->assign_group = value;
+    } else if (!std::strcmp(name, "assign_batch")) {
+        if (value != 0 && value != 4 && value != 8) return fail(c, HQ_ERR_ARG, "assign_batch in {0,4,8}");
+        c->assign_batch = value;
     } else if (!std::strcmp(name, "assign_rep")) {
         if (value != 1 && value != 2 && value != 4 && value != 16)
             return fail(c, HQ_ERR_ARG, "assign_rep in {1,2,4,16}");

@@ -181,7 +181,8 @@ int hq_profile_reset(hq_ctx *ctx);
 /* Tuning knobs (testing / benchmarking; defaults are the measured best):
  *   "grid"         argmin pruning resolution G2: 0 = exhaustive, 16, 32 (default), 64
  *   "cost_variant" 0 = one tile per workgroup (default), 1 = generic two-pass
- *                  path (any filter length), 2 = persistent pipelined tiles
+ *                  path (any filter length), 2 = persistent workgroups walking a run of
+ *                  tiles, the next tile's loads in flight during this one (slower here)
  *   "cost_tile"    0 = 16-row tiles (2 WG/CU); 1 = 8-row tiles with the vertical pass
  *                  split by opponent-channel group (4 WG/CU); 2 = 8-row tiles, 4-row
  *                  vertical items (4 WG/CU, default)
@@ -189,6 +190,8 @@ int hq_profile_reset(hq_ctx *ctx);
  *                  (default; only when the filters allow it), 0 = all taps
  *   "assign_rep"   palette replication in the assign kernel's LDS: 1 (default), 2, 4, 16
  *   "assign_group" palettes evaluated per pixel pass in the assign kernel: 1 (default), 2, 4
+ *   "assign_batch" pixels per memory round trip in the assign kernel: 4 (default), 8;
+ *                  0 = one-pixel-ahead prefetch (then "assign_rep" / "assign_group" apply)
  *   "assign_blocks_per_cu" workgroups per CU of the assign grid (default 8) */
 int hq_set_option(hq_ctx *ctx, const char *name, int value);
 

@@ -125,10 +125,12 @@ def test_eval_config2_1024_k64(ip, filt):
 # argmin edge cases (CL:179-193), bit-exact
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("grid", [64, 32, 16, 0])
-def test_assign_edge_cases(ip, grid):
+@pytest.mark.parametrize("batch", [0, 4, 8])
+def test_assign_edge_cases(ip, grid, batch):
     g = np.load(os.path.join(GOLD, "edge_assign.npz"))
     px = g["px"]  # 4096 pixels -> 64 x 64 image, values partly outside [0, 1]
     ip.setOption("grid", grid)
+    ip.setOption("assign_batch", batch)
     ip.setImage(px.reshape(-1), np.zeros_like(px).reshape(-1), 64, ip.illum)
     for name in ("dup", "clamped", "k1", "k256", "ties"):
         pal = g[f"pal_{name}"]
@@ -150,10 +152,13 @@ def test_assign_random_and_near_ties(ip, K):
         pal[K - 1, :3] = px[5, :3]
     ip.setImage(px.reshape(-1), np.zeros_like(px).reshape(-1), w, ip.illum)
     ref_idx, ref_used = c_oracle.assign(px, pal)
-    for grid, group, rep in ((64, 1, 4), (32, 4, 4), (32, 2, 4), (32, 4, 1), (16, 4, 2), (0, 1, 16)):
+    for grid, group, rep, batch in ((64, 1, 4, 0), (32, 4, 4, 0), (32, 2, 4, 0), (32, 4, 1, 0),
+                                    (16, 4, 2, 0), (0, 1, 16, 0), (32, 1, 1, 4), (32, 1, 1, 8),
+                                    (64, 1, 1, 8), (0, 1, 1, 4)):
         ip.setOption("grid", grid)
         ip.setOption("assign_group", group)
         ip.setOption("assign_rep", rep)
+        ip.setOption("assign_batch", batch)
         pals = [pal.reshape(-1), pal[::-1].copy().reshape(-1), pal.reshape(-1)]
         _, used = ip.computeQuantizationErrorPopulation(pals, 2.0, return_used=True)
         np.testing.assert_array_equal(ip.getIndices(0), ref_idx.astype(np.uint8))
