@@ -10,7 +10,6 @@ namespace hq {
 constexpr int kMaxK = 256;        // u8 palette indices (K <= 256 on this path)
 constexpr int kMaxTaps = 255;     // generic path limit (2*half+1)
 constexpr int kNumFilt = 7;       // separable filter pairs of the S-CIELAB stencil
-constexpr int kCostPartsPerTile = 1;  // fp64 partials per cost tile (sizing; launch_cost_fast)
 constexpr int kL1Cap = 31;        // level-1 candidate list capacity (32-B entry)
 constexpr int kL2Cap = 15;        // level-2 candidate list capacity (16-B entry)
 constexpr uint8_t kOverflow = 255;

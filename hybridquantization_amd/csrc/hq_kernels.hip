@@ -602,10 +602,8 @@ struct CostTaps {
     float h[kNumFilt][2 * HALF + 1];
 };
 
-// Taps are read through a constant-address-space pointer (uniform s_load per
-// filter).  The cost kernel launders it once per work item so the loads stay in
-// the item loop: hoisted out of the persistent loop, all 294 taps would be held
-// in registers (and spilled).
+// Taps are read through a constant-address-space pointer into device memory
+// (uniform s_load per filter; build_fast_taps holds both scalings).
 template <int HALF>
 using TapsPtr = const __attribute__((address_space(4))) CostTaps<HALF>*;
 
@@ -950,22 +948,18 @@ struct TileLab {
     }
 };
 
-// cost_tile: one workgroup = one TW x TH output tile of one palette per work
-// item; region = (TH + 2*HALF) rows x RW columns of indices.  Vertical pass
-// first on all RW region columns (separable filters commute), then horizontal
-// pass on the TW output columns, Opp->Lab, dE, fp64 partial per item.
+// cost_tile: one workgroup = one TW x TH output tile of one palette; region =
+// (TH + 2*HALF) rows x RW columns of indices.  Vertical pass first on all RW
+// region columns (separable filters commute), then horizontal pass on the TW
+// output columns, Opp->Lab, dE, one fp64 partial per (tile, palette).
 // VMODE: 0 = V items of RV rows on VALU, 1 = V split by channel group (VALU),
 // 2 = V pass on the matrix cores (vpass_mfma).
-// PERSIST = false: 1-D grid of ntiles * P, one item per workgroup; item
-// w = tile * P + p, XCD-relabelled so the P palettes of a tile run side by side
-// on one XCD and read its LabRef from L2 after the first.
-// PERSIST = true: a grid of OCC workgroups per CU, each walking a contiguous
-// run of items (XCD-relabelled, so an XCD covers one region of the image) as a
-// software pipeline: the next item's index rows and opponent entry are loaded
-// during this item's horizontal pass and written to LDS after it, its LabRef
-// then loaded during the next vertical pass -- the memory round trip that
-// starts every item of the one-shot grid is off the critical path.
-template <int HALF, int RW, int TH, int RV, int DE, int OCC, bool TRIM, int VMODE, bool PERSIST>
+// 1-D grid of ntiles * P: work item w = tile * P + p, XCD-relabelled so the P
+// palettes of a tile run side by side on one XCD and read its LabRef from L2
+// after the first.  (Persistent variants -- a workgroup walking a run of tiles
+// with the next tile's loads in flight in registers, or DMA'd into a second LDS
+// buffer -- measured 20-40% slower than this grid with 4 workgroups per CU.)
+template <int HALF, int RW, int TH, int RV, int DE, int OCC, bool TRIM, int VMODE>
 __global__ __launch_bounds__(256, OCC) void cost_tile_kernel(CostArgs a, int P_) {
     constexpr bool VSPLIT = VMODE == 1, VMFMA = VMODE == 2;
     constexpr int TW = RW - 2 * HALF;
@@ -995,141 +989,88 @@ __global__ __launch_bounds__(256, OCC) void cost_tile_kernel(CostArgs a, int P_)
     __shared__ __attribute__((aligned(16))) uint8_t s_idx[IDX_ROWS * IDXP];
     __shared__ double s_red[4];
     float* s_v = reinterpret_cast<float*>(s_v4);
-    int tid = threadIdx.x;
+    const int tid = threadIdx.x;
     const Geom& g = a.g;
+    const TileItem cur = tile_item<TW, TH>(a, xcd_remap(blockIdx.x, a.ntiles * P_), P_);
+    const TapsPtr<HALF> taps = (TapsPtr<HALF>)(uintptr_t)a.taps;  // flat -> constant: same address
 
-    const int N = a.ntiles * P_;
-    int it, it_end;
-    if constexpr (PERSIST) {
-        const int G = gridDim.x, b = xcd_remap(blockIdx.x, G);
-        it = (int)((int64_t)b * N / G);
-        it_end = (int)((int64_t)(b + 1) * N / G);
-        if (it >= it_end) return;  // uniform over the workgroup, before any barrier
-    } else {
-        it = xcd_remap(blockIdx.x, N);
-        it_end = it + 1;
-    }
-
-    auto commit_table = [&](const float4& ov) {
-        if constexpr (VMFMA) {
-            // every entry finite: the padding rows of the K = 32 step gather too
-            s_opph[tid] = tid < a.K ? make_uint4(split_f16(ov.x), split_f16(ov.y), split_f16(ov.z), 0u)
-                                    : make_uint4(0u, 0u, 0u, 0u);
-        } else if constexpr (VSPLIT) {
-            if (tid < a.K) {
-                s_oppA[tid] = ov.x;
-                s_oppB[tid] = make_float2(ov.y, ov.z);
-            }
-        } else {
-            if (tid < a.K) s_opp[tid] = ov;
-        }
-    };
-
-    TileItem cur = tile_item<TW, TH>(a, it, P_);
+    // ---- prologue: every fill load issued before the first wait (TileFill),
+    // LabRef after the LDS writes, in flight during the V pass
     TileFill<HALF, RW, TH> fill;
-    TileLab<TW, TH> lab;
     fill.issue(a, cur, tid);
     if constexpr (VMFMA) {
+        // every entry finite: the padding rows of the K = 32 step gather too
+        s_opph[tid] = tid < a.K ? make_uint4(split_f16(fill.ov.x), split_f16(fill.ov.y),
+                                             split_f16(fill.ov.z), 0u)
+                                : make_uint4(0u, 0u, 0u, 0u);
         for (int e = tid; e < (IDX_ROWS - RH) * IDXP / 4; e += 256)
-            reinterpret_cast<uint32_t*>(s_idx + RH * IDXP)[e] = 0u;  // never rewritten
+            reinterpret_cast<uint32_t*>(s_idx + RH * IDXP)[e] = 0u;
+    } else if constexpr (VSPLIT) {
+        if (tid < a.K) {
+            s_oppA[tid] = fill.ov.x;
+            s_oppB[tid] = make_float2(fill.ov.y, fill.ov.z);
+        }
+    } else {
+        if (tid < a.K) s_opp[tid] = fill.ov;
     }
-    commit_table(fill.ov);
     fill.template commit_idx<IDXP>(a, s_idx, tid);
-    lab.issue(a, cur, tid);  // in flight during the V pass
+    TileLab<TW, TH> lab;
+    lab.issue(a, cur, tid);
+    __syncthreads();
 
-    bool have_prev = false;
-    TileItem prev = cur;
-    for (;;) {
-        // Opaque per item: the taps pointer and the thread index.  Everything
-        // derived from them (tap loads, per-thread LDS / global offsets) stays in
-        // the item loop -- hoisted out of the persistent loop it would be held in
-        // registers across it and spilled.
-        TapsPtr<HALF> taps = (TapsPtr<HALF>)(uintptr_t)a.taps;  // flat -> constant: same address
-        asm volatile("" : "+s"(taps));
-        if constexpr (PERSIST) asm volatile("" : "+v"(tid));
-        __syncthreads();  // s_idx / table of `cur` written; s_v free; s_red of `prev` complete
-        if (PERSIST && have_prev && tid == 0)
-            a.partial[(int64_t)prev.p * a.ntiles + prev.tile] =
-                (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
-
-        // ---- vertical pass ----
-        // The filter loops are not unrolled so only one filter's 21 taps are live
-        // in SGPRs at a time (all 294 taps at once spill into VGPR lanes).
-        if constexpr (VMFMA) {
-            vpass_mfma<HALF, TH, RW, IDXP, SVP>(s_idx, s_opph, a.vfrag, s_v, tid);
-        } else if constexpr (VSPLIT) {
-            vpass_split<HALF, TH, RW, TRIM>(s_idx, s_oppA, s_oppB, taps, s_v, tid);
-        } else {
-            // thread = (region column c, rows [RV*gr, RV*gr+RV))
-            const int c = tid % RW, gr = tid / RW;
-            float o0[NIN], o1[NIN], o2[NIN];
-            float wsum = 0.f;  // .w (= 0) is consumed so the gather stays one ds_read_b128
+    // ---- vertical pass ----
+    // The filter loops are not unrolled so only one filter's 21 taps are live in
+    // SGPRs at a time (all 294 taps at once spill into VGPR lanes).
+    if constexpr (VMFMA) {
+        vpass_mfma<HALF, TH, RW, IDXP, SVP>(s_idx, s_opph, a.vfrag, s_v, tid);
+    } else if constexpr (VSPLIT) {
+        vpass_split<HALF, TH, RW, TRIM>(s_idx, s_oppA, s_oppB, taps, s_v, tid);
+    } else {
+        // thread = (region column c, rows [RV*gr, RV*gr+RV))
+        const int c = tid % RW, gr = tid / RW;
+        float o0[NIN], o1[NIN], o2[NIN];
+        float wsum = 0.f;  // .w (= 0) is consumed so the gather stays one ds_read_b128
 #pragma unroll
-            for (int r = 0; r < NIN; ++r) {
-                const float4 v = s_opp[s_idx[(gr * RV + r) * IDXP + c]];
-                o0[r] = v.x; o1[r] = v.y; o2[r] = v.z;
-                wsum += v.w;
-            }
-            o0[0] += wsum;  // wsum == 0 exactly (prep_palette writes .w = 0)
-            float* out = s_v + (gr * RV) * SVP + c;
-            vpass_all<HALF, RV, TH, RW, TRIM>(o0, o1, o2, taps, out);
+        for (int r = 0; r < NIN; ++r) {
+            const float4 v = s_opp[s_idx[(gr * RV + r) * IDXP + c]];
+            o0[r] = v.x; o1[r] = v.y; o2[r] = v.z;
+            wsum += v.w;
         }
-        const bool more = PERSIST && it + 1 < it_end;
-        TileItem next = cur;
-        if (more) {
-            next = tile_item<TW, TH>(a, it + 1, P_);
-            // scheduling fences keep the issue between the passes: interleaved into
-            // them, its addresses and destinations would be live across their peaks
-            __builtin_amdgcn_sched_barrier(0);
-            fill.issue(a, next, tid);  // in flight during the H pass
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        __syncthreads();  // s_v complete; s_idx / table free
-
-        // ---- horizontal pass + Lab + dE: item = (row y, 4-column run j) ----
-        double sum = 0.0;
-        // 32 run slots per row (NRUN used): a ds_read_b128 16-lane group then
-        // covers 16 distinct bank positions of one row (27 runs per row wrapped
-        // lanes into the next row's bank 0).
-        static_assert(NRUN <= 32, "runs per row");
-#pragma unroll
-        for (int h = 0; h < NH; ++h) {
-            const int item = tid + 256 * h, y = item >> 5, j = item & 31;
-            if (j >= NRUN) continue;
-            const float4* src = &s_v4[(y * SVP) / 4 + j];
-            float acc0[4], acc1[4], acc2[4];
-            hpass_all<HALF, TH, SVP, TRIM>(src, taps, acc0, acc1, acc2);
-            const int gy = cur.y0 + y, gx0 = cur.x0 + 4 * j;
-            if (gy < g.r1 && gx0 < g.W) {
-                const float4 L4 = lab.L[h], A4 = lab.A[h], B4 = lab.B[h];
-                const float Ls[4] = {L4.x, L4.y, L4.z, L4.w};
-                const float As[4] = {A4.x, A4.y, A4.z, A4.w};
-                const float Bs[4] = {B4.x, B4.y, B4.z, B4.w};
-                float part = 0.f;
-#pragma unroll
-                for (int xo = 0; xo < 4; ++xo) {
-                    const float3 l3 = opp2lab_fast(acc0[xo], acc1[xo], acc2[xo], a.m_lab);
-                    const float e = delta_e<DE>(Ls[xo], As[xo], Bs[xo], l3.x, l3.y, l3.z);
-                    part += (gx0 + xo < g.W) ? e : 0.f;
-                }
-                sum += (double)part;
-            }
-        }
-        sum = wave_sum_to_lane63(sum);
-        if ((tid & 63) == 63) s_red[tid >> 6] = sum;
-        if (!more) break;
-        // next item: LDS fill (s_idx / table free since the barrier above), then
-        // its LabRef and fragments, in flight across the barrier and V pass
-        __builtin_amdgcn_sched_barrier(0);
-        commit_table(fill.ov);
-        fill.template commit_idx<IDXP>(a, s_idx, tid);
-        lab.issue(a, next, tid);
-        __builtin_amdgcn_sched_barrier(0);
-        prev = cur;
-        have_prev = true;
-        cur = next;
-        ++it;
+        o0[0] += wsum;  // wsum == 0 exactly (prep_palette writes .w = 0)
+        vpass_all<HALF, RV, TH, RW, TRIM>(o0, o1, o2, taps, s_v + (gr * RV) * SVP + c);
     }
+    __syncthreads();
+
+    // ---- horizontal pass + Lab + dE: item = (row y, 4-column run j) ----
+    double sum = 0.0;
+    // 32 run slots per row (NRUN used): a ds_read_b128 16-lane group then
+    // covers 16 distinct bank positions of one row (27 runs per row wrapped
+    // lanes into the next row's bank 0).
+    static_assert(NRUN <= 32, "runs per row");
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        const int item = tid + 256 * h, y = item >> 5, j = item & 31;
+        if (j >= NRUN) continue;
+        float acc0[4], acc1[4], acc2[4];
+        hpass_all<HALF, TH, SVP, TRIM>(&s_v4[(y * SVP) / 4 + j], taps, acc0, acc1, acc2);
+        const int gy = cur.y0 + y, gx0 = cur.x0 + 4 * j;
+        if (gy < g.r1 && gx0 < g.W) {
+            const float4 L4 = lab.L[h], A4 = lab.A[h], B4 = lab.B[h];
+            const float Ls[4] = {L4.x, L4.y, L4.z, L4.w};
+            const float As[4] = {A4.x, A4.y, A4.z, A4.w};
+            const float Bs[4] = {B4.x, B4.y, B4.z, B4.w};
+            float part = 0.f;
+#pragma unroll
+            for (int xo = 0; xo < 4; ++xo) {
+                const float3 l3 = opp2lab_fast(acc0[xo], acc1[xo], acc2[xo], a.m_lab);
+                const float e = delta_e<DE>(Ls[xo], As[xo], Bs[xo], l3.x, l3.y, l3.z);
+                part += (gx0 + xo < g.W) ? e : 0.f;
+            }
+            sum += (double)part;
+        }
+    }
+    sum = wave_sum_to_lane63(sum);
+    if ((tid & 63) == 63) s_red[tid >> 6] = sum;
     __syncthreads();
     if (tid == 0)
         a.partial[(int64_t)cur.p * a.ntiles + cur.tile] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
@@ -1541,27 +1482,15 @@ void fast_tile_dims(int W, int own_rows, int tile_cfg, int* tiles_x, int* ntiles
     *ntiles = *tiles_x * ((own_rows + th - 1) / th);
 }
 
-// Persistent grids run POCC workgroups per CU: the pipeline's extra live state
-// (next item's loads, loop-carried coordinates) does not fit the one-shot
-// kernel's 128-VGPR budget at OCC = 4.
 template <int TH, int RV, int OCC, bool TRIM, int VMODE>
-static void launch_tile_cfg(const CostArgs& a, int P, int de, bool persistent, int num_cu,
-                            hipStream_t s) {
-    constexpr int POCC = OCC > 3 ? 3 : OCC;
-    const int N = a.ntiles * P;
-    const unsigned grid = persistent ? (unsigned)std::min(POCC * num_cu, N) : (unsigned)N;
-#define HQ_TILE_LAUNCH(DEV, PERS)                                                              \
-    hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, DEV, PERS ? POCC : OCC, TRIM, \
-                                         VMODE, PERS>),                                        \
-                       dim3(grid), dim3(256), 0, s, a, P)
-    if (de == 0) {
-        if (persistent) HQ_TILE_LAUNCH(0, true);
-        else HQ_TILE_LAUNCH(0, false);
-    } else {
-        if (persistent) HQ_TILE_LAUNCH(1, true);
-        else HQ_TILE_LAUNCH(1, false);
-    }
-#undef HQ_TILE_LAUNCH
+static void launch_tile_cfg(const CostArgs& a, int P, int de, hipStream_t s) {
+    const dim3 grid((unsigned)(a.ntiles * P));
+    if (de == 0)
+        hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, 0, OCC, TRIM, VMODE>), grid,
+                           dim3(256), 0, s, a, P);
+    else
+        hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, 1, OCC, TRIM, VMODE>), grid,
+                           dim3(256), 0, s, a, P);
 }
 
 // True when every tap of the narrow filters outside the trim window is below
@@ -1593,24 +1522,22 @@ void build_fast_taps(const float* k1, const float* k2, const float* k3, const fl
 }
 
 // a.taps = the two CostTaps<10> of build_fast_taps
-hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, int persistent, int tile_cfg,
-                            int num_cu, bool trim, int* parts_per_tile, hipStream_t s) {
+hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, int tile_cfg, bool trim,
+                            hipStream_t s) {
     CostArgs a = a0;
     if (tile_cfg == 3) a.taps = static_cast<const char*>(a0.taps) + sizeof(CostTaps<10>);
-    *parts_per_tile = 1;
-    const bool ps = persistent != 0;
     if (tile_cfg == 3) {
-        if (trim) launch_tile_cfg<8, 8, 4, true, 2>(a, P, de, ps, num_cu, s);
-        else launch_tile_cfg<8, 8, 4, false, 2>(a, P, de, ps, num_cu, s);
+        if (trim) launch_tile_cfg<8, 8, 4, true, 2>(a, P, de, s);
+        else launch_tile_cfg<8, 8, 4, false, 2>(a, P, de, s);
     } else if (tile_cfg == 1) {
-        if (trim) launch_tile_cfg<8, 8, 4, true, 1>(a, P, de, ps, num_cu, s);
-        else launch_tile_cfg<8, 8, 4, false, 1>(a, P, de, ps, num_cu, s);
+        if (trim) launch_tile_cfg<8, 8, 4, true, 1>(a, P, de, s);
+        else launch_tile_cfg<8, 8, 4, false, 1>(a, P, de, s);
     } else if (tile_cfg == 2) {
-        if (trim) launch_tile_cfg<8, 4, 4, true, 0>(a, P, de, ps, num_cu, s);
-        else launch_tile_cfg<8, 4, 4, false, 0>(a, P, de, ps, num_cu, s);
+        if (trim) launch_tile_cfg<8, 4, 4, true, 0>(a, P, de, s);
+        else launch_tile_cfg<8, 4, 4, false, 0>(a, P, de, s);
     } else {
-        if (trim) launch_tile_cfg<kFastTH, kFastRV, 2, true, 0>(a, P, de, ps, num_cu, s);
-        else launch_tile_cfg<kFastTH, kFastRV, 2, false, 0>(a, P, de, ps, num_cu, s);
+        if (trim) launch_tile_cfg<kFastTH, kFastRV, 2, true, 0>(a, P, de, s);
+        else launch_tile_cfg<kFastTH, kFastRV, 2, false, 0>(a, P, de, s);
     }
     return hipGetLastError();
 }

@@ -26,8 +26,7 @@ void fast_tile_dims(int W, int own_rows, int tile_cfg, int* tiles_x, int* ntiles
 void opp2xyz_over_illum(const float inv_illum[3], float m[9]);
 void build_vpass_fragments(const float* k1, const float* k2, const float* k3,
                            const float* absk3, uint16_t* out);
-hipError_t launch_cost_fast(const CostArgs&, int P, int de, int persistent, int tile_cfg,
-                            int num_cu, bool trim, int* parts_per_tile, hipStream_t);
+hipError_t launch_cost_fast(const CostArgs&, int P, int de, int tile_cfg, bool trim, hipStream_t);
 size_t fast_taps_bytes();
 void build_fast_taps(const float* k1, const float* k2, const float* k3, const float* absk3,
                      void* out);
@@ -110,7 +109,7 @@ struct hq_ctx {
 
     // options
     int G2 = 32;           // argmin grid resolution (0 = exhaustive)
-    int cost_variant = 0;  // 0 tiled (default), 1 generic two-pass, 2 persistent tiled
+    int cost_variant = 0;  // 0 tiled (default), 1 generic two-pass
     int assign_blocks_per_cu = 8;
     int assign_rep = 1;    // palette replication in the assign kernel's LDS
     int assign_group = 1;  // palettes per pixel pass in the assign kernel (1, 2, 4)
@@ -307,7 +306,7 @@ int ensure_population(hq_ctx* c, int P, int K) {
     fast_tile_dims(g.W, g.r1 - g.r0, c->tile_cfg, &tiles_x, &ntiles);
     const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
     const int64_t gen_blocks = (n_own + 255) / 256;
-    const int64_t nparts = std::max<int64_t>((int64_t)kCostPartsPerTile * ntiles, gen_blocks);
+    const int64_t nparts = std::max<int64_t>(ntiles, gen_blocks);
     const int nblocks = c->num_cu * c->assign_blocks_per_cu;
     HIP_TRY(c, c->d_pal_in.ensure(sizeof(float4) * (size_t)P * K));
     HIP_TRY(c, c->d_pal.ensure(sizeof(float4) * (size_t)P * kMaxK));
@@ -378,11 +377,9 @@ int enqueue_eval(hq_ctx* c, int P, int K) {
         ca.tiles_x = tiles_x;
         ca.ntiles = ntiles;
         opp2xyz_over_illum(inv, ca.m_lab);
-        int parts_per_tile = 1;
         ca.taps = c->d_taps.p;
-        HIP_TRY(c, launch_cost_fast(ca, P, c->de_type, c->cost_variant == 2, c->tile_cfg,
-                                    c->num_cu, c->trim && c->trim_ok, &parts_per_tile, s));
-        nparts = parts_per_tile * ntiles;
+        HIP_TRY(c, launch_cost_fast(ca, P, c->de_type, c->tile_cfg, c->trim && c->trim_ok, s));
+        nparts = ntiles;
     } else {
         HIP_TRY(c, c->d_gen_t.ensure(sizeof(float) * 7 * (size_t)g.n_ext));
         const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
@@ -864,7 +861,7 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
             return fail(c, HQ_ERR_ARG, "grid must be 0, 16, 32 or 64");
         c->G2 = value;
     } else if (!std::strcmp(name, "cost_variant")) {
-        if (value < 0 || value > 2) return fail(c, HQ_ERR_ARG, "cost_variant must be 0, 1 or 2");
+        if (value < 0 || value > 1) return fail(c, HQ_ERR_ARG, "cost_variant must be 0 or 1");
         c->cost_variant = value;
     } else if (!std::strcmp(name, "trim")) {
         c->trim = value != 0;

@@ -181,8 +181,7 @@ int hq_profile_reset(hq_ctx *ctx);
 /* Tuning knobs (testing / benchmarking; defaults are the measured best):
  *   "grid"         argmin pruning resolution G2: 0 = exhaustive, 16, 32 (default), 64
  *   "cost_variant" 0 = one tile per workgroup (default), 1 = generic two-pass
- *                  path (any filter length), 2 = persistent workgroups walking a run of
- *                  tiles, the next tile's loads in flight during this one (slower here)
+ *                  path (any filter length)
  *   "cost_tile"    0 = 16-row tiles (2 WG/CU); 1 = 8-row tiles with the vertical pass
  *                  split by opponent-channel group (4 WG/CU); 2 = 8-row tiles, 4-row
  *                  vertical items (4 WG/CU, default)

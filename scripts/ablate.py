@@ -104,6 +104,12 @@ def main():
     names = sys.argv[1:] or list(PATCHES)
     for name in names:
         s = src
+        if name.startswith("git:"):  # git:<rev> = that revision's kernels (A/B baseline)
+            rev = name[4:]
+            s = subprocess.check_output(["git", "-C", ROOT, "show",
+                                         f"{rev}:hybridquantization_amd/csrc/hq_kernels.hip"]).decode()
+            name = "rev_" + rev
+            PATCHES[name] = []
         for old, new in PATCHES[name]:
             if old not in s:
                 sys.exit(f"{name}: patch anchor not found")
