@@ -50,10 +50,11 @@ struct GridArgs {
     const uint8_t* dup;
     const int* pflags;
     uint8_t* lvl1;          // [P][G1^3][32]
-    uint8_t* lvl2;          // [P][G2^3][16]
+    uint8_t* lvl2;          // [ceil(P/4)][G2^3][4][16]: 4 palettes' entries per 64-B line
     int K;
     int G1;                 // level-1 resolution (G2 / 4)
-    int64_t lvl1_pitch, lvl2_pitch;  // bytes per palette
+    int64_t lvl1_pitch;     // bytes per palette
+    int64_t lvl2_gstride;   // bytes per group of 4 palettes (G2^3 * 64)
 };
 
 struct AssignArgs {
@@ -68,7 +69,8 @@ struct AssignArgs {
     uint32_t* used_mask;    // [P][nblocks][8]
     int64_t n_ext;
     int64_t idx_pitch;
-    int64_t lvl1_pitch, lvl2_pitch;
+    int64_t lvl1_pitch;     // bytes per palette
+    int64_t lvl2_gstride;   // bytes per group of 4 palettes (G2^3 * 64)
     int K;
     int G2;                 // 0 = exhaustive
     int nblocks;            // blocks per palette

@@ -230,6 +230,14 @@ __device__ __forceinline__ double ax_max2(double c, double lo, double hi) {
 
 #define HQ_CAND_MARGIN (1.0 + 1e-5)
 
+// Level-2 entries are interleaved by groups of 4 palettes: the 4 entries of one
+// cell share a 64-byte line, so a pixel evaluated under the 4 palettes of a
+// group fetches one line instead of 4 (random 16-B lookups are bound by the
+// line fetches they cause, not by their bytes).
+__host__ __device__ __forceinline__ int64_t lvl2_offset(int64_t gstride, int p, int64_t cell) {
+    return (int64_t)(p >> 2) * gstride + cell * 64 + (p & 3) * 16;
+}
+
 __global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
     const int p = blockIdx.y, cell = blockIdx.x, tid = threadIdx.x;
     const int G1 = a.G1, G2 = 4 * G1;
@@ -314,8 +322,7 @@ __global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
         }
         if (exh || n > kL2Cap) { w0 = kOverflow; w1 = w2 = w3 = 0; }
         else w0 |= (uint32_t)n;
-        uint8_t* l2e = a.lvl2 + (int64_t)p * a.lvl2_pitch +
-                       ((int64_t)(ci2 * G2 + cj2) * G2 + ck2) * 16;
+        uint8_t* l2e = a.lvl2 + lvl2_offset(a.lvl2_gstride, p, (int64_t)(ci2 * G2 + cj2) * G2 + ck2);
         *reinterpret_cast<uint4*>(l2e) = make_uint4(w0, w1, w2, w3);
     }
 }
@@ -327,15 +334,15 @@ __global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
 // ----------------------------------------------------------------------------
 // Level-2 entry lookup: returns false (exhaustive) for pixels outside [0,1]^3
 // or NaN, and for palettes flagged non-finite.
-__device__ __forceinline__ bool lvl2_lookup(float r, float g, float b, const uint8_t* lvl2p,
-                                            int G2, bool exh_pal, uint4& e) {
+__device__ __forceinline__ bool lvl2_lookup(float r, float g, float b, const uint8_t* lvl2,
+                                            int64_t gstride, int p, int G2, bool exh_pal, uint4& e) {
     const bool inside = r >= 0.f && r <= 1.f && g >= 0.f && g <= 1.f && b >= 0.f && b <= 1.f;
     e = make_uint4(0, 0, 0, 0);
     if (exh_pal || !inside) return false;
     const int ir = min((int)(r * (float)G2), G2 - 1);
     const int ig = min((int)(g * (float)G2), G2 - 1);
     const int ib = min((int)(b * (float)G2), G2 - 1);
-    e = *reinterpret_cast<const uint4*>(lvl2p + ((int64_t)(ir * G2 + ig) * G2 + ib) * 16);
+    e = *reinterpret_cast<const uint4*>(lvl2 + lvl2_offset(gstride, p, (int64_t)(ir * G2 + ig) * G2 + ib));
     return true;
 }
 
@@ -359,8 +366,9 @@ __device__ __noinline__ int argmin_exact_slow(float r, float g, float b, uint4 L
 // Exact argmin (CL:179-193 semantics) over the pixel's candidate list.
 // Candidates are ranked by d2; the reference ranks by sqrtf(d2), which can map
 // two different d2 onto one distance, and then keeps the lower index.  Equal
-// sqrtf values imply |d2a - d2b| < 2^-22 * d2, so lanes that ever compare two
-// d2 within 1e-6 relative are re-resolved with the reference loop (rare).
+// sqrtf values imply |d2a - d2b| < 2^-22 * d2, so lanes whose runner-up d2 lies
+// within 1e-6 relative of the best are re-resolved with the reference loop
+// (rare).
 template <int REP>
 __device__ __forceinline__ int argmin_from_entry(float r, float g, float b, uint4 L0, bool listed,
                                                  const float4* s_pal, int copy,
@@ -383,21 +391,37 @@ __device__ __forceinline__ int argmin_from_entry(float r, float g, float b, uint
     int bi = (L0.x >> 8) & 0xff;  // first candidate (lowest index)
     bool near = false;
     if (__any(cnt > 1)) {
-        float best2 = dist2(r, g, b, s_pal[bi * REP + copy]);
         const uint32_t words[8] = {L0.x, L0.y, L0.z, L0.w, L1.x, L1.y, L1.z, L1.w};
+        auto cand = [&](int i) { return (int)((words[(i + 1) >> 2] >> (8 * ((i + 1) & 3))) & 0xff); };
+        float best2 = dist2(r, g, b, s_pal[bi * REP + copy]);
+        // smallest d2 among the other candidates: a tie under sqrtf needs one
+        // within 2^-22 of the final best2 (one test at the end instead of one per
+        // candidate)
+        float second2 = INFINITY;
+        // the next candidate's colour is read while this one is evaluated (the
+        // loop is unrolled, so the hand-over is register renaming, not a copy);
+        // slots past a lane's list hold 0 (build_grid), a valid colour
+        int kn = cand(1);
+        float4 cn = s_pal[kn * REP + copy];
 #pragma unroll
         for (int i = 1; i < kL1Cap; ++i) {
             if (!__any(i < cnt)) break;
-            const int k = (words[(i + 1) >> 2] >> (8 * ((i + 1) & 3))) & 0xff;
-            const float4 c = s_pal[k * REP + copy];
+            const int k = kn;
+            const float4 c = cn;
+            if (i + 1 < kL1Cap) {
+                kn = cand(i + 1);
+                cn = s_pal[kn * REP + copy];
+            }
             asm volatile("" ::"v"(c.w));  // keep .w: one ds_read_b128 (16-lane groups), not b96
             const float d2 = dist2(r, g, b, c);
             const bool act = i < cnt;
-            near |= act && fabsf(d2 - best2) <= best2 * 1e-6f;
             const bool lt = act && d2 < best2;
+            const float other = lt ? best2 : d2;  // the one of the two that is not the best
+            second2 = act && other < second2 ? other : second2;
             best2 = lt ? d2 : best2;
             bi = lt ? k : bi;
         }
+        near = second2 <= best2 * (1.0f + 1e-6f);
     }
     if (__any(exh || near)) {
         if (exh || near) bi = argmin_exact_slow<REP>(r, g, b, L0, L1, cnt, exh, s_pal, copy, K);
@@ -425,7 +449,6 @@ __global__ __launch_bounds__(256) void assign_kernel(AssignArgs a, int P) {
     const bool exh_pal = a.pflags[p] != 0 || a.G2 == 0;
     const int copy = tid & (REP - 1);
     const uint8_t* lvl1p = a.lvl1 + (int64_t)p * a.lvl1_pitch;
-    const uint8_t* lvl2p = a.lvl2 + (int64_t)p * a.lvl2_pitch;
     uint8_t* idx = a.idx + (int64_t)p * a.idx_pitch;
     const int64_t chunk = 256 * PPT;
     const int64_t lane_off = (int64_t)(tid >> 6) * 64 * PPT + (tid & 63);
@@ -434,7 +457,7 @@ __global__ __launch_bounds__(256) void assign_kernel(AssignArgs a, int P) {
         bool in = q < a.n_ext;
         float r = in ? a.R[q] : 0.f, gv = in ? a.G[q] : 0.f, b = in ? a.B[q] : 0.f;
         uint4 e;
-        bool li = lvl2_lookup(r, gv, b, lvl2p, a.G2, exh_pal, e);
+        bool li = lvl2_lookup(r, gv, b, a.lvl2, a.lvl2_gstride, p, a.G2, exh_pal, e);
 #pragma unroll 1
         for (int j = 0; j < PPT; ++j) {
             // prefetch pixel j+1
@@ -443,7 +466,7 @@ __global__ __launch_bounds__(256) void assign_kernel(AssignArgs a, int P) {
             const float rn = inn ? a.R[qn] : 0.f, gn = inn ? a.G[qn] : 0.f,
                         bn = inn ? a.B[qn] : 0.f;
             uint4 en;
-            const bool lin = lvl2_lookup(rn, gn, bn, lvl2p, a.G2, exh_pal || !inn, en);
+            const bool lin = lvl2_lookup(rn, gn, bn, a.lvl2, a.lvl2_gstride, p, a.G2, exh_pal || !inn, en);
             const int k = argmin_from_entry<REP>(r, gv, b, e, li, s_pal, copy, lvl1p, a.G2, a.K);
             if (in) {
                 idx[q] = (uint8_t)k;
@@ -478,7 +501,6 @@ __global__ __launch_bounds__(256) void assign_batch_kernel(AssignArgs a, int P) 
     const bool exh_pal = a.pflags[p] != 0 || a.G2 == 0;
     const int copy = tid & (REP - 1);
     const uint8_t* lvl1p = a.lvl1 + (int64_t)p * a.lvl1_pitch;
-    const uint8_t* lvl2p = a.lvl2 + (int64_t)p * a.lvl2_pitch;
     uint8_t* idx = a.idx + (int64_t)p * a.idx_pitch;
     const int64_t chunk = 256 * PPT;
     const int64_t lane_off = (int64_t)(tid >> 6) * 64 * PPT + (tid & 63);
@@ -497,7 +519,8 @@ __global__ __launch_bounds__(256) void assign_batch_kernel(AssignArgs a, int P) 
         bool li[PPT];
 #pragma unroll
         for (int j = 0; j < PPT; ++j)
-            li[j] = lvl2_lookup(r[j], gv[j], b[j], lvl2p, a.G2, exh_pal || qb + 64 * j >= a.n_ext, e[j]);
+            li[j] = lvl2_lookup(r[j], gv[j], b[j], a.lvl2, a.lvl2_gstride, p, a.G2,
+                                exh_pal || qb + 64 * j >= a.n_ext, e[j]);
 #pragma unroll
         for (int j = 0; j < PPT; ++j) {
             const int64_t q = qb + 64 * j;
@@ -512,6 +535,185 @@ __global__ __launch_bounds__(256) void assign_batch_kernel(AssignArgs a, int P) 
     }
     __syncthreads();
     if (tid < 8) a.used_mask[((int64_t)p * a.nblocks + blk) * 8 + tid] = s_used[tid];
+}
+
+// assign_quad: the batched assign for a group of up to 4 palettes.  One pixel
+// pass serves the group: the pixel's RGB is read once, its cell index computed
+// once, and the group's 4 level-2 entries -- one 64-byte line of the
+// interleaved table -- arrive in one line fetch.  (Per palette, the random
+// 16-B lookups of assign_batch_kernel each pull a line from L2, and those
+// fetches, not the candidate loop, bound it: a fixed-cell ablation ran 40%
+// faster, a loop-free one 4%.)  Grid: nblocks * ceil(P/4), XCD-relabelled;
+// dynamic LDS = 4 * K * 16 B.
+template <int PPT>
+__global__ __launch_bounds__(256) void assign_quad_kernel(AssignArgs a, int P) {
+    extern __shared__ __attribute__((aligned(16))) float4 s_pal[];  // [4][K]
+    __shared__ uint32_t s_used[4][8];
+    const int ngroups = (P + 3) / 4;
+    const int w = xcd_remap(blockIdx.x, a.nblocks * ngroups);
+    const int grp = w % ngroups, blk = w / ngroups, tid = threadIdx.x;
+    const int p0 = 4 * grp, ng = min(4, P - p0);
+    for (int e = tid; e < ng * a.K; e += 256) {
+        const int pp = e / a.K, k = e - pp * a.K;
+        s_pal[e] = a.pal[(int64_t)(p0 + pp) * kMaxK + k];
+    }
+    if (tid < 32) s_used[tid >> 3][tid & 7] = 0;
+    __syncthreads();
+    bool exh_pal[4];
+#pragma unroll
+    for (int pp = 0; pp < 4; ++pp) exh_pal[pp] = pp >= ng || a.pflags[p0 + min(pp, ng - 1)] != 0 || a.G2 == 0;
+    const uint8_t* lines = a.lvl2 + (int64_t)grp * a.lvl2_gstride;
+    const int G2 = a.G2 > 0 ? a.G2 : 4;
+    const int64_t chunk = 256 * PPT;
+    const int64_t lane_off = (int64_t)(tid >> 6) * 64 * PPT + (tid & 63);
+    for (int64_t q0 = (int64_t)blk * chunk; q0 < a.n_ext; q0 += (int64_t)a.nblocks * chunk) {
+        const int64_t qb = q0 + lane_off;
+        float r[PPT], gv[PPT], b[PPT];
+#pragma unroll
+        for (int j = 0; j < PPT; ++j) {
+            const int64_t q = qb + 64 * j;
+            const bool in = q < a.n_ext;
+            r[j] = in ? a.R[q] : 0.f;
+            gv[j] = in ? a.G[q] : 0.f;
+            b[j] = in ? a.B[q] : 0.f;
+        }
+        uint4 e[PPT][4];
+        bool inside[PPT];
+#pragma unroll
+        for (int j = 0; j < PPT; ++j) {
+            inside[j] = qb + 64 * j < a.n_ext && r[j] >= 0.f && r[j] <= 1.f && gv[j] >= 0.f &&
+                        gv[j] <= 1.f && b[j] >= 0.f && b[j] <= 1.f;
+            const int64_t cell = (int64_t)(min((int)(r[j] * (float)G2), G2 - 1) * G2 +
+                                           min((int)(gv[j] * (float)G2), G2 - 1)) * G2 +
+                                 min((int)(b[j] * (float)G2), G2 - 1);
+            const uint4* line = reinterpret_cast<const uint4*>(lines + (inside[j] ? cell : 0) * 64);
+#pragma unroll
+            for (int pp = 0; pp < 4; ++pp)
+                e[j][pp] = (inside[j] && !exh_pal[pp]) ? line[pp] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < PPT; ++j) {
+            const int64_t q = qb + 64 * j;
+#pragma unroll
+            for (int pp = 0; pp < 4; ++pp) {
+                if (pp >= ng) break;
+                const int pq = p0 + pp;
+                const int k = argmin_from_entry<1>(r[j], gv[j], b[j], e[j][pp],
+                                                   inside[j] && !exh_pal[pp], s_pal + pp * a.K, 0,
+                                                   a.lvl1 + (int64_t)pq * a.lvl1_pitch, G2, a.K);
+                if (q < a.n_ext) {
+                    a.idx[(int64_t)pq * a.idx_pitch + q] = (uint8_t)k;
+                    const uint32_t bit = 1u << (k & 31);
+                    if (!(s_used[pp][k >> 5] & bit)) atomicOr(&s_used[pp][k >> 5], bit);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (tid < 8 * ng)
+        a.used_mask[((int64_t)(p0 + (tid >> 3)) * a.nblocks + blk) * 8 + (tid & 7)] =
+            s_used[tid >> 3][tid & 7];
+}
+
+// assign_pipe: assign_quad as a three-stage software pipeline over a thread's
+// pixels.  The level-2 lookup depends on the pixel's RGB, so a batch that loads
+// RGB, then looks up, then resolves pays two dependent memory round trips per
+// batch (a lookup made independent of the RGB ran 40% faster).  Here, while
+// pixel i is resolved, pixel i+1's line lookup and pixel i+2's RGB are in flight.
+__device__ __forceinline__ int64_t quad_cell(float r, float g, float b, int G2) {
+    return (int64_t)(min((int)(r * (float)G2), G2 - 1) * G2 + min((int)(g * (float)G2), G2 - 1)) * G2 +
+           min((int)(b * (float)G2), G2 - 1);
+}
+
+__global__ __launch_bounds__(256) void assign_pipe_kernel(AssignArgs a, int P) {
+    constexpr int PPT = 8;  // pixels per thread per chunk (the pipeline runs across chunks)
+    extern __shared__ __attribute__((aligned(16))) float4 s_pal[];  // [4][K]
+    __shared__ uint32_t s_used[4][8];
+    const int ngroups = (P + 3) / 4;
+    const int w = xcd_remap(blockIdx.x, a.nblocks * ngroups);
+    const int grp = w % ngroups, blk = w / ngroups, tid = threadIdx.x;
+    const int p0 = 4 * grp, ng = min(4, P - p0);
+    for (int e = tid; e < ng * a.K; e += 256) {
+        const int pp = e / a.K, k = e - pp * a.K;
+        s_pal[e] = a.pal[(int64_t)(p0 + pp) * kMaxK + k];
+    }
+    if (tid < 32) s_used[tid >> 3][tid & 7] = 0;
+    __syncthreads();
+    bool exh_pal[4];
+#pragma unroll
+    for (int pp = 0; pp < 4; ++pp) exh_pal[pp] = pp >= ng || a.pflags[p0 + min(pp, ng - 1)] != 0 || a.G2 == 0;
+    const uint8_t* lines = a.lvl2 + (int64_t)grp * a.lvl2_gstride;
+    const int G2 = a.G2 > 0 ? a.G2 : 4;
+    // pixel sequence of this thread: chunk c (stride nblocks), slot j < PPT
+    const int64_t chunk = 256 * PPT, cstride = (int64_t)a.nblocks * chunk;
+    const int64_t lane_off = (int64_t)(tid >> 6) * 64 * PPT + (tid & 63);
+    auto qpos = [&](int64_t i) {  // i-th pixel of this thread
+        return (int64_t)blk * chunk + (i / PPT) * cstride + lane_off + 64 * (i % PPT);
+    };
+    // Loads are unconditional (clamped addresses, results selected afterwards):
+    // predicated loads sit behind branches, and the compiler's wait counting
+    // then keeps at most one load in flight.
+    const int64_t qlast = a.n_ext - 1;
+    auto load_rgb = [&](int64_t q, float& r, float& g, float& b) {
+        const int64_t qc = min(q, qlast);
+        r = a.R[qc];
+        g = a.G[qc];
+        b = a.B[qc];
+    };
+    auto lookup = [&](int64_t q, float r, float g, float b, bool& inside, uint4 (&e)[4]) {
+        inside = q < a.n_ext && r >= 0.f && r <= 1.f && g >= 0.f && g <= 1.f && b >= 0.f && b <= 1.f;
+        const uint4* line = reinterpret_cast<const uint4*>(lines + (inside ? quad_cell(r, g, b, G2) : 0) * 64);
+#pragma unroll
+        for (int pp = 0; pp < 4; ++pp) e[pp] = line[pp];  // selected by the `listed` flag at use
+    };
+    // Pipeline, unrolled by two so every buffer has a fixed register set (a
+    // register copy of an in-flight load waits for it: rotating buffers at the
+    // loop end serialised the whole pipeline behind an s_waitcnt vmcnt(0)).
+    // Step i (parity h = i & 1): RGB(i+1) has landed -> its cell lookup goes out
+    // into E[h^1] and its RGB moves to X[h^1]; RGB(i+3) goes out into the freed
+    // buffer; pixel i is resolved from E[h], X[h] while those loads fly.
+    float rb[2], gb[2], bb[2];        // RGB loads in flight: pixel i+1 / i+2 by parity
+    float xr[2], xg[2], xb[2];        // RGB of pixels being looked up / resolved
+    uint4 E[2][4];
+    bool in_[2];
+    int64_t qq[2];
+    load_rgb(qpos(0), xr[0], xg[0], xb[0]);
+    qq[0] = qpos(0);
+    lookup(qq[0], xr[0], xg[0], xb[0], in_[0], E[0]);
+    load_rgb(qpos(1), rb[1], gb[1], bb[1]);
+    load_rgb(qpos(2), rb[0], gb[0], bb[0]);
+    auto resolve = [&](int h) {
+        const int64_t q = qq[h];
+#pragma unroll
+        for (int pp = 0; pp < 4; ++pp) {
+            if (pp >= ng) break;
+            const int pq = p0 + pp;
+            const int k = argmin_from_entry<1>(xr[h], xg[h], xb[h], E[h][pp], in_[h] && !exh_pal[pp],
+                                               s_pal + pp * a.K, 0,
+                                               a.lvl1 + (int64_t)pq * a.lvl1_pitch, G2, a.K);
+            a.idx[(int64_t)pq * a.idx_pitch + q] = (uint8_t)k;
+            const uint32_t bit = 1u << (k & 31);
+            if (!(s_used[pp][k >> 5] & bit)) atomicOr(&s_used[pp][k >> 5], bit);
+        }
+    };
+    auto step = [&](int64_t i, int h) {  // h == i & 1, a compile-time constant at each call
+        const int n = h ^ 1;
+        qq[n] = qpos(i + 1);
+        xr[n] = rb[n]; xg[n] = gb[n]; xb[n] = bb[n];  // RGB(i+1): landed, needed now anyway
+        lookup(qq[n], xr[n], xg[n], xb[n], in_[n], E[n]);
+        load_rgb(qpos(i + 3), rb[n], gb[n], bb[n]);
+        resolve(h);
+    };
+    for (int64_t i = 0;; i += 2) {
+        if (qpos(i) >= a.n_ext) break;
+        step(i, 0);
+        if (qpos(i + 1) >= a.n_ext) break;
+        step(i + 1, 1);
+    }
+    __syncthreads();
+    if (tid < 8 * ng)
+        a.used_mask[((int64_t)(p0 + (tid >> 3)) * a.nblocks + blk) * 8 + (tid & 7)] =
+            s_used[tid >> 3][tid & 7];
 }
 
 // assign_multi: grid (nblocks, ceil(P/PG)), dynamic LDS = PG*K*REP*16 B.  One
@@ -534,12 +736,10 @@ __global__ __launch_bounds__(256) void assign_multi_kernel(AssignArgs a, int P) 
     __syncthreads();
     const int copy = tid & (REP - 1);
     bool exh_pal[PG];
-    const uint8_t* lvl2p[PG];
 #pragma unroll
     for (int pp = 0; pp < PG; ++pp) {
         const int pq = min(p0 + pp, P - 1);
         exh_pal[pp] = a.pflags[pq] != 0 || a.G2 == 0;
-        lvl2p[pp] = a.lvl2 + (int64_t)pq * a.lvl2_pitch;
     }
     const int64_t chunk = 256 * PPT;
     const int64_t lane_off = (int64_t)(tid >> 6) * 64 * PPT + (tid & 63);
@@ -556,15 +756,16 @@ __global__ __launch_bounds__(256) void assign_multi_kernel(AssignArgs a, int P) 
                         bn = inn ? a.B[qn] : 0.f;
             // one cell index, PG table loads in flight
             const bool inside = r >= 0.f && r <= 1.f && gv >= 0.f && gv <= 1.f && b >= 0.f && b <= 1.f;
-            const int64_t cell = ((int64_t)(min((int)(r * (float)G2), G2 - 1) * G2 +
-                                            min((int)(gv * (float)G2), G2 - 1)) * G2 +
-                                  min((int)(b * (float)G2), G2 - 1)) * 16;
+            const int64_t cell = (int64_t)(min((int)(r * (float)G2), G2 - 1) * G2 +
+                                           min((int)(gv * (float)G2), G2 - 1)) * G2 +
+                                 min((int)(b * (float)G2), G2 - 1);
             uint4 e[PG];
             bool li[PG];
 #pragma unroll
             for (int pp = 0; pp < PG; ++pp) {
                 li[pp] = inside && !exh_pal[pp] && pp < ng;
-                e[pp] = li[pp] ? *reinterpret_cast<const uint4*>(lvl2p[pp] + cell)
+                e[pp] = li[pp] ? *reinterpret_cast<const uint4*>(
+                                     a.lvl2 + lvl2_offset(a.lvl2_gstride, min(p0 + pp, P - 1), cell))
                                : make_uint4(0, 0, 0, 0);
             }
 #pragma unroll
@@ -1389,8 +1590,27 @@ static hipError_t launch_assign_batch(const AssignArgs& a, int P, hipStream_t s)
 // rep: LDS replication of the palette (1, 4 or 16); lane l reads copy l % rep.
 // group > 1: one pixel pass serves `group` palettes (assign_multi_kernel).
 // batch: 4 or 8 = assign_batch_kernel with that many pixels per round trip
-// (single palette copy), 0 = assign_kernel.
+// (single palette copy), 0 = assign_kernel; with group 4, batch 1 or 2 =
+// assign_quad_kernel (4 palettes per pixel pass, PPT = batch).
+template <int PPT>
+static hipError_t launch_assign_quad(const AssignArgs& a, int P, hipStream_t s) {
+    const size_t lds = (size_t)4 * a.K * sizeof(float4);
+    const unsigned grid = (unsigned)(a.nblocks * ((P + 3) / 4));
+    hipLaunchKernelGGL((assign_quad_kernel<PPT>), dim3(grid), dim3(256), lds, s, a, P);
+    return hipGetLastError();
+}
+
+static hipError_t launch_assign_pipe(const AssignArgs& a, int P, hipStream_t s) {
+    const size_t lds = (size_t)4 * a.K * sizeof(float4);
+    const unsigned grid = (unsigned)(a.nblocks * ((P + 3) / 4));
+    hipLaunchKernelGGL(assign_pipe_kernel, dim3(grid), dim3(256), lds, s, a, P);
+    return hipGetLastError();
+}
+
 hipError_t launch_assign(const AssignArgs& a, int P, int rep, int group, int batch, hipStream_t s) {
+    if (group == 4 && batch == 3) return launch_assign_pipe(a, P, s);
+    if (group == 4 && batch == 1) return launch_assign_quad<1>(a, P, s);
+    if (group == 4 && batch == 2) return launch_assign_quad<2>(a, P, s);
     if (batch == 4) return launch_assign_batch<4>(a, P, s);
     if (batch == 8) return launch_assign_batch<8>(a, P, s);
     if (group == 4) {

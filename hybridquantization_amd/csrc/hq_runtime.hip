@@ -112,8 +112,9 @@ struct hq_ctx {
     int cost_variant = 0;  // 0 tiled (default), 1 generic two-pass
     int assign_blocks_per_cu = 8;
     int assign_rep = 1;    // palette replication in the assign kernel's LDS
-    int assign_group = 1;  // palettes per pixel pass in the assign kernel (1, 2, 4)
-    int assign_batch = 4;  // pixels per memory round trip (assign_batch_kernel: 4, 8; 0 = off)
+    int assign_group = 4;  // palettes per pixel pass in the assign kernel (1, 2, 4)
+    int assign_batch = 3;  // group 4: 3 = pipelined (assign_pipe_kernel), 1/2 = batched;
+                           // group 1: 4/8 = batched, 0 = one-pixel prefetch
     int tile_cfg = 2;      // cost tile: 0 = 16 rows, 1 = 8 rows + split V pass, 2 = 8 rows,
                            // 3 = 8 rows + V pass on the matrix cores
     int trim = 1;          // skip taps < 1e-9 of the peak of the narrow k1 filters
@@ -301,7 +302,7 @@ int ensure_population(hq_ctx* c, int P, int K) {
     const int G2 = c->G2 > 0 ? c->G2 : 4;
     const int G1 = G2 / 4;
     const int64_t l1p = round_up((int64_t)G1 * G1 * G1 * 32, 256);
-    const int64_t l2p = round_up((int64_t)G2 * G2 * G2 * 16, 256);
+    const int64_t l2g = round_up((int64_t)G2 * G2 * G2 * 64, 256);  // per group of 4 palettes
     int tiles_x, ntiles;
     fast_tile_dims(g.W, g.r1 - g.r0, c->tile_cfg, &tiles_x, &ntiles);
     const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
@@ -314,7 +315,7 @@ int ensure_population(hq_ctx* c, int P, int K) {
     HIP_TRY(c, c->d_dup.ensure((size_t)P * kMaxK));
     HIP_TRY(c, c->d_pflags.ensure(sizeof(int) * (size_t)P));
     HIP_TRY(c, c->d_lvl1.ensure((size_t)P * l1p));
-    HIP_TRY(c, c->d_lvl2.ensure((size_t)P * l2p));
+    HIP_TRY(c, c->d_lvl2.ensure((size_t)((P + 3) / 4) * l2g));
     HIP_TRY(c, c->d_idx.ensure((size_t)P * g.idx_pitch));
     HIP_TRY(c, c->d_used_mask.ensure(sizeof(uint32_t) * 8 * (size_t)P * nblocks));
     HIP_TRY(c, c->d_partial.ensure(sizeof(double) * (size_t)P * nparts));
@@ -338,7 +339,7 @@ int enqueue_eval(hq_ctx* c, int P, int K) {
     const int G2 = c->G2 > 0 ? c->G2 : 4;
     const int G1 = G2 / 4;
     const int64_t l1p = round_up((int64_t)G1 * G1 * G1 * 32, 256);
-    const int64_t l2p = round_up((int64_t)G2 * G2 * G2 * 16, 256);
+    const int64_t l2g = round_up((int64_t)G2 * G2 * G2 * 64, 256);  // per group of 4 palettes
     const int nblocks = c->num_cu * c->assign_blocks_per_cu;
     HIP_TRY(c, hipMemcpyAsync(c->d_pal_in.p, c->h_pal, sizeof(float) * 4 * (size_t)P * K,
                               hipMemcpyHostToDevice, s));
@@ -348,14 +349,14 @@ int enqueue_eval(hq_ctx* c, int P, int K) {
     HIP_TRY(c, launch_prep_palette(pa, P, s));
     if (c->G2 > 0) {
         GridArgs ga{c->d_pal.as<float4>(), c->d_dup.as<uint8_t>(), c->d_pflags.as<int>(),
-                    c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(), K, G1, l1p, l2p};
+                    c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(), K, G1, l1p, l2g};
         HIP_TRY(c, launch_build_grid(ga, P, s));
     }
     if (c->prof) HIP_TRY(c, hipEventRecord(c->ev[1], s));
     AssignArgs aa{c->d_R.as<float>(), c->d_G.as<float>(), c->d_B.as<float>(), c->d_pal.as<float4>(),
                   c->d_pflags.as<int>(), c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(),
                   c->d_idx.as<uint8_t>(), c->d_used_mask.as<uint32_t>(), g.n_ext, g.idx_pitch,
-                  l1p, l2p, K, c->G2, nblocks};
+                  l1p, l2g, K, c->G2, nblocks};
     HIP_TRY(c, launch_assign(aa, P, c->assign_rep, c->assign_group, c->assign_batch, s));
     if (c->prof) HIP_TRY(c, hipEventRecord(c->ev[2], s));
     int tiles_x, ntiles;
@@ -872,7 +873,8 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
         if (value != 1 && value != 2 && value != 4) return fail(c, HQ_ERR_ARG, "assign_group in {1,2,4}");
         c->assign_group = value;
     } else if (!std::strcmp(name, "assign_batch")) {
-        if (value != 0 && value != 4 && value != 8) return fail(c, HQ_ERR_ARG, "assign_batch in {0,4,8}");
+        if (value < 0 || value > 8 || value == 5 || value == 6 || value == 7)
+            return fail(c, HQ_ERR_ARG, "assign_batch in {0,1,2,3,4,8}");
         c->assign_batch = value;
     } else if (!std::strcmp(name, "assign_rep")) {
         if (value != 1 && value != 2 && value != 4 && value != 16)

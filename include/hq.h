@@ -187,10 +187,13 @@ int hq_profile_reset(hq_ctx *ctx);
  *                  vertical items (4 WG/CU, default)
  *   "trim"         1 = skip the narrow k1 filters' taps below 1e-9 of their peak
  *                  (default; only when the filters allow it), 0 = all taps
- *   "assign_rep"   palette replication in the assign kernel's LDS: 1 (default), 2, 4, 16
- *   "assign_group" palettes evaluated per pixel pass in the assign kernel: 1 (default), 2, 4
- *   "assign_batch" pixels per memory round trip in the assign kernel: 4 (default), 8;
- *                  0 = one-pixel-ahead prefetch (then "assign_rep" / "assign_group" apply)
+ *   "assign_group" palettes served by one pixel pass: 4 (default; their level-2 entries
+ *                  share one 64-byte line), 2, 1
+ *   "assign_batch" with group 4: 3 = software-pipelined (default: the next pixel's lookup
+ *                  and the one after's RGB in flight while a pixel is resolved), 1 or 2 =
+ *                  pixels per batch; with group 1: 4 or 8 = pixels per batch, 0 = one-pixel
+ *                  prefetch
+ *   "assign_rep"   palette replication in LDS for group 1/2 with batch 0: 1, 2, 4, 16
  *   "assign_blocks_per_cu" workgroups per CU of the assign grid (default 8) */
 int hq_set_option(hq_ctx *ctx, const char *name, int value);
 

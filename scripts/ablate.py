@@ -94,6 +94,20 @@ extern "C" int hq_debug_phases(unsigned long long* out, int reset) {
     return 0;
 }
 """}
+# assign_batch: first candidate only (no candidate loop / slow path)
+PATCHES["a_noloop"] = [(
+    "            const int k = argmin_from_entry<REP>(r[j], gv[j], b[j], e[j], li[j], s_pal, copy, lvl1p,\n                                                 a.G2, a.K);",
+    "            const int k = (int)((e[j].x >> 8) & 0xff) + (li[j] ? 0 : (int)s_pal[0].w);")]
+# assign_batch: cell entry from a fixed cell (no RGB -> lookup dependency, L2-hot)
+PATCHES["a_fixedcell"] = [(
+    "            li[j] = lvl2_lookup(r[j], gv[j], b[j], lvl2p, a.G2, exh_pal || qb + 64 * j >= a.n_ext, e[j]);",
+    "            li[j] = lvl2_lookup(0.5f, 0.5f, 0.5f + 1e-9f * r[j], lvl2p, a.G2, exh_pal || qb + 64 * j >= a.n_ext, e[j]);")]
+# assign_pipe: first candidate only
+PATCHES["p_noloop"] = [(
+    """            const int k = argmin_from_entry<1>(xr[h], xg[h], xb[h], E[h][pp], in_[h] && !exh_pal[pp],
+                                               s_pal + pp * a.K, 0,
+                                               a.lvl1 + (int64_t)pq * a.lvl1_pitch, G2, a.K);""",
+    """            const int k = (int)((E[h][pp].x >> 8) & 0xff) + (in_[h] ? 0 : (int)s_pal[0].w);""")]
 PATCHES["skeleton"] = PATCHES["novfma"] + PATCHES["nohfma"] + PATCHES["nolab"]
 PATCHES["skeleton_bcast"] = PATCHES["skeleton"] + PATCHES["gatherbcast"]
 

@@ -31,8 +31,9 @@ def main():
     ap.add_argument("--tile", type=int, default=2)
     ap.add_argument("--rep", type=int, default=1)
     ap.add_argument("--trim", type=int, default=1)
-    ap.add_argument("--group", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=4)
+    ap.add_argument("--group", type=int, default=4)
+    ap.add_argument("--batch", type=int, default=3)
+    ap.add_argument("--bpc", type=int, default=0, help="assign workgroups per CU (0 = library default)")
     ap.add_argument("--lib", default=None, help="alternative libhq build (scripts/ablate.py)")
     args = ap.parse_args()
     if args.lib:
@@ -47,6 +48,8 @@ def main():
     m.setOption("trim", args.trim)
     m.setOption("assign_group", args.group)
     m.setOption("assign_batch", args.batch)
+    if args.bpc:
+        m.setOption("assign_blocks_per_cu", args.bpc)
     W = H = args.size
     R, G, B = synthetic_planes(W, H, 1)
     _lib.check(lib.hq_set_image_planar_shard(m.ctx, _lib.fptr(R), _lib.fptr(G), _lib.fptr(B), W, H,
@@ -73,7 +76,7 @@ def main():
         n = C.c_int64()
         lib.hq_profile_get(m.ctx, k.encode(), C.byref(ms), C.byref(n))
         out.append(f"{k}={ms.value / max(n.value, 1):.4f}ms")
-    print(f"{os.path.basename(args.lib or 'libhq.so')} size={W} K={args.K} P={args.P} grid={args.grid} variant={args.variant} tile={args.tile} rep={args.rep} trim={args.trim} group={args.group} batch={args.batch}: "
+    print(f"{os.path.basename(args.lib or 'libhq.so')} size={W} K={args.K} P={args.P} grid={args.grid} variant={args.variant} tile={args.tile} rep={args.rep} trim={args.trim} group={args.group} batch={args.batch} bpc={args.bpc}: "
           f"{el / args.evals * 1e3:.3f} ms/eval-population, "
           f"{W * H * args.P * args.evals / el / 1e6:.1f} Mpx*evals/s  ", " ".join(out),
           "costs", costs.tolist())

@@ -125,12 +125,13 @@ def test_eval_config2_1024_k64(ip, filt):
 # argmin edge cases (CL:179-193), bit-exact
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("grid", [64, 32, 16, 0])
-@pytest.mark.parametrize("batch", [0, 4, 8])
-def test_assign_edge_cases(ip, grid, batch):
+@pytest.mark.parametrize("group_batch", [(1, 0), (1, 4), (1, 8), (4, 1), (4, 2), (4, 3)])
+def test_assign_edge_cases(ip, grid, group_batch):
     g = np.load(os.path.join(GOLD, "edge_assign.npz"))
     px = g["px"]  # 4096 pixels -> 64 x 64 image, values partly outside [0, 1]
     ip.setOption("grid", grid)
-    ip.setOption("assign_batch", batch)
+    ip.setOption("assign_group", group_batch[0])
+    ip.setOption("assign_batch", group_batch[1])
     ip.setImage(px.reshape(-1), np.zeros_like(px).reshape(-1), 64, ip.illum)
     for name in ("dup", "clamped", "k1", "k256", "ties"):
         pal = g[f"pal_{name}"]
@@ -154,7 +155,9 @@ def test_assign_random_and_near_ties(ip, K):
     ref_idx, ref_used = c_oracle.assign(px, pal)
     for grid, group, rep, batch in ((64, 1, 4, 0), (32, 4, 4, 0), (32, 2, 4, 0), (32, 4, 1, 0),
                                     (16, 4, 2, 0), (0, 1, 16, 0), (32, 1, 1, 4), (32, 1, 1, 8),
-                                    (64, 1, 1, 8), (0, 1, 1, 4)):
+                                    (64, 1, 1, 8), (0, 1, 1, 4), (32, 4, 1, 1), (32, 4, 1, 2),
+                                    (64, 4, 1, 2), (16, 4, 1, 1), (0, 4, 1, 2), (32, 4, 1, 3),
+                                    (64, 4, 1, 3), (0, 4, 1, 3)):
         ip.setOption("grid", grid)
         ip.setOption("assign_group", group)
         ip.setOption("assign_rep", rep)
