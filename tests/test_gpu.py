@@ -218,6 +218,25 @@ def test_row_block_shards_sum_to_full(gpu, filt):
     full.close()
 
 
+def test_rccl_single_rank_allreduce(gpu, filt):
+    """The multi-GPU path on one GPU: libhq's own RCCL communicator (unique id,
+    ncclCommInitRank, the fp64 all-reduce on the context stream) with one rank
+    leaves the costs and used flags unchanged."""
+    w, h, K, P = 80, 64, 48, 4
+    R, G, B = o.synthetic_image(w, h, seed=6)
+    rgba = o.inline_rgba(R, G, B).reshape(-1)
+    pals = np.stack([o.synthetic_palette(K, 80 + p) for p in range(P)]).reshape(P, -1)
+    m = hq.ImageManipulation(device=gpu)
+    hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
+    m.setImage(rgba, None, w, filt.illum, row_begin=0, row_end=h)
+    c0, u0 = m.computeQuantizationErrorPopulation(pals, 2.0, return_used=True)
+    m.initComm(1, 0, hq.ImageManipulation.commUniqueId())
+    c1, u1 = m.computeQuantizationErrorPopulation(pals, 2.0, return_used=True)
+    np.testing.assert_array_equal(c1, c0)
+    np.testing.assert_array_equal(u1, u0)
+    m.close()
+
+
 # ---------------------------------------------------------------------------
 # Final quantize (IM:770) and error image (IM:858)
 # ---------------------------------------------------------------------------
