@@ -53,7 +53,7 @@ def measured_traffic(size, K, P, grid, world):
     if world != 1 or (c.get("size"), c.get("K"), c.get("P"), c.get("grid")) != (size, K, P, grid):
         return None
     for name, v in d.get("kernels", {}).items():
-        if "cost_tile_kernel" in name:
+        if name.startswith("hq::cost_"):  # the fast cost kernel of the default tile config
             return int(v["traffic_bytes"])
     return None
 
@@ -180,7 +180,7 @@ def main():
     P = args.population
     n_own = W * (r1 - r0)
     value = W * H * P * args.steps / elapsed / 1e6
-    # Dominant kernel: cost_tile (S-CIELAB stencil + Opp->Lab + dE76).  With P > 1
+    # Dominant kernel: the cost kernel (S-CIELAB stencil + Opp->Lab + dE76).  With P > 1
     # palettes per launch its HBM bytes (LabRef once + P index images) amortise
     # and FP32 VALU bounds it: algorithmic flops per pixel-eval =
     # the reference's stencil, 7 separable filters x 2 passes x 21 taps x 2 flops
@@ -213,7 +213,7 @@ def main():
         "roofline": {"bound": "valu", "achieved": round(achieved_tf, 2), "peak": FP32_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4),
                      "traffic": traffic,
-                     "kernel": "cost_tile_kernel", "kernel_avg_ms": round(cost_ms, 4),
+                     "kernel": "cost_pair_kernel (cost_tile 4)", "kernel_avg_ms": round(cost_ms, 4),
                      "alg_flops_per_launch": alg_flops, "alg_bytes_per_launch": alg_bytes,
                      "hbm_GBs_alg": round(alg_bytes / (cost_ms * 1e-3) / 1e9, 1) if cost_ms > 0 else 0.0,
                      "note": "f32 VALU kernel; peak = MI355X FP32 vector (= FP32 MFMA) 157.3 TFLOP/s; "

@@ -812,7 +812,8 @@ using TapsPtr = const __attribute__((address_space(4))) CostTaps<HALF>*;
 // thread from RV + 2*HALF gathered inputs; results to s_v[f][row][col].
 // Taps [TLO, THI] only (the default filter set's narrow k1 filters have |taps|
 // below 1e-9 of their peak outside a short window; see trim_window()).
-template <int HALF, int RV, int TH, int RW, int TLO = 0, int THI = 2 * HALF>
+// PAIR: s_v holds row pairs, float2 (row 2m, row 2m+1) per column (cost_pair_kernel).
+template <int HALF, int RV, int TH, int RW, int TLO = 0, int THI = 2 * HALF, bool PAIR = false>
 __device__ __forceinline__ void vpass_filters(const float (&o)[RV + 2 * HALF],
                                               TapsPtr<HALF> taps, int f0, int f1,
                                               float* out) {
@@ -827,8 +828,16 @@ __device__ __forceinline__ void vpass_filters(const float (&o)[RV + 2 * HALF],
 #pragma unroll
             for (int y = 0; y < RV; ++y) acc[y] = fmaf(o[y + t], k, acc[y]);
         }
+        if constexpr (PAIR) {
+            static_assert(RV % 2 == 0, "whole row pairs per item");
 #pragma unroll
-        for (int y = 0; y < RV; ++y) out[(f * TH + y) * RW] = acc[y];
+            for (int y = 0; y < RV; y += 2)
+                *reinterpret_cast<float2*>(out + (f * (TH / 2) + y / 2) * RW * 2) =
+                    make_float2(acc[y], acc[y + 1]);
+        } else {
+#pragma unroll
+            for (int y = 0; y < RV; ++y) out[(f * TH + y) * RW] = acc[y];
+        }
     }
 }
 
@@ -871,22 +880,23 @@ __device__ __forceinline__ void hpass_filters(const float4* src, TapsPtr<HALF> t
 // in SGPRs (interleaving a channel's filters needs 63 and spills to VGPR lanes).
 constexpr int kTrimLo[3] = {7, 6, 5}, kTrimHi[3] = {13, 14, 15};
 
-template <int HALF, int RV, int TH, int RW, bool TRIM>
+template <int HALF, int RV, int TH, int RW, bool TRIM, bool PAIR = false>
 __device__ __forceinline__ void vpass_all(const float (&o0)[RV + 2 * HALF],
                                           const float (&o1)[RV + 2 * HALF],
                                           const float (&o2)[RV + 2 * HALF],
                                           TapsPtr<HALF> taps, float* out) {
+    constexpr int T2 = 2 * HALF;
     if constexpr (TRIM) {
-        vpass_filters<HALF, RV, TH, RW, kTrimLo[0], kTrimHi[0]>(o0, taps, 0, 1, out);
-        vpass_filters<HALF, RV, TH, RW>(o0, taps, 1, 3, out);
-        vpass_filters<HALF, RV, TH, RW, kTrimLo[1], kTrimHi[1]>(o1, taps, 3, 4, out);
-        vpass_filters<HALF, RV, TH, RW>(o1, taps, 4, 5, out);
-        vpass_filters<HALF, RV, TH, RW, kTrimLo[2], kTrimHi[2]>(o2, taps, 5, 6, out);
-        vpass_filters<HALF, RV, TH, RW>(o2, taps, 6, 7, out);
+        vpass_filters<HALF, RV, TH, RW, kTrimLo[0], kTrimHi[0], PAIR>(o0, taps, 0, 1, out);
+        vpass_filters<HALF, RV, TH, RW, 0, T2, PAIR>(o0, taps, 1, 3, out);
+        vpass_filters<HALF, RV, TH, RW, kTrimLo[1], kTrimHi[1], PAIR>(o1, taps, 3, 4, out);
+        vpass_filters<HALF, RV, TH, RW, 0, T2, PAIR>(o1, taps, 4, 5, out);
+        vpass_filters<HALF, RV, TH, RW, kTrimLo[2], kTrimHi[2], PAIR>(o2, taps, 5, 6, out);
+        vpass_filters<HALF, RV, TH, RW, 0, T2, PAIR>(o2, taps, 6, 7, out);
     } else {
-        vpass_filters<HALF, RV, TH, RW>(o0, taps, 0, 3, out);
-        vpass_filters<HALF, RV, TH, RW>(o1, taps, 3, 5, out);
-        vpass_filters<HALF, RV, TH, RW>(o2, taps, 5, 7, out);
+        vpass_filters<HALF, RV, TH, RW, 0, T2, PAIR>(o0, taps, 0, 3, out);
+        vpass_filters<HALF, RV, TH, RW, 0, T2, PAIR>(o1, taps, 3, 5, out);
+        vpass_filters<HALF, RV, TH, RW, 0, T2, PAIR>(o2, taps, 5, 7, out);
     }
 }
 
@@ -1530,6 +1540,151 @@ __global__ __launch_bounds__(256) void error_image_kernel(const float4* orig, co
 }
 
 // ----------------------------------------------------------------------------
+// cost_pair (cost_tile 4 / 5): the 8-row tile with s_v stored as row pairs,
+// float2 (row 2m, row 2m+1) per column.  The horizontal pass then runs
+// v_pk_fma_f32 across a row pair, so every tap reads a naturally aligned
+// register pair: the row layout's odd taps needed register-pair shuffles (17
+// moves per filter and item, ~29% of the pass's VALU instructions).  HR output
+// columns per item: HR = 2 gives 216 items per tile (balanced over 256 threads)
+// at 1.8x the LDS reads per output; HR = 4 keeps the reads but fills 108 threads.
+// ----------------------------------------------------------------------------
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+template <int HALF, int TH, int RW, int HR, int TLO = 0, int THI = 2 * HALF>
+__device__ __forceinline__ void hpass_pair_filters(const f32x4* src, TapsPtr<HALF> taps, int f0,
+                                                   int f1, f32x2 (&acc)[HR]) {
+    constexpr int NIN = HR + 2 * HALF;  // window columns (float2 each)
+    constexpr int NQ = (NIN + 1) / 2;   // ds_read_b128, two columns each
+#pragma unroll 1
+    for (int f = f0; f < f1; ++f) {
+        const f32x4* row = src + f * (TH / 2) * RW / 2;
+        f32x4 v[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) v[q] = row[q];
+        f32x2 in[2 * NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            in[2 * q] = v[q].xy;
+            in[2 * q + 1] = v[q].zw;
+        }
+#pragma unroll
+        for (int t = TLO; t <= THI; ++t) {
+            const float k = taps->h[f][t];
+            const f32x2 kk = {k, k};
+#pragma unroll
+            for (int xo = 0; xo < HR; ++xo) acc[xo] = __builtin_elementwise_fma(in[xo + t], kk, acc[xo]);
+        }
+    }
+}
+
+template <int HALF, int TH, int RW, int HR, bool TRIM>
+__device__ __forceinline__ void hpass_pair_all(const f32x4* src, TapsPtr<HALF> taps,
+                                               f32x2 (&acc0)[HR], f32x2 (&acc1)[HR],
+                                               f32x2 (&acc2)[HR]) {
+    constexpr int T2 = 2 * HALF;
+#pragma unroll
+    for (int xo = 0; xo < HR; ++xo) acc0[xo] = acc1[xo] = acc2[xo] = f32x2{0.f, 0.f};
+    if constexpr (TRIM) {
+        hpass_pair_filters<HALF, TH, RW, HR, kTrimLo[0], kTrimHi[0]>(src, taps, 0, 1, acc0);
+        hpass_pair_filters<HALF, TH, RW, HR, 0, T2>(src, taps, 1, 3, acc0);
+        hpass_pair_filters<HALF, TH, RW, HR, kTrimLo[1], kTrimHi[1]>(src, taps, 3, 4, acc1);
+        hpass_pair_filters<HALF, TH, RW, HR, 0, T2>(src, taps, 4, 5, acc1);
+        hpass_pair_filters<HALF, TH, RW, HR, kTrimLo[2], kTrimHi[2]>(src, taps, 5, 6, acc2);
+        hpass_pair_filters<HALF, TH, RW, HR, 0, T2>(src, taps, 6, 7, acc2);
+    } else {
+        hpass_pair_filters<HALF, TH, RW, HR, 0, T2>(src, taps, 0, 3, acc0);
+        hpass_pair_filters<HALF, TH, RW, HR, 0, T2>(src, taps, 3, 5, acc1);
+        hpass_pair_filters<HALF, TH, RW, HR, 0, T2>(src, taps, 5, 7, acc2);
+    }
+}
+
+template <int DE, bool TRIM, int HR>
+__global__ __launch_bounds__(256, 4) void cost_pair_kernel(CostArgs a, int P_) {
+    constexpr int HALF = 10, RW = 128, TH = 8, RV = 4;
+    constexpr int TW = RW - 2 * HALF, RH = TH + 2 * HALF, NIN = RV + 2 * HALF;
+    constexpr int NRUN = TW / HR;
+    constexpr int SLOTS = HR == 2 ? 64 : 32;  // run slots per row pair: 16-lane b128 groups
+    constexpr int NITEM = (TH / 2) * SLOTS;  // read consecutive 16-B columns pairs
+    static_assert(TW % HR == 0 && NRUN <= SLOTS && NITEM <= 256, "H items");
+    __shared__ f32x4 s_vq[kNumFilt * (TH / 2) * RW / 2];  // float2 per (filter, pair, column)
+    __shared__ float4 s_opp[kMaxK];
+    __shared__ __attribute__((aligned(16))) uint8_t s_idx[RH * RW];
+    __shared__ double s_red[4];
+    float* s_v = reinterpret_cast<float*>(s_vq);
+    const int tid = threadIdx.x;
+    const Geom& g = a.g;
+    const TileItem cur = tile_item<TW, TH>(a, xcd_remap(blockIdx.x, a.ntiles * P_), P_);
+    const TapsPtr<HALF> taps = (TapsPtr<HALF>)(uintptr_t)a.taps;
+
+    TileFill<HALF, RW, TH> fill;
+    fill.issue(a, cur, tid);
+    if (tid < a.K) s_opp[tid] = fill.ov;
+    fill.template commit_idx<RW>(a, s_idx, tid);
+    // this thread's H item: row pair m, columns HR*jr .. +HR-1; its LabRef now
+    const int m = tid / SLOTS, jr = tid % SLOTS;
+    const bool has_item = tid < NITEM && jr < NRUN;
+    const int gy0 = cur.y0 + 2 * m, gx0 = cur.x0 + HR * jr;
+    float labv[2][3][HR];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const bool ok = has_item && gy0 + r < g.r1 && gx0 < g.W;
+        const int off = ok ? (gy0 + r - g.r0) * g.lab_pitch + gx0 : 0;
+        const float* src3[3] = {a.labL, a.labA, a.labB};
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+            if constexpr (HR == 4) {
+                const float4 v = *reinterpret_cast<const float4*>(src3[ch] + off);
+                labv[r][ch][0] = v.x; labv[r][ch][1] = v.y; labv[r][ch][2] = v.z; labv[r][ch][3] = v.w;
+            } else {
+                const float2 v = *reinterpret_cast<const float2*>(src3[ch] + off);
+                labv[r][ch][0] = v.x; labv[r][ch][1] = v.y;
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- vertical pass (row-pair output layout): thread = (column c, rows RV*gr..) ----
+    {
+        const int c = tid % RW, gr = tid / RW;
+        float o0[NIN], o1[NIN], o2[NIN];
+        float wsum = 0.f;  // .w (= 0) is consumed so the gather stays one ds_read_b128
+#pragma unroll
+        for (int r = 0; r < NIN; ++r) {
+            const float4 v = s_opp[s_idx[(gr * RV + r) * RW + c]];
+            o0[r] = v.x; o1[r] = v.y; o2[r] = v.z;
+            wsum += v.w;
+        }
+        o0[0] += wsum;  // wsum == 0 exactly (prep_palette writes .w = 0)
+        vpass_all<HALF, RV, TH, RW, TRIM, true>(o0, o1, o2, taps, s_v + ((gr * RV / 2) * RW + c) * 2);
+    }
+    __syncthreads();
+
+    // ---- horizontal pass over the row pair + Lab + dE ----
+    double sum = 0.0;
+    if (has_item) {
+        f32x2 acc0[HR], acc1[HR], acc2[HR];
+        hpass_pair_all<HALF, TH, RW, HR, TRIM>(&s_vq[(m * RW + HR * jr) / 2], taps, acc0, acc1, acc2);
+        float part = 0.f;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+#pragma unroll
+            for (int xo = 0; xo < HR; ++xo) {
+                const float3 l3 = opp2lab_fast(acc0[xo][r], acc1[xo][r], acc2[xo][r], a.m_lab);
+                const float e = delta_e<DE>(labv[r][0][xo], labv[r][1][xo], labv[r][2][xo], l3.x,
+                                            l3.y, l3.z);
+                part += (gy0 + r < g.r1 && gx0 + xo < g.W) ? e : 0.f;
+            }
+        }
+        sum = (double)part;
+    }
+    sum = wave_sum_to_lane63(sum);
+    if ((tid & 63) == 63) s_red[tid >> 6] = sum;
+    __syncthreads();
+    if (tid == 0)
+        a.partial[(int64_t)cur.p * a.ntiles + cur.tile] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+}
+
+// ----------------------------------------------------------------------------
 // Launchers (host side of this translation unit)
 // ----------------------------------------------------------------------------
 static inline unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }
@@ -1694,7 +1849,7 @@ constexpr int kFastTW = kFastRW - 2 * kFastHalf;
 // tile rows of the fast path: cfg 0 = 16 (RV 8, 2 WG/CU); cfg 1 = 8 with the V
 // pass split by channel group (4 WG/CU); cfg 2 = 8 (RV 4, 4 WG/CU); cfg 3 = 8
 // with the V pass on the matrix cores
-int fast_tile_rows(int tile_cfg) { return tile_cfg == 0 ? kFastTH : 8; }
+int fast_tile_rows(int tile_cfg) { return tile_cfg == 0 ? kFastTH : 8; }  // cfg 4, 5: 8 rows
 
 void fast_tile_dims(int W, int own_rows, int tile_cfg, int* tiles_x, int* ntiles) {
     const int th = fast_tile_rows(tile_cfg);
@@ -1746,7 +1901,18 @@ hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, int tile_cfg, boo
                             hipStream_t s) {
     CostArgs a = a0;
     if (tile_cfg == 3) a.taps = static_cast<const char*>(a0.taps) + sizeof(CostTaps<10>);
-    if (tile_cfg == 3) {
+    if (tile_cfg == 4 || tile_cfg == 5) {
+        const dim3 grid((unsigned)(a.ntiles * P));
+#define HQ_PAIR(DEV, TR, HRV) hipLaunchKernelGGL((cost_pair_kernel<DEV, TR, HRV>), grid, dim3(256), 0, s, a, P)
+        if (tile_cfg == 4) {
+            if (de == 0) { if (trim) HQ_PAIR(0, true, 2); else HQ_PAIR(0, false, 2); }
+            else { if (trim) HQ_PAIR(1, true, 2); else HQ_PAIR(1, false, 2); }
+        } else {
+            if (de == 0) { if (trim) HQ_PAIR(0, true, 4); else HQ_PAIR(0, false, 4); }
+            else { if (trim) HQ_PAIR(1, true, 4); else HQ_PAIR(1, false, 4); }
+        }
+#undef HQ_PAIR
+    } else if (tile_cfg == 3) {
         if (trim) launch_tile_cfg<8, 8, 4, true, 2>(a, P, de, s);
         else launch_tile_cfg<8, 8, 4, false, 2>(a, P, de, s);
     } else if (tile_cfg == 1) {

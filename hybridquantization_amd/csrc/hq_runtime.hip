@@ -115,8 +115,9 @@ struct hq_ctx {
     int assign_group = 4;  // palettes per pixel pass in the assign kernel (1, 2, 4)
     int assign_batch = 3;  // group 4: 3 = pipelined (assign_pipe_kernel), 1/2 = batched;
                            // group 1: 4/8 = batched, 0 = one-pixel prefetch
-    int tile_cfg = 2;      // cost tile: 0 = 16 rows, 1 = 8 rows + split V pass, 2 = 8 rows,
-                           // 3 = 8 rows + V pass on the matrix cores
+    int tile_cfg = 4;      // cost tile: 0 = 16 rows, 1 = 8 rows + split V pass, 2 = 8 rows,
+                           // 3 = 8 rows + V pass on the matrix cores, 4 = 8 rows + row-pair
+                           // H pass (2 columns per item), 5 = row-pair H (4 columns)
     int trim = 1;          // skip taps < 1e-9 of the peak of the narrow k1 filters
     bool trim_ok = false;  // set by hq_set_filters (default 21-tap filter set)
 
@@ -867,7 +868,7 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
     } else if (!std::strcmp(name, "trim")) {
         c->trim = value != 0;
     } else if (!std::strcmp(name, "cost_tile")) {
-        if (value < 0 || value > 3) return fail(c, HQ_ERR_ARG, "cost_tile in {0,1,2,3}");
+        if (value < 0 || value > 5) return fail(c, HQ_ERR_ARG, "cost_tile in 0..5");
         c->tile_cfg = value;
     } else if (!std::strcmp(name, "assign_group")) {
         if (value != 1 && value != 2 && value != 4) return fail(c, HQ_ERR_ARG, "assign_group in {1,2,4}");
