@@ -85,21 +85,26 @@ __device__ __forceinline__ float3 opp2lab_ref(float o0, float o1, float o2, cons
     return make_float3(116.0f * fy - 16.0f, 500.0f * (fx - fy), 200.0f * (fy - fz));
 }
 
-// CL:201-231: dE76 (distance) or dE94.
+// CL:201-231: dE76 (distance) or dE94.  Hardware square root (v_sqrt_f32, ~1 ulp):
+// HIP's sqrtf is a correctly rounded ~10-instruction sequence, and the
+// reference's OpenCL distance()/sqrt is itself only ulp-accurate; the cost is
+// compared at 1e-4 relative.  (The argmin keeps sqrtf: its ties are exact.)
+__device__ __forceinline__ float hw_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+
 template <int DE>
 __device__ __forceinline__ float delta_e(float L1, float a1, float b1, float L2, float a2,
                                          float b2) {
     if constexpr (DE == 0) {
         const float dl = L1 - L2, da = a1 - a2, db = b1 - b2;
-        return sqrtf((dl * dl + da * da) + db * db);
+        return hw_sqrt((dl * dl + da * da) + db * db);
     } else {
         const float dL = L1 - L2;
-        const float c1 = sqrtf(fmaf(a1, a1, b1 * b1));
-        const float dC = c1 - sqrtf(fmaf(a2, a2, b2 * b2));
+        const float c1 = hw_sqrt(fmaf(a1, a1, b1 * b1));
+        const float dC = c1 - hw_sqrt(fmaf(a2, a2, b2 * b2));
         const float da = a1 - a2, db = b1 - b2;
-        const float dH = sqrtf(fmaf(da, da, db * db) - dC * dC);
+        const float dH = hw_sqrt(fmaf(da, da, db * db) - dC * dC);
         const float sc = 1.0f + 0.045f * c1, sh = 1.0f + 0.015f * c1;
-        return sqrtf(fmaf(dL, dL, fmaf(dC / sc, dC / sc, (dH / sh) * (dH / sh))));
+        return hw_sqrt(fmaf(dL, dL, fmaf(dC / sc, dC / sc, (dH / sh) * (dH / sh))));
     }
 }
 
