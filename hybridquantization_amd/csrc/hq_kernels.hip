@@ -163,7 +163,7 @@ __device__ __forceinline__ double wave_sum_to_lane63(double v) {
 }
 
 // ----------------------------------------------------------------------------
-// prep_palette: grid (P), block 256.
+// prep_palette: grid (P), block 1024.
 // ----------------------------------------------------------------------------
 // XCD-aware relabelling of a 1-D grid of N workgroups.  Workgroups are placed
 // round-robin over the 8 XCDs (b % 8), so XCD x is given the contiguous work
@@ -176,41 +176,50 @@ __device__ __forceinline__ int xcd_remap(int b, int N) {
     return x * q + min(x, r) + s;
 }
 
-__global__ __launch_bounds__(256) void prep_palette_kernel(PaletteArgs a) {
-    const int p = blockIdx.x, k = threadIdx.x;
+__global__ __launch_bounds__(1024) void prep_palette_kernel(PaletteArgs a) {
+    // 1024 threads: colour k = tid & 255 scans quarter q = tid >> 8 of the lower
+    // indices ([64q, 64q + 64)) for an exact duplicate; a quarter wholly above k
+    // is skipped by the whole wave.  (256 threads scanning all K entries each
+    // were latency-bound; a serial dependent loop was ~30 us.)
+    const int p = blockIdx.x, tid = threadIdx.x, k = tid & 255, q = tid >> 8;
     __shared__ float4 s[kMaxK];
+    __shared__ uint32_t s_dup[kMaxK / 32];
     __shared__ int s_nonfinite;
-    if (k == 0) s_nonfinite = 0;
-    __syncthreads();
+    if (tid < kMaxK / 32) s_dup[tid] = 0u;
+    if (tid == 0) s_nonfinite = 0;
     float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
     if (k < a.K) {
         c = a.pal_in[(int64_t)p * a.K + k];
         c.w = 0.f;  // SW:49: palettes carry .w = 0
+    }
+    __syncthreads();
+    if (q == 0 && k < a.K) {
         s[k] = c;
         if (!(isfinite(c.x) && isfinite(c.y) && isfinite(c.z))) atomicOr(&s_nonfinite, 1);
     }
     __syncthreads();
-    if (k < a.K) {
-        // exact duplicate at a lower index?  8 independent LDS reads per step
-        // (a serial dependent loop here was latency-bound at ~30 us).
-        // Uniform trip count (every lane scans all K entries, broadcast reads)
-        // so the loads pipeline; only the comparison is predicated on j < k.
+    const int j0 = q * 64;
+    if (j0 < (tid & 0xC0) + 64 && j0 < a.K) {  // wave-uniform: quarter may hold j < k
         bool dupb = false;
+        const int jn = min(64, a.K - j0);
 #pragma unroll 8
-        for (int j = 0; j < a.K; ++j) {
-            const float4 o = s[j];
-            dupb |= (j < k) & (o.x == c.x) & (o.y == c.y) & (o.z == c.z);
+        for (int u = 0; u < jn; ++u) {
+            const float4 o = s[j0 + u];
+            dupb |= (j0 + u < k) & (o.x == c.x) & (o.y == c.y) & (o.z == c.z);
         }
-        const uint8_t dup = dupb ? 1 : 0;
+        if (dupb && k < a.K) atomicOr(&s_dup[k >> 5], 1u << (k & 31));
+    }
+    __syncthreads();
+    if (q == 0 && k < a.K) {
         const float lr = srgb_lin(c.x), lg = srgb_lin(c.y), lb = srgb_lin(c.z);
         const float4 opp = make_float4(dot3(lr, lg, lb, c_RGB2Opp + 0),
                                        dot3(lr, lg, lb, c_RGB2Opp + 3),
                                        dot3(lr, lg, lb, c_RGB2Opp + 6), 0.f);
         a.pal[(int64_t)p * kMaxK + k] = c;
         a.opp[(int64_t)p * kMaxK + k] = opp;
-        a.dup[(int64_t)p * kMaxK + k] = dup;
+        a.dup[(int64_t)p * kMaxK + k] = (s_dup[k >> 5] >> (k & 31)) & 1u;
     }
-    if (k == 0) a.pflags[p] = s_nonfinite;
+    if (tid == 0) a.pflags[p] = s_nonfinite;
 }
 
 // ----------------------------------------------------------------------------
@@ -1349,45 +1358,58 @@ __global__ __launch_bounds__(256) void gen_vpass_kernel(GenArgs a) {
 // finalize: grid (P), block 256.  Fixed-order fp64 sum of the tile partials
 // and OR of the per-block used masks -> out[p] = {sum, used[0..K-1]}.
 // ----------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void finalize_kernel(FinalizeArgs a) {
+// finalize: one 1024-thread workgroup per palette.  Thread t sums partials
+// t, t + 1024, ... with all of its loads issued before the first add (one memory
+// round trip; 256 threads summing 8 at a time took ~10 dependent rounds), then
+// a fixed-order wave and workgroup reduction: bitwise reproducible.
+__global__ __launch_bounds__(1024) void finalize_kernel(FinalizeArgs a) {
+    constexpr int NT = 1024, NL = 24;  // loads in flight per thread per round
     const int p = blockIdx.x, tid = threadIdx.x;
-    __shared__ double s_red[4];
-    __shared__ uint32_t s_mask[256];
-    // 8 independent partial sums per thread (fixed order) for memory-level parallelism
+    __shared__ double s_red[NT / 64];
+    __shared__ uint32_t s_mask[NT];
     const double* part = a.partial + (int64_t)p * a.ntiles;
-    double s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int t0 = 0; t0 < a.ntiles; t0 += 256 * 8) {
+    double s = 0.0;
+    for (int t0 = 0; t0 < a.ntiles; t0 += NT * NL) {
+        double v[NL];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int t = t0 + u * 256 + tid;
-            s8[u] += t < a.ntiles ? part[t] : 0.0;
+        for (int u = 0; u < NL; ++u) {
+            const int t = t0 + u * NT + tid;
+            v[u] = t < a.ntiles ? part[t] : 0.0;
         }
+#pragma unroll
+        for (int u = 0; u < NL; ++u) s += v[u];
     }
-    double s = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
-    s = wave_sum(s);
-    if ((tid & 63) == 0) s_red[tid >> 6] = s;
+    s = wave_sum_to_lane63(s);
+    if ((tid & 63) == 63) s_red[tid >> 6] = s;
     // used: thread = (word w = tid & 7, block slice tid >> 3)
     uint32_t m = 0;
     const int w = tid & 7;
     const uint32_t* um = a.used_mask + (int64_t)p * a.nblocks * 8;
-    for (int b0 = tid >> 3; b0 < a.nblocks; b0 += 32 * 8) {
+    for (int b0 = tid >> 3; b0 < a.nblocks; b0 += (NT / 8) * 8) {
+        uint32_t mv[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const int b = b0 + 32 * u;
-            m |= b < a.nblocks ? um[b * 8 + w] : 0u;
+            const int b = b0 + (NT / 8) * u;
+            mv[u] = b < a.nblocks ? um[b * 8 + w] : 0u;
         }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) m |= mv[u];
     }
     s_mask[tid] = m;
     __syncthreads();
     double* out = a.out + (int64_t)p * (1 + a.K);
-    if (tid == 0) out[0] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+    if (tid == 0) {
+        double tot = 0.0;
+        for (int i = 0; i < NT / 64; ++i) tot += s_red[i];
+        out[0] = tot;
+    }
     if (tid < 8) {
         uint32_t acc = 0;
-        for (int i = tid; i < 256; i += 8) acc |= s_mask[i];
+        for (int i = tid; i < NT; i += 8) acc |= s_mask[i];
         s_mask[tid] = acc;  // slots 0..7 are only read after the barrier below
     }
     __syncthreads();
-    for (int k = tid; k < a.K; k += 256) out[1 + k] = (s_mask[k >> 5] >> (k & 31)) & 1u ? 1.0 : 0.0;
+    for (int k = tid; k < a.K; k += NT) out[1 + k] = (s_mask[k >> 5] >> (k & 31)) & 1u ? 1.0 : 0.0;
 }
 
 // ----------------------------------------------------------------------------
@@ -1700,7 +1722,7 @@ void opp2xyz_over_illum(const float inv_illum[3], float m[9]) {
 }
 
 hipError_t launch_prep_palette(const PaletteArgs& a, int P, hipStream_t s) {
-    hipLaunchKernelGGL(prep_palette_kernel, dim3(P), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(prep_palette_kernel, dim3(P), dim3(1024), 0, s, a);
     return hipGetLastError();
 }
 
@@ -1944,7 +1966,7 @@ hipError_t launch_cost_generic(const GenArgs& a, int de, hipStream_t s) {
 }
 
 hipError_t launch_finalize(const FinalizeArgs& a, int P, hipStream_t s) {
-    hipLaunchKernelGGL(finalize_kernel, dim3(P), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(finalize_kernel, dim3(P), dim3(1024), 0, s, a);
     return hipGetLastError();
 }
 

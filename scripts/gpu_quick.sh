@@ -5,7 +5,7 @@ mkdir -p gpurun_out/prof
 stop_if_fatal() { if [ "$1" -ge 124 ] || [ "$1" -eq 134 ] || [ "$1" -eq 139 ]; then echo "fatal rc=$1 at $2"; exit "$1"; fi; }
 timeout -k 10 900 python -m pytest tests -m gpu -q --maxfail=15 -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/pytest_gpu.log; stop_if_fatal $rc pytest
-IFS=';' read -r -a cfgs <<< "${CFGS:---variant 0;--variant 2;--variant 2 --trim 0;--variant 2 --tile 1}"
+IFS=";" read -r -a cfgs <<< "${CFGS:---tile 4;--tile 2}"
 for cfg in "${cfgs[@]}"; do
 timeout -k 10 300 python scripts/profile_eval.py --evals 10 $cfg > gpurun_out/prof/eval_cfg.log 2>&1
 rc=$?; cat gpurun_out/prof/eval_cfg.log; stop_if_fatal $rc eval
