@@ -213,7 +213,7 @@ def main():
         "roofline": {"bound": "valu", "achieved": round(achieved_tf, 2), "peak": FP32_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4),
                      "traffic": traffic,
-                     "kernel": "cost_pair_kernel (cost_tile 4)", "kernel_avg_ms": round(cost_ms, 4),
+                     "kernel": "cost_chan_kernel (cost_tile 6)", "kernel_avg_ms": round(cost_ms, 4),
                      "alg_flops_per_launch": alg_flops, "alg_bytes_per_launch": alg_bytes,
                      "hbm_GBs_alg": round(alg_bytes / (cost_ms * 1e-3) / 1e9, 1) if cost_ms > 0 else 0.0,
                      "note": "f32 VALU kernel; peak = MI355X FP32 vector (= FP32 MFMA) 157.3 TFLOP/s; "

@@ -830,7 +830,7 @@ using TapsPtr = const __attribute__((address_space(4))) CostTaps<HALF>*;
 template <int HALF, int RV, int TH, int RW, int TLO = 0, int THI = 2 * HALF, bool PAIR = false>
 __device__ __forceinline__ void vpass_filters(const float (&o)[RV + 2 * HALF],
                                               TapsPtr<HALF> taps, int f0, int f1,
-                                              float* out) {
+                                              float* out, int fslot = 0) {
 #pragma unroll 1
     for (int f = f0; f < f1; ++f) {
         float acc[RV];
@@ -846,7 +846,7 @@ __device__ __forceinline__ void vpass_filters(const float (&o)[RV + 2 * HALF],
             static_assert(RV % 2 == 0, "whole row pairs per item");
 #pragma unroll
             for (int y = 0; y < RV; y += 2)
-                *reinterpret_cast<float2*>(out + (f * (TH / 2) + y / 2) * RW * 2) =
+                *reinterpret_cast<float2*>(out + ((f - fslot) * (TH / 2) + y / 2) * RW * 2) =
                     make_float2(acc[y], acc[y + 1]);
         } else {
 #pragma unroll
@@ -1075,22 +1075,28 @@ template <int HALF, int RW, int TH>
 struct TileFill {
     static constexpr int TW = RW - 2 * HALF, RH = TH + 2 * HALF, DW = RW / 4;
     static constexpr int NFD = (RH * DW + 255) / 256, NFB = (RH * RW + 255) / 256;
+    static_assert((DW & (DW - 1)) == 0, "dword columns per row: a power of two");
     uint32_t lo[NFD], hi[NFD];  // interior tiles: aligned dword pairs of the index rows
+    uint32_t roff[NFD];         // their rows' byte offsets (alignment for commit)
     float4 ov;
     TileItem t;
     bool interior;
 
-    // interior index-row dword pair q of this thread: LDS dword e, source offset
+    // Byte offset of region row i in the palette's index image (reflection at the
+    // image edges, clamped to the rows held on this device).
     __device__ __forceinline__ static int row_base(const Geom& g, const TileItem& t, int i) {
         int gy = reflect_clamp(t.y0 - HALF + i, g.H);
         gy = min(max(gy, g.e0), g.e1 - 1);
-        // 32-bit offsets from the uniform palette base (the host keeps n_ext < 2^31):
-        // saddr + voffset loads, no 64-bit VGPR addresses
         return (gy - g.e0) * g.W + (t.x0 - HALF);
     }
 
     // Issue the loads; interior tiles only (edge tiles -- the image's first and
-    // last tile columns -- gather bytes with reflection at commit time).
+    // last tile columns -- gather bytes with reflection at commit time).  Tiles
+    // whose halo rows need neither reflection nor clamping (all but the image's
+    // and the shard's first and last tile rows) take row offsets from one
+    // multiply-add.  Loads are unconditional (rows clamped into the region) and
+    // use 32-bit unsigned offsets from the palette's base (saddr form); the host
+    // keeps a shard's index image below 2^31 bytes.
     __device__ __forceinline__ void issue(const CostArgs& a, const TileItem& ti, int tid) {
         static_assert(kMaxK == 256, "one opponent-table entry per thread");
         const Geom& g = a.g;
@@ -1099,17 +1105,18 @@ struct TileFill {
         ov = tid < a.K ? a.opp[(int64_t)t.p * kMaxK + tid] : make_float4(0.f, 0.f, 0.f, 0.f);
         interior = t.x0 - HALF >= 0 && t.x0 + TW + HALF <= g.W;
         if (interior) {
+            const int ytop = t.y0 - HALF;
+            const bool vfast = ytop >= 0 && ytop >= g.e0 && ytop + RH <= g.H && ytop + RH <= g.e1;
+            const int ubase = (ytop - g.e0) * g.W + (t.x0 - HALF);
 #pragma unroll
             for (int q = 0; q < NFD; ++q) {
-                const int e = tid + 256 * q;
-                lo[q] = hi[q] = 0u;
-                if (e < RH * DW) {
-                    const int base = row_base(g, t, e / DW);
-                    const uint32_t* src =
-                        reinterpret_cast<const uint32_t*>(idx + (base & ~3)) + e % DW;
-                    lo[q] = src[0];
-                    hi[q] = src[1];
-                }
+                const int e = min(tid + 256 * q, RH * DW - 1);
+                const int i = e / DW;
+                roff[q] = (uint32_t)(vfast ? ubase + i * g.W : row_base(g, t, i));
+                const uint32_t* src = reinterpret_cast<const uint32_t*>(
+                    idx + ((roff[q] & ~3u) + 4u * (uint32_t)(e % DW)));
+                lo[q] = src[0];
+                hi[q] = src[1];
             }
         }
     }
@@ -1124,23 +1131,19 @@ struct TileFill {
                 const int e = tid + 256 * q;
                 if (e < RH * DW)
                     reinterpret_cast<uint32_t*>(s_idx)[(e / DW) * (IDXP / 4) + e % DW] =
-                        __builtin_amdgcn_alignbyte(hi[q], lo[q],
-                                                   (uint32_t)(row_base(g, t, e / DW) & 3));
+                        __builtin_amdgcn_alignbyte(hi[q], lo[q], roff[q] & 3u);
             }
         } else {
             const uint8_t* idx = a.idx + (int64_t)t.p * g.idx_pitch;
             uint32_t b[NFB];
 #pragma unroll
             for (int q = 0; q < NFB; ++q) {  // all loads first: one round trip
-                const int e = tid + 256 * q;
-                b[q] = 0u;
-                if (e < RH * RW) {
-                    const int i = e / RW, j = e % RW;
-                    int gy = reflect_clamp(t.y0 - HALF + i, g.H);
-                    gy = min(max(gy, g.e0), g.e1 - 1);
-                    const int gx = reflect_clamp(t.x0 - HALF + j, g.W);
-                    b[q] = idx[(gy - g.e0) * g.W + gx];
-                }
+                const int e = min(tid + 256 * q, RH * RW - 1);
+                const int i = e / RW, j = e % RW;
+                int gy = reflect_clamp(t.y0 - HALF + i, g.H);
+                gy = min(max(gy, g.e0), g.e1 - 1);
+                const int gx = reflect_clamp(t.x0 - HALF + j, g.W);
+                b[q] = idx[(uint32_t)((gy - g.e0) * g.W + gx)];
             }
 #pragma unroll
             for (int q = 0; q < NFB; ++q) {
@@ -1579,12 +1582,12 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <int HALF, int TH, int RW, int HR, int TLO = 0, int THI = 2 * HALF>
 __device__ __forceinline__ void hpass_pair_filters(const f32x4* src, TapsPtr<HALF> taps, int f0,
-                                                   int f1, f32x2 (&acc)[HR]) {
+                                                   int f1, f32x2 (&acc)[HR], int fslot = 0) {
     constexpr int NIN = HR + 2 * HALF;  // window columns (float2 each)
     constexpr int NQ = (NIN + 1) / 2;   // ds_read_b128, two columns each
 #pragma unroll 1
     for (int f = f0; f < f1; ++f) {
-        const f32x4* row = src + f * (TH / 2) * RW / 2;
+        const f32x4* row = src + (f - fslot) * (TH / 2) * RW / 2;
         f32x4 v[NQ];
 #pragma unroll
         for (int q = 0; q < NQ; ++q) v[q] = row[q];
@@ -1655,15 +1658,16 @@ __global__ __launch_bounds__(256, 4) void cost_pair_kernel(CostArgs a, int P_) {
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
         const bool ok = has_item && gy0 + r < g.r1 && gx0 < g.W;
-        const int off = ok ? (gy0 + r - g.r0) * g.lab_pitch + gx0 : 0;
+        const uint32_t off = ok ? (uint32_t)((gy0 + r - g.r0) * g.lab_pitch + gx0) : 0u;
         const float* src3[3] = {a.labL, a.labA, a.labB};
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) {
+            const char* base = reinterpret_cast<const char*>(src3[ch]) + (off << 2);  // 32-bit bytes
             if constexpr (HR == 4) {
-                const float4 v = *reinterpret_cast<const float4*>(src3[ch] + off);
+                const float4 v = *reinterpret_cast<const float4*>(base);
                 labv[r][ch][0] = v.x; labv[r][ch][1] = v.y; labv[r][ch][2] = v.z; labv[r][ch][3] = v.w;
             } else {
-                const float2 v = *reinterpret_cast<const float2*>(src3[ch] + off);
+                const float2 v = *reinterpret_cast<const float2*>(base);
                 labv[r][ch][0] = v.x; labv[r][ch][1] = v.y;
             }
         }
@@ -1691,6 +1695,141 @@ __global__ __launch_bounds__(256, 4) void cost_pair_kernel(CostArgs a, int P_) {
     if (has_item) {
         f32x2 acc0[HR], acc1[HR], acc2[HR];
         hpass_pair_all<HALF, TH, RW, HR, TRIM>(&s_vq[(m * RW + HR * jr) / 2], taps, acc0, acc1, acc2);
+        float part = 0.f;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+#pragma unroll
+            for (int xo = 0; xo < HR; ++xo) {
+                const float3 l3 = opp2lab_fast(acc0[xo][r], acc1[xo][r], acc2[xo][r], a.m_lab);
+                const float e = delta_e<DE>(labv[r][0][xo], labv[r][1][xo], labv[r][2][xo], l3.x,
+                                            l3.y, l3.z);
+                part += (gy0 + r < g.r1 && gx0 + xo < g.W) ? e : 0.f;
+            }
+        }
+        sum = (double)part;
+    }
+    sum = wave_sum_to_lane63(sum);
+    if ((tid & 63) == 63) s_red[tid >> 6] = sum;
+    __syncthreads();
+    if (tid == 0)
+        a.partial[(int64_t)cur.p * a.ntiles + cur.tile] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+}
+
+
+// ----------------------------------------------------------------------------
+// cost_chan (cost_tile 6): cost_pair's tile and passes, run in two channel
+// groups -- channel 0's three filters (V then H), then channels 1-2's four --
+// so s_v holds at most four filter planes (16 KiB instead of 28) and each V
+// pass gathers only its group's channels from planar opponent tables (24 or 48
+// values live instead of 72).  23 KiB of LDS and <= 80 VGPRs: 6 workgroups per
+// CU instead of 4, more waves to cover the prologue's memory latency, for two
+// more barriers and the index bytes read twice.  LabRef is loaded after the
+// last vertical pass (loaded up front it spilled at 80 VGPRs).
+// ----------------------------------------------------------------------------
+template <int DE, bool TRIM>
+__global__ __launch_bounds__(256, 6) void cost_chan_kernel(CostArgs a, int P_) {
+    constexpr int HALF = 10, RW = 128, TH = 8, RV = 4, HR = 2, T2 = 2 * HALF;
+    constexpr int TW = RW - 2 * HALF, RH = TH + 2 * HALF, NIN = RV + 2 * HALF;
+    constexpr int NRUN = TW / HR, SLOTS = 64, NITEM = (TH / 2) * SLOTS;
+    constexpr int PLANE = (TH / 2) * RW / 2;  // f32x4 per filter plane (row pairs)
+    static_assert(NRUN <= SLOTS && NITEM <= 256, "H items");
+    __shared__ f32x4 s_vq[4 * PLANE];
+    __shared__ float s_ox[kMaxK];
+    __shared__ float2 s_oyz[kMaxK];
+    __shared__ __attribute__((aligned(16))) uint8_t s_idx[RH * RW];
+    __shared__ double s_red[4];
+    float* s_v = reinterpret_cast<float*>(s_vq);
+    const int tid = threadIdx.x;
+    const Geom& g = a.g;
+    const TileItem cur = tile_item<TW, TH>(a, xcd_remap(blockIdx.x, a.ntiles * P_), P_);
+    const TapsPtr<HALF> taps = (TapsPtr<HALF>)(uintptr_t)a.taps;
+
+    TileFill<HALF, RW, TH> fill;
+    fill.issue(a, cur, tid);
+    if (tid < a.K) {
+        s_ox[tid] = fill.ov.x;
+        s_oyz[tid] = make_float2(fill.ov.y, fill.ov.z);
+    }
+    fill.template commit_idx<RW>(a, s_idx, tid);
+    const int m = tid / SLOTS, jr = tid % SLOTS;
+    const bool has_item = tid < NITEM && jr < NRUN;
+    const int gy0 = cur.y0 + 2 * m, gx0 = cur.x0 + HR * jr;
+    __syncthreads();
+
+    const int c = tid % RW, gr = tid / RW;
+    float* vout = s_v + ((gr * RV / 2) * RW + c) * 2;
+    const f32x4* hsrc = &s_vq[(m * RW + HR * jr) / 2];
+    f32x2 acc0[HR], acc1[HR], acc2[HR];
+#pragma unroll
+    for (int xo = 0; xo < HR; ++xo) acc0[xo] = acc1[xo] = acc2[xo] = f32x2{0.f, 0.f};
+
+    // ---- group 0: channel 0 (filters 0-2 -> planes 0-2) ----
+    {
+        float o[NIN];
+#pragma unroll
+        for (int r = 0; r < NIN; ++r) o[r] = s_ox[s_idx[(gr * RV + r) * RW + c]];
+        if constexpr (TRIM) {
+            vpass_filters<HALF, RV, TH, RW, kTrimLo[0], kTrimHi[0], true>(o, taps, 0, 1, vout);
+            vpass_filters<HALF, RV, TH, RW, 0, T2, true>(o, taps, 1, 3, vout);
+        } else {
+            vpass_filters<HALF, RV, TH, RW, 0, T2, true>(o, taps, 0, 3, vout);
+        }
+    }
+    __syncthreads();
+    if (has_item) {
+        if constexpr (TRIM) {
+            hpass_pair_filters<HALF, TH, RW, HR, kTrimLo[0], kTrimHi[0]>(hsrc, taps, 0, 1, acc0);
+            hpass_pair_filters<HALF, TH, RW, HR, 0, T2>(hsrc, taps, 1, 3, acc0);
+        } else {
+            hpass_pair_filters<HALF, TH, RW, HR, 0, T2>(hsrc, taps, 0, 3, acc0);
+        }
+    }
+    __syncthreads();
+
+    // ---- group 1: channels 1 and 2 (filters 3-6 -> planes 0-3) ----
+    {
+        float o1[NIN], o2[NIN];
+#pragma unroll
+        for (int r = 0; r < NIN; ++r) {
+            const float2 v = s_oyz[s_idx[(gr * RV + r) * RW + c]];
+            o1[r] = v.x; o2[r] = v.y;
+        }
+        if constexpr (TRIM) {
+            vpass_filters<HALF, RV, TH, RW, kTrimLo[1], kTrimHi[1], true>(o1, taps, 3, 4, vout, 3);
+            vpass_filters<HALF, RV, TH, RW, 0, T2, true>(o1, taps, 4, 5, vout, 3);
+            vpass_filters<HALF, RV, TH, RW, kTrimLo[2], kTrimHi[2], true>(o2, taps, 5, 6, vout, 3);
+            vpass_filters<HALF, RV, TH, RW, 0, T2, true>(o2, taps, 6, 7, vout, 3);
+        } else {
+            vpass_filters<HALF, RV, TH, RW, 0, T2, true>(o1, taps, 3, 5, vout, 3);
+            vpass_filters<HALF, RV, TH, RW, 0, T2, true>(o2, taps, 5, 7, vout, 3);
+        }
+    }
+    float labv[2][3][HR];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const bool ok = has_item && gy0 + r < g.r1 && gx0 < g.W;
+        const uint32_t off = ok ? (uint32_t)((gy0 + r - g.r0) * g.lab_pitch + gx0) : 0u;
+        const float* src3[3] = {a.labL, a.labA, a.labB};
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+            const float2 v = *reinterpret_cast<const float2*>(
+                reinterpret_cast<const char*>(src3[ch]) + (off << 2));  // 32-bit byte offset
+            labv[r][ch][0] = v.x; labv[r][ch][1] = v.y;
+        }
+    }
+    __syncthreads();
+
+    double sum = 0.0;
+    if (has_item) {
+        if constexpr (TRIM) {
+            hpass_pair_filters<HALF, TH, RW, HR, kTrimLo[1], kTrimHi[1]>(hsrc, taps, 3, 4, acc1, 3);
+            hpass_pair_filters<HALF, TH, RW, HR, 0, T2>(hsrc, taps, 4, 5, acc1, 3);
+            hpass_pair_filters<HALF, TH, RW, HR, kTrimLo[2], kTrimHi[2]>(hsrc, taps, 5, 6, acc2, 3);
+            hpass_pair_filters<HALF, TH, RW, HR, 0, T2>(hsrc, taps, 6, 7, acc2, 3);
+        } else {
+            hpass_pair_filters<HALF, TH, RW, HR, 0, T2>(hsrc, taps, 3, 5, acc1, 3);
+            hpass_pair_filters<HALF, TH, RW, HR, 0, T2>(hsrc, taps, 5, 7, acc2, 3);
+        }
         float part = 0.f;
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
@@ -1876,7 +2015,7 @@ constexpr int kFastTW = kFastRW - 2 * kFastHalf;
 // tile rows of the fast path: cfg 0 = 16 (RV 8, 2 WG/CU); cfg 1 = 8 with the V
 // pass split by channel group (4 WG/CU); cfg 2 = 8 (RV 4, 4 WG/CU); cfg 3 = 8
 // with the V pass on the matrix cores
-int fast_tile_rows(int tile_cfg) { return tile_cfg == 0 ? kFastTH : 8; }  // cfg 4, 5: 8 rows
+int fast_tile_rows(int tile_cfg) { return tile_cfg == 0 ? kFastTH : 8; }  // cfg 1-6: 8 rows
 
 void fast_tile_dims(int W, int own_rows, int tile_cfg, int* tiles_x, int* ntiles) {
     const int th = fast_tile_rows(tile_cfg);
@@ -1939,6 +2078,12 @@ hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, int tile_cfg, boo
             else { if (trim) HQ_PAIR(1, true, 4); else HQ_PAIR(1, false, 4); }
         }
 #undef HQ_PAIR
+    } else if (tile_cfg == 6) {
+        const dim3 grid((unsigned)(a.ntiles * P));
+#define HQ_CHAN(DEV, TR) hipLaunchKernelGGL((cost_chan_kernel<DEV, TR>), grid, dim3(256), 0, s, a, P)
+        if (de == 0) { if (trim) HQ_CHAN(0, true); else HQ_CHAN(0, false); }
+        else { if (trim) HQ_CHAN(1, true); else HQ_CHAN(1, false); }
+#undef HQ_CHAN
     } else if (tile_cfg == 3) {
         if (trim) launch_tile_cfg<8, 8, 4, true, 2>(a, P, de, s);
         else launch_tile_cfg<8, 8, 4, false, 2>(a, P, de, s);

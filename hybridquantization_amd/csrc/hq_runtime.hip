@@ -115,9 +115,10 @@ struct hq_ctx {
     int assign_group = 4;  // palettes per pixel pass in the assign kernel (1, 2, 4)
     int assign_batch = 3;  // group 4: 3 = pipelined (assign_pipe_kernel), 1/2 = batched;
                            // group 1: 4/8 = batched, 0 = one-pixel prefetch
-    int tile_cfg = 4;      // cost tile: 0 = 16 rows, 1 = 8 rows + split V pass, 2 = 8 rows,
+    int tile_cfg = 6;      // cost tile: 0 = 16 rows, 1 = 8 rows + split V pass, 2 = 8 rows,
                            // 3 = 8 rows + V pass on the matrix cores, 4 = 8 rows + row-pair
-                           // H pass (2 columns per item), 5 = row-pair H (4 columns)
+                           // H pass (2 columns per item), 5 = row-pair H (4 columns),
+                           // 6 = row-pair in two channel groups (6 workgroups per CU; default)
     int trim = 1;          // skip taps < 1e-9 of the peak of the narrow k1 filters
     bool trim_ok = false;  // set by hq_set_filters (default 21-tap filter set)
 
@@ -290,9 +291,10 @@ int check_geom_args(hq_ctx* c, int w, int h, int r0, int r1) {
     if (w < c->half || h < c->half || w < 1 || h < 1)
         return fail(c, HQ_ERR_ARG, "image %dx%d smaller than the stencil half-width %d", w, h, c->half);
     if (r0 < 0 || r1 > h || r0 >= r1) return fail(c, HQ_ERR_ARG, "bad row range [%d,%d)", r0, r1);
-    // the cost kernels address a shard's index image and LabRef with 32-bit offsets
-    if ((int64_t)(w + 4) * (int64_t)(r1 - r0 + 2 * c->half) >= (int64_t)INT32_MAX)
-        return fail(c, HQ_ERR_UNSUPPORTED, "shard of %d x %d pixels exceeds 2^31; use more row blocks",
+    // the cost kernels address a shard's index image and its fp32 LabRef planes with
+    // 32-bit unsigned byte offsets: keep 4 bytes per (padded) pixel below 2^32
+    if ((int64_t)(w + 4) * (int64_t)(r1 - r0 + 2 * c->half) >= ((int64_t)1 << 30))
+        return fail(c, HQ_ERR_UNSUPPORTED, "shard of %d x %d pixels exceeds 2^30; use more row blocks",
                     w, r1 - r0);
     return HQ_OK;
 }
@@ -868,7 +870,7 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
     } else if (!std::strcmp(name, "trim")) {
         c->trim = value != 0;
     } else if (!std::strcmp(name, "cost_tile")) {
-        if (value < 0 || value > 5) return fail(c, HQ_ERR_ARG, "cost_tile in 0..5");
+        if (value < 0 || value > 6) return fail(c, HQ_ERR_ARG, "cost_tile in 0..6");
         c->tile_cfg = value;
     } else if (!std::strcmp(name, "assign_group")) {
         if (value != 1 && value != 2 && value != 4) return fail(c, HQ_ERR_ARG, "assign_group in {1,2,4}");

@@ -182,9 +182,10 @@ int hq_profile_reset(hq_ctx *ctx);
  *   "grid"         argmin pruning resolution G2: 0 = exhaustive, 16, 32 (default), 64
  *   "cost_variant" 0 = one tile per workgroup (default), 1 = generic two-pass
  *                  path (any filter length)
- *   "cost_tile"    8-row tiles at 4 WG/CU unless noted.  4 = horizontal pass over row
- *                  pairs (packed FMA across two rows, 2 columns per item; default);
- *                  5 = the same with 4 columns per item; 2 = row layout, 4-row vertical
+ *   "cost_tile"    8-row tiles at 4 WG/CU unless noted.  6 = horizontal pass over row
+ *                  pairs run in two opponent-channel groups (6 WG/CU; default); 4 = row
+ *                  pairs, all seven filters at once (packed FMA across two rows, 2 columns
+ *                  per item); 5 = the same with 4 columns per item; 2 = row layout, 4-row vertical
  *                  items; 1 = vertical pass split by opponent-channel group; 3 = vertical
  *                  pass on the matrix cores (split-f16 products); 0 = 16-row tiles (2 WG/CU)
  *   "trim"         1 = skip the narrow k1 filters' taps below 1e-9 of their peak

@@ -108,6 +108,47 @@ PATCHES["p_noloop"] = [(
                                                s_pal + pp * a.K, 0,
                                                a.lvl1 + (int64_t)pq * a.lvl1_pitch, G2, a.K);""",
     """            const int k = (int)((E[h][pp].x >> 8) & 0xff) + (in_[h] ? 0 : (int)s_pal[0].w);""")]
+# cost_pair: LabRef loaded after the vertical pass (register pressure during V)
+_LAB_BLOCK_START = "    float labv[2][3][HR];\n"
+_LAB_BLOCK_END = "    __syncthreads();\n\n    // ---- vertical pass (row-pair output layout)"
+
+
+def _lab_after_v(src):
+    i = src.index(_LAB_BLOCK_START)
+    j = src.index(_LAB_BLOCK_END, i)
+    block = src[i:j]
+    src = src[:i] + src[j:]
+    anchor = "    __syncthreads();\n\n    // ---- horizontal pass over the row pair + Lab + dE ----\n"
+    k = src.index(anchor)
+    return src[:k] + block + src[k:]
+
+
+TRANSFORMS = {"p_labafter": _lab_after_v}
+PATCHES["p_labafter"] = []
+# cost_pair: H-pass window reads at a wave-uniform address (LDS broadcast; results wrong)
+PATCHES["p_hbcast"] = [("        hpass_pair_all<HALF, TH, RW, HR, TRIM>(&s_vq[(m * RW + HR * jr) / 2], taps, acc0, acc1, acc2);",
+                        "        hpass_pair_all<HALF, TH, RW, HR, TRIM>(&s_vq[(tid >> 6) * 8], taps, acc0, acc1, acc2);")]
+# cost_pair: V-pass gathers at a wave-uniform table entry (results wrong)
+PATCHES["p_gbcast"] = [("            const float4 v = s_opp[s_idx[(gr * RV + r) * RW + c]];\n            o0[r] = v.x;",
+                        "            const float4 v = s_opp[(gr * RV + r + (s_idx[(gr * RV + r) * RW + c] >> 7)) & 255];\n            o0[r] = v.x;")]
+PATCHES["p_bothbcast"] = PATCHES["p_hbcast"] + PATCHES["p_gbcast"]
+# cost_chan: 5 workgroups per CU (96 VGPRs)
+PATCHES["c_occ5"] = [("__launch_bounds__(256, 6) void cost_chan_kernel", "__launch_bounds__(256, 5) void cost_chan_kernel")]
+
+
+def _chan_lab_late(src):
+    i = src.index("void cost_chan_kernel(")
+    a = src.index("    float labv[2][3][HR];\n", i)
+    b = src.index("    __syncthreads();\n", a)
+    block = src[a:b]
+    src = src[:a] + src[b:]
+    anchor = "    __syncthreads();\n\n    double sum = 0.0;\n"
+    k = src.index(anchor, i)
+    return src[:k] + block + src[k:]
+
+
+TRANSFORMS["c_lablate"] = _chan_lab_late
+PATCHES["c_lablate"] = []  # (now the product layout; kept for old revisions)
 PATCHES["skeleton"] = PATCHES["novfma"] + PATCHES["nohfma"] + PATCHES["nolab"]
 PATCHES["skeleton_bcast"] = PATCHES["skeleton"] + PATCHES["gatherbcast"]
 
@@ -128,6 +169,8 @@ def main():
             if old not in s:
                 sys.exit(f"{name}: patch anchor not found")
             s = s.replace(old, new)
+        if name in TRANSFORMS:
+            s = TRANSFORMS[name](s)
         s += APPEND.get(name, "")
         path = os.path.join(OUT, f"hq_kernels_{name}.hip")
         open(path, "w").write(s)

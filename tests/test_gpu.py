@@ -74,11 +74,11 @@ def test_labref_256_checksum(ip):
 # Candidate evaluation (IM:620-727): golden fixtures
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("grid", [64, 32, 16, 0])
-@pytest.mark.parametrize("variant", [(0, 4), (0, 5), (0, 2), (0, 0), (0, 1), (0, 3), (1, 0)])
+@pytest.mark.parametrize("variant", [(0, 4), (0, 5), (0, 6), (0, 2), (0, 0), (0, 1), (0, 3), (1, 0)])
 @pytest.mark.parametrize("name", ["case_64x48_k16", "case_97x53_k64"])
 def test_eval_golden(ip, name, grid, variant):
     """(cost_variant, cost_tile): 8-row tiles with the row-pair horizontal pass
-    (2 columns per item: default; 4 columns), row-layout 8-row tiles, 16-row
+    (2 columns per item: default; 4 columns; in two channel groups), row-layout 8-row tiles, 16-row
     tiles, the split vertical pass, the vertical pass on the matrix cores
     (split-f16 products), the generic two-pass path."""
     g, R, G, B = load_case(name)
@@ -315,7 +315,7 @@ def test_full_size_properties(gpu, filt):
     np.testing.assert_array_equal(m.getIndices(1), idx1)  # pruned == exhaustive argmin
     np.testing.assert_array_equal(c3, c1)
     m.setOption("grid", 64)
-    for variant, tile in ((1, 0), (0, 0), (0, 1), (0, 2), (0, 3), (0, 5)):
+    for variant, tile in ((1, 0), (0, 0), (0, 1), (0, 2), (0, 3), (0, 4), (0, 5)):
         m.setOption("cost_variant", variant)
         m.setOption("cost_tile", tile)
         c4 = m.computeQuantizationErrorPopulation(pals, 2.0)
