@@ -58,7 +58,7 @@ PATCHES["hsplit"] = [(
     ("            for (int xo = 0; xo < 4; ++xo) { if (t & 1) acc2[xo] = fmaf(in[xo + t], k, acc2[xo]); else acc[xo] = fmaf(in[xo + t], k, acc[xo]); }\n        }\n",
      "            for (int xo = 0; xo < 4; ++xo) { if (t & 1) acc2[xo] = fmaf(in[xo + t], k, acc2[xo]); else acc[xo] = fmaf(in[xo + t], k, acc[xo]); }\n        }\n#pragma unroll\n        for (int xo = 0; xo < 4; ++xo) acc[xo] += acc2[xo];\n")]
 # extra compiler flags per variant
-FLAGS = {"noslp": ["-fno-slp-vectorize"], "noslp_hsplit": ["-fno-slp-vectorize"]}
+FLAGS = {"noslp": [], "noslp_hsplit": []}  # -fno-slp-vectorize is now the product flag
 PATCHES["noslp"] = []
 PATCHES["noslp_hsplit"] = PATCHES["hsplit"]
 # per-phase s_memtime stamps of cost_tile_kernel, summed over waves (hq_debug_phases)
@@ -149,6 +149,9 @@ def _chan_lab_late(src):
 
 TRANSFORMS["c_lablate"] = _chan_lab_late
 PATCHES["c_lablate"] = []  # (now the product layout; kept for old revisions)
+# assign_pipe at 8 / 6 waves per SIMD (64 / 80 VGPRs)
+PATCHES["a_lb8"] = [("__launch_bounds__(256) void assign_pipe_kernel", "__launch_bounds__(256, 8) void assign_pipe_kernel")]
+PATCHES["a_lb6"] = [("__launch_bounds__(256) void assign_pipe_kernel", "__launch_bounds__(256, 6) void assign_pipe_kernel")]
 PATCHES["skeleton"] = PATCHES["novfma"] + PATCHES["nohfma"] + PATCHES["nolab"]
 PATCHES["skeleton_bcast"] = PATCHES["skeleton"] + PATCHES["gatherbcast"]
 
@@ -176,7 +179,7 @@ def main():
         open(path, "w").write(s)
         obj = os.path.join(OUT, f"hq_kernels_{name}.o")
         flags = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-I/opt/rocm/include",
-                 "-I" + CSRC, "-munsafe-fp-atomics", *FLAGS.get(name, [])]
+                 "-I" + CSRC, "-munsafe-fp-atomics", "-fno-slp-vectorize", *FLAGS.get(name, [])]
         subprocess.check_call(["/opt/rocm/bin/hipcc", *flags, "-c", path, "-o", obj])
         so = os.path.join(OUT, f"libhq_{name}.so")
         subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", obj,
