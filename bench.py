@@ -213,10 +213,13 @@ def main():
         "roofline": {"bound": "valu", "achieved": round(achieved_tf, 2), "peak": FP32_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4),
                      "traffic": traffic,
-                     "kernel": "cost_chan_kernel (cost_tile 6)", "kernel_avg_ms": round(cost_ms, 4),
+                     "kernel": "cost_mfma_kernel (cost_tile 7)", "kernel_avg_ms": round(cost_ms, 4),
                      "alg_flops_per_launch": alg_flops, "alg_bytes_per_launch": alg_bytes,
                      "hbm_GBs_alg": round(alg_bytes / (cost_ms * 1e-3) / 1e9, 1) if cost_ms > 0 else 0.0,
-                     "note": "f32 VALU kernel; peak = MI355X FP32 vector (= FP32 MFMA) 157.3 TFLOP/s; "
+                     "note": "fp32-accurate stencil: vertical taps on the matrix cores as split-f16 "
+                             "products (hi*hi+hi*lo+lo*hi, fp32 accumulate), horizontal taps, Lab and dE on "
+                             "FP32 VALU (the bound); achieved = the algorithm's fp32 flops / kernel time; "
+                             "peak = MI355X FP32 vector (= FP32 MFMA) 157.3 TFLOP/s; "
                              "traffic = HBM bytes/launch from the committed rocprofv3 FETCH_SIZE(x2)+WRITE_SIZE "
                              "passes (profiles/r01_hbm_traffic.json) when their config matches"},
         "metric_hbm_roofline_frac": round(value / eval_roof_mpx, 4),

@@ -82,6 +82,8 @@ struct CostArgs {
     const uint4* vfrag;     // cost_tile 3: [7][hi, lo][64 lanes] f16x8 B fragments of the
                             // vertical Toeplitz taps (build_vpass_fragments)
     const void* taps;       // CostTaps<10> in device memory (build_fast_taps)
+    const uint4* vfrag16;   // cost_tile 7: [trim][4 stacks][hi, lo][64 lanes] f16x8 A
+                            // fragments of the vertical taps (build_vpass_f16_stack_fragments)
     const float* labL;      // planar LabRef, owned rows, pitch lab_pitch
     const float* labA;
     const float* labB;

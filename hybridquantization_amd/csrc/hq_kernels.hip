@@ -1850,6 +1850,195 @@ __global__ __launch_bounds__(256, 6) void cost_chan_kernel(CostArgs a, int P_) {
         a.partial[(int64_t)cur.p * a.ntiles + cur.tile] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
 }
 
+
+// ----------------------------------------------------------------------------
+// cost_mfma (cost_tile 7): cost_chan with both vertical passes on the matrix
+// cores in split f16 (cf. vpass_mfma): per 16-column block and pair of filters
+// of one channel, one v_mfma_f32_16x16x32_f16 K-step covers the 28 region rows
+// (+4 zero-weight rows) as hi.hi + hi.lo + lo.hi (each product exact in the
+// fp32 accumulator; lo.lo ~2^-22 relative is dropped).  A = the stacked
+// Toeplitz taps (rows = filter pair x 8 output rows, x 2^16, split on the host:
+// build_vpass_f16_stack_fragments), B = the gathered opponent values (x 2^14),
+// read from per-channel (hi, lo) f16 dword tables that the prologue splits once
+// per tile, so the gathers need no conversion (one LDS read per value).  D (x 2^30, folded exactly into the
+// horizontal taps) holds 4 consecutive output rows of one filter and column per
+// lane: two row-pair stores.  Stacks (f0, f1), (f2, -), (f3, f4), (f5, f6); wave
+// w takes region columns 32w .. +31: 12 MFMAs per group and wave.
+// (An exact-fp32 version on v_mfma_f32_16x16x4_f32, 56 MFMAs per wave, was 9%
+// slower than the VALU pass: fp32 MFMA runs at the fp32 vector rate.)
+// ----------------------------------------------------------------------------
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+// D of one 16x16 stack block -> s_v row pairs: lane (c = l & 15, q = l >> 4)
+// holds rows 4(q & 1) .. +3 of the stack's filter q >> 1 at column c.
+__device__ __forceinline__ void store_vstack(float* s_v, const f32x4v& d, int plane_a, int plane_b,
+                                             int lk, int col) {
+    constexpr int RW = 128, PAIRS = 4;
+    const int plane = lk < 2 ? plane_a : plane_b;
+    if (plane < 0) return;
+    const int p0 = 2 * (lk & 1);
+    f32x2* v = reinterpret_cast<f32x2*>(s_v);
+    v[(plane * PAIRS + p0) * RW + col] = f32x2{d[0], d[1]};
+    v[(plane * PAIRS + p0 + 1) * RW + col] = f32x2{d[2], d[3]};
+}
+
+// B fragments of one 16-column block: region rows 8q .. 8q+7 (q = lane >> 4) of
+// column `col`.  Table entries hold (hi, lo) f16 of a channel in one dword
+// (split_f16), so one LDS read per value; v_perm packs the halves.
+__device__ __forceinline__ void pack_b(const uint32_t (&w)[8], f16x8& bh, f16x8& bl) {
+    u32x4 h, l;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        h[m] = __builtin_amdgcn_perm(w[2 * m + 1], w[2 * m], 0x05040100u);  // hi halves
+        l[m] = __builtin_amdgcn_perm(w[2 * m + 1], w[2 * m], 0x07060302u);  // lo halves
+    }
+    bh = __builtin_bit_cast(f16x8, h);
+    bl = __builtin_bit_cast(f16x8, l);
+}
+
+__device__ __forceinline__ f32x4v mfma3(const f16x8& ah, const f16x8& al, const f16x8& bh,
+                                        const f16x8& bl) {
+    f32x4v d = {0.f, 0.f, 0.f, 0.f};
+    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, d, 0, 0, 0);
+    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, d, 0, 0, 0);
+    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, d, 0, 0, 0);
+    return d;
+}
+
+template <int DE, bool TRIM>
+__global__ __launch_bounds__(256, 6) void cost_mfma_kernel(CostArgs a, int P_) {
+    constexpr int HALF = 10, RW = 128, TH = 8, HR = 2, T2 = 2 * HALF;
+    constexpr int TW = RW - 2 * HALF, RH = TH + 2 * HALF;
+    constexpr int NRUN = TW / HR, SLOTS = 64, NITEM = (TH / 2) * SLOTS;
+    constexpr int PLANE = (TH / 2) * RW / 2;  // f32x4 per filter plane (row pairs)
+    static_assert(NRUN <= SLOTS && NITEM <= 256 && RH <= 32, "tile");
+    __shared__ f32x4 s_vq[4 * PLANE];
+    __shared__ uint32_t s_ox[kMaxK];  // opponent x 2^14 as (hi, lo) f16 pairs: channel 0
+    __shared__ uint2 s_oyz[kMaxK];     // channels 1, 2
+    // 32 rows: the K = 32 step reads rows 28-31 too (zero taps; any finite index)
+    __shared__ __attribute__((aligned(16))) uint8_t s_idx[32 * RW];
+    __shared__ double s_red[4];
+    float* s_v = reinterpret_cast<float*>(s_vq);
+    const int tid = threadIdx.x;
+    const Geom& g = a.g;
+    const TileItem cur = tile_item<TW, TH>(a, xcd_remap(blockIdx.x, a.ntiles * P_), P_);
+    const TapsPtr<HALF> taps = (TapsPtr<HALF>)(uintptr_t)a.taps;  // H taps x 2^-30
+    const int lane = tid & 63, wv = tid >> 6, lc = lane & 15, lk = lane >> 4;
+    const uint4* frag = a.vfrag16 + (TRIM ? 4 * 2 * 64 : 0) + lane;  // [trim][stack][hi,lo][lane]
+
+    TileFill<HALF, RW, TH> fill;
+    fill.issue(a, cur, tid);
+    uint4 F0h = frag[(0 * 2 + 0) * 64], F0l = frag[(0 * 2 + 1) * 64];  // group 0 stacks
+    uint4 F1h = frag[(1 * 2 + 0) * 64], F1l = frag[(1 * 2 + 1) * 64];
+    // every entry (zeros for tid >= K): the zero-weight rows 28-31 gather arbitrary
+    // indices, and 0 x NaN would be NaN
+    s_ox[tid] = split_f16(fill.ov.x);
+    s_oyz[tid] = make_uint2(split_f16(fill.ov.y), split_f16(fill.ov.z));
+    fill.template commit_idx<RW>(a, s_idx, tid);
+    const int m = tid / SLOTS, jr = tid % SLOTS;
+    const bool has_item = tid < NITEM && jr < NRUN;
+    const int gy0 = cur.y0 + 2 * m, gx0 = cur.x0 + HR * jr;
+    __syncthreads();
+
+    const int col0 = 32 * wv + lc;
+    const f32x4* hsrc = &s_vq[(m * RW + HR * jr) / 2];
+    f32x2 acc0[HR], acc1[HR], acc2[HR];
+#pragma unroll
+    for (int xo = 0; xo < HR; ++xo) acc0[xo] = acc1[xo] = acc2[xo] = f32x2{0.f, 0.f};
+
+    // ---- group 0: channel 0 -> planes 0-2 ----
+    {
+        const f16x8 a0h = __builtin_bit_cast(f16x8, F0h), a0l = __builtin_bit_cast(f16x8, F0l);
+        const f16x8 a1h = __builtin_bit_cast(f16x8, F1h), a1l = __builtin_bit_cast(f16x8, F1l);
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            uint32_t w[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) w[j] = s_ox[s_idx[(8 * lk + j) * RW + col0 + 16 * bb]];
+            f16x8 bh, bl;
+            pack_b(w, bh, bl);
+            store_vstack(s_v, mfma3(a0h, a0l, bh, bl), 0, 1, lk, col0 + 16 * bb);
+            store_vstack(s_v, mfma3(a1h, a1l, bh, bl), 2, -1, lk, col0 + 16 * bb);
+        }
+    }
+    const uint4 F2h = frag[(2 * 2 + 0) * 64], F2l = frag[(2 * 2 + 1) * 64];  // group 1 stacks,
+    const uint4 F3h = frag[(3 * 2 + 0) * 64], F3l = frag[(3 * 2 + 1) * 64];  // in flight during H
+    __syncthreads();
+    if (has_item) {
+        if constexpr (TRIM) {
+            hpass_pair_filters<HALF, TH, RW, HR, kTrimLo[0], kTrimHi[0]>(hsrc, taps, 0, 1, acc0);
+            hpass_pair_filters<HALF, TH, RW, HR, 0, T2>(hsrc, taps, 1, 3, acc0);
+        } else {
+            hpass_pair_filters<HALF, TH, RW, HR, 0, T2>(hsrc, taps, 0, 3, acc0);
+        }
+    }
+    __syncthreads();
+
+    // ---- group 1: channels 1, 2 -> planes 0-3 ----
+    {
+        const f16x8 a2h = __builtin_bit_cast(f16x8, F2h), a2l = __builtin_bit_cast(f16x8, F2l);
+        const f16x8 a3h = __builtin_bit_cast(f16x8, F3h), a3l = __builtin_bit_cast(f16x8, F3l);
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            uint32_t wy[8], wz[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint2 e = s_oyz[s_idx[(8 * lk + j) * RW + col0 + 16 * bb]];
+                wy[j] = e.x; wz[j] = e.y;
+            }
+            f16x8 bh, bl;
+            pack_b(wy, bh, bl);
+            store_vstack(s_v, mfma3(a2h, a2l, bh, bl), 0, 1, lk, col0 + 16 * bb);
+            pack_b(wz, bh, bl);
+            store_vstack(s_v, mfma3(a3h, a3l, bh, bl), 2, 3, lk, col0 + 16 * bb);
+        }
+    }
+    float labv[2][3][HR];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const bool ok = has_item && gy0 + r < g.r1 && gx0 < g.W;
+        const uint32_t off = ok ? (uint32_t)((gy0 + r - g.r0) * g.lab_pitch + gx0) : 0u;
+        const float* src3[3] = {a.labL, a.labA, a.labB};
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+            const float2 v = *reinterpret_cast<const float2*>(
+                reinterpret_cast<const char*>(src3[ch]) + (off << 2));  // 32-bit byte offset
+            labv[r][ch][0] = v.x; labv[r][ch][1] = v.y;
+        }
+    }
+    __syncthreads();
+
+    double sum = 0.0;
+    if (has_item) {
+        if constexpr (TRIM) {
+            hpass_pair_filters<HALF, TH, RW, HR, kTrimLo[1], kTrimHi[1]>(hsrc, taps, 3, 4, acc1, 3);
+            hpass_pair_filters<HALF, TH, RW, HR, 0, T2>(hsrc, taps, 4, 5, acc1, 3);
+            hpass_pair_filters<HALF, TH, RW, HR, kTrimLo[2], kTrimHi[2]>(hsrc, taps, 5, 6, acc2, 3);
+            hpass_pair_filters<HALF, TH, RW, HR, 0, T2>(hsrc, taps, 6, 7, acc2, 3);
+        } else {
+            hpass_pair_filters<HALF, TH, RW, HR, 0, T2>(hsrc, taps, 3, 5, acc1, 3);
+            hpass_pair_filters<HALF, TH, RW, HR, 0, T2>(hsrc, taps, 5, 7, acc2, 3);
+        }
+        float part = 0.f;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+#pragma unroll
+            for (int xo = 0; xo < HR; ++xo) {
+                const float3 l3 = opp2lab_fast(acc0[xo][r], acc1[xo][r], acc2[xo][r], a.m_lab);
+                const float e = delta_e<DE>(labv[r][0][xo], labv[r][1][xo], labv[r][2][xo], l3.x,
+                                            l3.y, l3.z);
+                part += (gy0 + r < g.r1 && gx0 + xo < g.W) ? e : 0.f;
+            }
+        }
+        sum = (double)part;
+    }
+    sum = wave_sum_to_lane63(sum);
+    if ((tid & 63) == 63) s_red[tid >> 6] = sum;
+    __syncthreads();
+    if (tid == 0)
+        a.partial[(int64_t)cur.p * a.ntiles + cur.tile] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+}
+
 // ----------------------------------------------------------------------------
 // Launchers (host side of this translation unit)
 // ----------------------------------------------------------------------------
@@ -2007,6 +2196,39 @@ void build_vpass_fragments(const float* k1, const float* k2, const float* k3,
             }
 }
 
+// cost_tile 7: split-f16 A fragments of v_mfma_f32_16x16x32_f16 for the vertical
+// pass, [trim][stack][hi, lo][lane] x 8 halves (trim 0 = all 21 taps, 1 = the
+// narrow filters' significant windows).  Lane l holds A[i = l & 15][k = 8(l >> 4)
+// + j]: the tap (x 2^16) of filter stack[i >> 3] that multiplies region row k
+// into output row i & 7, i.e. tap d = k - (i & 7), zero outside [0, 20] (and
+// outside the window).
+size_t vpass_f16_stack_fragment_halves() { return 2 * 4 * 2 * 64 * 8; }
+
+void build_vpass_f16_stack_fragments(const float* k1, const float* k2, const float* k3,
+                                     const float* absk3, uint16_t* out) {
+    CostTaps<10> t;
+    make_taps10(k1, k2, k3, absk3, t);
+    const int stack[4][2] = {{0, 1}, {2, -1}, {3, 4}, {5, 6}};
+    for (int trim = 0; trim < 2; ++trim)
+        for (int st = 0; st < 4; ++st)
+            for (int l = 0; l < 64; ++l)
+                for (int j = 0; j < 8; ++j) {
+                    const int i = l & 15, k = 8 * (l >> 4) + j, r = i & 7, f = stack[st][i >> 3];
+                    const int d = k - r;
+                    float w = 0.f;
+                    if (f >= 0 && d >= 0 && d <= 20) {
+                        w = t.v[f][d];
+                        const int ch = f == 0 ? 0 : (f == 3 ? 1 : (f == 5 ? 2 : -1));
+                        if (trim && ch >= 0 && (d < kTrimLo[ch] || d > kTrimHi[ch])) w = 0.f;
+                    }
+                    w *= kVTapScale;
+                    const uint16_t hi = host_f16(w);
+                    const uint16_t lo = host_f16(w - host_f16_to_f32(hi));
+                    out[(((trim * 4 + st) * 2 + 0) * 64 + l) * 8 + j] = hi;
+                    out[(((trim * 4 + st) * 2 + 1) * 64 + l) * 8 + j] = lo;
+                }
+}
+
 // Tile geometry of the fast path (HALF = 10): RW = 128 region columns,
 // TW = 108 output columns, TH = 16 output rows, RV = 8 rows per V item.
 constexpr int kFastHalf = 10, kFastRW = 128, kFastTH = 16, kFastRV = 8;
@@ -2066,7 +2288,8 @@ void build_fast_taps(const float* k1, const float* k2, const float* k3, const fl
 hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, int tile_cfg, bool trim,
                             hipStream_t s) {
     CostArgs a = a0;
-    if (tile_cfg == 3) a.taps = static_cast<const char*>(a0.taps) + sizeof(CostTaps<10>);
+    if (tile_cfg == 3 || tile_cfg == 7)  // matrix-core V passes: outputs carry 2^30
+        a.taps = static_cast<const char*>(a0.taps) + sizeof(CostTaps<10>);
     if (tile_cfg == 4 || tile_cfg == 5) {
         const dim3 grid((unsigned)(a.ntiles * P));
 #define HQ_PAIR(DEV, TR, HRV) hipLaunchKernelGGL((cost_pair_kernel<DEV, TR, HRV>), grid, dim3(256), 0, s, a, P)
@@ -2084,6 +2307,12 @@ hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, int tile_cfg, boo
         if (de == 0) { if (trim) HQ_CHAN(0, true); else HQ_CHAN(0, false); }
         else { if (trim) HQ_CHAN(1, true); else HQ_CHAN(1, false); }
 #undef HQ_CHAN
+    } else if (tile_cfg == 7) {
+        const dim3 grid((unsigned)(a.ntiles * P));
+#define HQ_MFMA(DEV, TR) hipLaunchKernelGGL((cost_mfma_kernel<DEV, TR>), grid, dim3(256), 0, s, a, P)
+        if (de == 0) { if (trim) HQ_MFMA(0, true); else HQ_MFMA(0, false); }
+        else { if (trim) HQ_MFMA(1, true); else HQ_MFMA(1, false); }
+#undef HQ_MFMA
     } else if (tile_cfg == 3) {
         if (trim) launch_tile_cfg<8, 8, 4, true, 2>(a, P, de, s);
         else launch_tile_cfg<8, 8, 4, false, 2>(a, P, de, s);

@@ -182,8 +182,10 @@ int hq_profile_reset(hq_ctx *ctx);
  *   "grid"         argmin pruning resolution G2: 0 = exhaustive, 16, 32 (default), 64
  *   "cost_variant" 0 = one tile per workgroup (default), 1 = generic two-pass
  *                  path (any filter length)
- *   "cost_tile"    8-row tiles at 4 WG/CU unless noted.  6 = horizontal pass over row
- *                  pairs run in two opponent-channel groups (6 WG/CU; default); 4 = row
+ *   "cost_tile"    8-row tiles at 4 WG/CU unless noted.  7 = vertical passes on the
+ *                  matrix cores (split-f16 products, stacked filter pairs), horizontal
+ *                  pass over row pairs on VALU, in two opponent-channel groups (6 WG/CU;
+ *                  default); 6 = the same with the vertical passes on VALU; 4 = row
  *                  pairs, all seven filters at once (packed FMA across two rows, 2 columns
  *                  per item); 5 = the same with 4 columns per item; 2 = row layout, 4-row vertical
  *                  items; 1 = vertical pass split by opponent-channel group; 3 = vertical

@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--evals", type=int, default=10)
     ap.add_argument("--grid", type=int, default=32)
     ap.add_argument("--variant", type=int, default=0)
-    ap.add_argument("--tile", type=int, default=6)
+    ap.add_argument("--tile", type=int, default=7)
     ap.add_argument("--rep", type=int, default=1)
     ap.add_argument("--trim", type=int, default=1)
     ap.add_argument("--group", type=int, default=4)
