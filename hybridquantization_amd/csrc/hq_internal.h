@@ -82,8 +82,10 @@ struct CostArgs {
     const uint4* vfrag;     // cost_tile 3: [7][hi, lo][64 lanes] f16x8 B fragments of the
                             // vertical Toeplitz taps (build_vpass_fragments)
     const void* taps;       // CostTaps<10> in device memory (build_fast_taps)
-    const uint4* vfrag16;   // cost_tile 7: [trim][4 stacks][hi, lo][64 lanes] f16x8 A
+    const uint4* vfrag16;   // cost_tile 7, 8: [trim][4 stacks][hi, lo][64 lanes] f16x8 A
                             // fragments of the vertical taps (build_vpass_f16_stack_fragments)
+    const uint4* hfrag16;   // cost_tile 8: [trim][7 filters][hi, lo][64 lanes] f16x8 A
+                            // fragments of the horizontal taps (build_hpass_f16_fragments)
     const float* labL;      // planar LabRef, owned rows, pitch lab_pitch
     const float* labA;
     const float* labB;

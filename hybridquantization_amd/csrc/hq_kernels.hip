@@ -2039,6 +2039,169 @@ __global__ __launch_bounds__(256, 6) void cost_mfma_kernel(CostArgs a, int P_) {
         a.partial[(int64_t)cur.p * a.ntiles + cur.tile] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
 }
 
+
+// ----------------------------------------------------------------------------
+// cost_mm (cost_tile 8): both stencil passes on the matrix cores in split f16,
+// Lab / dE on VALU.  Tile = 8 rows x 96 output columns (8 blocks of 12), region
+// 28 (+4 zero-weight) rows x 128 columns, two opponent-channel groups as in
+// cost_mfma.
+//  - vertical pass: as cost_mfma (stacked filter pairs, one K = 32 step per
+//    16-column block), but D (x 2^30) is rescaled to x 2^12 and stored as f16
+//    hi / lo (hi = f16(v), lo = f16(v - hi)) in row-major planes;
+//  - horizontal pass: per 12-column output block, the 32 input columns of its
+//    window are one K = 32 step: D[x][n] += Htap[x][k] * V[row][12b + k] with
+//    n = (block of the wave's pair, row), hi.hi + hi.lo + lo.hi per filter, the
+//    filters of one channel accumulated in one D (x 2^28, folded into the
+//    Opp -> XYZ rows by the host, exactly);
+//  - Lab / dE: lane (n, q) holds output columns 12b + 4q .. +3 of one row
+//    (q = 3 is padding), LabRef as float4 loads.
+// LDS per tile: the H-pass B fragments are 2 x 16 B per lane and filter
+// (cost_pair's horizontal windows were 1.2 KB per item), the V-pass stores one
+// f16 per value and half.
+// ----------------------------------------------------------------------------
+constexpr int kMMTW = 96;                          // output columns per tile
+constexpr float kVToH = 1.0f / 262144.0f;          // 2^-18: V-pass D (x 2^30) -> x 2^12
+constexpr float kHTapScale = 65536.0f;             // 2^16
+constexpr float kHOutScale = 1.0f / 268435456.0f;  // 2^-28 (into m_lab)
+
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+// D of one V stack block -> f16 hi / lo rows of the planes: lane (c = l & 15,
+// q = l >> 4) holds rows 4(q & 1) .. +3 of filter q >> 1 at column `col`.
+template <int RS>
+__device__ __forceinline__ void store_vstack_f16(_Float16* s_vh, const f32x4v& d, int plane_a,
+                                                 int plane_b, int lk, int col) {
+    constexpr int RW = 128;
+    const int plane = lk < 2 ? plane_a : plane_b;
+    if (plane < 0) return;
+    _Float16* base = s_vh + (plane * 8 + 4 * (lk & 1)) * RS + col;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        const float x = d[v] * kVToH;
+        const _Float16 hi = (_Float16)x;
+        base[v * RS] = hi;
+        base[v * RS + RW] = (_Float16)(x - (float)hi);
+    }
+}
+
+template <int DE, bool TRIM>
+__global__ __launch_bounds__(256, 6) void cost_mm_kernel(CostArgs a, int P_) {
+    constexpr int HALF = 10, RW = 128, TH = 8, TW = kMMTW, RH = TH + 2 * HALF;
+    constexpr int RS = 2 * RW + 16;  // halves per plane row: hi row, lo row, 32 B pad
+    static_assert(RH <= 32 && TW == 8 * 12 && 12 * 7 + 32 <= RW, "tile");
+    __shared__ __attribute__((aligned(16))) _Float16 s_vh[4 * TH * RS];
+    __shared__ uint32_t s_ox[kMaxK];
+    __shared__ uint2 s_oyz[kMaxK];
+    __shared__ __attribute__((aligned(16))) uint8_t s_idx[32 * RW];
+    __shared__ double s_red[4];
+    const int tid = threadIdx.x;
+    const Geom& g = a.g;
+    const TileItem cur = tile_item<TW, TH>(a, xcd_remap(blockIdx.x, a.ntiles * P_), P_);
+    const int lane = tid & 63, wv = tid >> 6, lc = lane & 15, lk = lane >> 4;
+    const uint4* vfrag = a.vfrag16 + (TRIM ? 4 * 2 * 64 : 0) + lane;  // [trim][stack][hi,lo][lane]
+    const uint4* hfrag = a.hfrag16 + (TRIM ? 7 * 2 * 64 : 0) + lane;  // [trim][filter][hi,lo][lane]
+
+    TileFill<HALF, RW, TH> fill;  // region x0 - 10 .. x0 + 117 (stride 96)
+    fill.issue(a, cur, tid);
+    const uint4 F0h = vfrag[0 * 64], F0l = vfrag[1 * 64], F1h = vfrag[2 * 64], F1l = vfrag[3 * 64];
+    s_ox[tid] = split_f16(fill.ov.x);  // every entry (zeros past K): rows 28-31 gather any index
+    s_oyz[tid] = make_uint2(split_f16(fill.ov.y), split_f16(fill.ov.z));
+    fill.template commit_idx<RW>(a, s_idx, tid);
+    __syncthreads();
+
+    const int col0 = 32 * wv + lc;  // V pass: region columns of this wave's two 16-blocks
+    // H pass: lane (n = lc, q = lk): output block ob = 2 wv + (n >> 3), row hr = n & 7,
+    // B = input columns 12 ob + 8q .. +7 of row hr
+    const int ob = 2 * wv + (lc >> 3), hr = lc & 7;
+    const _Float16* hb = s_vh + hr * RS + 12 * ob + 8 * lk;
+    f32x4v D0 = {0.f, 0.f, 0.f, 0.f}, D1 = D0, D2 = D0;
+
+    auto hpass = [&](int f, int plane, f32x4v& D) {
+        const f16x8 ah = __builtin_bit_cast(f16x8, hfrag[(2 * f) * 64]);
+        const f16x8 al = __builtin_bit_cast(f16x8, hfrag[(2 * f + 1) * 64]);
+        const _Float16* p = hb + plane * 8 * RS;
+        const f16x4 h0 = *reinterpret_cast<const f16x4*>(p), h1 = *reinterpret_cast<const f16x4*>(p + 4);
+        const f16x4 l0 = *reinterpret_cast<const f16x4*>(p + RW),
+                    l1 = *reinterpret_cast<const f16x4*>(p + RW + 4);
+        const f16x8 bh = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+        const f16x8 bl = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+        D = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, D, 0, 0, 0);
+        D = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, D, 0, 0, 0);
+        D = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, D, 0, 0, 0);
+    };
+
+    // ---- group 0: channel 0 ----
+    {
+        const f16x8 a0h = __builtin_bit_cast(f16x8, F0h), a0l = __builtin_bit_cast(f16x8, F0l);
+        const f16x8 a1h = __builtin_bit_cast(f16x8, F1h), a1l = __builtin_bit_cast(f16x8, F1l);
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            uint32_t w[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) w[j] = s_ox[s_idx[(8 * lk + j) * RW + col0 + 16 * bb]];
+            f16x8 bh, bl;
+            pack_b(w, bh, bl);
+            store_vstack_f16<RS>(s_vh, mfma3(a0h, a0l, bh, bl), 0, 1, lk, col0 + 16 * bb);
+            store_vstack_f16<RS>(s_vh, mfma3(a1h, a1l, bh, bl), 2, -1, lk, col0 + 16 * bb);
+        }
+    }
+    const uint4 F2h = vfrag[4 * 64], F2l = vfrag[5 * 64], F3h = vfrag[6 * 64], F3l = vfrag[7 * 64];
+    __syncthreads();
+    hpass(0, 0, D0);
+    hpass(1, 1, D0);
+    hpass(2, 2, D0);
+    __syncthreads();
+
+    // ---- group 1: channels 1, 2 ----
+    {
+        const f16x8 a2h = __builtin_bit_cast(f16x8, F2h), a2l = __builtin_bit_cast(f16x8, F2l);
+        const f16x8 a3h = __builtin_bit_cast(f16x8, F3h), a3l = __builtin_bit_cast(f16x8, F3l);
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            uint32_t wy[8], wz[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint2 e = s_oyz[s_idx[(8 * lk + j) * RW + col0 + 16 * bb]];
+                wy[j] = e.x; wz[j] = e.y;
+            }
+            f16x8 bh, bl;
+            pack_b(wy, bh, bl);
+            store_vstack_f16<RS>(s_vh, mfma3(a2h, a2l, bh, bl), 0, 1, lk, col0 + 16 * bb);
+            pack_b(wz, bh, bl);
+            store_vstack_f16<RS>(s_vh, mfma3(a3h, a3l, bh, bl), 2, 3, lk, col0 + 16 * bb);
+        }
+    }
+    // LabRef of this lane's 4 outputs (row hr, columns 12 ob + 4 lk .. +3), in flight
+    const int gy = cur.y0 + hr, gx = cur.x0 + 12 * ob + 4 * lk;
+    const bool lab_ok = lk < 3 && gy < g.r1 && gx < g.W;
+    const uint32_t loff = lab_ok ? (uint32_t)((gy - g.r0) * g.lab_pitch + gx) : 0u;
+    const float4 Lr = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(a.labL) + (loff << 2));
+    const float4 Ar = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(a.labA) + (loff << 2));
+    const float4 Br = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(a.labB) + (loff << 2));
+    __syncthreads();
+    hpass(3, 0, D1);
+    hpass(4, 1, D1);
+    hpass(5, 2, D2);
+    hpass(6, 3, D2);
+
+    float part = 0.f;
+    if (lk < 3) {
+        const float lr[4] = {Lr.x, Lr.y, Lr.z, Lr.w}, ar[4] = {Ar.x, Ar.y, Ar.z, Ar.w},
+                    br[4] = {Br.x, Br.y, Br.z, Br.w};
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const float3 l3 = opp2lab_fast(D0[v], D1[v], D2[v], a.m_lab);
+            const float e = delta_e<DE>(lr[v], ar[v], br[v], l3.x, l3.y, l3.z);
+            part += (gy < g.r1 && gx + v < g.W) ? e : 0.f;
+        }
+    }
+    double sum = wave_sum_to_lane63((double)part);
+    if ((tid & 63) == 63) s_red[tid >> 6] = sum;
+    __syncthreads();
+    if (tid == 0)
+        a.partial[(int64_t)cur.p * a.ntiles + cur.tile] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+}
+
 // ----------------------------------------------------------------------------
 // Launchers (host side of this translation unit)
 // ----------------------------------------------------------------------------
@@ -2229,6 +2392,36 @@ void build_vpass_f16_stack_fragments(const float* k1, const float* k2, const flo
                 }
 }
 
+// cost_tile 8: split-f16 A fragments of the horizontal taps, [trim][filter][hi, lo]
+// [lane] x 8 halves.  Lane l holds A[x = l & 15][k = 8(l >> 4) + j]: the tap (x 2^16)
+// that multiplies window column k into output column x of a 12-column block, i.e.
+// tap d = k - x, zero outside [0, 20], for x >= 12 (padding rows) and outside the
+// narrow filters' windows when trimmed.
+size_t hpass_f16_fragment_halves() { return 2 * 7 * 2 * 64 * 8; }
+
+void build_hpass_f16_fragments(const float* k1, const float* k2, const float* k3,
+                               const float* absk3, uint16_t* out) {
+    CostTaps<10> t;
+    make_taps10(k1, k2, k3, absk3, t);
+    for (int trim = 0; trim < 2; ++trim)
+        for (int f = 0; f < kNumFilt; ++f)
+            for (int l = 0; l < 64; ++l)
+                for (int j = 0; j < 8; ++j) {
+                    const int x = l & 15, k = 8 * (l >> 4) + j, d = k - x;
+                    float w = 0.f;
+                    if (x < 12 && d >= 0 && d <= 20) {
+                        w = t.h[f][d];
+                        const int ch = f == 0 ? 0 : (f == 3 ? 1 : (f == 5 ? 2 : -1));
+                        if (trim && ch >= 0 && (d < kTrimLo[ch] || d > kTrimHi[ch])) w = 0.f;
+                    }
+                    w *= kHTapScale;
+                    const uint16_t hi = host_f16(w);
+                    const uint16_t lo = host_f16(w - host_f16_to_f32(hi));
+                    out[(((trim * 7 + f) * 2 + 0) * 64 + l) * 8 + j] = hi;
+                    out[(((trim * 7 + f) * 2 + 1) * 64 + l) * 8 + j] = lo;
+                }
+}
+
 // Tile geometry of the fast path (HALF = 10): RW = 128 region columns,
 // TW = 108 output columns, TH = 16 output rows, RV = 8 rows per V item.
 constexpr int kFastHalf = 10, kFastRW = 128, kFastTH = 16, kFastRV = 8;
@@ -2237,11 +2430,12 @@ constexpr int kFastTW = kFastRW - 2 * kFastHalf;
 // tile rows of the fast path: cfg 0 = 16 (RV 8, 2 WG/CU); cfg 1 = 8 with the V
 // pass split by channel group (4 WG/CU); cfg 2 = 8 (RV 4, 4 WG/CU); cfg 3 = 8
 // with the V pass on the matrix cores
-int fast_tile_rows(int tile_cfg) { return tile_cfg == 0 ? kFastTH : 8; }  // cfg 1-6: 8 rows
+int fast_tile_rows(int tile_cfg) { return tile_cfg == 0 ? kFastTH : 8; }  // cfg 1-8: 8 rows
 
 void fast_tile_dims(int W, int own_rows, int tile_cfg, int* tiles_x, int* ntiles) {
     const int th = fast_tile_rows(tile_cfg);
-    *tiles_x = (W + kFastTW - 1) / kFastTW;
+    const int tw = tile_cfg == 8 ? kMMTW : kFastTW;
+    *tiles_x = (W + tw - 1) / tw;
     *ntiles = *tiles_x * ((own_rows + th - 1) / th);
 }
 
@@ -2313,6 +2507,13 @@ hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, int tile_cfg, boo
         if (de == 0) { if (trim) HQ_MFMA(0, true); else HQ_MFMA(0, false); }
         else { if (trim) HQ_MFMA(1, true); else HQ_MFMA(1, false); }
 #undef HQ_MFMA
+    } else if (tile_cfg == 8) {
+        for (int i = 0; i < 9; ++i) a.m_lab[i] *= kHOutScale;  // H outputs carry 2^28 (exact)
+        const dim3 grid((unsigned)(a.ntiles * P));
+#define HQ_MM(DEV, TR) hipLaunchKernelGGL((cost_mm_kernel<DEV, TR>), grid, dim3(256), 0, s, a, P)
+        if (de == 0) { if (trim) HQ_MM(0, true); else HQ_MM(0, false); }
+        else { if (trim) HQ_MM(1, true); else HQ_MM(1, false); }
+#undef HQ_MM
     } else if (tile_cfg == 3) {
         if (trim) launch_tile_cfg<8, 8, 4, true, 2>(a, P, de, s);
         else launch_tile_cfg<8, 8, 4, false, 2>(a, P, de, s);

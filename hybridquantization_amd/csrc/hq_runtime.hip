@@ -28,6 +28,9 @@ void build_vpass_fragments(const float* k1, const float* k2, const float* k3,
                            const float* absk3, uint16_t* out);
 hipError_t launch_cost_fast(const CostArgs&, int P, int de, int tile_cfg, bool trim, hipStream_t);
 size_t vpass_f16_stack_fragment_halves();
+size_t hpass_f16_fragment_halves();
+void build_hpass_f16_fragments(const float* k1, const float* k2, const float* k3,
+                               const float* absk3, uint16_t* out);
 void build_vpass_f16_stack_fragments(const float* k1, const float* k2, const float* k3,
                                      const float* absk3, uint16_t* out);
 size_t fast_taps_bytes();
@@ -93,7 +96,8 @@ struct hq_ctx {
     DevBuf d_k1, d_k2, d_k3, d_absk3;
     DevBuf d_vfrag;  // cost_tile 3: Toeplitz B fragments [7][2][64] x 16 B (21-tap filters)
     DevBuf d_taps;   // fast path taps, build_fast_taps (21-tap filters)
-    DevBuf d_vfrag16;  // cost_tile 7: split-f16 MFMA A fragments of the stacked vertical taps
+    DevBuf d_vfrag16;  // cost_tile 7, 8: split-f16 MFMA A fragments of the stacked vertical taps
+    DevBuf d_hfrag16;  // cost_tile 8: split-f16 MFMA A fragments of the horizontal taps
 
     // image
     bool have_image = false;
@@ -123,7 +127,8 @@ struct hq_ctx {
                            // 3 = 8 rows + V pass on the matrix cores, 4 = 8 rows + row-pair
                            // H pass (2 columns per item), 5 = row-pair H (4 columns),
                            // 6 = row-pair in two channel groups (6 workgroups per CU),
-                           // 7 = 6 with the vertical passes on the matrix cores (split f16; default)
+                           // 7 = 6 with the vertical passes on the matrix cores (split f16; default),
+                           // 8 = both passes on the matrix cores (96-column tiles)
     int trim = 1;          // skip taps < 1e-9 of the peak of the narrow k1 filters
     bool trim_ok = false;  // set by hq_set_filters (default 21-tap filter set)
 
@@ -378,6 +383,7 @@ int enqueue_eval(hq_ctx* c, int P, int K) {
         ca.opp = c->d_opp.as<float4>();
         ca.vfrag = c->d_vfrag.as<uint4>();
         ca.vfrag16 = c->d_vfrag16.as<uint4>();
+        ca.hfrag16 = c->d_hfrag16.as<uint4>();
         ca.labL = c->d_labL.as<float>();
         ca.labA = c->d_labA.as<float>();
         ca.labB = c->d_labB.as<float>();
@@ -518,7 +524,7 @@ void hq_destroy(hq_ctx* c) {
                       &c->d_labL, &c->d_labA, &c->d_labB, &c->d_pal_in, &c->d_pal, &c->d_opp,
                       &c->d_dup, &c->d_pflags, &c->d_lvl1, &c->d_lvl2, &c->d_idx,
                       &c->d_used_mask, &c->d_partial, &c->d_out, &c->d_gen_t, &c->d_vfrag,
-                      &c->d_taps, &c->d_vfrag16})
+                      &c->d_taps, &c->d_vfrag16, &c->d_hfrag16})
         b->release();
     if (c->h_pal) (void)hipHostFree(c->h_pal);
     if (c->h_out) (void)hipHostFree(c->h_out);
@@ -564,6 +570,11 @@ int hq_set_filters(hq_ctx* c, int taps, const float* k1, const float* k2, const 
         build_vpass_f16_stack_fragments(k1, k2, k3, absk3, f16s.data());
         HIP_TRY(c, c->d_vfrag16.ensure(f16s.size() * sizeof(uint16_t)));
         HIP_TRY(c, hipMemcpy(c->d_vfrag16.p, f16s.data(), f16s.size() * sizeof(uint16_t),
+                             hipMemcpyHostToDevice));
+        std::vector<uint16_t> h16s(hpass_f16_fragment_halves());
+        build_hpass_f16_fragments(k1, k2, k3, absk3, h16s.data());
+        HIP_TRY(c, c->d_hfrag16.ensure(h16s.size() * sizeof(uint16_t)));
+        HIP_TRY(c, hipMemcpy(c->d_hfrag16.p, h16s.data(), h16s.size() * sizeof(uint16_t),
                              hipMemcpyHostToDevice));
         std::vector<char> tb(fast_taps_bytes());
         build_fast_taps(k1, k2, k3, absk3, tb.data());
@@ -881,7 +892,7 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
     } else if (!std::strcmp(name, "trim")) {
         c->trim = value != 0;
     } else if (!std::strcmp(name, "cost_tile")) {
-        if (value < 0 || value > 7) return fail(c, HQ_ERR_ARG, "cost_tile in 0..7");
+        if (value < 0 || value > 8) return fail(c, HQ_ERR_ARG, "cost_tile in 0..8");
         c->tile_cfg = value;
     } else if (!std::strcmp(name, "assign_group")) {
         if (value != 1 && value != 2 && value != 4) return fail(c, HQ_ERR_ARG, "assign_group in {1,2,4}");

@@ -152,6 +152,13 @@ PATCHES["c_lablate"] = []  # (now the product layout; kept for old revisions)
 # assign_pipe at 8 / 6 waves per SIMD (64 / 80 VGPRs)
 PATCHES["a_lb8"] = [("__launch_bounds__(256) void assign_pipe_kernel", "__launch_bounds__(256, 8) void assign_pipe_kernel")]
 PATCHES["a_lb6"] = [("__launch_bounds__(256) void assign_pipe_kernel", "__launch_bounds__(256, 6) void assign_pipe_kernel")]
+# cost_mfma / cost_mm: MFMA tap fragments loaded at a wave-uniform address (results wrong)
+PATCHES["m_fragbcast"] = [("    const uint4* frag = a.vfrag16 + (TRIM ? 4 * 2 * 64 : 0) + lane;  // [trim][stack][hi,lo][lane]",
+                           "    const uint4* frag = a.vfrag16 + (TRIM ? 4 * 2 * 64 : 0) + (lane >> 6);")]
+PATCHES["mm_fragbcast"] = [("    const uint4* vfrag = a.vfrag16 + (TRIM ? 4 * 2 * 64 : 0) + lane;  // [trim][stack][hi,lo][lane]",
+                            "    const uint4* vfrag = a.vfrag16 + (TRIM ? 4 * 2 * 64 : 0) + (lane >> 6);"),
+                           ("    const uint4* hfrag = a.hfrag16 + (TRIM ? 7 * 2 * 64 : 0) + lane;  // [trim][filter][hi,lo][lane]",
+                            "    const uint4* hfrag = a.hfrag16 + (TRIM ? 7 * 2 * 64 : 0) + (lane >> 6);")]
 PATCHES["skeleton"] = PATCHES["novfma"] + PATCHES["nohfma"] + PATCHES["nolab"]
 PATCHES["skeleton_bcast"] = PATCHES["skeleton"] + PATCHES["gatherbcast"]
 

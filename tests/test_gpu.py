@@ -74,7 +74,7 @@ def test_labref_256_checksum(ip):
 # Candidate evaluation (IM:620-727): golden fixtures
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("grid", [64, 32, 16, 0])
-@pytest.mark.parametrize("variant", [(0, 6), (0, 7), (0, 4), (0, 5), (0, 2), (0, 0), (0, 1), (0, 3), (1, 0)])
+@pytest.mark.parametrize("variant", [(0, 7), (0, 8), (0, 6), (0, 4), (0, 5), (0, 2), (0, 0), (0, 1), (0, 3), (1, 0)])
 @pytest.mark.parametrize("name", ["case_64x48_k16", "case_97x53_k64"])
 def test_eval_golden(ip, name, grid, variant):
     """(cost_variant, cost_tile): 8-row tiles with the row-pair horizontal pass
@@ -125,10 +125,11 @@ def test_eval_config2_1024_k64(ip, filt):
 
 @pytest.mark.parametrize("de", [hq.deltaETypes.CIE76, hq.deltaETypes.CIE94])
 @pytest.mark.parametrize("trim", [1, 0])
-def test_mfma_vertical_pass_matches_valu(gpu, de, trim):
+def test_mfma_passes_match_valu(gpu, de, trim):
     """cost_tile 7 runs the vertical taps on the matrix cores in split f16
-    (hi.hi + hi.lo + lo.hi, ~2^-22 relative per product dropped); its costs agree
-    with cost_tile 6's fp32 VALU pass to 1e-6 relative (the bar is 1e-4)."""
+    (hi.hi + hi.lo + lo.hi, ~2^-22 relative per product dropped), cost_tile 8 both
+    passes; their costs agree with cost_tile 6's fp32 VALU passes to 1e-6 relative
+    (the bar is 1e-4)."""
     w, h = 300, 77  # interior, edge and partial tiles
     R, G, B = o.synthetic_image(w, h, seed=5)
     m = hq.ImageManipulation(de, device=gpu)
@@ -137,11 +138,12 @@ def test_mfma_vertical_pass_matches_valu(gpu, de, trim):
     pals = [o.synthetic_palette(K, 7 + K) for K in (16, 64, 256)]
     m.setOption("trim", trim)
     out = {}
-    for tile in (6, 7):
+    for tile in (6, 7, 8):
         m.setOption("cost_tile", tile)
         out[tile] = np.array([m.computeQuantizationErrorPopulation([p.reshape(-1)], 2.0)[0]
                               for p in pals])
     np.testing.assert_allclose(out[7], out[6], rtol=1e-6)
+    np.testing.assert_allclose(out[8], out[6], rtol=1e-6)
     m.close()
 
 
@@ -338,7 +340,7 @@ def test_full_size_properties(gpu, filt):
     np.testing.assert_array_equal(m.getIndices(1), idx1)  # pruned == exhaustive argmin
     np.testing.assert_array_equal(c3, c1)
     m.setOption("grid", 64)
-    for variant, tile in ((1, 0), (0, 0), (0, 1), (0, 2), (0, 3), (0, 4), (0, 5), (0, 6)):
+    for variant, tile in ((1, 0), (0, 0), (0, 1), (0, 2), (0, 3), (0, 4), (0, 5), (0, 6), (0, 8)):
         m.setOption("cost_variant", variant)
         m.setOption("cost_tile", tile)
         c4 = m.computeQuantizationErrorPopulation(pals, 2.0)
