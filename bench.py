@@ -95,6 +95,8 @@ def main():
     ap.add_argument("--population", type=int, default=4)
     ap.add_argument("--grid", type=int, default=32)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--bands", type=int, default=-1,
+                    help="row bands of the assign/cost pipeline (-1 = library default)")
     ap.add_argument("--cpu-size", type=int, default=1024)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -121,6 +123,8 @@ def main():
         raise RuntimeError("bench.py: libhq could not open the GPU")
     sp = hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
     m.setOption("grid", args.grid)
+    if args.bands >= 0:
+        m.setOption("bands", args.bands)
     R, G, B = synthetic_planes(W, H, seed=args.seed)
     r0 = rank * H // world
     r1 = (rank + 1) * H // world

@@ -13,6 +13,7 @@ constexpr int kNumFilt = 7;       // separable filter pairs of the S-CIELAB sten
 constexpr int kL1Cap = 31;        // level-1 candidate list capacity (32-B entry)
 constexpr int kL2Cap = 15;        // level-2 candidate list capacity (16-B entry)
 constexpr uint8_t kOverflow = 255;
+constexpr int kMaxBands = 16;    // row bands of the banded assign -> cost pipeline
 
 // The 7 separable (vertical, horizontal) filter pairs of the candidate stencil,
 // CL:234-306 restated: channel 0 = k1.x (x) k1.x + k2.x (x) k2.x + |k3| (x) k3,
@@ -73,7 +74,9 @@ struct AssignArgs {
     int64_t lvl2_gstride;   // bytes per group of 4 palettes (G2^3 * 64)
     int K;
     int G2;                 // 0 = exhaustive
-    int nblocks;            // blocks per palette
+    int nblocks;            // blocks per palette in this launch
+    int mask_blocks;        // used_mask blocks per palette (all bands; = nblocks unbanded)
+    int mask_off;           // this launch's first used_mask block (band offset)
 };
 
 struct CostArgs {
@@ -93,7 +96,9 @@ struct CostArgs {
     Geom g;
     int K;
     int tiles_x;
-    int ntiles;
+    int ntiles;      // tiles of the shard (partial pitch per palette)
+    int tile0;       // first tile of this launch (row band; 0 unbanded)
+    int band_tiles;  // tiles in this launch (= ntiles unbanded)
     float m_lab[9];  // Opp->XYZ rows divided by the illuminant (CL:124-131), opp2xyz_over_illum()
 };
 

@@ -131,6 +131,15 @@ __device__ __forceinline__ float dist2(float r, float g, float b, float4 c) {
     return (dx * dx + dy * dy) + dz * dz;
 }
 
+// Ranking distance of the pruned argmin: the same sum with two FMAs.  All three
+// terms are non-negative, so it is within 3 ulp (< 2e-7 relative) of dist2;
+// argmin_from_entry re-resolves with dist2 + sqrtf whenever a runner-up lies
+// within 1e-6 relative, so the winner it returns is the reference's.
+__device__ __forceinline__ float dist2_rank(float r, float g, float b, float4 c) {
+    const float dx = r - c.x, dy = g - c.y, dz = b - c.z;
+    return __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
+}
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <typename V>
@@ -407,14 +416,14 @@ __device__ __forceinline__ int argmin_from_entry(float r, float g, float b, uint
     if (__any(cnt > 1)) {
         const uint32_t words[8] = {L0.x, L0.y, L0.z, L0.w, L1.x, L1.y, L1.z, L1.w};
         auto cand = [&](int i) { return (int)((words[(i + 1) >> 2] >> (8 * ((i + 1) & 3))) & 0xff); };
-        float best2 = dist2(r, g, b, s_pal[bi * REP + copy]);
-        // smallest d2 among the other candidates: a tie under sqrtf needs one
-        // within 2^-22 of the final best2 (one test at the end instead of one per
-        // candidate)
+        // Ranked by dist2_rank.  best2 <= second2 always, so the runner-up after a
+        // new value is the median of the three (v_med3_f32): 4 VALU per candidate
+        // to track best, runner-up and index (the compare-and-select form took 7).
+        // Slots past a lane's list (build_grid writes index 0 there) rank as +inf.
+        float best2 = dist2_rank(r, g, b, s_pal[bi * REP + copy]);
         float second2 = INFINITY;
         // the next candidate's colour is read while this one is evaluated (the
-        // loop is unrolled, so the hand-over is register renaming, not a copy);
-        // slots past a lane's list hold 0 (build_grid), a valid colour
+        // loop is unrolled, so the hand-over is register renaming, not a copy)
         int kn = cand(1);
         float4 cn = s_pal[kn * REP + copy];
 #pragma unroll
@@ -427,13 +436,11 @@ __device__ __forceinline__ int argmin_from_entry(float r, float g, float b, uint
                 cn = s_pal[kn * REP + copy];
             }
             asm volatile("" ::"v"(c.w));  // keep .w: one ds_read_b128 (16-lane groups), not b96
-            const float d2 = dist2(r, g, b, c);
-            const bool act = i < cnt;
-            const bool lt = act && d2 < best2;
-            const float other = lt ? best2 : d2;  // the one of the two that is not the best
-            second2 = act && other < second2 ? other : second2;
-            best2 = lt ? d2 : best2;
+            const float d2 = i < cnt ? dist2_rank(r, g, b, c) : INFINITY;
+            const bool lt = d2 < best2;  // a select, not fminf (which canonicalises its inputs)
             bi = lt ? k : bi;
+            second2 = __builtin_amdgcn_fmed3f(best2, second2, d2);
+            best2 = lt ? d2 : best2;
         }
         near = second2 <= best2 * (1.0f + 1e-6f);
     }
@@ -491,7 +498,7 @@ __global__ __launch_bounds__(256) void assign_kernel(AssignArgs a, int P) {
         }
     }
     __syncthreads();
-    if (tid < 8) a.used_mask[((int64_t)p * a.nblocks + blk) * 8 + tid] = s_used[tid];
+    if (tid < 8) a.used_mask[((int64_t)p * a.mask_blocks + a.mask_off + blk) * 8 + tid] = s_used[tid];
 }
 
 // assign_batch: the assign kernel with the memory round trips batched.  Per
@@ -548,7 +555,7 @@ __global__ __launch_bounds__(256) void assign_batch_kernel(AssignArgs a, int P) 
         }
     }
     __syncthreads();
-    if (tid < 8) a.used_mask[((int64_t)p * a.nblocks + blk) * 8 + tid] = s_used[tid];
+    if (tid < 8) a.used_mask[((int64_t)p * a.mask_blocks + a.mask_off + blk) * 8 + tid] = s_used[tid];
 }
 
 // assign_quad: the batched assign for a group of up to 4 palettes.  One pixel
@@ -625,7 +632,7 @@ __global__ __launch_bounds__(256) void assign_quad_kernel(AssignArgs a, int P) {
     }
     __syncthreads();
     if (tid < 8 * ng)
-        a.used_mask[((int64_t)(p0 + (tid >> 3)) * a.nblocks + blk) * 8 + (tid & 7)] =
+        a.used_mask[((int64_t)(p0 + (tid >> 3)) * a.mask_blocks + a.mask_off + blk) * 8 + (tid & 7)] =
             s_used[tid >> 3][tid & 7];
 }
 
@@ -726,7 +733,94 @@ __global__ __launch_bounds__(256) void assign_pipe_kernel(AssignArgs a, int P) {
     }
     __syncthreads();
     if (tid < 8 * ng)
-        a.used_mask[((int64_t)(p0 + (tid >> 3)) * a.nblocks + blk) * 8 + (tid & 7)] =
+        a.used_mask[((int64_t)(p0 + (tid >> 3)) * a.mask_blocks + a.mask_off + blk) * 8 + (tid & 7)] =
+            s_used[tid >> 3][tid & 7];
+}
+
+// assign_lane: assign_pipe with one (pixel, palette) pair per lane.  Lane l of
+// a wave takes palette l % ng of pixel l / ng (ng = the group's palettes, 64 / ng
+// pixels per wave instruction), so a pixel's level-2 line -- its 4 palettes'
+// 16-B entries -- is read by 4 neighbouring lanes in ONE global_load_dwordx4
+// that touches 16 cache lines, instead of 4 loads touching 64 lines each
+// (assign_pipe: every lane reads the whole line for its pixel).  Same three-stage
+// pipeline: while pair i is resolved, pair i+1's entry and pair i+2's RGB are in
+// flight.  Grid: nblocks * ceil(P/4), XCD-relabelled; dynamic LDS = 4 * K * 16 B.
+__global__ __launch_bounds__(256) void assign_lane_kernel(AssignArgs a, int P) {
+    constexpr int PPT = 8;  // wave instructions per thread per chunk
+    extern __shared__ __attribute__((aligned(16))) float4 s_pal[];  // [4][K]
+    __shared__ uint32_t s_used[4][8];
+    const int ngroups = (P + 3) / 4;
+    const int w = xcd_remap(blockIdx.x, a.nblocks * ngroups);
+    const int grp = w % ngroups, blk = w / ngroups, tid = threadIdx.x;
+    const int p0 = 4 * grp, ng = min(4, P - p0);
+    for (int e = tid; e < ng * a.K; e += 256) {
+        const int pp = e / a.K, k = e - pp * a.K;
+        s_pal[e] = a.pal[(int64_t)(p0 + pp) * kMaxK + k];
+    }
+    if (tid < 32) s_used[tid >> 3][tid & 7] = 0;
+    __syncthreads();
+    const int lane = tid & 63, wave = tid >> 6;
+    const int ppw = 64 / ng;                 // pixels per wave instruction
+    const int pp = lane % ng, pix = lane / ng;
+    const bool lane_ok = pix < ppw;          // ng = 3: lane 63 idles
+    const int pq = p0 + pp;
+    const bool exh = a.pflags[pq] != 0 || a.G2 == 0;
+    const float4* pal = s_pal + pp * a.K;
+    const uint8_t* lvl1p = a.lvl1 + (int64_t)pq * a.lvl1_pitch;
+    uint8_t* idx = a.idx + (int64_t)pq * a.idx_pitch;
+    const uint8_t* lines = a.lvl2 + (int64_t)grp * a.lvl2_gstride + 16 * pp;
+    const int G2 = a.G2 > 0 ? a.G2 : 4;
+    const int64_t chunk = 4 * PPT * ppw, cstride = (int64_t)a.nblocks * chunk;
+    const int64_t lane_off = (int64_t)wave * PPT * ppw + pix;
+    const int64_t qend = lane_ok ? a.n_ext : 0;
+    auto qpos = [&](int64_t i) {  // i-th pixel of this lane
+        return (int64_t)blk * chunk + (i / PPT) * cstride + lane_off + ppw * (i % PPT);
+    };
+    const int64_t qlast = a.n_ext - 1;
+    auto load_rgb = [&](int64_t q, float& r, float& g, float& b) {
+        const int64_t qc = min(q, qlast);
+        r = a.R[qc];
+        g = a.G[qc];
+        b = a.B[qc];
+    };
+    auto lookup = [&](int64_t q, float r, float g, float b, bool& inside, uint4& e) {
+        inside = q < qend && r >= 0.f && r <= 1.f && g >= 0.f && g <= 1.f && b >= 0.f && b <= 1.f;
+        e = *reinterpret_cast<const uint4*>(lines + (inside ? quad_cell(r, g, b, G2) : 0) * 64);
+    };
+    float rb[2], gb[2], bb[2];  // RGB loads in flight: pair i+1 / i+2 by parity
+    float xr[2], xg[2], xb[2];  // RGB of the pairs being looked up / resolved
+    uint4 E[2];
+    bool in_[2];
+    int64_t qq[2];
+    qq[0] = qpos(0);
+    load_rgb(qq[0], xr[0], xg[0], xb[0]);
+    lookup(qq[0], xr[0], xg[0], xb[0], in_[0], E[0]);
+    load_rgb(qpos(1), rb[1], gb[1], bb[1]);
+    load_rgb(qpos(2), rb[0], gb[0], bb[0]);
+    auto resolve = [&](int h) {
+        const int k = argmin_from_entry<1>(xr[h], xg[h], xb[h], E[h], in_[h] && !exh, pal, 0, lvl1p,
+                                           G2, a.K);
+        idx[qq[h]] = (uint8_t)k;
+        const uint32_t bit = 1u << (k & 31);
+        if (!(s_used[pp][k >> 5] & bit)) atomicOr(&s_used[pp][k >> 5], bit);
+    };
+    auto step = [&](int64_t i, int h) {  // h == i & 1, a compile-time constant at each call
+        const int n = h ^ 1;
+        qq[n] = qpos(i + 1);
+        xr[n] = rb[n]; xg[n] = gb[n]; xb[n] = bb[n];
+        lookup(qq[n], xr[n], xg[n], xb[n], in_[n], E[n]);
+        load_rgb(qpos(i + 3), rb[n], gb[n], bb[n]);
+        resolve(h);
+    };
+    for (int64_t i = 0;; i += 2) {
+        if (qpos(i) >= qend) break;
+        step(i, 0);
+        if (qpos(i + 1) >= qend) break;
+        step(i + 1, 1);
+    }
+    __syncthreads();
+    if (tid < 8 * ng)
+        a.used_mask[((int64_t)(p0 + (tid >> 3)) * a.mask_blocks + a.mask_off + blk) * 8 + (tid & 7)] =
             s_used[tid >> 3][tid & 7];
 }
 
@@ -801,7 +895,7 @@ __global__ __launch_bounds__(256) void assign_multi_kernel(AssignArgs a, int P) 
     }
     __syncthreads();
     if (tid < 8 * ng)
-        a.used_mask[((int64_t)(p0 + (tid >> 3)) * a.nblocks + blockIdx.x) * 8 + (tid & 7)] =
+        a.used_mask[((int64_t)(p0 + (tid >> 3)) * a.mask_blocks + a.mask_off + blockIdx.x) * 8 + (tid & 7)] =
             s_used[tid >> 3][tid & 7];
 }
 
@@ -1060,7 +1154,7 @@ template <int TW, int TH>
 __device__ __forceinline__ TileItem tile_item(const CostArgs& a, int w, int P) {
     TileItem t;
     t.p = w % P;
-    t.tile = w / P;
+    t.tile = a.tile0 + w / P;
     t.x0 = (t.tile % a.tiles_x) * TW;
     t.y0 = a.g.r0 + (t.tile / a.tiles_x) * TH;
     return t;
@@ -1219,7 +1313,7 @@ __global__ __launch_bounds__(256, OCC) void cost_tile_kernel(CostArgs a, int P_)
     float* s_v = reinterpret_cast<float*>(s_v4);
     const int tid = threadIdx.x;
     const Geom& g = a.g;
-    const TileItem cur = tile_item<TW, TH>(a, xcd_remap(blockIdx.x, a.ntiles * P_), P_);
+    const TileItem cur = tile_item<TW, TH>(a, xcd_remap(blockIdx.x, a.band_tiles * P_), P_);
     const TapsPtr<HALF> taps = (TapsPtr<HALF>)(uintptr_t)a.taps;  // flat -> constant: same address
 
     // ---- prologue: every fill load issued before the first wait (TileFill),
@@ -1643,7 +1737,7 @@ __global__ __launch_bounds__(256, 4) void cost_pair_kernel(CostArgs a, int P_) {
     float* s_v = reinterpret_cast<float*>(s_vq);
     const int tid = threadIdx.x;
     const Geom& g = a.g;
-    const TileItem cur = tile_item<TW, TH>(a, xcd_remap(blockIdx.x, a.ntiles * P_), P_);
+    const TileItem cur = tile_item<TW, TH>(a, xcd_remap(blockIdx.x, a.band_tiles * P_), P_);
     const TapsPtr<HALF> taps = (TapsPtr<HALF>)(uintptr_t)a.taps;
 
     TileFill<HALF, RW, TH> fill;
@@ -1741,7 +1835,7 @@ __global__ __launch_bounds__(256, 6) void cost_chan_kernel(CostArgs a, int P_) {
     float* s_v = reinterpret_cast<float*>(s_vq);
     const int tid = threadIdx.x;
     const Geom& g = a.g;
-    const TileItem cur = tile_item<TW, TH>(a, xcd_remap(blockIdx.x, a.ntiles * P_), P_);
+    const TileItem cur = tile_item<TW, TH>(a, xcd_remap(blockIdx.x, a.band_tiles * P_), P_);
     const TapsPtr<HALF> taps = (TapsPtr<HALF>)(uintptr_t)a.taps;
 
     TileFill<HALF, RW, TH> fill;
@@ -1921,7 +2015,7 @@ __global__ __launch_bounds__(256, 6) void cost_mfma_kernel(CostArgs a, int P_) {
     float* s_v = reinterpret_cast<float*>(s_vq);
     const int tid = threadIdx.x;
     const Geom& g = a.g;
-    const TileItem cur = tile_item<TW, TH>(a, xcd_remap(blockIdx.x, a.ntiles * P_), P_);
+    const TileItem cur = tile_item<TW, TH>(a, xcd_remap(blockIdx.x, a.band_tiles * P_), P_);
     const TapsPtr<HALF> taps = (TapsPtr<HALF>)(uintptr_t)a.taps;  // H taps x 2^-30
     const int lane = tid & 63, wv = tid >> 6, lc = lane & 15, lk = lane >> 4;
     const uint4* frag = a.vfrag16 + (TRIM ? 4 * 2 * 64 : 0) + lane;  // [trim][stack][hi,lo][lane]
@@ -2041,6 +2135,478 @@ __global__ __launch_bounds__(256, 6) void cost_mfma_kernel(CostArgs a, int P_) {
 
 
 // ----------------------------------------------------------------------------
+// cost_wide (cost_tile 11): cost_mfma with horizontal items of 4 output columns
+// of a row pair (108 items on waves 0-1): each filter's window is 24 row-pair
+// columns = 12 ds_read_b128 for 8 outputs, against 11 for cost_mfma's 4.  The
+// horizontal windows were ~45% of cost_mfma's LDS cycles, and LDS is what bounds
+// it.  A plain row-pair layout would put item j's reads 32 B apart, two lanes of
+// every 16-lane b128 group in one bank (why cost_tile 5 never paid); here each
+// row-pair row stores its column pairs split by parity: pair p = col / 2 goes to
+// half p & 1, position p >> 1, so read q of item j lands at half q & 1, position
+// j + q / 2 -- 16 B apart across the lanes, conflict-free.  The halves are 72
+// float2 apart (8 mod 16), so the V pass's 16-column float2 stores stay
+// conflict-free too.
+// ----------------------------------------------------------------------------
+constexpr int kWideHalf = 72;  // float2 per half of a permuted row-pair row (64 + 8 pad)
+
+// float2 position of column `col` in a permuted row-pair row
+__device__ __forceinline__ int wide_pos(int col) {
+    return ((col >> 1) & 1) * kWideHalf + ((col >> 2) << 1) + (col & 1);
+}
+
+template <int HALF, int TLO = 0, int THI = 2 * HALF>
+__device__ __forceinline__ void hpass_wide_filters(const f32x4* src, TapsPtr<HALF> taps, int f0,
+                                                   int f1, f32x2 (&acc)[4], int fslot, int pstride) {
+    constexpr int HR = 4, NIN = HR + 2 * HALF, NQ = NIN / 2;  // 12 reads of 2 columns
+#pragma unroll 1
+    for (int f = f0; f < f1; ++f) {
+        const f32x4* row = src + (f - fslot) * pstride;
+        f32x4 v[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) v[q] = row[(q & 1) * (kWideHalf / 2) + (q >> 1)];
+        f32x2 in[2 * NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            in[2 * q] = v[q].xy;
+            in[2 * q + 1] = v[q].zw;
+        }
+#pragma unroll
+        for (int t = TLO; t <= THI; ++t) {
+            const float k = taps->h[f][t];
+            const f32x2 kk = {k, k};
+#pragma unroll
+            for (int xo = 0; xo < HR; ++xo) acc[xo] = __builtin_elementwise_fma(in[xo + t], kk, acc[xo]);
+        }
+    }
+}
+
+// D of one 16x16 stack block -> permuted row pairs (cf. store_vstack)
+__device__ __forceinline__ void store_vstack_wide(float* s_v, const f32x4v& d, int plane_a,
+                                                  int plane_b, int lk, int col) {
+    constexpr int PAIRS = 4, ROW = 2 * kWideHalf;  // float2 per row-pair row
+    const int plane = lk < 2 ? plane_a : plane_b;
+    if (plane < 0) return;
+    const int p0 = 2 * (lk & 1);
+    f32x2* v = reinterpret_cast<f32x2*>(s_v);
+    const int pos = wide_pos(col);
+    v[(plane * PAIRS + p0) * ROW + pos] = f32x2{d[0], d[1]};
+    v[(plane * PAIRS + p0 + 1) * ROW + pos] = f32x2{d[2], d[3]};
+}
+
+template <int DE, bool TRIM>
+__global__ __launch_bounds__(256, 6) void cost_wide_kernel(CostArgs a, int P_) {
+    constexpr int HALF = 10, RW = 128, TH = 8, HR = 4, T2 = 2 * HALF;
+    constexpr int TW = RW - 2 * HALF, RH = TH + 2 * HALF;
+    constexpr int NRUN = TW / HR;                 // 27 items per row pair, 32 slots
+    constexpr int ROW = 2 * kWideHalf;            // float2 per row-pair row
+    constexpr int PLANE4 = (TH / 2) * ROW / 2;    // f32x4 per filter plane
+    static_assert(NRUN <= 32 && RH <= 32 && 4 * PLANE4 >= 512, "tile");
+    __shared__ f32x4 s_vq[4 * PLANE4];
+    __shared__ uint32_t s_ox[kMaxK];  // opponent x 2^14 as (hi, lo) f16 pairs: channel 0
+    __shared__ uint2 s_oyz[kMaxK];     // channels 1, 2
+    __shared__ __attribute__((aligned(16))) uint8_t s_idx[32 * RW];
+    __shared__ double s_red[4];
+    float* s_v = reinterpret_cast<float*>(s_vq);
+    const int tid = threadIdx.x;
+    const Geom& g = a.g;
+    const TileItem cur = tile_item<TW, TH>(a, xcd_remap(blockIdx.x, a.band_tiles * P_), P_);
+    const TapsPtr<HALF> taps = (TapsPtr<HALF>)(uintptr_t)a.taps;  // H taps x 2^-30
+    const int lane = tid & 63, wv = tid >> 6, lc = lane & 15, lk = lane >> 4;
+    const uint4* frag = a.vfrag16 + (TRIM ? 4 * 2 * 64 : 0) + lane;  // [trim][stack][hi,lo][lane]
+
+    TileFill<HALF, RW, TH> fill;
+    fill.issue(a, cur, tid);
+    uint4 F0h = frag[(0 * 2 + 0) * 64], F0l = frag[(0 * 2 + 1) * 64];
+    uint4 F1h = frag[(1 * 2 + 0) * 64], F1l = frag[(1 * 2 + 1) * 64];
+    s_ox[tid] = split_f16(fill.ov.x);
+    s_oyz[tid] = make_uint2(split_f16(fill.ov.y), split_f16(fill.ov.z));
+    fill.template commit_idx<RW>(a, s_idx, tid);
+    // H item: row pair m, output columns 4j .. 4j+3, shared by thread t (half 0,
+    // waves 0-1) and t + 128 (half 1): each applies about half of every channel
+    // group's taps -- half 0 filters 0, 1 (ch 0) and 3, 4 (ch 1), half 1 filter 2
+    // (ch 0) and 5, 6 (ch 2) -- and finishes one row of the pair after an exchange
+    // of partial sums, so all four waves carry the same horizontal work.
+    const int hh = tid >> 7, it = tid & 127, m = it >> 5, jr = it & 31;
+    const bool has_item = jr < NRUN;
+    const int gy = cur.y0 + 2 * m + hh, gx0 = cur.x0 + HR * jr;  // the row this thread finishes
+    __syncthreads();
+
+    const int col0 = 32 * wv + lc;
+    const f32x4* hsrc = &s_vq[(m * ROW) / 2 + jr];
+    f32x2 accA[HR], accB[HR];  // half 0: ch 0 part, ch 1; half 1: ch 0 part, ch 2
+#pragma unroll
+    for (int xo = 0; xo < HR; ++xo) accA[xo] = accB[xo] = f32x2{0.f, 0.f};
+
+    // ---- group 0: channel 0 -> planes 0-2 ----
+    {
+        const f16x8 a0h = __builtin_bit_cast(f16x8, F0h), a0l = __builtin_bit_cast(f16x8, F0l);
+        const f16x8 a1h = __builtin_bit_cast(f16x8, F1h), a1l = __builtin_bit_cast(f16x8, F1l);
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            uint32_t w[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) w[j] = s_ox[s_idx[(8 * lk + j) * RW + col0 + 16 * bb]];
+            f16x8 bh, bl;
+            pack_b(w, bh, bl);
+            store_vstack_wide(s_v, mfma3(a0h, a0l, bh, bl), 0, 1, lk, col0 + 16 * bb);
+            store_vstack_wide(s_v, mfma3(a1h, a1l, bh, bl), 2, -1, lk, col0 + 16 * bb);
+        }
+    }
+    const uint4 F2h = frag[(2 * 2 + 0) * 64], F2l = frag[(2 * 2 + 1) * 64];
+    const uint4 F3h = frag[(3 * 2 + 0) * 64], F3l = frag[(3 * 2 + 1) * 64];
+    __syncthreads();
+    if (has_item) {
+        if (hh == 0) {
+            if constexpr (TRIM) hpass_wide_filters<HALF, kTrimLo[0], kTrimHi[0]>(hsrc, taps, 0, 1, accA, 0, PLANE4);
+            else hpass_wide_filters<HALF, 0, T2>(hsrc, taps, 0, 1, accA, 0, PLANE4);
+            hpass_wide_filters<HALF, 0, T2>(hsrc, taps, 1, 2, accA, 0, PLANE4);
+        } else {
+            hpass_wide_filters<HALF, 0, T2>(hsrc, taps, 2, 3, accA, 0, PLANE4);
+        }
+    }
+    __syncthreads();
+
+    // ---- group 1: channels 1, 2 -> planes 0-3 ----
+    {
+        const f16x8 a2h = __builtin_bit_cast(f16x8, F2h), a2l = __builtin_bit_cast(f16x8, F2l);
+        const f16x8 a3h = __builtin_bit_cast(f16x8, F3h), a3l = __builtin_bit_cast(f16x8, F3l);
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            uint32_t wy[8], wz[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint2 e = s_oyz[s_idx[(8 * lk + j) * RW + col0 + 16 * bb]];
+                wy[j] = e.x; wz[j] = e.y;
+            }
+            f16x8 bh, bl;
+            pack_b(wy, bh, bl);
+            store_vstack_wide(s_v, mfma3(a2h, a2l, bh, bl), 0, 1, lk, col0 + 16 * bb);
+            pack_b(wz, bh, bl);
+            store_vstack_wide(s_v, mfma3(a3h, a3l, bh, bl), 2, 3, lk, col0 + 16 * bb);
+        }
+    }
+    __syncthreads();
+    if (has_item) {
+        const int fa = hh == 0 ? 3 : 5;  // trimmed filter of the channel
+        if constexpr (TRIM) {
+            if (hh == 0) hpass_wide_filters<HALF, kTrimLo[1], kTrimHi[1]>(hsrc, taps, 3, 4, accB, 3, PLANE4);
+            else hpass_wide_filters<HALF, kTrimLo[2], kTrimHi[2]>(hsrc, taps, 5, 6, accB, 3, PLANE4);
+        } else {
+            hpass_wide_filters<HALF, 0, T2>(hsrc, taps, fa, fa + 1, accB, 3, PLANE4);
+        }
+        hpass_wide_filters<HALF, 0, T2>(hsrc, taps, fa + 1, fa + 2, accB, 3, PLANE4);
+    }
+    // LabRef of the finished row, in flight across the exchange
+    float4 L4 = make_float4(0.f, 0.f, 0.f, 0.f), A4 = L4, B4 = L4;
+    {
+        const bool ok = has_item && gy < g.r1 && gx0 < g.W;
+        const uint32_t off = ok ? (uint32_t)((gy - g.r0) * g.lab_pitch + gx0) : 0u;
+        L4 = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(a.labL) + (off << 2));
+        A4 = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(a.labA) + (off << 2));
+        B4 = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(a.labB) + (off << 2));
+    }
+    __syncthreads();
+    // exchange: each thread passes on the row the other half finishes (row 1 - hh)
+    {
+        const int o = 1 - hh;
+        s_vq[tid] = f32x4{accA[0][o], accA[1][o], accA[2][o], accA[3][o]};
+        s_vq[256 + tid] = f32x4{accB[0][o], accB[1][o], accB[2][o], accB[3][o]};
+    }
+    __syncthreads();
+    double sum = 0.0;
+    if (has_item) {
+        const f32x4 pA = s_vq[tid ^ 128], pB = s_vq[256 + (tid ^ 128)];
+        const float Ls[4] = {L4.x, L4.y, L4.z, L4.w}, As[4] = {A4.x, A4.y, A4.z, A4.w},
+                    Bs[4] = {B4.x, B4.y, B4.z, B4.w};
+        float part = 0.f;
+#pragma unroll
+        for (int xo = 0; xo < HR; ++xo) {
+            const float c0 = accA[xo][hh] + pA[xo];           // channel 0: both halves' filters
+            const float c1 = hh == 0 ? accB[xo][0] : pB[xo];  // channel 1: half 0's
+            const float c2 = hh == 0 ? pB[xo] : accB[xo][1];  // channel 2: half 1's
+            const float3 l3 = opp2lab_fast(c0, c1, c2, a.m_lab);
+            const float e = delta_e<DE>(Ls[xo], As[xo], Bs[xo], l3.x, l3.y, l3.z);
+            part += (gy < g.r1 && gx0 + xo < g.W) ? e : 0.f;
+        }
+        sum = (double)part;
+    }
+    sum = wave_sum_to_lane63(sum);
+    if ((tid & 63) == 63) s_red[tid >> 6] = sum;
+    __syncthreads();
+    if (tid == 0)
+        a.partial[(int64_t)cur.p * a.ntiles + cur.tile] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+}
+
+
+// ----------------------------------------------------------------------------
+// cost_vt (cost_tile 9): cost_mfma with the vertical pass's operand roles
+// swapped, V^T = X^T . T^T, so each lane's D is 4 consecutive columns of one
+// output row (one ds_write_b128 per stack block), the horizontal pass on
+// 1-row x 4-column items (a 24-float window: 6 ds_read_b128 per filter for 4
+// outputs, against 11 for the row-pair items' 4 outputs), and the index region
+// stored column-major (CP bytes per column, rows contiguous), so a lane reads
+// the 8 region rows of its column with one ds_read_b64 instead of 8 ds_read_u8.
+// What bounds cost_mfma is LDS issue (PMC: ~78% of cycles LDS-active), and the
+// horizontal windows and the byte-wise index reads were ~half of it.
+// ----------------------------------------------------------------------------
+template <int HALF, int TH, int VP, int TLO = 0, int THI = 2 * HALF>
+__device__ __forceinline__ void hpass_row_filters(const f32x4* src, TapsPtr<HALF> taps, int f0,
+                                                  int f1, float (&acc)[4], int fslot) {
+    constexpr int NQ = (4 + 2 * HALF + 3) / 4;
+    static_assert(NQ == 6, "the asm barrier below names six vectors");
+#pragma unroll 1
+    for (int f = f0; f < f1; ++f) {
+        const f32x4* row = src + (f - fslot) * TH * VP / 4;
+        f32x4 v0 = row[0], v1 = row[1], v2 = row[2], v3 = row[3], v4 = row[4], v5 = row[5];
+        asm volatile("" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+v"(v4), "+v"(v5));
+        const f32x4 vv[NQ] = {v0, v1, v2, v3, v4, v5};
+        float in[4 * NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            in[4 * q] = vv[q].x; in[4 * q + 1] = vv[q].y; in[4 * q + 2] = vv[q].z; in[4 * q + 3] = vv[q].w;
+        }
+#pragma unroll
+        for (int t = TLO; t <= THI; ++t) {
+            const float k = taps->h[f][t];
+#pragma unroll
+            for (int xo = 0; xo < 4; ++xo) acc[xo] = fmaf(in[xo + t], k, acc[xo]);
+        }
+    }
+}
+
+// 4 x 4 byte transpose: v[i] byte c -> w[c] byte i.
+__device__ __forceinline__ void transpose4x4_u8(const uint32_t (&v)[4], uint32_t (&w)[4]) {
+    const uint32_t lo01 = __builtin_amdgcn_perm(v[1], v[0], 0x05010400u);  // v0b0 v1b0 v0b1 v1b1
+    const uint32_t hi01 = __builtin_amdgcn_perm(v[1], v[0], 0x07030602u);  // v0b2 v1b2 v0b3 v1b3
+    const uint32_t lo23 = __builtin_amdgcn_perm(v[3], v[2], 0x05010400u);
+    const uint32_t hi23 = __builtin_amdgcn_perm(v[3], v[2], 0x07030602u);
+    w[0] = __builtin_amdgcn_perm(lo23, lo01, 0x05040100u);
+    w[1] = __builtin_amdgcn_perm(lo23, lo01, 0x07060302u);
+    w[2] = __builtin_amdgcn_perm(hi23, hi01, 0x05040100u);
+    w[3] = __builtin_amdgcn_perm(hi23, hi01, 0x07060302u);
+}
+
+// Column-major fill of the 28 (+4 zero) x 128 index region: thread (cb = tid >> 3,
+// rb = tid & 7) loads rows 4rb .. 4rb+3 of region columns 4cb .. 4cb+3 (aligned
+// dword pairs + alignbyte, all loads before the first wait) and stores their
+// transpose as 4 dwords (4 rows of one column each).  Edge tiles gather bytes
+// with reflection at commit time.
+template <int HALF, int CP>
+struct TileFillT {
+    static constexpr int RW = 128, TH = 8, TW = RW - 2 * HALF, RH = TH + 2 * HALF;
+    static_assert(RH == 28 && CP % 8 == 0 && CP >= 32, "7 row blocks of 4 + one zero block");
+    uint32_t lo[4], hi[4], sh[4];
+    float4 ov;
+    TileItem t;
+    bool interior;
+
+    __device__ __forceinline__ static int row_base(const Geom& g, const TileItem& t, int i) {
+        int gy = reflect_clamp(t.y0 - HALF + i, g.H);
+        gy = min(max(gy, g.e0), g.e1 - 1);
+        return (gy - g.e0) * g.W + (t.x0 - HALF);
+    }
+
+    __device__ __forceinline__ void issue(const CostArgs& a, const TileItem& ti, int tid) {
+        const Geom& g = a.g;
+        t = ti;
+        const uint8_t* idx = a.idx + (int64_t)t.p * g.idx_pitch;
+        ov = tid < a.K ? a.opp[(int64_t)t.p * kMaxK + tid] : make_float4(0.f, 0.f, 0.f, 0.f);
+        interior = t.x0 - HALF >= 0 && t.x0 + TW + HALF <= g.W;
+        if (interior) {
+            const int cb = tid >> 3, rb = min(tid & 7, 6);  // rb 7: the zero rows (loads discarded)
+            const int ytop = t.y0 - HALF;
+            const bool vfast = ytop >= 0 && ytop >= g.e0 && ytop + RH <= g.H && ytop + RH <= g.e1;
+            const int ubase = (ytop - g.e0) * g.W + (t.x0 - HALF);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = 4 * rb + i;
+                const uint32_t off = (uint32_t)(vfast ? ubase + row * g.W : row_base(g, t, row));
+                sh[i] = off & 3u;
+                const uint32_t* src = reinterpret_cast<const uint32_t*>(idx + ((off & ~3u) + 4u * (uint32_t)cb));
+                lo[i] = src[0];
+                hi[i] = src[1];
+            }
+        }
+    }
+
+    __device__ __forceinline__ void commit_idx(const CostArgs& a, uint8_t* s_idx, int tid) const {
+        const Geom& g = a.g;
+        if (interior) {
+            const int cb = tid >> 3, rb = tid & 7;
+            uint32_t v[4], w[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = rb < 7 ? __builtin_amdgcn_alignbyte(hi[i], lo[i], sh[i]) : 0u;
+            transpose4x4_u8(v, w);
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                *reinterpret_cast<uint32_t*>(s_idx + (4 * cb + c) * CP + 4 * rb) = w[c];
+        } else {
+            constexpr int NFB = (RH * RW + 255) / 256;
+            const uint8_t* idx = a.idx + (int64_t)t.p * g.idx_pitch;
+            uint32_t b[NFB];
+#pragma unroll
+            for (int q = 0; q < NFB; ++q) {  // all loads first: one round trip
+                const int e = min(tid + 256 * q, RH * RW - 1);
+                const int i = e / RW, j = e % RW;
+                int gy = reflect_clamp(t.y0 - HALF + i, g.H);
+                gy = min(max(gy, g.e0), g.e1 - 1);
+                const int gx = reflect_clamp(t.x0 - HALF + j, g.W);
+                b[q] = idx[(uint32_t)((gy - g.e0) * g.W + gx)];
+            }
+#pragma unroll
+            for (int q = 0; q < NFB; ++q) {
+                const int e = tid + 256 * q;
+                if (e < RH * RW) s_idx[(e % RW) * CP + e / RW] = (uint8_t)b[q];
+            }
+            if (tid < RW) *reinterpret_cast<uint32_t*>(s_idx + tid * CP + RH) = 0u;  // rows 28-31
+        }
+    }
+};
+
+// D of one V^T stack block -> s_v rows: lane (c4 = l >> 4, n = l & 15) holds
+// columns 4 c4 .. +3 of output row n & 7 of the stack's filter n >> 3.
+template <int TH, int VP>
+__device__ __forceinline__ void store_vt(float* s_v, const f32x4v& d, int plane_a, int plane_b,
+                                         int n, int col) {
+    const int plane = n < 8 ? plane_a : plane_b;
+    if (plane < 0) return;
+    *reinterpret_cast<f32x4v*>(s_v + (plane * TH + (n & 7)) * VP + col) = d;
+}
+
+template <int DE, bool TRIM>
+__global__ __launch_bounds__(256, 6) void cost_vt_kernel(CostArgs a, int P_) {
+    constexpr int HALF = 10, RW = 128, TH = 8, T2 = 2 * HALF;
+    constexpr int TW = RW - 2 * HALF;
+    constexpr int NRUN = TW / 4;  // 27 runs of 4 output columns per row, 32 slots
+    constexpr int CP = 48;        // bytes per region column (32 rows + pad: conflict-free b64 reads)
+    constexpr int VP = RW + 4;    // floats per s_v row (528 B = 16 mod 128: conflict-free b128 stores)
+    __shared__ f32x4 s_v4[4 * TH * VP / 4];
+    __shared__ uint32_t s_ox[kMaxK];  // opponent x 2^14 as (hi, lo) f16 pairs: channel 0
+    __shared__ uint2 s_oyz[kMaxK];     // channels 1, 2
+    __shared__ __attribute__((aligned(16))) uint8_t s_idx[RW * CP];
+    __shared__ double s_red[4];
+    float* s_v = reinterpret_cast<float*>(s_v4);
+    const int tid = threadIdx.x;
+    const Geom& g = a.g;
+    const TileItem cur = tile_item<TW, TH>(a, xcd_remap(blockIdx.x, a.band_tiles * P_), P_);
+    const TapsPtr<HALF> taps = (TapsPtr<HALF>)(uintptr_t)a.taps;  // H taps x 2^-30
+    const int lane = tid & 63, wv = tid >> 6, lc = lane & 15, lk = lane >> 4;
+    const uint4* frag = a.vfrag16 + (TRIM ? 4 * 2 * 64 : 0) + lane;  // [trim][stack][hi,lo][lane]
+
+    TileFillT<HALF, CP> fill;
+    fill.issue(a, cur, tid);
+    uint4 F0h = frag[(0 * 2 + 0) * 64], F0l = frag[(0 * 2 + 1) * 64];  // group 0 stacks
+    uint4 F1h = frag[(1 * 2 + 0) * 64], F1l = frag[(1 * 2 + 1) * 64];
+    // every entry (zeros for tid >= K): the zero-weight rows 28-31 gather index 0
+    s_ox[tid] = split_f16(fill.ov.x);
+    s_oyz[tid] = make_uint2(split_f16(fill.ov.y), split_f16(fill.ov.z));
+    fill.commit_idx(a, s_idx, tid);
+    // H item: row y, output columns 4j .. 4j+3
+    const int y = tid >> 5, j = tid & 31;
+    const bool has_item = j < NRUN;
+    const int gy = cur.y0 + y, gx0 = cur.x0 + 4 * j;
+    __syncthreads();
+
+    // V pass: lane (c = lc, q = lk) gathers region rows 8q .. 8q+7 of column
+    // 32 wv + 16 bb + c (A = X^T fragment), D = 4 columns of one (filter, row)
+    const int colA = 32 * wv + lc;
+    const int colD = 32 * wv + 4 * lk;
+    const f32x4* hsrc = &s_v4[(y * VP) / 4 + j];
+    float acc0[4] = {0.f, 0.f, 0.f, 0.f}, acc1[4] = {0.f, 0.f, 0.f, 0.f}, acc2[4] = {0.f, 0.f, 0.f, 0.f};
+
+    // ---- group 0: channel 0 -> planes 0-2 ----
+    {
+        const f16x8 t0h = __builtin_bit_cast(f16x8, F0h), t0l = __builtin_bit_cast(f16x8, F0l);
+        const f16x8 t1h = __builtin_bit_cast(f16x8, F1h), t1l = __builtin_bit_cast(f16x8, F1l);
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            const uint2 ix = *reinterpret_cast<const uint2*>(s_idx + (colA + 16 * bb) * CP + 8 * lk);
+            uint32_t w[8];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                w[jj] = s_ox[(ix.x >> (8 * jj)) & 0xffu];
+                w[4 + jj] = s_ox[(ix.y >> (8 * jj)) & 0xffu];
+            }
+            f16x8 xh, xl;
+            pack_b(w, xh, xl);
+            store_vt<TH, VP>(s_v, mfma3(xh, xl, t0h, t0l), 0, 1, lc, colD + 16 * bb);
+            store_vt<TH, VP>(s_v, mfma3(xh, xl, t1h, t1l), 2, -1, lc, colD + 16 * bb);
+        }
+    }
+    const uint4 F2h = frag[(2 * 2 + 0) * 64], F2l = frag[(2 * 2 + 1) * 64];  // group 1 stacks,
+    const uint4 F3h = frag[(3 * 2 + 0) * 64], F3l = frag[(3 * 2 + 1) * 64];  // in flight during H
+    __syncthreads();
+    if (has_item) {
+        if constexpr (TRIM) {
+            hpass_row_filters<HALF, TH, VP, kTrimLo[0], kTrimHi[0]>(hsrc, taps, 0, 1, acc0, 0);
+            hpass_row_filters<HALF, TH, VP, 0, T2>(hsrc, taps, 1, 3, acc0, 0);
+        } else {
+            hpass_row_filters<HALF, TH, VP, 0, T2>(hsrc, taps, 0, 3, acc0, 0);
+        }
+    }
+    __syncthreads();
+
+    // ---- group 1: channels 1, 2 -> planes 0-3 ----
+    {
+        const f16x8 t2h = __builtin_bit_cast(f16x8, F2h), t2l = __builtin_bit_cast(f16x8, F2l);
+        const f16x8 t3h = __builtin_bit_cast(f16x8, F3h), t3l = __builtin_bit_cast(f16x8, F3l);
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            const uint2 ix = *reinterpret_cast<const uint2*>(s_idx + (colA + 16 * bb) * CP + 8 * lk);
+            uint32_t wy[8], wz[8];
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+                const uint2 e = s_oyz[((jj < 4 ? ix.x : ix.y) >> (8 * (jj & 3))) & 0xffu];
+                wy[jj] = e.x; wz[jj] = e.y;
+            }
+            f16x8 xh, xl;
+            pack_b(wy, xh, xl);
+            store_vt<TH, VP>(s_v, mfma3(xh, xl, t2h, t2l), 0, 1, lc, colD + 16 * bb);
+            pack_b(wz, xh, xl);
+            store_vt<TH, VP>(s_v, mfma3(xh, xl, t3h, t3l), 2, 3, lc, colD + 16 * bb);
+        }
+    }
+    float4 Lr = make_float4(0.f, 0.f, 0.f, 0.f), Ar = Lr, Br = Lr;
+    {
+        const bool ok = has_item && gy < g.r1 && gx0 < g.W;
+        const uint32_t off = ok ? (uint32_t)((gy - g.r0) * g.lab_pitch + gx0) : 0u;
+        Lr = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(a.labL) + (off << 2));
+        Ar = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(a.labA) + (off << 2));
+        Br = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(a.labB) + (off << 2));
+    }
+    __syncthreads();
+
+    double sum = 0.0;
+    if (has_item) {
+        if constexpr (TRIM) {
+            hpass_row_filters<HALF, TH, VP, kTrimLo[1], kTrimHi[1]>(hsrc, taps, 3, 4, acc1, 3);
+            hpass_row_filters<HALF, TH, VP, 0, T2>(hsrc, taps, 4, 5, acc1, 3);
+            hpass_row_filters<HALF, TH, VP, kTrimLo[2], kTrimHi[2]>(hsrc, taps, 5, 6, acc2, 3);
+            hpass_row_filters<HALF, TH, VP, 0, T2>(hsrc, taps, 6, 7, acc2, 3);
+        } else {
+            hpass_row_filters<HALF, TH, VP, 0, T2>(hsrc, taps, 3, 5, acc1, 3);
+            hpass_row_filters<HALF, TH, VP, 0, T2>(hsrc, taps, 5, 7, acc2, 3);
+        }
+        const float Ls[4] = {Lr.x, Lr.y, Lr.z, Lr.w}, As[4] = {Ar.x, Ar.y, Ar.z, Ar.w},
+                    Bs[4] = {Br.x, Br.y, Br.z, Br.w};
+        float part = 0.f;
+#pragma unroll
+        for (int xo = 0; xo < 4; ++xo) {
+            const float3 l3 = opp2lab_fast(acc0[xo], acc1[xo], acc2[xo], a.m_lab);
+            const float e = delta_e<DE>(Ls[xo], As[xo], Bs[xo], l3.x, l3.y, l3.z);
+            part += (gy < g.r1 && gx0 + xo < g.W) ? e : 0.f;
+        }
+        sum = (double)part;
+    }
+    sum = wave_sum_to_lane63(sum);
+    if ((tid & 63) == 63) s_red[tid >> 6] = sum;
+    __syncthreads();
+    if (tid == 0)
+        a.partial[(int64_t)cur.p * a.ntiles + cur.tile] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+}
+
+
+// ----------------------------------------------------------------------------
 // cost_mm (cost_tile 8): both stencil passes on the matrix cores in split f16,
 // Lab / dE on VALU.  Tile = 8 rows x 96 output columns (8 blocks of 12), region
 // 28 (+4 zero-weight) rows x 128 columns, two opponent-channel groups as in
@@ -2096,7 +2662,7 @@ __global__ __launch_bounds__(256, 6) void cost_mm_kernel(CostArgs a, int P_) {
     __shared__ double s_red[4];
     const int tid = threadIdx.x;
     const Geom& g = a.g;
-    const TileItem cur = tile_item<TW, TH>(a, xcd_remap(blockIdx.x, a.ntiles * P_), P_);
+    const TileItem cur = tile_item<TW, TH>(a, xcd_remap(blockIdx.x, a.band_tiles * P_), P_);
     const int lane = tid & 63, wv = tid >> 6, lc = lane & 15, lk = lane >> 4;
     const uint4* vfrag = a.vfrag16 + (TRIM ? 4 * 2 * 64 : 0) + lane;  // [trim][stack][hi,lo][lane]
     const uint4* hfrag = a.hfrag16 + (TRIM ? 7 * 2 * 64 : 0) + lane;  // [trim][filter][hi,lo][lane]
@@ -2169,6 +2735,167 @@ __global__ __launch_bounds__(256, 6) void cost_mm_kernel(CostArgs a, int P_) {
             store_vstack_f16<RS>(s_vh, mfma3(a2h, a2l, bh, bl), 0, 1, lk, col0 + 16 * bb);
             pack_b(wz, bh, bl);
             store_vstack_f16<RS>(s_vh, mfma3(a3h, a3l, bh, bl), 2, 3, lk, col0 + 16 * bb);
+        }
+    }
+    // LabRef of this lane's 4 outputs (row hr, columns 12 ob + 4 lk .. +3), in flight
+    const int gy = cur.y0 + hr, gx = cur.x0 + 12 * ob + 4 * lk;
+    const bool lab_ok = lk < 3 && gy < g.r1 && gx < g.W;
+    const uint32_t loff = lab_ok ? (uint32_t)((gy - g.r0) * g.lab_pitch + gx) : 0u;
+    const float4 Lr = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(a.labL) + (loff << 2));
+    const float4 Ar = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(a.labA) + (loff << 2));
+    const float4 Br = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(a.labB) + (loff << 2));
+    __syncthreads();
+    hpass(3, 0, D1);
+    hpass(4, 1, D1);
+    hpass(5, 2, D2);
+    hpass(6, 3, D2);
+
+    float part = 0.f;
+    if (lk < 3) {
+        const float lr[4] = {Lr.x, Lr.y, Lr.z, Lr.w}, ar[4] = {Ar.x, Ar.y, Ar.z, Ar.w},
+                    br[4] = {Br.x, Br.y, Br.z, Br.w};
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const float3 l3 = opp2lab_fast(D0[v], D1[v], D2[v], a.m_lab);
+            const float e = delta_e<DE>(lr[v], ar[v], br[v], l3.x, l3.y, l3.z);
+            part += (gy < g.r1 && gx + v < g.W) ? e : 0.f;
+        }
+    }
+    double sum = wave_sum_to_lane63((double)part);
+    if ((tid & 63) == 63) s_red[tid >> 6] = sum;
+    __syncthreads();
+    if (tid == 0)
+        a.partial[(int64_t)cur.p * a.ntiles + cur.tile] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+}
+
+// ----------------------------------------------------------------------------
+// cost_mh (cost_tile 10): both stencil passes on the matrix cores, built on
+// cost_vt's layout.  Tile = 8 rows x 96 output columns (8 blocks of 12), region
+// 28 (+4 zero) rows x 128 columns, column-major indices, two channel groups.
+//  - vertical pass: V^T = X^T . T^T as in cost_vt; each lane's D (4 columns of
+//    one filter row, x 2^30) is rescaled to x 2^12 and split into f16 hi / lo,
+//    one ds_write_b64 each into row-major planes (cost_mm wrote 8 ds_write_b16);
+//  - horizontal pass: per 12-column output block the 32 window columns are one
+//    K = 32 step, D[x][n] += Htap[x][k] . V[row][12 ob + k], n = (block of the
+//    wave's pair, row); the B fragment is 2 ds_read_b64 per half, the filters of
+//    a channel accumulate in one D (x 2^28, folded into the Opp -> XYZ rows);
+//  - no horizontal FMAs on the VALU and no horizontal windows in LDS (cost_vt's
+//    6 ds_read_b128 per filter and item).
+// s_vh: per (plane, row) a 544-B block = hi row (256 B), lo row (256 B), 32 B pad:
+// the B reads (rows r, 8 B at column offsets {0, 16, 24, 40} B) are conflict-free
+// at a stride of 32 (mod 256) B; planes are 16 B apart mod 128 for the stores.
+// ----------------------------------------------------------------------------
+template <int DE, bool TRIM>
+__global__ __launch_bounds__(256, 6) void cost_mh_kernel(CostArgs a, int P_) {
+    constexpr int HALF = 10, RW = 128, TH = 8, TW = kMMTW;
+    constexpr int CP = 48;                    // bytes per region column (column-major indices)
+    constexpr int RB = 544;                   // bytes per (plane, row) block: hi, lo, pad
+    constexpr int PB = TH * RB + 16;          // bytes per plane
+    static_assert(TW == 8 * 12 && 12 * 7 + 32 <= RW, "tile");
+    __shared__ __attribute__((aligned(16))) uint8_t s_vh[4 * PB];
+    __shared__ uint32_t s_ox[kMaxK];
+    __shared__ uint2 s_oyz[kMaxK];
+    __shared__ __attribute__((aligned(16))) uint8_t s_idx[RW * CP];
+    __shared__ double s_red[4];
+    const int tid = threadIdx.x;
+    const Geom& g = a.g;
+    const TileItem cur = tile_item<TW, TH>(a, xcd_remap(blockIdx.x, a.band_tiles * P_), P_);
+    const int lane = tid & 63, wv = tid >> 6, lc = lane & 15, lk = lane >> 4;
+    const uint4* vfrag = a.vfrag16 + (TRIM ? 4 * 2 * 64 : 0) + lane;  // [trim][stack][hi,lo][lane]
+    const uint4* hfrag = a.hfrag16 + (TRIM ? 7 * 2 * 64 : 0) + lane;  // [trim][filter][hi,lo][lane]
+    TileFillT<HALF, CP> fill;  // region x0 - 10 .. x0 + 117
+    fill.issue(a, cur, tid);
+    const uint4 F0h = vfrag[0 * 64], F0l = vfrag[1 * 64], F1h = vfrag[2 * 64], F1l = vfrag[3 * 64];
+    s_ox[tid] = split_f16(fill.ov.x);  // every entry (zeros past K): rows 28-31 gather index 0
+    s_oyz[tid] = make_uint2(split_f16(fill.ov.y), split_f16(fill.ov.z));
+    fill.commit_idx(a, s_idx, tid);
+    __syncthreads();
+
+    // V pass: lane (c = lc, q = lk) gathers region rows 8q .. +7 of column 32 wv + 16 bb + c
+    const int colA = 32 * wv + lc;
+    const int colD = 32 * wv + 4 * lk;  // + 16 bb: this lane's 4 D columns
+    auto store_v = [&](const f32x4v& d, int plane_a, int plane_b, int col) {
+        const int plane = lc < 8 ? plane_a : plane_b;
+        if (plane < 0) return;
+        uint8_t* base = s_vh + plane * PB + (lc & 7) * RB + col * 2;
+        f16x4 h, l;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const float x = d[v] * kVToH;
+            h[v] = (_Float16)x;
+            l[v] = (_Float16)(x - (float)h[v]);
+        }
+        *reinterpret_cast<f16x4*>(base) = h;
+        *reinterpret_cast<f16x4*>(base + 256) = l;
+    };
+    // H pass: lane (n = lc, q = lk): output block ob = 2 wv + (n >> 3), row hr = n & 7,
+    // B = window columns 12 ob + 8q .. +7 of row hr
+    const int ob = 2 * wv + (lc >> 3), hr = lc & 7;
+    const uint8_t* hb = s_vh + hr * RB + (12 * ob + 8 * lk) * 2;
+    f32x4v D0 = {0.f, 0.f, 0.f, 0.f}, D1 = D0, D2 = D0;
+    // The two 8-B halves of a B fragment are separate ds_read_b64 (32-lane groups over
+    // 64 banks: conflict-free at this row stride); an opaque offset keeps the compiler
+    // from merging them into one ds_read2_b64 (16-lane groups over 32 banks: 2-way).
+    uint32_t o8 = 8, o256 = 256, o264 = 264;
+    asm volatile("" : "+v"(o8), "+v"(o256), "+v"(o264));
+    auto hpass = [&](int f, int plane, f32x4v& D) {
+        const uint4 fh = hfrag[(2 * f) * 64], fl = hfrag[(2 * f + 1) * 64];
+        const f16x8 ah = __builtin_bit_cast(f16x8, fh), al = __builtin_bit_cast(f16x8, fl);
+        const uint8_t* p = hb + plane * PB;
+        const f16x4 h0 = *reinterpret_cast<const f16x4*>(p), h1 = *reinterpret_cast<const f16x4*>(p + o8);
+        const f16x4 l0 = *reinterpret_cast<const f16x4*>(p + o256),
+                    l1 = *reinterpret_cast<const f16x4*>(p + o264);
+        const f16x8 bh = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+        const f16x8 bl = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+        D = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, D, 0, 0, 0);
+        D = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, D, 0, 0, 0);
+        D = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, D, 0, 0, 0);
+    };
+
+    // ---- group 0: channel 0 ----
+    {
+        const f16x8 t0h = __builtin_bit_cast(f16x8, F0h), t0l = __builtin_bit_cast(f16x8, F0l);
+        const f16x8 t1h = __builtin_bit_cast(f16x8, F1h), t1l = __builtin_bit_cast(f16x8, F1l);
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            const uint2 ix = *reinterpret_cast<const uint2*>(s_idx + (colA + 16 * bb) * CP + 8 * lk);
+            uint32_t w[8];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                w[jj] = s_ox[(ix.x >> (8 * jj)) & 0xffu];
+                w[4 + jj] = s_ox[(ix.y >> (8 * jj)) & 0xffu];
+            }
+            f16x8 xh, xl;
+            pack_b(w, xh, xl);
+            store_v(mfma3(xh, xl, t0h, t0l), 0, 1, colD + 16 * bb);
+            store_v(mfma3(xh, xl, t1h, t1l), 2, -1, colD + 16 * bb);
+        }
+    }
+    const uint4 F2h = vfrag[4 * 64], F2l = vfrag[5 * 64], F3h = vfrag[6 * 64], F3l = vfrag[7 * 64];
+    __syncthreads();
+    hpass(0, 0, D0);
+    hpass(1, 1, D0);
+    hpass(2, 2, D0);
+    __syncthreads();
+
+    // ---- group 1: channels 1, 2 ----
+    {
+        const f16x8 t2h = __builtin_bit_cast(f16x8, F2h), t2l = __builtin_bit_cast(f16x8, F2l);
+        const f16x8 t3h = __builtin_bit_cast(f16x8, F3h), t3l = __builtin_bit_cast(f16x8, F3l);
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            const uint2 ix = *reinterpret_cast<const uint2*>(s_idx + (colA + 16 * bb) * CP + 8 * lk);
+            uint32_t wy[8], wz[8];
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+                const uint2 e = s_oyz[((jj < 4 ? ix.x : ix.y) >> (8 * (jj & 3))) & 0xffu];
+                wy[jj] = e.x; wz[jj] = e.y;
+            }
+            f16x8 xh, xl;
+            pack_b(wy, xh, xl);
+            store_v(mfma3(xh, xl, t2h, t2l), 0, 1, colD + 16 * bb);
+            pack_b(wz, xh, xl);
+            store_v(mfma3(xh, xl, t3h, t3l), 2, 3, colD + 16 * bb);
         }
     }
     // LabRef of this lane's 4 outputs (row hr, columns 12 ob + 4 lk .. +3), in flight
@@ -2280,7 +3007,15 @@ static hipError_t launch_assign_pipe(const AssignArgs& a, int P, hipStream_t s) 
     return hipGetLastError();
 }
 
+static hipError_t launch_assign_lane(const AssignArgs& a, int P, hipStream_t s) {
+    const size_t lds = (size_t)4 * a.K * sizeof(float4);
+    const unsigned grid = (unsigned)(a.nblocks * ((P + 3) / 4));
+    hipLaunchKernelGGL(assign_lane_kernel, dim3(grid), dim3(256), lds, s, a, P);
+    return hipGetLastError();
+}
+
 hipError_t launch_assign(const AssignArgs& a, int P, int rep, int group, int batch, hipStream_t s) {
+    if (group == 4 && batch == 5) return launch_assign_lane(a, P, s);
     if (group == 4 && batch == 3) return launch_assign_pipe(a, P, s);
     if (group == 4 && batch == 1) return launch_assign_quad<1>(a, P, s);
     if (group == 4 && batch == 2) return launch_assign_quad<2>(a, P, s);
@@ -2430,18 +3165,18 @@ constexpr int kFastTW = kFastRW - 2 * kFastHalf;
 // tile rows of the fast path: cfg 0 = 16 (RV 8, 2 WG/CU); cfg 1 = 8 with the V
 // pass split by channel group (4 WG/CU); cfg 2 = 8 (RV 4, 4 WG/CU); cfg 3 = 8
 // with the V pass on the matrix cores
-int fast_tile_rows(int tile_cfg) { return tile_cfg == 0 ? kFastTH : 8; }  // cfg 1-8: 8 rows
+int fast_tile_rows(int tile_cfg) { return tile_cfg == 0 ? kFastTH : 8; }  // cfg 1-11: 8 rows
 
 void fast_tile_dims(int W, int own_rows, int tile_cfg, int* tiles_x, int* ntiles) {
     const int th = fast_tile_rows(tile_cfg);
-    const int tw = tile_cfg == 8 ? kMMTW : kFastTW;
+    const int tw = (tile_cfg == 8 || tile_cfg == 10) ? kMMTW : kFastTW;
     *tiles_x = (W + tw - 1) / tw;
     *ntiles = *tiles_x * ((own_rows + th - 1) / th);
 }
 
 template <int TH, int RV, int OCC, bool TRIM, int VMODE>
 static void launch_tile_cfg(const CostArgs& a, int P, int de, hipStream_t s) {
-    const dim3 grid((unsigned)(a.ntiles * P));
+    const dim3 grid((unsigned)(a.band_tiles * P));
     if (de == 0)
         hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, 0, OCC, TRIM, VMODE>), grid,
                            dim3(256), 0, s, a, P);
@@ -2482,10 +3217,10 @@ void build_fast_taps(const float* k1, const float* k2, const float* k3, const fl
 hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, int tile_cfg, bool trim,
                             hipStream_t s) {
     CostArgs a = a0;
-    if (tile_cfg == 3 || tile_cfg == 7)  // matrix-core V passes: outputs carry 2^30
+    if (tile_cfg == 3 || tile_cfg == 7 || tile_cfg == 9 || tile_cfg == 11)  // matrix-core V passes: x 2^30
         a.taps = static_cast<const char*>(a0.taps) + sizeof(CostTaps<10>);
     if (tile_cfg == 4 || tile_cfg == 5) {
-        const dim3 grid((unsigned)(a.ntiles * P));
+        const dim3 grid((unsigned)(a.band_tiles * P));
 #define HQ_PAIR(DEV, TR, HRV) hipLaunchKernelGGL((cost_pair_kernel<DEV, TR, HRV>), grid, dim3(256), 0, s, a, P)
         if (tile_cfg == 4) {
             if (de == 0) { if (trim) HQ_PAIR(0, true, 2); else HQ_PAIR(0, false, 2); }
@@ -2496,20 +3231,39 @@ hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, int tile_cfg, boo
         }
 #undef HQ_PAIR
     } else if (tile_cfg == 6) {
-        const dim3 grid((unsigned)(a.ntiles * P));
+        const dim3 grid((unsigned)(a.band_tiles * P));
 #define HQ_CHAN(DEV, TR) hipLaunchKernelGGL((cost_chan_kernel<DEV, TR>), grid, dim3(256), 0, s, a, P)
         if (de == 0) { if (trim) HQ_CHAN(0, true); else HQ_CHAN(0, false); }
         else { if (trim) HQ_CHAN(1, true); else HQ_CHAN(1, false); }
 #undef HQ_CHAN
     } else if (tile_cfg == 7) {
-        const dim3 grid((unsigned)(a.ntiles * P));
+        const dim3 grid((unsigned)(a.band_tiles * P));
 #define HQ_MFMA(DEV, TR) hipLaunchKernelGGL((cost_mfma_kernel<DEV, TR>), grid, dim3(256), 0, s, a, P)
         if (de == 0) { if (trim) HQ_MFMA(0, true); else HQ_MFMA(0, false); }
         else { if (trim) HQ_MFMA(1, true); else HQ_MFMA(1, false); }
 #undef HQ_MFMA
+    } else if (tile_cfg == 11) {
+        const dim3 grid((unsigned)(a.band_tiles * P));
+#define HQ_WIDE(DEV, TR) hipLaunchKernelGGL((cost_wide_kernel<DEV, TR>), grid, dim3(256), 0, s, a, P)
+        if (de == 0) { if (trim) HQ_WIDE(0, true); else HQ_WIDE(0, false); }
+        else { if (trim) HQ_WIDE(1, true); else HQ_WIDE(1, false); }
+#undef HQ_WIDE
+    } else if (tile_cfg == 9) {
+        const dim3 grid((unsigned)(a.band_tiles * P));
+#define HQ_VT(DEV, TR) hipLaunchKernelGGL((cost_vt_kernel<DEV, TR>), grid, dim3(256), 0, s, a, P)
+        if (de == 0) { if (trim) HQ_VT(0, true); else HQ_VT(0, false); }
+        else { if (trim) HQ_VT(1, true); else HQ_VT(1, false); }
+#undef HQ_VT
+    } else if (tile_cfg == 10) {
+        for (int i = 0; i < 9; ++i) a.m_lab[i] *= kHOutScale;  // H outputs carry 2^28 (exact)
+        const dim3 grid((unsigned)(a.band_tiles * P));
+#define HQ_MH(DEV, TR) hipLaunchKernelGGL((cost_mh_kernel<DEV, TR>), grid, dim3(256), 0, s, a, P)
+        if (de == 0) { if (trim) HQ_MH(0, true); else HQ_MH(0, false); }
+        else { if (trim) HQ_MH(1, true); else HQ_MH(1, false); }
+#undef HQ_MH
     } else if (tile_cfg == 8) {
         for (int i = 0; i < 9; ++i) a.m_lab[i] *= kHOutScale;  // H outputs carry 2^28 (exact)
-        const dim3 grid((unsigned)(a.ntiles * P));
+        const dim3 grid((unsigned)(a.band_tiles * P));
 #define HQ_MM(DEV, TR) hipLaunchKernelGGL((cost_mm_kernel<DEV, TR>), grid, dim3(256), 0, s, a, P)
         if (de == 0) { if (trim) HQ_MM(0, true); else HQ_MM(0, false); }
         else { if (trim) HQ_MM(1, true); else HQ_MM(1, false); }

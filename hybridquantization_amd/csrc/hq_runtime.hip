@@ -23,6 +23,7 @@ hipError_t launch_prep_palette(const PaletteArgs&, int P, hipStream_t);
 hipError_t launch_build_grid(const GridArgs&, int P, hipStream_t);
 hipError_t launch_assign(const AssignArgs&, int P, int rep, int group, int batch, hipStream_t);
 void fast_tile_dims(int W, int own_rows, int tile_cfg, int* tiles_x, int* ntiles);
+int fast_tile_rows(int tile_cfg);
 void opp2xyz_over_illum(const float inv_illum[3], float m[9]);
 void build_vpass_fragments(const float* k1, const float* k2, const float* k3,
                            const float* absk3, uint16_t* out);
@@ -129,6 +130,8 @@ struct hq_ctx {
                            // 6 = row-pair in two channel groups (6 workgroups per CU),
                            // 7 = 6 with the vertical passes on the matrix cores (split f16; default),
                            // 8 = both passes on the matrix cores (96-column tiles)
+    int bands = 0;         // row bands of the assign -> cost pipeline (0/1 = one pass, serial)
+    int band_cpb = 2;      // banded assign: pixel chunks per block (blocks = chunks / cpb)
     int trim = 1;          // skip taps < 1e-9 of the peak of the narrow k1 filters
     bool trim_ok = false;  // set by hq_set_filters (default 21-tap filter set)
 
@@ -141,6 +144,23 @@ struct hq_ctx {
     ProfSlot prof_assign, prof_cost, prof_grid, prof_finalize;
     hipEvent_t ev[6] = {};
     int num_cu = 256;
+
+    // banded pipeline: assign of band j+1 (stream2) runs beside cost of band j (stream)
+    hipStream_t stream2 = nullptr;
+    hipEvent_t bev[kMaxBands + 1] = {};     // no timing: band j's indices written / grid ready
+    hipEvent_t pev[2 * kMaxBands + 2] = {};  // timing (profiling): per-band cost spans
+};
+
+// Row bands of the assign -> cost pipeline.  Cost band j covers tile rows
+// [t0, t1) of the shard; its index rows reach half rows past them, so assign
+// band j covers the extended rows [end(j-1), end(j)) with end(j) = the last row
+// cost band j reads: cost band j depends on assign bands <= j only.
+struct BandPlan {
+    int n = 1;
+    int64_t q0[kMaxBands], q1[kMaxBands];  // pixel range (extended rows) of assign band j
+    int blocks[kMaxBands], moff[kMaxBands];  // assign blocks per palette, used-mask offset
+    int t0[kMaxBands], t1[kMaxBands];        // cost tile range
+    int mask_blocks = 0;
 };
 
 struct hq_search {
@@ -309,6 +329,40 @@ int check_geom_args(hq_ctx* c, int w, int h, int r0, int r1) {
     return HQ_OK;
 }
 
+BandPlan plan_bands(const hq_ctx* c) {
+    const Geom& g = c->g;
+    BandPlan b;
+    int tiles_x, ntiles;
+    fast_tile_dims(g.W, g.r1 - g.r0, c->tile_cfg, &tiles_x, &ntiles);
+    const int trows = ntiles / tiles_x, th = fast_tile_rows(c->tile_cfg);
+    const int nblocks = c->num_cu * c->assign_blocks_per_cu;
+    const bool fast = c->cost_variant != 1 && c->half == 10;
+    b.n = fast ? std::max(1, std::min({c->bands, kMaxBands, trows})) : 1;
+    if (b.n == 1) {
+        b.q0[0] = 0; b.q1[0] = g.n_ext;
+        b.blocks[0] = nblocks; b.moff[0] = 0;
+        b.t0[0] = 0; b.t1[0] = ntiles;
+        b.mask_blocks = nblocks;
+        return b;
+    }
+    const int64_t chunk = 256 * 8;  // assign_pipe_kernel: 256 threads x PPT pixels
+    int row = g.e0;
+    for (int j = 0; j < b.n; ++j) {
+        const int tr0 = (int)((int64_t)trows * j / b.n), tr1 = (int)((int64_t)trows * (j + 1) / b.n);
+        const int end = j + 1 == b.n ? g.e1 : std::min(g.e1, std::max(row, g.r0 + th * tr1 + c->half));
+        b.q0[j] = (int64_t)(row - g.e0) * g.W;
+        b.q1[j] = (int64_t)(end - g.e0) * g.W;
+        const int64_t chunks = (b.q1[j] - b.q0[j] + chunk - 1) / chunk;
+        b.blocks[j] = (int)std::min<int64_t>(nblocks, (chunks + c->band_cpb - 1) / c->band_cpb);
+        b.moff[j] = b.mask_blocks;
+        b.mask_blocks += b.blocks[j];
+        b.t0[j] = tr0 * tiles_x;
+        b.t1[j] = tr1 * tiles_x;
+        row = end;
+    }
+    return b;
+}
+
 // Ensure population buffers for P palettes of K colours.
 int ensure_population(hq_ctx* c, int P, int K) {
     const Geom& g = c->g;
@@ -330,7 +384,8 @@ int ensure_population(hq_ctx* c, int P, int K) {
     HIP_TRY(c, c->d_lvl1.ensure((size_t)P * l1p));
     HIP_TRY(c, c->d_lvl2.ensure((size_t)((P + 3) / 4) * l2g));
     HIP_TRY(c, c->d_idx.ensure((size_t)P * g.idx_pitch));
-    HIP_TRY(c, c->d_used_mask.ensure(sizeof(uint32_t) * 8 * (size_t)P * nblocks));
+    const BandPlan bp = plan_bands(c);
+    HIP_TRY(c, c->d_used_mask.ensure(sizeof(uint32_t) * 8 * (size_t)P * std::max(nblocks, bp.mask_blocks)));
     HIP_TRY(c, c->d_partial.ensure(sizeof(double) * (size_t)P * nparts));
     HIP_TRY(c, c->d_out.ensure(sizeof(double) * (size_t)P * (1 + K)));
     return ensure_pinned(c, sizeof(float) * 4 * (size_t)P * K, sizeof(double) * (size_t)P * (1 + K));
@@ -366,19 +421,18 @@ int enqueue_eval(hq_ctx* c, int P, int K) {
         HIP_TRY(c, launch_build_grid(ga, P, s));
     }
     if (c->prof) HIP_TRY(c, hipEventRecord(c->ev[1], s));
+    const BandPlan bp = plan_bands(c);
     AssignArgs aa{c->d_R.as<float>(), c->d_G.as<float>(), c->d_B.as<float>(), c->d_pal.as<float4>(),
                   c->d_pflags.as<int>(), c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(),
                   c->d_idx.as<uint8_t>(), c->d_used_mask.as<uint32_t>(), g.n_ext, g.idx_pitch,
-                  l1p, l2g, K, c->G2, nblocks};
-    HIP_TRY(c, launch_assign(aa, P, c->assign_rep, c->assign_group, c->assign_batch, s));
-    if (c->prof) HIP_TRY(c, hipEventRecord(c->ev[2], s));
+                  l1p, l2g, K, c->G2, nblocks, bp.mask_blocks, 0};
     int tiles_x, ntiles;
     fast_tile_dims(g.W, g.r1 - g.r0, c->tile_cfg, &tiles_x, &ntiles);
     const float inv[3] = {1.0f / c->illum[0], 1.0f / c->illum[1], 1.0f / c->illum[2]};
     int nparts;
     const bool fast = c->cost_variant != 1 && c->half == 10;
+    CostArgs ca{};
     if (fast) {
-        CostArgs ca{};
         ca.idx = c->d_idx.as<uint8_t>();
         ca.opp = c->d_opp.as<float4>();
         ca.vfrag = c->d_vfrag.as<uint4>();
@@ -392,36 +446,78 @@ int enqueue_eval(hq_ctx* c, int P, int K) {
         ca.K = K;
         ca.tiles_x = tiles_x;
         ca.ntiles = ntiles;
+        ca.tile0 = 0;
+        ca.band_tiles = ntiles;
         opp2xyz_over_illum(inv, ca.m_lab);
         ca.taps = c->d_taps.p;
-        HIP_TRY(c, launch_cost_fast(ca, P, c->de_type, c->tile_cfg, c->trim && c->trim_ok, s));
+    }
+    if (bp.n > 1) {
+        // Banded pipeline: assign bands run back to back on stream2; cost band j
+        // waits for assign band j (the last one its index rows need) and runs on
+        // `s` beside assign band j+1, so the latency-bound assign shares the CUs
+        // with the VALU/LDS-bound cost kernel instead of running alone.
+        hipStream_t s2 = c->stream2;
+        HIP_TRY(c, hipEventRecord(c->bev[kMaxBands], s));  // palettes + grid ready
+        HIP_TRY(c, hipStreamWaitEvent(s2, c->bev[kMaxBands], 0));
+        for (int j = 0; j < bp.n; ++j) {
+            if (bp.blocks[j] > 0) {
+                AssignArgs ab = aa;
+                ab.R = aa.R + bp.q0[j];
+                ab.G = aa.G + bp.q0[j];
+                ab.B = aa.B + bp.q0[j];
+                ab.idx = aa.idx + bp.q0[j];
+                ab.n_ext = bp.q1[j] - bp.q0[j];
+                ab.nblocks = bp.blocks[j];
+                ab.mask_off = bp.moff[j];
+                HIP_TRY(c, launch_assign(ab, P, c->assign_rep, c->assign_group, c->assign_batch, s2));
+            }
+            HIP_TRY(c, hipEventRecord(c->bev[j], s2));
+        }
+        for (int j = 0; j < bp.n; ++j) {
+            HIP_TRY(c, hipStreamWaitEvent(s, c->bev[j], 0));
+            if (bp.t1[j] == bp.t0[j]) continue;
+            CostArgs cb = ca;
+            cb.tile0 = bp.t0[j];
+            cb.band_tiles = bp.t1[j] - bp.t0[j];
+            if (c->prof) HIP_TRY(c, hipEventRecord(c->pev[2 * j], s));
+            HIP_TRY(c, launch_cost_fast(cb, P, c->de_type, c->tile_cfg, c->trim && c->trim_ok, s));
+            if (c->prof) HIP_TRY(c, hipEventRecord(c->pev[2 * j + 1], s));
+        }
         nparts = ntiles;
+        if (c->prof) HIP_TRY(c, hipEventRecord(c->ev[2], s));  // assign + cost span
     } else {
-        HIP_TRY(c, c->d_gen_t.ensure(sizeof(float) * 7 * (size_t)g.n_ext));
-        const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
-        nparts = (int)((n_own + 255) / 256);
-        for (int p = 0; p < P; ++p) {
-            GenArgs ga{};
-            ga.idx = c->d_idx.as<uint8_t>() + (int64_t)p * g.idx_pitch;
-            ga.opp = c->d_opp.as<float4>() + (int64_t)p * kMaxK;
-            ga.k1 = c->d_k1.as<float>();
-            ga.k2 = c->d_k2.as<float>();
-            ga.k3 = c->d_k3.as<float>();
-            ga.absk3 = c->d_absk3.as<float>();
-            ga.t = c->d_gen_t.as<float>();
-            ga.labL = c->d_labL.as<float>();
-            ga.labA = c->d_labA.as<float>();
-            ga.labB = c->d_labB.as<float>();
-            ga.partial = c->d_partial.as<double>() + (int64_t)p * nparts;
-            ga.g = g;
-            ga.half = c->half;
-            opp2xyz_over_illum(inv, ga.m_lab);
-            HIP_TRY(c, launch_cost_generic(ga, c->de_type, s));
+        HIP_TRY(c, launch_assign(aa, P, c->assign_rep, c->assign_group, c->assign_batch, s));
+        if (c->prof) HIP_TRY(c, hipEventRecord(c->ev[2], s));
+        if (fast) {
+            HIP_TRY(c, launch_cost_fast(ca, P, c->de_type, c->tile_cfg, c->trim && c->trim_ok, s));
+            nparts = ntiles;
+        } else {
+            HIP_TRY(c, c->d_gen_t.ensure(sizeof(float) * 7 * (size_t)g.n_ext));
+            const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
+            nparts = (int)((n_own + 255) / 256);
+            for (int p = 0; p < P; ++p) {
+                GenArgs ga{};
+                ga.idx = c->d_idx.as<uint8_t>() + (int64_t)p * g.idx_pitch;
+                ga.opp = c->d_opp.as<float4>() + (int64_t)p * kMaxK;
+                ga.k1 = c->d_k1.as<float>();
+                ga.k2 = c->d_k2.as<float>();
+                ga.k3 = c->d_k3.as<float>();
+                ga.absk3 = c->d_absk3.as<float>();
+                ga.t = c->d_gen_t.as<float>();
+                ga.labL = c->d_labL.as<float>();
+                ga.labA = c->d_labA.as<float>();
+                ga.labB = c->d_labB.as<float>();
+                ga.partial = c->d_partial.as<double>() + (int64_t)p * nparts;
+                ga.g = g;
+                ga.half = c->half;
+                opp2xyz_over_illum(inv, ga.m_lab);
+                HIP_TRY(c, launch_cost_generic(ga, c->de_type, s));
+            }
         }
     }
     if (c->prof) HIP_TRY(c, hipEventRecord(c->ev[3], s));
     FinalizeArgs fa{c->d_partial.as<double>(), c->d_used_mask.as<uint32_t>(), c->d_out.as<double>(),
-                    nparts, nblocks, K};
+                    nparts, bp.mask_blocks, K};
     HIP_TRY(c, launch_finalize(fa, P, s));
     if (c->prof) HIP_TRY(c, hipEventRecord(c->ev[4], s));
     if (c->comm) {  // also with one rank (a no-op copy), so that path is exercised on one GPU
@@ -433,8 +529,14 @@ int enqueue_eval(hq_ctx* c, int P, int K) {
     HIP_TRY(c, hipStreamSynchronize(s));
     if (c->prof) {
         prof_add(c, c->prof_grid, c->ev[0], c->ev[1]);
-        prof_add(c, c->prof_assign, c->ev[1], c->ev[2]);
-        prof_add(c, c->prof_cost, c->ev[2], c->ev[3]);
+        if (bp.n > 1) {  // overlapped: "assign" = the assign + cost span, "cost" = per-band launches
+            prof_add(c, c->prof_assign, c->ev[1], c->ev[2]);
+            for (int j = 0; j < bp.n; ++j)
+                if (bp.t1[j] > bp.t0[j]) prof_add(c, c->prof_cost, c->pev[2 * j], c->pev[2 * j + 1]);
+        } else {
+            prof_add(c, c->prof_assign, c->ev[1], c->ev[2]);
+            prof_add(c, c->prof_cost, c->ev[2], c->ev[3]);
+        }
         prof_add(c, c->prof_finalize, c->ev[3], c->ev[4]);
     }
     c->last_P = P;
@@ -511,6 +613,12 @@ int hq_create(int device, int delta_e_type, hq_ctx** out) {
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         c->num_cu = prop.multiProcessorCount;
     for (auto& e : c->ev) (void)hipEventCreate(&e);
+    for (auto& e : c->pev) (void)hipEventCreate(&e);
+    for (auto& e : c->bev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
+        hq_destroy(c);
+        return HQ_ERR_DEVICE;
+    }
     *out = c;
     return HQ_OK;
 }
@@ -530,6 +638,11 @@ void hq_destroy(hq_ctx* c) {
     if (c->h_out) (void)hipHostFree(c->h_out);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
+    for (auto& e : c->pev)
+        if (e) (void)hipEventDestroy(e);
+    for (auto& e : c->bev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->stream2) (void)hipStreamSynchronize(c->stream2), (void)hipStreamDestroy(c->stream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -892,19 +1005,25 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
     } else if (!std::strcmp(name, "trim")) {
         c->trim = value != 0;
     } else if (!std::strcmp(name, "cost_tile")) {
-        if (value < 0 || value > 8) return fail(c, HQ_ERR_ARG, "cost_tile in 0..8");
+        if (value < 0 || value > 11) return fail(c, HQ_ERR_ARG, "cost_tile in 0..11");
         c->tile_cfg = value;
     } else if (!std::strcmp(name, "assign_group")) {
         if (value != 1 && value != 2 && value != 4) return fail(c, HQ_ERR_ARG, "assign_group in {1,2,4}");
         c->assign_group = value;
     } else if (!std::strcmp(name, "assign_batch")) {
-        if (value < 0 || value > 8 || value == 5 || value == 6 || value == 7)
-            return fail(c, HQ_ERR_ARG, "assign_batch in {0,1,2,3,4,8}");
+        if (value < 0 || value > 8 || value == 6 || value == 7 || (value == 5 && c->assign_group != 4))
+            return fail(c, HQ_ERR_ARG, "assign_batch in {0,1,2,3,4,8} (5: group 4)");
         c->assign_batch = value;
     } else if (!std::strcmp(name, "assign_rep")) {
         if (value != 1 && value != 2 && value != 4 && value != 16)
             return fail(c, HQ_ERR_ARG, "assign_rep in {1,2,4,16}");
         c->assign_rep = value;
+    } else if (!std::strcmp(name, "bands")) {
+        if (value < 0 || value > kMaxBands) return fail(c, HQ_ERR_ARG, "bands in [0,%d]", kMaxBands);
+        c->bands = value;
+    } else if (!std::strcmp(name, "band_cpb")) {
+        if (value < 1 || value > 64) return fail(c, HQ_ERR_ARG, "band_cpb in [1,64]");
+        c->band_cpb = value;
     } else if (!std::strcmp(name, "assign_blocks_per_cu")) {
         if (value < 1 || value > 64) return fail(c, HQ_ERR_ARG, "assign_blocks_per_cu in [1,64]");
         c->assign_blocks_per_cu = value;

@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--group", type=int, default=4)
     ap.add_argument("--batch", type=int, default=3)
     ap.add_argument("--bpc", type=int, default=0, help="assign workgroups per CU (0 = library default)")
+    ap.add_argument("--bands", type=int, default=-1, help="banded assign/cost pipeline (-1 = library default)")
+    ap.add_argument("--cpb", type=int, default=0, help="banded assign: chunks per block (0 = default)")
     ap.add_argument("--lib", default=None, help="alternative libhq build (scripts/ablate.py)")
     args = ap.parse_args()
     if args.lib:
@@ -50,6 +52,10 @@ def main():
     m.setOption("assign_batch", args.batch)
     if args.bpc:
         m.setOption("assign_blocks_per_cu", args.bpc)
+    if args.bands >= 0:
+        m.setOption("bands", args.bands)
+    if args.cpb:
+        m.setOption("band_cpb", args.cpb)
     W = H = args.size
     R, G, B = synthetic_planes(W, H, 1)
     _lib.check(lib.hq_set_image_planar_shard(m.ctx, _lib.fptr(R), _lib.fptr(G), _lib.fptr(B), W, H,
@@ -76,7 +82,7 @@ def main():
         n = C.c_int64()
         lib.hq_profile_get(m.ctx, k.encode(), C.byref(ms), C.byref(n))
         out.append(f"{k}={ms.value / max(n.value, 1):.4f}ms")
-    print(f"{os.path.basename(args.lib or 'libhq.so')} size={W} K={args.K} P={args.P} grid={args.grid} variant={args.variant} tile={args.tile} rep={args.rep} trim={args.trim} group={args.group} batch={args.batch} bpc={args.bpc}: "
+    print(f"{os.path.basename(args.lib or 'libhq.so')} size={W} K={args.K} P={args.P} grid={args.grid} variant={args.variant} tile={args.tile} rep={args.rep} trim={args.trim} group={args.group} batch={args.batch} bpc={args.bpc} bands={args.bands} cpb={args.cpb}: "
           f"{el / args.evals * 1e3:.3f} ms/eval-population, "
           f"{W * H * args.P * args.evals / el / 1e6:.1f} Mpx*evals/s  ", " ".join(out),
           "costs", costs.tolist())

@@ -74,7 +74,7 @@ def test_labref_256_checksum(ip):
 # Candidate evaluation (IM:620-727): golden fixtures
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("grid", [64, 32, 16, 0])
-@pytest.mark.parametrize("variant", [(0, 7), (0, 8), (0, 6), (0, 4), (0, 5), (0, 2), (0, 0), (0, 1), (0, 3), (1, 0)])
+@pytest.mark.parametrize("variant", [(0, 11), (0, 10), (0, 9), (0, 7), (0, 8), (0, 6), (0, 4), (0, 5), (0, 2), (0, 0), (0, 1), (0, 3), (1, 0)])
 @pytest.mark.parametrize("name", ["case_64x48_k16", "case_97x53_k64"])
 def test_eval_golden(ip, name, grid, variant):
     """(cost_variant, cost_tile): 8-row tiles with the row-pair horizontal pass
@@ -96,6 +96,31 @@ def test_eval_golden(ip, name, grid, variant):
     np.testing.assert_array_equal(used, g["used"])
     for p in range(len(pals)):
         np.testing.assert_array_equal(ip.getIndices(p), g["idx"][p])
+
+
+@pytest.mark.parametrize("bands", [2, 3, 16])
+@pytest.mark.parametrize("tile", [11, 10, 9, 7, 6, 8])
+@pytest.mark.parametrize("name", ["case_64x48_k16", "case_97x53_k64"])
+def test_eval_golden_banded(ip, name, tile, bands):
+    """The banded pipeline (assign of row band j+1 on a second stream beside the
+    cost of band j) gives the unbanded results bit for bit: same indices, same
+    per-tile partials summed in the same order, same used masks."""
+    g, R, G, B = load_case(name)
+    w = int(g["w"])
+    ip.setOption("cost_tile", tile)
+    ip.setOption("bands", bands)
+    ip.setOption("band_cpb", 1 + bands % 3)
+    ip.setImage(o.inline_rgba(R, G, B).reshape(-1), g["lab"].reshape(-1), w, ip.illum)
+    pals = g["palettes"]
+    costs, used = ip.computeQuantizationErrorPopulation(pals.reshape(len(pals), -1), 2.0,
+                                                        return_used=True)
+    np.testing.assert_allclose(costs, g["costs"], rtol=1e-6)
+    np.testing.assert_array_equal(used, g["used"])
+    for p in range(len(pals)):
+        np.testing.assert_array_equal(ip.getIndices(p), g["idx"][p])
+    ip.setOption("bands", 0)
+    c0 = ip.computeQuantizationErrorPopulation(pals.reshape(len(pals), -1), 2.0)
+    np.testing.assert_array_equal(costs, c0)
 
 
 def test_eval_config1_256_k16(ip):
@@ -138,12 +163,15 @@ def test_mfma_passes_match_valu(gpu, de, trim):
     pals = [o.synthetic_palette(K, 7 + K) for K in (16, 64, 256)]
     m.setOption("trim", trim)
     out = {}
-    for tile in (6, 7, 8):
+    for tile in (6, 7, 8, 9, 10, 11):
         m.setOption("cost_tile", tile)
         out[tile] = np.array([m.computeQuantizationErrorPopulation([p.reshape(-1)], 2.0)[0]
                               for p in pals])
     np.testing.assert_allclose(out[7], out[6], rtol=1e-6)
     np.testing.assert_allclose(out[8], out[6], rtol=1e-6)
+    np.testing.assert_allclose(out[9], out[6], rtol=1e-6)
+    np.testing.assert_allclose(out[10], out[6], rtol=1e-6)
+    np.testing.assert_allclose(out[11], out[6], rtol=1e-6)
     m.close()
 
 
@@ -151,7 +179,7 @@ def test_mfma_passes_match_valu(gpu, de, trim):
 # argmin edge cases (CL:179-193), bit-exact
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("grid", [64, 32, 16, 0])
-@pytest.mark.parametrize("group_batch", [(1, 0), (1, 4), (1, 8), (4, 1), (4, 2), (4, 3)])
+@pytest.mark.parametrize("group_batch", [(1, 0), (1, 4), (1, 8), (4, 1), (4, 2), (4, 3), (4, 5)])
 def test_assign_edge_cases(ip, grid, group_batch):
     g = np.load(os.path.join(GOLD, "edge_assign.npz"))
     px = g["px"]  # 4096 pixels -> 64 x 64 image, values partly outside [0, 1]
@@ -183,7 +211,8 @@ def test_assign_random_and_near_ties(ip, K):
                                     (16, 4, 2, 0), (0, 1, 16, 0), (32, 1, 1, 4), (32, 1, 1, 8),
                                     (64, 1, 1, 8), (0, 1, 1, 4), (32, 4, 1, 1), (32, 4, 1, 2),
                                     (64, 4, 1, 2), (16, 4, 1, 1), (0, 4, 1, 2), (32, 4, 1, 3),
-                                    (64, 4, 1, 3), (0, 4, 1, 3)):
+                                    (64, 4, 1, 3), (0, 4, 1, 3), (32, 4, 1, 5), (64, 4, 1, 5),
+                                    (16, 4, 1, 5), (0, 4, 1, 5)):
         ip.setOption("grid", grid)
         ip.setOption("assign_group", group)
         ip.setOption("assign_rep", rep)
@@ -196,6 +225,26 @@ def test_assign_random_and_near_ties(ip, K):
         rev_idx, rev_used = c_oracle.assign(px, pal[::-1].copy())
         np.testing.assert_array_equal(ip.getIndices(1), rev_idx.astype(np.uint8))
         np.testing.assert_array_equal(used[1], rev_used)
+
+
+@pytest.mark.parametrize("batch", [5, 3])
+@pytest.mark.parametrize("P", [1, 2, 5, 8])
+def test_assign_group_sizes(ip, P, batch):
+    """Groups of 1-4 palettes per pixel pass (P = 5: a full group and a group of
+    one; the lane kernel then runs 64 / ng pixels per wave instruction)."""
+    rng = np.random.default_rng(P)
+    w, h, K = 75, 41, 96
+    px = np.zeros((w * h, 4), np.float32)
+    px[:, :3] = (rng.integers(0, 256, (w * h, 3)) / 255.0).astype(np.float32)
+    pals = np.stack([o.synthetic_palette(K, 300 + p) for p in range(P)])
+    ip.setOption("assign_group", 4)
+    ip.setOption("assign_batch", batch)
+    ip.setImage(px.reshape(-1), np.zeros_like(px).reshape(-1), w, ip.illum)
+    _, used = ip.computeQuantizationErrorPopulation(pals.reshape(P, -1), 2.0, return_used=True)
+    for p in range(P):
+        ref_idx, ref_used = c_oracle.assign(px, pals[p])
+        np.testing.assert_array_equal(ip.getIndices(p), ref_idx.astype(np.uint8))
+        np.testing.assert_array_equal(used[p], ref_used)
 
 
 def test_nonfinite_palette_falls_back_exactly(ip):
@@ -232,6 +281,7 @@ def test_row_block_shards_sum_to_full(gpu, filt):
             sh = hq.ImageManipulation(device=gpu)
             hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, sh)
             sh.setImage(rgba, None, w, filt.illum, row_begin=r0, row_end=r1)
+            sh.setOption("bands", nshards)  # banded pipeline inside a shard
             part = np.zeros(P * (1 + K))
             hq._lib.check(lib.hq_eval_population_partial(sh.ctx, hq._lib.fptr(pals), P, K,
                                                          hq._lib.dptr(part)), sh.ctx)
@@ -339,8 +389,19 @@ def test_full_size_properties(gpu, filt):
     c3 = m.computeQuantizationErrorPopulation(pals, 2.0)
     np.testing.assert_array_equal(m.getIndices(1), idx1)  # pruned == exhaustive argmin
     np.testing.assert_array_equal(c3, c1)
+    for bands in (2, 5, 16):  # banded pipeline: bit-identical
+        m.setOption("bands", bands)
+        cb = m.computeQuantizationErrorPopulation(pals, 2.0)
+        np.testing.assert_array_equal(m.getIndices(1), idx1)
+        np.testing.assert_array_equal(cb, c1)
+    m.setOption("bands", 0)
+    for batch in (3, 5):  # assign: pixel-per-lane and (pixel, palette)-per-lane pipelines
+        m.setOption("assign_batch", batch)
+        cb = m.computeQuantizationErrorPopulation(pals, 2.0)
+        np.testing.assert_array_equal(m.getIndices(1), idx1)
+        np.testing.assert_array_equal(cb, c1)
     m.setOption("grid", 64)
-    for variant, tile in ((1, 0), (0, 0), (0, 1), (0, 2), (0, 3), (0, 4), (0, 5), (0, 6), (0, 8)):
+    for variant, tile in ((1, 0), (0, 0), (0, 1), (0, 2), (0, 3), (0, 4), (0, 5), (0, 6), (0, 8), (0, 9), (0, 10), (0, 11)):
         m.setOption("cost_variant", variant)
         m.setOption("cost_tile", tile)
         c4 = m.computeQuantizationErrorPopulation(pals, 2.0)
