@@ -183,10 +183,14 @@ bool Swasa::is_accepted(double delta_e) {
     return delta_e <= 0 || std::exp(-delta_e / (double)temperature_) > rng_.next_double();
 }
 
-bool Swasa::keeps_his_values(int iteration) {
+double Swasa::keep_threshold(int iteration) const {
     const float num = (float)iteration - p_.conv_delay * (float)p_.imax;
     const float den = p_.conv_spread * (float)p_.imax;
-    return -(std::tanh((double)(num / den))) / 2 + 0.5 > rng_.next_double();
+    return -(std::tanh((double)(num / den))) / 2 + 0.5;
+}
+
+bool Swasa::keeps_his_values(int iteration) {
+    return keep_threshold(iteration) > rng_.next_double();
 }
 
 float Swasa::max_step_width(int i) const {

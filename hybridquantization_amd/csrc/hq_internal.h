@@ -46,6 +46,37 @@ struct PaletteArgs {
     int K;
 };
 
+constexpr int kSaMaxP = 64;       // device-resident SWASA: largest population
+
+// sa_step_kernel: one accept + generate step of the device-resident SWASA search.
+struct SaArgs {
+    const double* out;      // [P][1+K] finalize sums + used flags of the last evaluation
+    const float* colors_in; // [P][4K] accepted palettes (ping)
+    float* colors_out;      // (pong)
+    const float* cand_in;   // [P][4K] candidates just evaluated
+    float* cand_out;        // [P][4K] next candidates (generate)
+    const double* err_in;   // [P] current errors
+    double* err_out;
+    const uint64_t* seed_in;  // java.util.Random state
+    uint64_t* seed_out;
+    double* best_err;       // [1]
+    float* best_colors;     // [4K]
+    const uint64_t* jump_A; // LCG jumps: n steps = A_n s + C_n mod 2^48, n = 0 .. 3K*P
+    const uint64_t* jump_C;
+    PaletteArgs prep;       // outputs of the palette prep of the next candidates
+    double n_total;         // pixels of the whole image
+    double keep_threshold;  // SW:59-62 -(tanh(num/den))/2 + 0.5 at the accepted iteration
+    float temperature;      // SW:54-57 temperature at the accepted iteration
+    float amax;             // SW:91-101 max_step_width(ite) / 256 for the generated iteration
+    float delta;            // SW:74-82 penalty per unused colour
+    int P, K;
+    int accept;             // 1: accept the evaluated population first
+    int init;               // accept as IM:490-493 (initial population) instead
+    int generate;           // 1: generate the next candidates (and prep them)
+    int random;             // generate SW:40-52 random colours instead of neighbours
+    int convergence;
+};
+
 struct GridArgs {
     const float4* pal;
     const uint8_t* dup;

@@ -185,22 +185,21 @@ __device__ __forceinline__ int xcd_remap(int b, int N) {
     return x * q + min(x, r) + s;
 }
 
-__global__ __launch_bounds__(1024) void prep_palette_kernel(PaletteArgs a) {
+// Palette prep of palette p by a 1024-thread workgroup; `c` is colour k = tid & 255
+// (threads with tid >= 256 pass the same colour as their k).
+__device__ __forceinline__ void prep_palette_body(const PaletteArgs& a, int p, float4 c) {
     // 1024 threads: colour k = tid & 255 scans quarter q = tid >> 8 of the lower
     // indices ([64q, 64q + 64)) for an exact duplicate; a quarter wholly above k
     // is skipped by the whole wave.  (256 threads scanning all K entries each
     // were latency-bound; a serial dependent loop was ~30 us.)
-    const int p = blockIdx.x, tid = threadIdx.x, k = tid & 255, q = tid >> 8;
+    const int tid = threadIdx.x, k = tid & 255, q = tid >> 8;
     __shared__ float4 s[kMaxK];
     __shared__ uint32_t s_dup[kMaxK / 32];
     __shared__ int s_nonfinite;
     if (tid < kMaxK / 32) s_dup[tid] = 0u;
     if (tid == 0) s_nonfinite = 0;
-    float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (k < a.K) {
-        c = a.pal_in[(int64_t)p * a.K + k];
-        c.w = 0.f;  // SW:49: palettes carry .w = 0
-    }
+    if (k < a.K) c.w = 0.f;  // SW:49: palettes carry .w = 0
+    else c = make_float4(0.f, 0.f, 0.f, 0.f);
     __syncthreads();
     if (q == 0 && k < a.K) {
         s[k] = c;
@@ -229,6 +228,144 @@ __global__ __launch_bounds__(1024) void prep_palette_kernel(PaletteArgs a) {
         a.dup[(int64_t)p * kMaxK + k] = (s_dup[k >> 5] >> (k & 31)) & 1u;
     }
     if (tid == 0) a.pflags[p] = s_nonfinite;
+}
+
+__global__ __launch_bounds__(1024) void prep_palette_kernel(PaletteArgs a) {
+    const int p = blockIdx.x, k = threadIdx.x & 255;
+    const float4 c = k < a.K ? a.pal_in[(int64_t)p * a.K + k] : make_float4(0.f, 0.f, 0.f, 0.f);
+    prep_palette_body(a, p, c);
+}
+
+// ----------------------------------------------------------------------------
+// sa_step: one step of the device-resident SWASA search (IM:497-568 with
+// SW:54-101), so an iteration needs no host round trip.  Grid (P), block 1024.
+//  - accept: the costs of the population just evaluated (finalize's
+//    [P][1+K] sums and used flags, all-reduced), C = sum/N + delta * #unused
+//    (IM:712; the repeated double additions of a float delta are exact, so the
+//    count times delta equals the host's loop), then the acceptance loop
+//    (SW:54-57, one next_double per positive delta), best tracking and the
+//    convergence loop (SW:59-62, IM:538-545) -- sequential on thread 0 of every
+//    workgroup, identically, so no workgroup waits for another;
+//  - generate: candidate palette p (SW:91-101 neighbours, or SW:40-52 random at
+//    the start), one java.util.Random draw per thread via a jump table
+//    (LCG^n = A_n s + C_n mod 2^48), then prep_palette_body.
+// State is ping-ponged (in -> out) so no workgroup overwrites what another reads.
+// Host-side values that depend only on the iteration (temperature, the
+// convergence threshold, the step width) arrive as arguments.
+// ----------------------------------------------------------------------------
+constexpr uint64_t kLcgMask = (1ull << 48) - 1;
+constexpr uint64_t kLcgMult = 0x5DEECE66Dull;
+
+__device__ __forceinline__ int32_t lcg_next(uint64_t& s, int bits) {
+    s = (s * kLcgMult + 0xBull) & kLcgMask;
+    return (int32_t)(int64_t)(s >> (48 - bits));
+}
+__device__ __forceinline__ double lcg_next_double(uint64_t& s) {
+    const int64_t hi = lcg_next(s, 26), lo = lcg_next(s, 27);
+    return (double)((hi << 27) + lo) * (1.0 / (double)(1LL << 53));
+}
+__device__ __forceinline__ uint64_t lcg_jump(uint64_t s, uint64_t A, uint64_t C) {
+    return (A * s + C) & kLcgMask;
+}
+
+__global__ __launch_bounds__(1024) void sa_step_kernel(SaArgs a) {
+#pragma clang fp contract(off)
+    const int p = blockIdx.x, tid = threadIdx.x, P = a.P, K = a.K, n4 = 4 * K;
+    __shared__ int s_unused[kSaMaxP];
+    __shared__ int s_src[kSaMaxP];   // >= 0: the palette comes from candidate s_src; -1: kept
+    __shared__ uint64_t s_seed;
+    __shared__ int s_best;           // candidate that set a new best (-1: none)
+    __shared__ double cur[kSaMaxP], err[kSaMaxP];  // thread 0's (in LDS, not scratch)
+    __shared__ float4 s_cand[kMaxK];
+    if (tid < P) s_unused[tid] = 0;
+    __syncthreads();
+    if (a.accept) {
+        for (int e = tid; e < P * K; e += 1024) {
+            const int i = e / K, k = e - i * K;
+            if (a.out[(int64_t)i * (1 + K) + 1 + k] == 0.0) atomicAdd(&s_unused[i], 1);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint64_t seed = *a.seed_in;
+            for (int i = 0; i < P; ++i) {
+                err[i] = a.out[(int64_t)i * (1 + K)] / a.n_total + (double)s_unused[i] * (double)a.delta;
+                cur[i] = a.init ? err[i] : a.err_in[i];
+                s_src[i] = a.init ? i : -1;
+            }
+            double best = a.init ? err[0] : *a.best_err;
+            int best_src = a.init ? 0 : -1;
+            if (a.init) {  // IM:490-493: argmin_first
+                for (int i = 1; i < P; ++i)
+                    if (best > err[i]) { best = err[i]; best_src = i; }
+            } else {
+                double minerror = 1.7976931348623157e308;
+                int minidx = 0;
+                for (int i = 0; i < P; ++i) {  // IM:518-537
+                    if (P > 1 && err[i] < minerror) { minerror = err[i]; minidx = i; }
+                    const double d = err[i] - cur[i];
+                    const bool acc = d <= 0 || exp(-d / (double)a.temperature) > lcg_next_double(seed);
+                    if (acc) {
+                        cur[i] = err[i];
+                        s_src[i] = i;
+                        if (cur[i] < best) { best = cur[i]; best_src = i; }
+                    }
+                }
+                for (int i = 0; a.convergence && P > 1 && i < P; ++i) {  // IM:538-545
+                    if (!(a.keep_threshold > lcg_next_double(seed))) {
+                        cur[i] = minerror;
+                        s_src[i] = minidx;
+                    }
+                }
+            }
+            s_seed = seed;
+            s_best = best_src;
+            if (p == 0) {
+                for (int i = 0; i < P; ++i) a.err_out[i] = cur[i];
+                *a.best_err = best;
+                *a.seed_out = a.generate ? lcg_jump(seed, a.jump_A[K * 3 * P], a.jump_C[K * 3 * P]) : seed;
+            }
+        }
+    } else if (tid == 0) {
+        s_seed = *a.seed_in;
+        s_best = -1;
+        for (int i = 0; i < P; ++i) s_src[i] = -1;
+        if (p == 0) {
+            for (int i = 0; i < P; ++i) a.err_out[i] = a.err_in[i];
+            *a.seed_out = a.generate ? lcg_jump(s_seed, a.jump_A[K * 3 * P], a.jump_C[K * 3 * P]) : s_seed;
+        }
+    }
+    __syncthreads();
+    // the accepted palette of member p
+    const int src = s_src[p];
+    const float* from = src >= 0 ? a.cand_in + (int64_t)src * n4 : a.colors_in + (int64_t)p * n4;
+    for (int e = tid; e < n4; e += 1024) a.colors_out[(int64_t)p * n4 + e] = from[e];
+    if (p == 0 && s_best >= 0)  // IM:533-536: the best palette so far
+        for (int e = tid; e < n4; e += 1024) a.best_colors[e] = a.cand_in[(int64_t)s_best * n4 + e];
+    if (!a.generate) return;
+    // candidate p: draw t = 3i + c of this palette's block (SW:91-101 / SW:40-52)
+    const uint64_t base = lcg_jump(s_seed, a.jump_A[K * 3 * p], a.jump_C[K * 3 * p]);
+    if (tid < 3 * K) {
+        const int i = tid / 3, c = tid - 3 * i;
+        const uint64_t st = lcg_jump(base, a.jump_A[tid + 1], a.jump_C[tid + 1]);
+        const float u = (float)(int32_t)(st >> 24) / (float)(1 << 24);
+        float v;
+        if (a.random) {
+            v = u;
+        } else {
+            const float step = (u * 2 - 1) * a.amax;
+            const float x = from[4 * i + c] + step;
+            v = x > 0.f ? (x > 1.f ? 1.f : x) : 0.f;  // clampf_java (SW:103-106)
+        }
+        reinterpret_cast<float*>(s_cand)[4 * i + c] = v;
+        a.cand_out[(int64_t)p * n4 + 4 * i + c] = v;
+    }
+    if (tid < K) {
+        reinterpret_cast<float*>(s_cand)[4 * tid + 3] = 0.f;
+        a.cand_out[(int64_t)p * n4 + 4 * tid + 3] = 0.f;
+    }
+    __syncthreads();
+    const int k = tid & 255;
+    prep_palette_body(a.prep, p, k < K ? s_cand[k] : make_float4(0.f, 0.f, 0.f, 0.f));
 }
 
 // ----------------------------------------------------------------------------
@@ -2941,6 +3078,11 @@ void opp2xyz_over_illum(const float inv_illum[3], float m[9]) {
 
 hipError_t launch_prep_palette(const PaletteArgs& a, int P, hipStream_t s) {
     hipLaunchKernelGGL(prep_palette_kernel, dim3(P), dim3(1024), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_sa_step(const SaArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(sa_step_kernel, dim3(a.P), dim3(1024), 0, s, a);
     return hipGetLastError();
 }
 

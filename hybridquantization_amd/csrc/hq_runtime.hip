@@ -20,6 +20,7 @@
 namespace hq {
 // launchers from hq_kernels.hip
 hipError_t launch_prep_palette(const PaletteArgs&, int P, hipStream_t);
+hipError_t launch_sa_step(const SaArgs&, hipStream_t);
 hipError_t launch_build_grid(const GridArgs&, int P, hipStream_t);
 hipError_t launch_assign(const AssignArgs&, int P, int rep, int group, int batch, hipStream_t);
 void fast_tile_dims(int W, int own_rows, int tile_cfg, int* tiles_x, int* ntiles);
@@ -130,6 +131,8 @@ struct hq_ctx {
                            // 6 = row-pair in two channel groups (6 workgroups per CU),
                            // 7 = 6 with the vertical passes on the matrix cores (split f16; default),
                            // 8 = both passes on the matrix cores (96-column tiles)
+    int sa_device = 1;     // hq_search_*: 1 = SWASA iterations resident on the device (no host
+                           // round trip per iteration), 0 = host-driven (one eval call each)
     int bands = 0;         // row bands of the assign -> cost pipeline (0/1 = one pass, serial)
     int band_cpb = 2;      // banded assign: pixel chunks per block (blocks = chunks / cpb)
     int trim = 1;          // skip taps < 1e-9 of the peak of the narrow k1 filters
@@ -165,8 +168,19 @@ struct BandPlan {
 
 struct hq_search {
     hq_ctx* ctx;
-    SearchDriver* driver;
+    SearchDriver* driver;  // host-driven search (sa_device = 0), else null
     int K;
+    // device-resident search: the SWASA state lives on the device, ping-ponged
+    // between [0] and [1] by sa_step_kernel; the host keeps the iteration-only
+    // quantities (temperature, step width, convergence threshold) in `pol`,
+    // whose RNG is unused.
+    Swasa* pol = nullptr;
+    hq_swasa_params prm{};
+    int P = 0, ite = 0, st = 0, cd = 0;  // state and candidate buffer parities
+    float t_acc = 0.f;                   // temperature / threshold of the iteration
+    double keep_acc = 0.0;               // whose population awaits acceptance
+    DevBuf colors[2], cand[2], err[2], seed[2], best_err, best_colors, jA, jC;
+    std::vector<hipEvent_t> pev;         // profiling: 5 events per iteration of a run
 };
 
 namespace {
@@ -399,9 +413,18 @@ void prof_add(hq_ctx* c, ProfSlot& s, hipEvent_t a, hipEvent_t b) {
     }
 }
 
-// Enqueue the whole evaluation of the P palettes already in h_pal; results
-// (partial sums + used flags) land in d_out; all-reduced if a comm is set.
-int enqueue_eval(hq_ctx* c, int P, int K) {
+PaletteArgs prep_args(hq_ctx* c, int K) {
+    return PaletteArgs{c->d_pal_in.as<float4>(), c->d_pal.as<float4>(), c->d_opp.as<float4>(),
+                       c->d_dup.as<uint8_t>(), c->d_pflags.as<int>(), K};
+}
+
+// Enqueue the evaluation of the P prepared palettes (d_pal, d_opp, d_dup,
+// d_pflags): grid, assign, cost, finalize into d_out (partial sums + used
+// flags), all-reduced if a comm is set.  ev (5 events, or null): ev[0] is
+// recorded by the caller before the palette prep; ev[1..4] after the grid, the
+// assign, the cost and the finalize kernels.  Band events (bands > 1) only with
+// the context's own profiling events.
+int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, BandPlan& bp) {
     const Geom& g = c->g;
     hipStream_t s = c->stream;
     const int G2 = c->G2 > 0 ? c->G2 : 4;
@@ -409,19 +432,14 @@ int enqueue_eval(hq_ctx* c, int P, int K) {
     const int64_t l1p = round_up((int64_t)G1 * G1 * G1 * 32, 256);
     const int64_t l2g = round_up((int64_t)G2 * G2 * G2 * 64, 256);  // per group of 4 palettes
     const int nblocks = c->num_cu * c->assign_blocks_per_cu;
-    HIP_TRY(c, hipMemcpyAsync(c->d_pal_in.p, c->h_pal, sizeof(float) * 4 * (size_t)P * K,
-                              hipMemcpyHostToDevice, s));
-    if (c->prof) HIP_TRY(c, hipEventRecord(c->ev[0], s));
-    PaletteArgs pa{c->d_pal_in.as<float4>(), c->d_pal.as<float4>(), c->d_opp.as<float4>(),
-                   c->d_dup.as<uint8_t>(), c->d_pflags.as<int>(), K};
-    HIP_TRY(c, launch_prep_palette(pa, P, s));
+    const bool band_ev = ev == c->ev;
     if (c->G2 > 0) {
         GridArgs ga{c->d_pal.as<float4>(), c->d_dup.as<uint8_t>(), c->d_pflags.as<int>(),
                     c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(), K, G1, l1p, l2g};
         HIP_TRY(c, launch_build_grid(ga, P, s));
     }
-    if (c->prof) HIP_TRY(c, hipEventRecord(c->ev[1], s));
-    const BandPlan bp = plan_bands(c);
+    if (ev) HIP_TRY(c, hipEventRecord(ev[1], s));
+    bp = plan_bands(c);
     AssignArgs aa{c->d_R.as<float>(), c->d_G.as<float>(), c->d_B.as<float>(), c->d_pal.as<float4>(),
                   c->d_pflags.as<int>(), c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(),
                   c->d_idx.as<uint8_t>(), c->d_used_mask.as<uint32_t>(), g.n_ext, g.idx_pitch,
@@ -479,15 +497,15 @@ int enqueue_eval(hq_ctx* c, int P, int K) {
             CostArgs cb = ca;
             cb.tile0 = bp.t0[j];
             cb.band_tiles = bp.t1[j] - bp.t0[j];
-            if (c->prof) HIP_TRY(c, hipEventRecord(c->pev[2 * j], s));
+            if (band_ev) HIP_TRY(c, hipEventRecord(c->pev[2 * j], s));
             HIP_TRY(c, launch_cost_fast(cb, P, c->de_type, c->tile_cfg, c->trim && c->trim_ok, s));
-            if (c->prof) HIP_TRY(c, hipEventRecord(c->pev[2 * j + 1], s));
+            if (band_ev) HIP_TRY(c, hipEventRecord(c->pev[2 * j + 1], s));
         }
         nparts = ntiles;
-        if (c->prof) HIP_TRY(c, hipEventRecord(c->ev[2], s));  // assign + cost span
+        if (ev) HIP_TRY(c, hipEventRecord(ev[2], s));  // assign + cost span
     } else {
         HIP_TRY(c, launch_assign(aa, P, c->assign_rep, c->assign_group, c->assign_batch, s));
-        if (c->prof) HIP_TRY(c, hipEventRecord(c->ev[2], s));
+        if (ev) HIP_TRY(c, hipEventRecord(ev[2], s));
         if (fast) {
             HIP_TRY(c, launch_cost_fast(ca, P, c->de_type, c->tile_cfg, c->trim && c->trim_ok, s));
             nparts = ntiles;
@@ -515,32 +533,51 @@ int enqueue_eval(hq_ctx* c, int P, int K) {
             }
         }
     }
-    if (c->prof) HIP_TRY(c, hipEventRecord(c->ev[3], s));
+    if (ev) HIP_TRY(c, hipEventRecord(ev[3], s));
     FinalizeArgs fa{c->d_partial.as<double>(), c->d_used_mask.as<uint32_t>(), c->d_out.as<double>(),
                     nparts, bp.mask_blocks, K};
     HIP_TRY(c, launch_finalize(fa, P, s));
-    if (c->prof) HIP_TRY(c, hipEventRecord(c->ev[4], s));
+    if (ev) HIP_TRY(c, hipEventRecord(ev[4], s));
     if (c->comm) {  // also with one rank (a no-op copy), so that path is exercised on one GPU
         NCCL_TRY(c, ncclAllReduce(c->d_out.p, c->d_out.p, (size_t)P * (1 + K), ncclFloat64, ncclSum,
                                   c->comm, s));
     }
+    c->last_P = P;
+    c->K_cur = K;
+    return HQ_OK;
+}
+
+// Add one evaluation's kernel times (its events have completed).
+void prof_accumulate(hq_ctx* c, const hipEvent_t* ev, const BandPlan& bp) {
+    prof_add(c, c->prof_grid, ev[0], ev[1]);
+    if (bp.n > 1) {  // overlapped: "assign" = the assign + cost span, "cost" = per-band launches
+        prof_add(c, c->prof_assign, ev[1], ev[2]);
+        if (ev == c->ev)
+            for (int j = 0; j < bp.n; ++j)
+                if (bp.t1[j] > bp.t0[j]) prof_add(c, c->prof_cost, c->pev[2 * j], c->pev[2 * j + 1]);
+    } else {
+        prof_add(c, c->prof_assign, ev[1], ev[2]);
+        prof_add(c, c->prof_cost, ev[2], ev[3]);
+    }
+    prof_add(c, c->prof_finalize, ev[3], ev[4]);
+}
+
+// Host-driven evaluation of the P palettes in h_pal: upload, prep, enqueue_core,
+// read back d_out into h_out.
+int enqueue_eval(hq_ctx* c, int P, int K) {
+    hipStream_t s = c->stream;
+    HIP_TRY(c, hipMemcpyAsync(c->d_pal_in.p, c->h_pal, sizeof(float) * 4 * (size_t)P * K,
+                              hipMemcpyHostToDevice, s));
+    const hipEvent_t* ev = c->prof ? c->ev : nullptr;
+    if (ev) HIP_TRY(c, hipEventRecord(ev[0], s));
+    HIP_TRY(c, launch_prep_palette(prep_args(c, K), P, s));
+    BandPlan bp;
+    int rc = enqueue_core(c, P, K, ev, bp);
+    if (rc) return rc;
     HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out.p, sizeof(double) * (size_t)P * (1 + K),
                               hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
-    if (c->prof) {
-        prof_add(c, c->prof_grid, c->ev[0], c->ev[1]);
-        if (bp.n > 1) {  // overlapped: "assign" = the assign + cost span, "cost" = per-band launches
-            prof_add(c, c->prof_assign, c->ev[1], c->ev[2]);
-            for (int j = 0; j < bp.n; ++j)
-                if (bp.t1[j] > bp.t0[j]) prof_add(c, c->prof_cost, c->pev[2 * j], c->pev[2 * j + 1]);
-        } else {
-            prof_add(c, c->prof_assign, c->ev[1], c->ev[2]);
-            prof_add(c, c->prof_cost, c->ev[2], c->ev[3]);
-        }
-        prof_add(c, c->prof_finalize, c->ev[3], c->ev[4]);
-    }
-    c->last_P = P;
-    c->K_cur = K;
+    if (ev) prof_accumulate(c, ev, bp);
     return HQ_OK;
 }
 
@@ -562,6 +599,128 @@ int eval_partial_into_hout(hq_ctx* c, const float* palettes, int P, int K) {
     if ((rc = ensure_population(c, P, K))) return rc;
     std::memcpy(c->h_pal, palettes, sizeof(float) * 4 * (size_t)P * K);
     return enqueue_eval(c, P, K);
+}
+
+}  // namespace
+
+namespace {
+
+// One sa_step launch: accept the population in cand[cd] (if `accept`), then
+// generate the next candidates into cand[1 - cd] (if `generate`).
+int enqueue_sa_step(hq_search* s, bool accept, bool init, bool generate, bool random, float amax) {
+    hq_ctx* c = s->ctx;
+    SaArgs a{};
+    a.out = c->d_out.as<double>();
+    a.colors_in = s->colors[s->st].as<float>();
+    a.colors_out = s->colors[1 - s->st].as<float>();
+    a.cand_in = s->cand[s->cd].as<float>();
+    a.cand_out = s->cand[1 - s->cd].as<float>();
+    a.err_in = s->err[s->st].as<double>();
+    a.err_out = s->err[1 - s->st].as<double>();
+    a.seed_in = s->seed[s->st].as<uint64_t>();
+    a.seed_out = s->seed[1 - s->st].as<uint64_t>();
+    a.best_err = s->best_err.as<double>();
+    a.best_colors = s->best_colors.as<float>();
+    a.jump_A = s->jA.as<uint64_t>();
+    a.jump_C = s->jC.as<uint64_t>();
+    a.prep = prep_args(c, s->K);
+    a.n_total = (double)c->g.W * (double)c->g.H;
+    a.keep_threshold = s->keep_acc;
+    a.temperature = s->t_acc;
+    a.amax = amax;
+    a.delta = s->prm.delta;
+    a.P = s->P;
+    a.K = s->K;
+    a.accept = accept;
+    a.init = init;
+    a.generate = generate;
+    a.random = random;
+    a.convergence = s->prm.convergence;
+    HIP_TRY(c, launch_sa_step(a, c->stream));
+    s->st = 1 - s->st;
+    if (generate) s->cd = 1 - s->cd;
+    return HQ_OK;
+}
+
+int ensure_events(hq_search* s, size_t n) {
+    while (s->pev.size() < n) {
+        hipEvent_t e;
+        HIP_TRY(s->ctx, hipEventCreate(&e));
+        s->pev.push_back(e);
+    }
+    return HQ_OK;
+}
+
+int device_search_create(hq_ctx* c, const hq_swasa_params* params, int K, uint64_t seed, hq_search* s) {
+    const int P = params->population;
+    s->prm = *params;
+    s->P = P;
+    s->pol = new Swasa(*params, seed);
+    int rc = ensure_population(c, P, K);
+    if (rc) return rc;
+    const size_t n4 = (size_t)P * 4 * K;
+    for (int i = 0; i < 2; ++i) {
+        HIP_TRY(c, s->colors[i].ensure(sizeof(float) * n4));
+        HIP_TRY(c, s->cand[i].ensure(sizeof(float) * n4));
+        HIP_TRY(c, s->err[i].ensure(sizeof(double) * P));
+        HIP_TRY(c, s->seed[i].ensure(sizeof(uint64_t)));
+    }
+    HIP_TRY(c, s->best_err.ensure(sizeof(double)));
+    HIP_TRY(c, s->best_colors.ensure(sizeof(float) * 4 * K));
+    // java.util.Random jumps: n steps = A_n s + C_n (mod 2^48), n = 0 .. 3KP
+    const size_t nj = (size_t)3 * K * P + 1;
+    std::vector<uint64_t> A(nj), C(nj);
+    const uint64_t mask = (1ull << 48) - 1, mult = 0x5DEECE66Dull;
+    A[0] = 1;
+    C[0] = 0;
+    for (size_t n = 1; n < nj; ++n) {
+        A[n] = (A[n - 1] * mult) & mask;
+        C[n] = (C[n - 1] * mult + 0xBull) & mask;
+    }
+    HIP_TRY(c, s->jA.ensure(sizeof(uint64_t) * nj));
+    HIP_TRY(c, s->jC.ensure(sizeof(uint64_t) * nj));
+    HIP_TRY(c, hipMemcpy(s->jA.p, A.data(), sizeof(uint64_t) * nj, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(s->jC.p, C.data(), sizeof(uint64_t) * nj, hipMemcpyHostToDevice));
+    const uint64_t s0 = (seed ^ mult) & mask;  // JavaRandom::set_seed
+    HIP_TRY(c, hipMemcpy(s->seed[0].p, &s0, sizeof s0, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemset(s->err[0].p, 0, sizeof(double) * P));
+    s->st = s->cd = 0;
+    // IM:385-493: random population (SW:40-52), its evaluation, argmin
+    if ((rc = enqueue_sa_step(s, false, false, true, true, 0.f))) return rc;
+    BandPlan bp;
+    if ((rc = enqueue_core(c, P, K, nullptr, bp))) return rc;
+    if ((rc = enqueue_sa_step(s, true, true, false, false, 0.f))) return rc;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    s->ite = 0;
+    return HQ_OK;
+}
+
+// IM:497-568 for up to `iterations` iterations, all enqueued before one sync.
+int device_search_run(hq_search* s, int iterations, int* ran) {
+    hq_ctx* c = s->ctx;
+    int done = 0, rc;
+    const bool prof = c->prof;
+    if (prof && (rc = ensure_events(s, (size_t)5 * iterations))) return rc;
+    std::vector<BandPlan> bps(prof ? iterations : 0);
+    for (; done < iterations && s->ite < s->prm.imax; ++done) {
+        const int ite = ++s->ite;
+        s->pol->reduce_temperature_if_necessary(ite);                  // IM:507
+        const float amax = s->pol->max_step_width(ite) / 256.0f;       // SW:91-101
+        const hipEvent_t* ev = prof ? &s->pev[(size_t)5 * done] : nullptr;
+        if (ev) HIP_TRY(c, hipEventRecord(ev[0], c->stream));
+        // accept the previous iteration's population (none at the first of a run)
+        if ((rc = enqueue_sa_step(s, done > 0, false, true, false, amax))) return rc;
+        BandPlan bp;
+        if ((rc = enqueue_core(c, s->P, s->K, ev, bp))) return rc;
+        if (prof) bps[done] = bp;
+        s->t_acc = s->pol->temperature();     // SW:54-57 at this iteration
+        s->keep_acc = s->pol->keep_threshold(ite);
+    }
+    if (done > 0 && (rc = enqueue_sa_step(s, true, false, false, false, 0.f))) return rc;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    for (int i = 0; prof && i < done; ++i) prof_accumulate(c, &s->pev[(size_t)5 * i], bps[i]);
+    if (ran) *ran = done;
+    return HQ_OK;
 }
 
 }  // namespace
@@ -934,15 +1093,34 @@ int hq_search_create(hq_ctx* c, const hq_swasa_params* params, int K, uint64_t s
     *out = nullptr;
     if (params->population < 1 || params->imax < 1 || params->iTc < 1 || K < 1)
         return fail(c, HQ_ERR_ARG, "bad SWASA parameters");
-    const float delta = params->delta;
-    auto eval = [c, delta](const float* pal, int P, int KK, double* costs) {
-        return hq_eval_population(c, pal, P, KK, delta, costs, nullptr);
-    };
-    hq_search* s = new hq_search{c, new SearchDriver(*params, K, seed, eval), K};
-    int rc = s->driver->start();
+    const bool device = c->sa_device && params->population <= kSaMaxP && K <= kMaxK;
+    hq_search* s = new hq_search{c, nullptr, K};
+    int rc;
+    if (device) {
+        if (!c->have_image) rc = fail(c, HQ_ERR_STATE, "no image set (hq_set_image)");
+        else if (c->de_type == HQ_DE_CIEDE2000)
+            rc = fail(c, HQ_ERR_UNSUPPORTED, "CIEDE2000 is unimplemented in the reference (CL:227-230)");
+        else rc = bind(c);
+        if (rc) {
+            hq_search_destroy(s);
+            return rc;
+        }
+        const bool full = c->g.r0 == 0 && c->g.r1 == c->g.H;
+        if (!full && !(c->comm && c->nranks > 1)) {
+            hq_search_destroy(s);
+            return fail(c, HQ_ERR_STATE, "sharded context without a communicator");
+        }
+        rc = device_search_create(c, params, K, seed, s);
+    } else {
+        const float delta = params->delta;
+        auto eval = [c, delta](const float* pal, int P, int KK, double* costs) {
+            return hq_eval_population(c, pal, P, KK, delta, costs, nullptr);
+        };
+        s->driver = new SearchDriver(*params, K, seed, eval);
+        rc = s->driver->start();
+    }
     if (rc) {
-        delete s->driver;
-        delete s;
+        hq_search_destroy(s);
         return rc;
     }
     *out = s;
@@ -951,11 +1129,25 @@ int hq_search_create(hq_ctx* c, const hq_swasa_params* params, int K, uint64_t s
 
 int hq_search_run(hq_search* s, int iterations, int* ran) {
     if (!s || iterations < 0) return HQ_ERR_ARG;
+    if (!s->driver) {
+        int rc = bind(s->ctx);
+        return rc ? rc : device_search_run(s, iterations, ran);
+    }
     return s->driver->run(iterations, ran, nullptr);
 }
 
 int hq_search_best(const hq_search* s, float* colors, double* best_error, int* iteration) {
     if (!s) return HQ_ERR_ARG;
+    if (!s->driver) {
+        hq_ctx* c = s->ctx;
+        int rc = bind(c);
+        if (rc) return rc;
+        if (colors)
+            HIP_TRY(c, hipMemcpy(colors, s->best_colors.p, sizeof(float) * 4 * s->K, hipMemcpyDeviceToHost));
+        if (best_error) HIP_TRY(c, hipMemcpy(best_error, s->best_err.p, sizeof(double), hipMemcpyDeviceToHost));
+        if (iteration) *iteration = s->ite;
+        return HQ_OK;
+    }
     if (colors) std::copy(s->driver->best_colors().begin(), s->driver->best_colors().end(), colors);
     if (best_error) *best_error = s->driver->best_error();
     if (iteration) *iteration = s->driver->iteration();
@@ -964,6 +1156,16 @@ int hq_search_best(const hq_search* s, float* colors, double* best_error, int* i
 
 void hq_search_destroy(hq_search* s) {
     if (!s) return;
+    if (!s->driver && s->ctx) {
+        (void)hipSetDevice(s->ctx->device);
+        (void)hipStreamSynchronize(s->ctx->stream);
+    }
+    for (hipEvent_t e : s->pev) (void)hipEventDestroy(e);
+    for (DevBuf* b : {&s->colors[0], &s->colors[1], &s->cand[0], &s->cand[1], &s->err[0], &s->err[1],
+                      &s->seed[0], &s->seed[1], &s->best_err, &s->best_colors, &s->jA,
+                      &s->jC})
+        b->release();
+    delete s->pol;
     delete s->driver;
     delete s;
 }
@@ -1018,6 +1220,8 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
         if (value != 1 && value != 2 && value != 4 && value != 16)
             return fail(c, HQ_ERR_ARG, "assign_rep in {1,2,4,16}");
         c->assign_rep = value;
+    } else if (!std::strcmp(name, "sa_device")) {
+        c->sa_device = value != 0;
     } else if (!std::strcmp(name, "bands")) {
         if (value < 0 || value > kMaxBands) return fail(c, HQ_ERR_ARG, "bands in [0,%d]", kMaxBands);
         c->bands = value;

@@ -42,6 +42,7 @@ class Swasa {
     void generate_random_colors(int K, float* out) ;        // SW:40-52
     bool is_accepted(double delta_e);                       // SW:54-57
     bool keeps_his_values(int iteration);                   // SW:59-62
+    double keep_threshold(int iteration) const;             // its left-hand side
     float max_step_width(int i) const;                      // SW:69-72
     double compute_penalty(const int32_t* used, int K) const;  // SW:74-82
     void reduce_temperature_if_necessary(int iteration);    // SW:84-89

@@ -189,7 +189,11 @@ int hq_profile_reset(hq_ctx *ctx);
  *                  pairs, all seven filters at once (packed FMA across two rows, 2 columns
  *                  per item); 5 = the same with 4 columns per item; 2 = row layout, 4-row vertical
  *                  items; 1 = vertical pass split by opponent-channel group; 3 = vertical
- *                  pass on the matrix cores (split-f16 products); 0 = 16-row tiles (2 WG/CU)
+ *                  pass on the matrix cores (split-f16 products); 0 = 16-row tiles (2 WG/CU);
+ *                  8 = both passes on the matrix cores (96-column tiles); 9 = 7 with the
+ *                  vertical MFMA's operands swapped, column-major indices, 1-row items;
+ *                  10 = both passes on the matrix cores on 9's layout; 11 = 7 with
+ *                  4-column row-pair items on a parity-split layout
  *   "trim"         1 = skip the narrow k1 filters' taps below 1e-9 of their peak
  *                  (default; only when the filters allow it), 0 = all taps
  *   "assign_group" palettes served by one pixel pass: 4 (default; their level-2 entries
@@ -197,9 +201,15 @@ int hq_profile_reset(hq_ctx *ctx);
  *   "assign_batch" with group 4: 3 = software-pipelined (default: the next pixel's lookup
  *                  and the one after's RGB in flight while a pixel is resolved), 1 or 2 =
  *                  pixels per batch; with group 1: 4 or 8 = pixels per batch, 0 = one-pixel
- *                  prefetch
+ *                  prefetch; with group 4, 5 = one (pixel, palette) pair per lane
  *   "assign_rep"   palette replication in LDS for group 1/2 with batch 0: 1, 2, 4, 16
- *   "assign_blocks_per_cu" workgroups per CU of the assign grid (default 8) */
+ *   "assign_blocks_per_cu" workgroups per CU of the assign grid (default 8)
+ *   "bands"        0 (default) or 2-16 row bands: assign of band j+1 on a second stream
+ *                  beside the cost of band j (bit-identical results)
+ *   "band_cpb"     banded assign: pixel chunks per workgroup (default 2)
+ *   "sa_device"    hq_search_*: 1 (default) = the SWASA iterations run on the device
+ *                  (accept/generate kernel, no host round trip per iteration; needs
+ *                  population <= 64), 0 = host-driven, one evaluation call each */
 int hq_set_option(hq_ctx *ctx, const char *name, int value);
 
 #ifdef __cplusplus

@@ -365,6 +365,43 @@ def test_search_matches_host_driver_on_oracle_costs(ip, filt):
     np.testing.assert_array_equal(best, hbest)
 
 
+@pytest.mark.parametrize("P", [1, 3, 4])
+def test_device_search_matches_host_driven(gpu, filt, P):
+    """The device-resident SWASA loop (sa_step_kernel: acceptance, convergence,
+    java.util.Random draws by jump table, neighbour generation) follows the
+    host-driven driver's trajectory exactly on the same GPU costs, across
+    resumed run() calls and up to imax."""
+    import ctypes as C
+    w, h, K = 96, 64, 16
+    R, G, B = o.synthetic_image(w, h, seed=9)
+    m = hq.ImageManipulation(device=gpu)
+    hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
+    m.setImage(o.inline_rgba(R, G, B).reshape(-1), None, w, filt.illum)
+    lib = hq.load()
+    res = {}
+    for dev in (0, 1):
+        m.setOption("sa_device", dev)
+        sw = hq.SWASA(population=P, imax=50, seed=5 + P, t0=0.05)
+        params = sw.params()
+        handle = C.c_void_p()
+        hq._lib.check(lib.hq_search_create(m.ctx, C.byref(params), K, sw.seed, C.byref(handle)), m.ctx)
+        ran = C.c_int()
+        total = 0
+        for chunk in (17, 1, 40):  # the last call stops at imax
+            hq._lib.check(lib.hq_search_run(handle, chunk, C.byref(ran)), m.ctx)
+            total += ran.value
+        best = np.zeros(4 * K, np.float32)
+        err = C.c_double()
+        it = C.c_int()
+        hq._lib.check(lib.hq_search_best(handle, hq._lib.fptr(best), C.byref(err), C.byref(it)), m.ctx)
+        lib.hq_search_destroy(handle)
+        res[dev] = (best, err.value, it.value, total)
+    assert res[0][2] == res[1][2] == res[0][3] == res[1][3] == 50
+    assert res[1][1] == res[0][1]
+    np.testing.assert_array_equal(res[1][0], res[0][0])
+    m.close()
+
+
 # ---------------------------------------------------------------------------
 # Full-size properties (4096^2, K = 256): determinism, grid == exhaustive,
 # fast == generic, shards == full.
