@@ -352,14 +352,20 @@ BandPlan plan_bands(const hq_ctx* c) {
     const int nblocks = c->num_cu * c->assign_blocks_per_cu;
     const bool fast = c->cost_variant != 1 && c->half == 10;
     b.n = fast ? std::max(1, std::min({c->bands, kMaxBands, trows})) : 1;
+    const int64_t chunk = 256 * 8;  // assign_pipe_kernel: 256 threads x PPT pixels
     if (b.n == 1) {
+        // no more workgroups than pixel chunks: idle workgroups still fill LDS, and
+        // after the XCD relabelling they would all sit on the last XCDs (a 512-row
+        // shard ran assign on half the chip: 0.071 vs 0.053 ms)
+        // (evening out the chunks per workgroup instead -- 1064 workgroups of 2 for
+        // 2128 chunks -- was slower than 2048 with 80 of them taking a second chunk)
         b.q0[0] = 0; b.q1[0] = g.n_ext;
-        b.blocks[0] = nblocks; b.moff[0] = 0;
+        b.blocks[0] = (int)std::max<int64_t>(1, std::min<int64_t>(nblocks, (g.n_ext + chunk - 1) / chunk));
+        b.moff[0] = 0;
         b.t0[0] = 0; b.t1[0] = ntiles;
-        b.mask_blocks = nblocks;
+        b.mask_blocks = b.blocks[0];
         return b;
     }
-    const int64_t chunk = 256 * 8;  // assign_pipe_kernel: 256 threads x PPT pixels
     int row = g.e0;
     for (int j = 0; j < b.n; ++j) {
         const int tr0 = (int)((int64_t)trows * j / b.n), tr1 = (int)((int64_t)trows * (j + 1) / b.n);
@@ -443,7 +449,7 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, BandPlan& bp) {
     AssignArgs aa{c->d_R.as<float>(), c->d_G.as<float>(), c->d_B.as<float>(), c->d_pal.as<float4>(),
                   c->d_pflags.as<int>(), c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(),
                   c->d_idx.as<uint8_t>(), c->d_used_mask.as<uint32_t>(), g.n_ext, g.idx_pitch,
-                  l1p, l2g, K, c->G2, nblocks, bp.mask_blocks, 0};
+                  l1p, l2g, K, c->G2, bp.n > 1 ? nblocks : bp.blocks[0], bp.mask_blocks, 0};
     int tiles_x, ntiles;
     fast_tile_dims(g.W, g.r1 - g.r0, c->tile_cfg, &tiles_x, &ntiles);
     const float inv[3] = {1.0f / c->illum[0], 1.0f / c->illum[1], 1.0f / c->illum[2]};

@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--bpc", type=int, default=0, help="assign workgroups per CU (0 = library default)")
     ap.add_argument("--bands", type=int, default=-1, help="banded assign/cost pipeline (-1 = library default)")
     ap.add_argument("--cpb", type=int, default=0, help="banded assign: chunks per block (0 = default)")
+    ap.add_argument("--rows", type=int, default=0,
+                    help="evaluate only the row shard [0, rows) of the image (an N-GPU rank's share)")
     ap.add_argument("--lib", default=None, help="alternative libhq build (scripts/ablate.py)")
     args = ap.parse_args()
     if args.lib:
@@ -58,14 +60,24 @@ def main():
         m.setOption("band_cpb", args.cpb)
     W = H = args.size
     R, G, B = synthetic_planes(W, H, 1)
+    rows = args.rows or H
     _lib.check(lib.hq_set_image_planar_shard(m.ctx, _lib.fptr(R), _lib.fptr(G), _lib.fptr(B), W, H,
-                                             _lib.fptr(sp.illuminant), 0, H), m.ctx)
+                                             _lib.fptr(sp.illuminant), 0, rows), m.ctx)
     rng = np.random.default_rng(0)
     pals = np.zeros((args.P, args.K, 4), np.float32)
     pals[..., :3] = rng.random((args.P, args.K, 3), dtype=np.float32)
     costs = np.zeros(args.P)
     flat = pals.reshape(-1)
-    lib.hq_eval_population(m.ctx, _lib.fptr(flat), args.P, args.K, 2.0, _lib.dptr(costs), None)
+    part = np.zeros(args.P * (1 + args.K))
+    if rows < H:  # a shard without a communicator: partial sums
+        def evaluate():
+            _lib.check(lib.hq_eval_population_partial(m.ctx, _lib.fptr(flat), args.P, args.K,
+                                                      _lib.dptr(part)), m.ctx)
+    else:
+        def evaluate():
+            _lib.check(lib.hq_eval_population(m.ctx, _lib.fptr(flat), args.P, args.K, 2.0,
+                                              _lib.dptr(costs), None), m.ctx)
+    evaluate()
     phases = getattr(lib, "hq_debug_phases", None) if args.lib else None
     ph = (C.c_ulonglong * 8)()
     if phases is not None:
@@ -73,8 +85,7 @@ def main():
     lib.hq_profile_enable(m.ctx, 1)
     t0 = time.perf_counter()
     for _ in range(args.evals):
-        _lib.check(lib.hq_eval_population(m.ctx, _lib.fptr(flat), args.P, args.K, 2.0,
-                                          _lib.dptr(costs), None), m.ctx)
+        evaluate()
     el = time.perf_counter() - t0
     out = []
     for k in ("grid", "assign", "cost", "finalize"):
@@ -84,7 +95,7 @@ def main():
         out.append(f"{k}={ms.value / max(n.value, 1):.4f}ms")
     print(f"{os.path.basename(args.lib or 'libhq.so')} size={W} K={args.K} P={args.P} grid={args.grid} variant={args.variant} tile={args.tile} rep={args.rep} trim={args.trim} group={args.group} batch={args.batch} bpc={args.bpc} bands={args.bands} cpb={args.cpb}: "
           f"{el / args.evals * 1e3:.3f} ms/eval-population, "
-          f"{W * H * args.P * args.evals / el / 1e6:.1f} Mpx*evals/s  ", " ".join(out),
+          f"{W * rows * args.P * args.evals / el / 1e6:.1f} Mpx*evals/s (rows {rows})  ", " ".join(out),
           "costs", costs.tolist())
     if phases is not None:
         phases(ph, 0)
