@@ -20,6 +20,8 @@
 // sqrtf(d2) (correctly rounded), strict '<' in ascending palette order.
 #include "hq_internal.h"
 
+#include <hip/hip_ext.h>
+
 #include <math.h>
 
 #include <algorithm>
@@ -450,40 +452,66 @@ __global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
         else v = (!ovf1 && tid - 1 < total) ? s_list[tid - 1] : 0;
         l1[tid] = v;
     }
-    if (tid < 64) {
-        const int ci2 = ci * 4 + (tid >> 4), cj2 = cj * 4 + ((tid >> 2) & 3), ck2 = ck * 4 + (tid & 3);
+    // Level 2: child c = tid >> 2 of this cell, its parent-list positions shared
+    // by the 4 threads of a quad (q = tid & 3 takes positions q, q+4, ...): T2 and
+    // the candidate mask are combined across the quad by shuffles, and each
+    // candidate's byte lands at its rank in ascending list order.  (One thread
+    // per child walking the list twice, on one wave of the four, made this
+    // kernel ~15 us per population.)
+    {
+        const int ch = tid >> 2, q = tid & 3;
+        const int ci2 = ci * 4 + (ch >> 4), cj2 = cj * 4 + ((ch >> 2) & 3), ck2 = ck * 4 + (ch & 3);
         const double inv2 = 1.0 / G2;
         const double l0 = ci2 * inv2, h0 = (ci2 + 1) * inv2;
         const double l1b = cj2 * inv2, h1 = (cj2 + 1) * inv2;
         const double l2 = ck2 * inv2, h2 = (ck2 + 1) * inv2;
-        uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-        int n = 0;
-        if (!exh) {
-            double T2 = INFINITY;
-            for (int i = 0; i < total; ++i) {
-                const float4 cc = s_col[s_list[i]];
-                T2 = fmin(T2, ax_max2(cc.x, l0, h0) + ax_max2(cc.y, l1b, h1) + ax_max2(cc.z, l2, h2));
-            }
-            const double thr = T2 * HQ_CAND_MARGIN;
-            for (int i = 0; i < total; ++i) {
-                const int k = s_list[i];
-                const float4 cc = s_col[k];
-                const double d = ax_min2(cc.x, l0, h0) + ax_min2(cc.y, l1b, h1) + ax_min2(cc.z, l2, h2);
-                if (d <= thr) {
-                    const int pos = n + 1;  // byte position in the entry
-                    const uint32_t v = (uint32_t)k << (8 * (pos & 3));
-                    if (pos < 4) w0 |= v;
-                    else if (pos < 8) w1 |= v;
-                    else if (pos < 12) w2 |= v;
-                    else if (pos < 16) w3 |= v;
-                    ++n;
+        // pass 1: T2 over the whole parent list (which can exceed 31 entries: the
+        // level-1 entry then overflows, the children still get lists)
+        double t2 = INFINITY;
+        for (int i = q; !exh && i < total; i += 4) {
+            const float4 cc = s_col[s_list[i]];
+            t2 = fmin(t2, ax_max2(cc.x, l0, h0) + ax_max2(cc.y, l1b, h1) + ax_max2(cc.z, l2, h2));
+        }
+        t2 = fmin(t2, __shfl_xor(t2, 1, 64));
+        t2 = fmin(t2, __shfl_xor(t2, 2, 64));
+        const double thr = t2 * HQ_CAND_MARGIN;
+        // pass 2, 32 positions at a time: candidate mask, ranks in list order
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        int n = 0;  // candidates so far (quad-uniform)
+        for (int b0 = 0; !exh && b0 < total && n <= kL2Cap; b0 += 32) {
+            uint32_t mine = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int i = b0 + q + 4 * j;
+                if (i < total) {
+                    const float4 cc = s_col[s_list[i]];
+                    const double d = ax_min2(cc.x, l0, h0) + ax_min2(cc.y, l1b, h1) + ax_min2(cc.z, l2, h2);
+                    if (d <= thr) mine |= 1u << (q + 4 * j);
                 }
             }
+            uint32_t M = mine | (uint32_t)__shfl_xor((int)mine, 1, 64);
+            M |= (uint32_t)__shfl_xor((int)M, 2, 64);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int r = q + 4 * j;
+                if ((mine >> r) & 1u) {
+                    const int pos = n + __popc(M & ((1u << r) - 1u)) + 1;  // byte in the entry
+                    if (pos <= kL2Cap) w[pos >> 2] |= (uint32_t)s_list[b0 + r] << (8 * (pos & 3));
+                }
+            }
+            n += __popc(M);
         }
-        if (exh || n > kL2Cap) { w0 = kOverflow; w1 = w2 = w3 = 0; }
-        else w0 |= (uint32_t)n;
-        uint8_t* l2e = a.lvl2 + lvl2_offset(a.lvl2_gstride, p, (int64_t)(ci2 * G2 + cj2) * G2 + ck2);
-        *reinterpret_cast<uint4*>(l2e) = make_uint4(w0, w1, w2, w3);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            w[m] |= (uint32_t)__shfl_xor((int)w[m], 1, 64);
+            w[m] |= (uint32_t)__shfl_xor((int)w[m], 2, 64);
+        }
+        if (q == 0) {
+            if (exh || n > kL2Cap) { w[0] = kOverflow; w[1] = w[2] = w[3] = 0; }
+            else w[0] |= (uint32_t)n;
+            uint8_t* l2e = a.lvl2 + lvl2_offset(a.lvl2_gstride, p, (int64_t)(ci2 * G2 + cj2) * G2 + ck2);
+            *reinterpret_cast<uint4*>(l2e) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
     }
 }
 
@@ -3076,18 +3104,34 @@ void opp2xyz_over_illum(const float inv_illum[3], float m[9]) {
     for (int i = 0; i < 9; ++i) m[i] = opp2xyz[i] * inv_illum[i / 3];
 }
 
+// Profiling: the next launches carry start/stop events in their dispatch packet
+// (hipExtLaunchKernel), so timing a kernel adds no marker packet between kernels
+// (each hipEventRecord between two kernels left the GPU idle ~5 us).
+static thread_local hipEvent_t t_ev_start = nullptr, t_ev_stop = nullptr;
+void set_launch_events(hipEvent_t start, hipEvent_t stop) {
+    t_ev_start = start;
+    t_ev_stop = stop;
+}
+#define HQ_LAUNCH(K, G, B, S, STREAM, ...)                                                   \
+    do {                                                                                     \
+        if (t_ev_start || t_ev_stop)                                                         \
+            hipExtLaunchKernelGGL(K, G, B, S, STREAM, t_ev_start, t_ev_stop, 0, __VA_ARGS__); \
+        else                                                                                 \
+            hipLaunchKernelGGL(K, G, B, S, STREAM, __VA_ARGS__);                             \
+    } while (0)
+
 hipError_t launch_prep_palette(const PaletteArgs& a, int P, hipStream_t s) {
-    hipLaunchKernelGGL(prep_palette_kernel, dim3(P), dim3(1024), 0, s, a);
+    HQ_LAUNCH(prep_palette_kernel, dim3(P), dim3(1024), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_sa_step(const SaArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(sa_step_kernel, dim3(a.P), dim3(1024), 0, s, a);
+    HQ_LAUNCH(sa_step_kernel, dim3(a.P), dim3(1024), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_build_grid(const GridArgs& a, int P, hipStream_t s) {
-    hipLaunchKernelGGL(build_grid_kernel, dim3(a.G1 * a.G1 * a.G1, P), dim3(256), 0, s, a);
+    HQ_LAUNCH(build_grid_kernel, dim3(a.G1 * a.G1 * a.G1, P), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
@@ -3102,7 +3146,7 @@ static hipError_t launch_assign_rep(const AssignArgs& a, int P, hipStream_t s) {
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    hipLaunchKernelGGL(assign_kernel<REP>, dim3(a.nblocks * P), dim3(256), lds, s, a, P);
+    HQ_LAUNCH(assign_kernel<REP>, dim3(a.nblocks * P), dim3(256), lds, s, a, P);
     return hipGetLastError();
 }
 
@@ -3117,7 +3161,7 @@ static hipError_t launch_assign_multi(const AssignArgs& a, int P, hipStream_t s)
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    hipLaunchKernelGGL((assign_multi_kernel<REP, PG>), dim3(a.nblocks, (P + PG - 1) / PG),
+    HQ_LAUNCH((assign_multi_kernel<REP, PG>), dim3(a.nblocks, (P + PG - 1) / PG),
                        dim3(256), lds, s, a, P);
     return hipGetLastError();
 }
@@ -3125,7 +3169,7 @@ static hipError_t launch_assign_multi(const AssignArgs& a, int P, hipStream_t s)
 template <int PPT>
 static hipError_t launch_assign_batch(const AssignArgs& a, int P, hipStream_t s) {
     const size_t lds = (size_t)a.K * sizeof(float4);
-    hipLaunchKernelGGL((assign_batch_kernel<1, PPT>), dim3(a.nblocks * P), dim3(256), lds, s, a, P);
+    HQ_LAUNCH((assign_batch_kernel<1, PPT>), dim3(a.nblocks * P), dim3(256), lds, s, a, P);
     return hipGetLastError();
 }
 
@@ -3138,21 +3182,21 @@ template <int PPT>
 static hipError_t launch_assign_quad(const AssignArgs& a, int P, hipStream_t s) {
     const size_t lds = (size_t)4 * a.K * sizeof(float4);
     const unsigned grid = (unsigned)(a.nblocks * ((P + 3) / 4));
-    hipLaunchKernelGGL((assign_quad_kernel<PPT>), dim3(grid), dim3(256), lds, s, a, P);
+    HQ_LAUNCH((assign_quad_kernel<PPT>), dim3(grid), dim3(256), lds, s, a, P);
     return hipGetLastError();
 }
 
 static hipError_t launch_assign_pipe(const AssignArgs& a, int P, hipStream_t s) {
     const size_t lds = (size_t)4 * a.K * sizeof(float4);
     const unsigned grid = (unsigned)(a.nblocks * ((P + 3) / 4));
-    hipLaunchKernelGGL(assign_pipe_kernel, dim3(grid), dim3(256), lds, s, a, P);
+    HQ_LAUNCH(assign_pipe_kernel, dim3(grid), dim3(256), lds, s, a, P);
     return hipGetLastError();
 }
 
 static hipError_t launch_assign_lane(const AssignArgs& a, int P, hipStream_t s) {
     const size_t lds = (size_t)4 * a.K * sizeof(float4);
     const unsigned grid = (unsigned)(a.nblocks * ((P + 3) / 4));
-    hipLaunchKernelGGL(assign_lane_kernel, dim3(grid), dim3(256), lds, s, a, P);
+    HQ_LAUNCH(assign_lane_kernel, dim3(grid), dim3(256), lds, s, a, P);
     return hipGetLastError();
 }
 
@@ -3320,10 +3364,10 @@ template <int TH, int RV, int OCC, bool TRIM, int VMODE>
 static void launch_tile_cfg(const CostArgs& a, int P, int de, hipStream_t s) {
     const dim3 grid((unsigned)(a.band_tiles * P));
     if (de == 0)
-        hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, 0, OCC, TRIM, VMODE>), grid,
+        HQ_LAUNCH((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, 0, OCC, TRIM, VMODE>), grid,
                            dim3(256), 0, s, a, P);
     else
-        hipLaunchKernelGGL((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, 1, OCC, TRIM, VMODE>), grid,
+        HQ_LAUNCH((cost_tile_kernel<kFastHalf, kFastRW, TH, RV, 1, OCC, TRIM, VMODE>), grid,
                            dim3(256), 0, s, a, P);
 }
 
@@ -3363,7 +3407,7 @@ hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, int tile_cfg, boo
         a.taps = static_cast<const char*>(a0.taps) + sizeof(CostTaps<10>);
     if (tile_cfg == 4 || tile_cfg == 5) {
         const dim3 grid((unsigned)(a.band_tiles * P));
-#define HQ_PAIR(DEV, TR, HRV) hipLaunchKernelGGL((cost_pair_kernel<DEV, TR, HRV>), grid, dim3(256), 0, s, a, P)
+#define HQ_PAIR(DEV, TR, HRV) HQ_LAUNCH((cost_pair_kernel<DEV, TR, HRV>), grid, dim3(256), 0, s, a, P)
         if (tile_cfg == 4) {
             if (de == 0) { if (trim) HQ_PAIR(0, true, 2); else HQ_PAIR(0, false, 2); }
             else { if (trim) HQ_PAIR(1, true, 2); else HQ_PAIR(1, false, 2); }
@@ -3374,39 +3418,39 @@ hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, int tile_cfg, boo
 #undef HQ_PAIR
     } else if (tile_cfg == 6) {
         const dim3 grid((unsigned)(a.band_tiles * P));
-#define HQ_CHAN(DEV, TR) hipLaunchKernelGGL((cost_chan_kernel<DEV, TR>), grid, dim3(256), 0, s, a, P)
+#define HQ_CHAN(DEV, TR) HQ_LAUNCH((cost_chan_kernel<DEV, TR>), grid, dim3(256), 0, s, a, P)
         if (de == 0) { if (trim) HQ_CHAN(0, true); else HQ_CHAN(0, false); }
         else { if (trim) HQ_CHAN(1, true); else HQ_CHAN(1, false); }
 #undef HQ_CHAN
     } else if (tile_cfg == 7) {
         const dim3 grid((unsigned)(a.band_tiles * P));
-#define HQ_MFMA(DEV, TR) hipLaunchKernelGGL((cost_mfma_kernel<DEV, TR>), grid, dim3(256), 0, s, a, P)
+#define HQ_MFMA(DEV, TR) HQ_LAUNCH((cost_mfma_kernel<DEV, TR>), grid, dim3(256), 0, s, a, P)
         if (de == 0) { if (trim) HQ_MFMA(0, true); else HQ_MFMA(0, false); }
         else { if (trim) HQ_MFMA(1, true); else HQ_MFMA(1, false); }
 #undef HQ_MFMA
     } else if (tile_cfg == 11) {
         const dim3 grid((unsigned)(a.band_tiles * P));
-#define HQ_WIDE(DEV, TR) hipLaunchKernelGGL((cost_wide_kernel<DEV, TR>), grid, dim3(256), 0, s, a, P)
+#define HQ_WIDE(DEV, TR) HQ_LAUNCH((cost_wide_kernel<DEV, TR>), grid, dim3(256), 0, s, a, P)
         if (de == 0) { if (trim) HQ_WIDE(0, true); else HQ_WIDE(0, false); }
         else { if (trim) HQ_WIDE(1, true); else HQ_WIDE(1, false); }
 #undef HQ_WIDE
     } else if (tile_cfg == 9) {
         const dim3 grid((unsigned)(a.band_tiles * P));
-#define HQ_VT(DEV, TR) hipLaunchKernelGGL((cost_vt_kernel<DEV, TR>), grid, dim3(256), 0, s, a, P)
+#define HQ_VT(DEV, TR) HQ_LAUNCH((cost_vt_kernel<DEV, TR>), grid, dim3(256), 0, s, a, P)
         if (de == 0) { if (trim) HQ_VT(0, true); else HQ_VT(0, false); }
         else { if (trim) HQ_VT(1, true); else HQ_VT(1, false); }
 #undef HQ_VT
     } else if (tile_cfg == 10) {
         for (int i = 0; i < 9; ++i) a.m_lab[i] *= kHOutScale;  // H outputs carry 2^28 (exact)
         const dim3 grid((unsigned)(a.band_tiles * P));
-#define HQ_MH(DEV, TR) hipLaunchKernelGGL((cost_mh_kernel<DEV, TR>), grid, dim3(256), 0, s, a, P)
+#define HQ_MH(DEV, TR) HQ_LAUNCH((cost_mh_kernel<DEV, TR>), grid, dim3(256), 0, s, a, P)
         if (de == 0) { if (trim) HQ_MH(0, true); else HQ_MH(0, false); }
         else { if (trim) HQ_MH(1, true); else HQ_MH(1, false); }
 #undef HQ_MH
     } else if (tile_cfg == 8) {
         for (int i = 0; i < 9; ++i) a.m_lab[i] *= kHOutScale;  // H outputs carry 2^28 (exact)
         const dim3 grid((unsigned)(a.band_tiles * P));
-#define HQ_MM(DEV, TR) hipLaunchKernelGGL((cost_mm_kernel<DEV, TR>), grid, dim3(256), 0, s, a, P)
+#define HQ_MM(DEV, TR) HQ_LAUNCH((cost_mm_kernel<DEV, TR>), grid, dim3(256), 0, s, a, P)
         if (de == 0) { if (trim) HQ_MM(0, true); else HQ_MM(0, false); }
         else { if (trim) HQ_MM(1, true); else HQ_MM(1, false); }
 #undef HQ_MM
@@ -3427,17 +3471,17 @@ hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, int tile_cfg, boo
 }
 
 hipError_t launch_cost_generic(const GenArgs& a, int de, hipStream_t s) {
-    hipLaunchKernelGGL(gen_hpass_kernel, dim3(blocks_for(a.g.n_ext)), dim3(256), 0, s, a);
+    HQ_LAUNCH(gen_hpass_kernel, dim3(blocks_for(a.g.n_ext)), dim3(256), 0, s, a);
     const int64_t n_own = (int64_t)a.g.W * (a.g.r1 - a.g.r0);
     if (de == 0)
-        hipLaunchKernelGGL(gen_vpass_kernel<0>, dim3(blocks_for(n_own)), dim3(256), 0, s, a);
+        HQ_LAUNCH(gen_vpass_kernel<0>, dim3(blocks_for(n_own)), dim3(256), 0, s, a);
     else
-        hipLaunchKernelGGL(gen_vpass_kernel<1>, dim3(blocks_for(n_own)), dim3(256), 0, s, a);
+        HQ_LAUNCH(gen_vpass_kernel<1>, dim3(blocks_for(n_own)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_finalize(const FinalizeArgs& a, int P, hipStream_t s) {
-    hipLaunchKernelGGL(finalize_kernel, dim3(P), dim3(1024), 0, s, a);
+    HQ_LAUNCH(finalize_kernel, dim3(P), dim3(1024), 0, s, a);
     return hipGetLastError();
 }
 

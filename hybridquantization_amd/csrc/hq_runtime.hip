@@ -21,6 +21,7 @@ namespace hq {
 // launchers from hq_kernels.hip
 hipError_t launch_prep_palette(const PaletteArgs&, int P, hipStream_t);
 hipError_t launch_sa_step(const SaArgs&, hipStream_t);
+void set_launch_events(hipEvent_t start, hipEvent_t stop);
 hipError_t launch_build_grid(const GridArgs&, int P, hipStream_t);
 hipError_t launch_assign(const AssignArgs&, int P, int rep, int group, int batch, hipStream_t);
 void fast_tile_dims(int W, int own_rows, int tile_cfg, int* tiles_x, int* ntiles);
@@ -145,7 +146,7 @@ struct hq_ctx {
     // profiling
     bool prof = false;
     ProfSlot prof_assign, prof_cost, prof_grid, prof_finalize;
-    hipEvent_t ev[6] = {};
+    hipEvent_t ev[8] = {};  // profiling: start/stop of grid, assign, cost, finalize
     int num_cu = 256;
 
     // banded pipeline: assign of band j+1 (stream2) runs beside cost of band j (stream)
@@ -180,7 +181,7 @@ struct hq_search {
     float t_acc = 0.f;                   // temperature / threshold of the iteration
     double keep_acc = 0.0;               // whose population awaits acceptance
     DevBuf colors[2], cand[2], err[2], seed[2], best_err, best_colors, jA, jC;
-    std::vector<hipEvent_t> pev;         // profiling: 5 events per iteration of a run
+    std::vector<hipEvent_t> pev;         // profiling: 8 events per iteration of a run
 };
 
 namespace {
@@ -426,10 +427,9 @@ PaletteArgs prep_args(hq_ctx* c, int K) {
 
 // Enqueue the evaluation of the P prepared palettes (d_pal, d_opp, d_dup,
 // d_pflags): grid, assign, cost, finalize into d_out (partial sums + used
-// flags), all-reduced if a comm is set.  ev (5 events, or null): ev[0] is
-// recorded by the caller before the palette prep; ev[1..4] after the grid, the
-// assign, the cost and the finalize kernels.  Band events (bands > 1) only with
-// the context's own profiling events.
+// flags), all-reduced if a comm is set.  ev (8 events, or null): start/stop of
+// the grid, assign, cost and finalize launches, carried by the launches
+// themselves (set_launch_events); banded cost launches use the context's pev.
 int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, BandPlan& bp) {
     const Geom& g = c->g;
     hipStream_t s = c->stream;
@@ -438,13 +438,18 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, BandPlan& bp) {
     const int64_t l1p = round_up((int64_t)G1 * G1 * G1 * 32, 256);
     const int64_t l2g = round_up((int64_t)G2 * G2 * G2 * 64, 256);  // per group of 4 palettes
     const int nblocks = c->num_cu * c->assign_blocks_per_cu;
-    const bool band_ev = ev == c->ev;
+    auto timed = [&](int slot) {
+        if (ev) set_launch_events(ev[2 * slot], ev[2 * slot + 1]);
+    };
+    auto untimed = [&]() { set_launch_events(nullptr, nullptr); };
     if (c->G2 > 0) {
         GridArgs ga{c->d_pal.as<float4>(), c->d_dup.as<uint8_t>(), c->d_pflags.as<int>(),
                     c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(), K, G1, l1p, l2g};
-        HIP_TRY(c, launch_build_grid(ga, P, s));
+        timed(0);
+        const hipError_t e = launch_build_grid(ga, P, s);
+        untimed();
+        HIP_TRY(c, e);
     }
-    if (ev) HIP_TRY(c, hipEventRecord(ev[1], s));
     bp = plan_bands(c);
     AssignArgs aa{c->d_R.as<float>(), c->d_G.as<float>(), c->d_B.as<float>(), c->d_pal.as<float4>(),
                   c->d_pflags.as<int>(), c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(),
@@ -481,7 +486,7 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, BandPlan& bp) {
         // `s` beside assign band j+1, so the latency-bound assign shares the CUs
         // with the VALU/LDS-bound cost kernel instead of running alone.
         hipStream_t s2 = c->stream2;
-        HIP_TRY(c, hipEventRecord(c->bev[kMaxBands], s));  // palettes + grid ready
+        HIP_TRY(c, hipEventRecord(c->bev[kMaxBands], s));  // palettes + grid ready (no timing)
         HIP_TRY(c, hipStreamWaitEvent(s2, c->bev[kMaxBands], 0));
         for (int j = 0; j < bp.n; ++j) {
             if (bp.blocks[j] > 0) {
@@ -503,17 +508,22 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, BandPlan& bp) {
             CostArgs cb = ca;
             cb.tile0 = bp.t0[j];
             cb.band_tiles = bp.t1[j] - bp.t0[j];
-            if (band_ev) HIP_TRY(c, hipEventRecord(c->pev[2 * j], s));
-            HIP_TRY(c, launch_cost_fast(cb, P, c->de_type, c->tile_cfg, c->trim && c->trim_ok, s));
-            if (band_ev) HIP_TRY(c, hipEventRecord(c->pev[2 * j + 1], s));
+            if (ev) set_launch_events(c->pev[2 * j], c->pev[2 * j + 1]);
+            const hipError_t e = launch_cost_fast(cb, P, c->de_type, c->tile_cfg, c->trim && c->trim_ok, s);
+            untimed();
+            HIP_TRY(c, e);
         }
         nparts = ntiles;
-        if (ev) HIP_TRY(c, hipEventRecord(ev[2], s));  // assign + cost span
     } else {
-        HIP_TRY(c, launch_assign(aa, P, c->assign_rep, c->assign_group, c->assign_batch, s));
-        if (ev) HIP_TRY(c, hipEventRecord(ev[2], s));
+        timed(1);
+        hipError_t e = launch_assign(aa, P, c->assign_rep, c->assign_group, c->assign_batch, s);
+        untimed();
+        HIP_TRY(c, e);
         if (fast) {
-            HIP_TRY(c, launch_cost_fast(ca, P, c->de_type, c->tile_cfg, c->trim && c->trim_ok, s));
+            timed(2);
+            e = launch_cost_fast(ca, P, c->de_type, c->tile_cfg, c->trim && c->trim_ok, s);
+            untimed();
+            HIP_TRY(c, e);
             nparts = ntiles;
         } else {
             HIP_TRY(c, c->d_gen_t.ensure(sizeof(float) * 7 * (size_t)g.n_ext));
@@ -535,15 +545,19 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, BandPlan& bp) {
                 ga.g = g;
                 ga.half = c->half;
                 opp2xyz_over_illum(inv, ga.m_lab);
-                HIP_TRY(c, launch_cost_generic(ga, c->de_type, s));
+                if (p == 0) timed(2);  // times the first palette's two launches (its V pass)
+                e = launch_cost_generic(ga, c->de_type, s);
+                untimed();
+                HIP_TRY(c, e);
             }
         }
     }
-    if (ev) HIP_TRY(c, hipEventRecord(ev[3], s));
     FinalizeArgs fa{c->d_partial.as<double>(), c->d_used_mask.as<uint32_t>(), c->d_out.as<double>(),
                     nparts, bp.mask_blocks, K};
-    HIP_TRY(c, launch_finalize(fa, P, s));
-    if (ev) HIP_TRY(c, hipEventRecord(ev[4], s));
+    timed(3);
+    const hipError_t ef = launch_finalize(fa, P, s);
+    untimed();
+    HIP_TRY(c, ef);
     if (c->comm) {  // also with one rank (a no-op copy), so that path is exercised on one GPU
         NCCL_TRY(c, ncclAllReduce(c->d_out.p, c->d_out.p, (size_t)P * (1 + K), ncclFloat64, ncclSum,
                                   c->comm, s));
@@ -555,17 +569,15 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, BandPlan& bp) {
 
 // Add one evaluation's kernel times (its events have completed).
 void prof_accumulate(hq_ctx* c, const hipEvent_t* ev, const BandPlan& bp) {
-    prof_add(c, c->prof_grid, ev[0], ev[1]);
-    if (bp.n > 1) {  // overlapped: "assign" = the assign + cost span, "cost" = per-band launches
-        prof_add(c, c->prof_assign, ev[1], ev[2]);
-        if (ev == c->ev)
-            for (int j = 0; j < bp.n; ++j)
-                if (bp.t1[j] > bp.t0[j]) prof_add(c, c->prof_cost, c->pev[2 * j], c->pev[2 * j + 1]);
+    if (c->G2 > 0) prof_add(c, c->prof_grid, ev[0], ev[1]);
+    if (bp.n > 1) {  // banded: per-band cost launches (assign overlaps them)
+        for (int j = 0; j < bp.n; ++j)
+            if (bp.t1[j] > bp.t0[j]) prof_add(c, c->prof_cost, c->pev[2 * j], c->pev[2 * j + 1]);
     } else {
-        prof_add(c, c->prof_assign, ev[1], ev[2]);
-        prof_add(c, c->prof_cost, ev[2], ev[3]);
+        prof_add(c, c->prof_assign, ev[2], ev[3]);
+        prof_add(c, c->prof_cost, ev[4], ev[5]);
     }
-    prof_add(c, c->prof_finalize, ev[3], ev[4]);
+    prof_add(c, c->prof_finalize, ev[6], ev[7]);
 }
 
 // Host-driven evaluation of the P palettes in h_pal: upload, prep, enqueue_core,
@@ -575,7 +587,6 @@ int enqueue_eval(hq_ctx* c, int P, int K) {
     HIP_TRY(c, hipMemcpyAsync(c->d_pal_in.p, c->h_pal, sizeof(float) * 4 * (size_t)P * K,
                               hipMemcpyHostToDevice, s));
     const hipEvent_t* ev = c->prof ? c->ev : nullptr;
-    if (ev) HIP_TRY(c, hipEventRecord(ev[0], s));
     HIP_TRY(c, launch_prep_palette(prep_args(c, K), P, s));
     BandPlan bp;
     int rc = enqueue_core(c, P, K, ev, bp);
@@ -706,14 +717,13 @@ int device_search_run(hq_search* s, int iterations, int* ran) {
     hq_ctx* c = s->ctx;
     int done = 0, rc;
     const bool prof = c->prof;
-    if (prof && (rc = ensure_events(s, (size_t)5 * iterations))) return rc;
+    if (prof && (rc = ensure_events(s, (size_t)8 * iterations))) return rc;
     std::vector<BandPlan> bps(prof ? iterations : 0);
     for (; done < iterations && s->ite < s->prm.imax; ++done) {
         const int ite = ++s->ite;
         s->pol->reduce_temperature_if_necessary(ite);                  // IM:507
         const float amax = s->pol->max_step_width(ite) / 256.0f;       // SW:91-101
-        const hipEvent_t* ev = prof ? &s->pev[(size_t)5 * done] : nullptr;
-        if (ev) HIP_TRY(c, hipEventRecord(ev[0], c->stream));
+        const hipEvent_t* ev = prof ? &s->pev[(size_t)8 * done] : nullptr;
         // accept the previous iteration's population (none at the first of a run)
         if ((rc = enqueue_sa_step(s, done > 0, false, true, false, amax))) return rc;
         BandPlan bp;
@@ -724,7 +734,7 @@ int device_search_run(hq_search* s, int iterations, int* ran) {
     }
     if (done > 0 && (rc = enqueue_sa_step(s, true, false, false, false, 0.f))) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    for (int i = 0; prof && i < done; ++i) prof_accumulate(c, &s->pev[(size_t)5 * i], bps[i]);
+    for (int i = 0; prof && i < done; ++i) prof_accumulate(c, &s->pev[(size_t)8 * i], bps[i]);
     if (ran) *ran = done;
     return HQ_OK;
 }
