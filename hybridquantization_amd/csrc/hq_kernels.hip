@@ -270,29 +270,36 @@ __device__ __forceinline__ uint64_t lcg_jump(uint64_t s, uint64_t A, uint64_t C)
     return (A * s + C) & kLcgMask;
 }
 
-__global__ __launch_bounds__(1024) void sa_step_kernel(SaArgs a) {
+// Block-shared SA state of one step (thread 0 runs the sequential logic).
+struct SaShared {
+    int unused[kSaMaxP];
+    int src[kSaMaxP];  // >= 0: member p continues from candidate src; -1: keeps its palette
+    double cur[kSaMaxP], err[kSaMaxP];
+    uint64_t seed;     // java.util.Random state after the acceptance draws
+    int best;          // candidate that set a new best (-1: none)
+};
+
+// Accept step (all threads of the block; returns after a barrier).  `writer`:
+// this block writes the shared outputs (errors, best error, next seed).
+__device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared& s) {
 #pragma clang fp contract(off)
-    const int p = blockIdx.x, tid = threadIdx.x, P = a.P, K = a.K, n4 = 4 * K;
-    __shared__ int s_unused[kSaMaxP];
-    __shared__ int s_src[kSaMaxP];   // >= 0: the palette comes from candidate s_src; -1: kept
-    __shared__ uint64_t s_seed;
-    __shared__ int s_best;           // candidate that set a new best (-1: none)
-    __shared__ double cur[kSaMaxP], err[kSaMaxP];  // thread 0's (in LDS, not scratch)
-    __shared__ float4 s_cand[kMaxK];
-    if (tid < P) s_unused[tid] = 0;
+    const int tid = threadIdx.x, nt = blockDim.x, P = a.P, K = a.K;
+    if (tid < P) s.unused[tid] = 0;
     __syncthreads();
     if (a.accept) {
-        for (int e = tid; e < P * K; e += 1024) {
+        for (int e = tid; e < P * K; e += nt) {
             const int i = e / K, k = e - i * K;
-            if (a.out[(int64_t)i * (1 + K) + 1 + k] == 0.0) atomicAdd(&s_unused[i], 1);
+            if (a.out[(int64_t)i * (1 + K) + 1 + k] == 0.0) atomicAdd(&s.unused[i], 1);
         }
         __syncthreads();
         if (tid == 0) {
             uint64_t seed = *a.seed_in;
+            double* cur = s.cur;
+            double* err = s.err;
             for (int i = 0; i < P; ++i) {
-                err[i] = a.out[(int64_t)i * (1 + K)] / a.n_total + (double)s_unused[i] * (double)a.delta;
+                err[i] = a.out[(int64_t)i * (1 + K)] / a.n_total + (double)s.unused[i] * (double)a.delta;
                 cur[i] = a.init ? err[i] : a.err_in[i];
-                s_src[i] = a.init ? i : -1;
+                s.src[i] = a.init ? i : -1;
             }
             double best = a.init ? err[0] : *a.best_err;
             int best_src = a.init ? 0 : -1;
@@ -308,47 +315,61 @@ __global__ __launch_bounds__(1024) void sa_step_kernel(SaArgs a) {
                     const bool acc = d <= 0 || exp(-d / (double)a.temperature) > lcg_next_double(seed);
                     if (acc) {
                         cur[i] = err[i];
-                        s_src[i] = i;
+                        s.src[i] = i;
                         if (cur[i] < best) { best = cur[i]; best_src = i; }
                     }
                 }
                 for (int i = 0; a.convergence && P > 1 && i < P; ++i) {  // IM:538-545
                     if (!(a.keep_threshold > lcg_next_double(seed))) {
                         cur[i] = minerror;
-                        s_src[i] = minidx;
+                        s.src[i] = minidx;
                     }
                 }
             }
-            s_seed = seed;
-            s_best = best_src;
-            if (p == 0) {
+            s.seed = seed;
+            s.best = best_src;
+            if (writer) {
                 for (int i = 0; i < P; ++i) a.err_out[i] = cur[i];
                 *a.best_err = best;
                 *a.seed_out = a.generate ? lcg_jump(seed, a.jump_A[K * 3 * P], a.jump_C[K * 3 * P]) : seed;
             }
         }
     } else if (tid == 0) {
-        s_seed = *a.seed_in;
-        s_best = -1;
-        for (int i = 0; i < P; ++i) s_src[i] = -1;
-        if (p == 0) {
+        s.seed = *a.seed_in;
+        s.best = -1;
+        for (int i = 0; i < P; ++i) s.src[i] = -1;
+        if (writer) {
             for (int i = 0; i < P; ++i) a.err_out[i] = a.err_in[i];
-            *a.seed_out = a.generate ? lcg_jump(s_seed, a.jump_A[K * 3 * P], a.jump_C[K * 3 * P]) : s_seed;
+            *a.seed_out = a.generate ? lcg_jump(s.seed, a.jump_A[K * 3 * P], a.jump_C[K * 3 * P]) : s.seed;
         }
     }
     __syncthreads();
-    // the accepted palette of member p
-    const int src = s_src[p];
+}
+
+// Member p's accepted palette (global); `lead` copies it to colors_out (and,
+// for p = 0, a new best to best_colors).
+__device__ __forceinline__ const float* sa_keep(const SaArgs& a, int p, bool lead, const SaShared& s) {
+    const int n4 = 4 * a.K, tid = threadIdx.x, nt = blockDim.x;
+    const int src = s.src[p];
     const float* from = src >= 0 ? a.cand_in + (int64_t)src * n4 : a.colors_in + (int64_t)p * n4;
-    for (int e = tid; e < n4; e += 1024) a.colors_out[(int64_t)p * n4 + e] = from[e];
-    if (p == 0 && s_best >= 0)  // IM:533-536: the best palette so far
-        for (int e = tid; e < n4; e += 1024) a.best_colors[e] = a.cand_in[(int64_t)s_best * n4 + e];
-    if (!a.generate) return;
-    // candidate p: draw t = 3i + c of this palette's block (SW:91-101 / SW:40-52)
-    const uint64_t base = lcg_jump(s_seed, a.jump_A[K * 3 * p], a.jump_C[K * 3 * p]);
-    if (tid < 3 * K) {
-        const int i = tid / 3, c = tid - 3 * i;
-        const uint64_t st = lcg_jump(base, a.jump_A[tid + 1], a.jump_C[tid + 1]);
+    if (lead) {
+        for (int e = tid; e < n4; e += nt) a.colors_out[(int64_t)p * n4 + e] = from[e];
+        if (p == 0 && s.best >= 0)  // IM:533-536: the best palette so far
+            for (int e = tid; e < n4; e += nt) a.best_colors[e] = a.cand_in[(int64_t)s.best * n4 + e];
+    }
+    return from;
+}
+
+// Candidate p into s_cand (.w = 0; cand_out too when `lead`): draw t = 3i + c of
+// this palette's block (SW:91-101 neighbours of `from`, or SW:40-52 random).
+__device__ __forceinline__ void sa_generate(const SaArgs& a, int p, const float* from, uint64_t seed,
+                                            float4* s_cand, bool lead) {
+#pragma clang fp contract(off)
+    const int K = a.K, n4 = 4 * K, tid = threadIdx.x, nt = blockDim.x;
+    const uint64_t base = lcg_jump(seed, a.jump_A[K * 3 * p], a.jump_C[K * 3 * p]);
+    for (int t = tid; t < 3 * K; t += nt) {
+        const int i = t / 3, c = t - 3 * i;
+        const uint64_t st = lcg_jump(base, a.jump_A[t + 1], a.jump_C[t + 1]);
         const float u = (float)(int32_t)(st >> 24) / (float)(1 << 24);
         float v;
         if (a.random) {
@@ -359,16 +380,27 @@ __global__ __launch_bounds__(1024) void sa_step_kernel(SaArgs a) {
             v = x > 0.f ? (x > 1.f ? 1.f : x) : 0.f;  // clampf_java (SW:103-106)
         }
         reinterpret_cast<float*>(s_cand)[4 * i + c] = v;
-        a.cand_out[(int64_t)p * n4 + 4 * i + c] = v;
+        if (lead) a.cand_out[(int64_t)p * n4 + 4 * i + c] = v;
     }
-    if (tid < K) {
-        reinterpret_cast<float*>(s_cand)[4 * tid + 3] = 0.f;
-        a.cand_out[(int64_t)p * n4 + 4 * tid + 3] = 0.f;
+    for (int k = tid; k < K; k += nt) {
+        reinterpret_cast<float*>(s_cand)[4 * k + 3] = 0.f;
+        if (lead) a.cand_out[(int64_t)p * n4 + 4 * k + 3] = 0.f;
     }
     __syncthreads();
-    const int k = tid & 255;
+}
+
+__global__ __launch_bounds__(1024) void sa_step_kernel(SaArgs a) {
+    const int p = blockIdx.x, K = a.K;
+    __shared__ SaShared s;
+    __shared__ float4 s_cand[kMaxK];
+    sa_accept(a, p == 0, s);
+    const float* from = sa_keep(a, p, true, s);
+    if (!a.generate) return;
+    sa_generate(a, p, from, s.seed, s_cand, true);
+    const int k = threadIdx.x & 255;
     prep_palette_body(a.prep, p, k < K ? s_cand[k] : make_float4(0.f, 0.f, 0.f, 0.f));
 }
+
 
 // ----------------------------------------------------------------------------
 // build_grid: grid (G1^3, P), block 256.  One workgroup per level-1 cell; it
@@ -400,8 +432,14 @@ __host__ __device__ __forceinline__ int64_t lvl2_offset(int64_t gstride, int p, 
     return (int64_t)(p >> 2) * gstride + cell * 64 + (p & 3) * 16;
 }
 
-__global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
-    const int p = blockIdx.y, cell = blockIdx.x, tid = threadIdx.x;
+// The grid work of level-1 cell `cell` of palette p; thread tid holds colour
+// tid (zeros past K) and whether it may be a candidate.  dedup: exact
+// duplicates are dropped from the cell's list itself (a colour equal to an
+// earlier one has the same bounds, so it is in the list exactly when that one
+// is): the lists of the palette-wide dup flags without their O(K^2) scan.
+__device__ __forceinline__ void grid_cell_body(const GridArgs& a, int p, int cell, float4 c,
+                                               bool valid, bool exh, bool dedup) {
+    const int tid = threadIdx.x;
     const int G1 = a.G1, G2 = 4 * G1;
     const int ci = cell / (G1 * G1), cj = (cell / G1) % G1, ck = cell % G1;
     __shared__ float4 s_col[kMaxK];
@@ -409,14 +447,6 @@ __global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
     __shared__ double s_min[4];
     __shared__ int s_wcount[4];
 
-    const bool exh = a.pflags[p] != 0;
-    const float4* pal = a.pal + (int64_t)p * kMaxK;
-    bool valid = false;
-    float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (tid < a.K) {
-        c = pal[tid];
-        valid = !exh && a.dup[(int64_t)p * kMaxK + tid] == 0;
-    }
     s_col[tid] = c;
     const double inv1 = 1.0 / G1;
     const double lo0 = ci * inv1, hi0 = (ci + 1) * inv1;
@@ -440,9 +470,31 @@ __global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
     __syncthreads();
     int base = 0;
     for (int w = 0; w < wave; ++w) base += s_wcount[w];
-    const int total = s_wcount[0] + s_wcount[1] + s_wcount[2] + s_wcount[3];
+    int total = s_wcount[0] + s_wcount[1] + s_wcount[2] + s_wcount[3];
     if (cand) s_list[base + __popcll(bal & ((1ull << lane) - 1ull))] = (uint8_t)tid;
     __syncthreads();
+    if (dedup) {
+        bool keep = false;
+        int kk = 0;
+        if (tid < total) {
+            kk = s_list[tid];
+            const float4 me = s_col[kk];
+            keep = true;
+            for (int j = 0; j < tid; ++j) {
+                const float4 o = s_col[s_list[j]];
+                if (o.x == me.x && o.y == me.y && o.z == me.z) { keep = false; break; }
+            }
+        }
+        __syncthreads();
+        const uint64_t bk = __ballot(keep);
+        if (lane == 0) s_wcount[wave] = __popcll(bk);
+        __syncthreads();
+        int b2 = 0;
+        for (int w = 0; w < wave; ++w) b2 += s_wcount[w];
+        total = s_wcount[0] + s_wcount[1] + s_wcount[2] + s_wcount[3];
+        if (keep) s_list[b2 + __popcll(bk & ((1ull << lane) - 1ull))] = (uint8_t)kk;
+        __syncthreads();
+    }
 
     uint8_t* l1 = a.lvl1 + (int64_t)p * a.lvl1_pitch + (int64_t)cell * 32;
     const bool ovf1 = exh || total > kL1Cap;
@@ -513,6 +565,48 @@ __global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
             *reinterpret_cast<uint4*>(l2e) = make_uint4(w[0], w[1], w[2], w[3]);
         }
     }
+}
+
+__global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
+    const int p = blockIdx.y, tid = threadIdx.x;
+    const bool exh = a.pflags[p] != 0;
+    bool valid = false;
+    float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (tid < a.K) {
+        c = a.pal[(int64_t)p * kMaxK + tid];
+        valid = !exh && a.dup[(int64_t)p * kMaxK + tid] == 0;
+    }
+    grid_cell_body(a, p, blockIdx.x, c, valid, exh, false);
+}
+
+// sa_step fused with build_grid: grid (G1^3, P), block 256.  Every workgroup
+// repeats the (cheap, sequential) acceptance and generates candidate p itself,
+// then builds its grid cell from it; cell 0 writes palette p's outputs (the
+// state, the candidate, its sanitised colours, opponent table and non-finite
+// flag).  Exact duplicates are dropped per cell list (grid_cell_body's dedup),
+// so the palette-wide O(K^2) duplicate scan is not needed.  One launch and one
+// dependent kernel boundary fewer per SA iteration.
+__global__ __launch_bounds__(256) void sa_grid_kernel(SaArgs a, GridArgs ga) {
+    const int p = blockIdx.y, cell = blockIdx.x, tid = threadIdx.x, K = a.K;
+    const bool lead = cell == 0;
+    __shared__ SaShared s;
+    __shared__ float4 s_cand[kMaxK];
+    sa_accept(a, lead && p == 0, s);
+    const float* from = sa_keep(a, p, lead, s);
+    sa_generate(a, p, from, s.seed, s_cand, lead);
+    const float4 c = tid < K ? s_cand[tid] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const bool bad = tid < K && !(isfinite(c.x) && isfinite(c.y) && isfinite(c.z));
+    const bool nonfinite = __syncthreads_or(bad);
+    if (lead && tid < K) {
+        const float lr = srgb_lin(c.x), lg = srgb_lin(c.y), lb = srgb_lin(c.z);
+        a.prep.pal[(int64_t)p * kMaxK + tid] = c;
+        a.prep.opp[(int64_t)p * kMaxK + tid] = make_float4(dot3(lr, lg, lb, c_RGB2Opp + 0),
+                                                           dot3(lr, lg, lb, c_RGB2Opp + 3),
+                                                           dot3(lr, lg, lb, c_RGB2Opp + 6), 0.f);
+        a.prep.dup[(int64_t)p * kMaxK + tid] = 0;
+    }
+    if (lead && tid == 0) a.prep.pflags[p] = nonfinite;
+    grid_cell_body(ga, p, cell, c, tid < K && !nonfinite, nonfinite, true);
 }
 
 // ----------------------------------------------------------------------------
@@ -877,7 +971,10 @@ __global__ __launch_bounds__(256) void assign_pipe_kernel(AssignArgs a, int P) {
             const int k = argmin_from_entry<1>(xr[h], xg[h], xb[h], E[h][pp], in_[h] && !exh_pal[pp],
                                                s_pal + pp * a.K, 0,
                                                a.lvl1 + (int64_t)pq * a.lvl1_pitch, G2, a.K);
-            a.idx[(int64_t)pq * a.idx_pitch + q] = (uint8_t)k;
+            // non-temporal: streamed out during the kernel rather than left dirty
+            // in L2 for the kernel boundary to write back (67 MB per population;
+            // ~0.5-1% per evaluation)
+            __builtin_nontemporal_store((uint8_t)k, &a.idx[(int64_t)pq * a.idx_pitch + q]);
             const uint32_t bit = 1u << (k & 31);
             if (!(s_used[pp][k >> 5] & bit)) atomicOr(&s_used[pp][k >> 5], bit);
         }
@@ -3127,6 +3224,11 @@ hipError_t launch_prep_palette(const PaletteArgs& a, int P, hipStream_t s) {
 
 hipError_t launch_sa_step(const SaArgs& a, hipStream_t s) {
     HQ_LAUNCH(sa_step_kernel, dim3(a.P), dim3(1024), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_sa_grid(const SaArgs& a, const GridArgs& ga, hipStream_t s) {
+    HQ_LAUNCH(sa_grid_kernel, dim3(ga.G1 * ga.G1 * ga.G1, a.P), dim3(256), 0, s, a, ga);
     return hipGetLastError();
 }
 

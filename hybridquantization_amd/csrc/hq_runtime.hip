@@ -21,6 +21,7 @@ namespace hq {
 // launchers from hq_kernels.hip
 hipError_t launch_prep_palette(const PaletteArgs&, int P, hipStream_t);
 hipError_t launch_sa_step(const SaArgs&, hipStream_t);
+hipError_t launch_sa_grid(const SaArgs&, const GridArgs&, hipStream_t);
 void set_launch_events(hipEvent_t start, hipEvent_t stop);
 hipError_t launch_build_grid(const GridArgs&, int P, hipStream_t);
 hipError_t launch_assign(const AssignArgs&, int P, int rep, int group, int batch, hipStream_t);
@@ -132,6 +133,8 @@ struct hq_ctx {
                            // 6 = row-pair in two channel groups (6 workgroups per CU),
                            // 7 = 6 with the vertical passes on the matrix cores (split f16; default),
                            // 8 = both passes on the matrix cores (96-column tiles)
+    int sa_fuse_grid = 0;  // device-resident search: SA step and candidate grid in one kernel
+                           // (sa_grid_kernel; 32.6 us against 12.6 + 13.5 us unfused: default off)
     int sa_device = 1;     // hq_search_*: 1 = SWASA iterations resident on the device (no host
                            // round trip per iteration), 0 = host-driven (one eval call each)
     int bands = 0;         // row bands of the assign -> cost pipeline (0/1 = one pass, serial)
@@ -430,21 +433,26 @@ PaletteArgs prep_args(hq_ctx* c, int K) {
 // flags), all-reduced if a comm is set.  ev (8 events, or null): start/stop of
 // the grid, assign, cost and finalize launches, carried by the launches
 // themselves (set_launch_events); banded cost launches use the context's pev.
-int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, BandPlan& bp) {
-    const Geom& g = c->g;
-    hipStream_t s = c->stream;
+GridArgs grid_args(hq_ctx* c, int K) {
     const int G2 = c->G2 > 0 ? c->G2 : 4;
     const int G1 = G2 / 4;
-    const int64_t l1p = round_up((int64_t)G1 * G1 * G1 * 32, 256);
-    const int64_t l2g = round_up((int64_t)G2 * G2 * G2 * 64, 256);  // per group of 4 palettes
+    return GridArgs{c->d_pal.as<float4>(), c->d_dup.as<uint8_t>(), c->d_pflags.as<int>(),
+                    c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(), K, G1,
+                    round_up((int64_t)G1 * G1 * G1 * 32, 256), round_up((int64_t)G2 * G2 * G2 * 64, 256)};
+}
+
+// grid_built: the candidate grid already exists (sa_grid_kernel built it).
+int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, BandPlan& bp, bool grid_built = false) {
+    const Geom& g = c->g;
+    hipStream_t s = c->stream;
+    const GridArgs ga = grid_args(c, K);
+    const int64_t l1p = ga.lvl1_pitch, l2g = ga.lvl2_gstride;
     const int nblocks = c->num_cu * c->assign_blocks_per_cu;
     auto timed = [&](int slot) {
         if (ev) set_launch_events(ev[2 * slot], ev[2 * slot + 1]);
     };
     auto untimed = [&]() { set_launch_events(nullptr, nullptr); };
-    if (c->G2 > 0) {
-        GridArgs ga{c->d_pal.as<float4>(), c->d_dup.as<uint8_t>(), c->d_pflags.as<int>(),
-                    c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(), K, G1, l1p, l2g};
+    if (c->G2 > 0 && !grid_built) {
         timed(0);
         const hipError_t e = launch_build_grid(ga, P, s);
         untimed();
@@ -624,7 +632,10 @@ namespace {
 
 // One sa_step launch: accept the population in cand[cd] (if `accept`), then
 // generate the next candidates into cand[1 - cd] (if `generate`).
-int enqueue_sa_step(hq_search* s, bool accept, bool init, bool generate, bool random, float amax) {
+// With generate and a candidate grid, one sa_grid_kernel launch also builds the
+// grid (*grid_built = true); ev (2 events, optional) times it.
+int enqueue_sa_step(hq_search* s, bool accept, bool init, bool generate, bool random, float amax,
+                    bool* grid_built = nullptr, const hipEvent_t* ev = nullptr) {
     hq_ctx* c = s->ctx;
     SaArgs a{};
     a.out = c->d_out.as<double>();
@@ -653,7 +664,12 @@ int enqueue_sa_step(hq_search* s, bool accept, bool init, bool generate, bool ra
     a.generate = generate;
     a.random = random;
     a.convergence = s->prm.convergence;
-    HIP_TRY(c, launch_sa_step(a, c->stream));
+    const bool fused = generate && c->G2 > 0 && c->sa_fuse_grid;
+    if (ev) set_launch_events(ev[0], ev[1]);
+    const hipError_t e = fused ? launch_sa_grid(a, grid_args(c, s->K), c->stream) : launch_sa_step(a, c->stream);
+    set_launch_events(nullptr, nullptr);
+    HIP_TRY(c, e);
+    if (grid_built) *grid_built = fused;
     s->st = 1 - s->st;
     if (generate) s->cd = 1 - s->cd;
     return HQ_OK;
@@ -703,9 +719,10 @@ int device_search_create(hq_ctx* c, const hq_swasa_params* params, int K, uint64
     HIP_TRY(c, hipMemset(s->err[0].p, 0, sizeof(double) * P));
     s->st = s->cd = 0;
     // IM:385-493: random population (SW:40-52), its evaluation, argmin
-    if ((rc = enqueue_sa_step(s, false, false, true, true, 0.f))) return rc;
+    bool built = false;
+    if ((rc = enqueue_sa_step(s, false, false, true, true, 0.f, &built))) return rc;
     BandPlan bp;
-    if ((rc = enqueue_core(c, P, K, nullptr, bp))) return rc;
+    if ((rc = enqueue_core(c, P, K, nullptr, bp, built))) return rc;
     if ((rc = enqueue_sa_step(s, true, true, false, false, 0.f))) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     s->ite = 0;
@@ -725,9 +742,10 @@ int device_search_run(hq_search* s, int iterations, int* ran) {
         const float amax = s->pol->max_step_width(ite) / 256.0f;       // SW:91-101
         const hipEvent_t* ev = prof ? &s->pev[(size_t)8 * done] : nullptr;
         // accept the previous iteration's population (none at the first of a run)
-        if ((rc = enqueue_sa_step(s, done > 0, false, true, false, amax))) return rc;
+        bool built = false;
+        if ((rc = enqueue_sa_step(s, done > 0, false, true, false, amax, &built, ev))) return rc;
         BandPlan bp;
-        if ((rc = enqueue_core(c, s->P, s->K, ev, bp))) return rc;
+        if ((rc = enqueue_core(c, s->P, s->K, ev, bp, built))) return rc;
         if (prof) bps[done] = bp;
         s->t_acc = s->pol->temperature();     // SW:54-57 at this iteration
         s->keep_acc = s->pol->keep_threshold(ite);
@@ -1238,6 +1256,8 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
         c->assign_rep = value;
     } else if (!std::strcmp(name, "sa_device")) {
         c->sa_device = value != 0;
+    } else if (!std::strcmp(name, "sa_fuse_grid")) {
+        c->sa_fuse_grid = value != 0;
     } else if (!std::strcmp(name, "bands")) {
         if (value < 0 || value > kMaxBands) return fail(c, HQ_ERR_ARG, "bands in [0,%d]", kMaxBands);
         c->bands = value;

@@ -379,8 +379,9 @@ def test_device_search_matches_host_driven(gpu, filt, P):
     m.setImage(o.inline_rgba(R, G, B).reshape(-1), None, w, filt.illum)
     lib = hq.load()
     res = {}
-    for dev in (0, 1):
-        m.setOption("sa_device", dev)
+    for dev in (0, 1, 2):  # host-driven; device, SA step fused with the grid; device, unfused
+        m.setOption("sa_device", int(dev > 0))
+        m.setOption("sa_fuse_grid", int(dev < 2))
         sw = hq.SWASA(population=P, imax=50, seed=5 + P, t0=0.05)
         params = sw.params()
         handle = C.c_void_p()
@@ -396,9 +397,10 @@ def test_device_search_matches_host_driven(gpu, filt, P):
         hq._lib.check(lib.hq_search_best(handle, hq._lib.fptr(best), C.byref(err), C.byref(it)), m.ctx)
         lib.hq_search_destroy(handle)
         res[dev] = (best, err.value, it.value, total)
-    assert res[0][2] == res[1][2] == res[0][3] == res[1][3] == 50
-    assert res[1][1] == res[0][1]
-    np.testing.assert_array_equal(res[1][0], res[0][0])
+    for dev in (1, 2):
+        assert res[dev][2] == res[0][2] == res[dev][3] == res[0][3] == 50
+        assert res[dev][1] == res[0][1]
+        np.testing.assert_array_equal(res[dev][0], res[0][0])
     m.close()
 
 
