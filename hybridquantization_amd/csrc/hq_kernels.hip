@@ -189,51 +189,66 @@ __device__ __forceinline__ int xcd_remap(int b, int N) {
 
 // Palette prep of palette p by a 1024-thread workgroup; `c` is colour k = tid & 255
 // (threads with tid >= 256 pass the same colour as their k).
+// Duplicate flags (colour k is a duplicate when an equal colour -- float
+// equality per channel -- sits at a lower index; the strict < of the argmin,
+// CL:179-193, never picks it, so build_grid leaves it out of lists) by an LDS
+// hash table of first occurrences: each colour claims or finds its key's slot
+// (open addressing, CAS on a representative index, equality checked against
+// the representative's colour), then atomicMin of its index on that slot; k is
+// a duplicate when the slot's minimum is below k.  +0/-0 hash alike (they
+// compare equal); a NaN channel equals nothing, so such a colour always takes
+// a fresh slot of its own.  (An all-pairs scan was O(K^2) VALU on one CU:
+// ~5 us per step at K = 256.)
+constexpr int kDupSlots = 2 * kMaxK;
+__device__ __forceinline__ uint32_t dup_hash(float4 c) {
+    const uint32_t x = __float_as_uint(c.x == 0.f ? 0.f : c.x);
+    const uint32_t y = __float_as_uint(c.y == 0.f ? 0.f : c.y);
+    const uint32_t z = __float_as_uint(c.z == 0.f ? 0.f : c.z);
+    const uint32_t h = x * 0x9E3779B1u ^ (y * 0x85EBCA77u + 0x27D4EB2Fu) ^ (z * 0xC2B2AE3Du + 0x165667B1u);
+    return (h ^ (h >> 15)) & (kDupSlots - 1);
+}
+
 __device__ __forceinline__ void prep_palette_body(const PaletteArgs& a, int p, float4 c) {
-    // 1024 threads: colour k = tid & 255 scans quarter q = tid >> 8 of the lower
-    // indices ([64q, 64q + 64)) for an exact duplicate; a quarter wholly above k
-    // is skipped by the whole wave.  (256 threads scanning all K entries each
-    // were latency-bound; a serial dependent loop was ~30 us.)
-    const int tid = threadIdx.x, k = tid & 255, q = tid >> 8;
+    // threads 0..K-1 handle colour k = tid; any block size >= K.
+    const int tid = threadIdx.x, k = tid;
     __shared__ float4 s[kMaxK];
-    __shared__ uint32_t s_dup[kMaxK / 32];
+    __shared__ uint32_t s_tab[kDupSlots], s_min[kDupSlots];
     __shared__ int s_nonfinite;
-    if (tid < kMaxK / 32) s_dup[tid] = 0u;
+    for (int i = tid; i < kDupSlots; i += blockDim.x) { s_tab[i] = ~0u; s_min[i] = ~0u; }
     if (tid == 0) s_nonfinite = 0;
-    if (k < a.K) c.w = 0.f;  // SW:49: palettes carry .w = 0
+    const bool own = k < a.K;
+    if (own) c.w = 0.f;  // SW:49: palettes carry .w = 0
     else c = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (own) s[k] = c;
     __syncthreads();
-    if (q == 0 && k < a.K) {
-        s[k] = c;
+    uint32_t slot = 0;
+    if (own) {
         if (!(isfinite(c.x) && isfinite(c.y) && isfinite(c.z))) atomicOr(&s_nonfinite, 1);
-    }
-    __syncthreads();
-    const int j0 = q * 64;
-    if (j0 < (tid & 0xC0) + 64 && j0 < a.K) {  // wave-uniform: quarter may hold j < k
-        bool dupb = false;
-        const int jn = min(64, a.K - j0);
-#pragma unroll 8
-        for (int u = 0; u < jn; ++u) {
-            const float4 o = s[j0 + u];
-            dupb |= (j0 + u < k) & (o.x == c.x) & (o.y == c.y) & (o.z == c.z);
+        slot = dup_hash(c);
+        for (;;) {
+            const uint32_t r = atomicCAS(&s_tab[slot], ~0u, (uint32_t)k);
+            if (r == ~0u) break;
+            const float4 o = s[r];
+            if (o.x == c.x && o.y == c.y && o.z == c.z) break;
+            slot = (slot + 1) & (kDupSlots - 1);
         }
-        if (dupb && k < a.K) atomicOr(&s_dup[k >> 5], 1u << (k & 31));
+        atomicMin(&s_min[slot], (uint32_t)k);
     }
     __syncthreads();
-    if (q == 0 && k < a.K) {
+    if (own) {
         const float lr = srgb_lin(c.x), lg = srgb_lin(c.y), lb = srgb_lin(c.z);
         const float4 opp = make_float4(dot3(lr, lg, lb, c_RGB2Opp + 0),
                                        dot3(lr, lg, lb, c_RGB2Opp + 3),
                                        dot3(lr, lg, lb, c_RGB2Opp + 6), 0.f);
         a.pal[(int64_t)p * kMaxK + k] = c;
         a.opp[(int64_t)p * kMaxK + k] = opp;
-        a.dup[(int64_t)p * kMaxK + k] = (s_dup[k >> 5] >> (k & 31)) & 1u;
+        a.dup[(int64_t)p * kMaxK + k] = s_min[slot] < (uint32_t)k ? 1u : 0u;
     }
     if (tid == 0) a.pflags[p] = s_nonfinite;
 }
 
 __global__ __launch_bounds__(1024) void prep_palette_kernel(PaletteArgs a) {
-    const int p = blockIdx.x, k = threadIdx.x & 255;
+    const int p = blockIdx.x, k = threadIdx.x;
     const float4 c = k < a.K ? a.pal_in[(int64_t)p * a.K + k] : make_float4(0.f, 0.f, 0.f, 0.f);
     prep_palette_body(a, p, c);
 }
@@ -274,34 +289,75 @@ __device__ __forceinline__ uint64_t lcg_jump(uint64_t s, uint64_t A, uint64_t C)
 struct SaShared {
     int unused[kSaMaxP];
     int src[kSaMaxP];  // >= 0: member p continues from candidate src; -1: keeps its palette
-    double cur[kSaMaxP], err[kSaMaxP];
-    uint64_t seed;     // java.util.Random state after the acceptance draws
+    double cur[kSaMaxP], err[kSaMaxP], ex[kSaMaxP];  // ex: exp(-(err - cur) / T), lanes in parallel
+    double sum[kSaMaxP], err_in[kSaMaxP];  // prefetched inputs of the sequential part
+    uint64_t seed;     // java.util.Random state (prefetched, then after the acceptance draws)
+    double best_in;
     int best;          // candidate that set a new best (-1: none)
 };
 
 // Accept step (all threads of the block; returns after a barrier).  `writer`:
-// this block writes the shared outputs (errors, best error, next seed).
+// this block writes the shared outputs (errors, best error, next seed).  Every
+// global input is loaded before the first barrier, in parallel, so the
+// sequential part on thread 0 works from LDS (a chain of dependent global
+// loads on one thread was most of this kernel's ~13 us).
 __device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared& s) {
 #pragma clang fp contract(off)
     const int tid = threadIdx.x, nt = blockDim.x, P = a.P, K = a.K;
+    constexpr int MAXF = 16;  // used flags per thread held in registers
+    const int nf = (P * K + nt - 1) / nt;
+    double fv[MAXF];
+    if (a.accept) {
+        if (tid < P) {
+            s.sum[tid] = a.out[(int64_t)tid * (1 + K)];
+            s.err_in[tid] = a.err_in[tid];
+        }
+        if (nf <= MAXF) {
+#pragma unroll
+            for (int j = 0; j < MAXF; ++j) {
+                const int e = tid + j * nt;
+                fv[j] = 1.0;
+                if (j < nf && e < P * K) {
+                    const int i = e / K, k = e - i * K;
+                    fv[j] = a.out[(int64_t)i * (1 + K) + 1 + k];
+                }
+            }
+        }
+    }
+    uint64_t jA = 0, jC = 0;  // the writer's jump past this step's draws
+    if (tid == 0) {
+        s.seed = *a.seed_in;
+        s.best_in = a.accept && !a.init ? *a.best_err : 0.0;
+        if (writer && a.generate) { jA = a.jump_A[K * 3 * P]; jC = a.jump_C[K * 3 * P]; }
+    }
     if (tid < P) s.unused[tid] = 0;
     __syncthreads();
     if (a.accept) {
-        for (int e = tid; e < P * K; e += nt) {
-            const int i = e / K, k = e - i * K;
-            if (a.out[(int64_t)i * (1 + K) + 1 + k] == 0.0) atomicAdd(&s.unused[i], 1);
+        if (nf <= MAXF) {
+#pragma unroll
+            for (int j = 0; j < MAXF; ++j) {
+                const int e = tid + j * nt;
+                if (j < nf && e < P * K && fv[j] == 0.0) atomicAdd(&s.unused[e / K], 1);
+            }
+        } else {
+            for (int e = tid; e < P * K; e += nt)
+                if (a.out[(int64_t)(e / K) * (1 + K) + 1 + e % K] == 0.0) atomicAdd(&s.unused[e / K], 1);
+        }
+        __syncthreads();
+        if (tid < P) {  // per member, in parallel: error, current, acceptance probability
+            const double e = s.sum[tid] / a.n_total + (double)s.unused[tid] * (double)a.delta;
+            const double c = a.init ? e : s.err_in[tid];
+            s.err[tid] = e;
+            s.cur[tid] = c;
+            s.ex[tid] = exp(-(e - c) / (double)a.temperature);
+            s.src[tid] = a.init ? tid : -1;
         }
         __syncthreads();
         if (tid == 0) {
-            uint64_t seed = *a.seed_in;
+            uint64_t seed = s.seed;
             double* cur = s.cur;
-            double* err = s.err;
-            for (int i = 0; i < P; ++i) {
-                err[i] = a.out[(int64_t)i * (1 + K)] / a.n_total + (double)s.unused[i] * (double)a.delta;
-                cur[i] = a.init ? err[i] : a.err_in[i];
-                s.src[i] = a.init ? i : -1;
-            }
-            double best = a.init ? err[0] : *a.best_err;
+            const double* err = s.err;
+            double best = a.init ? err[0] : s.best_in;
             int best_src = a.init ? 0 : -1;
             if (a.init) {  // IM:490-493: argmin_first
                 for (int i = 1; i < P; ++i)
@@ -312,7 +368,7 @@ __device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared
                 for (int i = 0; i < P; ++i) {  // IM:518-537
                     if (P > 1 && err[i] < minerror) { minerror = err[i]; minidx = i; }
                     const double d = err[i] - cur[i];
-                    const bool acc = d <= 0 || exp(-d / (double)a.temperature) > lcg_next_double(seed);
+                    const bool acc = d <= 0 || s.ex[i] > lcg_next_double(seed);
                     if (acc) {
                         cur[i] = err[i];
                         s.src[i] = i;
@@ -331,11 +387,10 @@ __device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared
             if (writer) {
                 for (int i = 0; i < P; ++i) a.err_out[i] = cur[i];
                 *a.best_err = best;
-                *a.seed_out = a.generate ? lcg_jump(seed, a.jump_A[K * 3 * P], a.jump_C[K * 3 * P]) : seed;
+                *a.seed_out = a.generate ? lcg_jump(seed, jA, jC) : seed;
             }
         }
     } else if (tid == 0) {
-        s.seed = *a.seed_in;
         s.best = -1;
         for (int i = 0; i < P; ++i) s.src[i] = -1;
         if (writer) {
@@ -346,37 +401,47 @@ __device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared
     __syncthreads();
 }
 
-// Member p's accepted palette (global); `lead` copies it to colors_out (and,
-// for p = 0, a new best to best_colors).
-__device__ __forceinline__ const float* sa_keep(const SaArgs& a, int p, bool lead, const SaShared& s) {
+// Member p's accepted palette into s_from (LDS, 4K floats); `lead` also copies
+// it to colors_out (and, for p = 0, a new best to best_colors).  The two likely
+// sources -- member p's candidate and its kept palette -- are read before the
+// acceptance (pf_cand, pf_col: element tid); only a convergence copy from
+// another member's candidate reads after it.
+__device__ __forceinline__ void sa_keep(const SaArgs& a, int p, bool lead, const SaShared& s,
+                                        float pf_cand, float pf_col, float* s_from) {
     const int n4 = 4 * a.K, tid = threadIdx.x, nt = blockDim.x;
     const int src = s.src[p];
-    const float* from = src >= 0 ? a.cand_in + (int64_t)src * n4 : a.colors_in + (int64_t)p * n4;
-    if (lead) {
-        for (int e = tid; e < n4; e += nt) a.colors_out[(int64_t)p * n4 + e] = from[e];
-        if (p == 0 && s.best >= 0)  // IM:533-536: the best palette so far
-            for (int e = tid; e < n4; e += nt) a.best_colors[e] = a.cand_in[(int64_t)s.best * n4 + e];
+    for (int e = tid; e < n4; e += nt) {
+        float v;
+        if (e == tid && src == p) v = pf_cand;
+        else if (e == tid && src < 0) v = pf_col;
+        else v = src >= 0 ? a.cand_in[(int64_t)src * n4 + e] : a.colors_in[(int64_t)p * n4 + e];
+        s_from[e] = v;
+        if (lead) a.colors_out[(int64_t)p * n4 + e] = v;
     }
-    return from;
+    if (lead && p == 0 && s.best >= 0)  // IM:533-536: the best palette so far
+        for (int e = tid; e < n4; e += nt) a.best_colors[e] = a.cand_in[(int64_t)s.best * n4 + e];
+    __syncthreads();
 }
 
 // Candidate p into s_cand (.w = 0; cand_out too when `lead`): draw t = 3i + c of
-// this palette's block (SW:91-101 neighbours of `from`, or SW:40-52 random).
-__device__ __forceinline__ void sa_generate(const SaArgs& a, int p, const float* from, uint64_t seed,
-                                            float4* s_cand, bool lead) {
+// this palette's block (SW:91-101 neighbours of s_from, or SW:40-52 random).
+// jA/jC: this thread's prefetched jump to its first draw (t = tid).
+__device__ __forceinline__ void sa_generate(const SaArgs& a, int p, const float* s_from, uint64_t seed,
+                                            float4* s_cand, bool lead, uint64_t jA, uint64_t jC,
+                                            uint64_t bA, uint64_t bC) {
 #pragma clang fp contract(off)
     const int K = a.K, n4 = 4 * K, tid = threadIdx.x, nt = blockDim.x;
-    const uint64_t base = lcg_jump(seed, a.jump_A[K * 3 * p], a.jump_C[K * 3 * p]);
+    const uint64_t base = lcg_jump(seed, bA, bC);  // bA, bC: jump_A/C[3Kp], prefetched
     for (int t = tid; t < 3 * K; t += nt) {
         const int i = t / 3, c = t - 3 * i;
-        const uint64_t st = lcg_jump(base, a.jump_A[t + 1], a.jump_C[t + 1]);
+        const uint64_t st = t == tid ? lcg_jump(base, jA, jC) : lcg_jump(base, a.jump_A[t + 1], a.jump_C[t + 1]);
         const float u = (float)(int32_t)(st >> 24) / (float)(1 << 24);
         float v;
         if (a.random) {
             v = u;
         } else {
             const float step = (u * 2 - 1) * a.amax;
-            const float x = from[4 * i + c] + step;
+            const float x = s_from[4 * i + c] + step;
             v = x > 0.f ? (x > 1.f ? 1.f : x) : 0.f;  // clampf_java (SW:103-106)
         }
         reinterpret_cast<float*>(s_cand)[4 * i + c] = v;
@@ -389,16 +454,59 @@ __device__ __forceinline__ void sa_generate(const SaArgs& a, int p, const float*
     __syncthreads();
 }
 
+// Prefetches of a step, issued before the acceptance: member p's candidate and
+// kept palette (element tid) and this thread's jump to draw tid.
+struct SaPf {
+    float cand = 0.f, col = 0.f;
+    uint64_t jA = 0, jC = 0, bA = 0, bC = 0;
+    __device__ __forceinline__ void load(const SaArgs& a, int p) {
+        const int n4 = 4 * a.K, tid = threadIdx.x;
+        if (tid < n4) {
+            if (a.accept) cand = a.cand_in[(int64_t)p * n4 + tid];
+            col = a.colors_in[(int64_t)p * n4 + tid];
+        }
+        if (a.generate && tid < 3 * a.K) {
+            jA = a.jump_A[tid + 1];
+            jC = a.jump_C[tid + 1];
+            bA = a.jump_A[3 * a.K * p];
+            bC = a.jump_C[3 * a.K * p];
+        }
+    }
+};
+
+// Build with -DHQ_SA_TIMING to print block 0's phase times (accept, keep,
+// generate, prep; wall_clock64 ticks of 10 ns) per launch.
 __global__ __launch_bounds__(1024) void sa_step_kernel(SaArgs a) {
     const int p = blockIdx.x, K = a.K;
     __shared__ SaShared s;
+    __shared__ float s_from[4 * kMaxK];
     __shared__ float4 s_cand[kMaxK];
+#ifdef HQ_SA_TIMING
+    const uint64_t t0 = wall_clock64();
+#endif
+    SaPf pf;
+    pf.load(a, p);
     sa_accept(a, p == 0, s);
-    const float* from = sa_keep(a, p, true, s);
+#ifdef HQ_SA_TIMING
+    const uint64_t t1 = wall_clock64();
+#endif
+    sa_keep(a, p, true, s, pf.cand, pf.col, s_from);
+#ifdef HQ_SA_TIMING
+    const uint64_t t2 = wall_clock64();
+#endif
     if (!a.generate) return;
-    sa_generate(a, p, from, s.seed, s_cand, true);
-    const int k = threadIdx.x & 255;
+    sa_generate(a, p, s_from, s.seed, s_cand, true, pf.jA, pf.jC, pf.bA, pf.bC);
+#ifdef HQ_SA_TIMING
+    const uint64_t t3 = wall_clock64();
+#endif
+    const int k = threadIdx.x;
     prep_palette_body(a.prep, p, k < K ? s_cand[k] : make_float4(0.f, 0.f, 0.f, 0.f));
+#ifdef HQ_SA_TIMING
+    __syncthreads();
+    if (threadIdx.x == 0 && p == 0)
+        printf("SA_T %d %d %d %d %d\n", a.accept, (int)(t1 - t0), (int)(t2 - t1), (int)(t3 - t2),
+               (int)(wall_clock64() - t3));
+#endif
 }
 
 
@@ -590,10 +698,13 @@ __global__ __launch_bounds__(256) void sa_grid_kernel(SaArgs a, GridArgs ga) {
     const int p = blockIdx.y, cell = blockIdx.x, tid = threadIdx.x, K = a.K;
     const bool lead = cell == 0;
     __shared__ SaShared s;
+    __shared__ float s_from[4 * kMaxK];
     __shared__ float4 s_cand[kMaxK];
+    SaPf pf;
+    pf.load(a, p);
     sa_accept(a, lead && p == 0, s);
-    const float* from = sa_keep(a, p, lead, s);
-    sa_generate(a, p, from, s.seed, s_cand, lead);
+    sa_keep(a, p, lead, s, pf.cand, pf.col, s_from);
+    sa_generate(a, p, s_from, s.seed, s_cand, lead, pf.jA, pf.jC, pf.bA, pf.bC);
     const float4 c = tid < K ? s_cand[tid] : make_float4(0.f, 0.f, 0.f, 0.f);
     const bool bad = tid < K && !(isfinite(c.x) && isfinite(c.y) && isfinite(c.z));
     const bool nonfinite = __syncthreads_or(bad);

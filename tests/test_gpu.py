@@ -227,6 +227,34 @@ def test_assign_random_and_near_ties(ip, K):
         np.testing.assert_array_equal(used[1], rev_used)
 
 
+@pytest.mark.parametrize("grid", [64, 32, 0])
+def test_assign_signed_zero_and_mass_duplicates(ip, grid):
+    """Duplicate flags (prep_palette's hash of first occurrences): +0/-0 channels
+    compare equal, long runs of one colour, and a palette of only a few distinct
+    colours (every slot chain collides) must still give the oracle's indices."""
+    rng = np.random.default_rng(11)
+    w = h = 64
+    px = np.zeros((w * h, 4), np.float32)
+    px[:, :3] = (rng.integers(0, 256, (w * h, 3)) / 255.0).astype(np.float32)
+    px[:64, :3] = 0.0
+    few = o.synthetic_palette(4, 9)
+    pal_few = few[rng.integers(0, 4, 256)].copy()
+    pal_zero = o.synthetic_palette(64, 12)
+    pal_zero[5, :3] = (0.0, 0.25, 0.0)
+    pal_zero[9, :3] = (-0.0, 0.25, -0.0)
+    pal_zero[2, :3] = (-0.0, -0.0, -0.0)
+    pal_zero[40, :3] = (0.0, 0.0, 0.0)
+    pal_run = o.synthetic_palette(200, 13)
+    pal_run[50:150] = pal_run[60]
+    ip.setOption("grid", grid)
+    ip.setImage(px.reshape(-1), np.zeros_like(px).reshape(-1), w, ip.illum)
+    pals = [pal_few, pal_zero, pal_run]
+    for pal in pals:
+        ip.computeQuantizationErrorPopulation([pal.reshape(-1)], 2.0)
+        ref_idx, _ = c_oracle.assign(px, pal)
+        np.testing.assert_array_equal(ip.getIndices(0), ref_idx.astype(np.uint8))
+
+
 @pytest.mark.parametrize("batch", [5, 3])
 @pytest.mark.parametrize("P", [1, 2, 5, 8])
 def test_assign_group_sizes(ip, P, batch):
