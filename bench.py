@@ -97,6 +97,11 @@ def main():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--bands", type=int, default=-1,
                     help="row bands of the assign/cost pipeline (-1 = library default)")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="extra libhq option (hq.h), repeatable; for experiments")
+    ap.add_argument("--shard-of", type=int, default=0, metavar="N",
+                    help="experiment: run rank 0's row block of an N-way split on one GPU, "
+                         "no collective (per-rank step time at N GPUs)")
     ap.add_argument("--cpu-size", type=int, default=1024)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -125,9 +130,15 @@ def main():
     m.setOption("grid", args.grid)
     if args.bands >= 0:
         m.setOption("bands", args.bands)
+    if args.shard_of > 0:
+        m.setOption("shard_solo", 1)
+    for kv in args.opt:
+        k, v = kv.split("=", 1)
+        m.setOption(k, int(v))
     R, G, B = synthetic_planes(W, H, seed=args.seed)
-    r0 = rank * H // world
-    r1 = (rank + 1) * H // world
+    split = args.shard_of if args.shard_of > 0 else world
+    r0 = rank * H // split
+    r1 = (rank + 1) * H // split
     _lib.check(lib.hq_set_image_planar_shard(m.ctx, _lib.fptr(R), _lib.fptr(G), _lib.fptr(B), W, H,
                                              _lib.fptr(sp.illuminant), r0, r1), m.ctx)
     del R, G, B
@@ -189,6 +200,8 @@ def main():
     P = args.population
     n_own = W * (r1 - r0)
     value = W * H * P * args.steps / elapsed / 1e6
+    if args.shard_of > 0:  # experiment: one rank's rows only (per-rank rate, not a job total)
+        value = n_own * P * args.steps / elapsed / 1e6
     # Dominant kernel: the cost kernel (S-CIELAB stencil + Opp->Lab + dE76).  With P > 1
     # palettes per launch its HBM bytes (LabRef once + P index images) amortise
     # and FP32 VALU bounds it: algorithmic flops per pixel-eval =
@@ -218,7 +231,9 @@ def main():
                                f"population P={P} palettes per step (BASELINE config 3)",
                    "image": f"{W}x{H}", "K": args.K, "population": P,
                    "parallelism": f"row-block x{world} + RCCL all-reduce" if world > 1 else "1 GPU",
-                   "argmin_grid": args.grid},
+                   "argmin_grid": args.grid,
+                   **({"shard_of": args.shard_of, "rows": [r0, r1]} if args.shard_of > 0 else {}),
+                   **({"options": args.opt} if args.opt else {})},
         "roofline": {"bound": "valu", "achieved": round(achieved_tf, 2), "peak": FP32_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4),
                      "traffic": traffic,

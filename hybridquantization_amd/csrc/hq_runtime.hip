@@ -134,6 +134,7 @@ struct hq_ctx {
                            // 7 = 6 with the vertical passes on the matrix cores (split f16; default),
                            // 8 = both passes on the matrix cores (96-column tiles)
     int sa_fuse_grid = 0;  // device-resident search: SA step and candidate grid in one kernel
+    int shard_solo = 0;    // experiment: a sharded search without a communicator (per-rank timing)
                            // (sa_grid_kernel; 32.6 us against 12.6 + 13.5 us unfused: default off)
     int sa_device = 1;     // hq_search_*: 1 = SWASA iterations resident on the device (no host
                            // round trip per iteration), 0 = host-driven (one eval call each)
@@ -1140,7 +1141,7 @@ int hq_search_create(hq_ctx* c, const hq_swasa_params* params, int K, uint64_t s
             return rc;
         }
         const bool full = c->g.r0 == 0 && c->g.r1 == c->g.H;
-        if (!full && !(c->comm && c->nranks > 1)) {
+        if (!full && !(c->comm && c->nranks > 1) && !c->shard_solo) {
             hq_search_destroy(s);
             return fail(c, HQ_ERR_STATE, "sharded context without a communicator");
         }
@@ -1256,6 +1257,8 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
         c->assign_rep = value;
     } else if (!std::strcmp(name, "sa_device")) {
         c->sa_device = value != 0;
+    } else if (!std::strcmp(name, "shard_solo")) {
+        c->shard_solo = value != 0;
     } else if (!std::strcmp(name, "sa_fuse_grid")) {
         c->sa_fuse_grid = value != 0;
     } else if (!std::strcmp(name, "bands")) {

@@ -209,7 +209,11 @@ int hq_profile_reset(hq_ctx *ctx);
  *   "band_cpb"     banded assign: pixel chunks per workgroup (default 2)
  *   "sa_device"    hq_search_*: 1 (default) = the SWASA iterations run on the device
  *                  (accept/generate kernel, no host round trip per iteration; needs
- *                  population <= 64), 0 = host-driven, one evaluation call each */
+ *                  population <= 64), 0 = host-driven, one evaluation call each
+ *   "sa_fuse_grid" device search: 1 = accept/generate and the candidate grid in one
+ *                  kernel (every grid workgroup repeats the acceptance); default 0
+ *   "shard_solo"   experiment only: let a row-block shard run hq_search_* without a
+ *                  communicator (its own partial costs; per-rank timing at N GPUs) */
 int hq_set_option(hq_ctx *ctx, const char *name, int value);
 
 #ifdef __cplusplus
