@@ -12,7 +12,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhq.so")
+LIB_PATH = os.environ.get("HQ_LIB_PATH") or os.path.join(_HERE, "libhq.so")  # override: A/B builds
 
 HQ_OK = 0
 HQ_ERR_ARG = 1

@@ -142,6 +142,30 @@ __device__ __forceinline__ float dist2_rank(float r, float g, float b, float4 c)
     return __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// (byte j of w) << 4 in one instruction (SDWA operand select): a list entry's
+// candidate index straight to its 16-byte LDS offset.
+__device__ __forceinline__ uint32_t byte_x16(uint32_t w, int j) {
+    uint32_t r;
+    switch (j) {
+    case 0: asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(w)); break;
+    case 1: asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(w)); break;
+    case 2: asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(w)); break;
+    default: asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(w)); break;
+    }
+    return r;
+}
+
+// dist2_rank with the x/y differences in one v_pk_add_f32 ({c.x, c.y} sit in
+// consecutive registers after the ds_read_b128; rg = {r, g}).  c - p is the
+// exact negation of p - c, so the squares and the result are bit-identical.
+__device__ __forceinline__ float dist2_rank_pk(f32x2 rg, float b, float4 c) {
+    const f32x2 d = f32x2{c.x, c.y} - rg;
+    const float dz = c.z - b;
+    return __builtin_fmaf(dz, dz, __builtin_fmaf(d.y, d.y, d.x * d.x));
+}
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <typename V>
@@ -790,10 +814,38 @@ __device__ __forceinline__ int argmin_from_entry(float r, float g, float b, uint
         // new value is the median of the three (v_med3_f32): 4 VALU per candidate
         // to track best, runner-up and index (the compare-and-select form took 7).
         // Slots past a lane's list (build_grid writes index 0 there) rank as +inf.
+        const f32x2 rg = {r, g};
         float best2 = dist2_rank(r, g, b, s_pal[bi * REP + copy]);
         float second2 = INFINITY;
         // the next candidate's colour is read while this one is evaluated (the
         // loop is unrolled, so the hand-over is register renaming, not a copy)
+        if constexpr (REP == 1) {
+            // Candidates tracked by LDS byte offset (index x 16): one SDWA shift
+            // takes list byte j straight to the ds_read_b128 address.
+            const char* base = reinterpret_cast<const char*>(s_pal);
+            auto at = [&](uint32_t off) { return *reinterpret_cast<const float4*>(base + off); };
+            auto cand16 = [&](int i) { return byte_x16(words[(i + 1) >> 2], (i + 1) & 3); };
+            uint32_t ba = (uint32_t)bi << 4;
+            uint32_t an = cand16(1);
+            float4 cn = at(an);
+#pragma unroll
+            for (int i = 1; i < kL1Cap; ++i) {
+                if (!__any(i < cnt)) break;
+                const uint32_t ak = an;
+                const float4 c = cn;
+                if (i + 1 < kL1Cap) {
+                    an = cand16(i + 1);
+                    cn = at(an);
+                }
+                asm volatile("" ::"v"(c.w));  // keep .w: one ds_read_b128 (16-lane groups), not b96
+                const float d2 = i < cnt ? dist2_rank_pk(rg, b, c) : INFINITY;
+                const bool lt = d2 < best2;
+                ba = lt ? ak : ba;
+                second2 = __builtin_amdgcn_fmed3f(best2, second2, d2);
+                best2 = lt ? d2 : best2;
+            }
+            bi = (int)(ba >> 4);
+        } else {
         int kn = cand(1);
         float4 cn = s_pal[kn * REP + copy];
 #pragma unroll
@@ -806,11 +858,12 @@ __device__ __forceinline__ int argmin_from_entry(float r, float g, float b, uint
                 cn = s_pal[kn * REP + copy];
             }
             asm volatile("" ::"v"(c.w));  // keep .w: one ds_read_b128 (16-lane groups), not b96
-            const float d2 = i < cnt ? dist2_rank(r, g, b, c) : INFINITY;
+            const float d2 = i < cnt ? dist2_rank_pk(rg, b, c) : INFINITY;
             const bool lt = d2 < best2;  // a select, not fminf (which canonicalises its inputs)
             bi = lt ? k : bi;
             second2 = __builtin_amdgcn_fmed3f(best2, second2, d2);
             best2 = lt ? d2 : best2;
+        }
         }
         near = second2 <= best2 * (1.0f + 1e-6f);
     }
@@ -1018,7 +1071,9 @@ __device__ __forceinline__ int64_t quad_cell(float r, float g, float b, int G2) 
 
 __global__ __launch_bounds__(256) void assign_pipe_kernel(AssignArgs a, int P) {
     constexpr int PPT = 8;  // pixels per thread per chunk (the pipeline runs across chunks)
-    extern __shared__ __attribute__((aligned(16))) float4 s_pal[];  // [4][K]
+    // [4][kMaxK]: a fixed palette stride, so each palette's base folds into the
+    // ds_read_b128 offset field and a candidate's address is its byte << 4
+    __shared__ __attribute__((aligned(16))) float4 s_pal[4 * kMaxK];
     __shared__ uint32_t s_used[4][8];
     const int ngroups = (P + 3) / 4;
     const int w = xcd_remap(blockIdx.x, a.nblocks * ngroups);
@@ -1026,7 +1081,7 @@ __global__ __launch_bounds__(256) void assign_pipe_kernel(AssignArgs a, int P) {
     const int p0 = 4 * grp, ng = min(4, P - p0);
     for (int e = tid; e < ng * a.K; e += 256) {
         const int pp = e / a.K, k = e - pp * a.K;
-        s_pal[e] = a.pal[(int64_t)(p0 + pp) * kMaxK + k];
+        s_pal[pp * kMaxK + k] = a.pal[(int64_t)(p0 + pp) * kMaxK + k];
     }
     if (tid < 32) s_used[tid >> 3][tid & 7] = 0;
     __syncthreads();
@@ -1080,7 +1135,7 @@ __global__ __launch_bounds__(256) void assign_pipe_kernel(AssignArgs a, int P) {
             if (pp >= ng) break;
             const int pq = p0 + pp;
             const int k = argmin_from_entry<1>(xr[h], xg[h], xb[h], E[h][pp], in_[h] && !exh_pal[pp],
-                                               s_pal + pp * a.K, 0,
+                                               s_pal + pp * kMaxK, 0,
                                                a.lvl1 + (int64_t)pq * a.lvl1_pitch, G2, a.K);
             // non-temporal: streamed out during the kernel rather than left dirty
             // in L2 for the kernel boundary to write back (67 MB per population;
@@ -2045,7 +2100,6 @@ __global__ __launch_bounds__(256) void error_image_kernel(const float4* orig, co
 // columns per item: HR = 2 gives 216 items per tile (balanced over 256 threads)
 // at 1.8x the LDS reads per output; HR = 4 keeps the reads but fills 108 threads.
 // ----------------------------------------------------------------------------
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <int HALF, int TH, int RW, int HR, int TLO = 0, int THI = 2 * HALF>
 __device__ __forceinline__ void hpass_pair_filters(const f32x4* src, TapsPtr<HALF> taps, int f0,
@@ -3400,7 +3454,7 @@ static hipError_t launch_assign_quad(const AssignArgs& a, int P, hipStream_t s) 
 }
 
 static hipError_t launch_assign_pipe(const AssignArgs& a, int P, hipStream_t s) {
-    const size_t lds = (size_t)4 * a.K * sizeof(float4);
+    const size_t lds = 0;  // static [4][kMaxK] palette table
     const unsigned grid = (unsigned)(a.nblocks * ((P + 3) / 4));
     HQ_LAUNCH(assign_pipe_kernel, dim3(grid), dim3(256), lds, s, a, P);
     return hipGetLastError();
