@@ -1079,15 +1079,6 @@ __global__ __launch_bounds__(256) void assign_pipe_kernel(AssignArgs a, int P) {
     const int w = xcd_remap(blockIdx.x, a.nblocks * ngroups);
     const int grp = w % ngroups, blk = w / ngroups, tid = threadIdx.x;
     const int p0 = 4 * grp, ng = min(4, P - p0);
-    for (int e = tid; e < ng * a.K; e += 256) {
-        const int pp = e / a.K, k = e - pp * a.K;
-        s_pal[pp * kMaxK + k] = a.pal[(int64_t)(p0 + pp) * kMaxK + k];
-    }
-    if (tid < 32) s_used[tid >> 3][tid & 7] = 0;
-    __syncthreads();
-    bool exh_pal[4];
-#pragma unroll
-    for (int pp = 0; pp < 4; ++pp) exh_pal[pp] = pp >= ng || a.pflags[p0 + min(pp, ng - 1)] != 0 || a.G2 == 0;
     const uint8_t* lines = a.lvl2 + (int64_t)grp * a.lvl2_gstride;
     const int G2 = a.G2 > 0 ? a.G2 : 4;
     // pixel sequence of this thread: chunk c (stride nblocks), slot j < PPT
@@ -1128,6 +1119,17 @@ __global__ __launch_bounds__(256) void assign_pipe_kernel(AssignArgs a, int P) {
     lookup(qq[0], xr[0], xg[0], xb[0], in_[0], E[0]);
     load_rgb(qpos(1), rb[1], gb[1], bb[1]);
     load_rgb(qpos(2), rb[0], gb[0], bb[0]);
+    // The palette table is filled while the first pixels' loads are in flight
+    // (the fill used to come first: one more memory round trip per workgroup).
+    for (int e = tid; e < ng * a.K; e += 256) {
+        const int pp = e / a.K, k = e - pp * a.K;
+        s_pal[pp * kMaxK + k] = a.pal[(int64_t)(p0 + pp) * kMaxK + k];
+    }
+    if (tid < 32) s_used[tid >> 3][tid & 7] = 0;
+    __syncthreads();
+    bool exh_pal[4];
+#pragma unroll
+    for (int pp = 0; pp < 4; ++pp) exh_pal[pp] = pp >= ng || a.pflags[p0 + min(pp, ng - 1)] != 0 || a.G2 == 0;
     auto resolve = [&](int h) {
         const int64_t q = qq[h];
 #pragma unroll
