@@ -432,6 +432,39 @@ def test_device_search_matches_host_driven(gpu, filt, P):
     m.close()
 
 
+def test_device_search_with_single_rank_comm(gpu, filt):
+    """The multi-GPU search loop on one GPU: with libhq's RCCL communicator the
+    all-reduce sits between finalize and sa_step in every iteration; with one
+    rank the trajectory must be the one without a communicator."""
+    import ctypes as C
+    w, h, K, P = 80, 72, 24, 4
+    R, G, B = o.synthetic_image(w, h, seed=12)
+    lib = hq.load()
+    res = []
+    for comm in (False, True):
+        m = hq.ImageManipulation(device=gpu)
+        hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
+        m.setImage(o.inline_rgba(R, G, B).reshape(-1), None, w, filt.illum)
+        if comm:
+            m.initComm(1, 0, hq.ImageManipulation.commUniqueId())
+        sw = hq.SWASA(population=P, imax=30, seed=21, t0=0.05)
+        params = sw.params()
+        handle = C.c_void_p()
+        hq._lib.check(lib.hq_search_create(m.ctx, C.byref(params), K, sw.seed, C.byref(handle)), m.ctx)
+        ran = C.c_int()
+        hq._lib.check(lib.hq_search_run(handle, 30, C.byref(ran)), m.ctx)
+        best = np.zeros(4 * K, np.float32)
+        err = C.c_double()
+        it = C.c_int()
+        hq._lib.check(lib.hq_search_best(handle, hq._lib.fptr(best), C.byref(err), C.byref(it)), m.ctx)
+        lib.hq_search_destroy(handle)
+        m.close()
+        res.append((best, err.value, ran.value))
+    assert res[0][2] == res[1][2] == 30
+    assert res[0][1] == res[1][1]
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+
+
 # ---------------------------------------------------------------------------
 # Full-size properties (4096^2, K = 256): determinism, grid == exhaustive,
 # fast == generic, shards == full.
