@@ -214,6 +214,11 @@ def main():
     traffic = measured_traffic(W, args.K, P, args.grid, world)
     # whole-evaluation view: the metric's 24 B/px-eval HBM-read roofline
     eval_roof_mpx = HBM_PEAK_GBS * 1e9 / 24.0 / 1e6 * args.gpus
+    # which BASELINE.json config this run's shape is (configs[2] is the default)
+    shape = (W, args.K, P)
+    cfg_name = {(4096, 256, 4): "BASELINE config 3", (1024, 64, 1): "BASELINE config 2",
+                (8192, 256, 4): "BASELINE config 4", (4096, 256, 64): "BASELINE config 5",
+                (256, 16, 4): "BASELINE config 1"}.get(shape, "not a BASELINE config")
     out = {
         "metric": "Mpixel*evals/s (SWASA dE cost) at 4096x4096 K=256",
         "value": round(value, 2),
@@ -228,7 +233,7 @@ def main():
         "dtype": "f32",
         "data": "synthetic (SplitMix64 u8 RGB image, java.util.Random-seeded SWASA palettes)",
         "config": {"workload": f"SWASA search iteration, {W}x{H} RGB image, K={args.K}, "
-                               f"population P={P} palettes per step (BASELINE config 3)",
+                               f"population P={P} palettes per step ({cfg_name})",
                    "image": f"{W}x{H}", "K": args.K, "population": P,
                    "parallelism": f"row-block x{world} + RCCL all-reduce" if world > 1 else "1 GPU",
                    "argmin_grid": args.grid,
