@@ -1069,16 +1069,20 @@ __device__ __forceinline__ int64_t quad_cell(float r, float g, float b, int G2) 
            min((int)(b * (float)G2), G2 - 1);
 }
 
+// NG = min(P, 4): the palettes a pixel pass can serve.  A population below 4
+// loads only its NG 16-B entries of each 64-B level-2 line (P = 1 issued four
+// dwordx4 lookups per pixel for one useful one) and keeps NG palette tables.
+template <int NG>
 __global__ __launch_bounds__(256) void assign_pipe_kernel(AssignArgs a, int P) {
     constexpr int PPT = 8;  // pixels per thread per chunk (the pipeline runs across chunks)
-    // [4][kMaxK]: a fixed palette stride, so each palette's base folds into the
+    // [NG][kMaxK]: a fixed palette stride, so each palette's base folds into the
     // ds_read_b128 offset field and a candidate's address is its byte << 4
-    __shared__ __attribute__((aligned(16))) float4 s_pal[4 * kMaxK];
-    __shared__ uint32_t s_used[4][8];
+    __shared__ __attribute__((aligned(16))) float4 s_pal[NG * kMaxK];
+    __shared__ uint32_t s_used[NG][8];
     const int ngroups = (P + 3) / 4;
     const int w = xcd_remap(blockIdx.x, a.nblocks * ngroups);
     const int grp = w % ngroups, blk = w / ngroups, tid = threadIdx.x;
-    const int p0 = 4 * grp, ng = min(4, P - p0);
+    const int p0 = 4 * grp, ng = min(NG, P - p0);
     const uint8_t* lines = a.lvl2 + (int64_t)grp * a.lvl2_gstride;
     const int G2 = a.G2 > 0 ? a.G2 : 4;
     // pixel sequence of this thread: chunk c (stride nblocks), slot j < PPT
@@ -1097,11 +1101,11 @@ __global__ __launch_bounds__(256) void assign_pipe_kernel(AssignArgs a, int P) {
         g = a.G[qc];
         b = a.B[qc];
     };
-    auto lookup = [&](int64_t q, float r, float g, float b, bool& inside, uint4 (&e)[4]) {
+    auto lookup = [&](int64_t q, float r, float g, float b, bool& inside, uint4 (&e)[NG]) {
         inside = q < a.n_ext && r >= 0.f && r <= 1.f && g >= 0.f && g <= 1.f && b >= 0.f && b <= 1.f;
         const uint4* line = reinterpret_cast<const uint4*>(lines + (inside ? quad_cell(r, g, b, G2) : 0) * 64);
 #pragma unroll
-        for (int pp = 0; pp < 4; ++pp) e[pp] = line[pp];  // selected by the `listed` flag at use
+        for (int pp = 0; pp < NG; ++pp) e[pp] = line[pp];  // selected by the `listed` flag at use
     };
     // Pipeline, unrolled by two so every buffer has a fixed register set (a
     // register copy of an in-flight load waits for it: rotating buffers at the
@@ -1111,7 +1115,7 @@ __global__ __launch_bounds__(256) void assign_pipe_kernel(AssignArgs a, int P) {
     // buffer; pixel i is resolved from E[h], X[h] while those loads fly.
     float rb[2], gb[2], bb[2];        // RGB loads in flight: pixel i+1 / i+2 by parity
     float xr[2], xg[2], xb[2];        // RGB of pixels being looked up / resolved
-    uint4 E[2][4];
+    uint4 E[2][NG];
     bool in_[2];
     int64_t qq[2];
     load_rgb(qpos(0), xr[0], xg[0], xb[0]);
@@ -1125,15 +1129,15 @@ __global__ __launch_bounds__(256) void assign_pipe_kernel(AssignArgs a, int P) {
         const int pp = e / a.K, k = e - pp * a.K;
         s_pal[pp * kMaxK + k] = a.pal[(int64_t)(p0 + pp) * kMaxK + k];
     }
-    if (tid < 32) s_used[tid >> 3][tid & 7] = 0;
+    if (tid < 8 * NG) s_used[tid >> 3][tid & 7] = 0;
     __syncthreads();
-    bool exh_pal[4];
+    bool exh_pal[NG];
 #pragma unroll
-    for (int pp = 0; pp < 4; ++pp) exh_pal[pp] = pp >= ng || a.pflags[p0 + min(pp, ng - 1)] != 0 || a.G2 == 0;
+    for (int pp = 0; pp < NG; ++pp) exh_pal[pp] = pp >= ng || a.pflags[p0 + min(pp, ng - 1)] != 0 || a.G2 == 0;
     auto resolve = [&](int h) {
         const int64_t q = qq[h];
 #pragma unroll
-        for (int pp = 0; pp < 4; ++pp) {
+        for (int pp = 0; pp < NG; ++pp) {
             if (pp >= ng) break;
             const int pq = p0 + pp;
             const int k = argmin_from_entry<1>(xr[h], xg[h], xb[h], E[h][pp], in_[h] && !exh_pal[pp],
@@ -3456,9 +3460,14 @@ static hipError_t launch_assign_quad(const AssignArgs& a, int P, hipStream_t s) 
 }
 
 static hipError_t launch_assign_pipe(const AssignArgs& a, int P, hipStream_t s) {
-    const size_t lds = 0;  // static [4][kMaxK] palette table
+    const size_t lds = 0;  // static [NG][kMaxK] palette table
     const unsigned grid = (unsigned)(a.nblocks * ((P + 3) / 4));
-    HQ_LAUNCH(assign_pipe_kernel, dim3(grid), dim3(256), lds, s, a, P);
+    switch (P) {
+    case 1: HQ_LAUNCH(assign_pipe_kernel<1>, dim3(grid), dim3(256), lds, s, a, P); break;
+    case 2: HQ_LAUNCH(assign_pipe_kernel<2>, dim3(grid), dim3(256), lds, s, a, P); break;
+    case 3: HQ_LAUNCH(assign_pipe_kernel<3>, dim3(grid), dim3(256), lds, s, a, P); break;
+    default: HQ_LAUNCH(assign_pipe_kernel<4>, dim3(grid), dim3(256), lds, s, a, P); break;
+    }
     return hipGetLastError();
 }
 

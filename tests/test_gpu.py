@@ -256,10 +256,11 @@ def test_assign_signed_zero_and_mass_duplicates(ip, grid):
 
 
 @pytest.mark.parametrize("batch", [5, 3])
-@pytest.mark.parametrize("P", [1, 2, 5, 8])
+@pytest.mark.parametrize("P", [1, 2, 3, 5, 8])
 def test_assign_group_sizes(ip, P, batch):
     """Groups of 1-4 palettes per pixel pass (P = 5: a full group and a group of
-    one; the lane kernel then runs 64 / ng pixels per wave instruction)."""
+    one; the lane kernel then runs 64 / ng pixels per wave instruction).  P = 1,
+    2, 3 run assign_pipe_kernel<NG = P>, P >= 4 its NG = 4 instance."""
     rng = np.random.default_rng(P)
     w, h, K = 75, 41, 96
     px = np.zeros((w * h, 4), np.float32)
