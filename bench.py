@@ -239,7 +239,7 @@ def main():
                    "argmin_grid": args.grid,
                    **({"shard_of": args.shard_of, "rows": [r0, r1]} if args.shard_of > 0 else {}),
                    **({"options": args.opt} if args.opt else {})},
-        "roofline": {"bound": "valu", "achieved": round(achieved_tf, 2), "peak": FP32_PEAK_TFLOPS,
+        "roofline": {"bound": "mfma", "limiter": "valu", "achieved": round(achieved_tf, 2), "peak": FP32_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4),
                      "traffic": traffic,
                      "kernel": "cost_mfma_kernel (cost_tile 7)", "kernel_avg_ms": round(cost_ms, 4),
@@ -247,8 +247,8 @@ def main():
                      "hbm_GBs_alg": round(alg_bytes / (cost_ms * 1e-3) / 1e9, 1) if cost_ms > 0 else 0.0,
                      "note": "fp32-accurate stencil: vertical taps on the matrix cores as split-f16 "
                              "products (hi*hi+hi*lo+lo*hi, fp32 accumulate), horizontal taps, Lab and dE on "
-                             "FP32 VALU (the bound); achieved = the algorithm's fp32 flops / kernel time; "
-                             "peak = MI355X FP32 vector (= FP32 MFMA) 157.3 TFLOP/s; "
+                             "FP32 VALU; achieved = the algorithm's fp32 flops / kernel time; "
+                             "bound mfma = the compute roof: peak = the dense FP32 MFMA peak for this f32 path, 157.3 TFLOP/s, which equals the FP32 vector peak on gfx950; limiter = the unit that saturates first in the PMC counters (VALU issue, with LDS close behind, DESIGN.md section 6); "
                              "traffic = HBM bytes/launch from the committed rocprofv3 FETCH_SIZE(x2)+WRITE_SIZE "
                              "passes (profiles/r01_hbm_traffic.json) when their config matches; kernel_avg_ms: HIP "
                              "events carried by the launches on the context stream over a second pass of the same "
