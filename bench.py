@@ -58,31 +58,85 @@ def measured_traffic(size, K, P, grid, world):
     return None
 
 
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(args):
-    """Oracle (C restatement, 'port') on this host's cores over a bounded sample."""
+    """BASELINE.md's CPU plan on this host's cores: the C restatement of the
+    reference's semantics (oracle/hq_oracle.c, 'port'; the reference's own Java
+    path computes no cost without OpenCL, IM:392, IM:590).  The headline value
+    is the same-shape eval (4096^2, K = 256) on every core this process may use;
+    also timed: the C1 256^2 / K = 16 full evaluation loop on those cores, and
+    one thread on a 1024^2 / K = 256 sample.  LabRef is setup, not timed (the
+    eval's work does not depend on its values, so a zero LabRef is used)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import c_oracle  # checker/baseline only
     import oracle as o
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    w = h = args.cpu_size
-    R, G, B = o.synthetic_image(w, h, seed=1)
-    rgba = o.inline_rgba(R, G, B)
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    # every core this process may use, capped at the box's CPU share for one GPU
+    # (OMP_NUM_THREADS, 16 on the GPU boxes, whose nproc shows the whole machine)
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = int(os.environ.get("HQ_CPU_THREADS", "0")) or min(usable or 1, share or usable or 1)
     f = o.design_filters()
-    lab = c_oracle.srgb_to_scielab(R, G, B, f, w)
-    evals = 0
+
+    def rate(w, K, nthreads, seconds, max_evals):
+        R, G, B = o.synthetic_image(w, w, seed=1)
+        rgba = o.inline_rgba(R, G, B)
+        lab = np.zeros_like(rgba)
+        c_oracle.eval_palette(rgba, lab, o.synthetic_palette(K, 1), f, w, nthreads=nthreads)  # warm
+        evals, t0 = 0, time.perf_counter()
+        while True:
+            c_oracle.eval_palette(rgba, lab, o.synthetic_palette(K, 2 + evals), f, w, nthreads=nthreads)
+            evals += 1
+            el = time.perf_counter() - t0
+            if el >= seconds or evals >= max_evals:
+                return w * w * evals / el / 1e6, evals, el
+
+    v, n, el = rate(args.size, args.K, threads, args.cpu_seconds, 64)
+    c1, n1, el1 = rate(256, 16, threads, 2.0, 4096)
+    st, ns, els = rate(1024, args.K, 1, 4.0, 64)
+    return {"value": round(v, 3), "unit": "Mpixel*evals/s", "cores": threads, "kind": "port",
+            "nproc": os.cpu_count(), "usable_cpus": usable, "cpu_share": share or None,
+            "cpu_model": _cpu_model(),
+            "sample": f"{args.size}x{args.size} image, K={args.K}: {n} candidate evaluations on "
+                      f"{threads} threads in {el:.1f} s (C restatement oracle/hq_oracle.c: "
+                      f"exhaustive argmin, S-CIELAB stencil, Lab, dE76, fp64 sum)",
+            "c1_256_k16": {"value": round(c1, 3), "evals": n1, "seconds": round(el1, 2),
+                           "threads": threads},
+            "single_thread_1024_k256": {"value": round(st, 3), "evals": ns,
+                                        "seconds": round(els, 2), "threads": 1}}
+
+
+def full_search(lib, _lib, m, K, P, seed, sa_device):
+    """BASELINE config 3 as the plugin runs it: one SWASA search of imax = 5000
+    iterations with the default schedule (HQ:197-224), P palettes per
+    iteration.  Returns wall time, iterations and the best error found."""
+    import hybridquantization_amd as hq
+
+    m.setOption("sa_device", sa_device)
+    sw = hq.SWASA(population=P, seed=seed)
+    params = sw.params()
+    s = C.c_void_p()
     t0 = time.perf_counter()
-    while True:
-        pal = o.synthetic_palette(args.K, 2 + evals)
-        c_oracle.eval_palette(rgba, lab, pal, f, w, nthreads=threads)
-        evals += 1
-        el = time.perf_counter() - t0
-        if el >= args.cpu_seconds or evals >= 4096:
-            break
-    return {"value": w * h * evals / el / 1e6, "unit": "Mpixel*evals/s", "cores": threads,
-            "kind": "port",
-            "sample": f"{w}x{h} image, K={args.K}, {evals} candidate evaluations "
-                      f"(C restatement oracle/hq_oracle.c, {threads} threads, {el:.1f} s)"}
+    _lib.check(lib.hq_search_create(m.ctx, C.byref(params), K, sw.seed, C.byref(s)), m.ctx)
+    ran = C.c_int()
+    _lib.check(lib.hq_search_run(s, params.imax, C.byref(ran)), m.ctx)
+    best = np.zeros(4 * K, np.float32)
+    err = C.c_double()
+    it = C.c_int()
+    _lib.check(lib.hq_search_best(s, _lib.fptr(best), C.byref(err), C.byref(it)), m.ctx)
+    wall = time.perf_counter() - t0
+    lib.hq_search_destroy(s)
+    m.setOption("sa_device", 1)
+    return {"wall_s": round(wall, 3), "iterations": it.value, "best_error": err.value}, best
 
 
 def main():
@@ -95,16 +149,15 @@ def main():
     ap.add_argument("--population", type=int, default=4)
     ap.add_argument("--grid", type=int, default=32)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--bands", type=int, default=-1,
-                    help="row bands of the assign/cost pipeline (-1 = library default)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="extra libhq option (hq.h), repeatable; for experiments")
     ap.add_argument("--shard-of", type=int, default=0, metavar="N",
                     help="experiment: run rank 0's row block of an N-way split on one GPU, "
                          "no collective (per-rank step time at N GPUs)")
-    ap.add_argument("--cpu-size", type=int, default=1024)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-full-search", action="store_true",
+                    help="skip the imax = 5000 search of BASELINE config 3 (extra keys)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -120,6 +173,7 @@ def main():
 
     import hybridquantization_amd as hq
     from hybridquantization_amd import _lib
+    from hybridquantization_amd import dist as hqd
 
     lib = hq.load()
     W = H = args.size
@@ -128,28 +182,18 @@ def main():
         raise RuntimeError("bench.py: libhq could not open the GPU")
     sp = hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
     m.setOption("grid", args.grid)
-    if args.bands >= 0:
-        m.setOption("bands", args.bands)
     if args.shard_of > 0:
         m.setOption("shard_solo", 1)
     for kv in args.opt:
         k, v = kv.split("=", 1)
         m.setOption(k, int(v))
     R, G, B = synthetic_planes(W, H, seed=args.seed)
-    split = args.shard_of if args.shard_of > 0 else world
-    r0 = rank * H // split
-    r1 = (rank + 1) * H // split
+    r0, r1 = hqd.shard_rows(H, args.shard_of if args.shard_of > 0 else world, rank)
     _lib.check(lib.hq_set_image_planar_shard(m.ctx, _lib.fptr(R), _lib.fptr(G), _lib.fptr(B), W, H,
                                              _lib.fptr(sp.illuminant), r0, r1), m.ctx)
     del R, G, B
     if world > 1:
-        import torch
-
-        uid = torch.zeros(128, dtype=torch.uint8)
-        if rank == 0:
-            uid = torch.frombuffer(bytearray(hq.ImageManipulation.commUniqueId()), dtype=torch.uint8)
-        dist.broadcast(uid, 0)
-        m.initComm(world, rank, bytes(uid.numpy().tobytes()))
+        hqd.init_comm(m, dist, world, rank)
 
     sw = hq.SWASA(population=args.population, imax=10 ** 9, seed=args.seed)
     params = sw.params()
@@ -179,11 +223,7 @@ def main():
     _lib.check(lib.hq_search_run(search, args.steps, C.byref(ran)), m.ctx)
     lib.hq_profile_enable(m.ctx, 0)
     if world > 1:
-        import torch
-
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = hqd.max_over_ranks(dist, elapsed)
 
     prof = {}
     for k in ("grid", "assign", "cost", "finalize"):
@@ -204,21 +244,37 @@ def main():
         value = n_own * P * args.steps / elapsed / 1e6
     # Dominant kernel: the cost kernel (S-CIELAB stencil + Opp->Lab + dE76).  With P > 1
     # palettes per launch its HBM bytes (LabRef once + P index images) amortise
-    # and FP32 VALU bounds it: algorithmic flops per pixel-eval =
-    # the reference's stencil, 7 separable filters x 2 passes x 21 taps x 2 flops
-    # = 588, + Opp->Lab / dE76 ~ 40 (DESIGN.md "Roofline accounting").
+    # and FP32 VALU bounds it.  Algorithmic flops per pixel-eval: the
+    # reference's stencil, 7 separable filters x 2 passes x 21 taps x 2 flops = 588,
+    # + Opp->Lab / dE76 ~ 40 (nominal 628); the kernel executes 2 x 111 significant
+    # taps (the narrow k1 filters trimmed) + Lab / dE = 484 (DESIGN.md "Roofline").
     cost_ms = prof["cost"][0]
     alg_flops = n_own * P * (588 + 40)
+    exec_flops = n_own * P * (2 * 2 * 111 + 40)
     achieved_tf = alg_flops / (cost_ms * 1e-3) / 1e12 if cost_ms > 0 else 0.0
+    exec_tf = exec_flops / (cost_ms * 1e-3) / 1e12 if cost_ms > 0 else 0.0
     alg_bytes = n_own * (12 + P)
+    hbm_gbs = alg_bytes / (cost_ms * 1e-3) / 1e9 if cost_ms > 0 else 0.0
     traffic = measured_traffic(W, args.K, P, args.grid, world)
     # whole-evaluation view: the metric's 24 B/px-eval HBM-read roofline
-    eval_roof_mpx = HBM_PEAK_GBS * 1e9 / 24.0 / 1e6 * args.gpus
+    eval_roof_mpx = HBM_PEAK_GBS * 1e9 / 24.0 / 1e6 * world
     # which BASELINE.json config this run's shape is (configs[2] is the default)
     shape = (W, args.K, P)
     cfg_name = {(4096, 256, 4): "BASELINE config 3", (1024, 64, 1): "BASELINE config 2",
                 (8192, 256, 4): "BASELINE config 4", (4096, 256, 64): "BASELINE config 5",
                 (256, 16, 4): "BASELINE config 1"}.get(shape, "not a BASELINE config")
+    search_line = None
+    if rank == 0 and world == 1 and args.shard_of == 0 and not args.no_full_search:
+        dev, bdev = full_search(lib, _lib, m, args.K, P, args.seed, 1)
+        host, bhost = full_search(lib, _lib, m, args.K, P, args.seed, 0)
+        search_line = {"config": f"BASELINE config 3: {W}x{H}, K={args.K}, P={P}, imax=5000, "
+                                 "default SWASA schedule (HQ:197-224), seed "
+                                 f"{args.seed}",
+                       "device_resident": dev, "host_driven": host,
+                       "ms_per_iteration_device": round(dev["wall_s"] / max(dev["iterations"], 1) * 1e3, 4),
+                       "device_host_agree": bool(dev["best_error"] == host["best_error"]
+                                                 and np.array_equal(bdev, bhost)
+                                                 and dev["iterations"] == host["iterations"])}
     out = {
         "metric": "Mpixel*evals/s (SWASA dE cost) at 4096x4096 K=256",
         "value": round(value, 2),
@@ -239,25 +295,32 @@ def main():
                    "argmin_grid": args.grid,
                    **({"shard_of": args.shard_of, "rows": [r0, r1]} if args.shard_of > 0 else {}),
                    **({"options": args.opt} if args.opt else {})},
-        "roofline": {"bound": "mfma", "limiter": "valu", "achieved": round(achieved_tf, 2), "peak": FP32_PEAK_TFLOPS,
+        "roofline": {"bound": "valu", "achieved": round(achieved_tf, 2), "peak": FP32_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4),
                      "traffic": traffic,
-                     "kernel": "cost_mfma_kernel (cost_tile 7)", "kernel_avg_ms": round(cost_ms, 4),
-                     "alg_flops_per_launch": alg_flops, "alg_bytes_per_launch": alg_bytes,
-                     "hbm_GBs_alg": round(alg_bytes / (cost_ms * 1e-3) / 1e9, 1) if cost_ms > 0 else 0.0,
+                     "kernel": "cost_mfma_kernel", "kernel_avg_ms": round(cost_ms, 4),
+                     "alg_flops_per_launch": alg_flops, "exec_flops_per_launch": exec_flops,
+                     "frac_executed_taps": round(exec_tf / FP32_PEAK_TFLOPS, 4),
+                     "alg_bytes_per_launch": alg_bytes, "hbm_GBs_alg": round(hbm_gbs, 1),
+                     "hbm_frac": round(hbm_gbs / HBM_PEAK_GBS, 4),
                      "note": "fp32-accurate stencil: vertical taps on the matrix cores as split-f16 "
                              "products (hi*hi+hi*lo+lo*hi, fp32 accumulate), horizontal taps, Lab and dE on "
-                             "FP32 VALU; achieved = the algorithm's fp32 flops / kernel time; "
-                             "bound mfma = the compute roof: peak = the dense FP32 MFMA peak for this f32 path, 157.3 TFLOP/s, which equals the FP32 vector peak on gfx950; limiter = the unit that saturates first in the PMC counters (VALU issue, with LDS close behind, DESIGN.md section 6); "
-                             "traffic = HBM bytes/launch from the committed rocprofv3 FETCH_SIZE(x2)+WRITE_SIZE "
-                             "passes (profiles/r01_hbm_traffic.json) when their config matches; kernel_avg_ms: HIP "
-                             "events carried by the launches on the context stream over a second pass of the same "
-                             "steps, right after the timed one (events idle the GPU ~5-10 us each, so the timed pass "
-                             "has none)"},
+                             "FP32 VALU.  bound valu: the compute roof is the FP32 vector peak, 157.3 TFLOP/s "
+                             "(the f32 MFMA peak is the same number on gfx950); achieved = the nominal 628 "
+                             "flop/px-eval of the reference's stencil + Lab/dE over the kernel time; "
+                             "frac_executed_taps = the 484 flop/px-eval the kernel executes (trimmed narrow "
+                             "filters); hbm_frac = the kernel's algorithmic bytes (LabRef 12 B + P index bytes "
+                             "per pixel) over its time against 8 TB/s; traffic = HBM bytes/launch from the "
+                             "committed rocprofv3 FETCH_SIZE(x2)+WRITE_SIZE passes when their config matches; "
+                             "kernel_avg_ms: HIP events carried by the launches on the context stream over a "
+                             "second pass of the same steps, right after the timed one (events idle the GPU "
+                             "~5-10 us each, so the timed pass has none)"},
         "metric_hbm_roofline_frac": round(value / eval_roof_mpx, 4),
         "kernel_avg_ms": {k: round(v[0], 4) for k, v in prof.items()},
         "best_error": berr.value,
     }
+    if search_line is not None:
+        out["full_search_c3"] = search_line
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)
     m.close()

@@ -12,6 +12,15 @@ package plugins.dbrasseur.hybridquantization;
  * so HQ, SP and SWASA compile unchanged against it.  The simulated-annealing
  * policy stays in Java (SWASA, with icy.util.Random as in the reference); only
  * the per-population candidate cost (IM:620-727) runs natively.
+ *
+ * Without libhq_jni or a GPU the class behaves like the reference without
+ * OpenCL (IM:79-92): the constructor prints a warning, updateOpenCLFilters only
+ * stores the packed filters, RGBtoXYZ takes the reference's Java path
+ * (IM:139-149), XYZtoScielab / findBestQuantization / quantize return zero
+ * arrays (IM:369, IM:590, IM:797).  computeError needs the GPU (the reference
+ * has no fallback there either, IM:858-894).
+ *
+ * This file has not been compiled: the build image has no JDK (INTEGRATION.md).
  */
 public class ImageManipulation {
     public enum deltaETypes {CIE76, CIE94, CIEDE2000}
@@ -53,32 +62,48 @@ public class ImageManipulation {
     }
 
     public float[] RGBtoXYZ(float[] R, float[] G, float[] B) {
-        require();
         float[] out = new float[4 * R.length];
-        nRGBtoXYZ(ctx, R, G, B, out);
+        if (openCLAvailable) {
+            nRGBtoXYZ(ctx, R, G, B, out);
+            return out;
+        }
+        for (int i = 0; i < R.length; i++) { // IM:139-149 Java mode
+            float[] xyz = ScielabProcessor.sRGBtoXYZ(new float[]{R[i], G[i], B[i]});
+            int off = i << 2;
+            out[off] = xyz[0];
+            out[off + 1] = xyz[1];
+            out[off + 2] = xyz[2];
+            out[off + 3] = 0.0f;
+        }
         return out;
     }
 
     public float[] XYZtoScielab(float[] XYZ, float[][][] filters, float[] absfilters, int w, float[] illuminant) {
-        require();
-        if (!filtersReady) updateOpenCLFilters(filters, absfilters);
         float[] lab = new float[XYZ.length];
+        if (!openCLAvailable) return lab; // IM:369
+        if (!filtersReady) updateOpenCLFilters(filters, absfilters);
         nXYZtoScielab(ctx, XYZ, w, illuminant, lab);
         return lab;
     }
 
-    /** Packs Ofilters[3][][] into k1/k2 (float4 taps) and k3/|k3| like IM:800-841. */
+    private int taps;
+    private float[] k1, k2, k3, absk3;
+
+    /** Packs Ofilters[3][][] into k1/k2 (float4 taps) and k3/|k3| like IM:800-841;
+     *  uploads them when the GPU is there (SP:180 calls this unconditionally). */
     public void updateOpenCLFilters(float[][][] filters, float[] absfilters) {
-        require();
-        int taps = filters[0][0].length;
-        float[] k1 = new float[4 * taps], k2 = new float[4 * taps];
+        taps = filters[0][0].length;
+        k1 = new float[4 * taps];
+        k2 = new float[4 * taps];
         for (int t = 0; t < taps; t++) {
             for (int c = 0; c < 3; c++) {
                 k1[4 * t + c] = filters[c][0][t];
                 k2[4 * t + c] = filters[c][1][t];
             }
         }
-        nSetFilters(ctx, taps, k1, k2, filters[0][2].clone(), absfilters.clone());
+        k3 = filters[0][2].clone();
+        absk3 = absfilters.clone();
+        if (openCLAvailable) nSetFilters(ctx, taps, k1, k2, k3, absk3);
         filtersReady = true;
     }
 

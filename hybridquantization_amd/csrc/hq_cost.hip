@@ -1,0 +1,591 @@
+// hq_cost.hip -- the S-CIELAB stencil cost of a population (CL:234-306,
+// vertical pass first), Opp->Lab (CL:124-145) and dE (CL:201-226) against the
+// precomputed LabRef, one fp64 partial per (tile, palette); plus the generic
+// two-pass path (any half-width) that cross-checks it.
+#include "hq_device.h"
+#include "hq_launch.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+namespace hq {
+
+// ----------------------------------------------------------------------------
+// Fast path (HALF = 10, the 21-tap filters of the default viewing set): a 1-D
+// grid of (output tile, palette) work items.  One workgroup = one TW x TH output
+// tile; its region = (TH + 2*HALF) rows x RW columns of palette indices.
+// Vertical pass first on all RW region columns (separable filters commute),
+// then the horizontal pass on the TW output columns, Opp->Lab, dE, fp64 partial.
+// ----------------------------------------------------------------------------
+// Tile geometry of the fast path: RW = 128 region columns, TW = 108 output
+// columns, TH = 8 output rows.
+constexpr int kFastHalf = 10, kFastRW = 128, kFastTH = 8;
+constexpr int kFastTW = kFastRW - 2 * kFastHalf;
+
+template <int HALF>
+struct CostTaps {
+    float v[kNumFilt][2 * HALF + 1];
+    float h[kNumFilt][2 * HALF + 1];
+};
+
+// Taps are read through a constant-address-space pointer into device memory
+// (uniform s_load per filter; build_fast_taps holds both scalings).
+template <int HALF>
+using TapsPtr = const __attribute__((address_space(4))) CostTaps<HALF>*;
+
+// TRIM: the narrow k1.x / k1.y / k1.z filters (f = 0, 3, 5) run over their
+// significant-tap windows kTrimLo..kTrimHi only (|taps| outside are below 1e-9
+// of the filter's peak for the default filter set; see trim_window_ok()).
+// Per-filter loops keep one filter's 21 taps live in SGPRs (interleaving a
+// channel's filters needs 63 and spills to VGPR lanes).
+constexpr int kTrimLo[3] = {7, 6, 5}, kTrimHi[3] = {13, 14, 15};
+
+// ---- vertical pass on the matrix cores --------------------------------------
+// The vertical pass of a filter over a 16-column block is a banded-Toeplitz
+// product with the block's TH + 2*HALF gathered input rows: one
+// v_mfma_f32_16x16x32_f16 K step (rows past the region zero-weighted).  fp32
+// accuracy from f16 operands: x = hi + lo (both f16, x scaled by 2^14 so lo
+// stays normal down to |x| ~ 1e-5) and the products hi.hi + hi.lo + lo.hi (each
+// exact in the f32 accumulator; the dropped lo.lo is ~2^-22 relative).  Taps
+// are split the same way on the host, scaled by 2^16
+// (build_vpass_f16_stack_fragments); the 2^30 total scale is folded into the
+// horizontal taps, exactly (a power of two).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr float kVDataScale = 16384.0f;                   // 2^14
+constexpr float kVTapScale = 65536.0f;                    // 2^16
+constexpr float kVOutScale = 1.0f / (16384.0f * 65536.0f);  // 2^-30
+
+// (hi, lo) f16 split of x * 2^14 in one dword, hi in bits 0-15.
+__device__ __forceinline__ uint32_t split_f16(float x) {
+    const float xs = x * kVDataScale;
+    const _Float16 hi = (_Float16)xs;
+    const _Float16 lo = (_Float16)(xs - (float)hi);
+    return (uint32_t)__builtin_bit_cast(uint16_t, hi) |
+           ((uint32_t)__builtin_bit_cast(uint16_t, lo) << 16);
+}
+
+// One work item of the cost pass: palette p over output tile `tile`.
+struct TileItem {
+    int p, tile, x0, y0;
+};
+
+template <int TW, int TH>
+__device__ __forceinline__ TileItem tile_item(const CostArgs& a, int w, int P) {
+    TileItem t;
+    t.p = w % P;
+    t.tile = w / P;
+    t.x0 = (t.tile % a.tiles_x) * TW;
+    t.y0 = a.g.r0 + (t.tile / a.tiles_x) * TH;
+    return t;
+}
+
+// The global loads that fill one item's LDS (index rows of its region, its
+// palette's opponent entry), held in registers between issue and commit.
+// Every load is issued before the first wait: vmcnt retires in order, so a
+// load -> wait -> store loop pays one memory round trip per trip (4 for the
+// interior index rows, 14 for the byte gathers of edge tiles).
+template <int HALF, int RW, int TH>
+struct TileFill {
+    static constexpr int TW = RW - 2 * HALF, RH = TH + 2 * HALF, DW = RW / 4;
+    static constexpr int NFD = (RH * DW + 255) / 256, NFB = (RH * RW + 255) / 256;
+    static_assert((DW & (DW - 1)) == 0, "dword columns per row: a power of two");
+    uint32_t lo[NFD], hi[NFD];  // interior tiles: aligned dword pairs of the index rows
+    uint32_t roff[NFD];         // their rows' byte offsets (alignment for commit)
+    float4 ov;
+    TileItem t;
+    bool interior;
+
+    // Byte offset of region row i in the palette's index image (reflection at the
+    // image edges, clamped to the rows held on this device).
+    __device__ __forceinline__ static int row_base(const Geom& g, const TileItem& t, int i) {
+        int gy = reflect_clamp(t.y0 - HALF + i, g.H);
+        gy = min(max(gy, g.e0), g.e1 - 1);
+        return (gy - g.e0) * g.W + (t.x0 - HALF);
+    }
+
+    // Issue the loads; interior tiles only (edge tiles -- the image's first and
+    // last tile columns -- gather bytes with reflection at commit time).  Tiles
+    // whose halo rows need neither reflection nor clamping (all but the image's
+    // and the shard's first and last tile rows) take row offsets from one
+    // multiply-add.  Loads are unconditional (rows clamped into the region) and
+    // use 32-bit unsigned offsets from the palette's base (saddr form); the host
+    // keeps a shard's index image below 2^31 bytes.
+    __device__ __forceinline__ void issue(const CostArgs& a, const TileItem& ti, int tid) {
+        static_assert(kMaxK == 256, "one opponent-table entry per thread");
+        const Geom& g = a.g;
+        t = ti;
+        const uint8_t* idx = a.idx + (int64_t)t.p * g.idx_pitch;
+        ov = tid < a.K ? a.opp[(int64_t)t.p * kMaxK + tid] : make_float4(0.f, 0.f, 0.f, 0.f);
+        interior = t.x0 - HALF >= 0 && t.x0 + TW + HALF <= g.W;
+        if (interior) {
+            const int ytop = t.y0 - HALF;
+            const bool vfast = ytop >= 0 && ytop >= g.e0 && ytop + RH <= g.H && ytop + RH <= g.e1;
+            const int ubase = (ytop - g.e0) * g.W + (t.x0 - HALF);
+#pragma unroll
+            for (int q = 0; q < NFD; ++q) {
+                const int e = min(tid + 256 * q, RH * DW - 1);
+                const int i = e / DW;
+                roff[q] = (uint32_t)(vfast ? ubase + i * g.W : row_base(g, t, i));
+                const uint32_t* src = reinterpret_cast<const uint32_t*>(
+                    idx + ((roff[q] & ~3u) + 4u * (uint32_t)(e % DW)));
+                lo[q] = src[0];
+                hi[q] = src[1];
+            }
+        }
+    }
+
+    // index rows into s_idx (row pitch IDXP bytes); the first write waits for the loads
+    template <int IDXP>
+    __device__ __forceinline__ void commit_idx(const CostArgs& a, uint8_t* s_idx, int tid) const {
+        const Geom& g = a.g;
+        if (interior) {
+#pragma unroll
+            for (int q = 0; q < NFD; ++q) {
+                const int e = tid + 256 * q;
+                if (e < RH * DW)
+                    reinterpret_cast<uint32_t*>(s_idx)[(e / DW) * (IDXP / 4) + e % DW] =
+                        __builtin_amdgcn_alignbyte(hi[q], lo[q], roff[q] & 3u);
+            }
+        } else {
+            const uint8_t* idx = a.idx + (int64_t)t.p * g.idx_pitch;
+            uint32_t b[NFB];
+#pragma unroll
+            for (int q = 0; q < NFB; ++q) {  // all loads first: one round trip
+                const int e = min(tid + 256 * q, RH * RW - 1);
+                const int i = e / RW, j = e % RW;
+                int gy = reflect_clamp(t.y0 - HALF + i, g.H);
+                gy = min(max(gy, g.e0), g.e1 - 1);
+                const int gx = reflect_clamp(t.x0 - HALF + j, g.W);
+                b[q] = idx[(uint32_t)((gy - g.e0) * g.W + gx)];
+            }
+#pragma unroll
+            for (int q = 0; q < NFB; ++q) {
+                const int e = tid + 256 * q;
+                if (e < RH * RW) s_idx[(e / RW) * IDXP + e % RW] = (uint8_t)b[q];
+            }
+        }
+    }
+};
+
+// Horizontal pass on row pairs: s_v holds float2 (row 2m, row 2m+1) per column,
+// so v_pk_fma_f32 runs across a row pair and every tap reads a naturally
+// aligned register pair (a row layout's odd taps needed register-pair shuffles,
+// ~29% of the pass's VALU instructions).  HR output columns per item.
+template <int HALF, int TH, int RW, int HR, int TLO = 0, int THI = 2 * HALF>
+__device__ __forceinline__ void hpass_pair_filters(const f32x4* src, TapsPtr<HALF> taps, int f0,
+                                                   int f1, f32x2 (&acc)[HR], int fslot = 0) {
+    constexpr int NIN = HR + 2 * HALF;  // window columns (float2 each)
+    constexpr int NQ = (NIN + 1) / 2;   // ds_read_b128, two columns each
+#pragma unroll 1
+    for (int f = f0; f < f1; ++f) {
+        const f32x4* row = src + (f - fslot) * (TH / 2) * RW / 2;
+        f32x4 v[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) v[q] = row[q];
+        f32x2 in[2 * NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            in[2 * q] = v[q].xy;
+            in[2 * q + 1] = v[q].zw;
+        }
+#pragma unroll
+        for (int t = TLO; t <= THI; ++t) {
+            const float k = taps->h[f][t];
+            const f32x2 kk = {k, k};
+#pragma unroll
+            for (int xo = 0; xo < HR; ++xo) acc[xo] = __builtin_elementwise_fma(in[xo + t], kk, acc[xo]);
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------
+// cost_mfma: 8-row tiles in two channel groups -- channel 0's three filters (V
+// then H), then channels 1-2's four -- so s_v holds at most four filter planes
+// (23 KiB of LDS, 6 workgroups per CU).  Both vertical passes on the matrix
+// cores in split f16: per 16-column block and pair of filters
+// of one channel, one v_mfma_f32_16x16x32_f16 K-step covers the 28 region rows
+// (+4 zero-weight rows) as hi.hi + hi.lo + lo.hi (each product exact in the
+// fp32 accumulator; lo.lo ~2^-22 relative is dropped).  A = the stacked
+// Toeplitz taps (rows = filter pair x 8 output rows, x 2^16, split on the host:
+// build_vpass_f16_stack_fragments), B = the gathered opponent values (x 2^14),
+// read from per-channel (hi, lo) f16 dword tables that the prologue splits once
+// per tile, so the gathers need no conversion (one LDS read per value).  D (x 2^30, folded exactly into the
+// horizontal taps) holds 4 consecutive output rows of one filter and column per
+// lane: two row-pair stores.  Stacks (f0, f1), (f2, -), (f3, f4), (f5, f6); wave
+// w takes region columns 32w .. +31: 12 MFMAs per group and wave.
+// (An exact-fp32 version on v_mfma_f32_16x16x4_f32, 56 MFMAs per wave, was 9%
+// slower than the VALU pass: fp32 MFMA runs at the fp32 vector rate.)
+// ----------------------------------------------------------------------------
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+// D of one 16x16 stack block -> s_v row pairs: lane (c = l & 15, q = l >> 4)
+// holds rows 4(q & 1) .. +3 of the stack's filter q >> 1 at column c.
+__device__ __forceinline__ void store_vstack(float* s_v, const f32x4v& d, int plane_a, int plane_b,
+                                             int lk, int col) {
+    constexpr int RW = 128, PAIRS = 4;
+    const int plane = lk < 2 ? plane_a : plane_b;
+    if (plane < 0) return;
+    const int p0 = 2 * (lk & 1);
+    f32x2* v = reinterpret_cast<f32x2*>(s_v);
+    v[(plane * PAIRS + p0) * RW + col] = f32x2{d[0], d[1]};
+    v[(plane * PAIRS + p0 + 1) * RW + col] = f32x2{d[2], d[3]};
+}
+
+// B fragments of one 16-column block: region rows 8q .. 8q+7 (q = lane >> 4) of
+// column `col`.  Table entries hold (hi, lo) f16 of a channel in one dword
+// (split_f16), so one LDS read per value; v_perm packs the halves.
+__device__ __forceinline__ void pack_b(const uint32_t (&w)[8], f16x8& bh, f16x8& bl) {
+    u32x4 h, l;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        h[m] = __builtin_amdgcn_perm(w[2 * m + 1], w[2 * m], 0x05040100u);  // hi halves
+        l[m] = __builtin_amdgcn_perm(w[2 * m + 1], w[2 * m], 0x07060302u);  // lo halves
+    }
+    bh = __builtin_bit_cast(f16x8, h);
+    bl = __builtin_bit_cast(f16x8, l);
+}
+
+__device__ __forceinline__ f32x4v mfma3(const f16x8& ah, const f16x8& al, const f16x8& bh,
+                                        const f16x8& bl) {
+    f32x4v d = {0.f, 0.f, 0.f, 0.f};
+    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, d, 0, 0, 0);
+    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, d, 0, 0, 0);
+    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, d, 0, 0, 0);
+    return d;
+}
+
+template <int DE, bool TRIM>
+__global__ __launch_bounds__(256, 6) void cost_mfma_kernel(CostArgs a, int P_) {
+    constexpr int HALF = 10, RW = 128, TH = 8, HR = 2, T2 = 2 * HALF;
+    constexpr int TW = RW - 2 * HALF, RH = TH + 2 * HALF;
+    constexpr int NRUN = TW / HR, SLOTS = 64, NITEM = (TH / 2) * SLOTS;
+    constexpr int PLANE = (TH / 2) * RW / 2;  // f32x4 per filter plane (row pairs)
+    static_assert(NRUN <= SLOTS && NITEM <= 256 && RH <= 32, "tile");
+    __shared__ f32x4 s_vq[4 * PLANE];
+    __shared__ uint32_t s_ox[kMaxK];  // opponent x 2^14 as (hi, lo) f16 pairs: channel 0
+    __shared__ uint2 s_oyz[kMaxK];     // channels 1, 2
+    // 32 rows: the K = 32 step reads rows 28-31 too (zero taps; any finite index)
+    __shared__ __attribute__((aligned(16))) uint8_t s_idx[32 * RW];
+    __shared__ double s_red[4];
+    float* s_v = reinterpret_cast<float*>(s_vq);
+    const int tid = threadIdx.x;
+    const Geom& g = a.g;
+    const TileItem cur = tile_item<TW, TH>(a, xcd_remap(blockIdx.x, a.ntiles * P_), P_);
+    const TapsPtr<HALF> taps = (TapsPtr<HALF>)(uintptr_t)a.taps;  // H taps x 2^-30
+    const int lane = tid & 63, wv = tid >> 6, lc = lane & 15, lk = lane >> 4;
+    const uint4* frag = a.vfrag16 + (TRIM ? 4 * 2 * 64 : 0) + lane;  // [trim][stack][hi,lo][lane]
+
+    TileFill<HALF, RW, TH> fill;
+    fill.issue(a, cur, tid);
+    uint4 F0h = frag[(0 * 2 + 0) * 64], F0l = frag[(0 * 2 + 1) * 64];  // group 0 stacks
+    uint4 F1h = frag[(1 * 2 + 0) * 64], F1l = frag[(1 * 2 + 1) * 64];
+    // every entry (zeros for tid >= K): the zero-weight rows 28-31 gather arbitrary
+    // indices, and 0 x NaN would be NaN
+    s_ox[tid] = split_f16(fill.ov.x);
+    s_oyz[tid] = make_uint2(split_f16(fill.ov.y), split_f16(fill.ov.z));
+    fill.template commit_idx<RW>(a, s_idx, tid);
+    const int m = tid / SLOTS, jr = tid % SLOTS;
+    const bool has_item = tid < NITEM && jr < NRUN;
+    const int gy0 = cur.y0 + 2 * m, gx0 = cur.x0 + HR * jr;
+    __syncthreads();
+
+    const int col0 = 32 * wv + lc;
+    const f32x4* hsrc = &s_vq[(m * RW + HR * jr) / 2];
+    f32x2 acc0[HR], acc1[HR], acc2[HR];
+#pragma unroll
+    for (int xo = 0; xo < HR; ++xo) acc0[xo] = acc1[xo] = acc2[xo] = f32x2{0.f, 0.f};
+
+    // ---- group 0: channel 0 -> planes 0-2 ----
+    {
+        const f16x8 a0h = __builtin_bit_cast(f16x8, F0h), a0l = __builtin_bit_cast(f16x8, F0l);
+        const f16x8 a1h = __builtin_bit_cast(f16x8, F1h), a1l = __builtin_bit_cast(f16x8, F1l);
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            uint32_t w[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) w[j] = s_ox[s_idx[(8 * lk + j) * RW + col0 + 16 * bb]];
+            f16x8 bh, bl;
+            pack_b(w, bh, bl);
+            store_vstack(s_v, mfma3(a0h, a0l, bh, bl), 0, 1, lk, col0 + 16 * bb);
+            store_vstack(s_v, mfma3(a1h, a1l, bh, bl), 2, -1, lk, col0 + 16 * bb);
+        }
+    }
+    const uint4 F2h = frag[(2 * 2 + 0) * 64], F2l = frag[(2 * 2 + 1) * 64];  // group 1 stacks,
+    const uint4 F3h = frag[(3 * 2 + 0) * 64], F3l = frag[(3 * 2 + 1) * 64];  // in flight during H
+    __syncthreads();
+    if (has_item) {
+        if constexpr (TRIM) {
+            hpass_pair_filters<HALF, TH, RW, HR, kTrimLo[0], kTrimHi[0]>(hsrc, taps, 0, 1, acc0);
+            hpass_pair_filters<HALF, TH, RW, HR, 0, T2>(hsrc, taps, 1, 3, acc0);
+        } else {
+            hpass_pair_filters<HALF, TH, RW, HR, 0, T2>(hsrc, taps, 0, 3, acc0);
+        }
+    }
+    __syncthreads();
+
+    // ---- group 1: channels 1, 2 -> planes 0-3 ----
+    {
+        const f16x8 a2h = __builtin_bit_cast(f16x8, F2h), a2l = __builtin_bit_cast(f16x8, F2l);
+        const f16x8 a3h = __builtin_bit_cast(f16x8, F3h), a3l = __builtin_bit_cast(f16x8, F3l);
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            uint32_t wy[8], wz[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint2 e = s_oyz[s_idx[(8 * lk + j) * RW + col0 + 16 * bb]];
+                wy[j] = e.x; wz[j] = e.y;
+            }
+            f16x8 bh, bl;
+            pack_b(wy, bh, bl);
+            store_vstack(s_v, mfma3(a2h, a2l, bh, bl), 0, 1, lk, col0 + 16 * bb);
+            pack_b(wz, bh, bl);
+            store_vstack(s_v, mfma3(a3h, a3l, bh, bl), 2, 3, lk, col0 + 16 * bb);
+        }
+    }
+    float labv[2][3][HR];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const bool ok = has_item && gy0 + r < g.r1 && gx0 < g.W;
+        const uint32_t off = ok ? (uint32_t)((gy0 + r - g.r0) * g.lab_pitch + gx0) : 0u;
+        const float* src3[3] = {a.labL, a.labA, a.labB};
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+            const float2 v = *reinterpret_cast<const float2*>(
+                reinterpret_cast<const char*>(src3[ch]) + (off << 2));  // 32-bit byte offset
+            labv[r][ch][0] = v.x; labv[r][ch][1] = v.y;
+        }
+    }
+    __syncthreads();
+
+    double sum = 0.0;
+    if (has_item) {
+        if constexpr (TRIM) {
+            hpass_pair_filters<HALF, TH, RW, HR, kTrimLo[1], kTrimHi[1]>(hsrc, taps, 3, 4, acc1, 3);
+            hpass_pair_filters<HALF, TH, RW, HR, 0, T2>(hsrc, taps, 4, 5, acc1, 3);
+            hpass_pair_filters<HALF, TH, RW, HR, kTrimLo[2], kTrimHi[2]>(hsrc, taps, 5, 6, acc2, 3);
+            hpass_pair_filters<HALF, TH, RW, HR, 0, T2>(hsrc, taps, 6, 7, acc2, 3);
+        } else {
+            hpass_pair_filters<HALF, TH, RW, HR, 0, T2>(hsrc, taps, 3, 5, acc1, 3);
+            hpass_pair_filters<HALF, TH, RW, HR, 0, T2>(hsrc, taps, 5, 7, acc2, 3);
+        }
+        float part = 0.f;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+#pragma unroll
+            for (int xo = 0; xo < HR; ++xo) {
+                const float3 l3 = opp2lab_fast(acc0[xo][r], acc1[xo][r], acc2[xo][r], a.m_lab);
+                const float e = delta_e<DE>(labv[r][0][xo], labv[r][1][xo], labv[r][2][xo], l3.x,
+                                            l3.y, l3.z);
+                part += (gy0 + r < g.r1 && gx0 + xo < g.W) ? e : 0.f;
+            }
+        }
+        sum = (double)part;
+    }
+    sum = wave_sum_to_lane63(sum);
+    if ((tid & 63) == 63) s_red[tid >> 6] = sum;
+    __syncthreads();
+    if (tid == 0)
+        a.partial[(int64_t)cur.p * a.ntiles + cur.tile] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+}
+
+// ----------------------------------------------------------------------------
+// Generic two-pass path (any half-width; option cost_variant 1): the reference's
+// computeScielabKernelsTemp (CL:234-272) and computeScielabKernelsEnd
+// (CL:274-306) restated per pixel through a [7][n_ext] fp32 scratch, one
+// palette per launch pair.  It cross-checks the fast path in the tests.
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void gen_hpass_kernel(GenArgs a) {
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (q >= a.g.n_ext) return;
+    const int ly = (int)(q / a.g.W), x = (int)(q % a.g.W);
+    const uint8_t* row = a.idx + (int64_t)ly * a.g.W;
+    float t1x = 0, t1y = 0, t1z = 0, t2x = 0, t2y = 0, t2z = 0, t3 = 0;
+    for (int i = -a.half, t = 0; i <= a.half; ++i, ++t) {  // CL:254-267
+        const float4 in = a.opp[row[reflect_only(x + i, a.g.W)]];
+        t1x = fmaf(in.x, a.k1[4 * t + 0], t1x);
+        t1y = fmaf(in.y, a.k1[4 * t + 1], t1y);
+        t1z = fmaf(in.z, a.k1[4 * t + 2], t1z);
+        t2x = fmaf(in.x, a.k2[4 * t + 0], t2x);
+        t2y = fmaf(in.y, a.k2[4 * t + 1], t2y);
+        t2z = fmaf(in.z, a.k2[4 * t + 2], t2z);
+        t3 = fmaf(in.x, a.k3[t], t3);
+    }
+    const int64_t n = a.g.n_ext;
+    a.t[q] = t1x; a.t[n + q] = t1y; a.t[2 * n + q] = t1z;
+    a.t[3 * n + q] = t2x; a.t[4 * n + q] = t2y; a.t[5 * n + q] = t2z;
+    a.t[6 * n + q] = t3;
+}
+
+template <int DE>
+__global__ __launch_bounds__(256) void gen_vpass_kernel(GenArgs a) {
+    __shared__ double s_red[4];
+    const int own_w = a.g.W;
+    const int64_t n_own = (int64_t)own_w * (a.g.r1 - a.g.r0);
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    double e = 0.0;
+    if (q < n_own) {
+        const int y = a.g.r0 + (int)(q / own_w), x = (int)(q % own_w);
+        const int64_t n = a.g.n_ext;
+        float ox = 0, oy = 0, oz = 0;
+        for (int i = -a.half, t = 0; i <= a.half; ++i, ++t) {  // CL:292-304
+            const int64_t s = (int64_t)(reflect_only(y + i, a.g.H) - a.g.e0) * a.g.W + x;
+            ox = fmaf(a.t[s], a.k1[4 * t + 0], fmaf(a.t[3 * n + s], a.k2[4 * t + 0], ox));
+            oy = fmaf(a.t[n + s], a.k1[4 * t + 1], fmaf(a.t[4 * n + s], a.k2[4 * t + 1], oy));
+            oz = fmaf(a.t[2 * n + s], a.k1[4 * t + 2], fmaf(a.t[5 * n + s], a.k2[4 * t + 2], oz));
+            ox = fmaf(a.t[6 * n + s], a.absk3[t], ox);
+        }
+        const float3 lab = opp2lab_fast(ox, oy, oz, a.m_lab);
+        const int64_t off = (int64_t)(y - a.g.r0) * a.g.lab_pitch + x;
+        e = (double)delta_e<DE>(a.labL[off], a.labA[off], a.labB[off], lab.x, lab.y, lab.z);
+    }
+    e = wave_sum(e);
+    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = e;
+    __syncthreads();
+    if (threadIdx.x == 0) a.partial[blockIdx.x] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+}
+
+// ----------------------------------------------------------------------------
+// Host side: tap tables, MFMA fragments, launchers
+// ----------------------------------------------------------------------------
+void opp2xyz_over_illum(const float inv_illum[3], float m[9]) {
+    static const float opp2xyz[9] = HQ_OPP2XYZ;
+    for (int i = 0; i < 9; ++i) m[i] = opp2xyz[i] * inv_illum[i / 3];
+}
+
+static void make_taps10(const float* k1, const float* k2, const float* k3, const float* absk3,
+                        CostTaps<10>& t) {
+    for (int i = 0; i < 21; ++i) {
+        // f: 0 k1.x, 1 k2.x, 2 k3 (|k3| vertical), 3 k1.y, 4 k2.y, 5 k1.z, 6 k2.z
+        t.v[0][i] = k1[4 * i + 0]; t.h[0][i] = k1[4 * i + 0];
+        t.v[1][i] = k2[4 * i + 0]; t.h[1][i] = k2[4 * i + 0];
+        t.v[2][i] = absk3[i];      t.h[2][i] = k3[i];
+        t.v[3][i] = k1[4 * i + 1]; t.h[3][i] = k1[4 * i + 1];
+        t.v[4][i] = k2[4 * i + 1]; t.h[4][i] = k2[4 * i + 1];
+        t.v[5][i] = k1[4 * i + 2]; t.h[5][i] = k1[4 * i + 2];
+        t.v[6][i] = k2[4 * i + 2]; t.h[6][i] = k2[4 * i + 2];
+    }
+}
+
+// f32 -> f16 bits, round to nearest even (host; finite inputs well inside the
+// f16 range after scaling, subnormal results included).
+static uint16_t host_f16(float x) {
+    uint32_t u;
+    std::memcpy(&u, &x, 4);
+    const uint32_t sign = (u >> 16) & 0x8000u;
+    const float ax = std::fabs(x);
+    if (ax < 5.9604645e-08f * 0.5f) return (uint16_t)sign;          // below half the smallest subnormal
+    if (ax < 6.1035156e-05f) {                                        // f16 subnormal: multiples of 2^-24
+        const float q = std::nearbyint(ax * 16777216.0f);             // round-half-even (default mode)
+        return (uint16_t)(sign | (uint32_t)q);
+    }
+    uint32_t a = u & 0x7fffffffu;
+    const uint32_t mant = a & 0x7fffffu;
+    int32_t e = (int32_t)(a >> 23) - 127 + 15;
+    uint32_t m = mant >> 13, rem = mant & 0x1fffu;
+    if (rem > 0x1000u || (rem == 0x1000u && (m & 1u))) {
+        if (++m == 0x400u) { m = 0; ++e; }
+    }
+    return (uint16_t)(sign | ((uint32_t)e << 10) | m);
+}
+
+static float host_f16_to_f32(uint16_t h) {
+    const uint32_t e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
+    const float v = e == 0 ? std::ldexp((float)m, -24) : std::ldexp((float)(m | 0x400u), (int)e - 25);
+    return (h & 0x8000u) ? -v : v;
+}
+
+// cost_tile 7: split-f16 A fragments of v_mfma_f32_16x16x32_f16 for the vertical
+// pass, [trim][stack][hi, lo][lane] x 8 halves (trim 0 = all 21 taps, 1 = the
+// narrow filters' significant windows).  Lane l holds A[i = l & 15][k = 8(l >> 4)
+// + j]: the tap (x 2^16) of filter stack[i >> 3] that multiplies region row k
+// into output row i & 7, i.e. tap d = k - (i & 7), zero outside [0, 20] (and
+// outside the window).
+size_t vpass_f16_stack_fragment_halves() { return 2 * 4 * 2 * 64 * 8; }
+
+void build_vpass_f16_stack_fragments(const float* k1, const float* k2, const float* k3,
+                                     const float* absk3, uint16_t* out) {
+    CostTaps<10> t;
+    make_taps10(k1, k2, k3, absk3, t);
+    const int stack[4][2] = {{0, 1}, {2, -1}, {3, 4}, {5, 6}};
+    for (int trim = 0; trim < 2; ++trim)
+        for (int st = 0; st < 4; ++st)
+            for (int l = 0; l < 64; ++l)
+                for (int j = 0; j < 8; ++j) {
+                    const int i = l & 15, k = 8 * (l >> 4) + j, r = i & 7, f = stack[st][i >> 3];
+                    const int d = k - r;
+                    float w = 0.f;
+                    if (f >= 0 && d >= 0 && d <= 20) {
+                        w = t.v[f][d];
+                        const int ch = f == 0 ? 0 : (f == 3 ? 1 : (f == 5 ? 2 : -1));
+                        if (trim && ch >= 0 && (d < kTrimLo[ch] || d > kTrimHi[ch])) w = 0.f;
+                    }
+                    w *= kVTapScale;
+                    const uint16_t hi = host_f16(w);
+                    const uint16_t lo = host_f16(w - host_f16_to_f32(hi));
+                    out[(((trim * 4 + st) * 2 + 0) * 64 + l) * 8 + j] = hi;
+                    out[(((trim * 4 + st) * 2 + 1) * 64 + l) * 8 + j] = lo;
+                }
+}
+
+bool trim_window_ok(const float* k1) {
+    const int ch[3] = {0, 1, 2};
+    for (int i = 0; i < 3; ++i) {
+        float peak = 0.f;
+        for (int t = 0; t < 21; ++t) peak = std::max(peak, std::fabs(k1[4 * t + ch[i]]));
+        for (int t = 0; t < 21; ++t)
+            if ((t < kTrimLo[i] || t > kTrimHi[i]) && std::fabs(k1[4 * t + ch[i]]) > 1e-9f * peak)
+                return false;
+    }
+    return true;
+}
+
+size_t fast_taps_bytes() { return 2 * sizeof(CostTaps<10>); }
+
+// [0] the taps as designed, [1] the same with the horizontal taps scaled by
+// 2^-30 (exact) for the matrix-core vertical pass, whose outputs carry 2^30.
+void build_fast_taps(const float* k1, const float* k2, const float* k3, const float* absk3,
+                     void* out) {
+    CostTaps<10> t[2];
+    make_taps10(k1, k2, k3, absk3, t[0]);
+    t[1] = t[0];
+    for (int f = 0; f < kNumFilt; ++f)
+        for (int i = 0; i < 2 * kFastHalf + 1; ++i) t[1].h[f][i] *= kVOutScale;
+    std::memcpy(out, t, sizeof t);
+}
+
+// a.taps = the two CostTaps<10> of build_fast_taps
+
+int fast_tile_rows() { return kFastTH; }
+
+void fast_tile_dims(int W, int own_rows, int* tiles_x, int* ntiles) {
+    *tiles_x = (W + kFastTW - 1) / kFastTW;
+    *ntiles = *tiles_x * ((own_rows + kFastTH - 1) / kFastTH);
+}
+
+// a.taps = the two CostTaps<10> of build_fast_taps; [1] carries the vertical
+// pass's 2^30 scale in its horizontal taps.
+hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, bool trim, hipStream_t s) {
+    CostArgs a = a0;
+    a.taps = static_cast<const char*>(a0.taps) + sizeof(CostTaps<10>);
+    const dim3 grid((unsigned)(a.ntiles * P));
+#define HQ_MFMA(DEV, TR) HQ_LAUNCH((cost_mfma_kernel<DEV, TR>), grid, dim3(256), 0, s, a, P)
+    if (de == 0) { if (trim) HQ_MFMA(0, true); else HQ_MFMA(0, false); }
+    else { if (trim) HQ_MFMA(1, true); else HQ_MFMA(1, false); }
+#undef HQ_MFMA
+    return hipGetLastError();
+}
+
+hipError_t launch_cost_generic(const GenArgs& a, int de, hipStream_t s) {
+    HQ_LAUNCH(gen_hpass_kernel, dim3(blocks_for(a.g.n_ext)), dim3(256), 0, s, a);
+    const int64_t n_own = (int64_t)a.g.W * (a.g.r1 - a.g.r0);
+    if (de == 0)
+        HQ_LAUNCH(gen_vpass_kernel<0>, dim3(blocks_for(n_own)), dim3(256), 0, s, a);
+    else
+        HQ_LAUNCH(gen_vpass_kernel<1>, dim3(blocks_for(n_own)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+
+}  // namespace hq

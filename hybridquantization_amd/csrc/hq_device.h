@@ -1,0 +1,194 @@
+// hq_device.h -- device helpers shared by the gfx950 kernels of libhq:
+// colour constants and conversions (CL:77-145), the frozen argmin distance
+// (CL:179-193), dE (CL:201-226), wave reductions and the XCD-aware grid
+// relabelling.  Included by every .hip translation unit of the library.
+#pragma once
+
+#include "hq_internal.h"
+
+#include <hip/hip_ext.h>
+
+#include <math.h>
+
+namespace hq {
+
+// ----------------------------------------------------------------------------
+// Colour constants (CL:77, CL:110, CL:118, CL:171; CL:120-123)
+// ----------------------------------------------------------------------------
+__constant__ float c_RGB2XYZ[9] = {0.4124564f, 0.3575761f, 0.1804375f, 0.2126729f, 0.7151522f,
+                                   0.0721750f, 0.0193339f, 0.1191920f, 0.9503041f};
+__constant__ float c_XYZ2Opp[9] = {0.2787336f,  0.7218031f, -0.1065520f, -0.4487736f, 0.2898056f,
+                                   -0.0771569f, 0.0859513f, -0.5899859f, 0.5011089f};
+#define HQ_OPP2XYZ {0.624045f, -1.87044f, -0.155304f, 1.36606f, 0.931563f, \
+                   0.433903f, 1.5013f,   1.41761f,  2.53307f}
+__constant__ float c_Opp2XYZ[9] = HQ_OPP2XYZ;
+__constant__ float c_RGB2Opp[9] = {0.266413f,  0.603167f, 0.00113333f, -0.124957f, 0.0375879f,
+                                   -0.133381f, -0.0803345f, -0.331467f, 0.449132f};
+
+#define LAB_DELTA3 (216.0f / 24389.0f)
+#define LAB_KAPPA (24389.0f / 27.0f)
+
+__device__ __forceinline__ float dot3(float x, float y, float z, const float* m) {
+    return (x * m[0] + y * m[1]) + z * m[2];
+}
+
+__device__ __forceinline__ float srgb_lin(float x) {  // CL:85-87, CL:194-196
+    return x <= 0.04045f ? x / 12.92f : powf((x + 0.055f) / 1.055f, 2.4f);
+}
+
+__device__ __forceinline__ float lab_f(float t) {  // CL:137
+    return t > LAB_DELTA3 ? cbrtf(t) : fmaf(LAB_KAPPA, t, 16.0f) * (1.0f / 116.0f);
+}
+
+// Branch-free f(t) of CL:137 for the hot path: cube root as exp2(log2(t)/3)
+// (v_log_f32 / v_exp_f32, about 3 ulp; no Newton step -- the cost tolerance is
+// 1e-4 relative and this moves the mean dE by ~1e-7), linear segment selected.
+__device__ __forceinline__ float lab_f_fast(float t) {
+    const float tc = fmaxf(t, LAB_DELTA3);  // cbrt branch only used for t > delta^3 > 0
+    const float y = __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(tc) * (1.0f / 3.0f));
+    const float lin = fmaf(LAB_KAPPA, t, 16.0f) * (1.0f / 116.0f);
+    return t > LAB_DELTA3 ? y : lin;
+}
+
+// CL:124-145 Opp2LAB for the hot path: m = Opp->XYZ with row r divided by the
+// illuminant's component r (opp2xyz_over_illum), so X/Xn etc. come out of the
+// 3x3 product directly.
+__device__ __forceinline__ float3 opp2lab_fast(float o0, float o1, float o2, const float* m) {
+    const float fx = lab_f_fast(dot3(o0, o1, o2, m + 0));
+    const float fy = lab_f_fast(dot3(o0, o1, o2, m + 3));
+    const float fz = lab_f_fast(dot3(o0, o1, o2, m + 6));
+    return make_float3(116.0f * fy - 16.0f, 500.0f * (fx - fy), 200.0f * (fy - fz));
+}
+
+// CL:124-145 with true division (setup paths: LabRef, quantize/error image).
+__device__ __forceinline__ float3 opp2lab_ref(float o0, float o1, float o2, const float* illum) {
+    const float X = dot3(o0, o1, o2, c_Opp2XYZ + 0);
+    const float Y = dot3(o0, o1, o2, c_Opp2XYZ + 3);
+    const float Z = dot3(o0, o1, o2, c_Opp2XYZ + 6);
+    const float fx = lab_f(X / illum[0]), fy = lab_f(Y / illum[1]), fz = lab_f(Z / illum[2]);
+    return make_float3(116.0f * fy - 16.0f, 500.0f * (fx - fy), 200.0f * (fy - fz));
+}
+
+// CL:201-231: dE76 (distance) or dE94.  Hardware square root (v_sqrt_f32, ~1 ulp):
+// HIP's sqrtf is a correctly rounded ~10-instruction sequence, and the
+// reference's OpenCL distance()/sqrt is itself only ulp-accurate; the cost is
+// compared at 1e-4 relative.  (The argmin keeps sqrtf: its ties are exact.)
+__device__ __forceinline__ float hw_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+
+template <int DE>
+__device__ __forceinline__ float delta_e(float L1, float a1, float b1, float L2, float a2,
+                                         float b2) {
+    if constexpr (DE == 0) {
+        const float dl = L1 - L2, da = a1 - a2, db = b1 - b2;
+        return hw_sqrt((dl * dl + da * da) + db * db);
+    } else {
+        const float dL = L1 - L2;
+        const float c1 = hw_sqrt(fmaf(a1, a1, b1 * b1));
+        const float dC = c1 - hw_sqrt(fmaf(a2, a2, b2 * b2));
+        const float da = a1 - a2, db = b1 - b2;
+        const float dH = hw_sqrt(fmaf(da, da, db * db) - dC * dC);
+        const float sc = 1.0f + 0.045f * c1, sh = 1.0f + 0.015f * c1;
+        return hw_sqrt(fmaf(dL, dL, fmaf(dC / sc, dC / sc, (dH / sh) * (dH / sh))));
+    }
+}
+
+// CL:256-263 reflection; clamped so garbage coordinates of partial tiles stay
+// in bounds (their results are masked).
+__device__ __forceinline__ int reflect_clamp(int j, int n) {
+    if (j < 0) j = -j - 1;
+    if (j >= n) j = 2 * n - j - 1;
+    return min(max(j, 0), n - 1);
+}
+
+__device__ __forceinline__ int reflect_only(int j, int n) {
+    if (j < 0) return -j - 1;
+    if (j >= n) return 2 * n - j - 1;
+    return j;
+}
+
+// Exact argmin distance ((dx*dx + dy*dy) + dz*dz), never fused: hipcc's default
+// -ffp-contract=fast would otherwise turn it into FMAs (and differently at
+// different call sites), breaking bit-exactness against the oracle.
+__device__ __forceinline__ float dist2(float r, float g, float b, float4 c) {
+#pragma clang fp contract(off)
+    const float dx = r - c.x, dy = g - c.y, dz = b - c.z;
+    return (dx * dx + dy * dy) + dz * dz;
+}
+
+// Ranking distance of the pruned argmin: the same sum with two FMAs.  All three
+// terms are non-negative, so it is within 3 ulp (< 2e-7 relative) of dist2;
+// argmin_from_entry re-resolves with dist2 + sqrtf whenever a runner-up lies
+// within 1e-6 relative, so the winner it returns is the reference's.
+__device__ __forceinline__ float dist2_rank(float r, float g, float b, float4 c) {
+    const float dx = r - c.x, dy = g - c.y, dz = b - c.z;
+    return __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// (byte j of w) << 4 in one instruction (SDWA operand select): a list entry's
+// candidate index straight to its 16-byte LDS offset.
+__device__ __forceinline__ uint32_t byte_x16(uint32_t w, int j) {
+    uint32_t r;
+    switch (j) {
+    case 0: asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(w)); break;
+    case 1: asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(w)); break;
+    case 2: asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(w)); break;
+    default: asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(w)); break;
+    }
+    return r;
+}
+
+// dist2_rank with the x/y differences in one v_pk_add_f32 ({c.x, c.y} sit in
+// consecutive registers after the ds_read_b128; rg = {r, g}).  c - p is the
+// exact negation of p - c, so the squares and the result are bit-identical.
+__device__ __forceinline__ float dist2_rank_pk(f32x2 rg, float b, float4 c) {
+    const f32x2 d = f32x2{c.x, c.y} - rg;
+    const float dz = c.z - b;
+    return __builtin_fmaf(dz, dz, __builtin_fmaf(d.y, d.y, d.x * d.x));
+}
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <typename V>
+__device__ __forceinline__ V wave_sum(V v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    return v;
+}
+
+// Sum of a double over the wave with DPP moves only (no LDS round trips: the
+// __shfl_down tree above is 12 dependent ds_bpermute for an f64).  Fixed order:
+// row_shr 1, 2, 4, 8 leave each 16-lane row's sum in its lane 15; row_bcast 15
+// and 31 fold the rows into lane 63, which alone holds the total.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, ROW_MASK, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, ROW_MASK, 0xf, true);
+    return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+__device__ __forceinline__ double wave_sum_to_lane63(double v) {
+    v += dpp_f64<0x111, 0xf>(v);  // row_shr:1
+    v += dpp_f64<0x112, 0xf>(v);  // row_shr:2
+    v += dpp_f64<0x114, 0xf>(v);  // row_shr:4
+    v += dpp_f64<0x118, 0xf>(v);  // row_shr:8
+    v += dpp_f64<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
+    v += dpp_f64<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3
+    return v;
+}
+
+// ----------------------------------------------------------------------------
+// XCD-aware relabelling of a 1-D grid of N workgroups.  Workgroups are placed
+// round-robin over the 8 XCDs (b % 8), so XCD x is given the contiguous work
+// range starting at x*(N/8) + min(x, N%8): neighbouring work items (the P
+// palettes of one tile or pixel block, adjacent tiles) then meet in one L2 and
+// LabRef / RGB reach HBM once instead of once per palette.  Bijective for any N;
+// placement only affects speed, never results.
+__device__ __forceinline__ int xcd_remap(int b, int N) {
+    const int q = N >> 3, r = N & 7, x = b & 7, s = b >> 3;
+    return x * q + min(x, r) + s;
+}
+
+}  // namespace hq

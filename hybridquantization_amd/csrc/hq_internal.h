@@ -13,7 +13,6 @@ constexpr int kNumFilt = 7;       // separable filter pairs of the S-CIELAB sten
 constexpr int kL1Cap = 31;        // level-1 candidate list capacity (32-B entry)
 constexpr int kL2Cap = 15;        // level-2 candidate list capacity (16-B entry)
 constexpr uint8_t kOverflow = 255;
-constexpr int kMaxBands = 16;    // row bands of the banded assign -> cost pipeline
 
 // The 7 separable (vertical, horizontal) filter pairs of the candidate stencil,
 // CL:234-306 restated: channel 0 = k1.x (x) k1.x + k2.x (x) k2.x + |k3| (x) k3,
@@ -105,21 +104,15 @@ struct AssignArgs {
     int64_t lvl2_gstride;   // bytes per group of 4 palettes (G2^3 * 64)
     int K;
     int G2;                 // 0 = exhaustive
-    int nblocks;            // blocks per palette in this launch
-    int mask_blocks;        // used_mask blocks per palette (all bands; = nblocks unbanded)
-    int mask_off;           // this launch's first used_mask block (band offset)
+    int nblocks;            // blocks per palette (= used_mask blocks per palette)
 };
 
 struct CostArgs {
     const uint8_t* idx;     // [P][idx_pitch]
     const float4* opp;      // [P][256]
-    const uint4* vfrag;     // cost_tile 3: [7][hi, lo][64 lanes] f16x8 B fragments of the
-                            // vertical Toeplitz taps (build_vpass_fragments)
-    const void* taps;       // CostTaps<10> in device memory (build_fast_taps)
-    const uint4* vfrag16;   // cost_tile 7, 8: [trim][4 stacks][hi, lo][64 lanes] f16x8 A
-                            // fragments of the vertical taps (build_vpass_f16_stack_fragments)
-    const uint4* hfrag16;   // cost_tile 8: [trim][7 filters][hi, lo][64 lanes] f16x8 A
-                            // fragments of the horizontal taps (build_hpass_f16_fragments)
+    const void* taps;       // CostTaps<10> x 2 in device memory (build_fast_taps)
+    const uint4* vfrag16;   // [trim][4 stacks][hi, lo][64 lanes] f16x8 A fragments of the
+                            // vertical taps (build_vpass_f16_stack_fragments)
     const float* labL;      // planar LabRef, owned rows, pitch lab_pitch
     const float* labA;
     const float* labB;
@@ -128,8 +121,6 @@ struct CostArgs {
     int K;
     int tiles_x;
     int ntiles;      // tiles of the shard (partial pitch per palette)
-    int tile0;       // first tile of this launch (row band; 0 unbanded)
-    int band_tiles;  // tiles in this launch (= ntiles unbanded)
     float m_lab[9];  // Opp->XYZ rows divided by the illuminant (CL:124-131), opp2xyz_over_illum()
 };
 

@@ -21,20 +21,13 @@ namespace hq {
 // launchers from hq_kernels.hip
 hipError_t launch_prep_palette(const PaletteArgs&, int P, hipStream_t);
 hipError_t launch_sa_step(const SaArgs&, hipStream_t);
-hipError_t launch_sa_grid(const SaArgs&, const GridArgs&, hipStream_t);
 void set_launch_events(hipEvent_t start, hipEvent_t stop);
 hipError_t launch_build_grid(const GridArgs&, int P, hipStream_t);
-hipError_t launch_assign(const AssignArgs&, int P, int rep, int group, int batch, hipStream_t);
-void fast_tile_dims(int W, int own_rows, int tile_cfg, int* tiles_x, int* ntiles);
-int fast_tile_rows(int tile_cfg);
+hipError_t launch_assign(const AssignArgs&, int P, hipStream_t);
+void fast_tile_dims(int W, int own_rows, int* tiles_x, int* ntiles);
 void opp2xyz_over_illum(const float inv_illum[3], float m[9]);
-void build_vpass_fragments(const float* k1, const float* k2, const float* k3,
-                           const float* absk3, uint16_t* out);
-hipError_t launch_cost_fast(const CostArgs&, int P, int de, int tile_cfg, bool trim, hipStream_t);
+hipError_t launch_cost_fast(const CostArgs&, int P, int de, bool trim, hipStream_t);
 size_t vpass_f16_stack_fragment_halves();
-size_t hpass_f16_fragment_halves();
-void build_hpass_f16_fragments(const float* k1, const float* k2, const float* k3,
-                               const float* absk3, uint16_t* out);
 void build_vpass_f16_stack_fragments(const float* k1, const float* k2, const float* k3,
                                      const float* absk3, uint16_t* out);
 size_t fast_taps_bytes();
@@ -98,10 +91,8 @@ struct hq_ctx {
     int taps = 0, half = 0;
     std::vector<float> k1, k2, k3, absk3;
     DevBuf d_k1, d_k2, d_k3, d_absk3;
-    DevBuf d_vfrag;  // cost_tile 3: Toeplitz B fragments [7][2][64] x 16 B (21-tap filters)
-    DevBuf d_taps;   // fast path taps, build_fast_taps (21-tap filters)
-    DevBuf d_vfrag16;  // cost_tile 7, 8: split-f16 MFMA A fragments of the stacked vertical taps
-    DevBuf d_hfrag16;  // cost_tile 8: split-f16 MFMA A fragments of the horizontal taps
+    DevBuf d_taps;     // fast path taps, build_fast_taps (21-tap filters)
+    DevBuf d_vfrag16;  // split-f16 MFMA A fragments of the stacked vertical taps
 
     // image
     bool have_image = false;
@@ -123,23 +114,9 @@ struct hq_ctx {
     int G2 = 32;           // argmin grid resolution (0 = exhaustive)
     int cost_variant = 0;  // 0 tiled (default), 1 generic two-pass
     int assign_blocks_per_cu = 8;
-    int assign_rep = 1;    // palette replication in the assign kernel's LDS
-    int assign_group = 4;  // palettes per pixel pass in the assign kernel (1, 2, 4)
-    int assign_batch = 3;  // group 4: 3 = pipelined (assign_pipe_kernel), 1/2 = batched;
-                           // group 1: 4/8 = batched, 0 = one-pixel prefetch
-    int tile_cfg = 7;      // cost tile: 0 = 16 rows, 1 = 8 rows + split V pass, 2 = 8 rows,
-                           // 3 = 8 rows + V pass on the matrix cores, 4 = 8 rows + row-pair
-                           // H pass (2 columns per item), 5 = row-pair H (4 columns),
-                           // 6 = row-pair in two channel groups (6 workgroups per CU),
-                           // 7 = 6 with the vertical passes on the matrix cores (split f16; default),
-                           // 8 = both passes on the matrix cores (96-column tiles)
-    int sa_fuse_grid = 0;  // device-resident search: SA step and candidate grid in one kernel
     int shard_solo = 0;    // experiment: a sharded search without a communicator (per-rank timing)
-                           // (sa_grid_kernel; 32.6 us against 12.6 + 13.5 us unfused: default off)
     int sa_device = 1;     // hq_search_*: 1 = SWASA iterations resident on the device (no host
                            // round trip per iteration), 0 = host-driven (one eval call each)
-    int bands = 0;         // row bands of the assign -> cost pipeline (0/1 = one pass, serial)
-    int band_cpb = 2;      // banded assign: pixel chunks per block (blocks = chunks / cpb)
     int trim = 1;          // skip taps < 1e-9 of the peak of the narrow k1 filters
     bool trim_ok = false;  // set by hq_set_filters (default 21-tap filter set)
 
@@ -152,23 +129,6 @@ struct hq_ctx {
     ProfSlot prof_assign, prof_cost, prof_grid, prof_finalize;
     hipEvent_t ev[8] = {};  // profiling: start/stop of grid, assign, cost, finalize
     int num_cu = 256;
-
-    // banded pipeline: assign of band j+1 (stream2) runs beside cost of band j (stream)
-    hipStream_t stream2 = nullptr;
-    hipEvent_t bev[kMaxBands + 1] = {};     // no timing: band j's indices written / grid ready
-    hipEvent_t pev[2 * kMaxBands + 2] = {};  // timing (profiling): per-band cost spans
-};
-
-// Row bands of the assign -> cost pipeline.  Cost band j covers tile rows
-// [t0, t1) of the shard; its index rows reach half rows past them, so assign
-// band j covers the extended rows [end(j-1), end(j)) with end(j) = the last row
-// cost band j reads: cost band j depends on assign bands <= j only.
-struct BandPlan {
-    int n = 1;
-    int64_t q0[kMaxBands], q1[kMaxBands];  // pixel range (extended rows) of assign band j
-    int blocks[kMaxBands], moff[kMaxBands];  // assign blocks per palette, used-mask offset
-    int t0[kMaxBands], t1[kMaxBands];        // cost tile range
-    int mask_blocks = 0;
 };
 
 struct hq_search {
@@ -348,44 +308,16 @@ int check_geom_args(hq_ctx* c, int w, int h, int r0, int r1) {
     return HQ_OK;
 }
 
-BandPlan plan_bands(const hq_ctx* c) {
-    const Geom& g = c->g;
-    BandPlan b;
-    int tiles_x, ntiles;
-    fast_tile_dims(g.W, g.r1 - g.r0, c->tile_cfg, &tiles_x, &ntiles);
-    const int trows = ntiles / tiles_x, th = fast_tile_rows(c->tile_cfg);
-    const int nblocks = c->num_cu * c->assign_blocks_per_cu;
-    const bool fast = c->cost_variant != 1 && c->half == 10;
-    b.n = fast ? std::max(1, std::min({c->bands, kMaxBands, trows})) : 1;
-    const int64_t chunk = 256 * 8;  // assign_pipe_kernel: 256 threads x PPT pixels
-    if (b.n == 1) {
-        // no more workgroups than pixel chunks: idle workgroups still fill LDS, and
-        // after the XCD relabelling they would all sit on the last XCDs (a 512-row
-        // shard ran assign on half the chip: 0.071 vs 0.053 ms)
-        // (evening out the chunks per workgroup instead -- 1064 workgroups of 2 for
-        // 2128 chunks -- was slower than 2048 with 80 of them taking a second chunk)
-        b.q0[0] = 0; b.q1[0] = g.n_ext;
-        b.blocks[0] = (int)std::max<int64_t>(1, std::min<int64_t>(nblocks, (g.n_ext + chunk - 1) / chunk));
-        b.moff[0] = 0;
-        b.t0[0] = 0; b.t1[0] = ntiles;
-        b.mask_blocks = b.blocks[0];
-        return b;
-    }
-    int row = g.e0;
-    for (int j = 0; j < b.n; ++j) {
-        const int tr0 = (int)((int64_t)trows * j / b.n), tr1 = (int)((int64_t)trows * (j + 1) / b.n);
-        const int end = j + 1 == b.n ? g.e1 : std::min(g.e1, std::max(row, g.r0 + th * tr1 + c->half));
-        b.q0[j] = (int64_t)(row - g.e0) * g.W;
-        b.q1[j] = (int64_t)(end - g.e0) * g.W;
-        const int64_t chunks = (b.q1[j] - b.q0[j] + chunk - 1) / chunk;
-        b.blocks[j] = (int)std::min<int64_t>(nblocks, (chunks + c->band_cpb - 1) / c->band_cpb);
-        b.moff[j] = b.mask_blocks;
-        b.mask_blocks += b.blocks[j];
-        b.t0[j] = tr0 * tiles_x;
-        b.t1[j] = tr1 * tiles_x;
-        row = end;
-    }
-    return b;
+// Assign workgroups per palette group: assign_blocks_per_cu per CU, but no more
+// than pixel chunks (256 threads x 8 pixels): idle workgroups still fill LDS,
+// and after the XCD relabelling they would all sit on the last XCDs (a 512-row
+// shard ran assign on half the chip: 0.071 vs 0.053 ms).  (Evening out the
+// chunks per workgroup instead -- 1064 workgroups of 2 for 2128 chunks -- was
+// slower than 2048 with 80 of them taking a second chunk.)
+int assign_blocks(const hq_ctx* c) {
+    const int64_t chunk = 256 * 8;
+    const int64_t nblocks = (int64_t)c->num_cu * c->assign_blocks_per_cu;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(nblocks, (c->g.n_ext + chunk - 1) / chunk));
 }
 
 // Ensure population buffers for P palettes of K colours.
@@ -396,11 +328,11 @@ int ensure_population(hq_ctx* c, int P, int K) {
     const int64_t l1p = round_up((int64_t)G1 * G1 * G1 * 32, 256);
     const int64_t l2g = round_up((int64_t)G2 * G2 * G2 * 64, 256);  // per group of 4 palettes
     int tiles_x, ntiles;
-    fast_tile_dims(g.W, g.r1 - g.r0, c->tile_cfg, &tiles_x, &ntiles);
+    fast_tile_dims(g.W, g.r1 - g.r0, &tiles_x, &ntiles);
     const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
     const int64_t gen_blocks = (n_own + 255) / 256;
     const int64_t nparts = std::max<int64_t>(ntiles, gen_blocks);
-    const int nblocks = c->num_cu * c->assign_blocks_per_cu;
+    const int nblocks = assign_blocks(c);
     HIP_TRY(c, c->d_pal_in.ensure(sizeof(float4) * (size_t)P * K));
     HIP_TRY(c, c->d_pal.ensure(sizeof(float4) * (size_t)P * kMaxK));
     HIP_TRY(c, c->d_opp.ensure(sizeof(float4) * (size_t)P * kMaxK));
@@ -409,8 +341,7 @@ int ensure_population(hq_ctx* c, int P, int K) {
     HIP_TRY(c, c->d_lvl1.ensure((size_t)P * l1p));
     HIP_TRY(c, c->d_lvl2.ensure((size_t)((P + 3) / 4) * l2g));
     HIP_TRY(c, c->d_idx.ensure((size_t)P * g.idx_pitch));
-    const BandPlan bp = plan_bands(c);
-    HIP_TRY(c, c->d_used_mask.ensure(sizeof(uint32_t) * 8 * (size_t)P * std::max(nblocks, bp.mask_blocks)));
+    HIP_TRY(c, c->d_used_mask.ensure(sizeof(uint32_t) * 8 * (size_t)P * nblocks));
     HIP_TRY(c, c->d_partial.ensure(sizeof(double) * (size_t)P * nparts));
     HIP_TRY(c, c->d_out.ensure(sizeof(double) * (size_t)P * (1 + K)));
     return ensure_pinned(c, sizeof(float) * 4 * (size_t)P * K, sizeof(double) * (size_t)P * (1 + K));
@@ -433,7 +364,7 @@ PaletteArgs prep_args(hq_ctx* c, int K) {
 // d_pflags): grid, assign, cost, finalize into d_out (partial sums + used
 // flags), all-reduced if a comm is set.  ev (8 events, or null): start/stop of
 // the grid, assign, cost and finalize launches, carried by the launches
-// themselves (set_launch_events); banded cost launches use the context's pev.
+// themselves (set_launch_events).
 GridArgs grid_args(hq_ctx* c, int K) {
     const int G2 = c->G2 > 0 ? c->G2 : 4;
     const int G1 = G2 / 4;
@@ -442,127 +373,78 @@ GridArgs grid_args(hq_ctx* c, int K) {
                     round_up((int64_t)G1 * G1 * G1 * 32, 256), round_up((int64_t)G2 * G2 * G2 * 64, 256)};
 }
 
-// grid_built: the candidate grid already exists (sa_grid_kernel built it).
-int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, BandPlan& bp, bool grid_built = false) {
+int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev) {
     const Geom& g = c->g;
     hipStream_t s = c->stream;
     const GridArgs ga = grid_args(c, K);
-    const int64_t l1p = ga.lvl1_pitch, l2g = ga.lvl2_gstride;
-    const int nblocks = c->num_cu * c->assign_blocks_per_cu;
     auto timed = [&](int slot) {
         if (ev) set_launch_events(ev[2 * slot], ev[2 * slot + 1]);
     };
     auto untimed = [&]() { set_launch_events(nullptr, nullptr); };
-    if (c->G2 > 0 && !grid_built) {
+    if (c->G2 > 0) {
         timed(0);
         const hipError_t e = launch_build_grid(ga, P, s);
         untimed();
         HIP_TRY(c, e);
     }
-    bp = plan_bands(c);
-    AssignArgs aa{c->d_R.as<float>(), c->d_G.as<float>(), c->d_B.as<float>(), c->d_pal.as<float4>(),
-                  c->d_pflags.as<int>(), c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(),
-                  c->d_idx.as<uint8_t>(), c->d_used_mask.as<uint32_t>(), g.n_ext, g.idx_pitch,
-                  l1p, l2g, K, c->G2, bp.n > 1 ? nblocks : bp.blocks[0], bp.mask_blocks, 0};
-    int tiles_x, ntiles;
-    fast_tile_dims(g.W, g.r1 - g.r0, c->tile_cfg, &tiles_x, &ntiles);
+    const int nblocks = assign_blocks(c);
+    const AssignArgs aa{c->d_R.as<float>(), c->d_G.as<float>(), c->d_B.as<float>(), c->d_pal.as<float4>(),
+                        c->d_pflags.as<int>(), c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(),
+                        c->d_idx.as<uint8_t>(), c->d_used_mask.as<uint32_t>(), g.n_ext, g.idx_pitch,
+                        ga.lvl1_pitch, ga.lvl2_gstride, K, c->G2, nblocks};
+    timed(1);
+    hipError_t e = launch_assign(aa, P, s);
+    untimed();
+    HIP_TRY(c, e);
     const float inv[3] = {1.0f / c->illum[0], 1.0f / c->illum[1], 1.0f / c->illum[2]};
     int nparts;
-    const bool fast = c->cost_variant != 1 && c->half == 10;
-    CostArgs ca{};
-    if (fast) {
+    if (c->cost_variant != 1 && c->half == 10) {
+        CostArgs ca{};
         ca.idx = c->d_idx.as<uint8_t>();
         ca.opp = c->d_opp.as<float4>();
-        ca.vfrag = c->d_vfrag.as<uint4>();
+        ca.taps = c->d_taps.p;
         ca.vfrag16 = c->d_vfrag16.as<uint4>();
-        ca.hfrag16 = c->d_hfrag16.as<uint4>();
         ca.labL = c->d_labL.as<float>();
         ca.labA = c->d_labA.as<float>();
         ca.labB = c->d_labB.as<float>();
         ca.partial = c->d_partial.as<double>();
         ca.g = g;
         ca.K = K;
-        ca.tiles_x = tiles_x;
-        ca.ntiles = ntiles;
-        ca.tile0 = 0;
-        ca.band_tiles = ntiles;
+        fast_tile_dims(g.W, g.r1 - g.r0, &ca.tiles_x, &ca.ntiles);
         opp2xyz_over_illum(inv, ca.m_lab);
-        ca.taps = c->d_taps.p;
-    }
-    if (bp.n > 1) {
-        // Banded pipeline: assign bands run back to back on stream2; cost band j
-        // waits for assign band j (the last one its index rows need) and runs on
-        // `s` beside assign band j+1, so the latency-bound assign shares the CUs
-        // with the VALU/LDS-bound cost kernel instead of running alone.
-        hipStream_t s2 = c->stream2;
-        HIP_TRY(c, hipEventRecord(c->bev[kMaxBands], s));  // palettes + grid ready (no timing)
-        HIP_TRY(c, hipStreamWaitEvent(s2, c->bev[kMaxBands], 0));
-        for (int j = 0; j < bp.n; ++j) {
-            if (bp.blocks[j] > 0) {
-                AssignArgs ab = aa;
-                ab.R = aa.R + bp.q0[j];
-                ab.G = aa.G + bp.q0[j];
-                ab.B = aa.B + bp.q0[j];
-                ab.idx = aa.idx + bp.q0[j];
-                ab.n_ext = bp.q1[j] - bp.q0[j];
-                ab.nblocks = bp.blocks[j];
-                ab.mask_off = bp.moff[j];
-                HIP_TRY(c, launch_assign(ab, P, c->assign_rep, c->assign_group, c->assign_batch, s2));
-            }
-            HIP_TRY(c, hipEventRecord(c->bev[j], s2));
-        }
-        for (int j = 0; j < bp.n; ++j) {
-            HIP_TRY(c, hipStreamWaitEvent(s, c->bev[j], 0));
-            if (bp.t1[j] == bp.t0[j]) continue;
-            CostArgs cb = ca;
-            cb.tile0 = bp.t0[j];
-            cb.band_tiles = bp.t1[j] - bp.t0[j];
-            if (ev) set_launch_events(c->pev[2 * j], c->pev[2 * j + 1]);
-            const hipError_t e = launch_cost_fast(cb, P, c->de_type, c->tile_cfg, c->trim && c->trim_ok, s);
-            untimed();
-            HIP_TRY(c, e);
-        }
-        nparts = ntiles;
-    } else {
-        timed(1);
-        hipError_t e = launch_assign(aa, P, c->assign_rep, c->assign_group, c->assign_batch, s);
+        timed(2);
+        e = launch_cost_fast(ca, P, c->de_type, c->trim && c->trim_ok, s);
         untimed();
         HIP_TRY(c, e);
-        if (fast) {
-            timed(2);
-            e = launch_cost_fast(ca, P, c->de_type, c->tile_cfg, c->trim && c->trim_ok, s);
+        nparts = ca.ntiles;
+    } else {
+        HIP_TRY(c, c->d_gen_t.ensure(sizeof(float) * 7 * (size_t)g.n_ext));
+        const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
+        nparts = (int)((n_own + 255) / 256);
+        for (int p = 0; p < P; ++p) {
+            GenArgs gn{};
+            gn.idx = c->d_idx.as<uint8_t>() + (int64_t)p * g.idx_pitch;
+            gn.opp = c->d_opp.as<float4>() + (int64_t)p * kMaxK;
+            gn.k1 = c->d_k1.as<float>();
+            gn.k2 = c->d_k2.as<float>();
+            gn.k3 = c->d_k3.as<float>();
+            gn.absk3 = c->d_absk3.as<float>();
+            gn.t = c->d_gen_t.as<float>();
+            gn.labL = c->d_labL.as<float>();
+            gn.labA = c->d_labA.as<float>();
+            gn.labB = c->d_labB.as<float>();
+            gn.partial = c->d_partial.as<double>() + (int64_t)p * nparts;
+            gn.g = g;
+            gn.half = c->half;
+            opp2xyz_over_illum(inv, gn.m_lab);
+            if (p == 0) timed(2);  // times the first palette's two launches
+            e = launch_cost_generic(gn, c->de_type, s);
             untimed();
             HIP_TRY(c, e);
-            nparts = ntiles;
-        } else {
-            HIP_TRY(c, c->d_gen_t.ensure(sizeof(float) * 7 * (size_t)g.n_ext));
-            const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
-            nparts = (int)((n_own + 255) / 256);
-            for (int p = 0; p < P; ++p) {
-                GenArgs ga{};
-                ga.idx = c->d_idx.as<uint8_t>() + (int64_t)p * g.idx_pitch;
-                ga.opp = c->d_opp.as<float4>() + (int64_t)p * kMaxK;
-                ga.k1 = c->d_k1.as<float>();
-                ga.k2 = c->d_k2.as<float>();
-                ga.k3 = c->d_k3.as<float>();
-                ga.absk3 = c->d_absk3.as<float>();
-                ga.t = c->d_gen_t.as<float>();
-                ga.labL = c->d_labL.as<float>();
-                ga.labA = c->d_labA.as<float>();
-                ga.labB = c->d_labB.as<float>();
-                ga.partial = c->d_partial.as<double>() + (int64_t)p * nparts;
-                ga.g = g;
-                ga.half = c->half;
-                opp2xyz_over_illum(inv, ga.m_lab);
-                if (p == 0) timed(2);  // times the first palette's two launches (its V pass)
-                e = launch_cost_generic(ga, c->de_type, s);
-                untimed();
-                HIP_TRY(c, e);
-            }
         }
     }
     FinalizeArgs fa{c->d_partial.as<double>(), c->d_used_mask.as<uint32_t>(), c->d_out.as<double>(),
-                    nparts, bp.mask_blocks, K};
+                    nparts, nblocks, K};
     timed(3);
     const hipError_t ef = launch_finalize(fa, P, s);
     untimed();
@@ -577,15 +459,10 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, BandPlan& bp, bo
 }
 
 // Add one evaluation's kernel times (its events have completed).
-void prof_accumulate(hq_ctx* c, const hipEvent_t* ev, const BandPlan& bp) {
+void prof_accumulate(hq_ctx* c, const hipEvent_t* ev) {
     if (c->G2 > 0) prof_add(c, c->prof_grid, ev[0], ev[1]);
-    if (bp.n > 1) {  // banded: per-band cost launches (assign overlaps them)
-        for (int j = 0; j < bp.n; ++j)
-            if (bp.t1[j] > bp.t0[j]) prof_add(c, c->prof_cost, c->pev[2 * j], c->pev[2 * j + 1]);
-    } else {
-        prof_add(c, c->prof_assign, ev[2], ev[3]);
-        prof_add(c, c->prof_cost, ev[4], ev[5]);
-    }
+    prof_add(c, c->prof_assign, ev[2], ev[3]);
+    prof_add(c, c->prof_cost, ev[4], ev[5]);
     prof_add(c, c->prof_finalize, ev[6], ev[7]);
 }
 
@@ -597,13 +474,12 @@ int enqueue_eval(hq_ctx* c, int P, int K) {
                               hipMemcpyHostToDevice, s));
     const hipEvent_t* ev = c->prof ? c->ev : nullptr;
     HIP_TRY(c, launch_prep_palette(prep_args(c, K), P, s));
-    BandPlan bp;
-    int rc = enqueue_core(c, P, K, ev, bp);
+    int rc = enqueue_core(c, P, K, ev);
     if (rc) return rc;
     HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out.p, sizeof(double) * (size_t)P * (1 + K),
                               hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
-    if (ev) prof_accumulate(c, ev, bp);
+    if (ev) prof_accumulate(c, ev);
     return HQ_OK;
 }
 
@@ -633,10 +509,7 @@ namespace {
 
 // One sa_step launch: accept the population in cand[cd] (if `accept`), then
 // generate the next candidates into cand[1 - cd] (if `generate`).
-// With generate and a candidate grid, one sa_grid_kernel launch also builds the
-// grid (*grid_built = true); ev (2 events, optional) times it.
-int enqueue_sa_step(hq_search* s, bool accept, bool init, bool generate, bool random, float amax,
-                    bool* grid_built = nullptr, const hipEvent_t* ev = nullptr) {
+int enqueue_sa_step(hq_search* s, bool accept, bool init, bool generate, bool random, float amax) {
     hq_ctx* c = s->ctx;
     SaArgs a{};
     a.out = c->d_out.as<double>();
@@ -665,12 +538,7 @@ int enqueue_sa_step(hq_search* s, bool accept, bool init, bool generate, bool ra
     a.generate = generate;
     a.random = random;
     a.convergence = s->prm.convergence;
-    const bool fused = generate && c->G2 > 0 && c->sa_fuse_grid;
-    if (ev) set_launch_events(ev[0], ev[1]);
-    const hipError_t e = fused ? launch_sa_grid(a, grid_args(c, s->K), c->stream) : launch_sa_step(a, c->stream);
-    set_launch_events(nullptr, nullptr);
-    HIP_TRY(c, e);
-    if (grid_built) *grid_built = fused;
+    HIP_TRY(c, launch_sa_step(a, c->stream));
     s->st = 1 - s->st;
     if (generate) s->cd = 1 - s->cd;
     return HQ_OK;
@@ -720,10 +588,8 @@ int device_search_create(hq_ctx* c, const hq_swasa_params* params, int K, uint64
     HIP_TRY(c, hipMemset(s->err[0].p, 0, sizeof(double) * P));
     s->st = s->cd = 0;
     // IM:385-493: random population (SW:40-52), its evaluation, argmin
-    bool built = false;
-    if ((rc = enqueue_sa_step(s, false, false, true, true, 0.f, &built))) return rc;
-    BandPlan bp;
-    if ((rc = enqueue_core(c, P, K, nullptr, bp, built))) return rc;
+    if ((rc = enqueue_sa_step(s, false, false, true, true, 0.f))) return rc;
+    if ((rc = enqueue_core(c, P, K, nullptr))) return rc;
     if ((rc = enqueue_sa_step(s, true, true, false, false, 0.f))) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     s->ite = 0;
@@ -734,26 +600,29 @@ int device_search_create(hq_ctx* c, const hq_swasa_params* params, int K, uint64
 int device_search_run(hq_search* s, int iterations, int* ran) {
     hq_ctx* c = s->ctx;
     int done = 0, rc;
+    // The context may have changed since hq_search_create or the last run (an
+    // option such as 'grid' or 'assign_blocks_per_cu', a new image): size its
+    // work buffers for the current geometry before enqueueing anything.
+    if (!c->have_image) return fail(c, HQ_ERR_STATE, "no image set (hq_set_image)");
+    if (c->de_type == HQ_DE_CIEDE2000)
+        return fail(c, HQ_ERR_UNSUPPORTED, "CIEDE2000 is unimplemented in the reference (CL:227-230)");
+    if ((rc = ensure_population(c, s->P, s->K))) return rc;
     const bool prof = c->prof;
     if (prof && (rc = ensure_events(s, (size_t)8 * iterations))) return rc;
-    std::vector<BandPlan> bps(prof ? iterations : 0);
     for (; done < iterations && s->ite < s->prm.imax; ++done) {
         const int ite = ++s->ite;
         s->pol->reduce_temperature_if_necessary(ite);                  // IM:507
         const float amax = s->pol->max_step_width(ite) / 256.0f;       // SW:91-101
         const hipEvent_t* ev = prof ? &s->pev[(size_t)8 * done] : nullptr;
         // accept the previous iteration's population (none at the first of a run)
-        bool built = false;
-        if ((rc = enqueue_sa_step(s, done > 0, false, true, false, amax, &built, ev))) return rc;
-        BandPlan bp;
-        if ((rc = enqueue_core(c, s->P, s->K, ev, bp, built))) return rc;
-        if (prof) bps[done] = bp;
+        if ((rc = enqueue_sa_step(s, done > 0, false, true, false, amax))) return rc;
+        if ((rc = enqueue_core(c, s->P, s->K, ev))) return rc;
         s->t_acc = s->pol->temperature();     // SW:54-57 at this iteration
         s->keep_acc = s->pol->keep_threshold(ite);
     }
     if (done > 0 && (rc = enqueue_sa_step(s, true, false, false, false, 0.f))) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    for (int i = 0; prof && i < done; ++i) prof_accumulate(c, &s->pev[(size_t)8 * i], bps[i]);
+    for (int i = 0; prof && i < done; ++i) prof_accumulate(c, &s->pev[(size_t)8 * i]);
     if (ran) *ran = done;
     return HQ_OK;
 }
@@ -807,12 +676,6 @@ int hq_create(int device, int delta_e_type, hq_ctx** out) {
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         c->num_cu = prop.multiProcessorCount;
     for (auto& e : c->ev) (void)hipEventCreate(&e);
-    for (auto& e : c->pev) (void)hipEventCreate(&e);
-    for (auto& e : c->bev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
-    if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
-        hq_destroy(c);
-        return HQ_ERR_DEVICE;
-    }
     *out = c;
     return HQ_OK;
 }
@@ -825,18 +688,13 @@ void hq_destroy(hq_ctx* c) {
     for (DevBuf* b : {&c->d_k1, &c->d_k2, &c->d_k3, &c->d_absk3, &c->d_R, &c->d_G, &c->d_B,
                       &c->d_labL, &c->d_labA, &c->d_labB, &c->d_pal_in, &c->d_pal, &c->d_opp,
                       &c->d_dup, &c->d_pflags, &c->d_lvl1, &c->d_lvl2, &c->d_idx,
-                      &c->d_used_mask, &c->d_partial, &c->d_out, &c->d_gen_t, &c->d_vfrag,
-                      &c->d_taps, &c->d_vfrag16, &c->d_hfrag16})
+                      &c->d_used_mask, &c->d_partial, &c->d_out, &c->d_gen_t, &c->d_taps,
+                      &c->d_vfrag16})
         b->release();
     if (c->h_pal) (void)hipHostFree(c->h_pal);
     if (c->h_out) (void)hipHostFree(c->h_out);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
-    for (auto& e : c->pev)
-        if (e) (void)hipEventDestroy(e);
-    for (auto& e : c->bev)
-        if (e) (void)hipEventDestroy(e);
-    if (c->stream2) (void)hipStreamSynchronize(c->stream2), (void)hipStreamDestroy(c->stream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -868,20 +726,10 @@ int hq_set_filters(hq_ctx* c, int taps, const float* k1, const float* k2, const 
     HIP_TRY(c, hipMemcpy(c->d_absk3.p, absk3, sizeof(float) * taps, hipMemcpyHostToDevice));
     c->trim_ok = taps == 21 && trim_window_ok(k1);
     if (taps == 21) {
-        std::vector<uint16_t> frag((size_t)kNumFilt * 2 * 64 * 8);
-        build_vpass_fragments(k1, k2, k3, absk3, frag.data());
-        HIP_TRY(c, c->d_vfrag.ensure(frag.size() * sizeof(uint16_t)));
-        HIP_TRY(c, hipMemcpy(c->d_vfrag.p, frag.data(), frag.size() * sizeof(uint16_t),
-                             hipMemcpyHostToDevice));
         std::vector<uint16_t> f16s(vpass_f16_stack_fragment_halves());
         build_vpass_f16_stack_fragments(k1, k2, k3, absk3, f16s.data());
         HIP_TRY(c, c->d_vfrag16.ensure(f16s.size() * sizeof(uint16_t)));
         HIP_TRY(c, hipMemcpy(c->d_vfrag16.p, f16s.data(), f16s.size() * sizeof(uint16_t),
-                             hipMemcpyHostToDevice));
-        std::vector<uint16_t> h16s(hpass_f16_fragment_halves());
-        build_hpass_f16_fragments(k1, k2, k3, absk3, h16s.data());
-        HIP_TRY(c, c->d_hfrag16.ensure(h16s.size() * sizeof(uint16_t)));
-        HIP_TRY(c, hipMemcpy(c->d_hfrag16.p, h16s.data(), h16s.size() * sizeof(uint16_t),
                              hipMemcpyHostToDevice));
         std::vector<char> tb(fast_taps_bytes());
         build_fast_taps(k1, k2, k3, absk3, tb.data());
@@ -1241,32 +1089,10 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
         c->cost_variant = value;
     } else if (!std::strcmp(name, "trim")) {
         c->trim = value != 0;
-    } else if (!std::strcmp(name, "cost_tile")) {
-        if (value < 0 || value > 11) return fail(c, HQ_ERR_ARG, "cost_tile in 0..11");
-        c->tile_cfg = value;
-    } else if (!std::strcmp(name, "assign_group")) {
-        if (value != 1 && value != 2 && value != 4) return fail(c, HQ_ERR_ARG, "assign_group in {1,2,4}");
-        c->assign_group = value;
-    } else if (!std::strcmp(name, "assign_batch")) {
-        if (value < 0 || value > 8 || value == 6 || value == 7 || (value == 5 && c->assign_group != 4))
-            return fail(c, HQ_ERR_ARG, "assign_batch in {0,1,2,3,4,8} (5: group 4)");
-        c->assign_batch = value;
-    } else if (!std::strcmp(name, "assign_rep")) {
-        if (value != 1 && value != 2 && value != 4 && value != 16)
-            return fail(c, HQ_ERR_ARG, "assign_rep in {1,2,4,16}");
-        c->assign_rep = value;
     } else if (!std::strcmp(name, "sa_device")) {
         c->sa_device = value != 0;
     } else if (!std::strcmp(name, "shard_solo")) {
         c->shard_solo = value != 0;
-    } else if (!std::strcmp(name, "sa_fuse_grid")) {
-        c->sa_fuse_grid = value != 0;
-    } else if (!std::strcmp(name, "bands")) {
-        if (value < 0 || value > kMaxBands) return fail(c, HQ_ERR_ARG, "bands in [0,%d]", kMaxBands);
-        c->bands = value;
-    } else if (!std::strcmp(name, "band_cpb")) {
-        if (value < 1 || value > 64) return fail(c, HQ_ERR_ARG, "band_cpb in [1,64]");
-        c->band_cpb = value;
     } else if (!std::strcmp(name, "assign_blocks_per_cu")) {
         if (value < 1 || value > 64) return fail(c, HQ_ERR_ARG, "assign_blocks_per_cu in [1,64]");
         c->assign_blocks_per_cu = value;

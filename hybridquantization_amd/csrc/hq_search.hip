@@ -1,0 +1,575 @@
+// hq_search.hip -- per-iteration kernels of the SWASA search around the
+// assign and cost kernels: palette prep (opponent table, duplicates, non-finite
+// guard), the device-resident SA step (IM:497-568 with SW:54-101), the exact
+// two-level candidate grid of the pruned argmin, and the fixed-order fp64
+// finalize (IM:736-768, SW:74-82).
+#include "hq_device.h"
+#include "hq_launch.h"
+
+namespace hq {
+
+// ----------------------------------------------------------------------------
+// prep_palette: grid (P), block 1024.
+// ----------------------------------------------------------------------------
+// Palette prep of palette p by a 1024-thread workgroup; `c` is colour k = tid & 255
+// (threads with tid >= 256 pass the same colour as their k).
+// Duplicate flags (colour k is a duplicate when an equal colour -- float
+// equality per channel -- sits at a lower index; the strict < of the argmin,
+// CL:179-193, never picks it, so build_grid leaves it out of lists) by an LDS
+// hash table of first occurrences: each colour claims or finds its key's slot
+// (open addressing, CAS on a representative index, equality checked against
+// the representative's colour), then atomicMin of its index on that slot; k is
+// a duplicate when the slot's minimum is below k.  +0/-0 hash alike (they
+// compare equal); a NaN channel equals nothing, so such a colour always takes
+// a fresh slot of its own.  (An all-pairs scan was O(K^2) VALU on one CU:
+// ~5 us per step at K = 256.)
+constexpr int kDupSlots = 2 * kMaxK;
+__device__ __forceinline__ uint32_t dup_hash(float4 c) {
+    const uint32_t x = __float_as_uint(c.x == 0.f ? 0.f : c.x);
+    const uint32_t y = __float_as_uint(c.y == 0.f ? 0.f : c.y);
+    const uint32_t z = __float_as_uint(c.z == 0.f ? 0.f : c.z);
+    const uint32_t h = x * 0x9E3779B1u ^ (y * 0x85EBCA77u + 0x27D4EB2Fu) ^ (z * 0xC2B2AE3Du + 0x165667B1u);
+    return (h ^ (h >> 15)) & (kDupSlots - 1);
+}
+
+__device__ __forceinline__ void prep_palette_body(const PaletteArgs& a, int p, float4 c) {
+    // threads 0..K-1 handle colour k = tid; any block size >= K.
+    const int tid = threadIdx.x, k = tid;
+    __shared__ float4 s[kMaxK];
+    __shared__ uint32_t s_tab[kDupSlots], s_min[kDupSlots];
+    __shared__ int s_nonfinite;
+    for (int i = tid; i < kDupSlots; i += blockDim.x) { s_tab[i] = ~0u; s_min[i] = ~0u; }
+    if (tid == 0) s_nonfinite = 0;
+    const bool own = k < a.K;
+    if (own) c.w = 0.f;  // SW:49: palettes carry .w = 0
+    else c = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (own) s[k] = c;
+    __syncthreads();
+    uint32_t slot = 0;
+    if (own) {
+        if (!(isfinite(c.x) && isfinite(c.y) && isfinite(c.z))) atomicOr(&s_nonfinite, 1);
+        slot = dup_hash(c);
+        for (;;) {
+            const uint32_t r = atomicCAS(&s_tab[slot], ~0u, (uint32_t)k);
+            if (r == ~0u) break;
+            const float4 o = s[r];
+            if (o.x == c.x && o.y == c.y && o.z == c.z) break;
+            slot = (slot + 1) & (kDupSlots - 1);
+        }
+        atomicMin(&s_min[slot], (uint32_t)k);
+    }
+    __syncthreads();
+    if (own) {
+        const float lr = srgb_lin(c.x), lg = srgb_lin(c.y), lb = srgb_lin(c.z);
+        const float4 opp = make_float4(dot3(lr, lg, lb, c_RGB2Opp + 0),
+                                       dot3(lr, lg, lb, c_RGB2Opp + 3),
+                                       dot3(lr, lg, lb, c_RGB2Opp + 6), 0.f);
+        a.pal[(int64_t)p * kMaxK + k] = c;
+        a.opp[(int64_t)p * kMaxK + k] = opp;
+        a.dup[(int64_t)p * kMaxK + k] = s_min[slot] < (uint32_t)k ? 1u : 0u;
+    }
+    if (tid == 0) a.pflags[p] = s_nonfinite;
+}
+
+__global__ __launch_bounds__(1024) void prep_palette_kernel(PaletteArgs a) {
+    const int p = blockIdx.x, k = threadIdx.x;
+    const float4 c = k < a.K ? a.pal_in[(int64_t)p * a.K + k] : make_float4(0.f, 0.f, 0.f, 0.f);
+    prep_palette_body(a, p, c);
+}
+
+// ----------------------------------------------------------------------------
+// sa_step: one step of the device-resident SWASA search (IM:497-568 with
+// SW:54-101), so an iteration needs no host round trip.  Grid (P), block 1024.
+//  - accept: the costs of the population just evaluated (finalize's
+//    [P][1+K] sums and used flags, all-reduced), C = sum/N + delta * #unused
+//    (IM:712; the repeated double additions of a float delta are exact, so the
+//    count times delta equals the host's loop), then the acceptance loop
+//    (SW:54-57, one next_double per positive delta), best tracking and the
+//    convergence loop (SW:59-62, IM:538-545) -- sequential on thread 0 of every
+//    workgroup, identically, so no workgroup waits for another;
+//  - generate: candidate palette p (SW:91-101 neighbours, or SW:40-52 random at
+//    the start), one java.util.Random draw per thread via a jump table
+//    (LCG^n = A_n s + C_n mod 2^48), then prep_palette_body.
+// State is ping-ponged (in -> out) so no workgroup overwrites what another reads.
+// Host-side values that depend only on the iteration (temperature, the
+// convergence threshold, the step width) arrive as arguments.
+// ----------------------------------------------------------------------------
+constexpr uint64_t kLcgMask = (1ull << 48) - 1;
+constexpr uint64_t kLcgMult = 0x5DEECE66Dull;
+
+__device__ __forceinline__ int32_t lcg_next(uint64_t& s, int bits) {
+    s = (s * kLcgMult + 0xBull) & kLcgMask;
+    return (int32_t)(int64_t)(s >> (48 - bits));
+}
+__device__ __forceinline__ double lcg_next_double(uint64_t& s) {
+    const int64_t hi = lcg_next(s, 26), lo = lcg_next(s, 27);
+    return (double)((hi << 27) + lo) * (1.0 / (double)(1LL << 53));
+}
+__device__ __forceinline__ uint64_t lcg_jump(uint64_t s, uint64_t A, uint64_t C) {
+    return (A * s + C) & kLcgMask;
+}
+
+// Block-shared SA state of one step (thread 0 runs the sequential logic).
+struct SaShared {
+    int unused[kSaMaxP];
+    int src[kSaMaxP];  // >= 0: member p continues from candidate src; -1: keeps its palette
+    double cur[kSaMaxP], err[kSaMaxP], ex[kSaMaxP];  // ex: exp(-(err - cur) / T), lanes in parallel
+    double sum[kSaMaxP], err_in[kSaMaxP];  // prefetched inputs of the sequential part
+    uint64_t seed;     // java.util.Random state (prefetched, then after the acceptance draws)
+    double best_in;
+    int best;          // candidate that set a new best (-1: none)
+};
+
+// Accept step (all threads of the block; returns after a barrier).  `writer`:
+// this block writes the shared outputs (errors, best error, next seed).  Every
+// global input is loaded before the first barrier, in parallel, so the
+// sequential part on thread 0 works from LDS (a chain of dependent global
+// loads on one thread was most of this kernel's ~13 us).
+__device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared& s) {
+#pragma clang fp contract(off)
+    const int tid = threadIdx.x, nt = blockDim.x, P = a.P, K = a.K;
+    constexpr int MAXF = 16;  // used flags per thread held in registers
+    const int nf = (P * K + nt - 1) / nt;
+    double fv[MAXF];
+    if (a.accept) {
+        if (tid < P) {
+            s.sum[tid] = a.out[(int64_t)tid * (1 + K)];
+            s.err_in[tid] = a.err_in[tid];
+        }
+        if (nf <= MAXF) {
+#pragma unroll
+            for (int j = 0; j < MAXF; ++j) {
+                const int e = tid + j * nt;
+                fv[j] = 1.0;
+                if (j < nf && e < P * K) {
+                    const int i = e / K, k = e - i * K;
+                    fv[j] = a.out[(int64_t)i * (1 + K) + 1 + k];
+                }
+            }
+        }
+    }
+    uint64_t jA = 0, jC = 0;  // the writer's jump past this step's draws
+    if (tid == 0) {
+        s.seed = *a.seed_in;
+        s.best_in = a.accept && !a.init ? *a.best_err : 0.0;
+        if (writer && a.generate) { jA = a.jump_A[K * 3 * P]; jC = a.jump_C[K * 3 * P]; }
+    }
+    if (tid < P) s.unused[tid] = 0;
+    __syncthreads();
+    if (a.accept) {
+        if (nf <= MAXF) {
+#pragma unroll
+            for (int j = 0; j < MAXF; ++j) {
+                const int e = tid + j * nt;
+                if (j < nf && e < P * K && fv[j] == 0.0) atomicAdd(&s.unused[e / K], 1);
+            }
+        } else {
+            for (int e = tid; e < P * K; e += nt)
+                if (a.out[(int64_t)(e / K) * (1 + K) + 1 + e % K] == 0.0) atomicAdd(&s.unused[e / K], 1);
+        }
+        __syncthreads();
+        if (tid < P) {  // per member, in parallel: error, current, acceptance probability
+            const double e = s.sum[tid] / a.n_total + (double)s.unused[tid] * (double)a.delta;
+            const double c = a.init ? e : s.err_in[tid];
+            s.err[tid] = e;
+            s.cur[tid] = c;
+            s.ex[tid] = exp(-(e - c) / (double)a.temperature);
+            s.src[tid] = a.init ? tid : -1;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint64_t seed = s.seed;
+            double* cur = s.cur;
+            const double* err = s.err;
+            double best = a.init ? err[0] : s.best_in;
+            int best_src = a.init ? 0 : -1;
+            if (a.init) {  // IM:490-493: argmin_first
+                for (int i = 1; i < P; ++i)
+                    if (best > err[i]) { best = err[i]; best_src = i; }
+            } else {
+                double minerror = 1.7976931348623157e308;
+                int minidx = 0;
+                for (int i = 0; i < P; ++i) {  // IM:518-537
+                    if (P > 1 && err[i] < minerror) { minerror = err[i]; minidx = i; }
+                    const double d = err[i] - cur[i];
+                    const bool acc = d <= 0 || s.ex[i] > lcg_next_double(seed);
+                    if (acc) {
+                        cur[i] = err[i];
+                        s.src[i] = i;
+                        if (cur[i] < best) { best = cur[i]; best_src = i; }
+                    }
+                }
+                for (int i = 0; a.convergence && P > 1 && i < P; ++i) {  // IM:538-545
+                    if (!(a.keep_threshold > lcg_next_double(seed))) {
+                        cur[i] = minerror;
+                        s.src[i] = minidx;
+                    }
+                }
+            }
+            s.seed = seed;
+            s.best = best_src;
+            if (writer) {
+                for (int i = 0; i < P; ++i) a.err_out[i] = cur[i];
+                *a.best_err = best;
+                *a.seed_out = a.generate ? lcg_jump(seed, jA, jC) : seed;
+            }
+        }
+    } else if (tid == 0) {
+        s.best = -1;
+        for (int i = 0; i < P; ++i) s.src[i] = -1;
+        if (writer) {
+            for (int i = 0; i < P; ++i) a.err_out[i] = a.err_in[i];
+            *a.seed_out = a.generate ? lcg_jump(s.seed, a.jump_A[K * 3 * P], a.jump_C[K * 3 * P]) : s.seed;
+        }
+    }
+    __syncthreads();
+}
+
+// Member p's accepted palette into s_from (LDS, 4K floats); `lead` also copies
+// it to colors_out (and, for p = 0, a new best to best_colors).  The two likely
+// sources -- member p's candidate and its kept palette -- are read before the
+// acceptance (pf_cand, pf_col: element tid); only a convergence copy from
+// another member's candidate reads after it.
+__device__ __forceinline__ void sa_keep(const SaArgs& a, int p, bool lead, const SaShared& s,
+                                        float pf_cand, float pf_col, float* s_from) {
+    const int n4 = 4 * a.K, tid = threadIdx.x, nt = blockDim.x;
+    const int src = s.src[p];
+    for (int e = tid; e < n4; e += nt) {
+        float v;
+        if (e == tid && src == p) v = pf_cand;
+        else if (e == tid && src < 0) v = pf_col;
+        else v = src >= 0 ? a.cand_in[(int64_t)src * n4 + e] : a.colors_in[(int64_t)p * n4 + e];
+        s_from[e] = v;
+        if (lead) a.colors_out[(int64_t)p * n4 + e] = v;
+    }
+    if (lead && p == 0 && s.best >= 0)  // IM:533-536: the best palette so far
+        for (int e = tid; e < n4; e += nt) a.best_colors[e] = a.cand_in[(int64_t)s.best * n4 + e];
+    __syncthreads();
+}
+
+// Candidate p into s_cand (.w = 0; cand_out too when `lead`): draw t = 3i + c of
+// this palette's block (SW:91-101 neighbours of s_from, or SW:40-52 random).
+// jA/jC: this thread's prefetched jump to its first draw (t = tid).
+__device__ __forceinline__ void sa_generate(const SaArgs& a, int p, const float* s_from, uint64_t seed,
+                                            float4* s_cand, bool lead, uint64_t jA, uint64_t jC,
+                                            uint64_t bA, uint64_t bC) {
+#pragma clang fp contract(off)
+    const int K = a.K, n4 = 4 * K, tid = threadIdx.x, nt = blockDim.x;
+    const uint64_t base = lcg_jump(seed, bA, bC);  // bA, bC: jump_A/C[3Kp], prefetched
+    for (int t = tid; t < 3 * K; t += nt) {
+        const int i = t / 3, c = t - 3 * i;
+        const uint64_t st = t == tid ? lcg_jump(base, jA, jC) : lcg_jump(base, a.jump_A[t + 1], a.jump_C[t + 1]);
+        const float u = (float)(int32_t)(st >> 24) / (float)(1 << 24);
+        float v;
+        if (a.random) {
+            v = u;
+        } else {
+            const float step = (u * 2 - 1) * a.amax;
+            const float x = s_from[4 * i + c] + step;
+            v = x > 0.f ? (x > 1.f ? 1.f : x) : 0.f;  // clampf_java (SW:103-106)
+        }
+        reinterpret_cast<float*>(s_cand)[4 * i + c] = v;
+        if (lead) a.cand_out[(int64_t)p * n4 + 4 * i + c] = v;
+    }
+    for (int k = tid; k < K; k += nt) {
+        reinterpret_cast<float*>(s_cand)[4 * k + 3] = 0.f;
+        if (lead) a.cand_out[(int64_t)p * n4 + 4 * k + 3] = 0.f;
+    }
+    __syncthreads();
+}
+
+// Prefetches of a step, issued before the acceptance: member p's candidate and
+// kept palette (element tid) and this thread's jump to draw tid.
+struct SaPf {
+    float cand = 0.f, col = 0.f;
+    uint64_t jA = 0, jC = 0, bA = 0, bC = 0;
+    __device__ __forceinline__ void load(const SaArgs& a, int p) {
+        const int n4 = 4 * a.K, tid = threadIdx.x;
+        if (tid < n4) {
+            if (a.accept) cand = a.cand_in[(int64_t)p * n4 + tid];
+            col = a.colors_in[(int64_t)p * n4 + tid];
+        }
+        if (a.generate && tid < 3 * a.K) {
+            jA = a.jump_A[tid + 1];
+            jC = a.jump_C[tid + 1];
+            bA = a.jump_A[3 * a.K * p];
+            bC = a.jump_C[3 * a.K * p];
+        }
+    }
+};
+
+// Build with -DHQ_SA_TIMING to print block 0's phase times (accept, keep,
+// generate, prep; wall_clock64 ticks of 10 ns) per launch.
+__global__ __launch_bounds__(1024) void sa_step_kernel(SaArgs a) {
+    const int p = blockIdx.x, K = a.K;
+    __shared__ SaShared s;
+    __shared__ float s_from[4 * kMaxK];
+    __shared__ float4 s_cand[kMaxK];
+#ifdef HQ_SA_TIMING
+    const uint64_t t0 = wall_clock64();
+#endif
+    SaPf pf;
+    pf.load(a, p);
+    sa_accept(a, p == 0, s);
+#ifdef HQ_SA_TIMING
+    const uint64_t t1 = wall_clock64();
+#endif
+    sa_keep(a, p, true, s, pf.cand, pf.col, s_from);
+#ifdef HQ_SA_TIMING
+    const uint64_t t2 = wall_clock64();
+#endif
+    if (!a.generate) return;
+    sa_generate(a, p, s_from, s.seed, s_cand, true, pf.jA, pf.jC, pf.bA, pf.bC);
+#ifdef HQ_SA_TIMING
+    const uint64_t t3 = wall_clock64();
+#endif
+    const int k = threadIdx.x;
+    prep_palette_body(a.prep, p, k < K ? s_cand[k] : make_float4(0.f, 0.f, 0.f, 0.f));
+#ifdef HQ_SA_TIMING
+    __syncthreads();
+    if (threadIdx.x == 0 && p == 0)
+        printf("SA_T %d %d %d %d %d\n", a.accept, (int)(t1 - t0), (int)(t2 - t1), (int)(t3 - t2),
+               (int)(wall_clock64() - t3));
+#endif
+}
+
+// ----------------------------------------------------------------------------
+// build_grid: grid (G1^3, P), block 256.  One workgroup per level-1 cell; it
+// also writes the 64 level-2 children (G2 = 4*G1).
+//
+// Exactness: for a closed box B and any pixel p in B, the reference winner k*
+// satisfies dmin2(B,k*) <= T(B)*(1+~1.1e-6) with T(B) = min_j dmax2(B,j) (fp32
+// rounding of d2 and the sqrt collapse bounded by ~18 ulp); candidates keep
+// dmin2 <= T*(1+1e-5).  Children lists are subsets of the parent list, and
+// the child's T is attained inside it, so level 2 needs only the parent list.
+// Entries: byte0 = count (255 = overflow), then ascending indices.
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ double ax_min2(double c, double lo, double hi) {
+    const double d = fmax(fmax(lo - c, c - hi), 0.0);
+    return d * d;
+}
+__device__ __forceinline__ double ax_max2(double c, double lo, double hi) {
+    const double d = fmax(c - lo, hi - c);
+    return d * d;
+}
+
+#define HQ_CAND_MARGIN (1.0 + 1e-5)
+
+// Level-2 entries are interleaved by groups of 4 palettes: the 4 entries of one
+// cell share a 64-byte line, so a pixel evaluated under the 4 palettes of a
+// group fetches one line instead of 4 (random 16-B lookups are bound by the
+// line fetches they cause, not by their bytes).
+__host__ __device__ __forceinline__ int64_t lvl2_offset(int64_t gstride, int p, int64_t cell) {
+    return (int64_t)(p >> 2) * gstride + cell * 64 + (p & 3) * 16;
+}
+
+// The grid work of level-1 cell `cell` of palette p; thread tid holds colour
+// tid (zeros past K) and whether it may be a candidate (prep_palette's
+// duplicate flags: an exact duplicate never wins the strict < of CL:186).
+__device__ __forceinline__ void grid_cell_body(const GridArgs& a, int p, int cell, float4 c,
+                                               bool valid, bool exh) {
+    const int tid = threadIdx.x;
+    const int G1 = a.G1, G2 = 4 * G1;
+    const int ci = cell / (G1 * G1), cj = (cell / G1) % G1, ck = cell % G1;
+    __shared__ float4 s_col[kMaxK];
+    __shared__ uint8_t s_list[kMaxK];
+    __shared__ double s_min[4];
+    __shared__ int s_wcount[4];
+
+    s_col[tid] = c;
+    const double inv1 = 1.0 / G1;
+    const double lo0 = ci * inv1, hi0 = (ci + 1) * inv1;
+    const double lo1 = cj * inv1, hi1 = (cj + 1) * inv1;
+    const double lo2 = ck * inv1, hi2 = (ck + 1) * inv1;
+    double dmin2 = INFINITY, dmax2 = INFINITY;
+    if (valid) {
+        dmin2 = ax_min2(c.x, lo0, hi0) + ax_min2(c.y, lo1, hi1) + ax_min2(c.z, lo2, hi2);
+        dmax2 = ax_max2(c.x, lo0, hi0) + ax_max2(c.y, lo1, hi1) + ax_max2(c.z, lo2, hi2);
+    }
+    double m = dmax2;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmin(m, __shfl_xor(m, off, 64));
+    const int wave = tid >> 6, lane = tid & 63;
+    if (lane == 0) s_min[wave] = m;
+    __syncthreads();
+    const double T1 = fmin(fmin(s_min[0], s_min[1]), fmin(s_min[2], s_min[3]));
+    const bool cand = valid && dmin2 <= T1 * HQ_CAND_MARGIN;
+    const uint64_t bal = __ballot(cand);
+    if (lane == 0) s_wcount[wave] = __popcll(bal);
+    __syncthreads();
+    int base = 0;
+    for (int w = 0; w < wave; ++w) base += s_wcount[w];
+    const int total = s_wcount[0] + s_wcount[1] + s_wcount[2] + s_wcount[3];
+    if (cand) s_list[base + __popcll(bal & ((1ull << lane) - 1ull))] = (uint8_t)tid;
+    __syncthreads();
+
+    uint8_t* l1 = a.lvl1 + (int64_t)p * a.lvl1_pitch + (int64_t)cell * 32;
+    const bool ovf1 = exh || total > kL1Cap;
+    if (tid < 32) {
+        uint8_t v;
+        if (tid == 0) v = ovf1 ? kOverflow : (uint8_t)total;
+        else v = (!ovf1 && tid - 1 < total) ? s_list[tid - 1] : 0;
+        l1[tid] = v;
+    }
+    // Level 2: child c = tid >> 2 of this cell, its parent-list positions shared
+    // by the 4 threads of a quad (q = tid & 3 takes positions q, q+4, ...): T2 and
+    // the candidate mask are combined across the quad by shuffles, and each
+    // candidate's byte lands at its rank in ascending list order.  (One thread
+    // per child walking the list twice, on one wave of the four, made this
+    // kernel ~15 us per population.)
+    {
+        const int ch = tid >> 2, q = tid & 3;
+        const int ci2 = ci * 4 + (ch >> 4), cj2 = cj * 4 + ((ch >> 2) & 3), ck2 = ck * 4 + (ch & 3);
+        const double inv2 = 1.0 / G2;
+        const double l0 = ci2 * inv2, h0 = (ci2 + 1) * inv2;
+        const double l1b = cj2 * inv2, h1 = (cj2 + 1) * inv2;
+        const double l2 = ck2 * inv2, h2 = (ck2 + 1) * inv2;
+        // pass 1: T2 over the whole parent list (which can exceed 31 entries: the
+        // level-1 entry then overflows, the children still get lists)
+        double t2 = INFINITY;
+        for (int i = q; !exh && i < total; i += 4) {
+            const float4 cc = s_col[s_list[i]];
+            t2 = fmin(t2, ax_max2(cc.x, l0, h0) + ax_max2(cc.y, l1b, h1) + ax_max2(cc.z, l2, h2));
+        }
+        t2 = fmin(t2, __shfl_xor(t2, 1, 64));
+        t2 = fmin(t2, __shfl_xor(t2, 2, 64));
+        const double thr = t2 * HQ_CAND_MARGIN;
+        // pass 2, 32 positions at a time: candidate mask, ranks in list order
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        int n = 0;  // candidates so far (quad-uniform)
+        for (int b0 = 0; !exh && b0 < total && n <= kL2Cap; b0 += 32) {
+            uint32_t mine = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int i = b0 + q + 4 * j;
+                if (i < total) {
+                    const float4 cc = s_col[s_list[i]];
+                    const double d = ax_min2(cc.x, l0, h0) + ax_min2(cc.y, l1b, h1) + ax_min2(cc.z, l2, h2);
+                    if (d <= thr) mine |= 1u << (q + 4 * j);
+                }
+            }
+            uint32_t M = mine | (uint32_t)__shfl_xor((int)mine, 1, 64);
+            M |= (uint32_t)__shfl_xor((int)M, 2, 64);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int r = q + 4 * j;
+                if ((mine >> r) & 1u) {
+                    const int pos = n + __popc(M & ((1u << r) - 1u)) + 1;  // byte in the entry
+                    if (pos <= kL2Cap) w[pos >> 2] |= (uint32_t)s_list[b0 + r] << (8 * (pos & 3));
+                }
+            }
+            n += __popc(M);
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            w[m] |= (uint32_t)__shfl_xor((int)w[m], 1, 64);
+            w[m] |= (uint32_t)__shfl_xor((int)w[m], 2, 64);
+        }
+        if (q == 0) {
+            if (exh || n > kL2Cap) { w[0] = kOverflow; w[1] = w[2] = w[3] = 0; }
+            else w[0] |= (uint32_t)n;
+            uint8_t* l2e = a.lvl2 + lvl2_offset(a.lvl2_gstride, p, (int64_t)(ci2 * G2 + cj2) * G2 + ck2);
+            *reinterpret_cast<uint4*>(l2e) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
+    const int p = blockIdx.y, tid = threadIdx.x;
+    const bool exh = a.pflags[p] != 0;
+    bool valid = false;
+    float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (tid < a.K) {
+        c = a.pal[(int64_t)p * kMaxK + tid];
+        valid = !exh && a.dup[(int64_t)p * kMaxK + tid] == 0;
+    }
+    grid_cell_body(a, p, blockIdx.x, c, valid, exh);
+}
+// ----------------------------------------------------------------------------
+// finalize: grid (P), block 256.  Fixed-order fp64 sum of the tile partials
+// and OR of the per-block used masks -> out[p] = {sum, used[0..K-1]}.
+// ----------------------------------------------------------------------------
+// finalize: one 1024-thread workgroup per palette.  Thread t sums partials
+// t, t + 1024, ... with all of its loads issued before the first add (one memory
+// round trip; 256 threads summing 8 at a time took ~10 dependent rounds), then
+// a fixed-order wave and workgroup reduction: bitwise reproducible.
+__global__ __launch_bounds__(1024) void finalize_kernel(FinalizeArgs a) {
+    constexpr int NT = 1024, NL = 24;  // loads in flight per thread per round
+    const int p = blockIdx.x, tid = threadIdx.x;
+    __shared__ double s_red[NT / 64];
+    __shared__ uint32_t s_mask[NT];
+    const double* part = a.partial + (int64_t)p * a.ntiles;
+    double s = 0.0;
+    for (int t0 = 0; t0 < a.ntiles; t0 += NT * NL) {
+        double v[NL];
+#pragma unroll
+        for (int u = 0; u < NL; ++u) {
+            const int t = t0 + u * NT + tid;
+            v[u] = t < a.ntiles ? part[t] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < NL; ++u) s += v[u];
+    }
+    s = wave_sum_to_lane63(s);
+    if ((tid & 63) == 63) s_red[tid >> 6] = s;
+    // used: thread = (word w = tid & 7, block slice tid >> 3)
+    uint32_t m = 0;
+    const int w = tid & 7;
+    const uint32_t* um = a.used_mask + (int64_t)p * a.nblocks * 8;
+    for (int b0 = tid >> 3; b0 < a.nblocks; b0 += (NT / 8) * 8) {
+        uint32_t mv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int b = b0 + (NT / 8) * u;
+            mv[u] = b < a.nblocks ? um[b * 8 + w] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) m |= mv[u];
+    }
+    s_mask[tid] = m;
+    __syncthreads();
+    double* out = a.out + (int64_t)p * (1 + a.K);
+    if (tid == 0) {
+        double tot = 0.0;
+        for (int i = 0; i < NT / 64; ++i) tot += s_red[i];
+        out[0] = tot;
+    }
+    if (tid < 8) {
+        uint32_t acc = 0;
+        for (int i = tid; i < NT; i += 8) acc |= s_mask[i];
+        s_mask[tid] = acc;  // slots 0..7 are only read after the barrier below
+    }
+    __syncthreads();
+    for (int k = tid; k < a.K; k += NT) out[1 + k] = (s_mask[k >> 5] >> (k & 31)) & 1u ? 1.0 : 0.0;
+}
+
+// ----------------------------------------------------------------------------
+// Launchers
+// ----------------------------------------------------------------------------
+thread_local hipEvent_t t_ev_start = nullptr, t_ev_stop = nullptr;
+void set_launch_events(hipEvent_t start, hipEvent_t stop) {
+    t_ev_start = start;
+    t_ev_stop = stop;
+}
+
+hipError_t launch_prep_palette(const PaletteArgs& a, int P, hipStream_t s) {
+    HQ_LAUNCH(prep_palette_kernel, dim3(P), dim3(1024), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_sa_step(const SaArgs& a, hipStream_t s) {
+    HQ_LAUNCH(sa_step_kernel, dim3(a.P), dim3(1024), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_build_grid(const GridArgs& a, int P, hipStream_t s) {
+    HQ_LAUNCH(build_grid_kernel, dim3(a.G1 * a.G1 * a.G1, P), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_finalize(const FinalizeArgs& a, int P, hipStream_t s) {
+    HQ_LAUNCH(finalize_kernel, dim3(P), dim3(1024), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace hq

@@ -63,7 +63,6 @@ class ImageManipulation:
             check(rc)
         self.openCLFiltersReady = False
         self._filters = None
-        self._image_key = None
 
     # IM:95
     def getOpenCLAvailable(self) -> bool:
@@ -86,7 +85,6 @@ class ImageManipulation:
               ctx)
         self._filters = (k1, k2, k3, ak3)
         self.openCLFiltersReady = True
-        self._image_key = None
 
     @property
     def halfSize(self) -> int:  # IM:408
@@ -125,7 +123,6 @@ class ImageManipulation:
         check(self._lib.hq_set_image_shard(ctx, fptr(rgb), fptr(lab) if lab is not None else None,
                                            int(w), h, fptr(il), int(row_begin), int(row_end)),
               ctx)
-        self._image_key = (id(rgbInline), id(labInline), int(w))
         self.w, self.h = int(w), h
 
     def getLabRef(self):
@@ -165,8 +162,10 @@ class ImageManipulation:
         ctx = self._require()
         if not self.openCLFiltersReady:
             self.updateOpenCLFilters(filters, absfilters)
-        if self._image_key != (id(inlinergbOriginal), id(inlineScielabOriginal), int(w)):
-            self.setImage(inlinergbOriginal, inlineScielabOriginal, w, illuminant)
+        # Always upload (IM:450-478 does too): an identity cache keyed on id() can
+        # match a new array that reuses a freed one's id, or miss an in-place edit,
+        # and the upload is small next to a 5000-iteration search.
+        self.setImage(inlinergbOriginal, inlineScielabOriginal, w, illuminant)
         sw = simulatedAnnealing
         params = sw.params()
         handle = C.c_void_p()

@@ -11,8 +11,7 @@
  *
  * Conventions
  *  - Plain C types only; host pointers are caller-owned and only read/written
- *    for the duration of the call.  Functions with a `_device` suffix take
- *    device pointers on the context's GPU instead.
+ *    for the duration of the call.
  *  - "inline float4" = the reference's RGBA / Lab layout: float[4*N], pixel
  *    p = y*w + x at [4p .. 4p+3], .w = 0 (HQ:279-291 makeinline).
  *  - Palettes: float[4*K] per palette with .w = 0 (SW:40-52); populations are
@@ -178,40 +177,19 @@ int hq_profile_enable(hq_ctx *ctx, int on);
 int hq_profile_get(hq_ctx *ctx, const char *kernel, double *total_ms, int64_t *launches);
 int hq_profile_reset(hq_ctx *ctx);
 
-/* Tuning knobs (testing / benchmarking; defaults are the measured best):
+/* Tuning knobs (testing / benchmarking; defaults are the measured best).  They
+ * may change between calls, also between hq_search_run calls of one search:
+ * every evaluation sizes the context's work buffers for the options and image
+ * in force when it is enqueued.
  *   "grid"         argmin pruning resolution G2: 0 = exhaustive, 16, 32 (default), 64
- *   "cost_variant" 0 = one tile per workgroup (default), 1 = generic two-pass
- *                  path (any filter length)
- *   "cost_tile"    8-row tiles at 4 WG/CU unless noted.  7 = vertical passes on the
- *                  matrix cores (split-f16 products, stacked filter pairs), horizontal
- *                  pass over row pairs on VALU, in two opponent-channel groups (6 WG/CU;
- *                  default); 6 = the same with the vertical passes on VALU; 4 = row
- *                  pairs, all seven filters at once (packed FMA across two rows, 2 columns
- *                  per item); 5 = the same with 4 columns per item; 2 = row layout, 4-row vertical
- *                  items; 1 = vertical pass split by opponent-channel group; 3 = vertical
- *                  pass on the matrix cores (split-f16 products); 0 = 16-row tiles (2 WG/CU);
- *                  8 = both passes on the matrix cores (96-column tiles); 9 = 7 with the
- *                  vertical MFMA's operands swapped, column-major indices, 1-row items;
- *                  10 = both passes on the matrix cores on 9's layout; 11 = 7 with
- *                  4-column row-pair items on a parity-split layout
+ *   "cost_variant" 0 = fast tiled path (default; 21-tap filters), 1 = generic
+ *                  two-pass path (any filter length; the fast path's cross-check)
  *   "trim"         1 = skip the narrow k1 filters' taps below 1e-9 of their peak
  *                  (default; only when the filters allow it), 0 = all taps
- *   "assign_group" palettes served by one pixel pass: 4 (default; their level-2 entries
- *                  share one 64-byte line), 2, 1
- *   "assign_batch" with group 4: 3 = software-pipelined (default: the next pixel's lookup
- *                  and the one after's RGB in flight while a pixel is resolved), 1 or 2 =
- *                  pixels per batch; with group 1: 4 or 8 = pixels per batch, 0 = one-pixel
- *                  prefetch; with group 4, 5 = one (pixel, palette) pair per lane
- *   "assign_rep"   palette replication in LDS for group 1/2 with batch 0: 1, 2, 4, 16
  *   "assign_blocks_per_cu" workgroups per CU of the assign grid (default 8)
- *   "bands"        0 (default) or 2-16 row bands: assign of band j+1 on a second stream
- *                  beside the cost of band j (bit-identical results)
- *   "band_cpb"     banded assign: pixel chunks per workgroup (default 2)
  *   "sa_device"    hq_search_*: 1 (default) = the SWASA iterations run on the device
  *                  (accept/generate kernel, no host round trip per iteration; needs
  *                  population <= 64), 0 = host-driven, one evaluation call each
- *   "sa_fuse_grid" device search: 1 = accept/generate and the candidate grid in one
- *                  kernel (every grid workgroup repeats the acceptance); default 0
  *   "shard_solo"   experiment only: let a row-block shard run hq_search_* without a
  *                  communicator (its own partial costs; per-rank timing at N GPUs) */
 int hq_set_option(hq_ctx *ctx, const char *name, int value);

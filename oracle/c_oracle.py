@@ -39,6 +39,9 @@ def lib():
         L.hqo_rgb_to_xyz.argtypes = [_f, _f, _f, C.c_longlong, _f]
         L.hqo_xyz_to_scielab.argtypes = [_f, C.c_int, C.c_int, _f, _f, _f, _f, C.c_int, _f, _f]
         L.hqo_xyz_to_scielab.restype = C.c_int
+        L.hqo_xyz_to_scielab_mt.argtypes = [_f, C.c_int, C.c_int, _f, _f, _f, _f, C.c_int, _f, _f,
+                                            C.c_int]
+        L.hqo_xyz_to_scielab_mt.restype = C.c_int
         L.hqo_compute_error.argtypes = [_f, _f, C.c_longlong, _f]
         L.hqo_compute_error.restype = C.c_double
         _LIB = L
@@ -62,8 +65,9 @@ def assign(rgb4, pal4):
     return idx, used
 
 
-def srgb_to_scielab(R, G, B, filt, w):
-    """LabRef of a planar image (IM:100-153 + IM:285-370) -> float4 [N,4]."""
+def srgb_to_scielab(R, G, B, filt, w, nthreads=1):
+    """LabRef of a planar image (IM:100-153 + IM:285-370) -> float4 [N,4].
+    nthreads splits the rows of each 1-D pass (same arithmetic)."""
     R, G, B = _c32(R), _c32(G), _c32(B)
     n = R.shape[0]
     xyz = np.zeros((n, 4), np.float32)
@@ -71,8 +75,8 @@ def srgb_to_scielab(R, G, B, filt, w):
     lab = np.zeros((n, 4), np.float32)
     k1, k2, k3, ak3, il = (_c32(filt.k1), _c32(filt.k2), _c32(filt.k3), _c32(filt.absk3),
                            _c32(filt.illum))
-    rc = lib().hqo_xyz_to_scielab(_p(xyz), w, n // w, _p(k1), _p(k2), _p(k3), _p(ak3),
-                                  filt.half, _p(il), _p(lab))
+    rc = lib().hqo_xyz_to_scielab_mt(_p(xyz), w, n // w, _p(k1), _p(k2), _p(k3), _p(ak3),
+                                     filt.half, _p(il), _p(lab), int(nthreads))
     if rc != 0:
         raise ValueError(f"hqo_xyz_to_scielab failed ({rc})")
     return lab

@@ -275,19 +275,25 @@ int hqo_rgb_to_xyz(const float *R, const float *G, const float *B, long long n, 
     return 0;
 }
 
-/* One 1-D pass of convolve4Channels / convolve1Channel (CL:2-74) along rows of
- * a (rows x n) array of float3, with the filter k[T][4]; chans = 3 or 1 (.x). */
-static void conv_rows(const float *in, float *out, int rows, int n, const float *k, int half,
-                      int chans, int update) {
-    for (int r = 0; r < rows; ++r)
-        for (int j = 0; j < n; ++j) {
+/* One 1-D pass of convolve4Channels / convolve1Channel (CL:2-74) along rows
+ * [lo, hi) of a (rows x n) array of float3, with the filter k[T][4]; chans = 3
+ * or 1 (.x).  Rows are independent, so threads split them (no effect on the
+ * arithmetic). */
+typedef struct {
+    const float *in; float *out; int n; const float *k; int half, chans, update;
+} conv_job;
+
+static void conv_rows(void *a, int lo, int hi) {
+    const conv_job *J = (const conv_job *)a;
+    for (int r = lo; r < hi; ++r)
+        for (int j = 0; j < J->n; ++j) {
             float acc[3] = {0, 0, 0};
-            for (int i = -half, t = 0; i <= half; ++i, ++t) {
-                const float *p = in + 3LL * ((long long)r * n + reflect(j + i, n));
-                for (int c = 0; c < chans; ++c) acc[c] = fmaf(p[c], k[4 * t + c], acc[c]);
+            for (int i = -J->half, t = 0; i <= J->half; ++i, ++t) {
+                const float *p = J->in + 3LL * ((long long)r * J->n + reflect(j + i, J->n));
+                for (int c = 0; c < J->chans; ++c) acc[c] = fmaf(p[c], J->k[4 * t + c], acc[c]);
             }
-            float *o = out + 3LL * ((long long)r * n + j);
-            for (int c = 0; c < chans; ++c) o[c] = update ? o[c] + acc[c] : acc[c];
+            float *o = J->out + 3LL * ((long long)r * J->n + j);
+            for (int c = 0; c < J->chans; ++c) o[c] = J->update ? o[c] + acc[c] : acc[c];
         }
 }
 
@@ -298,9 +304,9 @@ static void transpose3(const float *in, float *out, int rows, int n) {
             for (int c = 0; c < 3; ++c) out[3LL * ((long long)j * rows + r) + c] = in[3LL * ((long long)r * n + j) + c];
 }
 
-int hqo_xyz_to_scielab(const float *xyz4, int w, int h, const float *k1, const float *k2,
-                       const float *k3, const float *absk3, int half, const float *illum,
-                       float *lab4) {
+int hqo_xyz_to_scielab_mt(const float *xyz4, int w, int h, const float *k1, const float *k2,
+                          const float *k3, const float *absk3, int half, const float *illum,
+                          float *lab4, int nthreads) {
     if (w < half || h < half) return -1;
     long long n = (long long)w * h;
     int T = 2 * half + 1;
@@ -320,14 +326,22 @@ int hqo_xyz_to_scielab(const float *xyz4, int w, int h, const float *k1, const f
     const float *hk[3] = {k1, k2, k3v}, *vk[3] = {k1, k2, ak3v};
     for (int f = 0; f < 3; ++f) {
         int chans = f < 2 ? 3 : 1;
-        conv_rows(opp, tmp, h, w, hk[f], half, chans, 0);
+        conv_job hj = {opp, tmp, w, hk[f], half, chans, 0};
+        parallel_for(h, nthreads, conv_rows, &hj);
         transpose3(tmp, tmpT, h, w);                         /* now (w x h) */
-        conv_rows(tmpT, convT, w, h, vk[f], half, chans, f > 0);
+        conv_job vj = {tmpT, convT, h, vk[f], half, chans, f > 0};
+        parallel_for(w, nthreads, conv_rows, &vj);
     }
     transpose3(convT, conv, w, h);
     for (long long i = 0; i < n; ++i) opp2lab(conv + 3 * i, illum, lab4 + 4 * i);
     free(opp); free(tmp); free(tmpT); free(convT); free(conv); free(k3v); free(ak3v);
     return 0;
+}
+
+int hqo_xyz_to_scielab(const float *xyz4, int w, int h, const float *k1, const float *k2,
+                       const float *k3, const float *absk3, int half, const float *illum,
+                       float *lab4) {
+    return hqo_xyz_to_scielab_mt(xyz4, w, h, k1, k2, k3, absk3, half, illum, lab4, 1);
 }
 
 /* CL:201-209 CIEDE(-DCIE76) + IM:886-893 (computeError's host loop). */

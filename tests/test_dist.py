@@ -34,15 +34,22 @@ def _worker(rank, world, port, out):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     f, rgb3, lab, pals = _inputs()
-    r0, r1 = rank * H // world, (rank + 1) * H // world
+    from hybridquantization_amd.dist import shard_rows
+
+    r0, r1 = shard_rows(H, world, rank)
     part = torch.zeros(P, 1 + K, dtype=torch.float64)
     for p, pal in enumerate(pals):
         s, used = o.shard_partial(rgb3, lab, pal, f, W, H, r0, r1)
         part[p, 0] = s
         part[p, 1:] = torch.from_numpy(used.astype(np.float64))
     dist.all_reduce(part)  # the single exchange step of the sharded path
+    # bench.py's N > 1 control path (hybridquantization_amd.dist) on the same group
+    from hybridquantization_amd import dist as hqd
+
+    uid = hqd.broadcast_unique_id(dist, rank, lambda: bytes(range(128)))
+    el = hqd.max_over_ranks(dist, 0.5 + rank)
     if rank == 0:
-        out.put(part.numpy())
+        out.put((part.numpy(), uid, el, hqd.shard_rows(H, world, rank), hqd.shard_rows(H, world, 1)))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -61,10 +68,12 @@ def test_row_block_shards_allreduce_matches_full(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    red = q.get(timeout=240)
+    red, uid, el, b0, b1 = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    assert uid == bytes(range(128)) and el == 1.5
+    assert b0 == (0, H // 2) and b1 == (H // 2, H)
     f, rgb3, lab, pals = _inputs()
     rgba = o.inline_rgba(rgb3[:, 0], rgb3[:, 1], rgb3[:, 2])
     for p, pal in enumerate(pals):
