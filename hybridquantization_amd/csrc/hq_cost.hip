@@ -19,8 +19,8 @@ namespace hq {
 // then the horizontal pass on the TW output columns, Opp->Lab, dE, fp64 partial.
 // ----------------------------------------------------------------------------
 // Tile geometry of the fast path: RW = 128 region columns, TW = 108 output
-// columns, TH = 8 output rows.
-constexpr int kFastHalf = 10, kFastRW = 128, kFastTH = 8;
+// columns; 8 (cost_mfma_kernel) or 16 (cost16_kernel) output rows.
+constexpr int kFastHalf = 10, kFastRW = 128;
 constexpr int kFastTW = kFastRW - 2 * kFastHalf;
 
 template <int HALF>
@@ -275,7 +275,7 @@ __global__ __launch_bounds__(256, 6) void cost_mfma_kernel(CostArgs a, int P_) {
     const TileItem cur = tile_item<TW, TH>(a, xcd_remap(blockIdx.x, a.ntiles * P_), P_);
     const TapsPtr<HALF> taps = (TapsPtr<HALF>)(uintptr_t)a.taps;  // H taps x 2^-30
     const int lane = tid & 63, wv = tid >> 6, lc = lane & 15, lk = lane >> 4;
-    const uint4* frag = a.vfrag16 + (TRIM ? 4 * 2 * 64 : 0) + lane;  // [trim][stack][hi,lo][lane]
+    const uint4* frag = a.vfrag16 + (TRIM ? 2 * 4 * 2 * 64 : 0) + lane;  // [trim][half 0][stack][hi,lo][lane]
 
     TileFill<HALF, RW, TH> fill;
     fill.issue(a, cur, tid);
@@ -378,6 +378,249 @@ __global__ __launch_bounds__(256, 6) void cost_mfma_kernel(CostArgs a, int P_) {
                 const float3 l3 = opp2lab_fast(acc0[xo][r], acc1[xo][r], acc2[xo][r], a.m_lab);
                 const float e = delta_e<DE>(labv[r][0][xo], labv[r][1][xo], labv[r][2][xo], l3.x,
                                             l3.y, l3.z);
+                part += (gy0 + r < g.r1 && gx0 + xo < g.W) ? e : 0.f;
+            }
+        }
+        sum = (double)part;
+    }
+    sum = wave_sum_to_lane63(sum);
+    if ((tid & 63) == 63) s_red[tid >> 6] = sum;
+    __syncthreads();
+    if (tid == 0)
+        a.partial[(int64_t)cur.p * a.ntiles + cur.tile] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+}
+
+// ----------------------------------------------------------------------------
+// cost16: 16-row tiles.  The random opponent-table gathers of the vertical
+// pass and the horizontal windows are the kernel's LDS traffic, and LDS
+// bounds cost_mfma (PMC: ~77% of cycles LDS-active, a quarter of that in bank
+// conflicts of the random gathers).  A 16 x 108 tile needs a 36-row region:
+// - vertical pass: output rows 0-7 take region rows 0-31 (B0-B3, one 8-row
+//   block per lane group), rows 8-15 take rows 8-39 -- lane groups 1-3 keep
+//   B1-B3 and only lane group 0 gathers B4 = rows 32-39 (the half-1 A
+//   fragments permute K to match): 5 gathered blocks per 16 rows instead of 8;
+// - horizontal pass: items of 4 output columns x a row pair (216 items, one per
+//   thread of 8 row pairs x 32 slots), a 24-column window = 12 ds_read_b128
+//   per filter for 8 outputs (cost_mfma: 11 for 4).  Row-pair rows store their
+//   column pairs split by parity (pair p -> half p & 1, slot p >> 1), so read q
+//   of item j lands at half q & 1, slot j + q / 2: lanes 16 B apart, conflict
+//   free.  The vertical pass gives each 16-column MFMA block the 16 columns of
+//   one parity half of a 32-column range (lane n -> column 4(n >> 1) + 2 bb +
+//   (n & 1)), so a block's stores fill 16 contiguous float2 of one half:
+//   conflict free without padding the rows.
+// 40,480 B of LDS (32 KiB s_v, 36 index rows): 4 workgroups per CU.
+// ----------------------------------------------------------------------------
+constexpr int kTH16 = 16;
+constexpr int kWideHalf = 64;  // float2 per half of a permuted row-pair row
+
+// float2 position of column `col` in a permuted row-pair row: half = bit 1 of
+// col, 16-B slot col >> 2, float2 col & 1.
+__device__ __forceinline__ int wide_pos(int col) {
+    return ((col >> 1) & 1) * kWideHalf + ((col >> 2) << 1) + (col & 1);
+}
+
+// Horizontal pass of filter f for item j (output columns 4j .. 4j+3) of a row
+// pair: src = the row-pair row in plane 0; pstride = f32x4 per plane; taps
+// [TLO, THI].
+template <int HALF, int TLO = 0, int THI = 2 * HALF>
+__device__ __forceinline__ void hpass_wide(const f32x4* src, int j, TapsPtr<HALF> taps, int f,
+                                           int plane, int pstride, f32x2 (&acc)[4]) {
+    constexpr int HR = 4, NQ = (HR + 2 * HALF) / 2;  // 12 reads of 2 columns
+    // item j's read q: half q & 1, slot j + q / 2
+    const f32x4* row = src + plane * pstride + j;
+    f32x4 v[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) v[q] = row[(q & 1) * (kWideHalf / 2) + (q >> 1)];
+    f32x2 in[2 * NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        in[2 * q] = v[q].xy;
+        in[2 * q + 1] = v[q].zw;
+    }
+#pragma unroll
+    for (int t = TLO; t <= THI; ++t) {
+        const float k = taps->h[f][t];
+        const f32x2 kk = {k, k};
+#pragma unroll
+        for (int xo = 0; xo < HR; ++xo) acc[xo] = __builtin_elementwise_fma(in[xo + t], kk, acc[xo]);
+    }
+}
+
+// D of one 16x16 stack block of output-row half `half` -> permuted row pairs:
+// lane (c = l & 15, q = l >> 4) holds rows 8 half + 4(q & 1) .. +3 of the
+// stack's filter q >> 1 at column `col`.
+__device__ __forceinline__ void store_vstack16(float* s_v, const f32x4v& d, int plane_a,
+                                               int plane_b, int lk, int col, int half) {
+    constexpr int PAIRS = kTH16 / 2, ROW = 2 * kWideHalf;  // float2 per row-pair row
+    const int plane = lk < 2 ? plane_a : plane_b;
+    if (plane < 0) return;
+    const int p0 = 4 * half + 2 * (lk & 1);
+    f32x2* v = reinterpret_cast<f32x2*>(s_v);
+    const int pos = wide_pos(col);
+    v[(plane * PAIRS + p0) * ROW + pos] = f32x2{d[0], d[1]};
+    v[(plane * PAIRS + p0 + 1) * ROW + pos] = f32x2{d[2], d[3]};
+}
+
+// Region row of B4 slot j: rows 32-35, then rows 36-39 (zero taps) read row 35
+// again (any finite value will do).
+__device__ __forceinline__ constexpr int b4_row(int j) { return j < 4 ? 32 + j : 35; }
+
+template <int DE, bool TRIM>
+__global__ __launch_bounds__(256, 4) void cost16_kernel(CostArgs a, int P_) {
+    constexpr int HALF = 10, RW = 128, TH = kTH16, HR = 4, T2 = 2 * HALF;
+    constexpr int TW = RW - 2 * HALF, RH = TH + 2 * HALF;  // 108 x 16 outputs, 36 region rows
+    constexpr int NRUN = TW / HR;                          // 27 items per row pair, 32 slots
+    constexpr int PAIRS = TH / 2, ROW = 2 * kWideHalf;     // float2 per row-pair row
+    constexpr int PLANE4 = PAIRS * ROW / 2;                // f32x4 per filter plane
+    static_assert(NRUN <= 32 && b4_row(7) < RH, "tile");
+    __shared__ f32x4 s_vq[4 * PLANE4];
+    __shared__ uint32_t s_ox[kMaxK];  // opponent x 2^14 as (hi, lo) f16 pairs: channel 0
+    __shared__ uint2 s_oyz[kMaxK];     // channels 1, 2
+    __shared__ __attribute__((aligned(16))) uint8_t s_idx[RH * RW];
+    __shared__ double s_red[4];
+    float* s_v = reinterpret_cast<float*>(s_vq);
+    const int tid = threadIdx.x;
+    const Geom& g = a.g;
+    const TileItem cur = tile_item<TW, TH>(a, xcd_remap(blockIdx.x, a.ntiles * P_), P_);
+    const TapsPtr<HALF> taps = (TapsPtr<HALF>)(uintptr_t)a.taps;  // H taps x 2^-30
+    const int lane = tid & 63, wv = tid >> 6, lc = lane & 15, lk = lane >> 4;
+    // [trim][half][stack][hi, lo][lane]
+    const uint4* frag = a.vfrag16 + (TRIM ? 2 * 4 * 2 * 64 : 0) + lane;
+    auto F = [&](int half, int st, int hl) { return frag[((half * 4 + st) * 2 + hl) * 64]; };
+
+    TileFill<HALF, RW, TH> fill;
+    fill.issue(a, cur, tid);
+    uint4 A00h = F(0, 0, 0), A00l = F(0, 0, 1), A01h = F(0, 1, 0), A01l = F(0, 1, 1);  // half 0
+    uint4 A10h = F(1, 0, 0), A10l = F(1, 0, 1), A11h = F(1, 1, 0), A11l = F(1, 1, 1);  // half 1
+    // every entry (zeros for tid >= K): zero-weight rows gather arbitrary indices,
+    // and 0 x NaN would be NaN
+    s_ox[tid] = split_f16(fill.ov.x);
+    s_oyz[tid] = make_uint2(split_f16(fill.ov.y), split_f16(fill.ov.z));
+    fill.template commit_idx<RW>(a, s_idx, tid);
+    // H item: row pair m, output columns 4j .. 4j+3
+    const int m = tid >> 5, jr = tid & 31;
+    const bool has_item = jr < NRUN;
+    const int gy0 = cur.y0 + 2 * m, gx0 = cur.x0 + HR * jr;
+    __syncthreads();
+
+    // block bb of wave wv: the 16 columns of parity half bb of columns 32 wv .. +31
+    const int colb = 32 * wv + 4 * (lc >> 1) + (lc & 1);
+    const f32x4* hsrc = &s_vq[(m * ROW) / 2];
+    f32x2 acc0[HR], acc1[HR], acc2[HR];
+#pragma unroll
+    for (int xo = 0; xo < HR; ++xo) acc0[xo] = acc1[xo] = acc2[xo] = f32x2{0.f, 0.f};
+
+    // ---- group 0: channel 0 -> planes 0-2 ----
+    {
+        const f16x8 a00h = __builtin_bit_cast(f16x8, A00h), a00l = __builtin_bit_cast(f16x8, A00l);
+        const f16x8 a01h = __builtin_bit_cast(f16x8, A01h), a01l = __builtin_bit_cast(f16x8, A01l);
+        const f16x8 a10h = __builtin_bit_cast(f16x8, A10h), a10l = __builtin_bit_cast(f16x8, A10l);
+        const f16x8 a11h = __builtin_bit_cast(f16x8, A11h), a11l = __builtin_bit_cast(f16x8, A11l);
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            const int col = colb + 2 * bb;
+            uint32_t w[8], w4[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) w[j] = s_ox[s_idx[(8 * lk + j) * RW + col]];
+            if (lk == 0) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) w4[j] = s_ox[s_idx[b4_row(j) * RW + col]];
+            }
+            f16x8 bh, bl, ch, cl;
+            pack_b(w, bh, bl);
+            ch = bh; cl = bl;
+            if (lk == 0) pack_b(w4, ch, cl);
+            store_vstack16(s_v, mfma3(a00h, a00l, bh, bl), 0, 1, lk, col, 0);
+            store_vstack16(s_v, mfma3(a10h, a10l, ch, cl), 0, 1, lk, col, 1);
+            store_vstack16(s_v, mfma3(a01h, a01l, bh, bl), 2, -1, lk, col, 0);
+            store_vstack16(s_v, mfma3(a11h, a11l, ch, cl), 2, -1, lk, col, 1);
+        }
+    }
+    // group 1 stacks, in flight during the group 0 horizontal pass
+    A00h = F(0, 2, 0); A00l = F(0, 2, 1); A01h = F(0, 3, 0); A01l = F(0, 3, 1);
+    A10h = F(1, 2, 0); A10l = F(1, 2, 1); A11h = F(1, 3, 0); A11l = F(1, 3, 1);
+    __syncthreads();
+    if (has_item) {
+        if constexpr (TRIM) hpass_wide<HALF, kTrimLo[0], kTrimHi[0]>(hsrc, jr, taps, 0, 0, PLANE4, acc0);
+        else hpass_wide<HALF, 0, T2>(hsrc, jr, taps, 0, 0, PLANE4, acc0);
+        hpass_wide<HALF, 0, T2>(hsrc, jr, taps, 1, 1, PLANE4, acc0);
+        hpass_wide<HALF, 0, T2>(hsrc, jr, taps, 2, 2, PLANE4, acc0);
+    }
+    __syncthreads();
+
+    // ---- group 1: channels 1, 2 -> planes 0-3 ----
+    {
+        const f16x8 a02h = __builtin_bit_cast(f16x8, A00h), a02l = __builtin_bit_cast(f16x8, A00l);
+        const f16x8 a03h = __builtin_bit_cast(f16x8, A01h), a03l = __builtin_bit_cast(f16x8, A01l);
+        const f16x8 a12h = __builtin_bit_cast(f16x8, A10h), a12l = __builtin_bit_cast(f16x8, A10l);
+        const f16x8 a13h = __builtin_bit_cast(f16x8, A11h), a13l = __builtin_bit_cast(f16x8, A11l);
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            const int col = colb + 2 * bb;
+            uint32_t wy[8], wy4[8], wz[8], wz4[8];
+            {
+                uint2 e[8], e4[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) e[j] = s_oyz[s_idx[(8 * lk + j) * RW + col]];
+                if (lk == 0) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) e4[j] = s_oyz[s_idx[b4_row(j) * RW + col]];
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) e4[j] = e[j];
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    wy[j] = e[j].x; wz[j] = e[j].y; wy4[j] = e4[j].x; wz4[j] = e4[j].y;
+                }
+            }
+            f16x8 bh, bl, ch, cl;
+            pack_b(wy, bh, bl);
+            pack_b(wy4, ch, cl);
+            store_vstack16(s_v, mfma3(a02h, a02l, bh, bl), 0, 1, lk, col, 0);
+            store_vstack16(s_v, mfma3(a12h, a12l, ch, cl), 0, 1, lk, col, 1);
+            pack_b(wz, bh, bl);
+            pack_b(wz4, ch, cl);
+            store_vstack16(s_v, mfma3(a03h, a03l, bh, bl), 2, 3, lk, col, 0);
+            store_vstack16(s_v, mfma3(a13h, a13l, ch, cl), 2, 3, lk, col, 1);
+        }
+    }
+    // LabRef of the item's 2 x 4 pixels, in flight across the barrier
+    float4 lab[2][3];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const bool ok = has_item && gy0 + r < g.r1 && gx0 < g.W;
+        const uint32_t off = ok ? (uint32_t)((gy0 + r - g.r0) * g.lab_pitch + gx0) : 0u;
+        const float* src3[3] = {a.labL, a.labA, a.labB};
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch)
+            lab[r][ch] = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(src3[ch]) +
+                                                          (off << 2));  // 32-bit byte offset
+    }
+    __syncthreads();
+
+    double sum = 0.0;
+    if (has_item) {
+        if constexpr (TRIM) {
+            hpass_wide<HALF, kTrimLo[1], kTrimHi[1]>(hsrc, jr, taps, 3, 0, PLANE4, acc1);
+            hpass_wide<HALF, 0, T2>(hsrc, jr, taps, 4, 1, PLANE4, acc1);
+            hpass_wide<HALF, kTrimLo[2], kTrimHi[2]>(hsrc, jr, taps, 5, 2, PLANE4, acc2);
+        } else {
+            hpass_wide<HALF, 0, T2>(hsrc, jr, taps, 3, 0, PLANE4, acc1);
+            hpass_wide<HALF, 0, T2>(hsrc, jr, taps, 4, 1, PLANE4, acc1);
+            hpass_wide<HALF, 0, T2>(hsrc, jr, taps, 5, 2, PLANE4, acc2);
+        }
+        hpass_wide<HALF, 0, T2>(hsrc, jr, taps, 6, 3, PLANE4, acc2);
+        float part = 0.f;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const float Ls[4] = {lab[r][0].x, lab[r][0].y, lab[r][0].z, lab[r][0].w};
+            const float As[4] = {lab[r][1].x, lab[r][1].y, lab[r][1].z, lab[r][1].w};
+            const float Bs[4] = {lab[r][2].x, lab[r][2].y, lab[r][2].z, lab[r][2].w};
+#pragma unroll
+            for (int xo = 0; xo < HR; ++xo) {
+                const float3 l3 = opp2lab_fast(acc0[xo][r], acc1[xo][r], acc2[xo][r], a.m_lab);
+                const float e = delta_e<DE>(Ls[xo], As[xo], Bs[xo], l3.x, l3.y, l3.z);
                 part += (gy0 + r < g.r1 && gx0 + xo < g.W) ? e : 0.f;
             }
         }
@@ -496,13 +739,17 @@ static float host_f16_to_f32(uint16_t h) {
     return (h & 0x8000u) ? -v : v;
 }
 
-// cost_tile 7: split-f16 A fragments of v_mfma_f32_16x16x32_f16 for the vertical
-// pass, [trim][stack][hi, lo][lane] x 8 halves (trim 0 = all 21 taps, 1 = the
-// narrow filters' significant windows).  Lane l holds A[i = l & 15][k = 8(l >> 4)
-// + j]: the tap (x 2^16) of filter stack[i >> 3] that multiplies region row k
-// into output row i & 7, i.e. tap d = k - (i & 7), zero outside [0, 20] (and
-// outside the window).
-size_t vpass_f16_stack_fragment_halves() { return 2 * 4 * 2 * 64 * 8; }
+// Split-f16 A fragments of v_mfma_f32_16x16x32_f16 for the vertical pass,
+// [trim][half][stack][hi, lo][lane] x 8 halves (trim 0 = all 21 taps, 1 = the
+// narrow filters' significant windows).  Lane l holds A[i = l & 15][k = 8g + j],
+// g = l >> 4: the tap (x 2^16) of filter stack[i >> 3] that multiplies the
+// region row held in K slot k into output row 8 half + (i & 7), i.e. tap
+// d = row - 8 half - (i & 7), zero outside [0, 20] (and outside the window).
+// Half 0 (output rows 0-7) holds region rows 8g + j; half 1 (output rows 8-15
+// of a 16-row tile) reuses lane groups 1-3's rows 8-31 and gives lane group 0
+// rows 32-39, so its B operand costs one 8-row gather (by 16 lanes) instead of
+// four.
+size_t vpass_f16_stack_fragment_halves() { return 2 * 2 * 4 * 2 * 64 * 8; }
 
 void build_vpass_f16_stack_fragments(const float* k1, const float* k2, const float* k3,
                                      const float* absk3, uint16_t* out) {
@@ -510,11 +757,13 @@ void build_vpass_f16_stack_fragments(const float* k1, const float* k2, const flo
     make_taps10(k1, k2, k3, absk3, t);
     const int stack[4][2] = {{0, 1}, {2, -1}, {3, 4}, {5, 6}};
     for (int trim = 0; trim < 2; ++trim)
+        for (int half = 0; half < 2; ++half)
         for (int st = 0; st < 4; ++st)
             for (int l = 0; l < 64; ++l)
                 for (int j = 0; j < 8; ++j) {
-                    const int i = l & 15, k = 8 * (l >> 4) + j, r = i & 7, f = stack[st][i >> 3];
-                    const int d = k - r;
+                    const int i = l & 15, g = l >> 4, r = i & 7, f = stack[st][i >> 3];
+                    const int row = (half == 1 && g == 0) ? 32 + j : 8 * g + j;
+                    const int d = row - 8 * half - r;
                     float w = 0.f;
                     if (f >= 0 && d >= 0 && d <= 20) {
                         w = t.v[f][d];
@@ -524,8 +773,8 @@ void build_vpass_f16_stack_fragments(const float* k1, const float* k2, const flo
                     w *= kVTapScale;
                     const uint16_t hi = host_f16(w);
                     const uint16_t lo = host_f16(w - host_f16_to_f32(hi));
-                    out[(((trim * 4 + st) * 2 + 0) * 64 + l) * 8 + j] = hi;
-                    out[(((trim * 4 + st) * 2 + 1) * 64 + l) * 8 + j] = lo;
+                    out[((((trim * 2 + half) * 4 + st) * 2 + 0) * 64 + l) * 8 + j] = hi;
+                    out[((((trim * 2 + half) * 4 + st) * 2 + 1) * 64 + l) * 8 + j] = lo;
                 }
 }
 
@@ -557,23 +806,28 @@ void build_fast_taps(const float* k1, const float* k2, const float* k3, const fl
 
 // a.taps = the two CostTaps<10> of build_fast_taps
 
-int fast_tile_rows() { return kFastTH; }
-
-void fast_tile_dims(int W, int own_rows, int* tiles_x, int* ntiles) {
+// tile_rows: 8 (cost_mfma_kernel) or 16 (cost16_kernel)
+void fast_tile_dims(int W, int own_rows, int tile_rows, int* tiles_x, int* ntiles) {
     *tiles_x = (W + kFastTW - 1) / kFastTW;
-    *ntiles = *tiles_x * ((own_rows + kFastTH - 1) / kFastTH);
+    *ntiles = *tiles_x * ((own_rows + tile_rows - 1) / tile_rows);
 }
 
 // a.taps = the two CostTaps<10> of build_fast_taps; [1] carries the vertical
 // pass's 2^30 scale in its horizontal taps.
-hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, bool trim, hipStream_t s) {
+hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, bool trim, int tile_rows,
+                            hipStream_t s) {
     CostArgs a = a0;
     a.taps = static_cast<const char*>(a0.taps) + sizeof(CostTaps<10>);
     const dim3 grid((unsigned)(a.ntiles * P));
-#define HQ_MFMA(DEV, TR) HQ_LAUNCH((cost_mfma_kernel<DEV, TR>), grid, dim3(256), 0, s, a, P)
-    if (de == 0) { if (trim) HQ_MFMA(0, true); else HQ_MFMA(0, false); }
-    else { if (trim) HQ_MFMA(1, true); else HQ_MFMA(1, false); }
-#undef HQ_MFMA
+#define HQ_COST(KN, DEV, TR) HQ_LAUNCH((KN<DEV, TR>), grid, dim3(256), 0, s, a, P)
+    if (tile_rows == kTH16) {
+        if (de == 0) { if (trim) HQ_COST(cost16_kernel, 0, true); else HQ_COST(cost16_kernel, 0, false); }
+        else { if (trim) HQ_COST(cost16_kernel, 1, true); else HQ_COST(cost16_kernel, 1, false); }
+    } else {
+        if (de == 0) { if (trim) HQ_COST(cost_mfma_kernel, 0, true); else HQ_COST(cost_mfma_kernel, 0, false); }
+        else { if (trim) HQ_COST(cost_mfma_kernel, 1, true); else HQ_COST(cost_mfma_kernel, 1, false); }
+    }
+#undef HQ_COST
     return hipGetLastError();
 }
 

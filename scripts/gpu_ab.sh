@@ -1,15 +1,16 @@
-# A/B of two library builds on one box: ab/libhq_old.so vs ab/libhq_new.so, alternated
-# $REPS times, bench.py with $BENCH_ARGS (HQ_LIB_PATH selects the library).
+# Same-box A/B of bench variants: each line of $VARIANTS (';'-separated option lists,
+# e.g. "cost_rows=8;cost_rows=16") runs bench.py twice, alternating; one JSON per run.
 set -u
-export TMPDIR=/tmp
 mkdir -p gpurun_out/ab
-for i in $(seq 1 ${REPS:-3}); do
-  for v in old new; do
-    HQ_LIB_PATH=ab/libhq_$v.so timeout -k 10 300 python bench.py --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/ab/$v$i.json 2> gpurun_out/ab/$v$i.err
+i=0
+for rep in 1 2; do
+  IFS=';' read -ra VS <<< "$VARIANTS"
+  for v in "${VS[@]}"; do
+    i=$((i+1)); opts=""
+    for kv in $v; do opts="$opts --opt $kv"; done
+    timeout -k 10 300 python bench.py --no-cpu-baseline --no-full-search --steps ${STEPS:-100} $opts ${BENCH_ARGS:-} > gpurun_out/ab/run$i.json 2> gpurun_out/ab/run$i.err
     rc=$?
-    if [ $rc -ne 0 ]; then echo "$v$i rc=$rc"; tail -3 gpurun_out/ab/$v$i.err; exit $rc; fi
-    python3 -c "
-import json;d=json.loads(open('gpurun_out/ab/$v$i.json').read().strip().splitlines()[-1])
-print('$v', d['ms_per_step'], d['kernel_avg_ms'])"
+    python3 -c "import json,sys; d=json.load(open('gpurun_out/ab/run$i.json')); print('$v', d['value'], d['ms_per_step'], d['kernel_avg_ms'])" || { echo "rc=$rc"; tail -5 gpurun_out/ab/run$i.err; }
+    if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then exit $rc; fi
   done
 done

@@ -1,6 +1,6 @@
 """Profiling driver: repeated population evaluations at a given size (for rocprofv3).
 
-python scripts/profile_eval.py [--size 4096] [--K 256] [--P 4] [--evals 10] [--grid 64]
+python scripts/profile_eval.py [--size 4096] [--K 256] [--P 4] [--evals 10] [--opt NAME=VALUE ...]
 Prints per-kernel HIP-event averages and the end-to-end eval time.
 """
 
@@ -26,16 +26,8 @@ def main():
     ap.add_argument("--K", type=int, default=256)
     ap.add_argument("--P", type=int, default=4)
     ap.add_argument("--evals", type=int, default=10)
-    ap.add_argument("--grid", type=int, default=32)
-    ap.add_argument("--variant", type=int, default=0)
-    ap.add_argument("--tile", type=int, default=7)
-    ap.add_argument("--rep", type=int, default=1)
-    ap.add_argument("--trim", type=int, default=1)
-    ap.add_argument("--group", type=int, default=4)
-    ap.add_argument("--batch", type=int, default=3)
-    ap.add_argument("--bpc", type=int, default=0, help="assign workgroups per CU (0 = library default)")
-    ap.add_argument("--bands", type=int, default=-1, help="banded assign/cost pipeline (-1 = library default)")
-    ap.add_argument("--cpb", type=int, default=0, help="banded assign: chunks per block (0 = default)")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="libhq option (include/hq.h hq_set_option), repeatable")
     ap.add_argument("--rows", type=int, default=0,
                     help="evaluate only the row shard [0, rows) of the image (an N-GPU rank's share)")
     ap.add_argument("--lib", default=None, help="alternative libhq build (scripts/ablate.py)")
@@ -45,19 +37,9 @@ def main():
     lib = hq.load()
     m = hq.ImageManipulation(device=0)
     sp = hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
-    m.setOption("grid", args.grid)
-    m.setOption("cost_variant", args.variant)
-    m.setOption("cost_tile", args.tile)
-    m.setOption("assign_rep", args.rep)
-    m.setOption("trim", args.trim)
-    m.setOption("assign_group", args.group)
-    m.setOption("assign_batch", args.batch)
-    if args.bpc:
-        m.setOption("assign_blocks_per_cu", args.bpc)
-    if args.bands >= 0:
-        m.setOption("bands", args.bands)
-    if args.cpb:
-        m.setOption("band_cpb", args.cpb)
+    for kv in args.opt:
+        k, v = kv.split("=", 1)
+        m.setOption(k, int(v))
     W = H = args.size
     R, G, B = synthetic_planes(W, H, 1)
     rows = args.rows or H
@@ -93,7 +75,7 @@ def main():
         n = C.c_int64()
         lib.hq_profile_get(m.ctx, k.encode(), C.byref(ms), C.byref(n))
         out.append(f"{k}={ms.value / max(n.value, 1):.4f}ms")
-    print(f"{os.path.basename(args.lib or 'libhq.so')} size={W} K={args.K} P={args.P} grid={args.grid} variant={args.variant} tile={args.tile} rep={args.rep} trim={args.trim} group={args.group} batch={args.batch} bpc={args.bpc} bands={args.bands} cpb={args.cpb}: "
+    print(f"{os.path.basename(args.lib or 'libhq.so')} size={W} K={args.K} P={args.P} opts={args.opt}: "
           f"{el / args.evals * 1e3:.3f} ms/eval-population, "
           f"{W * rows * args.P * args.evals / el / 1e6:.1f} Mpx*evals/s (rows {rows})  ", " ".join(out),
           "costs", costs.tolist())

@@ -74,16 +74,19 @@ def test_labref_256_checksum(ip):
 # Candidate evaluation (IM:620-727): golden fixtures
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("grid", [64, 32, 16, 0])
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [(0, 16), (0, 8), (1, 16)])
 @pytest.mark.parametrize("name", ["case_64x48_k16", "case_97x53_k64"])
 def test_eval_golden(ip, name, grid, variant):
-    """cost_variant 0 = the fast tiled path (vertical passes on the matrix cores in
-    split f16, horizontal pass on VALU), 1 = the generic two-pass path; argmin
-    through candidate grids of 64^3, 32^3, 16^3 cells or exhaustive."""
+    """(cost_variant, cost_rows): 0 = the fast tiled path (vertical passes on the
+    matrix cores in split f16, horizontal pass on VALU) on 16-row tiles
+    (cost16_kernel, default) or 8-row tiles (cost_mfma_kernel), 1 = the generic
+    two-pass path; argmin through candidate grids of 64^3, 32^3, 16^3 cells or
+    exhaustive."""
     g, R, G, B = load_case(name)
     w = int(g["w"])
     ip.setOption("grid", grid)
-    ip.setOption("cost_variant", variant)
+    ip.setOption("cost_variant", variant[0])
+    ip.setOption("cost_rows", variant[1])
     ip.setImage(o.inline_rgba(R, G, B).reshape(-1), g["lab"].reshape(-1), w, ip.illum)
     pals = g["palettes"]
     costs, used = ip.computeQuantizationErrorPopulation(pals.reshape(len(pals), -1), 2.0,
@@ -119,20 +122,22 @@ def test_eval_config2_1024_k64(ip, filt):
     assert abs(cost - ref) <= COST_RTOL * abs(ref) * 0.1
 
 
+@pytest.mark.parametrize("rows", [16, 8])
 @pytest.mark.parametrize("de", [hq.deltaETypes.CIE76, hq.deltaETypes.CIE94])
 @pytest.mark.parametrize("trim", [1, 0])
-def test_fast_path_matches_generic(gpu, de, trim):
+def test_fast_path_matches_generic(gpu, de, trim, rows):
     """The fast path (split-f16 vertical products, hi.hi + hi.lo + lo.hi with ~2^-22
     relative per product dropped; trimmed narrow filters) agrees with the generic
     fp32 two-pass path to 1e-6 relative (the bar is 1e-4) on interior, edge and
     partial tiles."""
-    w, h = 300, 77
+    w, h = 300, 77 if rows == 8 else 93
     R, G, B = o.synthetic_image(w, h, seed=5)
     m = hq.ImageManipulation(de, device=gpu)
     sp = hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
     m.setImage(o.inline_rgba(R, G, B).reshape(-1), None, w, sp.illuminant)
     pals = [o.synthetic_palette(K, 7 + K) for K in (16, 64, 256)]
     m.setOption("trim", trim)
+    m.setOption("cost_rows", rows)
     out = {}
     for variant in (0, 1):
         m.setOption("cost_variant", variant)
@@ -441,6 +446,10 @@ def test_full_size_properties(gpu, filt):
     np.testing.assert_array_equal(m.getIndices(1), idx1)  # pruned == exhaustive argmin
     np.testing.assert_array_equal(c3, c1)
     m.setOption("grid", 64)
+    m.setOption("cost_rows", 8)
+    c8 = m.computeQuantizationErrorPopulation(pals, 2.0)
+    np.testing.assert_allclose(c8, c1, rtol=1e-6)  # 8-row tiles == 16-row tiles
+    m.setOption("cost_rows", 16)
     m.setOption("cost_variant", 1)
     c4 = m.computeQuantizationErrorPopulation(pals, 2.0)
     np.testing.assert_allclose(c4, c1, rtol=1e-6)  # generic two-pass == fast path
