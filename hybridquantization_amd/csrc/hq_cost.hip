@@ -57,6 +57,16 @@ constexpr float kVDataScale = 16384.0f;                   // 2^14
 constexpr float kVTapScale = 65536.0f;                    // 2^16
 constexpr float kVOutScale = 1.0f / (16384.0f * 65536.0f);  // 2^-30
 
+// Region row of K slot (g = lane >> 4, j) of the vertical pass's B operand.
+// Half 0 (output rows 0-7): rows 4j + g (lane group g holds every 4th row).
+// Half 1 (output rows 8-15 of a 16-row tile, rows 8-39): slots 0-5 are half
+// 0's slots 2-7 (rows 8 + 4j + g), slots 6 and 7 are rows 32 + g and 36 + g
+// (rows 36-39 carry zero taps), so every lane gathers 2 new values for half 1
+// (no divergent block gather).  The A fragments permute K to match.
+__host__ __device__ __forceinline__ constexpr int kv_row(int half, int g, int j) {
+    return half == 0 ? 4 * j + g : (j < 6 ? 4 * j + 8 + g : (j == 6 ? 32 + g : 36 + g));
+}
+
 // (hi, lo) f16 split of x * 2^14 in one dword, hi in bits 0-15.
 __device__ __forceinline__ uint32_t split_f16(float x) {
     const float xs = x * kVDataScale;
@@ -305,7 +315,7 @@ __global__ __launch_bounds__(256, 6) void cost_mfma_kernel(CostArgs a, int P_) {
         for (int bb = 0; bb < 2; ++bb) {
             uint32_t w[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) w[j] = s_ox[s_idx[(8 * lk + j) * RW + col0 + 16 * bb]];
+            for (int j = 0; j < 8; ++j) w[j] = s_ox[s_idx[kv_row(0, lk, j) * RW + col0 + 16 * bb]];
             f16x8 bh, bl;
             pack_b(w, bh, bl);
             store_vstack(s_v, mfma3(a0h, a0l, bh, bl), 0, 1, lk, col0 + 16 * bb);
@@ -334,7 +344,7 @@ __global__ __launch_bounds__(256, 6) void cost_mfma_kernel(CostArgs a, int P_) {
             uint32_t wy[8], wz[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const uint2 e = s_oyz[s_idx[(8 * lk + j) * RW + col0 + 16 * bb]];
+                const uint2 e = s_oyz[s_idx[kv_row(0, lk, j) * RW + col0 + 16 * bb]];
                 wy[j] = e.x; wz[j] = e.y;
             }
             f16x8 bh, bl;
@@ -375,9 +385,8 @@ __global__ __launch_bounds__(256, 6) void cost_mfma_kernel(CostArgs a, int P_) {
         for (int r = 0; r < 2; ++r) {
 #pragma unroll
             for (int xo = 0; xo < HR; ++xo) {
-                const float3 l3 = opp2lab_fast(acc0[xo][r], acc1[xo][r], acc2[xo][r], a.m_lab);
-                const float e = delta_e<DE>(labv[r][0][xo], labv[r][1][xo], labv[r][2][xo], l3.x,
-                                            l3.y, l3.z);
+                const float3 g3 = opp2g_fast(acc0[xo][r], acc1[xo][r], acc2[xo][r], a.m_lab);
+                const float e = delta_e_g<DE>(labv[r][0][xo], labv[r][1][xo], labv[r][2][xo], g3);
                 part += (gy0 + r < g.r1 && gx0 + xo < g.W) ? e : 0.f;
             }
         }
@@ -395,10 +404,10 @@ __global__ __launch_bounds__(256, 6) void cost_mfma_kernel(CostArgs a, int P_) {
 // pass and the horizontal windows are the kernel's LDS traffic, and LDS
 // bounds cost_mfma (PMC: ~77% of cycles LDS-active, a quarter of that in bank
 // conflicts of the random gathers).  A 16 x 108 tile needs a 36-row region:
-// - vertical pass: output rows 0-7 take region rows 0-31 (B0-B3, one 8-row
-//   block per lane group), rows 8-15 take rows 8-39 -- lane groups 1-3 keep
-//   B1-B3 and only lane group 0 gathers B4 = rows 32-39 (the half-1 A
-//   fragments permute K to match): 5 gathered blocks per 16 rows instead of 8;
+// - vertical pass: output rows 0-7 take region rows 0-31, rows 8-15 take rows
+//   8-39 (36-39 zero-weight): with lane group g holding every 4th row (kv_row),
+//   each lane keeps six of its eight half-0 values for half 1 and gathers two
+//   more -- 40 gathered rows per 16 output rows instead of 64, no divergence;
 // - horizontal pass: items of 4 output columns x a row pair (216 items, one per
 //   thread of 8 row pairs x 32 slots), a 24-column window = 12 ds_read_b128
 //   per filter for 8 outputs (cost_mfma: 11 for 4).  Row-pair rows store their
@@ -461,9 +470,11 @@ __device__ __forceinline__ void store_vstack16(float* s_v, const f32x4v& d, int 
     v[(plane * PAIRS + p0 + 1) * ROW + pos] = f32x2{d[2], d[3]};
 }
 
-// Region row of B4 slot j: rows 32-35, then rows 36-39 (zero taps) read row 35
-// again (any finite value will do).
-__device__ __forceinline__ constexpr int b4_row(int j) { return j < 4 ? 32 + j : 35; }
+// Index row of K slot (half 1, g, 7): rows 36-39 carry zero taps and are not in
+// the region: row 35 again (any finite value will do).
+__device__ __forceinline__ constexpr int kv_row_clamped(int half, int g, int j) {
+    return kv_row(half, g, j) < 36 ? kv_row(half, g, j) : 35;
+}
 
 template <int DE, bool TRIM>
 __global__ __launch_bounds__(256, 4) void cost16_kernel(CostArgs a, int P_) {
@@ -472,7 +483,7 @@ __global__ __launch_bounds__(256, 4) void cost16_kernel(CostArgs a, int P_) {
     constexpr int NRUN = TW / HR;                          // 27 items per row pair, 32 slots
     constexpr int PAIRS = TH / 2, ROW = 2 * kWideHalf;     // float2 per row-pair row
     constexpr int PLANE4 = PAIRS * ROW / 2;                // f32x4 per filter plane
-    static_assert(NRUN <= 32 && b4_row(7) < RH, "tile");
+    static_assert(NRUN <= 32 && kv_row(1, 3, 6) < RH, "tile");
     __shared__ f32x4 s_vq[4 * PLANE4];
     __shared__ uint32_t s_ox[kMaxK];  // opponent x 2^14 as (hi, lo) f16 pairs: channel 0
     __shared__ uint2 s_oyz[kMaxK];     // channels 1, 2
@@ -519,17 +530,15 @@ __global__ __launch_bounds__(256, 4) void cost16_kernel(CostArgs a, int P_) {
 #pragma unroll
         for (int bb = 0; bb < 2; ++bb) {
             const int col = colb + 2 * bb;
-            uint32_t w[8], w4[8];
+            // slots 0-7: half 0; slots 2-9: half 1 (kv_row)
+            uint32_t w[10];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) w[j] = s_ox[s_idx[(8 * lk + j) * RW + col]];
-            if (lk == 0) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) w4[j] = s_ox[s_idx[b4_row(j) * RW + col]];
-            }
+            for (int j = 0; j < 8; ++j) w[j] = s_ox[s_idx[kv_row(0, lk, j) * RW + col]];
+            w[8] = s_ox[s_idx[kv_row_clamped(1, lk, 6) * RW + col]];
+            w[9] = s_ox[s_idx[kv_row_clamped(1, lk, 7) * RW + col]];
             f16x8 bh, bl, ch, cl;
-            pack_b(w, bh, bl);
-            ch = bh; cl = bl;
-            if (lk == 0) pack_b(w4, ch, cl);
+            pack_b(*reinterpret_cast<const uint32_t(*)[8]>(&w[0]), bh, bl);
+            pack_b(*reinterpret_cast<const uint32_t(*)[8]>(&w[2]), ch, cl);
             store_vstack16(s_v, mfma3(a00h, a00l, bh, bl), 0, 1, lk, col, 0);
             store_vstack16(s_v, mfma3(a10h, a10l, ch, cl), 0, 1, lk, col, 1);
             store_vstack16(s_v, mfma3(a01h, a01l, bh, bl), 2, -1, lk, col, 0);
@@ -557,30 +566,20 @@ __global__ __launch_bounds__(256, 4) void cost16_kernel(CostArgs a, int P_) {
 #pragma unroll
         for (int bb = 0; bb < 2; ++bb) {
             const int col = colb + 2 * bb;
-            uint32_t wy[8], wy4[8], wz[8], wz4[8];
-            {
-                uint2 e[8], e4[8];
+            uint32_t wy[10], wz[10];  // slots 0-7: half 0; slots 2-9: half 1 (kv_row)
 #pragma unroll
-                for (int j = 0; j < 8; ++j) e[j] = s_oyz[s_idx[(8 * lk + j) * RW + col]];
-                if (lk == 0) {
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) e4[j] = s_oyz[s_idx[b4_row(j) * RW + col]];
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) e4[j] = e[j];
-                }
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    wy[j] = e[j].x; wz[j] = e[j].y; wy4[j] = e4[j].x; wz4[j] = e4[j].y;
-                }
+            for (int j = 0; j < 10; ++j) {
+                const int row = j < 8 ? kv_row(0, lk, j) : kv_row_clamped(1, lk, j - 2);
+                const uint2 e = s_oyz[s_idx[row * RW + col]];
+                wy[j] = e.x; wz[j] = e.y;
             }
             f16x8 bh, bl, ch, cl;
-            pack_b(wy, bh, bl);
-            pack_b(wy4, ch, cl);
+            pack_b(*reinterpret_cast<const uint32_t(*)[8]>(&wy[0]), bh, bl);
+            pack_b(*reinterpret_cast<const uint32_t(*)[8]>(&wy[2]), ch, cl);
             store_vstack16(s_v, mfma3(a02h, a02l, bh, bl), 0, 1, lk, col, 0);
             store_vstack16(s_v, mfma3(a12h, a12l, ch, cl), 0, 1, lk, col, 1);
-            pack_b(wz, bh, bl);
-            pack_b(wz4, ch, cl);
+            pack_b(*reinterpret_cast<const uint32_t(*)[8]>(&wz[0]), bh, bl);
+            pack_b(*reinterpret_cast<const uint32_t(*)[8]>(&wz[2]), ch, cl);
             store_vstack16(s_v, mfma3(a03h, a03l, bh, bl), 2, 3, lk, col, 0);
             store_vstack16(s_v, mfma3(a13h, a13l, ch, cl), 2, 3, lk, col, 1);
         }
@@ -619,8 +618,8 @@ __global__ __launch_bounds__(256, 4) void cost16_kernel(CostArgs a, int P_) {
             const float Bs[4] = {lab[r][2].x, lab[r][2].y, lab[r][2].z, lab[r][2].w};
 #pragma unroll
             for (int xo = 0; xo < HR; ++xo) {
-                const float3 l3 = opp2lab_fast(acc0[xo][r], acc1[xo][r], acc2[xo][r], a.m_lab);
-                const float e = delta_e<DE>(Ls[xo], As[xo], Bs[xo], l3.x, l3.y, l3.z);
+                const float3 g3 = opp2g_fast(acc0[xo][r], acc1[xo][r], acc2[xo][r], a.m_lab);
+                const float e = delta_e_g<DE>(Ls[xo], As[xo], Bs[xo], g3);
                 part += (gy0 + r < g.r1 && gx0 + xo < g.W) ? e : 0.f;
             }
         }
@@ -679,9 +678,9 @@ __global__ __launch_bounds__(256) void gen_vpass_kernel(GenArgs a) {
             oz = fmaf(a.t[2 * n + s], a.k1[4 * t + 2], fmaf(a.t[5 * n + s], a.k2[4 * t + 2], oz));
             ox = fmaf(a.t[6 * n + s], a.absk3[t], ox);
         }
-        const float3 lab = opp2lab_fast(ox, oy, oz, a.m_lab);
+        const float3 g3 = opp2g_fast(ox, oy, oz, a.m_lab);
         const int64_t off = (int64_t)(y - a.g.r0) * a.g.lab_pitch + x;
-        e = (double)delta_e<DE>(a.labL[off], a.labA[off], a.labB[off], lab.x, lab.y, lab.z);
+        e = (double)delta_e_g<DE>(a.labL[off], a.labA[off], a.labB[off], g3);
     }
     e = wave_sum(e);
     if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = e;
@@ -692,9 +691,11 @@ __global__ __launch_bounds__(256) void gen_vpass_kernel(GenArgs a) {
 // ----------------------------------------------------------------------------
 // Host side: tap tables, MFMA fragments, launchers
 // ----------------------------------------------------------------------------
+// Opp->XYZ (CL:118) with row r divided by the illuminant's component r and
+// scaled by 116^3 (lab_g_fast works on t' = 116^3 t).
 void opp2xyz_over_illum(const float inv_illum[3], float m[9]) {
     static const float opp2xyz[9] = HQ_OPP2XYZ;
-    for (int i = 0; i < 9; ++i) m[i] = opp2xyz[i] * inv_illum[i / 3];
+    for (int i = 0; i < 9; ++i) m[i] = (float)((double)opp2xyz[i] * inv_illum[i / 3] * 1560896.0);
 }
 
 static void make_taps10(const float* k1, const float* k2, const float* k3, const float* absk3,
@@ -745,10 +746,9 @@ static float host_f16_to_f32(uint16_t h) {
 // g = l >> 4: the tap (x 2^16) of filter stack[i >> 3] that multiplies the
 // region row held in K slot k into output row 8 half + (i & 7), i.e. tap
 // d = row - 8 half - (i & 7), zero outside [0, 20] (and outside the window).
-// Half 0 (output rows 0-7) holds region rows 8g + j; half 1 (output rows 8-15
-// of a 16-row tile) reuses lane groups 1-3's rows 8-31 and gives lane group 0
-// rows 32-39, so its B operand costs one 8-row gather (by 16 lanes) instead of
-// four.
+// The region row of K slot (g, j) is kv_row(half, g, j): half 1 (output rows
+// 8-15 of a 16-row tile) reuses six of half 0's slots per lane, so its B
+// operand costs two gathered values per lane instead of eight.
 size_t vpass_f16_stack_fragment_halves() { return 2 * 2 * 4 * 2 * 64 * 8; }
 
 void build_vpass_f16_stack_fragments(const float* k1, const float* k2, const float* k3,
@@ -762,7 +762,7 @@ void build_vpass_f16_stack_fragments(const float* k1, const float* k2, const flo
             for (int l = 0; l < 64; ++l)
                 for (int j = 0; j < 8; ++j) {
                     const int i = l & 15, g = l >> 4, r = i & 7, f = stack[st][i >> 3];
-                    const int row = (half == 1 && g == 0) ? 32 + j : 8 * g + j;
+                    const int row = kv_row(half, g, j);
                     const int d = row - 8 * half - r;
                     float w = 0.f;
                     if (f >= 0 && d >= 0 && d <= 20) {

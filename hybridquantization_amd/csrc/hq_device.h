@@ -40,24 +40,26 @@ __device__ __forceinline__ float lab_f(float t) {  // CL:137
     return t > LAB_DELTA3 ? cbrtf(t) : fmaf(LAB_KAPPA, t, 16.0f) * (1.0f / 116.0f);
 }
 
-// Branch-free f(t) of CL:137 for the hot path: cube root as exp2(log2(t)/3)
-// (v_log_f32 / v_exp_f32, about 3 ulp; no Newton step -- the cost tolerance is
-// 1e-4 relative and this moves the mean dE by ~1e-7), linear segment selected.
-__device__ __forceinline__ float lab_f_fast(float t) {
-    const float tc = fmaxf(t, LAB_DELTA3);  // cbrt branch only used for t > delta^3 > 0
+// The hot path's Opp->Lab (CL:124-145) works on t' = 116^3 t: m = Opp->XYZ with
+// row r divided by the illuminant's component r and multiplied by 116^3
+// (opp2xyz_over_illum), so g(t') = 116 f(t) needs no scaling of its own:
+// cube root as exp2(log2(t')/3) (v_log_f32 / v_exp_f32, about 3 ulp; no Newton
+// step -- the cost tolerance is 1e-4 relative and this moves the mean dE by
+// ~1e-7), the linear segment fma(kappa / 116^3, t', 16), selected branch-free.
+#define LAB_G3 1560896.0f  // 116^3
+__device__ __forceinline__ float lab_g_fast(float t) {
+    constexpr float thr = LAB_DELTA3 * LAB_G3;  // t > delta^3 <=> t' > delta^3 116^3
+    const float tc = fmaxf(t, thr);             // cbrt branch only used for t' > thr > 0
     const float y = __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(tc) * (1.0f / 3.0f));
-    const float lin = fmaf(LAB_KAPPA, t, 16.0f) * (1.0f / 116.0f);
-    return t > LAB_DELTA3 ? y : lin;
+    const float lin = fmaf(LAB_KAPPA / LAB_G3, t, 16.0f);
+    return t > thr ? y : lin;
 }
 
-// CL:124-145 Opp2LAB for the hot path: m = Opp->XYZ with row r divided by the
-// illuminant's component r (opp2xyz_over_illum), so X/Xn etc. come out of the
-// 3x3 product directly.
-__device__ __forceinline__ float3 opp2lab_fast(float o0, float o1, float o2, const float* m) {
-    const float fx = lab_f_fast(dot3(o0, o1, o2, m + 0));
-    const float fy = lab_f_fast(dot3(o0, o1, o2, m + 3));
-    const float fz = lab_f_fast(dot3(o0, o1, o2, m + 6));
-    return make_float3(116.0f * fy - 16.0f, 500.0f * (fx - fy), 200.0f * (fy - fz));
+// 116 (f(X/Xn), f(Y/Yn), f(Z/Zn)) of an opponent colour: L = g.y - 16,
+// a = (500/116)(g.x - g.y), b = (200/116)(g.y - g.z).
+__device__ __forceinline__ float3 opp2g_fast(float o0, float o1, float o2, const float* m) {
+    return make_float3(lab_g_fast(dot3(o0, o1, o2, m + 0)), lab_g_fast(dot3(o0, o1, o2, m + 3)),
+                       lab_g_fast(dot3(o0, o1, o2, m + 6)));
 }
 
 // CL:124-145 with true division (setup paths: LabRef, quantize/error image).
@@ -89,6 +91,21 @@ __device__ __forceinline__ float delta_e(float L1, float a1, float b1, float L2,
         const float dH = hw_sqrt(fmaf(da, da, db * db) - dC * dC);
         const float sc = 1.0f + 0.045f * c1, sh = 1.0f + 0.015f * c1;
         return hw_sqrt(fmaf(dL, dL, fmaf(dC / sc, dC / sc, (dH / sh) * (dH / sh))));
+    }
+}
+
+// dE (CL:201-226) between a reference Lab and the Lab of g = opp2g_fast(...):
+// for dE76 the 500/116 and 200/116 scalings fold into one fma per channel.
+template <int DE>
+__device__ __forceinline__ float delta_e_g(float Lr, float Ar, float Br, float3 g) {
+    if constexpr (DE == 0) {
+        const float dl = (Lr + 16.0f) - g.y;
+        const float da = fmaf(-500.0f / 116.0f, g.x - g.y, Ar);
+        const float db = fmaf(-200.0f / 116.0f, g.y - g.z, Br);
+        return hw_sqrt((dl * dl + da * da) + db * db);
+    } else {
+        return delta_e<DE>(Lr, Ar, Br, g.y - 16.0f, (500.0f / 116.0f) * (g.x - g.y),
+                           (200.0f / 116.0f) * (g.y - g.z));
     }
 }
 

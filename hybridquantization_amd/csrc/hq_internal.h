@@ -121,7 +121,7 @@ struct CostArgs {
     int K;
     int tiles_x;
     int ntiles;      // tiles of the shard (partial pitch per palette)
-    float m_lab[9];  // Opp->XYZ rows divided by the illuminant (CL:124-131), opp2xyz_over_illum()
+    float m_lab[9];  // Opp->XYZ rows / illuminant x 116^3 (CL:124-131), opp2xyz_over_illum()
 };
 
 struct FinalizeArgs {
@@ -148,7 +148,7 @@ struct GenArgs {
     double* partial;         // [nblocks]
     Geom g;
     int half;
-    float m_lab[9];  // Opp->XYZ rows divided by the illuminant (CL:124-131), opp2xyz_over_illum()
+    float m_lab[9];  // Opp->XYZ rows / illuminant x 116^3 (CL:124-131), opp2xyz_over_illum()
 };
 
 }  // namespace hq
