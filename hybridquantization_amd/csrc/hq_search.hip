@@ -344,16 +344,25 @@ __global__ __launch_bounds__(1024) void sa_step_kernel(SaArgs a) {
 // the child's T is attained inside it, so level 2 needs only the parent list.
 // Entries: byte0 = count (255 = overflow), then ascending indices.
 // ----------------------------------------------------------------------------
-__device__ __forceinline__ double ax_min2(double c, double lo, double hi) {
-    const double d = fmax(fmax(lo - c, c - hi), 0.0);
+// Box bounds in fp32.  Box edges are multiples of 1/G (G a power of two):
+// exact.  Valid colours are finite (prep_palette routes non-finite palettes to
+// the exhaustive path), so every term is a correctly rounded difference,
+// squared and summed with non-negative terms: each bound is within 3 ulp
+// (2e-7 relative) of its exact value, and the 1e-5 margin covers that on
+// both sides of the test on top of the reference's own 1.1e-6.  An fp32
+// overflow (|colour| > 1e19) gives inf bounds: T = inf makes every colour a
+// candidate, which overflows the list into the exhaustive loop.  (fp64 was
+// ~570 VALU instructions per wave at half the fp32 rate.)
+__device__ __forceinline__ float ax_min2(float c, float lo, float hi) {
+    const float d = fmaxf(fmaxf(lo - c, c - hi), 0.f);
     return d * d;
 }
-__device__ __forceinline__ double ax_max2(double c, double lo, double hi) {
-    const double d = fmax(c - lo, hi - c);
+__device__ __forceinline__ float ax_max2(float c, float lo, float hi) {
+    const float d = fmaxf(c - lo, hi - c);
     return d * d;
 }
 
-#define HQ_CAND_MARGIN (1.0 + 1e-5)
+#define HQ_CAND_MARGIN (1.0f + 1e-5f)
 
 // Level-2 entries are interleaved by groups of 4 palettes: the 4 entries of one
 // cell share a 64-byte line, so a pixel evaluated under the 4 palettes of a
@@ -361,6 +370,33 @@ __device__ __forceinline__ double ax_max2(double c, double lo, double hi) {
 // line fetches they cause, not by their bytes).
 __host__ __device__ __forceinline__ int64_t lvl2_offset(int64_t gstride, int p, int64_t cell) {
     return (int64_t)(p >> 2) * gstride + cell * 64 + (p & 3) * 16;
+}
+
+// Per-axis child terms of the level-2 pass: s_ax[axis][j][i] = the bound of
+// parent-list entry i along `axis` for the child at position j (0..3) of the
+// cell on that axis.  A child's bound is the sum of its three axis terms, so
+// the 64 children share 12 terms per entry instead of 64 x 3.  Pitch 260:
+// the children of a wave that differ in position along an axis read rows 4
+// banks apart (a plain 256 pitch put them in one bank).
+constexpr int kAxPitch = kMaxK + 4;
+
+template <bool MAX>
+__device__ __forceinline__ void axis_terms(float (*s_ax)[4][kAxPitch], const float4* s_col,
+                                           const uint8_t* s_list, int total, int ci, int cj, int ck,
+                                           float inv2) {
+    const int t = threadIdx.x;
+    if (t < total) {
+        const float4 cc = s_col[s_list[t]];
+        const float v[3] = {cc.x, cc.y, cc.z};
+        const int base[3] = {4 * ci, 4 * cj, 4 * ck};
+#pragma unroll
+        for (int ax = 0; ax < 3; ++ax)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float lo = (float)(base[ax] + j) * inv2, hi = (float)(base[ax] + j + 1) * inv2;
+                s_ax[ax][j][t] = MAX ? ax_max2(v[ax], lo, hi) : ax_min2(v[ax], lo, hi);
+            }
+    }
 }
 
 // The grid work of level-1 cell `cell` of palette p; thread tid holds colour
@@ -373,33 +409,34 @@ __device__ __forceinline__ void grid_cell_body(const GridArgs& a, int p, int cel
     const int ci = cell / (G1 * G1), cj = (cell / G1) % G1, ck = cell % G1;
     __shared__ float4 s_col[kMaxK];
     __shared__ uint8_t s_list[kMaxK];
-    __shared__ double s_min[4];
+    __shared__ float s_min[4];
     __shared__ int s_wcount[4];
+    __shared__ float s_ax[3][4][kAxPitch];
 
     s_col[tid] = c;
-    const double inv1 = 1.0 / G1;
-    const double lo0 = ci * inv1, hi0 = (ci + 1) * inv1;
-    const double lo1 = cj * inv1, hi1 = (cj + 1) * inv1;
-    const double lo2 = ck * inv1, hi2 = (ck + 1) * inv1;
-    double dmin2 = INFINITY, dmax2 = INFINITY;
+    const float inv1 = 1.0f / (float)G1;
+    const float lo0 = ci * inv1, hi0 = (ci + 1) * inv1;
+    const float lo1 = cj * inv1, hi1 = (cj + 1) * inv1;
+    const float lo2 = ck * inv1, hi2 = (ck + 1) * inv1;
+    float dmin2 = INFINITY, dmax2 = INFINITY;
     if (valid) {
-        dmin2 = ax_min2(c.x, lo0, hi0) + ax_min2(c.y, lo1, hi1) + ax_min2(c.z, lo2, hi2);
-        dmax2 = ax_max2(c.x, lo0, hi0) + ax_max2(c.y, lo1, hi1) + ax_max2(c.z, lo2, hi2);
+        dmin2 = (ax_min2(c.x, lo0, hi0) + ax_min2(c.y, lo1, hi1)) + ax_min2(c.z, lo2, hi2);
+        dmax2 = (ax_max2(c.x, lo0, hi0) + ax_max2(c.y, lo1, hi1)) + ax_max2(c.z, lo2, hi2);
     }
-    double m = dmax2;
+    float m = dmax2;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) m = fmin(m, __shfl_xor(m, off, 64));
+    for (int off = 32; off > 0; off >>= 1) m = fminf(m, __shfl_xor(m, off, 64));
     const int wave = tid >> 6, lane = tid & 63;
     if (lane == 0) s_min[wave] = m;
     __syncthreads();
-    const double T1 = fmin(fmin(s_min[0], s_min[1]), fmin(s_min[2], s_min[3]));
+    const float T1 = fminf(fminf(s_min[0], s_min[1]), fminf(s_min[2], s_min[3]));
     const bool cand = valid && dmin2 <= T1 * HQ_CAND_MARGIN;
     const uint64_t bal = __ballot(cand);
     if (lane == 0) s_wcount[wave] = __popcll(bal);
     __syncthreads();
     int base = 0;
     for (int w = 0; w < wave; ++w) base += s_wcount[w];
-    const int total = s_wcount[0] + s_wcount[1] + s_wcount[2] + s_wcount[3];
+    const int total = exh ? 0 : s_wcount[0] + s_wcount[1] + s_wcount[2] + s_wcount[3];
     if (cand) s_list[base + __popcll(bal & ((1ull << lane) - 1ull))] = (uint8_t)tid;
     __syncthreads();
 
@@ -411,66 +448,64 @@ __device__ __forceinline__ void grid_cell_body(const GridArgs& a, int p, int cel
         else v = (!ovf1 && tid - 1 < total) ? s_list[tid - 1] : 0;
         l1[tid] = v;
     }
-    // Level 2: child c = tid >> 2 of this cell, its parent-list positions shared
-    // by the 4 threads of a quad (q = tid & 3 takes positions q, q+4, ...): T2 and
-    // the candidate mask are combined across the quad by shuffles, and each
-    // candidate's byte lands at its rank in ascending list order.  (One thread
-    // per child walking the list twice, on one wave of the four, made this
-    // kernel ~15 us per population.)
-    {
-        const int ch = tid >> 2, q = tid & 3;
-        const int ci2 = ci * 4 + (ch >> 4), cj2 = cj * 4 + ((ch >> 2) & 3), ck2 = ck * 4 + (ch & 3);
-        const double inv2 = 1.0 / G2;
-        const double l0 = ci2 * inv2, h0 = (ci2 + 1) * inv2;
-        const double l1b = cj2 * inv2, h1 = (cj2 + 1) * inv2;
-        const double l2 = ck2 * inv2, h2 = (ck2 + 1) * inv2;
-        // pass 1: T2 over the whole parent list (which can exceed 31 entries: the
-        // level-1 entry then overflows, the children still get lists)
-        double t2 = INFINITY;
-        for (int i = q; !exh && i < total; i += 4) {
-            const float4 cc = s_col[s_list[i]];
-            t2 = fmin(t2, ax_max2(cc.x, l0, h0) + ax_max2(cc.y, l1b, h1) + ax_max2(cc.z, l2, h2));
-        }
-        t2 = fmin(t2, __shfl_xor(t2, 1, 64));
-        t2 = fmin(t2, __shfl_xor(t2, 2, 64));
-        const double thr = t2 * HQ_CAND_MARGIN;
-        // pass 2, 32 positions at a time: candidate mask, ranks in list order
-        uint32_t w[4] = {0u, 0u, 0u, 0u};
-        int n = 0;  // candidates so far (quad-uniform)
-        for (int b0 = 0; !exh && b0 < total && n <= kL2Cap; b0 += 32) {
-            uint32_t mine = 0;
+    // Level 2: child ch = tid >> 2 of this cell at axis positions (a0, a1, a2),
+    // its parent-list positions shared by the 4 threads of a quad (q = tid & 3
+    // takes positions q, q+4, ...): T2 and the candidate mask are combined
+    // across the quad by shuffles, and each candidate's byte lands at its rank
+    // in ascending list order.  Pass 1 reads dmax^2 axis terms, pass 2 dmin^2
+    // terms (the same LDS, rewritten between the passes).
+    const float inv2 = 1.0f / (float)G2;
+    const int ch = tid >> 2, q = tid & 3;
+    const int a0 = ch >> 4, a1 = (ch >> 2) & 3, a2 = ch & 3;
+    axis_terms<true>(s_ax, s_col, s_list, total, ci, cj, ck, inv2);
+    __syncthreads();
+    // pass 1: T2 over the whole parent list (which can exceed 31 entries: the
+    // level-1 entry then overflows, the children still get lists)
+    float t2 = INFINITY;
+    for (int i = q; i < total; i += 4)
+        t2 = fminf(t2, (s_ax[0][a0][i] + s_ax[1][a1][i]) + s_ax[2][a2][i]);
+    t2 = fminf(t2, __shfl_xor(t2, 1, 64));
+    t2 = fminf(t2, __shfl_xor(t2, 2, 64));
+    const float thr = t2 * HQ_CAND_MARGIN;
+    __syncthreads();
+    axis_terms<false>(s_ax, s_col, s_list, total, ci, cj, ck, inv2);
+    __syncthreads();
+    // pass 2, 32 positions at a time: candidate mask, ranks in list order
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    int n = 0;  // candidates so far (quad-uniform)
+    for (int b0 = 0; b0 < total && n <= kL2Cap; b0 += 32) {
+        uint32_t mine = 0;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int i = b0 + q + 4 * j;
-                if (i < total) {
-                    const float4 cc = s_col[s_list[i]];
-                    const double d = ax_min2(cc.x, l0, h0) + ax_min2(cc.y, l1b, h1) + ax_min2(cc.z, l2, h2);
-                    if (d <= thr) mine |= 1u << (q + 4 * j);
-                }
+        for (int j = 0; j < 8; ++j) {
+            const int i = b0 + q + 4 * j;
+            if (i < total) {
+                const float d = (s_ax[0][a0][i] + s_ax[1][a1][i]) + s_ax[2][a2][i];
+                if (d <= thr) mine |= 1u << (q + 4 * j);
             }
-            uint32_t M = mine | (uint32_t)__shfl_xor((int)mine, 1, 64);
-            M |= (uint32_t)__shfl_xor((int)M, 2, 64);
+        }
+        uint32_t M = mine | (uint32_t)__shfl_xor((int)mine, 1, 64);
+        M |= (uint32_t)__shfl_xor((int)M, 2, 64);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int r = q + 4 * j;
-                if ((mine >> r) & 1u) {
-                    const int pos = n + __popc(M & ((1u << r) - 1u)) + 1;  // byte in the entry
-                    if (pos <= kL2Cap) w[pos >> 2] |= (uint32_t)s_list[b0 + r] << (8 * (pos & 3));
-                }
+        for (int j = 0; j < 8; ++j) {
+            const int r = q + 4 * j;
+            if ((mine >> r) & 1u) {
+                const int pos = n + __popc(M & ((1u << r) - 1u)) + 1;  // byte in the entry
+                if (pos <= kL2Cap) w[pos >> 2] |= (uint32_t)s_list[b0 + r] << (8 * (pos & 3));
             }
-            n += __popc(M);
         }
+        n += __popc(M);
+    }
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            w[m] |= (uint32_t)__shfl_xor((int)w[m], 1, 64);
-            w[m] |= (uint32_t)__shfl_xor((int)w[m], 2, 64);
-        }
-        if (q == 0) {
-            if (exh || n > kL2Cap) { w[0] = kOverflow; w[1] = w[2] = w[3] = 0; }
-            else w[0] |= (uint32_t)n;
-            uint8_t* l2e = a.lvl2 + lvl2_offset(a.lvl2_gstride, p, (int64_t)(ci2 * G2 + cj2) * G2 + ck2);
-            *reinterpret_cast<uint4*>(l2e) = make_uint4(w[0], w[1], w[2], w[3]);
-        }
+    for (int k = 0; k < 4; ++k) {
+        w[k] |= (uint32_t)__shfl_xor((int)w[k], 1, 64);
+        w[k] |= (uint32_t)__shfl_xor((int)w[k], 2, 64);
+    }
+    if (q == 0) {
+        if (exh || n > kL2Cap) { w[0] = kOverflow; w[1] = w[2] = w[3] = 0; }
+        else w[0] |= (uint32_t)n;
+        const int ci2 = ci * 4 + a0, cj2 = cj * 4 + a1, ck2 = ck * 4 + a2;
+        uint8_t* l2e = a.lvl2 + lvl2_offset(a.lvl2_gstride, p, (int64_t)(ci2 * G2 + cj2) * G2 + ck2);
+        *reinterpret_cast<uint4*>(l2e) = make_uint4(w[0], w[1], w[2], w[3]);
     }
 }
 

@@ -461,6 +461,33 @@ def test_full_size_properties(gpu, filt):
     m.close()
 
 
+@pytest.mark.parametrize("rows", [16, 8])
+def test_fused_finalize_alternating_populations(gpu, filt, rows):
+    """Two different populations evaluated alternately give, every time,
+    bitwise the costs and used flags of their first evaluation (no state of one
+    evaluation -- partials, used masks, level-2 lines -- leaks into the next),
+    and agree with the generic two-pass path."""
+    w = h = 4096
+    K, P = 256, 4
+    R, G, B = o.synthetic_image(w, h, seed=3)
+    m = _planar_ctx(gpu, R, G, B, w, h, filt.illum)
+    m.setOption("cost_rows", rows)
+    pops = [np.stack([o.synthetic_palette(K, 40 + 10 * s + p) for p in range(P)]).reshape(P, -1)
+            for s in range(2)]
+    first = [m.computeQuantizationErrorPopulation(pp, 2.0, return_used=True) for pp in pops]
+    for it in range(6):
+        c, u = m.computeQuantizationErrorPopulation(pops[it & 1], 2.0, return_used=True)
+        np.testing.assert_array_equal(c, first[it & 1][0])
+        np.testing.assert_array_equal(u, first[it & 1][1])
+    assert not np.array_equal(first[0][0], first[1][0])
+    m.setOption("cost_variant", 1)
+    for s in range(2):
+        c, u = m.computeQuantizationErrorPopulation(pops[s], 2.0, return_used=True)
+        np.testing.assert_allclose(c, first[s][0], rtol=1e-6)
+        np.testing.assert_array_equal(u, first[s][1])
+    m.close()
+
+
 # ---------------------------------------------------------------------------
 # BASELINE.json configs at their full sizes against the oracle (C3, C4, C5).
 # The C oracle runs one 4096^2/K=256 evaluation in about 1 s on 16 threads.
