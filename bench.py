@@ -42,19 +42,23 @@ def synthetic_planes(w, h, seed=1):
     return [((z >> np.uint64(8 * c)) & np.uint64(0xFF)).astype(np.float32) / s for c in range(3)]
 
 
-def measured_traffic(size, K, P, grid, world):
-    """HBM bytes per cost_tile launch from the committed PMC passes (or None)."""
-    path = os.path.join(ROOT, "profiles", "r01_hbm_traffic.json")
-    try:
-        d = json.load(open(path))
-    except (OSError, ValueError):
-        return None
-    c = d.get("config", {})
-    if world != 1 or (c.get("size"), c.get("K"), c.get("P"), c.get("grid")) != (size, K, P, grid):
-        return None
-    for name, v in d.get("kernels", {}).items():
-        if name.startswith("hq::cost_"):  # the fast cost kernel of the default tile config
-            return int(v["traffic_bytes"])
+def measured_traffic(size, K, P, grid, world, kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC passes
+    (profiles/rNN_hbm_traffic.json), or None when none matches this config."""
+    import glob
+
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_hbm_traffic.json")))
+    for path in reversed(paths):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        c = d.get("config", {})
+        if world != 1 or (c.get("size"), c.get("K"), c.get("P"), c.get("grid")) != (size, K, P, grid):
+            continue
+        for name, v in d.get("kernels", {}).items():
+            if name.startswith("hq::" + kernel):
+                return int(v["traffic_bytes"])
     return None
 
 
@@ -255,7 +259,11 @@ def main():
     exec_tf = exec_flops / (cost_ms * 1e-3) / 1e12 if cost_ms > 0 else 0.0
     alg_bytes = n_own * (12 + P)
     hbm_gbs = alg_bytes / (cost_ms * 1e-3) / 1e9 if cost_ms > 0 else 0.0
-    traffic = measured_traffic(W, args.K, P, args.grid, world)
+    opts = dict(kv.split("=", 1) for kv in args.opt)
+    rows = int(opts.get("cost_rows", 16))
+    kernel = ("gen_vpass_kernel" if int(opts.get("cost_variant", 0)) == 1
+              else {16: "cost16_kernel", 8: "cost_mfma_kernel"}.get(rows, "cost16_kernel"))
+    traffic = measured_traffic(W, args.K, P, args.grid, world, kernel)
     # whole-evaluation view: the metric's 24 B/px-eval HBM-read roofline
     eval_roof_mpx = HBM_PEAK_GBS * 1e9 / 24.0 / 1e6 * world
     # which BASELINE.json config this run's shape is (configs[2] is the default)
@@ -298,7 +306,7 @@ def main():
         "roofline": {"bound": "valu", "achieved": round(achieved_tf, 2), "peak": FP32_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4),
                      "traffic": traffic,
-                     "kernel": "cost_mfma_kernel", "kernel_avg_ms": round(cost_ms, 4),
+                     "kernel": kernel, "kernel_avg_ms": round(cost_ms, 4),
                      "alg_flops_per_launch": alg_flops, "exec_flops_per_launch": exec_flops,
                      "frac_executed_taps": round(exec_tf / FP32_PEAK_TFLOPS, 4),
                      "alg_bytes_per_launch": alg_bytes, "hbm_GBs_alg": round(hbm_gbs, 1),
