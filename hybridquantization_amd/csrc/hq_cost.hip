@@ -100,7 +100,7 @@ template <int HALF, int RW, int TH>
 struct TileFill {
     static constexpr int TW = RW - 2 * HALF, RH = TH + 2 * HALF, DW = RW / 4;
     static constexpr int NFD = (RH * DW + 255) / 256, NFB = (RH * RW + 255) / 256;
-    static_assert((DW & (DW - 1)) == 0, "dword columns per row: a power of two");
+    static_assert(RW % 4 == 0, "whole dwords per region row");
     uint32_t lo[NFD], hi[NFD];  // interior tiles: aligned dword pairs of the index rows
     uint32_t roff[NFD];         // their rows' byte offsets (alignment for commit)
     float4 ov;
@@ -424,14 +424,15 @@ constexpr int kWideHalf = 64;  // float2 per half of a permuted row-pair row
 
 // float2 position of column `col` in a permuted row-pair row: half = bit 1 of
 // col, 16-B slot col >> 2, float2 col & 1.
+template <int WH = kWideHalf>
 __device__ __forceinline__ int wide_pos(int col) {
-    return ((col >> 1) & 1) * kWideHalf + ((col >> 2) << 1) + (col & 1);
+    return ((col >> 1) & 1) * WH + ((col >> 2) << 1) + (col & 1);
 }
 
 // Horizontal pass of filter f for item j (output columns 4j .. 4j+3) of a row
 // pair: src = the row-pair row in plane 0; pstride = f32x4 per plane; taps
 // [TLO, THI].
-template <int HALF, int TLO = 0, int THI = 2 * HALF>
+template <int HALF, int TLO = 0, int THI = 2 * HALF, int WH = kWideHalf>
 __device__ __forceinline__ void hpass_wide(const f32x4* src, int j, TapsPtr<HALF> taps, int f,
                                            int plane, int pstride, f32x2 (&acc)[4]) {
     constexpr int HR = 4, NQ = (HR + 2 * HALF) / 2;  // 12 reads of 2 columns
@@ -439,7 +440,7 @@ __device__ __forceinline__ void hpass_wide(const f32x4* src, int j, TapsPtr<HALF
     const f32x4* row = src + plane * pstride + j;
     f32x4 v[NQ];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) v[q] = row[(q & 1) * (kWideHalf / 2) + (q >> 1)];
+    for (int q = 0; q < NQ; ++q) v[q] = row[(q & 1) * (WH / 2) + (q >> 1)];
     f32x2 in[2 * NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
@@ -458,14 +459,15 @@ __device__ __forceinline__ void hpass_wide(const f32x4* src, int j, TapsPtr<HALF
 // D of one 16x16 stack block of output-row half `half` -> permuted row pairs:
 // lane (c = l & 15, q = l >> 4) holds rows 8 half + 4(q & 1) .. +3 of the
 // stack's filter q >> 1 at column `col`.
+template <int WH = kWideHalf>
 __device__ __forceinline__ void store_vstack16(float* s_v, const f32x4v& d, int plane_a,
                                                int plane_b, int lk, int col, int half) {
-    constexpr int PAIRS = kTH16 / 2, ROW = 2 * kWideHalf;  // float2 per row-pair row
+    constexpr int PAIRS = kTH16 / 2, ROW = 2 * WH;  // float2 per row-pair row
     const int plane = lk < 2 ? plane_a : plane_b;
     if (plane < 0) return;
     const int p0 = 4 * half + 2 * (lk & 1);
     f32x2* v = reinterpret_cast<f32x2*>(s_v);
-    const int pos = wide_pos(col);
+    const int pos = wide_pos<WH>(col);
     v[(plane * PAIRS + p0) * ROW + pos] = f32x2{d[0], d[1]};
     v[(plane * PAIRS + p0 + 1) * ROW + pos] = f32x2{d[2], d[3]};
 }
@@ -626,6 +628,184 @@ __global__ __launch_bounds__(256, 4) void cost16_kernel(CostArgs a, int P_) {
         sum = (double)part;
     }
     sum = wave_sum_to_lane63(sum);
+    if ((tid & 63) == 63) s_red[tid >> 6] = sum;
+    __syncthreads();
+    if (tid == 0)
+        a.partial[(int64_t)cur.p * a.ntiles + cur.tile] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+}
+
+// ----------------------------------------------------------------------------
+// cost16w: 16 x 128 tiles (option cost_cols 128).  cost16's 108-column tile
+// gives 27 horizontal items per row pair to 32 threads: 16% of the lanes idle
+// through the horizontal pass and Lab/dE, its two largest VALU parts.  128
+// output columns give 32 items per row pair -- every lane busy -- for a
+// 148-column region: 10 vertical-pass blocks of 16 columns (5 ranges of 32,
+// blocks w, w+4, w+8 on wave w), 25% more vertical work for 18.5% more
+// outputs.  The 160-column row-pair planes (30 KiB for three) only fit 4
+// workgroups per CU three filters at a time, so the channels run in three
+// phases: channel 0 (f0, f1, f2), channel 1 (f3, f4), channel 2 (f5, f6).
+// Channels 1 and 2 share one gather per region row; channel 2's vertical
+// results wait in registers through channel 1's horizontal pass.  39,584 B of
+// LDS.
+// ----------------------------------------------------------------------------
+constexpr int kWHalfW = 80;  // float2 per half of a 160-column permuted row-pair row
+
+template <int DE, bool TRIM>
+__global__ __launch_bounds__(256, 4) void cost16w_kernel(CostArgs a, int P_) {
+    constexpr int HALF = 10, TH = kTH16, HR = 4, T2 = 2 * HALF;
+    constexpr int TW = 128, RWL = TW + 2 * HALF, RW = 160;  // outputs, region read, LDS pitch
+    constexpr int RH = TH + 2 * HALF;                       // 36 region rows
+    constexpr int PAIRS = TH / 2, ROW = 2 * kWHalfW;        // float2 per row-pair row
+    constexpr int PLANE4 = PAIRS * ROW / 2;                 // f32x4 per filter plane
+    constexpr int NBLK = RW / 16;                           // vertical-pass blocks
+    static_assert(TW / HR == 32 && kv_row(1, 3, 6) < RH && RWL <= RW, "tile");
+    __shared__ f32x4 s_vq[3 * PLANE4];
+    __shared__ uint32_t s_ox[kMaxK];  // opponent x 2^14 as (hi, lo) f16 pairs: channel 0
+    __shared__ uint2 s_oyz[kMaxK];     // channels 1, 2
+    __shared__ __attribute__((aligned(16))) uint8_t s_idx[RH * RW];
+    __shared__ double s_red[4];
+    float* s_v = reinterpret_cast<float*>(s_vq);
+    const int tid = threadIdx.x;
+    const Geom& g = a.g;
+    const TileItem cur = tile_item<TW, TH>(a, xcd_remap(blockIdx.x, a.ntiles * P_), P_);
+    const TapsPtr<HALF> taps = (TapsPtr<HALF>)(uintptr_t)a.taps;  // H taps x 2^-30
+    const int lane = tid & 63, wv = tid >> 6, lc = lane & 15, lk = lane >> 4;
+    // [trim][half][stack][hi, lo][lane]
+    const uint4* frag = a.vfrag16 + (TRIM ? 2 * 4 * 2 * 64 : 0) + lane;
+    auto F = [&](int half, int st, int hl) { return frag[((half * 4 + st) * 2 + hl) * 64]; };
+
+    TileFill<HALF, RWL, TH> fill;
+    fill.issue(a, cur, tid);
+    uint4 A00h = F(0, 0, 0), A00l = F(0, 0, 1), A01h = F(0, 1, 0), A01l = F(0, 1, 1);  // half 0
+    uint4 A10h = F(1, 0, 0), A10l = F(1, 0, 1), A11h = F(1, 1, 0), A11l = F(1, 1, 1);  // half 1
+    // every entry (zeros for tid >= K): zero-weight rows and the columns past
+    // the region gather arbitrary indices, and 0 x NaN would be NaN
+    s_ox[tid] = split_f16(fill.ov.x);
+    s_oyz[tid] = make_uint2(split_f16(fill.ov.y), split_f16(fill.ov.z));
+    fill.template commit_idx<RW>(a, s_idx, tid);
+    // H item: row pair m, output columns 4j .. 4j+3 (every thread has one)
+    const int m = tid >> 5, jr = tid & 31;
+    const int gy0 = cur.y0 + 2 * m, gx0 = cur.x0 + HR * jr;
+    const f32x4* hsrc = &s_vq[(m * ROW) / 2];
+    f32x2 acc0[HR], acc1[HR], acc2[HR];
+#pragma unroll
+    for (int xo = 0; xo < HR; ++xo) acc0[xo] = acc1[xo] = acc2[xo] = f32x2{0.f, 0.f};
+    __syncthreads();
+
+    // Vertical pass of channel `ch` on this wave's blocks: stacks (s0: planes
+    // pa0/pb0) and, for channel 0, (s1: plane pa1).  Block b = wset + 4i covers
+    // the 16 columns of parity half b & 1 of range b >> 1.  Block sets 0 and 1
+    // hold 3 blocks, sets 2 and 3 hold 2: the sets rotate with the workgroup,
+    // so the extra blocks do not land on the same SIMDs in every workgroup.
+    const int wset = (wv + (int)blockIdx.x) & 3;
+    auto vpass0 = [&](const f16x8& h0h, const f16x8& h0l, const f16x8& h1h, const f16x8& h1l,
+                      const f16x8& k0h, const f16x8& k0l, const f16x8& k1h, const f16x8& k1l) {
+        const uint32_t* tab = s_ox;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int b = wset + 4 * i;
+            if (b >= NBLK) break;
+            const int col = 32 * (b >> 1) + 4 * (lc >> 1) + (lc & 1) + 2 * (b & 1);
+            uint32_t w[10];  // slots 0-7: half 0; slots 2-9: half 1 (kv_row)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) w[j] = tab[s_idx[kv_row(0, lk, j) * RW + col]];
+            w[8] = tab[s_idx[kv_row_clamped(1, lk, 6) * RW + col]];
+            w[9] = tab[s_idx[kv_row_clamped(1, lk, 7) * RW + col]];
+            f16x8 bh, bl, chh, chl;
+            pack_b(*reinterpret_cast<const uint32_t(*)[8]>(&w[0]), bh, bl);
+            pack_b(*reinterpret_cast<const uint32_t(*)[8]>(&w[2]), chh, chl);
+            store_vstack16<kWHalfW>(s_v, mfma3(h0h, h0l, bh, bl), 0, 1, lk, col, 0);
+            store_vstack16<kWHalfW>(s_v, mfma3(h1h, h1l, chh, chl), 0, 1, lk, col, 1);
+            store_vstack16<kWHalfW>(s_v, mfma3(k0h, k0l, bh, bl), 2, -1, lk, col, 0);
+            store_vstack16<kWHalfW>(s_v, mfma3(k1h, k1l, chh, chl), 2, -1, lk, col, 1);
+        }
+    };
+    auto H = [](const uint4& u) { return __builtin_bit_cast(f16x8, u); };
+
+    // ---- channel 0: stacks (f0, f1) -> planes 0, 1 and (f2, -) -> plane 2 ----
+    vpass0(H(A00h), H(A00l), H(A10h), H(A10l), H(A01h), H(A01l), H(A11h), H(A11l));
+    // channel 1-2 stacks, in flight during channel 0's horizontal pass
+    A00h = F(0, 2, 0); A00l = F(0, 2, 1); A01h = F(0, 3, 0); A01l = F(0, 3, 1);
+    A10h = F(1, 2, 0); A10l = F(1, 2, 1); A11h = F(1, 3, 0); A11l = F(1, 3, 1);
+    __syncthreads();
+    if constexpr (TRIM) hpass_wide<HALF, kTrimLo[0], kTrimHi[0], kWHalfW>(hsrc, jr, taps, 0, 0, PLANE4, acc0);
+    else hpass_wide<HALF, 0, T2, kWHalfW>(hsrc, jr, taps, 0, 0, PLANE4, acc0);
+    hpass_wide<HALF, 0, T2, kWHalfW>(hsrc, jr, taps, 1, 1, PLANE4, acc0);
+    hpass_wide<HALF, 0, T2, kWHalfW>(hsrc, jr, taps, 2, 2, PLANE4, acc0);
+    __syncthreads();
+
+    // ---- channels 1, 2: one gather of (y, z) per region row; stack (f3, f4)
+    // -> planes 0, 1 now, stack (f5, f6)'s results held in registers until
+    // channel 1's horizontal pass has read the planes ----
+    f32x4v d5[3][2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int b = wset + 4 * i;
+        if (b >= NBLK) break;
+        const int col = 32 * (b >> 1) + 4 * (lc >> 1) + (lc & 1) + 2 * (b & 1);
+        uint32_t wy[10], wz[10];  // slots 0-7: half 0; slots 2-9: half 1 (kv_row)
+#pragma unroll
+        for (int j = 0; j < 10; ++j) {
+            const int row = j < 8 ? kv_row(0, lk, j) : kv_row_clamped(1, lk, j - 2);
+            const uint2 e = s_oyz[s_idx[row * RW + col]];
+            wy[j] = e.x; wz[j] = e.y;
+        }
+        f16x8 bh, bl, chh, chl;
+        pack_b(*reinterpret_cast<const uint32_t(*)[8]>(&wy[0]), bh, bl);
+        pack_b(*reinterpret_cast<const uint32_t(*)[8]>(&wy[2]), chh, chl);
+        store_vstack16<kWHalfW>(s_v, mfma3(H(A00h), H(A00l), bh, bl), 0, 1, lk, col, 0);
+        store_vstack16<kWHalfW>(s_v, mfma3(H(A10h), H(A10l), chh, chl), 0, 1, lk, col, 1);
+        pack_b(*reinterpret_cast<const uint32_t(*)[8]>(&wz[0]), bh, bl);
+        pack_b(*reinterpret_cast<const uint32_t(*)[8]>(&wz[2]), chh, chl);
+        d5[i][0] = mfma3(H(A01h), H(A01l), bh, bl);
+        d5[i][1] = mfma3(H(A11h), H(A11l), chh, chl);
+    }
+    __syncthreads();
+    if constexpr (TRIM) hpass_wide<HALF, kTrimLo[1], kTrimHi[1], kWHalfW>(hsrc, jr, taps, 3, 0, PLANE4, acc1);
+    else hpass_wide<HALF, 0, T2, kWHalfW>(hsrc, jr, taps, 3, 0, PLANE4, acc1);
+    hpass_wide<HALF, 0, T2, kWHalfW>(hsrc, jr, taps, 4, 1, PLANE4, acc1);
+    __syncthreads();
+
+    // ---- channel 2: stack (f5, f6) -> planes 0, 1 ----
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int b = wset + 4 * i;
+        if (b >= NBLK) break;
+        const int col = 32 * (b >> 1) + 4 * (lc >> 1) + (lc & 1) + 2 * (b & 1);
+        store_vstack16<kWHalfW>(s_v, d5[i][0], 0, 1, lk, col, 0);
+        store_vstack16<kWHalfW>(s_v, d5[i][1], 0, 1, lk, col, 1);
+    }
+    // LabRef of the item's 2 x 4 pixels, in flight across the barrier
+    float4 lab[2][3];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const bool ok = gy0 + r < g.r1 && gx0 < g.W;
+        const uint32_t off = ok ? (uint32_t)((gy0 + r - g.r0) * g.lab_pitch + gx0) : 0u;
+        const float* src3[3] = {a.labL, a.labA, a.labB};
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch)
+            lab[r][ch] = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(src3[ch]) +
+                                                          (off << 2));  // 32-bit byte offset
+    }
+    __syncthreads();
+    if constexpr (TRIM) hpass_wide<HALF, kTrimLo[2], kTrimHi[2], kWHalfW>(hsrc, jr, taps, 5, 0, PLANE4, acc2);
+    else hpass_wide<HALF, 0, T2, kWHalfW>(hsrc, jr, taps, 5, 0, PLANE4, acc2);
+    hpass_wide<HALF, 0, T2, kWHalfW>(hsrc, jr, taps, 6, 1, PLANE4, acc2);
+
+    float part = 0.f;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const float Ls[4] = {lab[r][0].x, lab[r][0].y, lab[r][0].z, lab[r][0].w};
+        const float As[4] = {lab[r][1].x, lab[r][1].y, lab[r][1].z, lab[r][1].w};
+        const float Bs[4] = {lab[r][2].x, lab[r][2].y, lab[r][2].z, lab[r][2].w};
+#pragma unroll
+        for (int xo = 0; xo < HR; ++xo) {
+            const float3 g3 = opp2g_fast(acc0[xo][r], acc1[xo][r], acc2[xo][r], a.m_lab);
+            const float e = delta_e_g<DE>(Ls[xo], As[xo], Bs[xo], g3);
+            part += (gy0 + r < g.r1 && gx0 + xo < g.W) ? e : 0.f;
+        }
+    }
+    double sum = wave_sum_to_lane63((double)part);
     if ((tid & 63) == 63) s_red[tid >> 6] = sum;
     __syncthreads();
     if (tid == 0)
@@ -807,20 +987,24 @@ void build_fast_taps(const float* k1, const float* k2, const float* k3, const fl
 // a.taps = the two CostTaps<10> of build_fast_taps
 
 // tile_rows: 8 (cost_mfma_kernel) or 16 (cost16_kernel)
-void fast_tile_dims(int W, int own_rows, int tile_rows, int* tiles_x, int* ntiles) {
-    *tiles_x = (W + kFastTW - 1) / kFastTW;
+void fast_tile_dims(int W, int own_rows, int tile_rows, int tile_cols, int* tiles_x, int* ntiles) {
+    const int tw = tile_rows == kTH16 && tile_cols == 128 ? 128 : kFastTW;
+    *tiles_x = (W + tw - 1) / tw;
     *ntiles = *tiles_x * ((own_rows + tile_rows - 1) / tile_rows);
 }
 
 // a.taps = the two CostTaps<10> of build_fast_taps; [1] carries the vertical
 // pass's 2^30 scale in its horizontal taps.
 hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, bool trim, int tile_rows,
-                            hipStream_t s) {
+                            int tile_cols, hipStream_t s) {
     CostArgs a = a0;
     a.taps = static_cast<const char*>(a0.taps) + sizeof(CostTaps<10>);
     const dim3 grid((unsigned)(a.ntiles * P));
 #define HQ_COST(KN, DEV, TR) HQ_LAUNCH((KN<DEV, TR>), grid, dim3(256), 0, s, a, P)
-    if (tile_rows == kTH16) {
+    if (tile_rows == kTH16 && tile_cols == 128) {
+        if (de == 0) { if (trim) HQ_COST(cost16w_kernel, 0, true); else HQ_COST(cost16w_kernel, 0, false); }
+        else { if (trim) HQ_COST(cost16w_kernel, 1, true); else HQ_COST(cost16w_kernel, 1, false); }
+    } else if (tile_rows == kTH16) {
         if (de == 0) { if (trim) HQ_COST(cost16_kernel, 0, true); else HQ_COST(cost16_kernel, 0, false); }
         else { if (trim) HQ_COST(cost16_kernel, 1, true); else HQ_COST(cost16_kernel, 1, false); }
     } else {
