@@ -260,10 +260,9 @@ def main():
     alg_bytes = n_own * (12 + P)
     hbm_gbs = alg_bytes / (cost_ms * 1e-3) / 1e9 if cost_ms > 0 else 0.0
     opts = dict(kv.split("=", 1) for kv in args.opt)
-    rows, cols = int(opts.get("cost_rows", 16)), int(opts.get("cost_cols", 128))
+    rows = int(opts.get("cost_rows", 16))
     kernel = ("gen_vpass_kernel" if int(opts.get("cost_variant", 0)) == 1
-              else "cost_mfma_kernel" if rows == 8
-              else "cost16w_kernel" if cols == 128 else "cost16_kernel")
+              else "cost_mfma_kernel" if rows == 8 else "cost16w_kernel")
     traffic = measured_traffic(W, args.K, P, args.grid, world, kernel)
     # whole-evaluation view: the metric's 24 B/px-eval HBM-read roofline
     eval_roof_mpx = HBM_PEAK_GBS * 1e9 / 24.0 / 1e6 * world

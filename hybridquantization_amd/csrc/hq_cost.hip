@@ -18,8 +18,8 @@ namespace hq {
 // Vertical pass first on all RW region columns (separable filters commute),
 // then the horizontal pass on the TW output columns, Opp->Lab, dE, fp64 partial.
 // ----------------------------------------------------------------------------
-// Tile geometry of the fast path: RW = 128 region columns, TW = 108 output
-// columns; 8 (cost_mfma_kernel) or 16 (cost16_kernel) output rows.
+// Tile geometry of the fast path: 8 x 108 output tiles of a 28 x 128 region
+// (cost_mfma_kernel) or 16 x 128 tiles of a 36 x 148 region (cost16w_kernel).
 constexpr int kFastHalf = 10, kFastRW = 128;
 constexpr int kFastTW = kFastRW - 2 * kFastHalf;
 
@@ -59,12 +59,13 @@ constexpr float kVOutScale = 1.0f / (16384.0f * 65536.0f);  // 2^-30
 
 // Region row of K slot (g = lane >> 4, j) of the vertical pass's B operand.
 // Half 0 (output rows 0-7): rows 4j + g (lane group g holds every 4th row).
-// Half 1 (output rows 8-15 of a 16-row tile, rows 8-39): slots 0-5 are half
-// 0's slots 2-7 (rows 8 + 4j + g), slots 6 and 7 are rows 32 + g and 36 + g
-// (rows 36-39 carry zero taps), so every lane gathers 2 new values for half 1
-// (no divergent block gather).  The A fragments permute K to match.
+// Half 1 (output rows 8-15 of a 16-row tile, rows 8-39): slots 2-7 are half
+// 0's slots 2-7 (rows 8-31), slots 0 and 1 are rows 32 + g and 36 + g (rows
+// 36-39 carry zero taps).  Every lane gathers 2 new values for half 1, and
+// half 1's B operand is half 0's with only its first dword replaced (same
+// registers, no moves: pack_b_halves).  The A fragments permute K to match.
 __host__ __device__ __forceinline__ constexpr int kv_row(int half, int g, int j) {
-    return half == 0 ? 4 * j + g : (j < 6 ? 4 * j + 8 + g : (j == 6 ? 32 + g : 36 + g));
+    return half == 0 || j >= 2 ? 4 * j + g : (j == 0 ? 32 + g : 36 + g);
 }
 
 // (hi, lo) f16 split of x * 2^14 in one dword, hi in bits 0-15.
@@ -257,6 +258,21 @@ __device__ __forceinline__ void pack_b(const uint32_t (&w)[8], f16x8& bh, f16x8&
     bl = __builtin_bit_cast(f16x8, l);
 }
 
+// Both halves' B operands of a 16-row tile's block: w[0..7] = half 0's slots,
+// w[8], w[9] = half 1's slots 0 and 1 (kv_row).  Half 1's operand is half 0's
+// with dword 0 replaced: the caller issues half 0's MFMAs, then writes nh / nl
+// into dword 0 (the registers are reused in place).
+__device__ __forceinline__ void pack_b_halves(const uint32_t (&w)[10], u32x4& h, u32x4& l,
+                                              uint32_t& nh, uint32_t& nl) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        h[m] = __builtin_amdgcn_perm(w[2 * m + 1], w[2 * m], 0x05040100u);  // hi halves
+        l[m] = __builtin_amdgcn_perm(w[2 * m + 1], w[2 * m], 0x07060302u);  // lo halves
+    }
+    nh = __builtin_amdgcn_perm(w[9], w[8], 0x05040100u);
+    nl = __builtin_amdgcn_perm(w[9], w[8], 0x07060302u);
+}
+
 __device__ __forceinline__ f32x4v mfma3(const f16x8& ah, const f16x8& al, const f16x8& bh,
                                         const f16x8& bl) {
     f32x4v d = {0.f, 0.f, 0.f, 0.f};
@@ -400,31 +416,37 @@ __global__ __launch_bounds__(256, 6) void cost_mfma_kernel(CostArgs a, int P_) {
 }
 
 // ----------------------------------------------------------------------------
-// cost16: 16-row tiles.  The random opponent-table gathers of the vertical
-// pass and the horizontal windows are the kernel's LDS traffic, and LDS
-// bounds cost_mfma (PMC: ~77% of cycles LDS-active, a quarter of that in bank
-// conflicts of the random gathers).  A 16 x 108 tile needs a 36-row region:
+// cost16w: 16 x 128 output tiles of a 36 x 148 region.  The random
+// opponent-table gathers of the vertical pass and the horizontal windows are
+// the kernel's LDS traffic; FP32 VALU issue (horizontal taps, Lab/dE) bounds it.
 // - vertical pass: output rows 0-7 take region rows 0-31, rows 8-15 take rows
 //   8-39 (36-39 zero-weight): with lane group g holding every 4th row (kv_row),
 //   each lane keeps six of its eight half-0 values for half 1 and gathers two
-//   more -- 40 gathered rows per 16 output rows instead of 64, no divergence;
-// - horizontal pass: items of 4 output columns x a row pair (216 items, one per
-//   thread of 8 row pairs x 32 slots), a 24-column window = 12 ds_read_b128
-//   per filter for 8 outputs (cost_mfma: 11 for 4).  Row-pair rows store their
-//   column pairs split by parity (pair p -> half p & 1, slot p >> 1), so read q
-//   of item j lands at half q & 1, slot j + q / 2: lanes 16 B apart, conflict
-//   free.  The vertical pass gives each 16-column MFMA block the 16 columns of
-//   one parity half of a 32-column range (lane n -> column 4(n >> 1) + 2 bb +
-//   (n & 1)), so a block's stores fill 16 contiguous float2 of one half:
-//   conflict free without padding the rows.
-// 40,480 B of LDS (32 KiB s_v, 36 index rows): 4 workgroups per CU.
+//   more -- 40 gathered rows per 16 output rows instead of 64, no divergence.
+//   10 blocks of 16 columns (5 ranges of 32) cover the 148 region columns
+//   (+12 unread): each block is the 16 columns of one parity half of a range
+//   (lane n -> column 4(n >> 1) + 2 (b & 1) + (n & 1)), so its stores fill 16
+//   contiguous float2 of one half: conflict free without padding.  Block sets
+//   {s, s+4, s+8} go to the waves, rotated per workgroup.
+// - horizontal pass: items of 4 output columns x a row pair (256 items, one per
+//   thread: 8 row pairs x 32), a 24-column window = 12 ds_read_b128 per filter
+//   for 8 outputs.  Row-pair rows store their column pairs split by parity
+//   (pair p -> half p & 1, slot p >> 1), so read q of item j lands at half
+//   q & 1, slot j + q / 2: lanes 16 B apart, conflict free.  (The 108-column
+//   tile of a 128-column region gave 27 items to 32 threads: 16% of the lanes
+//   idle through the horizontal pass and Lab/dE; 0.398 vs 0.383 ms.)
+// - the 160-column row-pair planes (30 KiB for three) fit 4 workgroups per CU
+//   three filters at a time, so the channels run in three phases: channel 0
+//   (f0, f1, f2), channel 1 (f3, f4), channel 2 (f5, f6).  Channels 1 and 2
+//   share one gather per region row; channel 2's vertical results wait in
+//   registers through channel 1's horizontal pass.  39,584 B of LDS.
 // ----------------------------------------------------------------------------
 constexpr int kTH16 = 16;
-constexpr int kWideHalf = 64;  // float2 per half of a permuted row-pair row
+constexpr int kWHalfW = 80;  // float2 per half of a 160-column permuted row-pair row
 
 // float2 position of column `col` in a permuted row-pair row: half = bit 1 of
 // col, 16-B slot col >> 2, float2 col & 1.
-template <int WH = kWideHalf>
+template <int WH = kWHalfW>
 __device__ __forceinline__ int wide_pos(int col) {
     return ((col >> 1) & 1) * WH + ((col >> 2) << 1) + (col & 1);
 }
@@ -432,7 +454,7 @@ __device__ __forceinline__ int wide_pos(int col) {
 // Horizontal pass of filter f for item j (output columns 4j .. 4j+3) of a row
 // pair: src = the row-pair row in plane 0; pstride = f32x4 per plane; taps
 // [TLO, THI].
-template <int HALF, int TLO = 0, int THI = 2 * HALF, int WH = kWideHalf>
+template <int HALF, int TLO = 0, int THI = 2 * HALF, int WH = kWHalfW>
 __device__ __forceinline__ void hpass_wide(const f32x4* src, int j, TapsPtr<HALF> taps, int f,
                                            int plane, int pstride, f32x2 (&acc)[4]) {
     constexpr int HR = 4, NQ = (HR + 2 * HALF) / 2;  // 12 reads of 2 columns
@@ -459,7 +481,7 @@ __device__ __forceinline__ void hpass_wide(const f32x4* src, int j, TapsPtr<HALF
 // D of one 16x16 stack block of output-row half `half` -> permuted row pairs:
 // lane (c = l & 15, q = l >> 4) holds rows 8 half + 4(q & 1) .. +3 of the
 // stack's filter q >> 1 at column `col`.
-template <int WH = kWideHalf>
+template <int WH = kWHalfW>
 __device__ __forceinline__ void store_vstack16(float* s_v, const f32x4v& d, int plane_a,
                                                int plane_b, int lk, int col, int half) {
     constexpr int PAIRS = kTH16 / 2, ROW = 2 * WH;  // float2 per row-pair row
@@ -472,183 +494,12 @@ __device__ __forceinline__ void store_vstack16(float* s_v, const f32x4v& d, int 
     v[(plane * PAIRS + p0 + 1) * ROW + pos] = f32x2{d[2], d[3]};
 }
 
-// Index row of K slot (half 1, g, 7): rows 36-39 carry zero taps and are not in
+// Index row of K slot (half 1, g, 1): rows 36-39 carry zero taps and are not in
 // the region: row 35 again (any finite value will do).
 __device__ __forceinline__ constexpr int kv_row_clamped(int half, int g, int j) {
     return kv_row(half, g, j) < 36 ? kv_row(half, g, j) : 35;
 }
 
-template <int DE, bool TRIM>
-__global__ __launch_bounds__(256, 4) void cost16_kernel(CostArgs a, int P_) {
-    constexpr int HALF = 10, RW = 128, TH = kTH16, HR = 4, T2 = 2 * HALF;
-    constexpr int TW = RW - 2 * HALF, RH = TH + 2 * HALF;  // 108 x 16 outputs, 36 region rows
-    constexpr int NRUN = TW / HR;                          // 27 items per row pair, 32 slots
-    constexpr int PAIRS = TH / 2, ROW = 2 * kWideHalf;     // float2 per row-pair row
-    constexpr int PLANE4 = PAIRS * ROW / 2;                // f32x4 per filter plane
-    static_assert(NRUN <= 32 && kv_row(1, 3, 6) < RH, "tile");
-    __shared__ f32x4 s_vq[4 * PLANE4];
-    __shared__ uint32_t s_ox[kMaxK];  // opponent x 2^14 as (hi, lo) f16 pairs: channel 0
-    __shared__ uint2 s_oyz[kMaxK];     // channels 1, 2
-    __shared__ __attribute__((aligned(16))) uint8_t s_idx[RH * RW];
-    __shared__ double s_red[4];
-    float* s_v = reinterpret_cast<float*>(s_vq);
-    const int tid = threadIdx.x;
-    const Geom& g = a.g;
-    const TileItem cur = tile_item<TW, TH>(a, xcd_remap(blockIdx.x, a.ntiles * P_), P_);
-    const TapsPtr<HALF> taps = (TapsPtr<HALF>)(uintptr_t)a.taps;  // H taps x 2^-30
-    const int lane = tid & 63, wv = tid >> 6, lc = lane & 15, lk = lane >> 4;
-    // [trim][half][stack][hi, lo][lane]
-    const uint4* frag = a.vfrag16 + (TRIM ? 2 * 4 * 2 * 64 : 0) + lane;
-    auto F = [&](int half, int st, int hl) { return frag[((half * 4 + st) * 2 + hl) * 64]; };
-
-    TileFill<HALF, RW, TH> fill;
-    fill.issue(a, cur, tid);
-    uint4 A00h = F(0, 0, 0), A00l = F(0, 0, 1), A01h = F(0, 1, 0), A01l = F(0, 1, 1);  // half 0
-    uint4 A10h = F(1, 0, 0), A10l = F(1, 0, 1), A11h = F(1, 1, 0), A11l = F(1, 1, 1);  // half 1
-    // every entry (zeros for tid >= K): zero-weight rows gather arbitrary indices,
-    // and 0 x NaN would be NaN
-    s_ox[tid] = split_f16(fill.ov.x);
-    s_oyz[tid] = make_uint2(split_f16(fill.ov.y), split_f16(fill.ov.z));
-    fill.template commit_idx<RW>(a, s_idx, tid);
-    // H item: row pair m, output columns 4j .. 4j+3
-    const int m = tid >> 5, jr = tid & 31;
-    const bool has_item = jr < NRUN;
-    const int gy0 = cur.y0 + 2 * m, gx0 = cur.x0 + HR * jr;
-    __syncthreads();
-
-    // block bb of wave wv: the 16 columns of parity half bb of columns 32 wv .. +31
-    const int colb = 32 * wv + 4 * (lc >> 1) + (lc & 1);
-    const f32x4* hsrc = &s_vq[(m * ROW) / 2];
-    f32x2 acc0[HR], acc1[HR], acc2[HR];
-#pragma unroll
-    for (int xo = 0; xo < HR; ++xo) acc0[xo] = acc1[xo] = acc2[xo] = f32x2{0.f, 0.f};
-
-    // ---- group 0: channel 0 -> planes 0-2 ----
-    {
-        const f16x8 a00h = __builtin_bit_cast(f16x8, A00h), a00l = __builtin_bit_cast(f16x8, A00l);
-        const f16x8 a01h = __builtin_bit_cast(f16x8, A01h), a01l = __builtin_bit_cast(f16x8, A01l);
-        const f16x8 a10h = __builtin_bit_cast(f16x8, A10h), a10l = __builtin_bit_cast(f16x8, A10l);
-        const f16x8 a11h = __builtin_bit_cast(f16x8, A11h), a11l = __builtin_bit_cast(f16x8, A11l);
-#pragma unroll
-        for (int bb = 0; bb < 2; ++bb) {
-            const int col = colb + 2 * bb;
-            // slots 0-7: half 0; slots 2-9: half 1 (kv_row)
-            uint32_t w[10];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) w[j] = s_ox[s_idx[kv_row(0, lk, j) * RW + col]];
-            w[8] = s_ox[s_idx[kv_row_clamped(1, lk, 6) * RW + col]];
-            w[9] = s_ox[s_idx[kv_row_clamped(1, lk, 7) * RW + col]];
-            f16x8 bh, bl, ch, cl;
-            pack_b(*reinterpret_cast<const uint32_t(*)[8]>(&w[0]), bh, bl);
-            pack_b(*reinterpret_cast<const uint32_t(*)[8]>(&w[2]), ch, cl);
-            store_vstack16(s_v, mfma3(a00h, a00l, bh, bl), 0, 1, lk, col, 0);
-            store_vstack16(s_v, mfma3(a10h, a10l, ch, cl), 0, 1, lk, col, 1);
-            store_vstack16(s_v, mfma3(a01h, a01l, bh, bl), 2, -1, lk, col, 0);
-            store_vstack16(s_v, mfma3(a11h, a11l, ch, cl), 2, -1, lk, col, 1);
-        }
-    }
-    // group 1 stacks, in flight during the group 0 horizontal pass
-    A00h = F(0, 2, 0); A00l = F(0, 2, 1); A01h = F(0, 3, 0); A01l = F(0, 3, 1);
-    A10h = F(1, 2, 0); A10l = F(1, 2, 1); A11h = F(1, 3, 0); A11l = F(1, 3, 1);
-    __syncthreads();
-    if (has_item) {
-        if constexpr (TRIM) hpass_wide<HALF, kTrimLo[0], kTrimHi[0]>(hsrc, jr, taps, 0, 0, PLANE4, acc0);
-        else hpass_wide<HALF, 0, T2>(hsrc, jr, taps, 0, 0, PLANE4, acc0);
-        hpass_wide<HALF, 0, T2>(hsrc, jr, taps, 1, 1, PLANE4, acc0);
-        hpass_wide<HALF, 0, T2>(hsrc, jr, taps, 2, 2, PLANE4, acc0);
-    }
-    __syncthreads();
-
-    // ---- group 1: channels 1, 2 -> planes 0-3 ----
-    {
-        const f16x8 a02h = __builtin_bit_cast(f16x8, A00h), a02l = __builtin_bit_cast(f16x8, A00l);
-        const f16x8 a03h = __builtin_bit_cast(f16x8, A01h), a03l = __builtin_bit_cast(f16x8, A01l);
-        const f16x8 a12h = __builtin_bit_cast(f16x8, A10h), a12l = __builtin_bit_cast(f16x8, A10l);
-        const f16x8 a13h = __builtin_bit_cast(f16x8, A11h), a13l = __builtin_bit_cast(f16x8, A11l);
-#pragma unroll
-        for (int bb = 0; bb < 2; ++bb) {
-            const int col = colb + 2 * bb;
-            uint32_t wy[10], wz[10];  // slots 0-7: half 0; slots 2-9: half 1 (kv_row)
-#pragma unroll
-            for (int j = 0; j < 10; ++j) {
-                const int row = j < 8 ? kv_row(0, lk, j) : kv_row_clamped(1, lk, j - 2);
-                const uint2 e = s_oyz[s_idx[row * RW + col]];
-                wy[j] = e.x; wz[j] = e.y;
-            }
-            f16x8 bh, bl, ch, cl;
-            pack_b(*reinterpret_cast<const uint32_t(*)[8]>(&wy[0]), bh, bl);
-            pack_b(*reinterpret_cast<const uint32_t(*)[8]>(&wy[2]), ch, cl);
-            store_vstack16(s_v, mfma3(a02h, a02l, bh, bl), 0, 1, lk, col, 0);
-            store_vstack16(s_v, mfma3(a12h, a12l, ch, cl), 0, 1, lk, col, 1);
-            pack_b(*reinterpret_cast<const uint32_t(*)[8]>(&wz[0]), bh, bl);
-            pack_b(*reinterpret_cast<const uint32_t(*)[8]>(&wz[2]), ch, cl);
-            store_vstack16(s_v, mfma3(a03h, a03l, bh, bl), 2, 3, lk, col, 0);
-            store_vstack16(s_v, mfma3(a13h, a13l, ch, cl), 2, 3, lk, col, 1);
-        }
-    }
-    // LabRef of the item's 2 x 4 pixels, in flight across the barrier
-    float4 lab[2][3];
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-        const bool ok = has_item && gy0 + r < g.r1 && gx0 < g.W;
-        const uint32_t off = ok ? (uint32_t)((gy0 + r - g.r0) * g.lab_pitch + gx0) : 0u;
-        const float* src3[3] = {a.labL, a.labA, a.labB};
-#pragma unroll
-        for (int ch = 0; ch < 3; ++ch)
-            lab[r][ch] = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(src3[ch]) +
-                                                          (off << 2));  // 32-bit byte offset
-    }
-    __syncthreads();
-
-    double sum = 0.0;
-    if (has_item) {
-        if constexpr (TRIM) {
-            hpass_wide<HALF, kTrimLo[1], kTrimHi[1]>(hsrc, jr, taps, 3, 0, PLANE4, acc1);
-            hpass_wide<HALF, 0, T2>(hsrc, jr, taps, 4, 1, PLANE4, acc1);
-            hpass_wide<HALF, kTrimLo[2], kTrimHi[2]>(hsrc, jr, taps, 5, 2, PLANE4, acc2);
-        } else {
-            hpass_wide<HALF, 0, T2>(hsrc, jr, taps, 3, 0, PLANE4, acc1);
-            hpass_wide<HALF, 0, T2>(hsrc, jr, taps, 4, 1, PLANE4, acc1);
-            hpass_wide<HALF, 0, T2>(hsrc, jr, taps, 5, 2, PLANE4, acc2);
-        }
-        hpass_wide<HALF, 0, T2>(hsrc, jr, taps, 6, 3, PLANE4, acc2);
-        float part = 0.f;
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            const float Ls[4] = {lab[r][0].x, lab[r][0].y, lab[r][0].z, lab[r][0].w};
-            const float As[4] = {lab[r][1].x, lab[r][1].y, lab[r][1].z, lab[r][1].w};
-            const float Bs[4] = {lab[r][2].x, lab[r][2].y, lab[r][2].z, lab[r][2].w};
-#pragma unroll
-            for (int xo = 0; xo < HR; ++xo) {
-                const float3 g3 = opp2g_fast(acc0[xo][r], acc1[xo][r], acc2[xo][r], a.m_lab);
-                const float e = delta_e_g<DE>(Ls[xo], As[xo], Bs[xo], g3);
-                part += (gy0 + r < g.r1 && gx0 + xo < g.W) ? e : 0.f;
-            }
-        }
-        sum = (double)part;
-    }
-    sum = wave_sum_to_lane63(sum);
-    if ((tid & 63) == 63) s_red[tid >> 6] = sum;
-    __syncthreads();
-    if (tid == 0)
-        a.partial[(int64_t)cur.p * a.ntiles + cur.tile] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
-}
-
-// ----------------------------------------------------------------------------
-// cost16w: 16 x 128 tiles (option cost_cols 128).  cost16's 108-column tile
-// gives 27 horizontal items per row pair to 32 threads: 16% of the lanes idle
-// through the horizontal pass and Lab/dE, its two largest VALU parts.  128
-// output columns give 32 items per row pair -- every lane busy -- for a
-// 148-column region: 10 vertical-pass blocks of 16 columns (5 ranges of 32,
-// blocks w, w+4, w+8 on wave w), 25% more vertical work for 18.5% more
-// outputs.  The 160-column row-pair planes (30 KiB for three) only fit 4
-// workgroups per CU three filters at a time, so the channels run in three
-// phases: channel 0 (f0, f1, f2), channel 1 (f3, f4), channel 2 (f5, f6).
-// Channels 1 and 2 share one gather per region row; channel 2's vertical
-// results wait in registers through channel 1's horizontal pass.  39,584 B of
-// LDS.
-// ----------------------------------------------------------------------------
-constexpr int kWHalfW = 80;  // float2 per half of a 160-column permuted row-pair row
 
 template <int DE, bool TRIM>
 __global__ __launch_bounds__(256, 4) void cost16w_kernel(CostArgs a, int P_) {
@@ -658,7 +509,7 @@ __global__ __launch_bounds__(256, 4) void cost16w_kernel(CostArgs a, int P_) {
     constexpr int PAIRS = TH / 2, ROW = 2 * kWHalfW;        // float2 per row-pair row
     constexpr int PLANE4 = PAIRS * ROW / 2;                 // f32x4 per filter plane
     constexpr int NBLK = RW / 16;                           // vertical-pass blocks
-    static_assert(TW / HR == 32 && kv_row(1, 3, 6) < RH && RWL <= RW, "tile");
+    static_assert(TW / HR == 32 && kv_row(1, 3, 0) < RH && RWL <= RW, "tile");
     __shared__ f32x4 s_vq[3 * PLANE4];
     __shared__ uint32_t s_ox[kMaxK];  // opponent x 2^14 as (hi, lo) f16 pairs: channel 0
     __shared__ uint2 s_oyz[kMaxK];     // channels 1, 2
@@ -698,6 +549,7 @@ __global__ __launch_bounds__(256, 4) void cost16w_kernel(CostArgs a, int P_) {
     // hold 3 blocks, sets 2 and 3 hold 2: the sets rotate with the workgroup,
     // so the extra blocks do not land on the same SIMDs in every workgroup.
     const int wset = (wv + (int)blockIdx.x) & 3;
+    auto B = [](const u32x4& u) { return __builtin_bit_cast(f16x8, u); };
     auto vpass0 = [&](const f16x8& h0h, const f16x8& h0l, const f16x8& h1h, const f16x8& h1l,
                       const f16x8& k0h, const f16x8& k0l, const f16x8& k1h, const f16x8& k1l) {
         const uint32_t* tab = s_ox;
@@ -706,18 +558,21 @@ __global__ __launch_bounds__(256, 4) void cost16w_kernel(CostArgs a, int P_) {
             const int b = wset + 4 * i;
             if (b >= NBLK) break;
             const int col = 32 * (b >> 1) + 4 * (lc >> 1) + (lc & 1) + 2 * (b & 1);
-            uint32_t w[10];  // slots 0-7: half 0; slots 2-9: half 1 (kv_row)
+            uint32_t w[10];  // slots 0-7: half 0; w[8], w[9]: half 1's slots 0, 1 (kv_row)
 #pragma unroll
             for (int j = 0; j < 8; ++j) w[j] = tab[s_idx[kv_row(0, lk, j) * RW + col]];
-            w[8] = tab[s_idx[kv_row_clamped(1, lk, 6) * RW + col]];
-            w[9] = tab[s_idx[kv_row_clamped(1, lk, 7) * RW + col]];
-            f16x8 bh, bl, chh, chl;
-            pack_b(*reinterpret_cast<const uint32_t(*)[8]>(&w[0]), bh, bl);
-            pack_b(*reinterpret_cast<const uint32_t(*)[8]>(&w[2]), chh, chl);
-            store_vstack16<kWHalfW>(s_v, mfma3(h0h, h0l, bh, bl), 0, 1, lk, col, 0);
-            store_vstack16<kWHalfW>(s_v, mfma3(h1h, h1l, chh, chl), 0, 1, lk, col, 1);
-            store_vstack16<kWHalfW>(s_v, mfma3(k0h, k0l, bh, bl), 2, -1, lk, col, 0);
-            store_vstack16<kWHalfW>(s_v, mfma3(k1h, k1l, chh, chl), 2, -1, lk, col, 1);
+            w[8] = tab[s_idx[kv_row_clamped(1, lk, 0) * RW + col]];
+            w[9] = tab[s_idx[kv_row_clamped(1, lk, 1) * RW + col]];
+            u32x4 bh, bl;
+            uint32_t nh, nl;
+            pack_b_halves(w, bh, bl, nh, nl);
+            const f32x4v d00 = mfma3(h0h, h0l, B(bh), B(bl)), d01 = mfma3(k0h, k0l, B(bh), B(bl));
+            bh[0] = nh; bl[0] = nl;
+            const f32x4v d10 = mfma3(h1h, h1l, B(bh), B(bl)), d11 = mfma3(k1h, k1l, B(bh), B(bl));
+            store_vstack16<kWHalfW>(s_v, d00, 0, 1, lk, col, 0);
+            store_vstack16<kWHalfW>(s_v, d01, 2, -1, lk, col, 0);
+            store_vstack16<kWHalfW>(s_v, d10, 0, 1, lk, col, 1);
+            store_vstack16<kWHalfW>(s_v, d11, 2, -1, lk, col, 1);
         }
     };
     auto H = [](const uint4& u) { return __builtin_bit_cast(f16x8, u); };
@@ -743,22 +598,25 @@ __global__ __launch_bounds__(256, 4) void cost16w_kernel(CostArgs a, int P_) {
         const int b = wset + 4 * i;
         if (b >= NBLK) break;
         const int col = 32 * (b >> 1) + 4 * (lc >> 1) + (lc & 1) + 2 * (b & 1);
-        uint32_t wy[10], wz[10];  // slots 0-7: half 0; slots 2-9: half 1 (kv_row)
+        uint32_t wy[10], wz[10];  // slots 0-7: half 0; [8], [9]: half 1's slots 0, 1
 #pragma unroll
         for (int j = 0; j < 10; ++j) {
-            const int row = j < 8 ? kv_row(0, lk, j) : kv_row_clamped(1, lk, j - 2);
+            const int row = j < 8 ? kv_row(0, lk, j) : kv_row_clamped(1, lk, j - 8);
             const uint2 e = s_oyz[s_idx[row * RW + col]];
             wy[j] = e.x; wz[j] = e.y;
         }
-        f16x8 bh, bl, chh, chl;
-        pack_b(*reinterpret_cast<const uint32_t(*)[8]>(&wy[0]), bh, bl);
-        pack_b(*reinterpret_cast<const uint32_t(*)[8]>(&wy[2]), chh, chl);
-        store_vstack16<kWHalfW>(s_v, mfma3(H(A00h), H(A00l), bh, bl), 0, 1, lk, col, 0);
-        store_vstack16<kWHalfW>(s_v, mfma3(H(A10h), H(A10l), chh, chl), 0, 1, lk, col, 1);
-        pack_b(*reinterpret_cast<const uint32_t(*)[8]>(&wz[0]), bh, bl);
-        pack_b(*reinterpret_cast<const uint32_t(*)[8]>(&wz[2]), chh, chl);
-        d5[i][0] = mfma3(H(A01h), H(A01l), bh, bl);
-        d5[i][1] = mfma3(H(A11h), H(A11l), chh, chl);
+        u32x4 bh, bl;
+        uint32_t nh, nl;
+        pack_b_halves(wy, bh, bl, nh, nl);
+        const f32x4v d30 = mfma3(H(A00h), H(A00l), B(bh), B(bl));
+        bh[0] = nh; bl[0] = nl;
+        const f32x4v d31 = mfma3(H(A10h), H(A10l), B(bh), B(bl));
+        store_vstack16<kWHalfW>(s_v, d30, 0, 1, lk, col, 0);
+        store_vstack16<kWHalfW>(s_v, d31, 0, 1, lk, col, 1);
+        pack_b_halves(wz, bh, bl, nh, nl);
+        d5[i][0] = mfma3(H(A01h), H(A01l), B(bh), B(bl));
+        bh[0] = nh; bl[0] = nl;
+        d5[i][1] = mfma3(H(A11h), H(A11l), B(bh), B(bl));
     }
     __syncthreads();
     if constexpr (TRIM) hpass_wide<HALF, kTrimLo[1], kTrimHi[1], kWHalfW>(hsrc, jr, taps, 3, 0, PLANE4, acc1);
@@ -986,9 +844,9 @@ void build_fast_taps(const float* k1, const float* k2, const float* k3, const fl
 
 // a.taps = the two CostTaps<10> of build_fast_taps
 
-// tile_rows: 8 (cost_mfma_kernel) or 16 (cost16_kernel)
-void fast_tile_dims(int W, int own_rows, int tile_rows, int tile_cols, int* tiles_x, int* ntiles) {
-    const int tw = tile_rows == kTH16 && tile_cols == 128 ? 128 : kFastTW;
+// tile_rows: 8 (cost_mfma_kernel, 8 x 108 tiles) or 16 (cost16w_kernel, 16 x 128 tiles)
+void fast_tile_dims(int W, int own_rows, int tile_rows, int* tiles_x, int* ntiles) {
+    const int tw = tile_rows == kTH16 ? 128 : kFastTW;
     *tiles_x = (W + tw - 1) / tw;
     *ntiles = *tiles_x * ((own_rows + tile_rows - 1) / tile_rows);
 }
@@ -996,17 +854,14 @@ void fast_tile_dims(int W, int own_rows, int tile_rows, int tile_cols, int* tile
 // a.taps = the two CostTaps<10> of build_fast_taps; [1] carries the vertical
 // pass's 2^30 scale in its horizontal taps.
 hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, bool trim, int tile_rows,
-                            int tile_cols, hipStream_t s) {
+                            hipStream_t s) {
     CostArgs a = a0;
     a.taps = static_cast<const char*>(a0.taps) + sizeof(CostTaps<10>);
     const dim3 grid((unsigned)(a.ntiles * P));
 #define HQ_COST(KN, DEV, TR) HQ_LAUNCH((KN<DEV, TR>), grid, dim3(256), 0, s, a, P)
-    if (tile_rows == kTH16 && tile_cols == 128) {
+    if (tile_rows == kTH16) {
         if (de == 0) { if (trim) HQ_COST(cost16w_kernel, 0, true); else HQ_COST(cost16w_kernel, 0, false); }
         else { if (trim) HQ_COST(cost16w_kernel, 1, true); else HQ_COST(cost16w_kernel, 1, false); }
-    } else if (tile_rows == kTH16) {
-        if (de == 0) { if (trim) HQ_COST(cost16_kernel, 0, true); else HQ_COST(cost16_kernel, 0, false); }
-        else { if (trim) HQ_COST(cost16_kernel, 1, true); else HQ_COST(cost16_kernel, 1, false); }
     } else {
         if (de == 0) { if (trim) HQ_COST(cost_mfma_kernel, 0, true); else HQ_COST(cost_mfma_kernel, 0, false); }
         else { if (trim) HQ_COST(cost_mfma_kernel, 1, true); else HQ_COST(cost_mfma_kernel, 1, false); }

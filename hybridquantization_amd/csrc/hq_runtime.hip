@@ -24,10 +24,9 @@ hipError_t launch_sa_step(const SaArgs&, hipStream_t);
 void set_launch_events(hipEvent_t start, hipEvent_t stop);
 hipError_t launch_build_grid(const GridArgs&, int P, hipStream_t);
 hipError_t launch_assign(const AssignArgs&, int P, hipStream_t);
-void fast_tile_dims(int W, int own_rows, int tile_rows, int tile_cols, int* tiles_x, int* ntiles);
+void fast_tile_dims(int W, int own_rows, int tile_rows, int* tiles_x, int* ntiles);
 void opp2xyz_over_illum(const float inv_illum[3], float m[9]);
-hipError_t launch_cost_fast(const CostArgs&, int P, int de, bool trim, int tile_rows, int tile_cols,
-                            hipStream_t);
+hipError_t launch_cost_fast(const CostArgs&, int P, int de, bool trim, int tile_rows, hipStream_t);
 size_t vpass_f16_stack_fragment_halves();
 void build_vpass_f16_stack_fragments(const float* k1, const float* k2, const float* k3,
                                      const float* absk3, uint16_t* out);
@@ -114,8 +113,7 @@ struct hq_ctx {
     // options
     int G2 = 32;           // argmin grid resolution (0 = exhaustive)
     int cost_variant = 0;  // 0 tiled (default), 1 generic two-pass
-    int cost_rows = 16;    // fast path tile rows: 16 (cost16_kernel) or 8 (cost_mfma_kernel)
-    int cost_cols = 128;   // 16-row tiles: 128 (cost16w_kernel) or 108 output columns (cost16_kernel)
+    int cost_rows = 16;    // fast path tiles: 16 x 128 (cost16w_kernel) or 8 x 108 (cost_mfma_kernel)
     int assign_blocks_per_cu = 8;
     int shard_solo = 0;    // experiment: a sharded search without a communicator (per-rank timing)
     int sa_device = 1;     // hq_search_*: 1 = SWASA iterations resident on the device (no host
@@ -331,7 +329,7 @@ int ensure_population(hq_ctx* c, int P, int K) {
     const int64_t l1p = round_up((int64_t)G1 * G1 * G1 * 32, 256);
     const int64_t l2g = round_up((int64_t)G2 * G2 * G2 * 64, 256);  // per group of 4 palettes
     int tiles_x, ntiles;
-    fast_tile_dims(g.W, g.r1 - g.r0, 8, 108, &tiles_x, &ntiles);  // the most tiles of any config
+    fast_tile_dims(g.W, g.r1 - g.r0, 8, &tiles_x, &ntiles);  // the most tiles of any config
     const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
     const int64_t gen_blocks = (n_own + 255) / 256;
     const int64_t nparts = std::max<int64_t>(ntiles, gen_blocks);
@@ -416,10 +414,10 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev) {
         ca.partial = c->d_partial.as<double>();
         ca.g = g;
         ca.K = K;
-        fast_tile_dims(g.W, g.r1 - g.r0, c->cost_rows, c->cost_cols, &ca.tiles_x, &ca.ntiles);
+        fast_tile_dims(g.W, g.r1 - g.r0, c->cost_rows, &ca.tiles_x, &ca.ntiles);
         opp2xyz_over_illum(inv, ca.m_lab);
         timed(2);
-        e = launch_cost_fast(ca, P, c->de_type, c->trim && c->trim_ok, c->cost_rows, c->cost_cols, s);
+        e = launch_cost_fast(ca, P, c->de_type, c->trim && c->trim_ok, c->cost_rows, s);
         untimed();
         HIP_TRY(c, e);
         nparts = ca.ntiles;
@@ -1098,9 +1096,7 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
     } else if (!std::strcmp(name, "cost_rows")) {
         if (value != 8 && value != 16) return fail(c, HQ_ERR_ARG, "cost_rows must be 8 or 16");
         c->cost_rows = value;
-    } else if (!std::strcmp(name, "cost_cols")) {
-        if (value != 108 && value != 128) return fail(c, HQ_ERR_ARG, "cost_cols must be 108 or 128");
-        c->cost_cols = value;
+
     } else if (!std::strcmp(name, "sa_device")) {
         c->sa_device = value != 0;
     } else if (!std::strcmp(name, "shard_solo")) {

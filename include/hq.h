@@ -184,8 +184,7 @@ int hq_profile_reset(hq_ctx *ctx);
  *   "grid"         argmin pruning resolution G2: 0 = exhaustive, 16, 32 (default), 64
  *   "cost_variant" 0 = fast tiled path (default; 21-tap filters), 1 = generic
  *                  two-pass path (any filter length; the fast path's cross-check)
- *   "cost_rows"    fast path tile rows: 16 (default) or 8 (8 x 108 tiles)
- *   "cost_cols"    16-row tiles: 128 output columns (default) or 108
+ *   "cost_rows"    fast path tiles: 16 (16 x 128 outputs, default) or 8 (8 x 108)
  *   "trim"         1 = skip the narrow k1 filters' taps below 1e-9 of their peak
  *                  (default; only when the filters allow it), 0 = all taps
  *   "assign_blocks_per_cu" workgroups per CU of the assign grid (default 8)
