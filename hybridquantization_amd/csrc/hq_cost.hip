@@ -650,7 +650,7 @@ __global__ __launch_bounds__(256, 4) void cost16w_kernel(CostArgs a, int P_) {
     else hpass_wide<HALF, 0, T2, kWHalfW>(hsrc, jr, taps, 5, 0, PLANE4, acc2);
     hpass_wide<HALF, 0, T2, kWHalfW>(hsrc, jr, taps, 6, 1, PLANE4, acc2);
 
-    float part = 0.f;
+    float e[2][HR];
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
         const float Ls[4] = {lab[r][0].x, lab[r][0].y, lab[r][0].z, lab[r][0].w};
@@ -659,9 +659,22 @@ __global__ __launch_bounds__(256, 4) void cost16w_kernel(CostArgs a, int P_) {
 #pragma unroll
         for (int xo = 0; xo < HR; ++xo) {
             const float3 g3 = opp2g_fast(acc0[xo][r], acc1[xo][r], acc2[xo][r], a.m_lab);
-            const float e = delta_e_g<DE>(Ls[xo], As[xo], Bs[xo], g3);
-            part += (gy0 + r < g.r1 && gx0 + xo < g.W) ? e : 0.f;
+            e[r][xo] = delta_e_g<DE>(Ls[xo], As[xo], Bs[xo], g3);
         }
+    }
+    // tiles inside the image and shard (all but the last tile column and row)
+    // sum without per-pixel masks
+    float part = 0.f;
+    if (cur.x0 + TW <= g.W && cur.y0 + TH <= g.r1) {
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int xo = 0; xo < HR; ++xo) part += e[r][xo];
+    } else {
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int xo = 0; xo < HR; ++xo) part += (gy0 + r < g.r1 && gx0 + xo < g.W) ? e[r][xo] : 0.f;
     }
     double sum = wave_sum_to_lane63((double)part);
     if ((tid & 63) == 63) s_red[tid >> 6] = sum;

@@ -49,8 +49,8 @@ __device__ __forceinline__ float lab_f(float t) {  // CL:137
 #define LAB_G3 1560896.0f  // 116^3
 __device__ __forceinline__ float lab_g_fast(float t) {
     constexpr float thr = LAB_DELTA3 * LAB_G3;  // t > delta^3 <=> t' > delta^3 116^3
-    const float tc = fmaxf(t, thr);             // cbrt branch only used for t' > thr > 0
-    const float y = __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(tc) * (1.0f / 3.0f));
+    // y is only selected for t' > thr > 0 (for t' <= 0 it is 0 or NaN, discarded)
+    const float y = __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(t) * (1.0f / 3.0f));
     const float lin = fmaf(LAB_KAPPA / LAB_G3, t, 16.0f);
     return t > thr ? y : lin;
 }
