@@ -61,7 +61,8 @@ constexpr float kVOutScale = 1.0f / (16384.0f * 65536.0f);  // 2^-30
 // Half 0 (output rows 0-7): rows 4j + g (lane group g holds every 4th row).
 // Half 1 (output rows 8-15 of a 16-row tile, rows 8-39): slots 2-7 are half
 // 0's slots 2-7 (rows 8-31), slots 0 and 1 are rows 32 + g and 36 + g (rows
-// 36-39 carry zero taps).  Every lane gathers 2 new values for half 1, and
+// 36-39 carry zero taps, so slot 1 needs no gather: 0).  Every lane gathers one
+// new value for half 1, and
 // half 1's B operand is half 0's with only its first dword replaced (same
 // registers, no moves: pack_b_halves).  The A fragments permute K to match.
 __host__ __device__ __forceinline__ constexpr int kv_row(int half, int g, int j) {
@@ -421,8 +422,9 @@ __global__ __launch_bounds__(256, 6) void cost_mfma_kernel(CostArgs a, int P_) {
 // the kernel's LDS traffic; FP32 VALU issue (horizontal taps, Lab/dE) bounds it.
 // - vertical pass: output rows 0-7 take region rows 0-31, rows 8-15 take rows
 //   8-39 (36-39 zero-weight): with lane group g holding every 4th row (kv_row),
-//   each lane keeps six of its eight half-0 values for half 1 and gathers two
-//   more -- 40 gathered rows per 16 output rows instead of 64, no divergence.
+//   each lane keeps six of its eight half-0 values for half 1, gathers one
+//   more and zeroes one (rows 36-39) -- 36 gathered rows per 16 output rows
+//   instead of 64, no divergence.
 //   10 blocks of 16 columns (5 ranges of 32) cover the 148 region columns
 //   (+12 unread): each block is the 16 columns of one parity half of a range
 //   (lane n -> column 4(n >> 1) + 2 (b & 1) + (n & 1)), so its stores fill 16
@@ -494,11 +496,6 @@ __device__ __forceinline__ void store_vstack16(float* s_v, const f32x4v& d, int 
     v[(plane * PAIRS + p0 + 1) * ROW + pos] = f32x2{d[2], d[3]};
 }
 
-// Index row of K slot (half 1, g, 1): rows 36-39 carry zero taps and are not in
-// the region: row 35 again (any finite value will do).
-__device__ __forceinline__ constexpr int kv_row_clamped(int half, int g, int j) {
-    return kv_row(half, g, j) < 36 ? kv_row(half, g, j) : 35;
-}
 
 
 template <int DE, bool TRIM>
@@ -561,8 +558,8 @@ __global__ __launch_bounds__(256, 4) void cost16w_kernel(CostArgs a, int P_) {
             uint32_t w[10];  // slots 0-7: half 0; w[8], w[9]: half 1's slots 0, 1 (kv_row)
 #pragma unroll
             for (int j = 0; j < 8; ++j) w[j] = tab[s_idx[kv_row(0, lk, j) * RW + col]];
-            w[8] = tab[s_idx[kv_row_clamped(1, lk, 0) * RW + col]];
-            w[9] = tab[s_idx[kv_row_clamped(1, lk, 1) * RW + col]];
+            w[8] = tab[s_idx[kv_row(1, lk, 0) * RW + col]];
+            w[9] = 0u;  // K slot (half 1, g, 1) = row 36 + g: zero taps, not in the region
             u32x4 bh, bl;
             uint32_t nh, nl;
             pack_b_halves(w, bh, bl, nh, nl);
@@ -600,11 +597,12 @@ __global__ __launch_bounds__(256, 4) void cost16w_kernel(CostArgs a, int P_) {
         const int col = 32 * (b >> 1) + 4 * (lc >> 1) + (lc & 1) + 2 * (b & 1);
         uint32_t wy[10], wz[10];  // slots 0-7: half 0; [8], [9]: half 1's slots 0, 1
 #pragma unroll
-        for (int j = 0; j < 10; ++j) {
-            const int row = j < 8 ? kv_row(0, lk, j) : kv_row_clamped(1, lk, j - 8);
+        for (int j = 0; j < 9; ++j) {
+            const int row = j < 8 ? kv_row(0, lk, j) : kv_row(1, lk, 0);
             const uint2 e = s_oyz[s_idx[row * RW + col]];
             wy[j] = e.x; wz[j] = e.y;
         }
+        wy[9] = wz[9] = 0u;  // row 36 + g: zero taps, not in the region
         u32x4 bh, bl;
         uint32_t nh, nl;
         pack_b_halves(wy, bh, bl, nh, nl);
