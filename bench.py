@@ -199,6 +199,30 @@ def main():
     if world > 1:
         hqd.init_comm(m, dist, world, rank)
 
+    P = args.population
+    # BASELINE config 3's real search (imax = 5000, default schedule) is its own
+    # measurement (extra key `full_search_c3`).  It runs before the benchmark's
+    # search: the GPU's clocks take ~0.1 s of sustained load to settle, and a
+    # timed region of a few steps straight after set-up measured ~7% slow (20
+    # vs 100 steps: 0.72 vs 0.67 ms).  At N > 1 every rank runs it, device-
+    # resident with the communicator (the same path as the timed steps).
+    search_line = None
+    if not args.no_full_search:
+        dev, bdev = full_search(lib, _lib, m, args.K, P, args.seed, 1)
+        where = (f"rows [{r0}, {r1}) of an {args.shard_of}-way split, no collective" if args.shard_of > 0
+                 else f"{world} GPU(s)")
+        search_line = {"config": f"BASELINE config 3: {W}x{H}, K={args.K}, P={P}, imax=5000, "
+                                 "default SWASA schedule (HQ:197-224), seed "
+                                 f"{args.seed}, {where}",
+                       "device_resident": dev,
+                       "ms_per_iteration_device": round(dev["wall_s"] / max(dev["iterations"], 1) * 1e3, 4)}
+        if world == 1 and args.shard_of == 0:  # the host-driven driver must agree bit for bit
+            host, bhost = full_search(lib, _lib, m, args.K, P, args.seed, 0)
+            search_line["host_driven"] = host
+            search_line["device_host_agree"] = bool(dev["best_error"] == host["best_error"]
+                                                    and np.array_equal(bdev, bhost)
+                                                    and dev["iterations"] == host["iterations"])
+
     sw = hq.SWASA(population=args.population, imax=10 ** 9, seed=args.seed)
     params = sw.params()
     search = C.c_void_p()
@@ -241,7 +265,6 @@ def main():
     lib.hq_search_best(search, _lib.fptr(best), C.byref(berr), C.byref(it))
     lib.hq_search_destroy(search)
 
-    P = args.population
     n_own = W * (r1 - r0)
     value = W * H * P * args.steps / elapsed / 1e6
     if args.shard_of > 0:  # experiment: one rank's rows only (per-rank rate, not a job total)
@@ -271,18 +294,6 @@ def main():
     cfg_name = {(4096, 256, 4): "BASELINE config 3", (1024, 64, 1): "BASELINE config 2",
                 (8192, 256, 4): "BASELINE config 4", (4096, 256, 64): "BASELINE config 5",
                 (256, 16, 4): "BASELINE config 1"}.get(shape, "not a BASELINE config")
-    search_line = None
-    if rank == 0 and world == 1 and args.shard_of == 0 and not args.no_full_search:
-        dev, bdev = full_search(lib, _lib, m, args.K, P, args.seed, 1)
-        host, bhost = full_search(lib, _lib, m, args.K, P, args.seed, 0)
-        search_line = {"config": f"BASELINE config 3: {W}x{H}, K={args.K}, P={P}, imax=5000, "
-                                 "default SWASA schedule (HQ:197-224), seed "
-                                 f"{args.seed}",
-                       "device_resident": dev, "host_driven": host,
-                       "ms_per_iteration_device": round(dev["wall_s"] / max(dev["iterations"], 1) * 1e3, 4),
-                       "device_host_agree": bool(dev["best_error"] == host["best_error"]
-                                                 and np.array_equal(bdev, bhost)
-                                                 and dev["iterations"] == host["iterations"])}
     out = {
         "metric": "Mpixel*evals/s (SWASA dE cost) at 4096x4096 K=256",
         "value": round(value, 2),
@@ -327,7 +338,7 @@ def main():
         "kernel_avg_ms": {k: round(v[0], 4) for k, v in prof.items()},
         "best_error": berr.value,
     }
-    if search_line is not None:
+    if search_line is not None and rank == 0:
         out["full_search_c3"] = search_line
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)
