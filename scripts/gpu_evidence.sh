@@ -13,7 +13,7 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $E/smoke.
 rc=$?; echo "smoke rc=$rc"; tail -2 $E/smoke.log; fatal $rc smoke
 timeout -k 10 600 python bench.py > $E/bench.json 2> $E/bench.err
 rc=$?; echo "bench rc=$rc"; cut -c1-300 $E/bench.json; fatal $rc bench
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $E/trace -o bench -- python3 bench.py --no-cpu-baseline --no-full-search > $E/bench_under_rocprof.json 2> $E/bench_under_rocprof.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $E/trace -o bench -- python3 bench.py --no-cpu-baseline > $E/bench_under_rocprof.json 2> $E/bench_under_rocprof.err
 rc=$?; echo "trace rc=$rc"; fatal $rc trace
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 120 rocprofv3 --pmc $c --kernel-include-regex "cost|assign|build_grid|sa_step|finalize" -f csv -d $E/traffic_$c -o run -- python3 scripts/profile_eval.py --evals 3 > $E/traffic_$c.log 2>&1
@@ -27,10 +27,12 @@ for set in "SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ
   rc=$?; echo "pmc$i rc=$rc"; fatal $rc pmc$i
 done
 : > $E/configs.jsonl
-for cfg in "--size 1024 --K 64 --population 1" "--population 1" "" "--size 8192 --shard-of 8" "--population 64 --steps 10 --warmup 2"; do
-  timeout -k 10 300 python bench.py --no-cpu-baseline --no-full-search $cfg >> $E/configs.jsonl 2>> $E/configs.err
+# each line starts on settled clocks: the full C3-schedule search of its shape first
+# (C5's 64-palette search would take ~1 min: 10 warm-up steps, ~0.1 s, instead)
+for cfg in "--size 1024 --K 64 --population 1" "--population 1" "" "--size 8192 --shard-of 8" "--population 64 --steps 20 --warmup 10 --no-full-search"; do
+  timeout -k 10 300 python bench.py --no-cpu-baseline $cfg >> $E/configs.jsonl 2>> $E/configs.err
   rc=$?; echo "config [$cfg] rc=$rc"; fatal $rc "config $cfg"
 done
-timeout -k 10 200 python bench.py --no-cpu-baseline --no-full-search --shard-of 8 --steps 200 > $E/shard8.json 2> $E/shard8.err
+timeout -k 10 200 python bench.py --no-cpu-baseline --shard-of 8 --steps 200 > $E/shard8.json 2> $E/shard8.err
 rc=$?; echo "shard8 rc=$rc"; cut -c1-200 $E/shard8.json; fatal $rc shard8
 exit 0
