@@ -1,7 +1,7 @@
 """Instruction mix of one kernel in a hipcc -S listing, per loop body.
 
     hipcc --offload-arch=gfx950 -O3 --cuda-device-only -S -o k.s hq_kernels.hip
-    python scripts/isa_mix.py k.s cost_tile_kernelILi10ELi128ELi8ELi4ELi0ELi3ELb1
+    python scripts/isa_mix.py k.s cost16w_kernelILi0ELb1
 
 A loop is a label that a later s_cbranch/s_branch jumps back to; its body is the
 text between the label and that branch.  Used to see where VALU issue goes
