@@ -482,18 +482,21 @@ __device__ __forceinline__ void hpass_wide(const f32x4* src, int j, TapsPtr<HALF
 
 // D of one 16x16 stack block of output-row half `half` -> permuted row pairs:
 // lane (c = l & 15, q = l >> 4) holds rows 8 half + 4(q & 1) .. +3 of the
-// stack's filter q >> 1 at column `col`.
-template <int WH = kWHalfW>
-__device__ __forceinline__ void store_vstack16(float* s_v, const f32x4v& d, int plane_a,
-                                               int plane_b, int lk, int col, int half) {
-    constexpr int PAIRS = kTH16 / 2, ROW = 2 * WH;  // float2 per row-pair row
-    const int plane = lk < 2 ? plane_a : plane_b;
-    if (plane < 0) return;
-    const int p0 = 4 * half + 2 * (lk & 1);
-    f32x2* v = reinterpret_cast<f32x2*>(s_v);
-    const int pos = wide_pos<WH>(col);
-    v[(plane * PAIRS + p0) * ROW + pos] = f32x2{d[0], d[1]};
-    v[(plane * PAIRS + p0 + 1) * ROW + pos] = f32x2{d[2], d[3]};
+// stack's filter q >> 1 at its column.  Addresses hoisted: `base` = the
+// lane's float2 slot of block set i = 0, half 0 in its plane (vstack_base);
+// block i and half add compile-time offsets (block b + 4 moves 64 columns =
+// 32 float2 of the permuted row).
+template <int WH>
+__device__ __forceinline__ f32x2* vstack_base(float* s_v, int plane, int lk, int col0) {
+    constexpr int PAIRS = kTH16 / 2, ROW = 2 * WH;
+    return reinterpret_cast<f32x2*>(s_v) + (plane * PAIRS + 2 * (lk & 1)) * ROW + wide_pos<WH>(col0);
+}
+template <int WH>
+__device__ __forceinline__ void store_vstack_at(f32x2* base, const f32x4v& d, int i, int half) {
+    constexpr int ROW = 2 * WH;
+    f32x2* v = base + 4 * half * ROW + 32 * i;
+    v[0] = f32x2{d[0], d[1]};
+    v[ROW] = f32x2{d[2], d[3]};
 }
 
 
@@ -546,6 +549,10 @@ __global__ __launch_bounds__(256, 4) void cost16w_kernel(CostArgs a, int P_) {
     // hold 3 blocks, sets 2 and 3 hold 2: the sets rotate with the workgroup,
     // so the extra blocks do not land on the same SIMDs in every workgroup.
     const int wset = (wv + (int)blockIdx.x) & 3;
+    // block wset + 4i covers column col0 + 64 i of its parity half
+    const int col0 = 32 * (wset >> 1) + 4 * (lc >> 1) + (lc & 1) + 2 * (wset & 1);
+    f32x2* const st01 = vstack_base<kWHalfW>(s_v, lk < 2 ? 0 : 1, lk, col0);  // stacks -> planes 0, 1
+    f32x2* const st2 = vstack_base<kWHalfW>(s_v, 2, lk, col0);                // (f2, -) -> plane 2
     auto B = [](const u32x4& u) { return __builtin_bit_cast(f16x8, u); };
     auto vpass0 = [&](const f16x8& h0h, const f16x8& h0l, const f16x8& h1h, const f16x8& h1l,
                       const f16x8& k0h, const f16x8& k0l, const f16x8& k1h, const f16x8& k1l) {
@@ -554,7 +561,7 @@ __global__ __launch_bounds__(256, 4) void cost16w_kernel(CostArgs a, int P_) {
         for (int i = 0; i < 3; ++i) {
             const int b = wset + 4 * i;
             if (b >= NBLK) break;
-            const int col = 32 * (b >> 1) + 4 * (lc >> 1) + (lc & 1) + 2 * (b & 1);
+            const int col = col0 + 64 * i;
             uint32_t w[10];  // slots 0-7: half 0; w[8], w[9]: half 1's slots 0, 1 (kv_row)
 #pragma unroll
             for (int j = 0; j < 8; ++j) w[j] = tab[s_idx[kv_row(0, lk, j) * RW + col]];
@@ -566,10 +573,12 @@ __global__ __launch_bounds__(256, 4) void cost16w_kernel(CostArgs a, int P_) {
             const f32x4v d00 = mfma3(h0h, h0l, B(bh), B(bl)), d01 = mfma3(k0h, k0l, B(bh), B(bl));
             bh[0] = nh; bl[0] = nl;
             const f32x4v d10 = mfma3(h1h, h1l, B(bh), B(bl)), d11 = mfma3(k1h, k1l, B(bh), B(bl));
-            store_vstack16<kWHalfW>(s_v, d00, 0, 1, lk, col, 0);
-            store_vstack16<kWHalfW>(s_v, d01, 2, -1, lk, col, 0);
-            store_vstack16<kWHalfW>(s_v, d10, 0, 1, lk, col, 1);
-            store_vstack16<kWHalfW>(s_v, d11, 2, -1, lk, col, 1);
+            store_vstack_at<kWHalfW>(st01, d00, i, 0);
+            store_vstack_at<kWHalfW>(st01, d10, i, 1);
+            if (lk < 2) {  // the (f2, -) stack's second filter slot is empty
+                store_vstack_at<kWHalfW>(st2, d01, i, 0);
+                store_vstack_at<kWHalfW>(st2, d11, i, 1);
+            }
         }
     };
     auto H = [](const uint4& u) { return __builtin_bit_cast(f16x8, u); };
@@ -594,7 +603,7 @@ __global__ __launch_bounds__(256, 4) void cost16w_kernel(CostArgs a, int P_) {
     for (int i = 0; i < 3; ++i) {
         const int b = wset + 4 * i;
         if (b >= NBLK) break;
-        const int col = 32 * (b >> 1) + 4 * (lc >> 1) + (lc & 1) + 2 * (b & 1);
+        const int col = col0 + 64 * i;
         uint32_t wy[10], wz[10];  // slots 0-7: half 0; [8], [9]: half 1's slots 0, 1
 #pragma unroll
         for (int j = 0; j < 9; ++j) {
@@ -609,8 +618,8 @@ __global__ __launch_bounds__(256, 4) void cost16w_kernel(CostArgs a, int P_) {
         const f32x4v d30 = mfma3(H(A00h), H(A00l), B(bh), B(bl));
         bh[0] = nh; bl[0] = nl;
         const f32x4v d31 = mfma3(H(A10h), H(A10l), B(bh), B(bl));
-        store_vstack16<kWHalfW>(s_v, d30, 0, 1, lk, col, 0);
-        store_vstack16<kWHalfW>(s_v, d31, 0, 1, lk, col, 1);
+        store_vstack_at<kWHalfW>(st01, d30, i, 0);
+        store_vstack_at<kWHalfW>(st01, d31, i, 1);
         pack_b_halves(wz, bh, bl, nh, nl);
         d5[i][0] = mfma3(H(A01h), H(A01l), B(bh), B(bl));
         bh[0] = nh; bl[0] = nl;
@@ -627,9 +636,8 @@ __global__ __launch_bounds__(256, 4) void cost16w_kernel(CostArgs a, int P_) {
     for (int i = 0; i < 3; ++i) {
         const int b = wset + 4 * i;
         if (b >= NBLK) break;
-        const int col = 32 * (b >> 1) + 4 * (lc >> 1) + (lc & 1) + 2 * (b & 1);
-        store_vstack16<kWHalfW>(s_v, d5[i][0], 0, 1, lk, col, 0);
-        store_vstack16<kWHalfW>(s_v, d5[i][1], 0, 1, lk, col, 1);
+        store_vstack_at<kWHalfW>(st01, d5[i][0], i, 0);
+        store_vstack_at<kWHalfW>(st01, d5[i][1], i, 1);
     }
     // LabRef of the item's 2 x 4 pixels, in flight across the barrier
     float4 lab[2][3];
