@@ -98,11 +98,18 @@ __device__ __forceinline__ TileItem tile_item(const CostArgs& a, int w, int P) {
 // Every load is issued before the first wait: vmcnt retires in order, so a
 // load -> wait -> store loop pays one memory round trip per trip (4 for the
 // interior index rows, 14 for the byte gathers of edge tiles).
+// Interior rows are read as DW = RW / 4 dword pairs: the first 32 dword columns
+// by a (row, column) = (tid / 32 + 8q, tid % 32) map (shifts and masks, row
+// offsets one multiply-add), the DW - 32 tail columns (cost16w's 148-byte rows:
+// 5) by a second, short pass.
 template <int HALF, int RW, int TH>
 struct TileFill {
     static constexpr int TW = RW - 2 * HALF, RH = TH + 2 * HALF, DW = RW / 4;
-    static constexpr int NFD = (RH * DW + 255) / 256, NFB = (RH * RW + 255) / 256;
-    static_assert(RW % 4 == 0, "whole dwords per region row");
+    static constexpr int DWT = DW - 32;                                   // tail dword columns
+    static constexpr int DWTD = DWT > 0 ? DWT : 1;                        // its divisor (no tail: unused)
+    static constexpr int NM = (RH * 32 + 255) / 256, NT = (RH * DWT + 255) / 256;
+    static constexpr int NFD = NM + NT, NFB = (RH * RW + 255) / 256;
+    static_assert(RW % 4 == 0 && DW >= 32 && DWT < 32, "whole dwords per region row, 32 <= DW < 64");
     uint32_t lo[NFD], hi[NFD];  // interior tiles: aligned dword pairs of the index rows
     uint32_t roff[NFD];         // their rows' byte offsets (alignment for commit)
     float4 ov;
@@ -135,15 +142,19 @@ struct TileFill {
             const int ytop = t.y0 - HALF;
             const bool vfast = ytop >= 0 && ytop >= g.e0 && ytop + RH <= g.H && ytop + RH <= g.e1;
             const int ubase = (ytop - g.e0) * g.W + (t.x0 - HALF);
-#pragma unroll
-            for (int q = 0; q < NFD; ++q) {
-                const int e = min(tid + 256 * q, RH * DW - 1);
-                const int i = e / DW;
+            auto load = [&](int q, int i, int c) {
                 roff[q] = (uint32_t)(vfast ? ubase + i * g.W : row_base(g, t, i));
-                const uint32_t* src = reinterpret_cast<const uint32_t*>(
-                    idx + ((roff[q] & ~3u) + 4u * (uint32_t)(e % DW)));
+                const uint32_t* src =
+                    reinterpret_cast<const uint32_t*>(idx + ((roff[q] & ~3u) + 4u * (uint32_t)c));
                 lo[q] = src[0];
                 hi[q] = src[1];
+            };
+#pragma unroll
+            for (int q = 0; q < NM; ++q) load(q, min((tid >> 5) + 8 * q, RH - 1), tid & 31);
+#pragma unroll
+            for (int q = 0; q < NT; ++q) {
+                const int e = min(tid + 256 * q, RH * DWT - 1);
+                load(NM + q, e / DWTD, 32 + e % DWTD);
             }
         }
     }
@@ -153,12 +164,19 @@ struct TileFill {
     __device__ __forceinline__ void commit_idx(const CostArgs& a, uint8_t* s_idx, int tid) const {
         const Geom& g = a.g;
         if (interior) {
+            uint32_t* s32 = reinterpret_cast<uint32_t*>(s_idx);
 #pragma unroll
-            for (int q = 0; q < NFD; ++q) {
+            for (int q = 0; q < NM; ++q) {
+                const int i = (tid >> 5) + 8 * q;
+                if (i < RH)
+                    s32[i * (IDXP / 4) + (tid & 31)] = __builtin_amdgcn_alignbyte(hi[q], lo[q], roff[q] & 3u);
+            }
+#pragma unroll
+            for (int q = 0; q < NT; ++q) {
                 const int e = tid + 256 * q;
-                if (e < RH * DW)
-                    reinterpret_cast<uint32_t*>(s_idx)[(e / DW) * (IDXP / 4) + e % DW] =
-                        __builtin_amdgcn_alignbyte(hi[q], lo[q], roff[q] & 3u);
+                if (e < RH * DWT)
+                    s32[(e / DWTD) * (IDXP / 4) + 32 + e % DWTD] =
+                        __builtin_amdgcn_alignbyte(hi[NM + q], lo[NM + q], roff[NM + q] & 3u);
             }
         } else {
             const uint8_t* idx = a.idx + (int64_t)t.p * g.idx_pitch;
