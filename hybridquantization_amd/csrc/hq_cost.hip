@@ -53,7 +53,6 @@ constexpr int kTrimLo[3] = {7, 6, 5}, kTrimHi[3] = {13, 14, 15};
 // horizontal taps, exactly (a power of two).
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-constexpr float kVDataScale = 16384.0f;                   // 2^14
 constexpr float kVTapScale = 65536.0f;                    // 2^16
 constexpr float kVOutScale = 1.0f / (16384.0f * 65536.0f);  // 2^-30
 
@@ -69,14 +68,6 @@ __host__ __device__ __forceinline__ constexpr int kv_row(int half, int g, int j)
     return half == 0 || j >= 2 ? 4 * j + g : (j == 0 ? 32 + g : 36 + g);
 }
 
-// (hi, lo) f16 split of x * 2^14 in one dword, hi in bits 0-15.
-__device__ __forceinline__ uint32_t split_f16(float x) {
-    const float xs = x * kVDataScale;
-    const _Float16 hi = (_Float16)xs;
-    const _Float16 lo = (_Float16)(xs - (float)hi);
-    return (uint32_t)__builtin_bit_cast(uint16_t, hi) |
-           ((uint32_t)__builtin_bit_cast(uint16_t, lo) << 16);
-}
 
 // One work item of the cost pass: palette p over output tile `tile`.
 struct TileItem {
@@ -112,7 +103,7 @@ struct TileFill {
     static_assert(RW % 4 == 0 && DW >= 32 && DWT < 32, "whole dwords per region row, 32 <= DW < 64");
     uint32_t lo[NFD], hi[NFD];  // interior tiles: aligned dword pairs of the index rows
     uint32_t roff[NFD];         // their rows' byte offsets (alignment for commit)
-    float4 ov;
+    uint4 ov;  // the palette's split opponent entry tid (zeros past K)
     TileItem t;
     bool interior;
 
@@ -136,7 +127,7 @@ struct TileFill {
         const Geom& g = a.g;
         t = ti;
         const uint8_t* idx = a.idx + (int64_t)t.p * g.idx_pitch;
-        ov = tid < a.K ? a.opp[(int64_t)t.p * kMaxK + tid] : make_float4(0.f, 0.f, 0.f, 0.f);
+        ov = tid < a.K ? a.opp16[(int64_t)t.p * kMaxK + tid] : make_uint4(0u, 0u, 0u, 0u);
         interior = t.x0 - HALF >= 0 && t.x0 + TW + HALF <= g.W;
         if (interior) {
             const int ytop = t.y0 - HALF;
@@ -328,8 +319,8 @@ __global__ __launch_bounds__(256, 6) void cost_mfma_kernel(CostArgs a, int P_) {
     uint4 F1h = frag[(1 * 2 + 0) * 64], F1l = frag[(1 * 2 + 1) * 64];
     // every entry (zeros for tid >= K): the zero-weight rows 28-31 gather arbitrary
     // indices, and 0 x NaN would be NaN
-    s_ox[tid] = split_f16(fill.ov.x);
-    s_oyz[tid] = make_uint2(split_f16(fill.ov.y), split_f16(fill.ov.z));
+    s_ox[tid] = fill.ov.x;
+    s_oyz[tid] = make_uint2(fill.ov.y, fill.ov.z);
     fill.template commit_idx<RW>(a, s_idx, tid);
     const int m = tid / SLOTS, jr = tid % SLOTS;
     const bool has_item = tid < NITEM && jr < NRUN;
@@ -549,8 +540,8 @@ __global__ __launch_bounds__(256, 4) void cost16w_kernel(CostArgs a, int P_) {
     uint4 A10h = F(1, 0, 0), A10l = F(1, 0, 1), A11h = F(1, 1, 0), A11l = F(1, 1, 1);  // half 1
     // every entry (zeros for tid >= K): zero-weight rows and the columns past
     // the region gather arbitrary indices, and 0 x NaN would be NaN
-    s_ox[tid] = split_f16(fill.ov.x);
-    s_oyz[tid] = make_uint2(split_f16(fill.ov.y), split_f16(fill.ov.z));
+    s_ox[tid] = fill.ov.x;
+    s_oyz[tid] = make_uint2(fill.ov.y, fill.ov.z);
     fill.template commit_idx<RW>(a, s_idx, tid);
     // H item: row pair m, output columns 4j .. 4j+3 (every thread has one)
     const int m = tid >> 5, jr = tid & 31;

@@ -109,6 +109,17 @@ __device__ __forceinline__ float delta_e_g(float Lr, float Ar, float Br, float3 
     }
 }
 
+// (hi, lo) f16 split of x * 2^14 in one dword, hi in bits 0-15: the vertical
+// stencil's MFMA data operand (hq_cost.hip), made once per palette by the prep.
+constexpr float kVDataScale = 16384.0f;  // 2^14
+__device__ __forceinline__ uint32_t split_f16(float x) {
+    const float xs = x * kVDataScale;
+    const _Float16 hi = (_Float16)xs;
+    const _Float16 lo = (_Float16)(xs - (float)hi);
+    return (uint32_t)__builtin_bit_cast(uint16_t, hi) |
+           ((uint32_t)__builtin_bit_cast(uint16_t, lo) << 16);
+}
+
 // CL:256-263 reflection; clamped so garbage coordinates of partial tiles stay
 // in bounds (their results are masked).
 __device__ __forceinline__ int reflect_clamp(int j, int n) {

@@ -40,6 +40,7 @@ struct PaletteArgs {
     const float4* pal_in;   // [P][K] host-uploaded palettes
     float4* pal;            // [P][256] sanitised colours (.w = 0)
     float4* opp;            // [P][256] opponent colour of each palette entry (CL:194-198)
+    uint4* opp16;           // [P][256] its channels x 2^14 as (hi, lo) f16 pairs (split_f16), .w = 0
     uint8_t* dup;           // [P][256] 1 if an identical colour exists at a lower index
     int* pflags;            // [P] bit0: non-finite colour present -> exhaustive argmin
     int K;
@@ -109,7 +110,7 @@ struct AssignArgs {
 
 struct CostArgs {
     const uint8_t* idx;     // [P][idx_pitch]
-    const float4* opp;      // [P][256]
+    const uint4* opp16;     // [P][256] split opponent table (PaletteArgs::opp16)
     const void* taps;       // CostTaps<10> x 2 in device memory (build_fast_taps)
     const uint4* vfrag16;   // [trim][4 stacks][hi, lo][64 lanes] f16x8 A fragments of the
                             // vertical taps (build_vpass_f16_stack_fragments)

@@ -103,7 +103,7 @@ struct hq_ctx {
 
     // population work buffers
     int P_cap = 0, K_cur = 0;
-    DevBuf d_pal_in, d_pal, d_opp, d_dup, d_pflags, d_lvl1, d_lvl2, d_idx, d_used_mask,
+    DevBuf d_pal_in, d_pal, d_opp, d_opp16, d_dup, d_pflags, d_lvl1, d_lvl2, d_idx, d_used_mask,
         d_partial, d_out, d_gen_t;
     float* h_pal = nullptr;   // pinned [P][K][4]
     double* h_out = nullptr;  // pinned [P][1+K]
@@ -337,6 +337,7 @@ int ensure_population(hq_ctx* c, int P, int K) {
     HIP_TRY(c, c->d_pal_in.ensure(sizeof(float4) * (size_t)P * K));
     HIP_TRY(c, c->d_pal.ensure(sizeof(float4) * (size_t)P * kMaxK));
     HIP_TRY(c, c->d_opp.ensure(sizeof(float4) * (size_t)P * kMaxK));
+    HIP_TRY(c, c->d_opp16.ensure(sizeof(uint4) * (size_t)P * kMaxK));
     HIP_TRY(c, c->d_dup.ensure((size_t)P * kMaxK));
     HIP_TRY(c, c->d_pflags.ensure(sizeof(int) * (size_t)P));
     HIP_TRY(c, c->d_lvl1.ensure((size_t)P * l1p));
@@ -361,7 +362,7 @@ void prof_add(hq_ctx* c, ProfSlot& s, hipEvent_t a, hipEvent_t b) {
 
 PaletteArgs prep_args(hq_ctx* c, int K) {
     return PaletteArgs{c->d_pal_in.as<float4>(), c->d_pal.as<float4>(), c->d_opp.as<float4>(),
-                       c->d_dup.as<uint8_t>(), c->d_pflags.as<int>(), K};
+                       c->d_opp16.as<uint4>(), c->d_dup.as<uint8_t>(), c->d_pflags.as<int>(), K};
 }
 
 // Enqueue the evaluation of the P prepared palettes (d_pal, d_opp, d_dup,
@@ -405,7 +406,7 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev) {
     if (c->cost_variant != 1 && c->half == 10) {
         CostArgs ca{};
         ca.idx = c->d_idx.as<uint8_t>();
-        ca.opp = c->d_opp.as<float4>();
+        ca.opp16 = c->d_opp16.as<uint4>();
         ca.taps = c->d_taps.p;
         ca.vfrag16 = c->d_vfrag16.as<uint4>();
         ca.labL = c->d_labL.as<float>();
@@ -690,7 +691,7 @@ void hq_destroy(hq_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     for (DevBuf* b : {&c->d_k1, &c->d_k2, &c->d_k3, &c->d_absk3, &c->d_R, &c->d_G, &c->d_B,
-                      &c->d_labL, &c->d_labA, &c->d_labB, &c->d_pal_in, &c->d_pal, &c->d_opp,
+                      &c->d_labL, &c->d_labA, &c->d_labB, &c->d_pal_in, &c->d_pal, &c->d_opp, &c->d_opp16,
                       &c->d_dup, &c->d_pflags, &c->d_lvl1, &c->d_lvl2, &c->d_idx,
                       &c->d_used_mask, &c->d_partial, &c->d_out, &c->d_gen_t, &c->d_taps,
                       &c->d_vfrag16})

@@ -66,6 +66,7 @@ __device__ __forceinline__ void prep_palette_body(const PaletteArgs& a, int p, f
                                        dot3(lr, lg, lb, c_RGB2Opp + 6), 0.f);
         a.pal[(int64_t)p * kMaxK + k] = c;
         a.opp[(int64_t)p * kMaxK + k] = opp;
+        a.opp16[(int64_t)p * kMaxK + k] = make_uint4(split_f16(opp.x), split_f16(opp.y), split_f16(opp.z), 0u);
         a.dup[(int64_t)p * kMaxK + k] = s_min[slot] < (uint32_t)k ? 1u : 0u;
     }
     if (tid == 0) a.pflags[p] = s_nonfinite;
