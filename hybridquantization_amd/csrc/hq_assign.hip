@@ -164,10 +164,9 @@ __global__ __launch_bounds__(256) void assign_pipe_kernel(AssignArgs a, int P) {
     load_rgb(qpos(2), rb[0], gb[0], bb[0]);
     // The palette table is filled while the first pixels' loads are in flight
     // (the fill used to come first: one more memory round trip per workgroup).
-    for (int e = tid; e < ng * a.K; e += 256) {
-        const int pp = e / a.K, k = e - pp * a.K;
-        s_pal[pp * kMaxK + k] = a.pal[(int64_t)(p0 + pp) * kMaxK + k];
-    }
+    static_assert(kMaxK == 256, "one table entry per thread and palette");
+    for (int pp = 0; pp < ng; ++pp)
+        if (tid < a.K) s_pal[pp * kMaxK + tid] = a.pal[(int64_t)(p0 + pp) * kMaxK + tid];
     if (tid < 8 * NG) s_used[tid >> 3][tid & 7] = 0;
     __syncthreads();
     bool exh_pal[NG];
