@@ -124,25 +124,31 @@ __global__ __launch_bounds__(256) void assign_pipe_kernel(AssignArgs a, int P) {
     const int p0 = 4 * grp, ng = min(NG, P - p0);
     const uint8_t* lines = a.lvl2 + (int64_t)grp * a.lvl2_gstride;
     const int G2 = a.G2 > 0 ? a.G2 : 4;
-    // pixel sequence of this thread: chunk c (stride nblocks), slot j < PPT
-    const int64_t chunk = 256 * PPT, cstride = (int64_t)a.nblocks * chunk;
-    const int64_t lane_off = (int64_t)(tid >> 6) * 64 * PPT + (tid & 63);
-    auto qpos = [&](int64_t i) {  // i-th pixel of this thread
-        return (int64_t)blk * chunk + (i / PPT) * cstride + lane_off + 64 * (i % PPT);
+    // pixel sequence of this thread: chunk c (stride nblocks), slot j < PPT.
+    // Positions and byte offsets are 32-bit (the host keeps a shard's extended
+    // rows below 2^30 pixels), so loads and stores take the scalar-base form.
+    const uint32_t chunk = 256 * PPT, cstride = (uint32_t)a.nblocks * chunk;
+    const uint32_t qbase = (uint32_t)blk * chunk + (uint32_t)(tid >> 6) * 64 * PPT + (tid & 63);
+    auto qpos = [&](int i) {  // i-th pixel of this thread
+        return qbase + (uint32_t)(i / PPT) * cstride + 64u * (uint32_t)(i % PPT);
     };
     // Loads are unconditional (clamped addresses, results selected afterwards):
     // predicated loads sit behind branches, and the compiler's wait counting
     // then keeps at most one load in flight.
-    const int64_t qlast = a.n_ext - 1;
-    auto load_rgb = [&](int64_t q, float& r, float& g, float& b) {
-        const int64_t qc = min(q, qlast);
-        r = a.R[qc];
-        g = a.G[qc];
-        b = a.B[qc];
+    const uint32_t n_ext = (uint32_t)a.n_ext, qlast = n_ext - 1;
+    auto at = [](const float* base, uint32_t q) {
+        return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + (q << 2));
     };
-    auto lookup = [&](int64_t q, float r, float g, float b, bool& inside, uint4 (&e)[NG]) {
-        inside = q < a.n_ext && r >= 0.f && r <= 1.f && g >= 0.f && g <= 1.f && b >= 0.f && b <= 1.f;
-        const uint4* line = reinterpret_cast<const uint4*>(lines + (inside ? quad_cell(r, g, b, G2) : 0) * 64);
+    auto load_rgb = [&](uint32_t q, float& r, float& g, float& b) {
+        const uint32_t qc = min(q, qlast);
+        r = at(a.R, qc);
+        g = at(a.G, qc);
+        b = at(a.B, qc);
+    };
+    auto lookup = [&](uint32_t q, float r, float g, float b, bool& inside, uint4 (&e)[NG]) {
+        inside = q < n_ext && r >= 0.f && r <= 1.f && g >= 0.f && g <= 1.f && b >= 0.f && b <= 1.f;
+        const uint4* line =
+            reinterpret_cast<const uint4*>(lines + (inside ? (uint32_t)quad_cell(r, g, b, G2) : 0u) * 64u);
 #pragma unroll
         for (int pp = 0; pp < NG; ++pp) e[pp] = line[pp];  // selected by the `listed` flag at use
     };
@@ -156,7 +162,7 @@ __global__ __launch_bounds__(256) void assign_pipe_kernel(AssignArgs a, int P) {
     float xr[2], xg[2], xb[2];        // RGB of pixels being looked up / resolved
     uint4 E[2][NG];
     bool in_[2];
-    int64_t qq[2];
+    uint32_t qq[2];
     load_rgb(qpos(0), xr[0], xg[0], xb[0]);
     qq[0] = qpos(0);
     lookup(qq[0], xr[0], xg[0], xb[0], in_[0], E[0]);
@@ -169,11 +175,14 @@ __global__ __launch_bounds__(256) void assign_pipe_kernel(AssignArgs a, int P) {
         if (tid < a.K) s_pal[pp * kMaxK + tid] = a.pal[(int64_t)(p0 + pp) * kMaxK + tid];
     if (tid < 8 * NG) s_used[tid >> 3][tid & 7] = 0;
     __syncthreads();
+    uint8_t* idx_base[NG];  // each palette's index image
+#pragma unroll
+    for (int pp = 0; pp < NG; ++pp) idx_base[pp] = a.idx + (int64_t)(p0 + min(pp, ng - 1)) * a.idx_pitch;
     bool exh_pal[NG];
 #pragma unroll
     for (int pp = 0; pp < NG; ++pp) exh_pal[pp] = pp >= ng || a.pflags[p0 + min(pp, ng - 1)] != 0 || a.G2 == 0;
     auto resolve = [&](int h) {
-        const int64_t q = qq[h];
+        const uint32_t q = qq[h];
 #pragma unroll
         for (int pp = 0; pp < NG; ++pp) {
             if (pp >= ng) break;
@@ -184,12 +193,12 @@ __global__ __launch_bounds__(256) void assign_pipe_kernel(AssignArgs a, int P) {
             // non-temporal: streamed out during the kernel rather than left dirty
             // in L2 for the kernel boundary to write back (67 MB per population;
             // ~0.5-1% per evaluation)
-            __builtin_nontemporal_store((uint8_t)k, &a.idx[(int64_t)pq * a.idx_pitch + q]);
+            __builtin_nontemporal_store((uint8_t)k, idx_base[pp] + q);
             const uint32_t bit = 1u << (k & 31);
             if (!(s_used[pp][k >> 5] & bit)) atomicOr(&s_used[pp][k >> 5], bit);
         }
     };
-    auto step = [&](int64_t i, int h) {  // h == i & 1, a compile-time constant at each call
+    auto step = [&](int i, int h) {  // h == i & 1, a compile-time constant at each call
         const int n = h ^ 1;
         qq[n] = qpos(i + 1);
         xr[n] = rb[n]; xg[n] = gb[n]; xb[n] = bb[n];  // RGB(i+1): landed, needed now anyway
@@ -197,10 +206,10 @@ __global__ __launch_bounds__(256) void assign_pipe_kernel(AssignArgs a, int P) {
         load_rgb(qpos(i + 3), rb[n], gb[n], bb[n]);
         resolve(h);
     };
-    for (int64_t i = 0;; i += 2) {
-        if (qpos(i) >= a.n_ext) break;
+    for (int i = 0;; i += 2) {
+        if (qpos(i) >= n_ext) break;
         step(i, 0);
-        if (qpos(i + 1) >= a.n_ext) break;
+        if (qpos(i + 1) >= n_ext) break;
         step(i + 1, 1);
     }
     __syncthreads();
