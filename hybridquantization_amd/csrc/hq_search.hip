@@ -38,6 +38,7 @@ __device__ __forceinline__ void prep_palette_body(const PaletteArgs& a, int p, f
     __shared__ float4 s[kMaxK];
     __shared__ uint32_t s_tab[kDupSlots], s_min[kDupSlots];
     __shared__ int s_nonfinite;
+    __shared__ float s_lin[3 * kMaxK];
     for (int i = tid; i < kDupSlots; i += blockDim.x) { s_tab[i] = ~0u; s_min[i] = ~0u; }
     if (tid == 0) s_nonfinite = 0;
     const bool own = k < a.K;
@@ -45,6 +46,13 @@ __device__ __forceinline__ void prep_palette_body(const PaletteArgs& a, int p, f
     else c = make_float4(0.f, 0.f, 0.f, 0.f);
     if (own) s[k] = c;
     __syncthreads();
+    // linear RGB (CL:85-87), one component per thread: a colour's three powf
+    // run on three threads (12 waves) instead of one after another (4 waves)
+    for (int t = tid; t < 3 * a.K; t += blockDim.x) {
+        const float4 cc = s[t / 3];
+        const int ch = t % 3;
+        s_lin[t] = srgb_lin(ch == 0 ? cc.x : (ch == 1 ? cc.y : cc.z));
+    }
     uint32_t slot = 0;
     if (own) {
         if (!(isfinite(c.x) && isfinite(c.y) && isfinite(c.z))) atomicOr(&s_nonfinite, 1);
@@ -60,7 +68,7 @@ __device__ __forceinline__ void prep_palette_body(const PaletteArgs& a, int p, f
     }
     __syncthreads();
     if (own) {
-        const float lr = srgb_lin(c.x), lg = srgb_lin(c.y), lb = srgb_lin(c.z);
+        const float lr = s_lin[3 * k], lg = s_lin[3 * k + 1], lb = s_lin[3 * k + 2];
         const float4 opp = make_float4(dot3(lr, lg, lb, c_RGB2Opp + 0),
                                        dot3(lr, lg, lb, c_RGB2Opp + 3),
                                        dot3(lr, lg, lb, c_RGB2Opp + 6), 0.f);
