@@ -167,10 +167,16 @@ __device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared
     __syncthreads();
     if (a.accept) {
         if (nf <= MAXF) {
-#pragma unroll
-            for (int j = 0; j < MAXF; ++j) {
-                const int e = tid + j * nt;
-                if (j < nf && e < P * K && fv[j] == 0.0) atomicAdd(&s.unused[e / K], 1);
+            // a wave's flags are consecutive: one ballot count per palette it spans
+            // (one LDS atomic per wave instead of one per unused colour)
+            for (int j = 0; j < nf; ++j) {
+                const int e = tid + j * nt, e0 = (tid & ~63) + j * nt;
+                const bool z = e < P * K && fv[j] == 0.0;
+                const int pe = e / K, plo = e0 / K, phi = min((e0 + 63) / K, P - 1);
+                for (int pp = plo; pp <= phi; ++pp) {
+                    const int n = __popcll(__ballot(z && pe == pp));
+                    if ((tid & 63) == 0 && n) atomicAdd(&s.unused[pp], n);
+                }
             }
         } else {
             for (int e = tid; e < P * K; e += nt)
