@@ -462,7 +462,7 @@ def test_full_size_properties(gpu, filt):
 
 
 @pytest.mark.parametrize("rows", [16, 8])
-def test_fused_finalize_alternating_populations(gpu, filt, rows):
+def test_alternating_populations_bitwise(gpu, filt, rows):
     """Two different populations evaluated alternately give, every time,
     bitwise the costs and used flags of their first evaluation (no state of one
     evaluation -- partials, used masks, level-2 lines -- leaks into the next),
