@@ -231,8 +231,9 @@ __device__ __forceinline__ void hpass_pair_filters(const f32x4* src, TapsPtr<HAL
 // fp32 accumulator; lo.lo ~2^-22 relative is dropped).  A = the stacked
 // Toeplitz taps (rows = filter pair x 8 output rows, x 2^16, split on the host:
 // build_vpass_f16_stack_fragments), B = the gathered opponent values (x 2^14),
-// read from per-channel (hi, lo) f16 dword tables that the prologue splits once
-// per tile, so the gathers need no conversion (one LDS read per value).  D (x 2^30, folded exactly into the
+// read from per-channel (hi, lo) f16 dword tables (split once per palette by
+// the prep, PaletteArgs::opp16), so the gathers need no conversion (one LDS
+// read per value).  D (x 2^30, folded exactly into the
 // horizontal taps) holds 4 consecutive output rows of one filter and column per
 // lane: two row-pair stores.  Stacks (f0, f1), (f2, -), (f3, f4), (f5, f6); wave
 // w takes region columns 32w .. +31: 12 MFMAs per group and wave.
