@@ -113,7 +113,7 @@ __device__ __forceinline__ int64_t quad_cell(float r, float g, float b, int G2) 
 // dwordx4 lookups per pixel for one useful one) and keeps NG palette tables.
 template <int NG>
 __global__ __launch_bounds__(256) void assign_pipe_kernel(AssignArgs a, int P) {
-    constexpr int PPT = 8;  // pixels per thread per chunk (the pipeline runs across chunks)
+    constexpr int PPT = kAssignPPT;  // pixels per thread per chunk (the pipeline runs across chunks)
     // [NG][kMaxK]: a fixed palette stride, so each palette's base folds into the
     // ds_read_b128 offset field and a candidate's address is its byte << 4
     __shared__ __attribute__((aligned(16))) float4 s_pal[NG * kMaxK];

@@ -46,6 +46,11 @@ struct PaletteArgs {
     int K;
 };
 
+#ifndef HQ_ASSIGN_PPT
+#define HQ_ASSIGN_PPT 4
+#endif
+constexpr int kAssignPPT = HQ_ASSIGN_PPT;  // assign: pixels per thread per 256-thread chunk
+                                           // (4: as fast as 8 or 16 at 4096^2, 6% faster on a 512-row shard)
 constexpr int kSaMaxP = 64;       // device-resident SWASA: largest population
 
 // sa_step_kernel: one accept + generate step of the device-resident SWASA search.

@@ -316,7 +316,7 @@ int check_geom_args(hq_ctx* c, int w, int h, int r0, int r1) {
 // chunks per workgroup instead -- 1064 workgroups of 2 for 2128 chunks -- was
 // slower than 2048 with 80 of them taking a second chunk.)
 int assign_blocks(const hq_ctx* c) {
-    const int64_t chunk = 256 * 8;
+    const int64_t chunk = 256 * kAssignPPT;
     const int64_t nblocks = (int64_t)c->num_cu * c->assign_blocks_per_cu;
     return (int)std::max<int64_t>(1, std::min<int64_t>(nblocks, (c->g.n_ext + chunk - 1) / chunk));
 }
