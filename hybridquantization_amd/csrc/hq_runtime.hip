@@ -114,7 +114,7 @@ struct hq_ctx {
     int G2 = 32;           // argmin grid resolution (0 = exhaustive)
     int cost_variant = 0;  // 0 tiled (default), 1 generic two-pass
     int cost_rows = 16;    // fast path tiles: 16 x 128 (cost16w_kernel) or 8 x 108 (cost_mfma_kernel)
-    int assign_blocks_per_cu = 8;
+    int assign_blocks_per_cu = 16;  // 4096^2: 4 chunks per workgroup; 0.632 -> 0.605 ms per step vs 8
     int shard_solo = 0;    // experiment: a sharded search without a communicator (per-rank timing)
     int sa_device = 1;     // hq_search_*: 1 = SWASA iterations resident on the device (no host
                            // round trip per iteration), 0 = host-driven (one eval call each)
@@ -310,7 +310,7 @@ int check_geom_args(hq_ctx* c, int w, int h, int r0, int r1) {
 }
 
 // Assign workgroups per palette group: assign_blocks_per_cu per CU, but no more
-// than pixel chunks (256 threads x 8 pixels): idle workgroups still fill LDS,
+// than pixel chunks (256 threads x kAssignPPT pixels): idle workgroups still fill LDS,
 // and after the XCD relabelling they would all sit on the last XCDs (a 512-row
 // shard ran assign on half the chip: 0.071 vs 0.053 ms).  (Evening out the
 // chunks per workgroup instead -- 1064 workgroups of 2 for 2128 chunks -- was

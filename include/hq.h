@@ -187,7 +187,7 @@ int hq_profile_reset(hq_ctx *ctx);
  *   "cost_rows"    fast path tiles: 16 (16 x 128 outputs, default) or 8 (8 x 108)
  *   "trim"         1 = skip the narrow k1 filters' taps below 1e-9 of their peak
  *                  (default; only when the filters allow it), 0 = all taps
- *   "assign_blocks_per_cu" workgroups per CU of the assign grid (default 8)
+ *   "assign_blocks_per_cu" workgroups per CU of the assign grid (default 16)
  *   "sa_device"    hq_search_*: 1 (default) = the SWASA iterations run on the device
  *                  (accept/generate kernel, no host round trip per iteration; needs
  *                  population <= 64), 0 = host-driven, one evaluation call each
