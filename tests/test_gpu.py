@@ -425,6 +425,28 @@ def test_device_search_with_single_rank_comm(gpu, filt):
 # Full-size properties (4096^2, K = 256): determinism, grid == exhaustive,
 # fast == generic, shards == full.
 # ---------------------------------------------------------------------------
+@pytest.mark.parametrize("w,h,P", [(1003, 517, 4), (1003, 517, 3), (37, 29, 5)])
+def test_assign_workgroup_count_invariance(gpu, filt, w, h, P):
+    """The assign grid (option assign_blocks_per_cu: 1 workgroup per CU up to 64,
+    default 16) only changes which workgroup takes which pixel chunk: indices,
+    used flags and costs are bitwise the same for every count, also when an
+    image has fewer chunks than workgroups (37 x 29)."""
+    K = 256
+    R, G, B = o.synthetic_image(w, h, seed=11)
+    m = _planar_ctx(gpu, R, G, B, w, h, filt.illum)
+    pals = np.stack([o.synthetic_palette(K, 40 + p) for p in range(P)]).reshape(P, -1)
+    ref_c, ref_used = m.computeQuantizationErrorPopulation(pals, 2.0, return_used=True)
+    ref_idx = [m.getIndices(p) for p in range(P)]
+    for nb in (1, 5, 64, 16):
+        m.setOption("assign_blocks_per_cu", nb)
+        c, used = m.computeQuantizationErrorPopulation(pals, 2.0, return_used=True)
+        np.testing.assert_array_equal(c, ref_c, err_msg=f"blocks {nb}")
+        np.testing.assert_array_equal(used, ref_used, err_msg=f"blocks {nb}")
+        for p in range(P):
+            np.testing.assert_array_equal(m.getIndices(p), ref_idx[p], err_msg=f"blocks {nb} palette {p}")
+    m.close()
+
+
 def test_full_size_properties(gpu, filt):
     w = h = 4096
     K = 256
