@@ -26,6 +26,16 @@ def _gpu_available() -> bool:
         return False
 
 
+def pytest_terminal_summary(terminalreporter):
+    """Evidence of the native path: the libhq shared objects this process mapped."""
+    try:
+        with open("/proc/self/maps") as f:
+            libs = sorted({ln.split()[-1] for ln in f if "libhq" in ln and ln.rstrip().endswith(".so")})
+    except OSError:
+        libs = []
+    terminalreporter.write_line("mapped libhq: " + (", ".join(libs) if libs else "none"))
+
+
 @pytest.fixture(scope="session")
 def gpu():
     """Skip-free guard: a gpu-marked test run without a device is an error."""
