@@ -10,8 +10,10 @@
  * the constructor).  Arrays are pinned with Get/ReleasePrimitiveArrayCritical
  * for the duration of the call only (caller-owned, IM:271-283 semantics).
  * Every array length is checked against what the hq_* call will touch before
- * anything is pinned (IllegalArgumentException), and a failed pin raises
- * OutOfMemoryError, so a mismatched caller never reaches native memory.
+ * anything is pinned (IllegalArgumentException), and a failed pin releases
+ * what is held before raising OutOfMemoryError (pin_all), so a mismatched
+ * caller never reaches native memory and no JNI call runs inside a critical
+ * region.
  */
 #include <jni.h>
 #include <stdint.h>
@@ -42,27 +44,42 @@ static int bad_len(JNIEnv *env, jarray a, long long need, const char *what) {
 }
 
 typedef struct {
-    jarray arr;
+    jarray arr;  /* may be NULL (optional argument): left unpinned */
     void *ptr;
+    int out;     /* written by the call: copied back only when it succeeds */
 } pin_t;
 
-static void *pin(JNIEnv *env, jarray a, pin_t *p) {
-    p->arr = a;
-    p->ptr = a ? (*env)->GetPrimitiveArrayCritical(env, a, NULL) : NULL;
-    return p->ptr;
-}
-
-/* 1 (OutOfMemoryError thrown) if a requested pin of a non-null array failed */
-static int pin_failed(JNIEnv *env, const pin_t *p, int n) {
-    for (int i = 0; i < n; ++i)
-        if (p[i].arr && !p[i].ptr)
-            return throw_class(env, "java/lang/OutOfMemoryError", "libhq: cannot pin a Java array");
+/* Pins p[0..n) in order with GetPrimitiveArrayCritical.  JNI allows no other
+ * JNI call while a critical region is open, so on the first failed pin this
+ * stops, releases every array it already holds (JNI_ABORT), and only then
+ * throws OutOfMemoryError -- unless the VM already raised an exception, which
+ * is kept.  Returns 0 when every non-null array is pinned. */
+static int pin_all(JNIEnv *env, pin_t *p, int n) {
+    for (int i = 0; i < n; ++i) p[i].ptr = NULL;
+    for (int i = 0; i < n; ++i) {
+        if (!p[i].arr) continue;
+        p[i].ptr = (*env)->GetPrimitiveArrayCritical(env, p[i].arr, NULL);
+        if (!p[i].ptr) {
+            for (int j = i - 1; j >= 0; --j)
+                if (p[j].ptr) {
+                    (*env)->ReleasePrimitiveArrayCritical(env, p[j].arr, p[j].ptr, JNI_ABORT);
+                    p[j].ptr = NULL;
+                }
+            if (!(*env)->ExceptionCheck(env))
+                throw_class(env, "java/lang/OutOfMemoryError", "libhq: cannot pin a Java array");
+            return 1;
+        }
+    }
     return 0;
 }
 
-static void unpin(JNIEnv *env, pin_t *p, int commit) {
-    if (p->arr && p->ptr) (*env)->ReleasePrimitiveArrayCritical(env, p->arr, p->ptr, commit ? 0 : JNI_ABORT);
-    p->ptr = NULL;
+/* Releases in reverse order; output arrays are committed only when ok. */
+static void unpin_all(JNIEnv *env, pin_t *p, int n, int ok) {
+    for (int i = n - 1; i >= 0; --i)
+        if (p[i].ptr) {
+            (*env)->ReleasePrimitiveArrayCritical(env, p[i].arr, p[i].ptr, ok && p[i].out ? 0 : JNI_ABORT);
+            p[i].ptr = NULL;
+        }
 }
 
 /* IM:52 -> hq_create; returns 0 when no GPU (caller sets openCLAvailable=false) */
@@ -88,12 +105,11 @@ JNIEXPORT void JNICALL JNI_FN(nSetFilters)(JNIEnv *env, jclass cls, jlong h, jin
         if (taps < 1) throw_class(env, "java/lang/IllegalArgumentException", "taps < 1");
         return;
     }
-    pin_t p[4];
-    const float *a = pin(env, k1, &p[0]), *b = pin(env, k2, &p[1]), *c = pin(env, k3, &p[2]),
-                *d = pin(env, absk3, &p[3]);
-    int st = pin_failed(env, p, 4) ? -1 : hq_set_filters(ctx, taps, a, b, c, d);
-    for (int i = 3; i >= 0; --i) unpin(env, &p[i], 0);
-    if (st > 0) throw_status(env, ctx, st);
+    pin_t p[4] = {{k1, NULL, 0}, {k2, NULL, 0}, {k3, NULL, 0}, {absk3, NULL, 0}};
+    if (pin_all(env, p, 4)) return;
+    int st = hq_set_filters(ctx, taps, p[0].ptr, p[1].ptr, p[2].ptr, p[3].ptr);
+    unpin_all(env, p, 4, st == 0);
+    if (st) throw_status(env, ctx, st);
 }
 
 /* IM:100 RGBtoXYZ(R, G, B) */
@@ -107,13 +123,11 @@ JNIEXPORT void JNICALL JNI_FN(nRGBtoXYZ)(JNIEnv *env, jclass cls, jlong h, jfloa
         if (n < 1) throw_class(env, "java/lang/IllegalArgumentException", "empty image");
         return;
     }
-    pin_t p[4];
-    const float *r = pin(env, R, &p[0]), *g = pin(env, G, &p[1]), *b = pin(env, B, &p[2]);
-    float *o = pin(env, out, &p[3]);
-    int st = pin_failed(env, p, 4) ? -1 : hq_rgb_to_xyz(ctx, r, g, b, n, o);
-    unpin(env, &p[3], st == 0);
-    for (int i = 2; i >= 0; --i) unpin(env, &p[i], 0);
-    if (st > 0) throw_status(env, ctx, st);
+    pin_t p[4] = {{R, NULL, 0}, {G, NULL, 0}, {B, NULL, 0}, {out, NULL, 1}};
+    if (pin_all(env, p, 4)) return;
+    int st = hq_rgb_to_xyz(ctx, p[0].ptr, p[1].ptr, p[2].ptr, n, p[3].ptr);
+    unpin_all(env, p, 4, st == 0);
+    if (st) throw_status(env, ctx, st);
 }
 
 /* IM:285 XYZtoScielab(XYZ, filters, absfilters, w, illuminant) */
@@ -128,12 +142,11 @@ JNIEXPORT void JNICALL JNI_FN(nXYZtoScielab)(JNIEnv *env, jclass cls, jlong h, j
         if (hgt < 1) throw_class(env, "java/lang/IllegalArgumentException", "image shorter than one row");
         return;
     }
-    pin_t p[3];
-    const float *a = pin(env, xyz, &p[0]), *il = pin(env, illum, &p[1]);
-    float *o = pin(env, out, &p[2]);
-    int st = pin_failed(env, p, 3) ? -1 : hq_xyz_to_scielab(ctx, a, w, hgt, il, o);
-    unpin(env, &p[2], st == 0); unpin(env, &p[1], 0); unpin(env, &p[0], 0);
-    if (st > 0) throw_status(env, ctx, st);
+    pin_t p[3] = {{xyz, NULL, 0}, {illum, NULL, 0}, {out, NULL, 1}};
+    if (pin_all(env, p, 3)) return;
+    int st = hq_xyz_to_scielab(ctx, p[0].ptr, w, hgt, p[1].ptr, p[2].ptr);
+    unpin_all(env, p, 3, st == 0);
+    if (st) throw_status(env, ctx, st);
 }
 
 /* IM:450-478: device-resident inline RGBA image + inline S-CIELAB */
@@ -148,11 +161,11 @@ JNIEXPORT void JNICALL JNI_FN(nSetImage)(JNIEnv *env, jclass cls, jlong h, jfloa
         if (hgt < 1) throw_class(env, "java/lang/IllegalArgumentException", "image shorter than one row");
         return;
     }
-    pin_t p[3];
-    const float *a = pin(env, rgba, &p[0]), *b = pin(env, lab, &p[1]), *il = pin(env, illum, &p[2]);
-    int st = pin_failed(env, p, 3) ? -1 : hq_set_image(ctx, a, b, w, hgt, il);
-    unpin(env, &p[2], 0); unpin(env, &p[1], 0); unpin(env, &p[0], 0);
-    if (st > 0) throw_status(env, ctx, st);
+    pin_t p[3] = {{rgba, NULL, 0}, {lab, NULL, 0}, {illum, NULL, 0}};  /* lab may be NULL */
+    if (pin_all(env, p, 3)) return;
+    int st = hq_set_image(ctx, p[0].ptr, p[1].ptr, w, hgt, p[2].ptr);
+    unpin_all(env, p, 3, st == 0);
+    if (st) throw_status(env, ctx, st);
 }
 
 /* IM:620 computeQuantizationErrorPopulation: palettes[P*4K] -> mean dE per
@@ -166,13 +179,11 @@ JNIEXPORT void JNICALL JNI_FN(nEvalPopulation)(JNIEnv *env, jclass cls, jlong h,
     if (bad_len(env, palettes, 4LL * P * K, "palettes: P*4K floats") ||
         bad_len(env, meanOut, P, "mean: P doubles") || bad_len(env, usedOut, (long long)P * K, "used: P*K ints"))
         return;
-    pin_t p[3];
-    const float *a = pin(env, palettes, &p[0]);
-    double *m = pin(env, meanOut, &p[1]);
-    int32_t *u = (int32_t *)pin(env, usedOut, &p[2]);
-    int st = pin_failed(env, p, 3) ? -1 : hq_eval_population(ctx, a, P, K, 0.0f, m, u);
-    unpin(env, &p[2], st == 0); unpin(env, &p[1], st == 0); unpin(env, &p[0], 0);
-    if (st > 0) throw_status(env, ctx, st);
+    pin_t p[3] = {{palettes, NULL, 0}, {meanOut, NULL, 1}, {usedOut, NULL, 1}};
+    if (pin_all(env, p, 3)) return;
+    int st = hq_eval_population(ctx, p[0].ptr, P, K, 0.0f, p[1].ptr, (int32_t *)p[2].ptr);
+    unpin_all(env, p, 3, st == 0);
+    if (st) throw_status(env, ctx, st);
 }
 
 /* IM:770 quantize(inlineImageRGB, colors) */
@@ -186,12 +197,11 @@ JNIEXPORT void JNICALL JNI_FN(nQuantize)(JNIEnv *env, jclass cls, jlong h, jfloa
         if (n < 1 || K < 1) throw_class(env, "java/lang/IllegalArgumentException", "empty image or palette");
         return;
     }
-    pin_t p[3];
-    const float *a = pin(env, rgba, &p[0]), *c = pin(env, colors, &p[1]);
-    float *o = pin(env, out, &p[2]);
-    int st = pin_failed(env, p, 3) ? -1 : hq_quantize(ctx, a, n, c, K, o, NULL);
-    unpin(env, &p[2], st == 0); unpin(env, &p[1], 0); unpin(env, &p[0], 0);
-    if (st > 0) throw_status(env, ctx, st);
+    pin_t p[3] = {{rgba, NULL, 0}, {colors, NULL, 0}, {out, NULL, 1}};
+    if (pin_all(env, p, 3)) return;
+    int st = hq_quantize(ctx, p[0].ptr, n, p[1].ptr, K, p[2].ptr, NULL);
+    unpin_all(env, p, 3, st == 0);
+    if (st) throw_status(env, ctx, st);
 }
 
 /* IM:858 computeError(original, quantized, errorImage) */
@@ -207,11 +217,10 @@ JNIEXPORT jdouble JNICALL JNI_FN(nComputeError)(JNIEnv *env, jclass cls, jlong h
         return 0.0;
     }
     double mean = 0.0;
-    pin_t p[3];
-    const float *a = pin(env, orig, &p[0]), *b = pin(env, quant, &p[1]);
-    float *e = pin(env, errImg, &p[2]);
-    int st = pin_failed(env, p, 3) ? -1 : hq_compute_error(ctx, a, b, n, e, &mean);
-    unpin(env, &p[2], st == 0); unpin(env, &p[1], 0); unpin(env, &p[0], 0);
-    if (st > 0) throw_status(env, ctx, st);
+    pin_t p[3] = {{orig, NULL, 0}, {quant, NULL, 0}, {errImg, NULL, 1}};  /* errImg may be NULL */
+    if (pin_all(env, p, 3)) return 0.0;
+    int st = hq_compute_error(ctx, p[0].ptr, p[1].ptr, n, p[2].ptr, &mean);
+    unpin_all(env, p, 3, st == 0);
+    if (st) throw_status(env, ctx, st);
     return mean;
 }

@@ -120,6 +120,7 @@ struct hq_ctx {
                            // round trip per iteration), 0 = host-driven (one eval call each)
     int trim = 1;          // skip taps < 1e-9 of the peak of the narrow k1 filters
     bool trim_ok = false;  // set by hq_set_filters (default 21-tap filter set)
+    bool pal_generic = false;  // this population needs the generic cost path (palette_fits_fast)
 
     // comm
     ncclComm_t comm = nullptr;
@@ -403,7 +404,7 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev) {
     HIP_TRY(c, e);
     const float inv[3] = {1.0f / c->illum[0], 1.0f / c->illum[1], 1.0f / c->illum[2]};
     int nparts;
-    if (c->cost_variant != 1 && c->half == 10) {
+    if (c->cost_variant != 1 && c->half == 10 && !c->pal_generic) {
         CostArgs ca{};
         ca.idx = c->d_idx.as<uint8_t>();
         ca.opp16 = c->d_opp16.as<uint4>();
@@ -499,13 +500,32 @@ int check_eval_args(hq_ctx* c, const float* palettes, int P, int K) {
     return HQ_OK;
 }
 
+// The fast cost kernels take the opponent colours as split f16 of x * 2^14
+// (split_f16): |opp| must stay below 65504 / 2^14 ~ 4.  RGB2Opp's largest
+// absolute row sum is 0.871, so a palette channel x in [-59, 1.93] keeps
+// |opp| < 4 (lin(x) = x / 12.92 below 0.04045, ((x + 0.055) / 1.055)^2.4
+// above).  Colours outside [-32, 1.9] -- never produced by the SA, which
+// clamps to [0, 1] (SW:103-106), but accepted by hq_eval_population -- and
+// non-finite colours send the population to the generic fp32 path.
+bool palette_fits_fast(const float* pal, int P, int K) {
+    for (size_t i = 0, n = (size_t)P * K; i < n; ++i)
+        for (int ch = 0; ch < 3; ++ch) {
+            const float x = pal[4 * i + ch];
+            if (!(x >= -32.0f && x <= 1.9f)) return false;
+        }
+    return true;
+}
+
 int eval_partial_into_hout(hq_ctx* c, const float* palettes, int P, int K) {
     int rc = check_eval_args(c, palettes, P, K);
     if (rc) return rc;
     if ((rc = bind(c))) return rc;
     if ((rc = ensure_population(c, P, K))) return rc;
     std::memcpy(c->h_pal, palettes, sizeof(float) * 4 * (size_t)P * K);
-    return enqueue_eval(c, P, K);
+    c->pal_generic = !palette_fits_fast(palettes, P, K);
+    rc = enqueue_eval(c, P, K);
+    c->pal_generic = false;  // device-resident searches generate clamped palettes
+    return rc;
 }
 
 }  // namespace

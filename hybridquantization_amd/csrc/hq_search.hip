@@ -536,10 +536,10 @@ __global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
     grid_cell_body(a, p, blockIdx.x, c, valid, exh);
 }
 // ----------------------------------------------------------------------------
-// finalize: grid (P), block 256.  Fixed-order fp64 sum of the tile partials
+// finalize: grid (P), block 1024.  Fixed-order fp64 sum of the tile partials
 // and OR of the per-block used masks -> out[p] = {sum, used[0..K-1]}.
 // ----------------------------------------------------------------------------
-// finalize: one 1024-thread workgroup per palette.  Thread t sums partials
+// One 1024-thread workgroup per palette.  Thread t sums partials
 // t, t + 1024, ... with all of its loads issued before the first add (one memory
 // round trip; 256 threads summing 8 at a time took ~10 dependent rounds), then
 // a fixed-order wave and workgroup reduction: bitwise reproducible.

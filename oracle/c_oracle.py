@@ -36,6 +36,8 @@ def lib():
                                _f, C.c_float, C.c_int, C.c_int, _i32, _i32, _f, _d, _d]
         L.hqo_eval.restype = C.c_int
         L.hqo_assign.argtypes = [_f, C.c_longlong, _f, C.c_int, _i32, _i32]
+        L.hqo_assign_mt.argtypes = [_f, C.c_longlong, _f, C.c_int, _i32, _i32, C.c_int]
+        L.hqo_assign_mt.restype = C.c_int
         L.hqo_rgb_to_xyz.argtypes = [_f, _f, _f, C.c_longlong, _f]
         L.hqo_xyz_to_scielab.argtypes = [_f, C.c_int, C.c_int, _f, _f, _f, _f, C.c_int, _f, _f]
         L.hqo_xyz_to_scielab.restype = C.c_int
@@ -56,12 +58,16 @@ def _c32(a):
     return np.ascontiguousarray(a, dtype=np.float32)
 
 
-def assign(rgb4, pal4):
+def assign(rgb4, pal4, nthreads=1):
+    """Exhaustive argmin (CL:179-193) -> (idx[N] int32, used[K] int32)."""
     rgb4, pal4 = _c32(rgb4), _c32(pal4)
     n, K = rgb4.shape[0], pal4.shape[0]
     idx = np.zeros(n, np.int32)
     used = np.zeros(K, np.int32)
-    lib().hqo_assign(_p(rgb4), n, _p(pal4), K, _p(idx, _i32), _p(used, _i32))
+    if nthreads > 1:
+        lib().hqo_assign_mt(_p(rgb4), n, _p(pal4), K, _p(idx, _i32), _p(used, _i32), int(nthreads))
+    else:
+        lib().hqo_assign(_p(rgb4), n, _p(pal4), K, _p(idx, _i32), _p(used, _i32))
     return idx, used
 
 

@@ -117,6 +117,29 @@ int hqo_assign(const float *rgb4, long long n, const float *pal4, int K, int32_t
     return 0;
 }
 
+/* hqo_assign over pixel ranges on nthreads threads (same per-pixel arithmetic). */
+typedef struct { const float *rgb4, *pal4; long long n; int K, chunks; int32_t *idx; } assign_mt_ctx;
+
+static void assign_chunks(void *a, int lo, int hi) {
+    assign_mt_ctx *c = (assign_mt_ctx *)a;
+    for (int ch = lo; ch < hi; ++ch) {
+        const long long b = c->n * ch / c->chunks, e = c->n * (ch + 1) / c->chunks;
+        for (long long i = b; i < e; ++i) c->idx[i] = argmin_px(c->rgb4 + 4 * i, c->pal4, c->K);
+    }
+}
+
+int hqo_assign_mt(const float *rgb4, long long n, const float *pal4, int K, int32_t *idx,
+                  int32_t *used, int nthreads) {
+    if (!idx || n < 1 || K < 1) return -1;
+    assign_mt_ctx c = {rgb4, pal4, n, K, nthreads > 1 ? 8 * nthreads : 1, idx};
+    parallel_for(c.chunks, nthreads, assign_chunks, &c);
+    if (used) {
+        memset(used, 0, sizeof(int32_t) * (size_t)K);
+        for (long long i = 0; i < n; ++i) used[idx[i]] = 1;   /* CL:193 */
+    }
+    return 0;
+}
+
 /* ------------------------------------------------------------------------ */
 /* Candidate cost: steps a-h.                                                */
 /* ------------------------------------------------------------------------ */

@@ -103,7 +103,7 @@ def test_two_process_shards_allreduce_to_full(gpu):
     costs, used = m.computeQuantizationErrorPopulation(pals, 2.0, return_used=True)
     m.close()
     ref = ref.reshape(P, 1 + K)
-    # H // 2 = 65 rows is not a multiple of the 8-row tile: the shards' tiles
+    # H // 2 = 65 rows is not a multiple of the 16-row cost16w tile: the shards' tiles
     # group the pixels differently from the full image's, so the fp32 per-item
     # sums inside a tile round differently (~1e-9); aligned shards agree to 1e-9
     # (test_gpu.py::test_config4_8192_shards_sum_to_full)

@@ -233,6 +233,80 @@ def test_assign_group_sizes(ip, P):
         np.testing.assert_array_equal(used[p], ref_used)
 
 
+@pytest.mark.parametrize("grid", [64, 32, 16])
+def test_grid_margin_adversarial(ip, grid):
+    """build_grid's fp32 box bounds and its 1e-5 candidate margin (hq_search.hip)
+    on the inputs that sit exactly on the decision boundaries: pixels on cell
+    faces i/G2 (and on 0.0 / 1.0) and one ulp either side, palette colours on
+    faces and corners, colour pairs mirrored across a face (exactly equidistant
+    from the pixels on the face: the lower index must win, CL:186), and colour
+    pairs one ulp apart.  Pruned argmin == exhaustive == the oracle, bit for bit,
+    indices and used flags (CL:179-193)."""
+    rng = np.random.default_rng(2024 + grid)
+    w, h = 128, 96
+    n = w * h
+    faces = (np.arange(grid + 1) / grid).astype(np.float32)  # exact: G2 is a power of two
+    vals = np.concatenate([faces, np.nextafter(faces[:-1], np.float32(2)),
+                           np.nextafter(faces[1:], np.float32(-1))])
+    px = np.zeros((n, 4), np.float32)
+    px[:, :3] = rng.choice(vals, size=(n, 3))
+    px[:64, :3] = 1.0
+    px[64:128, :3] = 0.0
+    K = 256
+    pals = np.zeros((4, K, 4), np.float32)
+    pals[0, :, :3] = rng.choice(faces, size=(K, 3))  # faces and corners
+    # mirrored pairs across a face f on one axis; pixels placed on the face
+    for i in range(K // 2):
+        ax = i % 3
+        f = faces[rng.integers(1, grid)]
+        d = np.float32(rng.integers(1, 8)) / np.float32(4 * grid)
+        base = rng.choice(faces, 3)
+        a, b = base.copy(), base.copy()
+        a[ax], b[ax] = f - d, f + d
+        pals[1, 2 * i, :3], pals[1, 2 * i + 1, :3] = np.clip(a, 0, 1), np.clip(b, 0, 1)
+        on = base.copy()
+        on[ax] = f
+        px[128 + i, :3] = on
+    # pairs one ulp apart, on faces and at random points
+    c = np.where(rng.random((K // 2, 3)) < 0.5, rng.choice(faces, (K // 2, 3)),
+                 rng.random((K // 2, 3), dtype=np.float32)).astype(np.float32)
+    pals[2, 0::2, :3] = c
+    pals[2, 1::2, :3] = np.nextafter(c, np.float32(2))
+    # u8-grid colours with face values mixed in and exact duplicates
+    pals[3, :, :3] = (rng.integers(0, 256, (K, 3)) / 255.0).astype(np.float32)
+    pals[3, ::7, 0] = rng.choice(faces, len(pals[3, ::7]))
+    pals[3, 200:210] = pals[3, 3]
+    ip.setImage(px.reshape(-1), np.zeros_like(px).reshape(-1), w, ip.illum)
+    refs = [c_oracle.assign(px, pals[p]) for p in range(4)]
+    for g in (grid, 0):
+        ip.setOption("grid", g)
+        _, used = ip.computeQuantizationErrorPopulation(pals.reshape(4, -1), 2.0, return_used=True)
+        for p in range(4):
+            np.testing.assert_array_equal(ip.getIndices(p), refs[p][0].astype(np.uint8),
+                                          err_msg=f"grid {g} palette {p}")
+            np.testing.assert_array_equal(used[p], refs[p][1], err_msg=f"grid {g} palette {p}")
+
+
+def test_out_of_range_palette_takes_generic_path(ip, filt):
+    """A palette colour beyond the fast path's split-f16 range (G = 2.5: its
+    opponent value x 2^14 overflows f16) is routed to the generic fp32 path
+    (palette_fits_fast, hq_runtime.hip): a finite cost equal to the oracle's,
+    indices bit-exact.  The SA itself only produces colours in [0, 1]."""
+    g, R, G, B = load_case("case_97x53_k64")
+    w = int(g["w"])
+    rgba = o.inline_rgba(R, G, B)
+    ip.setImage(rgba.reshape(-1), g["lab"].reshape(-1), w, ip.illum)
+    pal = g["palettes"][0].copy()
+    pal[3, 1] = 2.5
+    pal[5, 2] = -40.0
+    pals = np.stack([pal, g["palettes"][1]])
+    costs = ip.computeQuantizationErrorPopulation(pals.reshape(2, -1), 2.0)
+    for p in range(2):
+        ref, parts = c_oracle.eval_palette(rgba, g["lab"], pals[p], filt, w, return_parts=True)
+        assert np.isfinite(costs[p]) and abs(costs[p] - ref) <= 1e-6 * abs(ref), (p, costs[p], ref)
+        np.testing.assert_array_equal(ip.getIndices(p), parts["idx"].astype(np.uint8))
+
+
 def test_nonfinite_palette_falls_back_exactly(ip):
     w = h = 32
     px = np.zeros((w * h, 4), np.float32)
@@ -562,16 +636,18 @@ def test_config3_4096_k256_p4_vs_oracle(gpu, filt):
 def test_config5_p64_one_launch(gpu, filt):
     """C5 (4096x4096, K = 256, P = 64 palettes in one launch): every cost and
     used flag is bit-identical to 64 separate single-palette evaluations (same
-    per-tile partials, same fixed-order sum), and palettes 0, 31 and 63 match
-    the oracle (device LabRef as the oracle's input: LabRef parity at this size
-    is test_config3's)."""
+    per-tile partials, same fixed-order sum); all 64 palettes' used flags and 8
+    palettes' indices equal the oracle's argmin, and palettes 0, 31 and 63's
+    costs match the oracle (device LabRef as the oracle's input: LabRef parity
+    at this size is test_config3's)."""
     w = h = 4096
     K, P = 256, 64
     R, G, B = o.synthetic_image(w, h, seed=1)
     m = _planar_ctx(gpu, R, G, B, w, h, filt.illum)
     pals = np.stack([o.synthetic_palette(K, 100 + p) for p in range(P)])
     costs, used = m.computeQuantizationErrorPopulation(pals.reshape(P, -1), 2.0, return_used=True)
-    idx63 = m.getIndices(63)
+    checked = (0, 9, 18, 27, 36, 45, 54, 63)
+    idx = {p: m.getIndices(p) for p in checked}
     assert np.all(np.isfinite(costs))
     for p in range(P):
         c1, u1 = m.computeQuantizationErrorPopulation(pals[p].reshape(1, -1), 2.0, return_used=True)
@@ -581,21 +657,23 @@ def test_config5_p64_one_launch(gpu, filt):
     m.close()
     rgba = o.inline_rgba(R, G, B)
     nt = _threads()
+    for p in range(P):  # every palette's used flags against the oracle's argmin
+        ref_idx, ref_used = c_oracle.assign(rgba, pals[p], nthreads=nt)
+        np.testing.assert_array_equal(used[p], ref_used, err_msg=f"palette {p}")
+        if p in idx:
+            np.testing.assert_array_equal(idx[p], ref_idx.astype(np.uint8), err_msg=f"palette {p}")
     for p in (0, 31, 63):
         ref, parts = c_oracle.eval_palette(rgba, lab, pals[p], filt, w, nthreads=nt,
                                            return_parts=True)
         assert abs(costs[p] - ref) <= COST_RTOL * abs(ref), (p, costs[p], ref)
-        np.testing.assert_array_equal(used[p], parts["used"])
-        if p == 63:
-            np.testing.assert_array_equal(idx63, parts["idx"].astype(np.uint8))
 
 
 def test_config4_8192_shards_sum_to_full(gpu, filt):
     """C4 (8192x8192, K = 256, row-block shards of 8 GPUs): the partials of the
     eight 1024-row shards (each with its +-10 halo rows, evaluated in its own
     context) sum to the full-image evaluation (fp64 sums to 1e-9 relative, used
-    flags exact), and the full image matches the oracle on one palette (device
-    LabRef as the oracle's input; LabRef parity is test_config3's)."""
+    flags exact), the device LabRef equals the oracle's at 8192^2 (2e-4), and the
+    full image matches the oracle on one palette (cost, used flags, indices)."""
     w = h = 8192
     K, P, N = 256, 4, 8
     R, G, B = o.synthetic_image(w, h, seed=1)
@@ -619,6 +697,9 @@ def test_config4_8192_shards_sum_to_full(gpu, filt):
     acc, ref = acc.reshape(P, 1 + K), ref.reshape(P, 1 + K)
     np.testing.assert_allclose(acc[:, 0], ref[:, 0], rtol=1e-9)
     np.testing.assert_array_equal(acc[:, 1:] > 0, ref[:, 1:] > 0)
+    lab_ref = c_oracle.srgb_to_scielab(R, G, B, filt, w, nthreads=_threads())
+    np.testing.assert_allclose(lab, lab_ref, atol=2e-4)  # device LabRef at 8192^2
+    del lab_ref
     rgba = o.inline_rgba(R, G, B)
     del R, G, B
     cost, parts = c_oracle.eval_palette(rgba, lab, pals[0].reshape(K, 4), filt, w,
