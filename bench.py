@@ -170,6 +170,8 @@ def main():
     ap.add_argument("--population", type=int, default=4)
     ap.add_argument("--grid", type=int, default=32)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--dpi", type=int, default=72, help="viewing geometry (HQ:229-231): screen dpi")
+    ap.add_argument("--distance", type=float, default=45.0, help="viewing distance in cm")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="extra libhq option (hq.h), repeatable; for experiments")
     ap.add_argument("--shard-of", type=int, default=0, metavar="N",
@@ -201,7 +203,7 @@ def main():
     m = hq.ImageManipulation(hq.deltaETypes.CIE76, device=local)
     if not m.getOpenCLAvailable():
         raise RuntimeError("bench.py: libhq could not open the GPU")
-    sp = hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
+    sp = hq.ScielabProcessor(args.dpi, args.distance, hq.Whitepoint.D65, None, m)
     m.setOption("grid", args.grid)
     if args.shard_of > 0:
         m.setOption("shard_solo", 1)
@@ -330,6 +332,8 @@ def main():
                    "image": f"{W}x{H}", "K": args.K, "population": P,
                    "parallelism": f"row-block x{world} + RCCL all-reduce" if world > 1 else "1 GPU",
                    "argmin_grid": args.grid,
+                   **({"dpi": args.dpi, "distance_cm": args.distance}
+                      if (args.dpi, args.distance) != (72, 45.0) else {}),
                    **({"shard_of": args.shard_of, "rows": [r0, r1]} if args.shard_of > 0 else {}),
                    **({"options": args.opt} if args.opt else {})},
         "roofline": {"bound": "valu", "achieved": round(achieved_tf, 2), "peak": FP32_PEAK_TFLOPS,

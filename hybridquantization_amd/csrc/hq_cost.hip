@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <vector>
 
 namespace hq {
 
@@ -427,66 +428,110 @@ __global__ __launch_bounds__(256, 6) void cost_mfma_kernel(CostArgs a, int P_) {
 }
 
 // ----------------------------------------------------------------------------
-// cost16w: 16 x 128 output tiles of a 36 x 148 region.  The random
+// cost16w<HB>: 16 x 128 output tiles of a (16 + 2 HB) x (128 + 2 HB) region,
+// HB = the tap bucket's half-width: the filters' own half-width H <= HB sits
+// centred in 2 HB + 1 taps (zero-padded; Tile16, fast_bucket), so every viewing
+// geometry of the plugin (dpi, distance: HQ:229-231, SP:80-102, IM:408) up to
+// H = 24 runs this kernel.  HB = 10 is the default 21-tap set.  The random
 // opponent-table gathers of the vertical pass and the horizontal windows are
 // the kernel's LDS traffic; FP32 VALU issue (horizontal taps, Lab/dE) bounds it.
-// - vertical pass: output rows 0-7 take region rows 0-31, rows 8-15 take rows
-//   8-39 (36-39 zero-weight): with lane group g holding every 4th row (kv_row),
-//   each lane keeps six of its eight half-0 values for half 1, gathers one
-//   more and zeroes one (rows 36-39) -- 36 gathered rows per 16 output rows
-//   instead of 64, no divergence.
-//   10 blocks of 16 columns (5 ranges of 32) cover the 148 region columns
-//   (+12 unread): each block is the 16 columns of one parity half of a range
+// - vertical pass on the matrix cores: output rows 0-7 take region rows
+//   0 .. 32 S - 1 (S K steps of 32 rows), rows 8-15 take rows 8 .. 32 S + 7.
+//   Lane group g holds every 4th row (kv_row: K slot (g, j) of step s = row
+//   32 s + 4 j + g), so half 1's operand of step s is half 0's with dword 0
+//   replaced by the next step's dword 0: each lane gathers 8 S + 2 rows (the
+//   ones past the region are zero, not gathered) for 2 x 8 output rows, no
+//   divergence.  At HB = 10 (S = 1): 36 gathered rows per 16 output rows.
+//   RW / 16 blocks of 16 columns (ranges of 32) cover the region columns
+//   (+ unread ones): each block is the 16 columns of one parity half of a range
 //   (lane n -> column 4(n >> 1) + 2 (b & 1) + (n & 1)), so its stores fill 16
 //   contiguous float2 of one half: conflict free without padding.  Block sets
 //   {s, s+4, s+8} go to the waves, rotated per workgroup.
 // - horizontal pass: items of 4 output columns x a row pair (256 items, one per
-//   thread: 8 row pairs x 32), a 24-column window = 12 ds_read_b128 per filter
-//   for 8 outputs.  Row-pair rows store their column pairs split by parity
-//   (pair p -> half p & 1, slot p >> 1), so read q of item j lands at half
-//   q & 1, slot j + q / 2: lanes 16 B apart, conflict free.  (The 108-column
-//   tile of a 128-column region gave 27 items to 32 threads: 16% of the lanes
-//   idle through the horizontal pass and Lab/dE; 0.398 vs 0.383 ms.)
-// - the 160-column row-pair planes (30 KiB for three) fit 4 workgroups per CU
-//   three filters at a time, so the channels run in three phases: channel 0
-//   (f0, f1, f2), channel 1 (f3, f4), channel 2 (f5, f6).  Channels 1 and 2
-//   share one gather per region row; channel 2's vertical results wait in
-//   registers through channel 1's horizontal pass.  39,584 B of LDS.
+//   thread: 8 row pairs x 32), a (4 + 2 HB)-column window = 2 + HB ds_read_b128
+//   per filter for 8 outputs.  Row-pair rows store their column pairs split by
+//   parity (pair p -> half p & 1, slot p >> 1), so read q of item j lands at
+//   half q & 1, slot j + q / 2: lanes 16 B apart, conflict free.  (The
+//   108-column tile of a 128-column region gave 27 items to 32 threads: 16% of
+//   the lanes idle through the horizontal pass and Lab/dE; 0.398 vs 0.383 ms.)
+// - the row-pair planes fit 4 workgroups per CU (3 for HB > 10) three filters
+//   at a time, so the channels run in three phases: channel 0 (f0, f1, f2),
+//   channel 1 (f3, f4), channel 2 (f5, f6).  Channels 1 and 2 share one gather
+//   per region row; channel 2's vertical results wait in registers through
+//   channel 1's horizontal pass.  HB = 10: 39,584 B of LDS.
 // ----------------------------------------------------------------------------
 constexpr int kTH16 = 16;
-constexpr int kWHalfW = 80;  // float2 per half of a 160-column permuted row-pair row
+
+template <int HB>
+struct Tile16 {
+    static constexpr int TH = kTH16, TW = 128, HR = 4;
+    static constexpr int RWL = TW + 2 * HB;            // region columns read
+    static constexpr int RW = (RWL + 31) / 32 * 32;    // LDS pitch: whole 32-column ranges
+    static constexpr int RH = TH + 2 * HB;             // region rows
+    static constexpr int NBLK = RW / 16;               // vertical-pass column blocks
+    static constexpr int NSET = (NBLK + 3) / 4;        // blocks per wave (at most)
+    static constexpr int WH = RW / 2;                  // float2 per half of a permuted row-pair row
+    static constexpr int S = (8 + 2 * HB + 31) / 32;   // K steps of 32 rows per output-row half
+    static constexpr int NJ = 8 * S + 2;               // K slots (rows 4 n + g) a lane gathers
+    static constexpr int PLANE4 = (TH / 2) * RW / 2;   // f32x4 per filter plane
+    static constexpr int NQ = (HR + 2 * HB) / 2;       // horizontal window reads per filter
+    static_assert(RWL % 4 == 0 && RWL / 4 >= 32 && RWL / 4 < 64, "TileFill: 32 <= dwords per row < 64");
+    static_assert(NSET <= 3, "three blocks per wave at most");
+};
+
+// Significant half-windows of the narrow k1.x / k1.y / k1.z filters per bucket:
+// the largest over every geometry whose H falls in the bucket (checked per
+// filter set at hq_set_filters: trim_window_ok; the windows of 18 dpi x 13
+// distance settings were swept with the oracle's filter design, SP:66-254).
+__host__ __device__ constexpr int trim_w(int HB, int ch) {
+    return HB == 10 ? (ch == 0 ? 3 : ch == 1 ? 4 : 5)
+         : HB == 16 ? (ch == 0 ? 4 : ch == 1 ? 6 : 8)
+         : HB == 20 ? (ch == 0 ? 5 : ch == 1 ? 7 : 10)
+                    : (ch == 0 ? 6 : ch == 1 ? 9 : 12);
+}
+
+// Region row of K slot (g, j) of step s for output-row half `half` (see above).
+__host__ __device__ __forceinline__ constexpr int kv_row_s(int half, int s, int g, int j) {
+    return half == 0 || j >= 2 ? 32 * s + 4 * j + g : 32 * (s + 1) + 4 * j + g;
+}
 
 // float2 position of column `col` in a permuted row-pair row: half = bit 1 of
 // col, 16-B slot col >> 2, float2 col & 1.
-template <int WH = kWHalfW>
+template <int WH>
 __device__ __forceinline__ int wide_pos(int col) {
     return ((col >> 1) & 1) * WH + ((col >> 2) << 1) + (col & 1);
 }
 
 // Horizontal pass of filter f for item j (output columns 4j .. 4j+3) of a row
 // pair: src = the row-pair row in plane 0; pstride = f32x4 per plane; taps
-// [TLO, THI].
-template <int HALF, int TLO = 0, int THI = 2 * HALF, int WH = kWHalfW>
-__device__ __forceinline__ void hpass_wide(const f32x4* src, int j, TapsPtr<HALF> taps, int f,
+// [TLO, THI].  Item j's read q (columns 4j + 2q, +1) sits at half q & 1,
+// slot j + q / 2.  Windows longer than 24 columns run in chunks of 12 taps
+// (each chunk's reads issued together) to bound the live registers.
+template <int HB, int TLO = 0, int THI = 2 * HB, int WH = 80>
+__device__ __forceinline__ void hpass_wide(const f32x4* src, int j, TapsPtr<HB> taps, int f,
                                            int plane, int pstride, f32x2 (&acc)[4]) {
-    constexpr int HR = 4, NQ = (HR + 2 * HALF) / 2;  // 12 reads of 2 columns
-    // item j's read q: half q & 1, slot j + q / 2
+    constexpr int HR = 4;
+    constexpr int CH = HB <= 10 ? 2 * HB + 1 : 12;  // taps per chunk
     const f32x4* row = src + plane * pstride + j;
-    f32x4 v[NQ];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) v[q] = row[(q & 1) * (WH / 2) + (q >> 1)];
-    f32x2 in[2 * NQ];
+    for (int t0 = TLO; t0 <= THI; t0 += CH) {
+        const int t1 = t0 + CH - 1 < THI ? t0 + CH - 1 : THI;
+        const int q0 = t0 / 2, q1 = (t1 + HR - 1) / 2;  // reads covering columns t0 .. t1 + 3
+        f32x2 in[2 * (CH / 2 + 3)];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        in[2 * q] = v[q].xy;
-        in[2 * q + 1] = v[q].zw;
-    }
+        for (int q = q0; q <= q1; ++q) {
+            const f32x4 v = row[(q & 1) * (WH / 2) + (q >> 1)];
+            in[2 * (q - q0)] = v.xy;
+            in[2 * (q - q0) + 1] = v.zw;
+        }
 #pragma unroll
-    for (int t = TLO; t <= THI; ++t) {
-        const float k = taps->h[f][t];
-        const f32x2 kk = {k, k};
+        for (int t = t0; t <= t1; ++t) {
+            const float k = taps->h[f][t];
+            const f32x2 kk = {k, k};
 #pragma unroll
-        for (int xo = 0; xo < HR; ++xo) acc[xo] = __builtin_elementwise_fma(in[xo + t], kk, acc[xo]);
+            for (int xo = 0; xo < HR; ++xo)
+                acc[xo] = __builtin_elementwise_fma(in[xo + t - 2 * q0], kk, acc[xo]);
+        }
     }
 }
 
@@ -509,17 +554,53 @@ __device__ __forceinline__ void store_vstack_at(f32x2* base, const f32x4v& d, in
     v[ROW] = f32x2{d[2], d[3]};
 }
 
+__device__ __forceinline__ f32x4v mfma3_acc(const f16x8& ah, const f16x8& al, const f16x8& bh,
+                                            const f16x8& bl, f32x4v d) {
+    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, d, 0, 0, 0);
+    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, d, 0, 0, 0);
+    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, d, 0, 0, 0);
+    return d;
+}
 
+// One column block's vertical products for up to two stacks: w[NJ] = the
+// gathered (hi, lo) dwords of rows 4 n + g; A[stack][half][step][hi, lo] the
+// split-f16 tap fragments.  d[stack][half] = both halves' 16 x 16 blocks.
+template <int S, int NST>
+__device__ __forceinline__ void vblock(const uint32_t (&w)[8 * S + 2], const uint4 (&A)[NST][2][S][2],
+                                       f32x4v (&d)[NST][2]) {
+    auto H = [](const uint4& u) { return __builtin_bit_cast(f16x8, u); };
+    auto B = [](const u32x4& u) { return __builtin_bit_cast(f16x8, u); };
+#pragma unroll
+    for (int st = 0; st < NST; ++st) d[st][0] = d[st][1] = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        u32x4 bh, bl;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            bh[m] = __builtin_amdgcn_perm(w[8 * s + 2 * m + 1], w[8 * s + 2 * m], 0x05040100u);  // hi halves
+            bl[m] = __builtin_amdgcn_perm(w[8 * s + 2 * m + 1], w[8 * s + 2 * m], 0x07060302u);  // lo halves
+        }
+        const uint32_t nh = __builtin_amdgcn_perm(w[8 * s + 9], w[8 * s + 8], 0x05040100u);
+        const uint32_t nl = __builtin_amdgcn_perm(w[8 * s + 9], w[8 * s + 8], 0x07060302u);
+#pragma unroll
+        for (int st = 0; st < NST; ++st)
+            d[st][0] = mfma3_acc(H(A[st][0][s][0]), H(A[st][0][s][1]), B(bh), B(bl), d[st][0]);
+        bh[0] = nh;  // half 1 of step s: half 0's operand with dword 0 of step s + 1
+        bl[0] = nl;
+#pragma unroll
+        for (int st = 0; st < NST; ++st)
+            d[st][1] = mfma3_acc(H(A[st][1][s][0]), H(A[st][1][s][1]), B(bh), B(bl), d[st][1]);
+    }
+}
 
-template <int DE, bool TRIM>
-__global__ __launch_bounds__(256, 4) void cost16w_kernel(CostArgs a, int P_) {
-    constexpr int HALF = 10, TH = kTH16, HR = 4, T2 = 2 * HALF;
-    constexpr int TW = 128, RWL = TW + 2 * HALF, RW = 160;  // outputs, region read, LDS pitch
-    constexpr int RH = TH + 2 * HALF;                       // 36 region rows
-    constexpr int PAIRS = TH / 2, ROW = 2 * kWHalfW;        // float2 per row-pair row
-    constexpr int PLANE4 = PAIRS * ROW / 2;                 // f32x4 per filter plane
-    constexpr int NBLK = RW / 16;                           // vertical-pass blocks
-    static_assert(TW / HR == 32 && kv_row(1, 3, 0) < RH && RWL <= RW, "tile");
+template <int HB, int DE, bool TRIM>
+__global__ __launch_bounds__(256, HB == 10 ? 4 : (HB == 16 ? 3 : 2)) void cost16w_kernel(CostArgs a, int P_) {
+    using Gm = Tile16<HB>;
+    constexpr int TH = kTH16, HR = 4, T2 = 2 * HB, TW = Gm::TW, RWL = Gm::RWL, RW = Gm::RW;
+    constexpr int RH = Gm::RH, WH = Gm::WH, NBLK = Gm::NBLK, NSET = Gm::NSET, S = Gm::S, NJ = Gm::NJ;
+    constexpr int ROW = 2 * WH, PLANE4 = Gm::PLANE4;
+    constexpr int L0 = HB - trim_w(HB, 0), L1 = HB - trim_w(HB, 1), L2 = HB - trim_w(HB, 2);
+    static_assert(TW / HR == 32, "tile");
     __shared__ f32x4 s_vq[3 * PLANE4];
     __shared__ uint32_t s_ox[kMaxK];  // opponent x 2^14 as (hi, lo) f16 pairs: channel 0
     __shared__ uint2 s_oyz[kMaxK];     // channels 1, 2
@@ -529,16 +610,24 @@ __global__ __launch_bounds__(256, 4) void cost16w_kernel(CostArgs a, int P_) {
     const int tid = threadIdx.x;
     const Geom& g = a.g;
     const TileItem cur = tile_item<TW, TH>(a, xcd_remap(blockIdx.x, a.ntiles * P_), P_);
-    const TapsPtr<HALF> taps = (TapsPtr<HALF>)(uintptr_t)a.taps;  // H taps x 2^-30
+    const TapsPtr<HB> taps = (TapsPtr<HB>)(uintptr_t)a.taps;  // H taps x 2^-30
     const int lane = tid & 63, wv = tid >> 6, lc = lane & 15, lk = lane >> 4;
-    // [trim][half][stack][hi, lo][lane]
-    const uint4* frag = a.vfrag16 + (TRIM ? 2 * 4 * 2 * 64 : 0) + lane;
-    auto F = [&](int half, int st, int hl) { return frag[((half * 4 + st) * 2 + hl) * 64]; };
+    // [trim][half][step][stack][hi, lo][lane]
+    const uint4* frag = a.vfrag16 + (TRIM ? 2 * S * 4 * 2 * 64 : 0) + lane;
+    auto F = [&](int half, int s, int st, int hl) { return frag[(((half * S + s) * 4 + st) * 2 + hl) * 64]; };
 
-    TileFill<HALF, RWL, TH> fill;
+    TileFill<HB, RWL, TH> fill;
     fill.issue(a, cur, tid);
-    uint4 A00h = F(0, 0, 0), A00l = F(0, 0, 1), A01h = F(0, 1, 0), A01l = F(0, 1, 1);  // half 0
-    uint4 A10h = F(1, 0, 0), A10l = F(1, 0, 1), A11h = F(1, 1, 0), A11l = F(1, 1, 1);  // half 1
+    uint4 A[2][2][S][2];  // channel 0's stacks (f0, f1), (f2, -); then channels 1-2's
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                A[st][h][s][0] = F(h, s, st, 0);
+                A[st][h][s][1] = F(h, s, st, 1);
+            }
     // every entry (zeros for tid >= K): zero-weight rows and the columns past
     // the region gather arbitrary indices, and 0 x NaN would be NaN
     s_ox[tid] = fill.ov.x;
@@ -553,101 +642,108 @@ __global__ __launch_bounds__(256, 4) void cost16w_kernel(CostArgs a, int P_) {
     for (int xo = 0; xo < HR; ++xo) acc0[xo] = acc1[xo] = acc2[xo] = f32x2{0.f, 0.f};
     __syncthreads();
 
-    // Vertical pass of channel `ch` on this wave's blocks: stacks (s0: planes
-    // pa0/pb0) and, for channel 0, (s1: plane pa1).  Block b = wset + 4i covers
-    // the 16 columns of parity half b & 1 of range b >> 1.  Block sets 0 and 1
-    // hold 3 blocks, sets 2 and 3 hold 2: the sets rotate with the workgroup,
-    // so the extra blocks do not land on the same SIMDs in every workgroup.
+    // Block b = wset + 4i covers the 16 columns of parity half b & 1 of range
+    // b >> 1.  With 10 blocks, sets 0 and 1 hold 3 blocks and sets 2 and 3 hold
+    // 2: the sets rotate with the workgroup, so the extra blocks do not land on
+    // the same SIMDs in every workgroup.
     const int wset = (wv + (int)blockIdx.x) & 3;
-    // block wset + 4i covers column col0 + 64 i of its parity half
     const int col0 = 32 * (wset >> 1) + 4 * (lc >> 1) + (lc & 1) + 2 * (wset & 1);
-    f32x2* const st01 = vstack_base<kWHalfW>(s_v, lk < 2 ? 0 : 1, lk, col0);  // stacks -> planes 0, 1
-    f32x2* const st2 = vstack_base<kWHalfW>(s_v, 2, lk, col0);                // (f2, -) -> plane 2
-    auto B = [](const u32x4& u) { return __builtin_bit_cast(f16x8, u); };
-    auto vpass0 = [&](const f16x8& h0h, const f16x8& h0l, const f16x8& h1h, const f16x8& h1l,
-                      const f16x8& k0h, const f16x8& k0l, const f16x8& k1h, const f16x8& k1l) {
-        const uint32_t* tab = s_ox;
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const int b = wset + 4 * i;
-            if (b >= NBLK) break;
-            const int col = col0 + 64 * i;
-            uint32_t w[10];  // slots 0-7: half 0; w[8], w[9]: half 1's slots 0, 1 (kv_row)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) w[j] = tab[s_idx[kv_row(0, lk, j) * RW + col]];
-            w[8] = tab[s_idx[kv_row(1, lk, 0) * RW + col]];
-            w[9] = 0u;  // K slot (half 1, g, 1) = row 36 + g: zero taps, not in the region
-            u32x4 bh, bl;
-            uint32_t nh, nl;
-            pack_b_halves(w, bh, bl, nh, nl);
-            const f32x4v d00 = mfma3(h0h, h0l, B(bh), B(bl)), d01 = mfma3(k0h, k0l, B(bh), B(bl));
-            bh[0] = nh; bl[0] = nl;
-            const f32x4v d10 = mfma3(h1h, h1l, B(bh), B(bl)), d11 = mfma3(k1h, k1l, B(bh), B(bl));
-            store_vstack_at<kWHalfW>(st01, d00, i, 0);
-            store_vstack_at<kWHalfW>(st01, d10, i, 1);
-            if (lk < 2) {  // the (f2, -) stack's second filter slot is empty
-                store_vstack_at<kWHalfW>(st2, d01, i, 0);
-                store_vstack_at<kWHalfW>(st2, d11, i, 1);
-            }
-        }
+    f32x2* const st01 = vstack_base<WH>(s_v, lk < 2 ? 0 : 1, lk, col0);  // stacks -> planes 0, 1
+    f32x2* const st2 = vstack_base<WH>(s_v, 2, lk, col0);                // (f2, -) -> plane 2
+    // gather of K slot n (rows 4 n + lk) of column col from a table; slots past
+    // the region are zero (zero taps), a partly covered slot reads a clamped row
+    auto gather_row = [&](int n, int col) {
+        const int row = 4 * n + lk;
+        return (4 * n + 3 < RH ? row : min(row, RH - 1)) * RW + col;
     };
-    auto H = [](const uint4& u) { return __builtin_bit_cast(f16x8, u); };
 
     // ---- channel 0: stacks (f0, f1) -> planes 0, 1 and (f2, -) -> plane 2 ----
-    vpass0(H(A00h), H(A00l), H(A10h), H(A10l), H(A01h), H(A01l), H(A11h), H(A11l));
-    // channel 1-2 stacks, in flight during channel 0's horizontal pass
-    A00h = F(0, 2, 0); A00l = F(0, 2, 1); A01h = F(0, 3, 0); A01l = F(0, 3, 1);
-    A10h = F(1, 2, 0); A10l = F(1, 2, 1); A11h = F(1, 3, 0); A11l = F(1, 3, 1);
+#pragma unroll
+    for (int i = 0; i < NSET; ++i) {
+        const int b = wset + 4 * i;
+        if (b >= NBLK) break;
+        const int col = col0 + 64 * i;
+        uint32_t w[NJ];
+#pragma unroll
+        for (int n = 0; n < NJ; ++n) w[n] = 4 * n < RH ? s_ox[s_idx[gather_row(n, col)]] : 0u;
+        f32x4v d[2][2];
+        vblock<S, 2>(w, A, d);
+        store_vstack_at<WH>(st01, d[0][0], i, 0);
+        store_vstack_at<WH>(st01, d[0][1], i, 1);
+        if (lk < 2) {  // the (f2, -) stack's second filter slot is empty
+            store_vstack_at<WH>(st2, d[1][0], i, 0);
+            store_vstack_at<WH>(st2, d[1][1], i, 1);
+        }
+    }
+    // channel 1-2 stacks: in flight during channel 0's horizontal pass with one
+    // K step (32 VGPRs); with two, loaded after it (64 VGPRs would spill)
+    auto load_a12 = [&]() {
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    A[st][h][s][0] = F(h, s, 2 + st, 0);
+                    A[st][h][s][1] = F(h, s, 2 + st, 1);
+                }
+    };
+    if constexpr (S == 1) load_a12();
     __syncthreads();
-    if constexpr (TRIM) hpass_wide<HALF, kTrimLo[0], kTrimHi[0], kWHalfW>(hsrc, jr, taps, 0, 0, PLANE4, acc0);
-    else hpass_wide<HALF, 0, T2, kWHalfW>(hsrc, jr, taps, 0, 0, PLANE4, acc0);
-    hpass_wide<HALF, 0, T2, kWHalfW>(hsrc, jr, taps, 1, 1, PLANE4, acc0);
-    hpass_wide<HALF, 0, T2, kWHalfW>(hsrc, jr, taps, 2, 2, PLANE4, acc0);
+    if constexpr (TRIM) hpass_wide<HB, L0, T2 - L0, WH>(hsrc, jr, taps, 0, 0, PLANE4, acc0);
+    else hpass_wide<HB, 0, T2, WH>(hsrc, jr, taps, 0, 0, PLANE4, acc0);
+    hpass_wide<HB, 0, T2, WH>(hsrc, jr, taps, 1, 1, PLANE4, acc0);
+    hpass_wide<HB, 0, T2, WH>(hsrc, jr, taps, 2, 2, PLANE4, acc0);
     __syncthreads();
 
     // ---- channels 1, 2: one gather of (y, z) per region row; stack (f3, f4)
     // -> planes 0, 1 now, stack (f5, f6)'s results held in registers until
     // channel 1's horizontal pass has read the planes ----
-    f32x4v d5[3][2];
+    if constexpr (S > 1) load_a12();
+    f32x4v d5[NSET][2];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < NSET; ++i) {
         const int b = wset + 4 * i;
         if (b >= NBLK) break;
         const int col = col0 + 64 * i;
-        uint32_t wy[10], wz[10];  // slots 0-7: half 0; [8], [9]: half 1's slots 0, 1
+        uint32_t wy[NJ], wz[NJ];
 #pragma unroll
-        for (int j = 0; j < 9; ++j) {
-            const int row = j < 8 ? kv_row(0, lk, j) : kv_row(1, lk, 0);
-            const uint2 e = s_oyz[s_idx[row * RW + col]];
-            wy[j] = e.x; wz[j] = e.y;
+        for (int n = 0; n < NJ; ++n) {
+            if (4 * n < RH) {
+                const uint2 e = s_oyz[s_idx[gather_row(n, col)]];
+                wy[n] = e.x; wz[n] = e.y;
+            } else {
+                wy[n] = wz[n] = 0u;
+            }
         }
-        wy[9] = wz[9] = 0u;  // row 36 + g: zero taps, not in the region
-        u32x4 bh, bl;
-        uint32_t nh, nl;
-        pack_b_halves(wy, bh, bl, nh, nl);
-        const f32x4v d30 = mfma3(H(A00h), H(A00l), B(bh), B(bl));
-        bh[0] = nh; bl[0] = nl;
-        const f32x4v d31 = mfma3(H(A10h), H(A10l), B(bh), B(bl));
-        store_vstack_at<kWHalfW>(st01, d30, i, 0);
-        store_vstack_at<kWHalfW>(st01, d31, i, 1);
-        pack_b_halves(wz, bh, bl, nh, nl);
-        d5[i][0] = mfma3(H(A01h), H(A01l), B(bh), B(bl));
-        bh[0] = nh; bl[0] = nl;
-        d5[i][1] = mfma3(H(A11h), H(A11l), B(bh), B(bl));
+        {
+            const uint4(&Ay)[1][2][S][2] = *reinterpret_cast<const uint4(*)[1][2][S][2]>(&A[0]);
+            f32x4v d[1][2];
+            vblock<S, 1>(wy, Ay, d);
+            store_vstack_at<WH>(st01, d[0][0], i, 0);
+            store_vstack_at<WH>(st01, d[0][1], i, 1);
+        }
+        {
+            const uint4(&Az)[1][2][S][2] = *reinterpret_cast<const uint4(*)[1][2][S][2]>(&A[1]);
+            f32x4v d[1][2];
+            vblock<S, 1>(wz, Az, d);
+            d5[i][0] = d[0][0];
+            d5[i][1] = d[0][1];
+        }
     }
     __syncthreads();
-    if constexpr (TRIM) hpass_wide<HALF, kTrimLo[1], kTrimHi[1], kWHalfW>(hsrc, jr, taps, 3, 0, PLANE4, acc1);
-    else hpass_wide<HALF, 0, T2, kWHalfW>(hsrc, jr, taps, 3, 0, PLANE4, acc1);
-    hpass_wide<HALF, 0, T2, kWHalfW>(hsrc, jr, taps, 4, 1, PLANE4, acc1);
+    if constexpr (TRIM) hpass_wide<HB, L1, T2 - L1, WH>(hsrc, jr, taps, 3, 0, PLANE4, acc1);
+    else hpass_wide<HB, 0, T2, WH>(hsrc, jr, taps, 3, 0, PLANE4, acc1);
+    hpass_wide<HB, 0, T2, WH>(hsrc, jr, taps, 4, 1, PLANE4, acc1);
     __syncthreads();
 
     // ---- channel 2: stack (f5, f6) -> planes 0, 1 ----
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < NSET; ++i) {
         const int b = wset + 4 * i;
         if (b >= NBLK) break;
-        store_vstack_at<kWHalfW>(st01, d5[i][0], i, 0);
-        store_vstack_at<kWHalfW>(st01, d5[i][1], i, 1);
+        store_vstack_at<WH>(st01, d5[i][0], i, 0);
+        store_vstack_at<WH>(st01, d5[i][1], i, 1);
     }
     // LabRef of the item's 2 x 4 pixels, in flight across the barrier
     float4 lab[2][3];
@@ -662,9 +758,9 @@ __global__ __launch_bounds__(256, 4) void cost16w_kernel(CostArgs a, int P_) {
                                                           (off << 2));  // 32-bit byte offset
     }
     __syncthreads();
-    if constexpr (TRIM) hpass_wide<HALF, kTrimLo[2], kTrimHi[2], kWHalfW>(hsrc, jr, taps, 5, 0, PLANE4, acc2);
-    else hpass_wide<HALF, 0, T2, kWHalfW>(hsrc, jr, taps, 5, 0, PLANE4, acc2);
-    hpass_wide<HALF, 0, T2, kWHalfW>(hsrc, jr, taps, 6, 1, PLANE4, acc2);
+    if constexpr (TRIM) hpass_wide<HB, L2, T2 - L2, WH>(hsrc, jr, taps, 5, 0, PLANE4, acc2);
+    else hpass_wide<HB, 0, T2, WH>(hsrc, jr, taps, 5, 0, PLANE4, acc2);
+    hpass_wide<HB, 0, T2, WH>(hsrc, jr, taps, 6, 1, PLANE4, acc2);
 
     float e[2][HR];
 #pragma unroll
@@ -705,11 +801,12 @@ __global__ __launch_bounds__(256, 4) void cost16w_kernel(CostArgs a, int P_) {
 // (CL:274-306) restated per pixel through a [7][n_ext] fp32 scratch, one
 // palette per launch pair.  It cross-checks the fast path in the tests.
 // ----------------------------------------------------------------------------
+template <typename IT>
 __global__ __launch_bounds__(256) void gen_hpass_kernel(GenArgs a) {
     const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (q >= a.g.n_ext) return;
     const int ly = (int)(q / a.g.W), x = (int)(q % a.g.W);
-    const uint8_t* row = a.idx + (int64_t)ly * a.g.W;
+    const IT* row = static_cast<const IT*>(a.idx) + (int64_t)ly * a.g.W;
     float t1x = 0, t1y = 0, t1z = 0, t2x = 0, t2y = 0, t2z = 0, t3 = 0;
     for (int i = -a.half, t = 0; i <= a.half; ++i, ++t) {  // CL:254-267
         const float4 in = a.opp[row[reflect_only(x + i, a.g.W)]];
@@ -765,17 +862,30 @@ void opp2xyz_over_illum(const float inv_illum[3], float m[9]) {
     for (int i = 0; i < 9; ++i) m[i] = (float)((double)opp2xyz[i] * inv_illum[i / 3] * 1560896.0);
 }
 
-static void make_taps10(const float* k1, const float* k2, const float* k3, const float* absk3,
-                        CostTaps<10>& t) {
-    for (int i = 0; i < 21; ++i) {
-        // f: 0 k1.x, 1 k2.x, 2 k3 (|k3| vertical), 3 k1.y, 4 k2.y, 5 k1.z, 6 k2.z
-        t.v[0][i] = k1[4 * i + 0]; t.h[0][i] = k1[4 * i + 0];
-        t.v[1][i] = k2[4 * i + 0]; t.h[1][i] = k2[4 * i + 0];
-        t.v[2][i] = absk3[i];      t.h[2][i] = k3[i];
-        t.v[3][i] = k1[4 * i + 1]; t.h[3][i] = k1[4 * i + 1];
-        t.v[4][i] = k2[4 * i + 1]; t.h[4][i] = k2[4 * i + 1];
-        t.v[5][i] = k1[4 * i + 2]; t.h[5][i] = k1[4 * i + 2];
-        t.v[6][i] = k2[4 * i + 2]; t.h[6][i] = k2[4 * i + 2];
+// The fast path's tap bucket for a filter half-width H (halfSize, IM:408): the
+// smallest of 10, 16, 20, 24 that holds it; 0 = none (H > 24: the generic path).
+int fast_bucket(int half) {
+    return half <= 10 ? 10 : half <= 16 ? 16 : half <= 20 ? 20 : half <= 24 ? 24 : 0;
+}
+
+static int bucket_steps(int HB) { return (8 + 2 * HB + 31) / 32; }
+
+// The 7 filters (f: 0 k1.x, 1 k2.x, 2 k3 (|k3| vertical), 3 k1.y, 4 k2.y,
+// 5 k1.z, 6 k2.z) of half-width H centred in 2 HB + 1 taps (zeros around):
+// v[f][d], h[f][d], d = 0 .. 2 HB, row-major [7][2 HB + 1].
+static void bucket_taps(const float* k1, const float* k2, const float* k3, const float* absk3, int H,
+                        int HB, std::vector<float>& v, std::vector<float>& h) {
+    const int T = 2 * HB + 1, off = HB - H;
+    v.assign(kNumFilt * T, 0.f);
+    h.assign(kNumFilt * T, 0.f);
+    for (int i = 0; i < 2 * H + 1; ++i) {
+        const int d = i + off;
+        const float vv[7] = {k1[4 * i], k2[4 * i], absk3[i], k1[4 * i + 1], k2[4 * i + 1], k1[4 * i + 2], k2[4 * i + 2]};
+        const float hh[7] = {k1[4 * i], k2[4 * i], k3[i], k1[4 * i + 1], k2[4 * i + 1], k1[4 * i + 2], k2[4 * i + 2]};
+        for (int f = 0; f < kNumFilt; ++f) {
+            v[f * T + d] = vv[f];
+            h[f * T + d] = hh[f];
+        }
     }
 }
 
@@ -808,70 +918,86 @@ static float host_f16_to_f32(uint16_t h) {
 }
 
 // Split-f16 A fragments of v_mfma_f32_16x16x32_f16 for the vertical pass,
-// [trim][half][stack][hi, lo][lane] x 8 halves (trim 0 = all 21 taps, 1 = the
-// narrow filters' significant windows).  Lane l holds A[i = l & 15][k = 8g + j],
-// g = l >> 4: the tap (x 2^16) of filter stack[i >> 3] that multiplies the
-// region row held in K slot k into output row 8 half + (i & 7), i.e. tap
-// d = row - 8 half - (i & 7), zero outside [0, 20] (and outside the window).
-// The region row of K slot (g, j) is kv_row(half, g, j): half 1 (output rows
-// 8-15 of a 16-row tile) reuses six of half 0's slots per lane, so its B
-// operand costs two gathered values per lane instead of eight.
-size_t vpass_f16_stack_fragment_halves() { return 2 * 2 * 4 * 2 * 64 * 8; }
+// [trim][half][step][stack][hi, lo][lane] x 8 halves (trim 0 = all taps, 1 =
+// the narrow filters' significant windows).  Lane l holds A[i = l & 15][k = 8g
+// + j], g = l >> 4: the tap (x 2^16) of filter stack[i >> 3] that multiplies
+// the region row held in K slot k of step s into output row 8 half + (i & 7),
+// i.e. bucket tap d = row - 8 half - (i & 7), zero outside [0, 2 HB] (and
+// outside the trimmed window).  The region row of K slot (g, j) is
+// kv_row_s(half, s, g, j): half 1 (output rows 8-15 of a 16-row tile) reuses
+// six of half 0's slots per lane, so its B operand costs two gathered values
+// per lane per step instead of eight.  At HB = 10 (one step) this is also the
+// layout cost_mfma_kernel reads (half 0 only).
+size_t vpass_f16_stack_fragment_halves(int HB) { return (size_t)2 * 2 * bucket_steps(HB) * 4 * 2 * 64 * 8; }
 
-void build_vpass_f16_stack_fragments(const float* k1, const float* k2, const float* k3,
+void build_vpass_f16_stack_fragments(int HB, int H, const float* k1, const float* k2, const float* k3,
                                      const float* absk3, uint16_t* out) {
-    CostTaps<10> t;
-    make_taps10(k1, k2, k3, absk3, t);
+    std::vector<float> tv, th;
+    bucket_taps(k1, k2, k3, absk3, H, HB, tv, th);
+    const int T = 2 * HB + 1, S = bucket_steps(HB);
     const int stack[4][2] = {{0, 1}, {2, -1}, {3, 4}, {5, 6}};
     for (int trim = 0; trim < 2; ++trim)
         for (int half = 0; half < 2; ++half)
-        for (int st = 0; st < 4; ++st)
-            for (int l = 0; l < 64; ++l)
-                for (int j = 0; j < 8; ++j) {
-                    const int i = l & 15, g = l >> 4, r = i & 7, f = stack[st][i >> 3];
-                    const int row = kv_row(half, g, j);
-                    const int d = row - 8 * half - r;
-                    float w = 0.f;
-                    if (f >= 0 && d >= 0 && d <= 20) {
-                        w = t.v[f][d];
-                        const int ch = f == 0 ? 0 : (f == 3 ? 1 : (f == 5 ? 2 : -1));
-                        if (trim && ch >= 0 && (d < kTrimLo[ch] || d > kTrimHi[ch])) w = 0.f;
-                    }
-                    w *= kVTapScale;
-                    const uint16_t hi = host_f16(w);
-                    const uint16_t lo = host_f16(w - host_f16_to_f32(hi));
-                    out[((((trim * 2 + half) * 4 + st) * 2 + 0) * 64 + l) * 8 + j] = hi;
-                    out[((((trim * 2 + half) * 4 + st) * 2 + 1) * 64 + l) * 8 + j] = lo;
-                }
+            for (int s = 0; s < S; ++s)
+                for (int st = 0; st < 4; ++st)
+                    for (int l = 0; l < 64; ++l)
+                        for (int j = 0; j < 8; ++j) {
+                            const int i = l & 15, g = l >> 4, r = i & 7, f = stack[st][i >> 3];
+                            const int row = kv_row_s(half, s, g, j);
+                            const int d = row - 8 * half - r;
+                            float w = 0.f;
+                            if (f >= 0 && d >= 0 && d < T) {
+                                w = tv[f * T + d];
+                                const int ch = f == 0 ? 0 : (f == 3 ? 1 : (f == 5 ? 2 : -1));
+                                if (trim && ch >= 0 && std::abs(d - HB) > trim_w(HB, ch)) w = 0.f;
+                            }
+                            w *= kVTapScale;
+                            const uint16_t hi = host_f16(w);
+                            const uint16_t lo = host_f16(w - host_f16_to_f32(hi));
+                            const size_t base = (((((size_t)trim * 2 + half) * S + s) * 4 + st) * 2) * 64;
+                            out[((base + 0 * 64) + l) * 8 + j] = hi;
+                            out[((base + 1 * 64) + l) * 8 + j] = lo;
+                        }
 }
 
-bool trim_window_ok(const float* k1) {
-    const int ch[3] = {0, 1, 2};
-    for (int i = 0; i < 3; ++i) {
+// The narrow k1 filters' taps outside the bucket's trimmed windows are below
+// 1e-9 of their peak (then the fast path may skip them; else it runs all taps).
+bool trim_window_ok(const float* k1, int H, int HB) {
+    for (int ch = 0; ch < 3; ++ch) {
         float peak = 0.f;
-        for (int t = 0; t < 21; ++t) peak = std::max(peak, std::fabs(k1[4 * t + ch[i]]));
-        for (int t = 0; t < 21; ++t)
-            if ((t < kTrimLo[i] || t > kTrimHi[i]) && std::fabs(k1[4 * t + ch[i]]) > 1e-9f * peak)
-                return false;
+        for (int t = 0; t < 2 * H + 1; ++t) peak = std::max(peak, std::fabs(k1[4 * t + ch]));
+        for (int t = 0; t < 2 * H + 1; ++t)
+            if (std::abs(t - H) > trim_w(HB, ch) && std::fabs(k1[4 * t + ch]) > 1e-9f * peak) return false;
     }
     return true;
 }
 
-size_t fast_taps_bytes() { return 2 * sizeof(CostTaps<10>); }
+template <int HB>
+static size_t taps_bytes() { return 2 * sizeof(CostTaps<HB>); }
 
-// [0] the taps as designed, [1] the same with the horizontal taps scaled by
-// 2^-30 (exact) for the matrix-core vertical pass, whose outputs carry 2^30.
-void build_fast_taps(const float* k1, const float* k2, const float* k3, const float* absk3,
-                     void* out) {
-    CostTaps<10> t[2];
-    make_taps10(k1, k2, k3, absk3, t[0]);
-    t[1] = t[0];
-    for (int f = 0; f < kNumFilt; ++f)
-        for (int i = 0; i < 2 * kFastHalf + 1; ++i) t[1].h[f][i] *= kVOutScale;
-    std::memcpy(out, t, sizeof t);
+size_t fast_taps_bytes(int HB) {
+    switch (HB) {
+    case 10: return taps_bytes<10>();
+    case 16: return taps_bytes<16>();
+    case 20: return taps_bytes<20>();
+    default: return taps_bytes<24>();
+    }
 }
 
-// a.taps = the two CostTaps<10> of build_fast_taps
+// [0] the bucket's taps as designed, [1] the same with the horizontal taps
+// scaled by 2^-30 (exact) for the matrix-core vertical pass, whose outputs
+// carry 2^30.  Layout: two CostTaps<HB>.
+void build_fast_taps(int HB, int H, const float* k1, const float* k2, const float* k3, const float* absk3,
+                     void* out) {
+    std::vector<float> tv, th;
+    bucket_taps(k1, k2, k3, absk3, H, HB, tv, th);
+    const size_t n = tv.size();  // == sizeof(CostTaps<HB>) / 8
+    float* o = static_cast<float*>(out);
+    for (int copy = 0; copy < 2; ++copy, o += 2 * n) {
+        std::memcpy(o, tv.data(), n * sizeof(float));
+        for (size_t i = 0; i < n; ++i) o[n + i] = copy ? th[i] * kVOutScale : th[i];
+    }
+}
 
 // tile_rows: 8 (cost_mfma_kernel, 8 x 108 tiles) or 16 (cost16w_kernel, 16 x 128 tiles)
 void fast_tile_dims(int W, int own_rows, int tile_rows, int* tiles_x, int* ntiles) {
@@ -880,27 +1006,48 @@ void fast_tile_dims(int W, int own_rows, int tile_rows, int* tiles_x, int* ntile
     *ntiles = *tiles_x * ((own_rows + tile_rows - 1) / tile_rows);
 }
 
-// a.taps = the two CostTaps<10> of build_fast_taps; [1] carries the vertical
-// pass's 2^30 scale in its horizontal taps.
-hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, bool trim, int tile_rows,
+// a.taps = the two CostTaps<HB> of build_fast_taps; [1] carries the vertical
+// pass's 2^30 scale in its horizontal taps.  8-row tiles: HB = 10 only.
+template <int HB>
+static void launch_cost16w(const CostArgs& a0, int P, int de, bool trim, hipStream_t s) {
+    CostArgs a = a0;
+    a.taps = static_cast<const char*>(a0.taps) + sizeof(CostTaps<HB>);
+    const dim3 grid((unsigned)(a.ntiles * P));
+    if (de == 0) {
+        if (trim) HQ_LAUNCH((cost16w_kernel<HB, 0, true>), grid, dim3(256), 0, s, a, P);
+        else HQ_LAUNCH((cost16w_kernel<HB, 0, false>), grid, dim3(256), 0, s, a, P);
+    } else {
+        if (trim) HQ_LAUNCH((cost16w_kernel<HB, 1, true>), grid, dim3(256), 0, s, a, P);
+        else HQ_LAUNCH((cost16w_kernel<HB, 1, false>), grid, dim3(256), 0, s, a, P);
+    }
+}
+
+hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, bool trim, int tile_rows, int HB,
                             hipStream_t s) {
+    if (tile_rows == kTH16) {
+        switch (HB) {
+        case 10: launch_cost16w<10>(a0, P, de, trim, s); break;
+        case 16: launch_cost16w<16>(a0, P, de, trim, s); break;
+        case 20: launch_cost16w<20>(a0, P, de, trim, s); break;
+        case 24: launch_cost16w<24>(a0, P, de, trim, s); break;
+        default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
+    if (HB != 10) return hipErrorInvalidValue;
     CostArgs a = a0;
     a.taps = static_cast<const char*>(a0.taps) + sizeof(CostTaps<10>);
     const dim3 grid((unsigned)(a.ntiles * P));
 #define HQ_COST(KN, DEV, TR) HQ_LAUNCH((KN<DEV, TR>), grid, dim3(256), 0, s, a, P)
-    if (tile_rows == kTH16) {
-        if (de == 0) { if (trim) HQ_COST(cost16w_kernel, 0, true); else HQ_COST(cost16w_kernel, 0, false); }
-        else { if (trim) HQ_COST(cost16w_kernel, 1, true); else HQ_COST(cost16w_kernel, 1, false); }
-    } else {
-        if (de == 0) { if (trim) HQ_COST(cost_mfma_kernel, 0, true); else HQ_COST(cost_mfma_kernel, 0, false); }
-        else { if (trim) HQ_COST(cost_mfma_kernel, 1, true); else HQ_COST(cost_mfma_kernel, 1, false); }
-    }
+    if (de == 0) { if (trim) HQ_COST(cost_mfma_kernel, 0, true); else HQ_COST(cost_mfma_kernel, 0, false); }
+    else { if (trim) HQ_COST(cost_mfma_kernel, 1, true); else HQ_COST(cost_mfma_kernel, 1, false); }
 #undef HQ_COST
     return hipGetLastError();
 }
 
-hipError_t launch_cost_generic(const GenArgs& a, int de, hipStream_t s) {
-    HQ_LAUNCH(gen_hpass_kernel, dim3(blocks_for(a.g.n_ext)), dim3(256), 0, s, a);
+hipError_t launch_cost_generic(const GenArgs& a, int de, bool idx32, hipStream_t s) {
+    if (idx32) HQ_LAUNCH(gen_hpass_kernel<uint32_t>, dim3(blocks_for(a.g.n_ext)), dim3(256), 0, s, a);
+    else HQ_LAUNCH(gen_hpass_kernel<uint8_t>, dim3(blocks_for(a.g.n_ext)), dim3(256), 0, s, a);
     const int64_t n_own = (int64_t)a.g.W * (a.g.r1 - a.g.r0);
     if (de == 0)
         HQ_LAUNCH(gen_vpass_kernel<0>, dim3(blocks_for(n_own)), dim3(256), 0, s, a);
@@ -908,6 +1055,5 @@ hipError_t launch_cost_generic(const GenArgs& a, int de, hipStream_t s) {
         HQ_LAUNCH(gen_vpass_kernel<1>, dim3(blocks_for(n_own)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
-
 
 }  // namespace hq

@@ -7,7 +7,8 @@
 
 namespace hq {
 
-constexpr int kMaxK = 256;        // u8 palette indices (K <= 256 on this path)
+constexpr int kMaxK = 256;        // u8 palette indices (K <= 256 on the tiled path)
+constexpr int kMaxKWide = 1 << 24;  // K > 256: 32-bit indices (the plugin's limit, HQ:192)
 constexpr int kMaxTaps = 255;     // generic path limit (2*half+1)
 constexpr int kNumFilt = 7;       // separable filter pairs of the S-CIELAB stencil
 constexpr int kL1Cap = 31;        // level-1 candidate list capacity (32-B entry)
@@ -111,6 +112,7 @@ struct AssignArgs {
     int K;
     int G2;                 // 0 = exhaustive
     int nblocks;            // blocks per palette (= used_mask blocks per palette)
+    int variant;            // 0 assign_pipe_kernel, 1 assign_quad_kernel (P >= 4)
 };
 
 struct CostArgs {
@@ -137,12 +139,29 @@ struct FinalizeArgs {
     int ntiles;
     int nblocks;
     int K;
+    const uint32_t* used32; // K > 256: [P][K] used flags (assign_wide), replaces used_mask
+};
+
+// Palettes of K > 256 colours (hq_wide.hip).
+struct WideArgs {
+    const float4* pal_in;   // [P][K] host-uploaded palettes
+    float4* pal;            // [P][K] .w = 0
+    float4* opp;            // [P][K] opponent colours (CL:194-198)
+    int* pflags;            // [P] bit 0: non-finite colour (zeroed before prep)
+    const float* R;         // planar extended rows
+    const float* G;
+    const float* B;
+    uint32_t* idx32;        // [P][idx_pitch] 32-bit palette indices
+    uint32_t* used32;       // [P][K] used flags (zeroed before assign)
+    int64_t n_ext;
+    int64_t idx_pitch;      // elements per palette
+    int K;
 };
 
 // Generic two-pass path (any half-width), one palette per launch.
 struct GenArgs {
-    const uint8_t* idx;      // palette's index image (extended rows)
-    const float4* opp;       // palette's opponent table [256]
+    const void* idx;         // palette's index image (extended rows): u8, or u32 for K > 256
+    const float4* opp;       // palette's opponent table [max(K, 256)]
     const float* k1;         // [T][4]
     const float* k2;         // [T][4]
     const float* k3;         // [T]

@@ -26,16 +26,19 @@ hipError_t launch_build_grid(const GridArgs&, int P, hipStream_t);
 hipError_t launch_assign(const AssignArgs&, int P, hipStream_t);
 void fast_tile_dims(int W, int own_rows, int tile_rows, int* tiles_x, int* ntiles);
 void opp2xyz_over_illum(const float inv_illum[3], float m[9]);
-hipError_t launch_cost_fast(const CostArgs&, int P, int de, bool trim, int tile_rows, hipStream_t);
-size_t vpass_f16_stack_fragment_halves();
-void build_vpass_f16_stack_fragments(const float* k1, const float* k2, const float* k3,
+hipError_t launch_cost_fast(const CostArgs&, int P, int de, bool trim, int tile_rows, int HB, hipStream_t);
+int fast_bucket(int half);
+size_t vpass_f16_stack_fragment_halves(int HB);
+void build_vpass_f16_stack_fragments(int HB, int H, const float* k1, const float* k2, const float* k3,
                                      const float* absk3, uint16_t* out);
-size_t fast_taps_bytes();
-void build_fast_taps(const float* k1, const float* k2, const float* k3, const float* absk3,
+size_t fast_taps_bytes(int HB);
+void build_fast_taps(int HB, int H, const float* k1, const float* k2, const float* k3, const float* absk3,
                      void* out);
-bool trim_window_ok(const float* k1);
+bool trim_window_ok(const float* k1, int H, int HB);
 
-hipError_t launch_cost_generic(const GenArgs&, int de, hipStream_t);
+hipError_t launch_cost_generic(const GenArgs&, int de, bool idx32, hipStream_t);
+hipError_t launch_prep_wide(const WideArgs&, int P, hipStream_t);
+hipError_t launch_assign_wide(const WideArgs&, int P, hipStream_t);
 hipError_t launch_finalize(const FinalizeArgs&, int P, hipStream_t);
 hipError_t launch_labref_opp(const float*, const float*, const float*, float4*, int64_t, hipStream_t);
 hipError_t launch_xyz_to_opp(const float4*, float4*, int64_t, hipStream_t);
@@ -91,7 +94,8 @@ struct hq_ctx {
     int taps = 0, half = 0;
     std::vector<float> k1, k2, k3, absk3;
     DevBuf d_k1, d_k2, d_k3, d_absk3;
-    DevBuf d_taps;     // fast path taps, build_fast_taps (21-tap filters)
+    int fast_hb = 0;   // fast path tap bucket (fast_bucket(half)); 0 = generic path only
+    DevBuf d_taps;     // fast path taps, build_fast_taps (the filters centred in the bucket)
     DevBuf d_vfrag16;  // split-f16 MFMA A fragments of the stacked vertical taps
 
     // image
@@ -105,6 +109,7 @@ struct hq_ctx {
     int P_cap = 0, K_cur = 0;
     DevBuf d_pal_in, d_pal, d_opp, d_opp16, d_dup, d_pflags, d_lvl1, d_lvl2, d_idx, d_used_mask,
         d_partial, d_out, d_gen_t;
+    DevBuf d_idx32, d_used32;  // K > 256 (hq_wide.hip): 32-bit index images, per-colour used flags
     float* h_pal = nullptr;   // pinned [P][K][4]
     double* h_out = nullptr;  // pinned [P][1+K]
     size_t h_pal_bytes = 0, h_out_bytes = 0;
@@ -114,12 +119,13 @@ struct hq_ctx {
     int G2 = 32;           // argmin grid resolution (0 = exhaustive)
     int cost_variant = 0;  // 0 tiled (default), 1 generic two-pass
     int cost_rows = 16;    // fast path tiles: 16 x 128 (cost16w_kernel) or 8 x 108 (cost_mfma_kernel)
+    int assign_variant = 0;  // 0 assign_pipe_kernel, 1 assign_quad_kernel (P >= 4)
     int assign_blocks_per_cu = 16;  // 4096^2: 4 chunks per workgroup; 0.632 -> 0.605 ms per step vs 8
     int shard_solo = 0;    // experiment: a sharded search without a communicator (per-rank timing)
     int sa_device = 1;     // hq_search_*: 1 = SWASA iterations resident on the device (no host
                            // round trip per iteration), 0 = host-driven (one eval call each)
     int trim = 1;          // skip taps < 1e-9 of the peak of the narrow k1 filters
-    bool trim_ok = false;  // set by hq_set_filters (default 21-tap filter set)
+    bool trim_ok = false;  // set by hq_set_filters (the bucket's narrow-filter windows hold)
     bool pal_generic = false;  // this population needs the generic cost path (palette_fits_fast)
 
     // comm
@@ -336,8 +342,12 @@ int ensure_population(hq_ctx* c, int P, int K) {
     const int64_t nparts = std::max<int64_t>(ntiles, gen_blocks);
     const int nblocks = assign_blocks(c);
     HIP_TRY(c, c->d_pal_in.ensure(sizeof(float4) * (size_t)P * K));
-    HIP_TRY(c, c->d_pal.ensure(sizeof(float4) * (size_t)P * kMaxK));
-    HIP_TRY(c, c->d_opp.ensure(sizeof(float4) * (size_t)P * kMaxK));
+    HIP_TRY(c, c->d_pal.ensure(sizeof(float4) * (size_t)P * std::max(K, kMaxK)));
+    HIP_TRY(c, c->d_opp.ensure(sizeof(float4) * (size_t)P * std::max(K, kMaxK)));
+    if (K > kMaxK) {
+        HIP_TRY(c, c->d_idx32.ensure(sizeof(uint32_t) * (size_t)P * g.idx_pitch));
+        HIP_TRY(c, c->d_used32.ensure(sizeof(uint32_t) * (size_t)P * K));
+    }
     HIP_TRY(c, c->d_opp16.ensure(sizeof(uint4) * (size_t)P * kMaxK));
     HIP_TRY(c, c->d_dup.ensure((size_t)P * kMaxK));
     HIP_TRY(c, c->d_pflags.ensure(sizeof(int) * (size_t)P));
@@ -379,6 +389,74 @@ GridArgs grid_args(hq_ctx* c, int K) {
                     round_up((int64_t)G1 * G1 * G1 * 32, 256), round_up((int64_t)G2 * G2 * G2 * 64, 256)};
 }
 
+// The generic two-pass cost (CL:234-306 per pixel, any half-width) of P
+// palettes, one launch pair each: index images at idx_base (u8, or u32 when
+// idx32) with c->g.idx_pitch elements per palette, opponent tables of
+// opp_stride entries per palette in d_opp.  Times the first palette's pair.
+int enqueue_generic_cost(hq_ctx* c, int P, const void* idx_base, bool idx32, int opp_stride,
+                         const hipEvent_t* ev, int* nparts_out) {
+    const Geom& g = c->g;
+    hipStream_t s = c->stream;
+    HIP_TRY(c, c->d_gen_t.ensure(sizeof(float) * 7 * (size_t)g.n_ext));
+    const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
+    const int nparts = (int)((n_own + 255) / 256);
+    const float inv[3] = {1.0f / c->illum[0], 1.0f / c->illum[1], 1.0f / c->illum[2]};
+    for (int p = 0; p < P; ++p) {
+        GenArgs gn{};
+        gn.idx = static_cast<const char*>(idx_base) + (int64_t)p * g.idx_pitch * (idx32 ? 4 : 1);
+        gn.opp = c->d_opp.as<float4>() + (int64_t)p * opp_stride;
+        gn.k1 = c->d_k1.as<float>();
+        gn.k2 = c->d_k2.as<float>();
+        gn.k3 = c->d_k3.as<float>();
+        gn.absk3 = c->d_absk3.as<float>();
+        gn.t = c->d_gen_t.as<float>();
+        gn.labL = c->d_labL.as<float>();
+        gn.labA = c->d_labA.as<float>();
+        gn.labB = c->d_labB.as<float>();
+        gn.partial = c->d_partial.as<double>() + (int64_t)p * nparts;
+        gn.g = g;
+        gn.half = c->half;
+        opp2xyz_over_illum(inv, gn.m_lab);
+        if (p == 0 && ev) set_launch_events(ev[4], ev[5]);  // the first palette's two launches
+        const hipError_t e = launch_cost_generic(gn, c->de_type, idx32, s);
+        set_launch_events(nullptr, nullptr);
+        HIP_TRY(c, e);
+    }
+    *nparts_out = nparts;
+    return HQ_OK;
+}
+
+// K > 256 (hq_wide.hip): prep, exhaustive argmin into 32-bit indices and
+// per-colour used flags, the generic cost, finalize, [all-reduce].
+int enqueue_wide(hq_ctx* c, int P, int K, const hipEvent_t* ev) {
+    const Geom& g = c->g;
+    hipStream_t s = c->stream;
+    WideArgs wa{c->d_pal_in.as<float4>(), c->d_pal.as<float4>(), c->d_opp.as<float4>(), c->d_pflags.as<int>(),
+                c->d_R.as<float>(), c->d_G.as<float>(), c->d_B.as<float>(), c->d_idx32.as<uint32_t>(),
+                c->d_used32.as<uint32_t>(), g.n_ext, g.idx_pitch, K};
+    HIP_TRY(c, hipMemsetAsync(c->d_pflags.p, 0, sizeof(int) * (size_t)P, s));
+    HIP_TRY(c, launch_prep_wide(wa, P, s));
+    HIP_TRY(c, hipMemsetAsync(c->d_used32.p, 0, sizeof(uint32_t) * (size_t)P * K, s));
+    if (ev) set_launch_events(ev[2], ev[3]);
+    const hipError_t e = launch_assign_wide(wa, P, s);
+    set_launch_events(nullptr, nullptr);
+    HIP_TRY(c, e);
+    int nparts = 0;
+    int rc = enqueue_generic_cost(c, P, c->d_idx32.p, true, K, ev, &nparts);
+    if (rc) return rc;
+    FinalizeArgs fa{c->d_partial.as<double>(), nullptr, c->d_out.as<double>(), nparts, 0, K,
+                    c->d_used32.as<uint32_t>()};
+    if (ev) set_launch_events(ev[6], ev[7]);
+    const hipError_t ef = launch_finalize(fa, P, s);
+    set_launch_events(nullptr, nullptr);
+    HIP_TRY(c, ef);
+    if (c->comm)
+        NCCL_TRY(c, ncclAllReduce(c->d_out.p, c->d_out.p, (size_t)P * (1 + K), ncclFloat64, ncclSum, c->comm, s));
+    c->last_P = P;
+    c->K_cur = K;
+    return HQ_OK;
+}
+
 int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev) {
     const Geom& g = c->g;
     hipStream_t s = c->stream;
@@ -397,14 +475,16 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev) {
     const AssignArgs aa{c->d_R.as<float>(), c->d_G.as<float>(), c->d_B.as<float>(), c->d_pal.as<float4>(),
                         c->d_pflags.as<int>(), c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(),
                         c->d_idx.as<uint8_t>(), c->d_used_mask.as<uint32_t>(), g.n_ext, g.idx_pitch,
-                        ga.lvl1_pitch, ga.lvl2_gstride, K, c->G2, nblocks};
+                        ga.lvl1_pitch, ga.lvl2_gstride, K, c->G2, nblocks, c->assign_variant};
     timed(1);
     hipError_t e = launch_assign(aa, P, s);
     untimed();
     HIP_TRY(c, e);
     const float inv[3] = {1.0f / c->illum[0], 1.0f / c->illum[1], 1.0f / c->illum[2]};
     int nparts;
-    if (c->cost_variant != 1 && c->half == 10 && !c->pal_generic) {
+    if (c->cost_variant != 1 && c->fast_hb > 0 && !c->pal_generic) {
+        // 8-row tiles (cost_mfma_kernel) exist for the 21-tap bucket only
+        const int rows = c->fast_hb == 10 ? c->cost_rows : 16;
         CostArgs ca{};
         ca.idx = c->d_idx.as<uint8_t>();
         ca.opp16 = c->d_opp16.as<uint4>();
@@ -416,41 +496,19 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev) {
         ca.partial = c->d_partial.as<double>();
         ca.g = g;
         ca.K = K;
-        fast_tile_dims(g.W, g.r1 - g.r0, c->cost_rows, &ca.tiles_x, &ca.ntiles);
+        fast_tile_dims(g.W, g.r1 - g.r0, rows, &ca.tiles_x, &ca.ntiles);
         opp2xyz_over_illum(inv, ca.m_lab);
         timed(2);
-        e = launch_cost_fast(ca, P, c->de_type, c->trim && c->trim_ok, c->cost_rows, s);
+        e = launch_cost_fast(ca, P, c->de_type, c->trim && c->trim_ok, rows, c->fast_hb, s);
         untimed();
         HIP_TRY(c, e);
         nparts = ca.ntiles;
     } else {
-        HIP_TRY(c, c->d_gen_t.ensure(sizeof(float) * 7 * (size_t)g.n_ext));
-        const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
-        nparts = (int)((n_own + 255) / 256);
-        for (int p = 0; p < P; ++p) {
-            GenArgs gn{};
-            gn.idx = c->d_idx.as<uint8_t>() + (int64_t)p * g.idx_pitch;
-            gn.opp = c->d_opp.as<float4>() + (int64_t)p * kMaxK;
-            gn.k1 = c->d_k1.as<float>();
-            gn.k2 = c->d_k2.as<float>();
-            gn.k3 = c->d_k3.as<float>();
-            gn.absk3 = c->d_absk3.as<float>();
-            gn.t = c->d_gen_t.as<float>();
-            gn.labL = c->d_labL.as<float>();
-            gn.labA = c->d_labA.as<float>();
-            gn.labB = c->d_labB.as<float>();
-            gn.partial = c->d_partial.as<double>() + (int64_t)p * nparts;
-            gn.g = g;
-            gn.half = c->half;
-            opp2xyz_over_illum(inv, gn.m_lab);
-            if (p == 0) timed(2);  // times the first palette's two launches
-            e = launch_cost_generic(gn, c->de_type, s);
-            untimed();
-            HIP_TRY(c, e);
-        }
+        int rc = enqueue_generic_cost(c, P, c->d_idx.p, false, kMaxK, ev, &nparts);
+        if (rc) return rc;
     }
     FinalizeArgs fa{c->d_partial.as<double>(), c->d_used_mask.as<uint32_t>(), c->d_out.as<double>(),
-                    nparts, nblocks, K};
+                    nparts, nblocks, K, nullptr};
     timed(3);
     const hipError_t ef = launch_finalize(fa, P, s);
     untimed();
@@ -479,8 +537,13 @@ int enqueue_eval(hq_ctx* c, int P, int K) {
     HIP_TRY(c, hipMemcpyAsync(c->d_pal_in.p, c->h_pal, sizeof(float) * 4 * (size_t)P * K,
                               hipMemcpyHostToDevice, s));
     const hipEvent_t* ev = c->prof ? c->ev : nullptr;
-    HIP_TRY(c, launch_prep_palette(prep_args(c, K), P, s));
-    int rc = enqueue_core(c, P, K, ev);
+    int rc;
+    if (K > kMaxK) {
+        rc = enqueue_wide(c, P, K, ev);
+    } else {
+        HIP_TRY(c, launch_prep_palette(prep_args(c, K), P, s));
+        rc = enqueue_core(c, P, K, ev);
+    }
     if (rc) return rc;
     HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out.p, sizeof(double) * (size_t)P * (1 + K),
                               hipMemcpyDeviceToHost, s));
@@ -493,8 +556,8 @@ int check_eval_args(hq_ctx* c, const float* palettes, int P, int K) {
     if (!c) return HQ_ERR_ARG;
     if (!c->have_image) return fail(c, HQ_ERR_STATE, "no image set (hq_set_image)");
     if (!palettes || P < 1 || K < 1) return fail(c, HQ_ERR_ARG, "bad palettes / P=%d / K=%d", P, K);
-    if (K > kMaxK)
-        return fail(c, HQ_ERR_UNSUPPORTED, "K=%d > %d: the u8 index path supports K <= 256", K, kMaxK);
+    if (K > kMaxKWide)
+        return fail(c, HQ_ERR_ARG, "K=%d > %d (the plugin's limit, HQ:192)", K, kMaxKWide);
     if (c->de_type == HQ_DE_CIEDE2000)
         return fail(c, HQ_ERR_UNSUPPORTED, "CIEDE2000 is unimplemented in the reference (CL:227-230)");
     return HQ_OK;
@@ -714,7 +777,7 @@ void hq_destroy(hq_ctx* c) {
                       &c->d_labL, &c->d_labA, &c->d_labB, &c->d_pal_in, &c->d_pal, &c->d_opp, &c->d_opp16,
                       &c->d_dup, &c->d_pflags, &c->d_lvl1, &c->d_lvl2, &c->d_idx,
                       &c->d_used_mask, &c->d_partial, &c->d_out, &c->d_gen_t, &c->d_taps,
-                      &c->d_vfrag16})
+                      &c->d_vfrag16, &c->d_idx32, &c->d_used32})
         b->release();
     if (c->h_pal) (void)hipHostFree(c->h_pal);
     if (c->h_out) (void)hipHostFree(c->h_out);
@@ -749,15 +812,20 @@ int hq_set_filters(hq_ctx* c, int taps, const float* k1, const float* k2, const 
     HIP_TRY(c, hipMemcpy(c->d_k2.p, k2, sizeof(float) * 4 * taps, hipMemcpyHostToDevice));
     HIP_TRY(c, hipMemcpy(c->d_k3.p, k3, sizeof(float) * taps, hipMemcpyHostToDevice));
     HIP_TRY(c, hipMemcpy(c->d_absk3.p, absk3, sizeof(float) * taps, hipMemcpyHostToDevice));
-    c->trim_ok = taps == 21 && trim_window_ok(k1);
-    if (taps == 21) {
-        std::vector<uint16_t> f16s(vpass_f16_stack_fragment_halves());
-        build_vpass_f16_stack_fragments(k1, k2, k3, absk3, f16s.data());
+    // fast path: the filters centred in the smallest tap bucket that holds them
+    // (half-widths up to 24: every dpi / viewing distance of HQ:229-231 up to
+    // ~200 dpi at 45 cm); longer filters take the generic path
+    c->fast_hb = fast_bucket(c->half);
+    c->trim_ok = c->fast_hb > 0 && trim_window_ok(k1, c->half, c->fast_hb);
+    if (c->fast_hb > 0) {
+        const int HB = c->fast_hb;
+        std::vector<uint16_t> f16s(vpass_f16_stack_fragment_halves(HB));
+        build_vpass_f16_stack_fragments(HB, c->half, k1, k2, k3, absk3, f16s.data());
         HIP_TRY(c, c->d_vfrag16.ensure(f16s.size() * sizeof(uint16_t)));
         HIP_TRY(c, hipMemcpy(c->d_vfrag16.p, f16s.data(), f16s.size() * sizeof(uint16_t),
                              hipMemcpyHostToDevice));
-        std::vector<char> tb(fast_taps_bytes());
-        build_fast_taps(k1, k2, k3, absk3, tb.data());
+        std::vector<char> tb(fast_taps_bytes(HB));
+        build_fast_taps(HB, c->half, k1, k2, k3, absk3, tb.data());
         HIP_TRY(c, c->d_taps.ensure(tb.size()));
         HIP_TRY(c, hipMemcpy(c->d_taps.p, tb.data(), tb.size(), hipMemcpyHostToDevice));
     }
@@ -855,6 +923,8 @@ int hq_eval_population(hq_ctx* c, const float* palettes, int P, int K, float del
 int hq_get_indices(hq_ctx* c, int p, uint8_t* idx) {
     if (!c || !idx) return HQ_ERR_ARG;
     if (p < 0 || p >= c->last_P) return fail(c, HQ_ERR_ARG, "palette %d not in last population", p);
+    if (c->K_cur > kMaxK)
+        return fail(c, HQ_ERR_STATE, "K=%d > 256: indices are 32-bit (hq_get_indices32)", c->K_cur);
     int rc = bind(c);
     if (rc) return rc;
     const Geom& g = c->g;
@@ -862,6 +932,26 @@ int hq_get_indices(hq_ctx* c, int p, uint8_t* idx) {
     const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
     HIP_TRY(c, hipMemcpy(idx, c->d_idx.as<uint8_t>() + (int64_t)p * g.idx_pitch + off, n_own,
                          hipMemcpyDeviceToHost));
+    return HQ_OK;
+}
+
+int hq_get_indices32(hq_ctx* c, int p, uint32_t* idx) {
+    if (!c || !idx) return HQ_ERR_ARG;
+    if (p < 0 || p >= c->last_P) return fail(c, HQ_ERR_ARG, "palette %d not in last population", p);
+    int rc = bind(c);
+    if (rc) return rc;
+    const Geom& g = c->g;
+    const int64_t off = (int64_t)(g.r0 - g.e0) * g.W;
+    const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
+    if (c->K_cur > kMaxK) {
+        HIP_TRY(c, hipMemcpy(idx, c->d_idx32.as<uint32_t>() + (int64_t)p * g.idx_pitch + off,
+                             sizeof(uint32_t) * n_own, hipMemcpyDeviceToHost));
+        return HQ_OK;
+    }
+    std::vector<uint8_t> b((size_t)n_own);
+    HIP_TRY(c, hipMemcpy(b.data(), c->d_idx.as<uint8_t>() + (int64_t)p * g.idx_pitch + off, n_own,
+                         hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < n_own; ++i) idx[i] = b[i];
     return HQ_OK;
 }
 
@@ -1122,6 +1212,9 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
         c->sa_device = value != 0;
     } else if (!std::strcmp(name, "shard_solo")) {
         c->shard_solo = value != 0;
+    } else if (!std::strcmp(name, "assign_variant")) {
+        if (value < 0 || value > 1) return fail(c, HQ_ERR_ARG, "assign_variant must be 0 or 1");
+        c->assign_variant = value;
     } else if (!std::strcmp(name, "assign_blocks_per_cu")) {
         if (value < 1 || value > 64) return fail(c, HQ_ERR_ARG, "assign_blocks_per_cu in [1,64]");
         c->assign_blocks_per_cu = value;

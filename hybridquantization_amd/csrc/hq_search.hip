@@ -571,7 +571,7 @@ __global__ __launch_bounds__(1024) void finalize_kernel(FinalizeArgs a) {
     uint32_t m = 0;
     const int w = tid & 7;
     const uint32_t* um = a.used_mask + (int64_t)p * a.nblocks * 8;
-    for (int b0 = tid >> 3; b0 < a.nblocks; b0 += (NT / 8) * MU) {
+    for (int b0 = tid >> 3; !a.used32 && b0 < a.nblocks; b0 += (NT / 8) * MU) {
         uint32_t mv[MU];
 #pragma unroll
         for (int u = 0; u < MU; ++u) {
@@ -584,6 +584,16 @@ __global__ __launch_bounds__(1024) void finalize_kernel(FinalizeArgs a) {
     s_mask[tid] = m;
     __syncthreads();
     double* out = a.out + (int64_t)p * (1 + a.K);
+    if (a.used32) {  // K > 256: the reference's per-colour flags (assign_wide)
+        if (tid == 0) {
+            double tot = 0.0;
+            for (int i = 0; i < NT / 64; ++i) tot += s_red[i];
+            out[0] = tot;
+        }
+        const uint32_t* u = a.used32 + (int64_t)p * a.K;
+        for (int k = tid; k < a.K; k += NT) out[1 + k] = u[k] != 0u ? 1.0 : 0.0;
+        return;
+    }
     if (tid == 0) {
         double tot = 0.0;
         for (int i = 0; i < NT / 64; ++i) tot += s_red[i];

@@ -144,10 +144,18 @@ class ImageManipulation:
         return (costs, used) if return_used else costs
 
     def getIndices(self, p: int = 0):
-        """u8 palette index per pixel of palette p of the last population."""
+        """u8 palette index per pixel of palette p of the last population (K <= 256)."""
         ctx = self._require()
         out = np.zeros(self.w * self.h, np.uint8)
         check(self._lib.hq_get_indices(ctx, int(p), out.ctypes.data_as(_lib._u8)), ctx)
+        return out
+
+    def getIndices32(self, p: int = 0):
+        """32-bit palette index per pixel of palette p of the last population (any K,
+        the int index of CL:172-193)."""
+        ctx = self._require()
+        out = np.zeros(self.w * self.h, np.uint32)
+        check(self._lib.hq_get_indices32(ctx, int(p), out.ctypes.data_as(C.POINTER(C.c_uint32))), ctx)
         return out
 
     # IM:383

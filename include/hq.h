@@ -104,7 +104,9 @@ int hq_set_image_planar_shard(hq_ctx *ctx, const float *R, const float *G, const
 /* Reads back the device S-CIELAB of the owned rows as inline float4. */
 int hq_get_labref(hq_ctx *ctx, float *lab4);
 
-/* IM:620 computeQuantizationErrorPopulation for P palettes of K colours:
+/* IM:620 computeQuantizationErrorPopulation for P palettes of K colours
+ * (K in [1, 2^24] as the plugin allows, HQ:192; K > 256 runs the exhaustive
+ * argmin with 32-bit indices and the generic stencil path):
  * costs[p] = mean dE76 + delta * #unused (IM:712, SW:74-82); used[p*K+k] in
  * {0,1} (CL:193), may be NULL.  On a sharded context with a communicator the
  * partial sums are all-reduced over RCCL first. */
@@ -116,8 +118,12 @@ int hq_eval_population(hq_ctx *ctx, const float *palettes, int P, int K, float d
 int hq_eval_population_partial(hq_ctx *ctx, const float *palettes, int P, int K,
                                double *partial);
 /* Per-pixel palette indices (u8, K <= 256) of the last evaluated population's
- * palette p over the owned rows (w*(row_end-row_begin) bytes). */
+ * palette p over the owned rows (w*(row_end-row_begin) bytes).  HQ_ERR_STATE
+ * when that population had K > 256 colours. */
 int hq_get_indices(hq_ctx *ctx, int p, uint8_t *idx);
+/* The same for any K (1 .. 2^24, HQ:192): 32-bit indices, w*(row_end-row_begin)
+ * of them -- the reference's int index of CL:172-193. */
+int hq_get_indices32(hq_ctx *ctx, int p, uint32_t *idx);
 
 /* IM:770 quantize(inlineImageRGB, colors): chosen colour per pixel (CL:147-170).
  * used (K ints) may be NULL. */

@@ -148,6 +148,50 @@ def test_fast_path_matches_generic(gpu, de, trim, rows):
 
 
 # ---------------------------------------------------------------------------
+# Viewing geometry (HQ:229-231 dpi / distance -> SP:80-102 tap count -> IM:408
+# halfSize): the fast path runs the filters centred in a tap bucket of
+# half-width 10, 16, 20 or 24; longer filters take the generic path.
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("dpi,vd,half", [(96, 60.0, 19), (150, 30.0, 15), (72, 30.0, 7),
+                                         (96, 70.0, 22), (200, 30.0, 20), (300, 50.0, 51)])
+def test_viewing_geometry_vs_oracle(gpu, dpi, vd, half):
+    """Non-default dpi / viewing distance on a 256 x 256 and a ragged 301 x 173
+    image: device LabRef within 2e-4, every cost within 1e-5 relative of the
+    oracle (the bar is 1e-4), indices and used flags bit-exact; the fast path
+    (bucketed taps, trimmed or not) equals the generic fp32 two-pass path to
+    1e-6 relative."""
+    f = o.design_filters(dpi, vd)
+    assert f.half == half
+    nt = _threads()
+    for (w, h) in ((256, 256), (301, 173)):
+        R, G, B = o.synthetic_image(w, h, seed=w + dpi)
+        rgba = o.inline_rgba(R, G, B)
+        m = hq.ImageManipulation(device=gpu)
+        sp = hq.ScielabProcessor(dpi, vd, hq.Whitepoint.D65, None, m)
+        m.setImage(rgba.reshape(-1), None, w, sp.illuminant)  # device LabRef
+        lab_dev = m.getLabRef().reshape(-1, 4)
+        lab = c_oracle.srgb_to_scielab(R, G, B, f, w, nthreads=nt)
+        np.testing.assert_allclose(lab_dev, lab, atol=2e-4)
+        pals = np.stack([o.synthetic_palette(64, 500 + p) for p in range(4)])
+        costs, used = m.computeQuantizationErrorPopulation(pals.reshape(4, -1), 2.0, return_used=True)
+        for p in range(4):
+            ref, parts = c_oracle.eval_palette(rgba, lab_dev, pals[p], f, w, nthreads=nt,
+                                               return_parts=True)
+            assert abs(costs[p] - ref) <= 1e-5 * abs(ref), (w, p, costs[p], ref)
+            np.testing.assert_array_equal(used[p], parts["used"])
+            np.testing.assert_array_equal(m.getIndices(p), parts["idx"].astype(np.uint8))
+        out = {}
+        for variant, trim in ((1, 1), (0, 0), (0, 1)):
+            m.setOption("cost_variant", variant)
+            m.setOption("trim", trim)
+            out[(variant, trim)] = m.computeQuantizationErrorPopulation(pals.reshape(4, -1), 2.0)
+        np.testing.assert_array_equal(out[(0, 1)], costs)
+        np.testing.assert_allclose(out[(0, 0)], out[(1, 1)], rtol=1e-6)
+        np.testing.assert_allclose(out[(0, 1)], out[(1, 1)], rtol=1e-6)
+        m.close()
+
+
+# ---------------------------------------------------------------------------
 # argmin edge cases (CL:179-193), bit-exact
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("grid", [64, 32, 16, 0])
@@ -216,10 +260,13 @@ def test_assign_signed_zero_and_mass_duplicates(ip, grid):
         np.testing.assert_array_equal(ip.getIndices(0), ref_idx.astype(np.uint8))
 
 
-@pytest.mark.parametrize("P", [1, 2, 3, 5, 8])
-def test_assign_group_sizes(ip, P):
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("P", [1, 2, 3, 5, 6, 8])
+def test_assign_group_sizes(ip, P, variant):
     """Groups of 1-4 palettes per pixel pass (P = 5: a full group and a group of
-    one).  P = 1, 2, 3 run assign_pipe_kernel<NG = P>, P >= 4 its NG = 4 instance."""
+    one).  P = 1, 2, 3 run assign_pipe_kernel<NG = P>; P >= 4 its NG = 4 instance
+    (variant 0) or assign_quad_kernel (variant 1: lanes = (pixel, palette))."""
+    ip.setOption("assign_variant", variant)
     rng = np.random.default_rng(P)
     w, h, K = 75, 41, 96
     px = np.zeros((w * h, 4), np.float32)
@@ -233,8 +280,9 @@ def test_assign_group_sizes(ip, P):
         np.testing.assert_array_equal(used[p], ref_used)
 
 
+@pytest.mark.parametrize("variant", [0, 1])
 @pytest.mark.parametrize("grid", [64, 32, 16])
-def test_grid_margin_adversarial(ip, grid):
+def test_grid_margin_adversarial(ip, grid, variant):
     """build_grid's fp32 box bounds and its 1e-5 candidate margin (hq_search.hip)
     on the inputs that sit exactly on the decision boundaries: pixels on cell
     faces i/G2 (and on 0.0 / 1.0) and one ulp either side, palette colours on
@@ -276,6 +324,7 @@ def test_grid_margin_adversarial(ip, grid):
     pals[3, :, :3] = (rng.integers(0, 256, (K, 3)) / 255.0).astype(np.float32)
     pals[3, ::7, 0] = rng.choice(faces, len(pals[3, ::7]))
     pals[3, 200:210] = pals[3, 3]
+    ip.setOption("assign_variant", variant)
     ip.setImage(px.reshape(-1), np.zeros_like(px).reshape(-1), w, ip.illum)
     refs = [c_oracle.assign(px, pals[p]) for p in range(4)]
     for g in (grid, 0):
@@ -305,6 +354,59 @@ def test_out_of_range_palette_takes_generic_path(ip, filt):
         ref, parts = c_oracle.eval_palette(rgba, g["lab"], pals[p], filt, w, return_parts=True)
         assert np.isfinite(costs[p]) and abs(costs[p] - ref) <= 1e-6 * abs(ref), (p, costs[p], ref)
         np.testing.assert_array_equal(ip.getIndices(p), parts["idx"].astype(np.uint8))
+
+
+@pytest.mark.parametrize("K", [257, 1024, 4096])
+def test_wide_palette_vs_oracle(gpu, filt, K):
+    """K > 256 (the plugin allows up to 2^24, HybridQuantization.java:192):
+    32-bit indices from the exhaustive argmin (hq_wide.hip) and the generic
+    stencil path.  Indices and used flags bit-exact against the oracle's
+    argmin (CL:172-193), costs within 1e-5 relative (the bar is 1e-4), on a
+    256 x 256 image with duplicate colours, colours one ulp apart and colours
+    equal to pixels (exact ties)."""
+    w = h = 256
+    R, G, B = o.synthetic_image(w, h, seed=K)
+    rgba = o.inline_rgba(R, G, B)
+    m = hq.ImageManipulation(device=gpu)
+    hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
+    m.setImage(rgba.reshape(-1), None, w, filt.illum)
+    lab = m.getLabRef().reshape(-1, 4)
+    pals = np.stack([o.synthetic_palette(K, 900 + p) for p in range(2)])
+    pals[0, K // 2, :3] = np.nextafter(pals[0, 3, :3], np.float32(1))
+    pals[0, K - 1] = pals[0, 7]
+    pals[1, 100:110, :3] = rgba[1000:1010, :3]
+    pals[1, K - 5:, :3] = rgba[1000:1005, :3]  # same colours again at higher indices
+    costs, used = m.computeQuantizationErrorPopulation(pals.reshape(2, -1), 2.0, return_used=True)
+    nt = _threads()
+    for p in range(2):
+        ref, parts = c_oracle.eval_palette(rgba, lab, pals[p], filt, w, nthreads=nt, return_parts=True)
+        assert abs(costs[p] - ref) <= 1e-5 * abs(ref), (p, costs[p], ref)
+        np.testing.assert_array_equal(used[p], parts["used"])
+        np.testing.assert_array_equal(m.getIndices32(p), parts["idx"].astype(np.uint32))
+    with pytest.raises(hq.HQError):
+        m.getIndices(0)  # u8 indices only exist for K <= 256
+    m.close()
+
+
+def test_wide_palette_search_runs_host_driven(ip, filt):
+    """A SWASA search with K > 256 runs the host-driven loop (the device-resident
+    step keeps palettes in LDS, K <= 256) on the wide evaluation path and follows
+    the same native driver fed with oracle costs."""
+    w, h, K = 40, 32, 300
+    R, G, B = o.synthetic_image(w, h, seed=21)
+    rgba = o.inline_rgba(R, G, B)
+    lab = c_oracle.srgb_to_scielab(R, G, B, filt, w)
+    ip.setImage(rgba.reshape(-1), lab.reshape(-1), w, filt.illum)
+    sw = hq.SWASA(population=2, imax=6, seed=31, t0=0.5)
+    best = ip.findBestQuantization(rgba.reshape(-1), lab.reshape(-1), w, K, sw, None, None, filt.illum)
+    gpu_err = ip.bestError
+
+    def ev(ps):
+        return [c_oracle.eval_palette(rgba, lab, p, filt, w) for p in ps]
+
+    hbest, herr, _ = hq.SWASA(population=2, imax=6, seed=31, t0=0.5).search_host(K, ev)
+    assert abs(gpu_err - herr) <= 1e-5 * abs(herr)
+    np.testing.assert_array_equal(best, hbest)
 
 
 def test_nonfinite_palette_falls_back_exactly(ip):
@@ -499,8 +601,9 @@ def test_device_search_with_single_rank_comm(gpu, filt):
 # Full-size properties (4096^2, K = 256): determinism, grid == exhaustive,
 # fast == generic, shards == full.
 # ---------------------------------------------------------------------------
+@pytest.mark.parametrize("variant", [0, 1])
 @pytest.mark.parametrize("w,h,P", [(1003, 517, 4), (1003, 517, 3), (37, 29, 5)])
-def test_assign_workgroup_count_invariance(gpu, filt, w, h, P):
+def test_assign_workgroup_count_invariance(gpu, filt, w, h, P, variant):
     """The assign grid (option assign_blocks_per_cu: 1 workgroup per CU up to 64,
     default 16) only changes which workgroup takes which pixel chunk: indices,
     used flags and costs are bitwise the same for every count, also when an
@@ -508,6 +611,7 @@ def test_assign_workgroup_count_invariance(gpu, filt, w, h, P):
     K = 256
     R, G, B = o.synthetic_image(w, h, seed=11)
     m = _planar_ctx(gpu, R, G, B, w, h, filt.illum)
+    m.setOption("assign_variant", variant)
     pals = np.stack([o.synthetic_palette(K, 40 + p) for p in range(P)]).reshape(P, -1)
     ref_c, ref_used = m.computeQuantizationErrorPopulation(pals, 2.0, return_used=True)
     ref_idx = [m.getIndices(p) for p in range(P)]
