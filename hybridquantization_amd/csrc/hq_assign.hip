@@ -213,131 +213,18 @@ __global__ __launch_bounds__(256) void assign_pipe_kernel(AssignArgs a, int P) {
         step(i + 1, 1);
     }
     __syncthreads();
-    if (tid < 8 * ng)
-        a.used_mask[((int64_t)(p0 + (tid >> 3)) * a.nblocks + blk) * 8 + (tid & 7)] =
-            s_used[tid >> 3][tid & 7];
-}
-
-// ----------------------------------------------------------------------------
-// assign_quad: grid (nblocks * ceil(P/4)), block 256, XCD-relabelled; P >= 4.
-// ----------------------------------------------------------------------------
-// Lanes are (pixel, palette) pairs: lane 4i + pp serves palette p0 + pp of the
-// group for pixels 4i .. 4i+3 of the wave's 64-pixel run, one pixel per slot
-// (slot s: pixel 4i + s).  The four lanes of a pixel read the four 16-B
-// entries of its 64-B level-2 line with one dwordx4 load between them -- a
-// wave load touches 16 lines instead of 64, and a pixel costs one line lookup
-// instead of four (assign_pipe issues one dwordx4 per palette, each touching
-// 64 lines) -- and each lane resolves its own (pixel, palette) pair, so nothing
-// is redistributed.  After a run's four slots a lane holds the indices of 4
-// consecutive pixels: one dword store, so each store instruction writes 64
-// contiguous bytes into each of the group's 4 index images.  Chunks and the
-// three-stage pipeline are assign_pipe's: 256 * kAssignPPT pixels per chunk.
-__global__ __launch_bounds__(256) void assign_quad_kernel(AssignArgs a, int P) {
-    constexpr int RUNS = kAssignPPT;  // 64-pixel runs per wave per chunk
-    __shared__ __attribute__((aligned(16))) float4 s_pal[4 * kMaxK];
-    __shared__ uint32_t s_used[4][8];
-    const int ngroups = (P + 3) / 4;
-    const int w = xcd_remap(blockIdx.x, a.nblocks * ngroups);
-    const int grp = w % ngroups, blk = w / ngroups, tid = threadIdx.x;
-    const int p0 = 4 * grp, ng = min(4, P - p0);
-    const int lane = tid & 63, pp = lane & 3;
-    // lanes past the group's last palette repeat it (results discarded): the
-    // level-2 entries of palettes that do not exist were never written
-    const int pc = min(pp, ng - 1);
-    const bool act = pp < ng;
-    const uint8_t* lines = a.lvl2 + (int64_t)grp * a.lvl2_gstride;
-    const int G2 = a.G2 > 0 ? a.G2 : 4;
-    const uint32_t chunk = 256 * kAssignPPT, cstride = (uint32_t)a.nblocks * chunk;
-    const uint32_t wbase = (uint32_t)blk * chunk + (uint32_t)(tid >> 6) * (64u * RUNS);
-    auto run_base = [&](int i) { return wbase + (uint32_t)(i / (4 * RUNS)) * cstride + 64u * (uint32_t)((i >> 2) % RUNS); };
-    const uint32_t lq = 4u * (uint32_t)(lane >> 2);
-    auto qpos = [&](int i) { return run_base(i) + lq + (uint32_t)(i & 3); };
-    const uint32_t n_ext = (uint32_t)a.n_ext, qlast = n_ext - 1;
-    auto at = [](const float* base, uint32_t q) {
-        return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + (q << 2));
-    };
-    auto load_rgb = [&](uint32_t q, float& r, float& g, float& b) {
-        const uint32_t qc = min(q, qlast);
-        r = at(a.R, qc);
-        g = at(a.G, qc);
-        b = at(a.B, qc);
-    };
-    const uint32_t eoff = 16u * (uint32_t)pc;  // this lane's entry in a 64-B line
-    // lanes past the image end (the last run) take a one-candidate list: no
-    // exhaustive loop for pixels that are not stored
-    auto lookup = [&](uint32_t q, float r, float g, float b, bool& inside, uint4& e) {
-        const bool dead = q >= n_ext;
-        inside = r >= 0.f && r <= 1.f && g >= 0.f && g <= 1.f && b >= 0.f && b <= 1.f;
-        e = *reinterpret_cast<const uint4*>(
-            lines + ((inside && !dead ? (uint32_t)quad_cell(r, g, b, G2) : 0u) * 64u + eoff));
-        if (dead) { e = make_uint4(1u, 0u, 0u, 0u); inside = true; }
-    };
-    float rb[2], gb[2], bb[2];
-    float xr[2], xg[2], xb[2];
-    uint4 E[2];
-    bool in_[2];
-    uint32_t qq[2];
-    load_rgb(qpos(0), xr[0], xg[0], xb[0]);
-    qq[0] = qpos(0);
-    lookup(qq[0], xr[0], xg[0], xb[0], in_[0], E[0]);
-    load_rgb(qpos(1), rb[1], gb[1], bb[1]);
-    load_rgb(qpos(2), rb[0], gb[0], bb[0]);
-    static_assert(kMaxK == 256, "one table entry per thread and palette");
-    for (int q = 0; q < ng; ++q)
-        if (tid < a.K) s_pal[q * kMaxK + tid] = a.pal[(int64_t)(p0 + q) * kMaxK + tid];
-    if (tid < 32) s_used[tid >> 3][tid & 7] = 0;
-    __syncthreads();
-    // 32-bit offsets from the group's first index image: the host keeps
-    // idx_pitch < 2^30 + 512, so 3 pitches + a position stay below 2^32
-    uint8_t* const idx_grp = a.idx + (int64_t)p0 * a.idx_pitch;
-    const uint32_t idx_off = (uint32_t)pc * (uint32_t)a.idx_pitch;
-    const bool exh = a.pflags[p0 + pc] != 0 || a.G2 == 0;
-    const float4* pal_l = s_pal + pc * kMaxK;
-    const uint8_t* lvl1_l = a.lvl1 + (int64_t)(p0 + pc) * a.lvl1_pitch;
-    uint32_t* used_l = s_used[pc];
-    uint32_t packed = 0;  // this run's 4 indices, byte s = slot s
-    auto resolve = [&](int h, int slot) {
-        const uint32_t q = qq[h];
-        const int k = argmin_from_entry(xr[h], xg[h], xb[h], E[h], in_[h] && !exh, pal_l, lvl1_l, G2, a.K);
-        packed |= (uint32_t)k << (8 * slot);
-        if (act && q < n_ext) {
-            const uint32_t bit = 1u << (k & 31);
-            if (!(used_l[k >> 5] & bit)) atomicOr(&used_l[k >> 5], bit);
-        }
-    };
-    auto step = [&](int i, int h, int slot) {
-        const int n = h ^ 1;
-        qq[n] = qpos(i + 1);
-        xr[n] = rb[n]; xg[n] = gb[n]; xb[n] = bb[n];
-        lookup(qq[n], xr[n], xg[n], xb[n], in_[n], E[n]);
-        load_rgb(qpos(i + 3), rb[n], gb[n], bb[n]);
-        resolve(h, slot);
-    };
-    auto flush = [&](int i) {  // after slot i + 3: pixels qpos(i) .. qpos(i) + 3
-        const uint32_t q = qpos(i);
-        if (act) {
-            if (q + 3 < n_ext) {
-                __builtin_nontemporal_store(packed, reinterpret_cast<uint32_t*>(idx_grp + (idx_off + q)));
-            } else {
-                for (int s = 0; s < 4; ++s)
-                    if (q + s < n_ext) idx_grp[idx_off + q + s] = (uint8_t)(packed >> (8 * s));
-            }
-        }
-        packed = 0;
-    };
-    // a wave's run is 64 pixels; the run loop runs while any of them exists
-    // (wave-uniform trip count)
-    for (int i = 0;; i += 4) {
-        if (run_base(i) >= n_ext) break;
-        step(i, 0, 0);
-        step(i + 1, 1, 1);
-        step(i + 2, 0, 2);
-        step(i + 3, 1, 3);
-        flush(i);
+    // the workgroup's used bits into the palette's 8 words (OR is order-free:
+    // the result does not depend on which workgroup gets there first).  A
+    // device-scope load first, so only bits nobody has set yet cost an atomic:
+    // after the first workgroups every colour of a 256-colour palette is
+    // usually in, and 2,000-4,000 workgroups' atomics on the same 32 words
+    // serialised at the end of a short (row-block shard) launch.
+    if (tid < 8 * ng) {
+        const uint32_t m = s_used[tid >> 3][tid & 7];
+        uint32_t* gw = &a.used_glob[(p0 + (tid >> 3)) * 8 + (tid & 7)];
+        const uint32_t seen = __hip_atomic_load(gw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (m & ~seen) atomicOr(gw, m);
     }
-    __syncthreads();
-    if (tid < 8 * ng)
-        a.used_mask[((int64_t)(p0 + (tid >> 3)) * a.nblocks + blk) * 8 + (tid & 7)] = s_used[tid >> 3][tid & 7];
 }
 
 // ----------------------------------------------------------------------------
@@ -345,10 +232,6 @@ __global__ __launch_bounds__(256) void assign_quad_kernel(AssignArgs a, int P) {
 // ----------------------------------------------------------------------------
 hipError_t launch_assign(const AssignArgs& a, int P, hipStream_t s) {
     const unsigned grid = (unsigned)(a.nblocks * ((P + 3) / 4));
-    if (a.variant == 1 && P >= 4) {
-        HQ_LAUNCH(assign_quad_kernel, dim3(grid), dim3(256), 0, s, a, P);
-        return hipGetLastError();
-    }
     switch (P) {
     case 1: HQ_LAUNCH(assign_pipe_kernel<1>, dim3(grid), dim3(256), 0, s, a, P); break;
     case 2: HQ_LAUNCH(assign_pipe_kernel<2>, dim3(grid), dim3(256), 0, s, a, P); break;

@@ -465,7 +465,7 @@ constexpr int kTH16 = 16;
 template <int HB>
 struct Tile16 {
     static constexpr int TH = kTH16, TW = 128, HR = 4;
-    static constexpr int RWL = TW + 2 * HB;            // region columns read
+    static constexpr int RWL = (TW + 2 * HB + 3) / 4 * 4;  // region columns read (whole dwords)
     static constexpr int RW = (RWL + 31) / 32 * 32;    // LDS pitch: whole 32-column ranges
     static constexpr int RH = TH + 2 * HB;             // region rows
     static constexpr int NBLK = RW / 16;               // vertical-pass column blocks
@@ -485,8 +485,8 @@ struct Tile16 {
 // distance settings were swept with the oracle's filter design, SP:66-254).
 __host__ __device__ constexpr int trim_w(int HB, int ch) {
     return HB == 10 ? (ch == 0 ? 3 : ch == 1 ? 4 : 5)
-         : HB == 16 ? (ch == 0 ? 4 : ch == 1 ? 6 : 8)
-         : HB == 20 ? (ch == 0 ? 5 : ch == 1 ? 7 : 10)
+         : HB == 15 ? (ch == 0 ? 4 : ch == 1 ? 5 : 7)
+         : HB == 19 ? (ch == 0 ? 5 : ch == 1 ? 7 : 9)
                     : (ch == 0 ? 6 : ch == 1 ? 9 : 12);
 }
 
@@ -511,7 +511,7 @@ template <int HB, int TLO = 0, int THI = 2 * HB, int WH = 80>
 __device__ __forceinline__ void hpass_wide(const f32x4* src, int j, TapsPtr<HB> taps, int f,
                                            int plane, int pstride, f32x2 (&acc)[4]) {
     constexpr int HR = 4;
-    constexpr int CH = HB <= 10 ? 2 * HB + 1 : 12;  // taps per chunk
+    constexpr int CH = HB <= 10 ? 2 * HB + 1 : 8;  // taps per chunk
     const f32x4* row = src + plane * pstride + j;
 #pragma unroll
     for (int t0 = TLO; t0 <= THI; t0 += CH) {
@@ -593,8 +593,15 @@ __device__ __forceinline__ void vblock(const uint32_t (&w)[8 * S + 2], const uin
     }
 }
 
+#ifndef HQ_LB19
+#define HQ_LB19 3  // waves per SIMD of the 19-tap bucket
+#endif
+// occupancy per bucket: LDS allows 4 workgroups per CU at HB = 10, 3 above
+template <int HB>
+constexpr int cost16w_waves() { return HB == 10 ? 4 : HB == 15 ? 3 : HB == 19 ? HQ_LB19 : 2; }
+
 template <int HB, int DE, bool TRIM>
-__global__ __launch_bounds__(256, HB == 10 ? 4 : (HB == 16 ? 3 : 2)) void cost16w_kernel(CostArgs a, int P_) {
+__global__ __launch_bounds__(256, cost16w_waves<HB>()) void cost16w_kernel(CostArgs a, int P_) {
     using Gm = Tile16<HB>;
     constexpr int TH = kTH16, HR = 4, T2 = 2 * HB, TW = Gm::TW, RWL = Gm::RWL, RW = Gm::RW;
     constexpr int RH = Gm::RH, WH = Gm::WH, NBLK = Gm::NBLK, NSET = Gm::NSET, S = Gm::S, NJ = Gm::NJ;
@@ -863,9 +870,11 @@ void opp2xyz_over_illum(const float inv_illum[3], float m[9]) {
 }
 
 // The fast path's tap bucket for a filter half-width H (halfSize, IM:408): the
-// smallest of 10, 16, 20, 24 that holds it; 0 = none (H > 24: the generic path).
+// smallest of 10, 15, 19, 24 that holds it; 0 = none (H > 24: the generic path).
+// 72 dpi / 45 cm (the default) is H = 10, 150 dpi / 30 cm H = 15, 96 dpi /
+// 60 cm H = 19: those run without zero taps.
 int fast_bucket(int half) {
-    return half <= 10 ? 10 : half <= 16 ? 16 : half <= 20 ? 20 : half <= 24 ? 24 : 0;
+    return half <= 10 ? 10 : half <= 15 ? 15 : half <= 19 ? 19 : half <= 24 ? 24 : 0;
 }
 
 static int bucket_steps(int HB) { return (8 + 2 * HB + 31) / 32; }
@@ -978,8 +987,8 @@ static size_t taps_bytes() { return 2 * sizeof(CostTaps<HB>); }
 size_t fast_taps_bytes(int HB) {
     switch (HB) {
     case 10: return taps_bytes<10>();
-    case 16: return taps_bytes<16>();
-    case 20: return taps_bytes<20>();
+    case 15: return taps_bytes<15>();
+    case 19: return taps_bytes<19>();
     default: return taps_bytes<24>();
     }
 }
@@ -1027,8 +1036,8 @@ hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, bool trim, int ti
     if (tile_rows == kTH16) {
         switch (HB) {
         case 10: launch_cost16w<10>(a0, P, de, trim, s); break;
-        case 16: launch_cost16w<16>(a0, P, de, trim, s); break;
-        case 20: launch_cost16w<20>(a0, P, de, trim, s); break;
+        case 15: launch_cost16w<15>(a0, P, de, trim, s); break;
+        case 19: launch_cost16w<19>(a0, P, de, trim, s); break;
         case 24: launch_cost16w<24>(a0, P, de, trim, s); break;
         default: return hipErrorInvalidValue;
         }

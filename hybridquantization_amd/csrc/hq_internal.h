@@ -53,6 +53,7 @@ struct PaletteArgs {
 constexpr int kAssignPPT = HQ_ASSIGN_PPT;  // assign: pixels per thread per 256-thread chunk
                                            // (4: as fast as 8 or 16 at 4096^2, 6% faster on a 512-row shard)
 constexpr int kSaMaxP = 64;       // device-resident SWASA: largest population
+constexpr int kFoldMaxP = 8;      // largest population whose accept step folds the finalize
 
 // sa_step_kernel: one accept + generate step of the device-resident SWASA search.
 struct SaArgs {
@@ -70,6 +71,13 @@ struct SaArgs {
     const uint64_t* jump_A; // LCG jumps: n steps = A_n s + C_n mod 2^48, n = 0 .. 3K*P
     const uint64_t* jump_C;
     PaletteArgs prep;       // outputs of the palette prep of the next candidates
+    // fold (no communicator, P <= kFoldMaxP): the accept step reduces the cost
+    // kernel's partials and the used bits itself (finalize's order), so no
+    // finalize launch sits between the cost kernel and this step
+    const double* partial;  // [P][ntiles]
+    const uint32_t* used_glob;  // [P][8]
+    int ntiles;
+    int fold;
     double n_total;         // pixels of the whole image
     double keep_threshold;  // SW:59-62 -(tanh(num/den))/2 + 0.5 at the accepted iteration
     float temperature;      // SW:54-57 temperature at the accepted iteration
@@ -89,6 +97,7 @@ struct GridArgs {
     const int* pflags;
     uint8_t* lvl1;          // [P][G1^3][32]
     uint8_t* lvl2;          // [ceil(P/4)][G2^3][4][16]: 4 palettes' entries per 64-B line
+    uint32_t* used_glob;    // [P][8] used-colour bits, zeroed here for the assign that follows
     int K;
     int G1;                 // level-1 resolution (G2 / 4)
     int64_t lvl1_pitch;     // bytes per palette
@@ -104,15 +113,14 @@ struct AssignArgs {
     const uint8_t* lvl1;
     const uint8_t* lvl2;
     uint8_t* idx;           // [P][idx_pitch]
-    uint32_t* used_mask;    // [P][nblocks][8]
+    uint32_t* used_glob;    // [P][8] used-colour bits: every workgroup ORs its own in (atomics)
     int64_t n_ext;
     int64_t idx_pitch;
     int64_t lvl1_pitch;     // bytes per palette
     int64_t lvl2_gstride;   // bytes per group of 4 palettes (G2^3 * 64)
     int K;
     int G2;                 // 0 = exhaustive
-    int nblocks;            // blocks per palette (= used_mask blocks per palette)
-    int variant;            // 0 assign_pipe_kernel, 1 assign_quad_kernel (P >= 4)
+    int nblocks;            // workgroups per palette group
 };
 
 struct CostArgs {
@@ -134,10 +142,9 @@ struct CostArgs {
 
 struct FinalizeArgs {
     const double* partial;  // [P][ntiles]
-    const uint32_t* used_mask;  // [P][nblocks][8]
+    const uint32_t* used_glob;  // [P][8] used-colour bits (assign)
     double* out;            // [P][1+K]
     int ntiles;
-    int nblocks;
     int K;
     const uint32_t* used32; // K > 256: [P][K] used flags (assign_wide), replaces used_mask
 };

@@ -114,12 +114,12 @@ struct hq_ctx {
     double* h_out = nullptr;  // pinned [P][1+K]
     size_t h_pal_bytes = 0, h_out_bytes = 0;
     int last_P = 0;
+    int last_nparts = 0;  // cost partials per palette of the last evaluation
 
     // options
     int G2 = 32;           // argmin grid resolution (0 = exhaustive)
     int cost_variant = 0;  // 0 tiled (default), 1 generic two-pass
     int cost_rows = 16;    // fast path tiles: 16 x 128 (cost16w_kernel) or 8 x 108 (cost_mfma_kernel)
-    int assign_variant = 0;  // 0 assign_pipe_kernel, 1 assign_quad_kernel (P >= 4)
     int assign_blocks_per_cu = 16;  // 4096^2: 4 chunks per workgroup; 0.632 -> 0.605 ms per step vs 8
     int shard_solo = 0;    // experiment: a sharded search without a communicator (per-rank timing)
     int sa_device = 1;     // hq_search_*: 1 = SWASA iterations resident on the device (no host
@@ -150,6 +150,7 @@ struct hq_search {
     Swasa* pol = nullptr;
     hq_swasa_params prm{};
     int P = 0, ite = 0, st = 0, cd = 0;  // state and candidate buffer parities
+    bool fold = false;                   // accept steps reduce the partials (no finalize launch)
     float t_acc = 0.f;                   // temperature / threshold of the iteration
     double keep_acc = 0.0;               // whose population awaits acceptance
     DevBuf colors[2], cand[2], err[2], seed[2], best_err, best_colors, jA, jC;
@@ -340,7 +341,6 @@ int ensure_population(hq_ctx* c, int P, int K) {
     const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
     const int64_t gen_blocks = (n_own + 255) / 256;
     const int64_t nparts = std::max<int64_t>(ntiles, gen_blocks);
-    const int nblocks = assign_blocks(c);
     HIP_TRY(c, c->d_pal_in.ensure(sizeof(float4) * (size_t)P * K));
     HIP_TRY(c, c->d_pal.ensure(sizeof(float4) * (size_t)P * std::max(K, kMaxK)));
     HIP_TRY(c, c->d_opp.ensure(sizeof(float4) * (size_t)P * std::max(K, kMaxK)));
@@ -357,7 +357,7 @@ int ensure_population(hq_ctx* c, int P, int K) {
     // bytes past a region's last column (past the buffer on the last palette's
     // last row when idx_pitch has no padding)
     HIP_TRY(c, c->d_idx.ensure((size_t)P * g.idx_pitch + 256));
-    HIP_TRY(c, c->d_used_mask.ensure(sizeof(uint32_t) * 8 * (size_t)P * nblocks));
+    HIP_TRY(c, c->d_used_mask.ensure(sizeof(uint32_t) * 8 * (size_t)P));
     HIP_TRY(c, c->d_partial.ensure(sizeof(double) * (size_t)P * nparts));
     HIP_TRY(c, c->d_out.ensure(sizeof(double) * (size_t)P * (1 + K)));
     return ensure_pinned(c, sizeof(float) * 4 * (size_t)P * K, sizeof(double) * (size_t)P * (1 + K));
@@ -385,7 +385,7 @@ GridArgs grid_args(hq_ctx* c, int K) {
     const int G2 = c->G2 > 0 ? c->G2 : 4;
     const int G1 = G2 / 4;
     return GridArgs{c->d_pal.as<float4>(), c->d_dup.as<uint8_t>(), c->d_pflags.as<int>(),
-                    c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(), K, G1,
+                    c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(), c->d_used_mask.as<uint32_t>(), K, G1,
                     round_up((int64_t)G1 * G1 * G1 * 32, 256), round_up((int64_t)G2 * G2 * G2 * 64, 256)};
 }
 
@@ -444,7 +444,7 @@ int enqueue_wide(hq_ctx* c, int P, int K, const hipEvent_t* ev) {
     int nparts = 0;
     int rc = enqueue_generic_cost(c, P, c->d_idx32.p, true, K, ev, &nparts);
     if (rc) return rc;
-    FinalizeArgs fa{c->d_partial.as<double>(), nullptr, c->d_out.as<double>(), nparts, 0, K,
+    FinalizeArgs fa{c->d_partial.as<double>(), nullptr, c->d_out.as<double>(), nparts, K,
                     c->d_used32.as<uint32_t>()};
     if (ev) set_launch_events(ev[6], ev[7]);
     const hipError_t ef = launch_finalize(fa, P, s);
@@ -457,7 +457,7 @@ int enqueue_wide(hq_ctx* c, int P, int K, const hipEvent_t* ev) {
     return HQ_OK;
 }
 
-int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev) {
+int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = false) {
     const Geom& g = c->g;
     hipStream_t s = c->stream;
     const GridArgs ga = grid_args(c, K);
@@ -465,17 +465,19 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev) {
         if (ev) set_launch_events(ev[2 * slot], ev[2 * slot + 1]);
     };
     auto untimed = [&]() { set_launch_events(nullptr, nullptr); };
-    if (c->G2 > 0) {
+    if (c->G2 > 0) {  // (build_grid also zeroes the used bits)
         timed(0);
         const hipError_t e = launch_build_grid(ga, P, s);
         untimed();
         HIP_TRY(c, e);
+    } else {
+        HIP_TRY(c, hipMemsetAsync(c->d_used_mask.p, 0, sizeof(uint32_t) * 8 * (size_t)P, s));
     }
     const int nblocks = assign_blocks(c);
     const AssignArgs aa{c->d_R.as<float>(), c->d_G.as<float>(), c->d_B.as<float>(), c->d_pal.as<float4>(),
                         c->d_pflags.as<int>(), c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(),
                         c->d_idx.as<uint8_t>(), c->d_used_mask.as<uint32_t>(), g.n_ext, g.idx_pitch,
-                        ga.lvl1_pitch, ga.lvl2_gstride, K, c->G2, nblocks, c->assign_variant};
+                        ga.lvl1_pitch, ga.lvl2_gstride, K, c->G2, nblocks};
     timed(1);
     hipError_t e = launch_assign(aa, P, s);
     untimed();
@@ -507,12 +509,15 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev) {
         int rc = enqueue_generic_cost(c, P, c->d_idx.p, false, kMaxK, ev, &nparts);
         if (rc) return rc;
     }
-    FinalizeArgs fa{c->d_partial.as<double>(), c->d_used_mask.as<uint32_t>(), c->d_out.as<double>(),
-                    nparts, nblocks, K, nullptr};
-    timed(3);
-    const hipError_t ef = launch_finalize(fa, P, s);
-    untimed();
-    HIP_TRY(c, ef);
+    c->last_nparts = nparts;
+    if (!fold) {  // (a folding search's accept step reduces the partials itself)
+        FinalizeArgs fa{c->d_partial.as<double>(), c->d_used_mask.as<uint32_t>(), c->d_out.as<double>(),
+                        nparts, K, nullptr};
+        timed(3);
+        const hipError_t ef = launch_finalize(fa, P, s);
+        untimed();
+        HIP_TRY(c, ef);
+    }
     if (c->comm) {  // also with one rank (a no-op copy), so that path is exercised on one GPU
         NCCL_TRY(c, ncclAllReduce(c->d_out.p, c->d_out.p, (size_t)P * (1 + K), ncclFloat64, ncclSum,
                                   c->comm, s));
@@ -523,11 +528,11 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev) {
 }
 
 // Add one evaluation's kernel times (its events have completed).
-void prof_accumulate(hq_ctx* c, const hipEvent_t* ev) {
+void prof_accumulate(hq_ctx* c, const hipEvent_t* ev, bool finalize = true) {
     if (c->G2 > 0) prof_add(c, c->prof_grid, ev[0], ev[1]);
     prof_add(c, c->prof_assign, ev[2], ev[3]);
     prof_add(c, c->prof_cost, ev[4], ev[5]);
-    prof_add(c, c->prof_finalize, ev[6], ev[7]);
+    if (finalize) prof_add(c, c->prof_finalize, ev[6], ev[7]);
 }
 
 // Host-driven evaluation of the P palettes in h_pal: upload, prep, enqueue_core,
@@ -626,6 +631,10 @@ int enqueue_sa_step(hq_search* s, bool accept, bool init, bool generate, bool ra
     a.generate = generate;
     a.random = random;
     a.convergence = s->prm.convergence;
+    a.partial = c->d_partial.as<double>();
+    a.used_glob = c->d_used_mask.as<uint32_t>();
+    a.ntiles = c->last_nparts;
+    a.fold = s->fold;
     HIP_TRY(c, launch_sa_step(a, c->stream));
     s->st = 1 - s->st;
     if (generate) s->cd = 1 - s->cd;
@@ -645,6 +654,9 @@ int device_search_create(hq_ctx* c, const hq_swasa_params* params, int K, uint64
     const int P = params->population;
     s->prm = *params;
     s->P = P;
+    // no communicator: nothing has to see the finalized sums, so the accept
+    // step reduces the partials itself (one launch less per iteration)
+    s->fold = !c->comm && P <= kFoldMaxP;
     s->pol = new Swasa(*params, seed);
     int rc = ensure_population(c, P, K);
     if (rc) return rc;
@@ -677,7 +689,7 @@ int device_search_create(hq_ctx* c, const hq_swasa_params* params, int K, uint64
     s->st = s->cd = 0;
     // IM:385-493: random population (SW:40-52), its evaluation, argmin
     if ((rc = enqueue_sa_step(s, false, false, true, true, 0.f))) return rc;
-    if ((rc = enqueue_core(c, P, K, nullptr))) return rc;
+    if ((rc = enqueue_core(c, P, K, nullptr, s->fold))) return rc;
     if ((rc = enqueue_sa_step(s, true, true, false, false, 0.f))) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     s->ite = 0;
@@ -695,6 +707,8 @@ int device_search_run(hq_search* s, int iterations, int* ran) {
     if (c->de_type == HQ_DE_CIEDE2000)
         return fail(c, HQ_ERR_UNSUPPORTED, "CIEDE2000 is unimplemented in the reference (CL:227-230)");
     if ((rc = ensure_population(c, s->P, s->K))) return rc;
+    if (s->fold && c->comm)
+        return fail(c, HQ_ERR_STATE, "communicator set after hq_search_create: recreate the search");
     const bool prof = c->prof;
     if (prof && (rc = ensure_events(s, (size_t)8 * iterations))) return rc;
     for (; done < iterations && s->ite < s->prm.imax; ++done) {
@@ -704,13 +718,13 @@ int device_search_run(hq_search* s, int iterations, int* ran) {
         const hipEvent_t* ev = prof ? &s->pev[(size_t)8 * done] : nullptr;
         // accept the previous iteration's population (none at the first of a run)
         if ((rc = enqueue_sa_step(s, done > 0, false, true, false, amax))) return rc;
-        if ((rc = enqueue_core(c, s->P, s->K, ev))) return rc;
+        if ((rc = enqueue_core(c, s->P, s->K, ev, s->fold))) return rc;
         s->t_acc = s->pol->temperature();     // SW:54-57 at this iteration
         s->keep_acc = s->pol->keep_threshold(ite);
     }
     if (done > 0 && (rc = enqueue_sa_step(s, true, false, false, false, 0.f))) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    for (int i = 0; prof && i < done; ++i) prof_accumulate(c, &s->pev[(size_t)8 * i]);
+    for (int i = 0; prof && i < done; ++i) prof_accumulate(c, &s->pev[(size_t)8 * i], !s->fold);
     if (ran) *ran = done;
     return HQ_OK;
 }
@@ -1212,9 +1226,6 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
         c->sa_device = value != 0;
     } else if (!std::strcmp(name, "shard_solo")) {
         c->shard_solo = value != 0;
-    } else if (!std::strcmp(name, "assign_variant")) {
-        if (value < 0 || value > 1) return fail(c, HQ_ERR_ARG, "assign_variant must be 0 or 1");
-        c->assign_variant = value;
     } else if (!std::strcmp(name, "assign_blocks_per_cu")) {
         if (value < 1 || value > 64) return fail(c, HQ_ERR_ARG, "assign_blocks_per_cu in [1,64]");
         c->assign_blocks_per_cu = value;

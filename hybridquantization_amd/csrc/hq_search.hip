@@ -118,12 +118,43 @@ __device__ __forceinline__ uint64_t lcg_jump(uint64_t s, uint64_t A, uint64_t C)
     return (A * s + C) & kLcgMask;
 }
 
+// Fixed-order sums of the cost kernel's per-tile partials by a 1024-thread
+// block (IM:736-768's fp64 sum, in an order of our own that never changes):
+// thread t adds partials t, t + 1024, t + 2048, ... of palette p in that order
+// into acc[p]; the caller then folds the lanes with wave_sum_to_lane63 and the
+// 16 wave sums in ascending order.  finalize_kernel and sa_step's fold both
+// use it, so a search that folds the finalize into its accept step gets the
+// host-driven evaluation's sums bit for bit.  NL loads per palette in flight.
+template <int MAXP, int NL>
+__device__ __forceinline__ void thread_partial_sums(const double* part, int ntiles, int P,
+                                                    double (&acc)[MAXP]) {
+    constexpr int NT = 1024;
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int p = 0; p < MAXP; ++p) acc[p] = 0.0;
+    for (int t0 = 0; t0 < ntiles; t0 += NT * NL) {
+        double v[MAXP][NL];
+#pragma unroll
+        for (int p = 0; p < MAXP; ++p)
+#pragma unroll
+            for (int u = 0; u < NL; ++u) {
+                const int t = t0 + u * NT + tid;
+                v[p][u] = p < P && t < ntiles ? part[(int64_t)p * ntiles + t] : 0.0;
+            }
+#pragma unroll
+        for (int p = 0; p < MAXP; ++p)
+#pragma unroll
+            for (int u = 0; u < NL; ++u) acc[p] += v[p][u];
+    }
+}
+
 // Block-shared SA state of one step (thread 0 runs the sequential logic).
 struct SaShared {
     int unused[kSaMaxP];
     int src[kSaMaxP];  // >= 0: member p continues from candidate src; -1: keeps its palette
     double cur[kSaMaxP], err[kSaMaxP], ex[kSaMaxP];  // ex: exp(-(err - cur) / T), lanes in parallel
     double sum[kSaMaxP], err_in[kSaMaxP];  // prefetched inputs of the sequential part
+    double fold_red[kFoldMaxP][16];  // fold: per-wave partial sums of each palette
     uint64_t seed;     // java.util.Random state (prefetched, then after the acceptance draws)
     double best_in;
     int best;          // candidate that set a new best (-1: none)
@@ -140,7 +171,20 @@ __device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared
     constexpr int MAXF = 16;  // used flags per thread held in registers
     const int nf = (P * K + nt - 1) / nt;
     double fv[MAXF];
-    if (a.accept) {
+    double fold_acc[kFoldMaxP];
+    uint32_t fold_word = 0u;
+    if (a.accept && a.fold) {  // the finalize's work, folded (P <= kFoldMaxP)
+        if (tid < P) s.err_in[tid] = a.err_in[tid];
+        if (P <= 4) {
+            double acc4[4];
+            thread_partial_sums<4, 8>(a.partial, a.ntiles, P, acc4);
+#pragma unroll
+            for (int p = 0; p < kFoldMaxP; ++p) fold_acc[p] = p < 4 ? acc4[p] : 0.0;
+        } else {
+            thread_partial_sums<kFoldMaxP, 4>(a.partial, a.ntiles, P, fold_acc);
+        }
+        if (tid < 8 * P) fold_word = a.used_glob[tid];
+    } else if (a.accept) {
         if (tid < P) {
             s.sum[tid] = a.out[(int64_t)tid * (1 + K)];
             s.err_in[tid] = a.err_in[tid];
@@ -165,7 +209,20 @@ __device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared
     }
     if (tid < P) s.unused[tid] = 0;
     __syncthreads();
-    if (a.accept) {
+    if (a.accept && a.fold) {
+#pragma unroll
+        for (int p = 0; p < kFoldMaxP; ++p) {
+            if (p >= P) break;
+            const double w = wave_sum_to_lane63(fold_acc[p]);
+            if ((tid & 63) == 63) s.fold_red[p][tid >> 6] = w;
+        }
+        if (tid < 8 * P) {  // unused colours: clear bits below K
+            const int nbits = min(max(K - 32 * (tid & 7), 0), 32);
+            const uint32_t valid = nbits >= 32 ? ~0u : ((1u << nbits) - 1u);
+            const int clear = nbits - __popc(fold_word & valid);
+            if (clear) atomicAdd(&s.unused[tid >> 3], clear);
+        }
+    } else if (a.accept) {
         if (nf <= MAXF) {
             // a wave's flags are consecutive: one ballot count per palette it spans
             // (one LDS atomic per wave instead of one per unused colour)
@@ -182,8 +239,15 @@ __device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared
             for (int e = tid; e < P * K; e += nt)
                 if (a.out[(int64_t)(e / K) * (1 + K) + 1 + e % K] == 0.0) atomicAdd(&s.unused[e / K], 1);
         }
+    }
+    if (a.accept) {
         __syncthreads();
         if (tid < P) {  // per member, in parallel: error, current, acceptance probability
+            if (a.fold) {  // finalize's order: the 16 wave sums ascending
+                double tot = 0.0;
+                for (int i = 0; i < 16; ++i) tot += s.fold_red[tid][i];
+                s.sum[tid] = tot;
+            }
             const double e = s.sum[tid] / a.n_total + (double)s.unused[tid] * (double)a.delta;
             const double c = a.init ? e : s.err_in[tid];
             s.err[tid] = e;
@@ -477,11 +541,19 @@ __device__ __forceinline__ void grid_cell_body(const GridArgs& a, int p, int cel
     // pass 1: T2 over the whole parent list (which can exceed 31 entries: the
     // level-1 entry then overflows, the children still get lists)
     float t2 = INFINITY;
-    for (int i = q; i < total; i += 4)
-        t2 = fminf(t2, (s_ax[0][a0][i] + s_ax[1][a1][i]) + s_ax[2][a2][i]);
-    t2 = fminf(t2, __shfl_xor(t2, 1, 64));
-    t2 = fminf(t2, __shfl_xor(t2, 2, 64));
+    int t2pos = 0;  // the parent-list position attaining T2 (the child's closest-in-the-worst-case colour)
+    for (int i = q; i < total; i += 4) {
+        const float d = (s_ax[0][a0][i] + s_ax[1][a1][i]) + s_ax[2][a2][i];
+        if (d < t2) { t2 = d; t2pos = i; }
+    }
+#pragma unroll
+    for (int m = 1; m <= 2; m <<= 1) {
+        const float o = __shfl_xor(t2, m, 64);
+        const int op = __shfl_xor(t2pos, m, 64);
+        if (o < t2 || (o == t2 && op < t2pos)) { t2 = o; t2pos = op; }
+    }
     const float thr = t2 * HQ_CAND_MARGIN;
+    const int bstar = total > 0 ? (int)s_list[t2pos] : 0;
     __syncthreads();
     axis_terms<false>(s_ax, s_col, s_list, total, ci, cj, ck, inv2);
     __syncthreads();
@@ -515,6 +587,81 @@ __device__ __forceinline__ void grid_cell_body(const GridArgs& a, int p, int cel
         w[k] |= (uint32_t)__shfl_xor((int)w[k], 1, 64);
         w[k] |= (uint32_t)__shfl_xor((int)w[k], 2, 64);
     }
+    // Dominance pruning (exact).  Candidate a of the child's list is dropped
+    // when b* -- the colour attaining T2, the child's nearest in the worst
+    // case -- is nearer than a to EVERY point of the child box by a margin:
+    // f(p) = |p - a|^2 - |p - b|^2 = c . p + |a|^2 - |b|^2 with c = 2 (b - a) is
+    // linear, so its minimum over the box is at the corner picked axis by axis.
+    // For a pixel p in the box the reference's fp32 d^2 is within ~3e-7
+    // relative of the exact one, and its sqrtf separates two d^2 that differ by
+    // more than 2^-21 relative, so f(p) > 1.1e-6 dmax^2(B, a) makes
+    // sqrtf(d_a) > sqrtf(d_b) strictly: a never wins, not even a tie
+    // (CL:179-192).  The test asks f_min > 1e-5 (dmax^2(B, a) + S), S bounding
+    // the terms of the fp32 evaluation of f_min (its own rounding is < 1e-6 S).
+    // Every reference winner stays listed, so the pruned argmin is unchanged;
+    // the lists shrink (uniform noise, K = 256, G2 = 32: mean 2.7 -> 2.05, the
+    // longest of 64 pixels' lists 7.9 -> 5.9; against every other candidate
+    // instead of b* only: 2.0 / 5.2, at O(n^2) build cost), and with them
+    // assign's candidate loop, which runs each wave's longest list.
+#ifndef HQ_NO_DOMINANCE
+    if (!exh && n >= 2 && n <= kL2Cap) {
+#else
+    if (false) {
+#endif
+        const float blo[3] = {(float)(4 * ci + a0) * inv2, (float)(4 * cj + a1) * inv2,
+                              (float)(4 * ck + a2) * inv2};
+        const float bhi[3] = {blo[0] + inv2, blo[1] + inv2, blo[2] + inv2};
+        const float4 cb = s_col[bstar];
+        const float vb[3] = {cb.x, cb.y, cb.z};
+        const float nb = (vb[0] * vb[0] + vb[1] * vb[1]) + vb[2] * vb[2];
+        uint32_t drop = 0u;
+        // list position i = q + 4t sits in byte (i + 1) & 3 of word (i + 1) >> 2
+        const int sh = 8 * ((q + 1) & 3), wo = (q + 1) >> 2;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int i = q + 4 * t;
+            if (i >= n) break;
+            const uint32_t word = wo ? w[t < 3 ? t + 1 : 3] : w[t];
+            const int ka = (int)((word >> sh) & 0xffu);
+            if (ka == bstar) continue;
+            const float4 ca = s_col[ka];
+            const float va[3] = {ca.x, ca.y, ca.z};
+            const float dmax2a = (ax_max2(va[0], blo[0], bhi[0]) + ax_max2(va[1], blo[1], bhi[1])) +
+                                 ax_max2(va[2], blo[2], bhi[2]);
+            const float na = (va[0] * va[0] + va[1] * va[1]) + va[2] * va[2];
+            float fmin = na - nb, S = na + nb + dmax2a;
+#pragma unroll
+            for (int ax = 0; ax < 3; ++ax) {
+                const float cc = 2.0f * (vb[ax] - va[ax]);
+                const float tl = cc * blo[ax], th = cc * bhi[ax];
+                fmin += fminf(tl, th);
+                S += fmaxf(fabsf(tl), fabsf(th));
+            }
+            if (fmin > 1e-5f * S) drop |= 1u << i;
+        }
+        drop |= (uint32_t)__shfl_xor((int)drop, 1, 64);
+        drop |= (uint32_t)__shfl_xor((int)drop, 2, 64);
+        if (drop) {  // rebuild the entry from the kept positions, ascending
+            uint32_t x0 = 0u, x1 = 0u, x2 = 0u, x3 = 0u;
+            int kept = 0;
+#pragma unroll
+            for (int i = kL2Cap - 1; i >= 0; --i) {
+                if (i < n && !((drop >> i) & 1u)) {
+                    x3 = (x3 << 8) | (x2 >> 24);
+                    x2 = (x2 << 8) | (x1 >> 24);
+                    x1 = (x1 << 8) | (x0 >> 24);
+                    x0 = (x0 << 8) | ((w[(i + 1) >> 2] >> (8 * ((i + 1) & 3))) & 0xffu);
+                    ++kept;
+                }
+            }
+            // the count's byte goes in below the first kept candidate
+            w[3] = (x3 << 8) | (x2 >> 24);
+            w[2] = (x2 << 8) | (x1 >> 24);
+            w[1] = (x1 << 8) | (x0 >> 24);
+            w[0] = x0 << 8;
+            n = kept;
+        }
+    }
     if (q == 0) {
         if (exh || n > kL2Cap) { w[0] = kOverflow; w[1] = w[2] = w[3] = 0; }
         else w[0] |= (uint32_t)n;
@@ -526,6 +673,7 @@ __device__ __forceinline__ void grid_cell_body(const GridArgs& a, int p, int cel
 
 __global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
     const int p = blockIdx.y, tid = threadIdx.x;
+    if (blockIdx.x == 0 && tid < 8) a.used_glob[p * 8 + tid] = 0u;  // for the assign that follows
     const bool exh = a.pflags[p] != 0;
     bool valid = false;
     float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -537,75 +685,30 @@ __global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
 }
 // ----------------------------------------------------------------------------
 // finalize: grid (P), block 1024.  Fixed-order fp64 sum of the tile partials
-// and OR of the per-block used masks -> out[p] = {sum, used[0..K-1]}.
+// (thread_partial_sums) and the used bits -> out[p] = {sum, used[0..K-1]}.
 // ----------------------------------------------------------------------------
-// One 1024-thread workgroup per palette.  Thread t sums partials
-// t, t + 1024, ... with all of its loads issued before the first add (one memory
-// round trip; 256 threads summing 8 at a time took ~10 dependent rounds), then
-// a fixed-order wave and workgroup reduction: bitwise reproducible.
 __global__ __launch_bounds__(1024) void finalize_kernel(FinalizeArgs a) {
-    constexpr int NT = 1024, NL = 24;  // loads in flight per thread per round
-#ifndef HQ_FIN_MU
-#define HQ_FIN_MU 32
-#endif
-    constexpr int MU = HQ_FIN_MU;      // used-mask words in flight per thread per round (32: the
-                                       // 4096 assign blocks of C3 in one round; 6.6 -> 6.1 us vs 8)
+    constexpr int NT = 1024;
     const int p = blockIdx.x, tid = threadIdx.x;
     __shared__ double s_red[NT / 64];
-    __shared__ uint32_t s_mask[NT];
-    const double* part = a.partial + (int64_t)p * a.ntiles;
-    double s = 0.0;
-    for (int t0 = 0; t0 < a.ntiles; t0 += NT * NL) {
-        double v[NL];
-#pragma unroll
-        for (int u = 0; u < NL; ++u) {
-            const int t = t0 + u * NT + tid;
-            v[u] = t < a.ntiles ? part[t] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < NL; ++u) s += v[u];
-    }
-    s = wave_sum_to_lane63(s);
+    double acc[1];
+    thread_partial_sums<1, 24>(a.partial + (int64_t)p * a.ntiles, a.ntiles, 1, acc);
+    const double s = wave_sum_to_lane63(acc[0]);
     if ((tid & 63) == 63) s_red[tid >> 6] = s;
-    // used: thread = (word w = tid & 7, block slice tid >> 3)
-    uint32_t m = 0;
-    const int w = tid & 7;
-    const uint32_t* um = a.used_mask + (int64_t)p * a.nblocks * 8;
-    for (int b0 = tid >> 3; !a.used32 && b0 < a.nblocks; b0 += (NT / 8) * MU) {
-        uint32_t mv[MU];
-#pragma unroll
-        for (int u = 0; u < MU; ++u) {
-            const int b = b0 + (NT / 8) * u;
-            mv[u] = b < a.nblocks ? um[b * 8 + w] : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < MU; ++u) m |= mv[u];
-    }
-    s_mask[tid] = m;
     __syncthreads();
     double* out = a.out + (int64_t)p * (1 + a.K);
-    if (a.used32) {  // K > 256: the reference's per-colour flags (assign_wide)
-        if (tid == 0) {
-            double tot = 0.0;
-            for (int i = 0; i < NT / 64; ++i) tot += s_red[i];
-            out[0] = tot;
-        }
-        const uint32_t* u = a.used32 + (int64_t)p * a.K;
-        for (int k = tid; k < a.K; k += NT) out[1 + k] = u[k] != 0u ? 1.0 : 0.0;
-        return;
-    }
     if (tid == 0) {
         double tot = 0.0;
         for (int i = 0; i < NT / 64; ++i) tot += s_red[i];
         out[0] = tot;
     }
-    if (tid < 8) {
-        uint32_t acc = 0;
-        for (int i = tid; i < NT; i += 8) acc |= s_mask[i];
-        s_mask[tid] = acc;  // slots 0..7 are only read after the barrier below
+    if (a.used32) {  // K > 256: the reference's per-colour flags (assign_wide)
+        const uint32_t* u = a.used32 + (int64_t)p * a.K;
+        for (int k = tid; k < a.K; k += NT) out[1 + k] = u[k] != 0u ? 1.0 : 0.0;
+    } else {
+        const uint32_t* u = a.used_glob + (int64_t)p * 8;
+        for (int k = tid; k < a.K; k += NT) out[1 + k] = (u[k >> 5] >> (k & 31)) & 1u ? 1.0 : 0.0;
     }
-    __syncthreads();
-    for (int k = tid; k < a.K; k += NT) out[1 + k] = (s_mask[k >> 5] >> (k & 31)) & 1u ? 1.0 : 0.0;
 }
 
 // ----------------------------------------------------------------------------

@@ -150,10 +150,11 @@ def test_fast_path_matches_generic(gpu, de, trim, rows):
 # ---------------------------------------------------------------------------
 # Viewing geometry (HQ:229-231 dpi / distance -> SP:80-102 tap count -> IM:408
 # halfSize): the fast path runs the filters centred in a tap bucket of
-# half-width 10, 16, 20 or 24; longer filters take the generic path.
+# half-width 10, 15, 19 or 24; longer filters take the generic path.
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("dpi,vd,half", [(96, 60.0, 19), (150, 30.0, 15), (72, 30.0, 7),
-                                         (96, 70.0, 22), (200, 30.0, 20), (300, 50.0, 51)])
+                                         (100, 55.0, 18), (96, 70.0, 22), (200, 30.0, 20),
+                                         (300, 50.0, 51)])
 def test_viewing_geometry_vs_oracle(gpu, dpi, vd, half):
     """Non-default dpi / viewing distance on a 256 x 256 and a ragged 301 x 173
     image: device LabRef within 2e-4, every cost within 1e-5 relative of the
@@ -260,13 +261,10 @@ def test_assign_signed_zero_and_mass_duplicates(ip, grid):
         np.testing.assert_array_equal(ip.getIndices(0), ref_idx.astype(np.uint8))
 
 
-@pytest.mark.parametrize("variant", [0, 1])
 @pytest.mark.parametrize("P", [1, 2, 3, 5, 6, 8])
-def test_assign_group_sizes(ip, P, variant):
+def test_assign_group_sizes(ip, P):
     """Groups of 1-4 palettes per pixel pass (P = 5: a full group and a group of
-    one).  P = 1, 2, 3 run assign_pipe_kernel<NG = P>; P >= 4 its NG = 4 instance
-    (variant 0) or assign_quad_kernel (variant 1: lanes = (pixel, palette))."""
-    ip.setOption("assign_variant", variant)
+    one).  P = 1, 2, 3 run assign_pipe_kernel<NG = P>, P >= 4 its NG = 4 instance."""
     rng = np.random.default_rng(P)
     w, h, K = 75, 41, 96
     px = np.zeros((w * h, 4), np.float32)
@@ -280,9 +278,8 @@ def test_assign_group_sizes(ip, P, variant):
         np.testing.assert_array_equal(used[p], ref_used)
 
 
-@pytest.mark.parametrize("variant", [0, 1])
 @pytest.mark.parametrize("grid", [64, 32, 16])
-def test_grid_margin_adversarial(ip, grid, variant):
+def test_grid_margin_adversarial(ip, grid):
     """build_grid's fp32 box bounds and its 1e-5 candidate margin (hq_search.hip)
     on the inputs that sit exactly on the decision boundaries: pixels on cell
     faces i/G2 (and on 0.0 / 1.0) and one ulp either side, palette colours on
@@ -324,7 +321,6 @@ def test_grid_margin_adversarial(ip, grid, variant):
     pals[3, :, :3] = (rng.integers(0, 256, (K, 3)) / 255.0).astype(np.float32)
     pals[3, ::7, 0] = rng.choice(faces, len(pals[3, ::7]))
     pals[3, 200:210] = pals[3, 3]
-    ip.setOption("assign_variant", variant)
     ip.setImage(px.reshape(-1), np.zeros_like(px).reshape(-1), w, ip.illum)
     refs = [c_oracle.assign(px, pals[p]) for p in range(4)]
     for g in (grid, 0):
@@ -407,6 +403,38 @@ def test_wide_palette_search_runs_host_driven(ip, filt):
     hbest, herr, _ = hq.SWASA(population=2, imax=6, seed=31, t0=0.5).search_host(K, ev)
     assert abs(gpu_err - herr) <= 1e-5 * abs(herr)
     np.testing.assert_array_equal(best, hbest)
+
+
+@pytest.mark.parametrize("P", [1, 4, 6])
+def test_used_flags_from_sparse_pixels(gpu, filt, P):
+    """Used flags are OR'ed into 8 words per palette by every assign workgroup
+    (device-scope atomics, hq_assign.hip): a colour used by a single pixel in
+    one corner of a 2048 x 2048 image -- one workgroup on one XCD -- must still
+    be flagged, and one used nowhere must not (CL:193).  Mostly-grey image with
+    200 isolated pixels of their own colours spread over the image."""
+    w = h = 2048
+    rng = np.random.default_rng(17 + P)
+    R = np.full(w * h, 0.5, np.float32)
+    G = R.copy()
+    B = R.copy()
+    K = 256
+    pals = np.zeros((P, K, 4), np.float32)
+    where = rng.choice(w * h, 200, replace=False)
+    cols = (rng.integers(0, 256, (200, 3)) / 255.0).astype(np.float32)
+    R[where], G[where], B[where] = cols[:, 0], cols[:, 1], cols[:, 2]
+    for p in range(P):
+        pals[p, :, :3] = (rng.integers(0, 256, (K, 3)) / 255.0).astype(np.float32)
+        pals[p, 0, :3] = 0.5  # the grey
+        sel = rng.choice(200, 100, replace=False)
+        pals[p, 1 + np.arange(100), :3] = cols[sel]
+    m = _planar_ctx(gpu, R, G, B, w, h, filt.illum)
+    _, used = m.computeQuantizationErrorPopulation(pals.reshape(P, -1), 2.0, return_used=True)
+    m.close()
+    rgba = o.inline_rgba(R, G, B)
+    for p in range(P):
+        _, ref_used = c_oracle.assign(rgba, pals[p], nthreads=_threads())
+        np.testing.assert_array_equal(used[p], ref_used, err_msg=f"palette {p}")
+        assert 50 < ref_used.sum() < 200
 
 
 def test_nonfinite_palette_falls_back_exactly(ip):
@@ -601,9 +629,8 @@ def test_device_search_with_single_rank_comm(gpu, filt):
 # Full-size properties (4096^2, K = 256): determinism, grid == exhaustive,
 # fast == generic, shards == full.
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("variant", [0, 1])
 @pytest.mark.parametrize("w,h,P", [(1003, 517, 4), (1003, 517, 3), (37, 29, 5)])
-def test_assign_workgroup_count_invariance(gpu, filt, w, h, P, variant):
+def test_assign_workgroup_count_invariance(gpu, filt, w, h, P):
     """The assign grid (option assign_blocks_per_cu: 1 workgroup per CU up to 64,
     default 16) only changes which workgroup takes which pixel chunk: indices,
     used flags and costs are bitwise the same for every count, also when an
@@ -611,7 +638,6 @@ def test_assign_workgroup_count_invariance(gpu, filt, w, h, P, variant):
     K = 256
     R, G, B = o.synthetic_image(w, h, seed=11)
     m = _planar_ctx(gpu, R, G, B, w, h, filt.illum)
-    m.setOption("assign_variant", variant)
     pals = np.stack([o.synthetic_palette(K, 40 + p) for p in range(P)]).reshape(P, -1)
     ref_c, ref_used = m.computeQuantizationErrorPopulation(pals, 2.0, return_used=True)
     ref_idx = [m.getIndices(p) for p in range(P)]
