@@ -112,7 +112,10 @@ __device__ __forceinline__ int64_t quad_cell(float r, float g, float b, int G2) 
 // loads only its NG 16-B entries of each 64-B level-2 line (P = 1 issued four
 // dwordx4 lookups per pixel for one useful one) and keeps NG palette tables.
 template <int NG>
-__global__ __launch_bounds__(256) void assign_pipe_kernel(AssignArgs a, int P) {
+#ifndef HQ_ASSIGN_WAVES
+#define HQ_ASSIGN_WAVES 1
+#endif
+__global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(AssignArgs a, int P) {
     constexpr int PPT = kAssignPPT;  // pixels per thread per chunk (the pipeline runs across chunks)
     // [NG][kMaxK]: a fixed palette stride, so each palette's base folds into the
     // ds_read_b128 offset field and a candidate's address is its byte << 4

@@ -48,10 +48,13 @@ struct PaletteArgs {
 };
 
 #ifndef HQ_ASSIGN_PPT
-#define HQ_ASSIGN_PPT 4
+#define HQ_ASSIGN_PPT 1
 #endif
-constexpr int kAssignPPT = HQ_ASSIGN_PPT;  // assign: pixels per thread per 256-thread chunk
-                                           // (4: as fast as 8 or 16 at 4096^2, 6% faster on a 512-row shard)
+constexpr int kAssignPPT = HQ_ASSIGN_PPT;  // assign: pixels per thread per 256-thread chunk.  1, with
+                                           // one resident round of workgroups (6 per CU), makes the
+                                           // pixel sequence a grid stride: every thread gets the same
+                                           // number of pixels +-1 (512-row shard 0.1306 -> 0.1261 ms per
+                                           // step vs 4 per chunk at 16 per CU; 4096^2 unchanged)
 constexpr int kSaMaxP = 64;       // device-resident SWASA: largest population
 constexpr int kFoldMaxP = 8;      // largest population whose accept step folds the finalize
 

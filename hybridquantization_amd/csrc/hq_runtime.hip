@@ -120,7 +120,9 @@ struct hq_ctx {
     int G2 = 32;           // argmin grid resolution (0 = exhaustive)
     int cost_variant = 0;  // 0 tiled (default), 1 generic two-pass
     int cost_rows = 16;    // fast path tiles: 16 x 128 (cost16w_kernel) or 8 x 108 (cost_mfma_kernel)
-    int assign_blocks_per_cu = 16;  // 4096^2: 4 chunks per workgroup; 0.632 -> 0.605 ms per step vs 8
+    int assign_blocks_per_cu = 0;  // 0 = auto: assign_pipe_kernel<NG>'s residency (NG = 4: 78 VGPRs,
+                                   // 6 waves per SIMD; NG = 3: 7; NG <= 2: 8), one round of
+                                   // workgroups, each thread a grid-stride pixel sequence
     int shard_solo = 0;    // experiment: a sharded search without a communicator (per-rank timing)
     int sa_device = 1;     // hq_search_*: 1 = SWASA iterations resident on the device (no host
                            // round trip per iteration), 0 = host-driven (one eval call each)
@@ -323,9 +325,11 @@ int check_geom_args(hq_ctx* c, int w, int h, int r0, int r1) {
 // shard ran assign on half the chip: 0.071 vs 0.053 ms).  (Evening out the
 // chunks per workgroup instead -- 1064 workgroups of 2 for 2128 chunks -- was
 // slower than 2048 with 80 of them taking a second chunk.)
-int assign_blocks(const hq_ctx* c) {
+int assign_blocks(const hq_ctx* c, int P) {
     const int64_t chunk = 256 * kAssignPPT;
-    const int64_t nblocks = (int64_t)c->num_cu * c->assign_blocks_per_cu;
+    const int ng = std::min(P, 4);
+    const int per_cu = c->assign_blocks_per_cu > 0 ? c->assign_blocks_per_cu : (ng >= 4 ? 6 : ng == 3 ? 7 : 8);
+    const int64_t nblocks = (int64_t)c->num_cu * per_cu;
     return (int)std::max<int64_t>(1, std::min<int64_t>(nblocks, (c->g.n_ext + chunk - 1) / chunk));
 }
 
@@ -473,7 +477,7 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
     } else {
         HIP_TRY(c, hipMemsetAsync(c->d_used_mask.p, 0, sizeof(uint32_t) * 8 * (size_t)P, s));
     }
-    const int nblocks = assign_blocks(c);
+    const int nblocks = assign_blocks(c, P);
     const AssignArgs aa{c->d_R.as<float>(), c->d_G.as<float>(), c->d_B.as<float>(), c->d_pal.as<float4>(),
                         c->d_pflags.as<int>(), c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(),
                         c->d_idx.as<uint8_t>(), c->d_used_mask.as<uint32_t>(), g.n_ext, g.idx_pitch,
@@ -1227,7 +1231,7 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
     } else if (!std::strcmp(name, "shard_solo")) {
         c->shard_solo = value != 0;
     } else if (!std::strcmp(name, "assign_blocks_per_cu")) {
-        if (value < 1 || value > 64) return fail(c, HQ_ERR_ARG, "assign_blocks_per_cu in [1,64]");
+        if (value < 0 || value > 64) return fail(c, HQ_ERR_ARG, "assign_blocks_per_cu in [0,64] (0 = auto)");
         c->assign_blocks_per_cu = value;
     } else {
         return fail(c, HQ_ERR_ARG, "unknown option '%s'", name);

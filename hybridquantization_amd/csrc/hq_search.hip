@@ -673,6 +673,9 @@ __device__ __forceinline__ void grid_cell_body(const GridArgs& a, int p, int cel
 
 __global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
     const int p = blockIdx.y, tid = threadIdx.x;
+#ifdef HQ_GRID_TIMING  // diagnostic build: per-workgroup start / end (wall_clock64, 100 MHz)
+    const uint64_t t_start = wall_clock64();
+#endif
     if (blockIdx.x == 0 && tid < 8) a.used_glob[p * 8 + tid] = 0u;  // for the assign that follows
     const bool exh = a.pflags[p] != 0;
     bool valid = false;
@@ -682,6 +685,12 @@ __global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
         valid = !exh && a.dup[(int64_t)p * kMaxK + tid] == 0;
     }
     grid_cell_body(a, p, blockIdx.x, c, valid, exh);
+#ifdef HQ_GRID_TIMING
+    __syncthreads();
+    if (tid == 0)
+        printf("GRID_T %d %d %llu %llu\n", p, (int)blockIdx.x, (unsigned long long)t_start,
+               (unsigned long long)wall_clock64());
+#endif
 }
 // ----------------------------------------------------------------------------
 // finalize: grid (P), block 1024.  Fixed-order fp64 sum of the tile partials

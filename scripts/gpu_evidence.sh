@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 E=gpurun_out/ev
 mkdir -p $E
 fatal() { if [ "$1" -ne 0 ]; then echo "FAILED rc=$1 at $2"; exit "$1"; fi; }
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $E/pytest_gpu.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -rA --durations=0 --timeout 300 --timeout-method thread -p no:cacheprovider > $E/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -2 $E/pytest_gpu.log; fatal $rc pytest
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $E/smoke.log 2>&1
 rc=$?; echo "smoke rc=$rc"; tail -2 $E/smoke.log; fatal $rc smoke
@@ -29,7 +29,9 @@ done
 : > $E/configs.jsonl
 # each line starts on settled clocks: the full C3-schedule search of its shape first
 # (C5's 64-palette search would take ~1 min: 10 warm-up steps, ~0.1 s, instead)
-for cfg in "--size 1024 --K 64 --population 1" "--population 1" "" "--size 8192 --shard-of 8" "--population 64 --steps 20 --warmup 10 --no-full-search"; do
+for cfg in "--size 1024 --K 64 --population 1" "--population 1" "" "--size 8192 --shard-of 8" "--population 64 --steps 20 --warmup 10 --no-full-search" \
+           "--dpi 96 --distance 60 --no-full-search" "--dpi 150 --distance 30 --no-full-search" \
+           "--size 1024 --K 1024 --steps 10 --warmup 2 --no-full-search"; do
   timeout -k 10 300 python bench.py --no-cpu-baseline $cfg >> $E/configs.jsonl 2>> $E/configs.err
   rc=$?; echo "config [$cfg] rc=$rc"; fatal $rc "config $cfg"
 done

@@ -1,0 +1,41 @@
+"""Diagnostic: per-workgroup start/end stamps of build_grid (a library built with
+-DHQ_GRID_TIMING, HQ_LIB_PATH) over a few 4096^2 / K=256 / P=4 evaluations;
+prints the dispatch spread and the workgroup durations of the last one."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if len(sys.argv) > 1 and sys.argv[1] == "run":
+    sys.path.insert(0, ROOT)
+    import numpy as np
+    import bench
+    import hybridquantization_amd as hq
+    from hybridquantization_amd import _lib
+    lib = hq.load()
+    m = hq.ImageManipulation(device=0)
+    sp = hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
+    W = int(os.environ.get("GT_SIZE", "4096"))
+    R, G, B = bench.synthetic_planes(W, W)
+    _lib.check(lib.hq_set_image_planar_shard(m.ctx, _lib.fptr(R), _lib.fptr(G), _lib.fptr(B), W, W,
+                                             _lib.fptr(sp.illuminant), 0, W), m.ctx)
+    rng = np.random.default_rng(1)
+    for it in range(3):
+        pal = rng.random((4, 256, 4), dtype=np.float32)
+        pal[..., 3] = 0
+        print("EVAL", it, flush=True)
+        m.computeQuantizationErrorPopulation(pal.reshape(4, -1), 2.0)
+    m.close()
+    sys.exit(0)
+out = subprocess.run([sys.executable, __file__, "run"], capture_output=True, text=True, timeout=300).stdout
+evals = out.split("EVAL")
+last = [l.split() for l in evals[-1].splitlines() if l.startswith("GRID_T")]
+st = [int(x[3]) for x in last]
+en = [int(x[4]) for x in last]
+t0 = min(st)
+durs = sorted((e - s) / 100.0 for s, e in zip(st, en))  # 100 MHz ticks -> us
+starts = sorted((s - t0) / 100.0 for s in st)
+print(f"{len(last)} workgroups; start spread {starts[-1]:.2f} us (50% by {starts[len(starts)//2]:.2f}); "
+      f"end {max((e - t0) / 100.0 for e in en):.2f} us")
+print("duration us: min %.2f med %.2f p90 %.2f max %.2f" % (durs[0], durs[len(durs) // 2],
+                                                           durs[int(len(durs) * 0.9)], durs[-1]))
