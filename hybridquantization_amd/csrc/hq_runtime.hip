@@ -22,7 +22,7 @@ namespace hq {
 hipError_t launch_prep_palette(const PaletteArgs&, int P, hipStream_t);
 hipError_t launch_sa_step(const SaArgs&, hipStream_t);
 void set_launch_events(hipEvent_t start, hipEvent_t stop);
-hipError_t launch_build_grid(const GridArgs&, int P, int variant, hipStream_t);
+hipError_t launch_build_grid(const GridArgs&, int P, hipStream_t);
 hipError_t launch_assign(const AssignArgs&, int P, hipStream_t);
 void fast_tile_dims(int W, int own_rows, int tile_rows, int* tiles_x, int* ntiles);
 void opp2xyz_over_illum(const float inv_illum[3], float m[9]);
@@ -119,7 +119,6 @@ struct hq_ctx {
     // options
     int G2 = 32;           // argmin grid resolution (0 = exhaustive)
     int cost_variant = 0;  // 0 tiled (default), 1 generic two-pass
-    int grid_variant = 1;  // build_grid: 1 wave form (default), 0 workgroup form
     int cost_rows = 16;    // fast path tiles: 16 x 128 (cost16w_kernel) or 8 x 108 (cost_mfma_kernel)
     int assign_blocks_per_cu = 0;  // 0 = auto: assign_pipe_kernel<NG>'s residency (NG = 4: 78 VGPRs,
                                    // 6 waves per SIMD; NG = 3: 7; NG <= 2: 8), one round of
@@ -472,7 +471,7 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
     auto untimed = [&]() { set_launch_events(nullptr, nullptr); };
     if (c->G2 > 0) {  // (build_grid also zeroes the used bits)
         timed(0);
-        const hipError_t e = launch_build_grid(ga, P, c->grid_variant, s);
+        const hipError_t e = launch_build_grid(ga, P, s);
         untimed();
         HIP_TRY(c, e);
     } else {
@@ -1218,9 +1217,6 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
         if (value != 0 && value != 16 && value != 32 && value != 64)
             return fail(c, HQ_ERR_ARG, "grid must be 0, 16, 32 or 64");
         c->G2 = value;
-    } else if (!std::strcmp(name, "grid_variant")) {
-        if (value < 0 || value > 1) return fail(c, HQ_ERR_ARG, "grid_variant must be 0 or 1");
-        c->grid_variant = value;
     } else if (!std::strcmp(name, "cost_variant")) {
         if (value < 0 || value > 1) return fail(c, HQ_ERR_ARG, "cost_variant must be 0 or 1");
         c->cost_variant = value;

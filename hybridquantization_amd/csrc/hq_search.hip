@@ -698,141 +698,6 @@ __global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
 #endif
 }
 // ----------------------------------------------------------------------------
-// build_grid, wave form (default): grid (G1^3, P), block 256 = four waves that
-// never wait for each other.  Every wave builds the level-1 list of the cell
-// itself -- 4 colours per lane, a wave min of dmax^2 and four ballots -- and
-// then the level-2 entries of 16 of the cell's 64 children (children 16w ..
-// 16w+15, a quad of lanes per child), with each child's bounds computed from
-// the colours.  No barrier: a wave's LDS accesses complete in issue order, so
-// its lanes read what its other lanes wrote.  Same candidate test and the same
-// fp32 expressions as grid_cell_body, so the same lists.  The workgroup form
-// (grid_cell_body) spent ~8 barriers per cell with one colour per thread; its
-// slowest cells set the launch (13.4 us at P = 4 with its median workgroup at
-// ~6 us).
-// ----------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void build_grid_wave_kernel(GridArgs a) {
-    const int p = blockIdx.y, cell = blockIdx.x, tid = threadIdx.x;
-    const int wv = tid >> 6, lane = tid & 63;
-    __shared__ float4 s_col[4][kMaxK];  // wave-private copies of the palette
-    __shared__ uint8_t s_list[4][kMaxK];
-    float4* col = s_col[wv];
-    uint8_t* lst = s_list[wv];
-    if (cell == 0 && tid < 8) a.used_glob[p * 8 + tid] = 0u;  // for the assign that follows
-    const bool exh = a.pflags[p] != 0;
-    const int G1 = a.G1, G2 = 4 * G1;
-    const int ci = cell / (G1 * G1), cj = (cell / G1) % G1, ck = cell % G1;
-    const float inv1 = 1.0f / (float)G1;
-    const float lo0 = ci * inv1, hi0 = (ci + 1) * inv1;
-    const float lo1 = cj * inv1, hi1 = (cj + 1) * inv1;
-    const float lo2 = ck * inv1, hi2 = (ck + 1) * inv1;
-    // level 1: colours lane + 64 j
-    float dmin2[4];
-    bool valid[4];
-    float m = INFINITY;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int k = lane + 64 * j;
-        float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
-        valid[j] = false;
-        if (k < a.K) {
-            c = a.pal[(int64_t)p * kMaxK + k];
-            valid[j] = !exh && a.dup[(int64_t)p * kMaxK + k] == 0;
-        }
-        col[k] = c;
-        dmin2[j] = INFINITY;
-        if (valid[j]) {
-            dmin2[j] = (ax_min2(c.x, lo0, hi0) + ax_min2(c.y, lo1, hi1)) + ax_min2(c.z, lo2, hi2);
-            m = fminf(m, (ax_max2(c.x, lo0, hi0) + ax_max2(c.y, lo1, hi1)) + ax_max2(c.z, lo2, hi2));
-        }
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) m = fminf(m, __shfl_xor(m, off, 64));
-    const float T1 = m;
-    int total = 0;
-    const uint64_t below = (1ull << lane) - 1ull;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {  // ascending colour index: j-major, then lane
-        const bool cand = valid[j] && dmin2[j] <= T1 * HQ_CAND_MARGIN;
-        const uint64_t bal = __ballot(cand);
-        if (cand) lst[total + __popcll(bal & below)] = (uint8_t)(lane + 64 * j);
-        total += __popcll(bal);
-    }
-    if (exh) total = 0;
-    __builtin_amdgcn_wave_barrier();
-    if (wv == 0 && lane < 32) {
-        const bool ovf1 = exh || total > kL1Cap;
-        uint8_t v;
-        if (lane == 0) v = ovf1 ? kOverflow : (uint8_t)total;
-        else v = (!ovf1 && lane - 1 < total) ? lst[lane - 1] : 0;
-        a.lvl1[(int64_t)p * a.lvl1_pitch + (int64_t)cell * 32 + lane] = v;
-    }
-    // level 2: child ch = 16 wv + (lane >> 2) at axis positions (a0, a1, a2)
-    const float inv2 = 1.0f / (float)G2;
-    const int ch = 16 * wv + (lane >> 2), q = lane & 3;
-    const int a0 = ch >> 4, a1 = (ch >> 2) & 3, a2 = ch & 3;
-    const float blo[3] = {(float)(4 * ci + a0) * inv2, (float)(4 * cj + a1) * inv2, (float)(4 * ck + a2) * inv2};
-    const float bhi[3] = {(float)(4 * ci + a0 + 1) * inv2, (float)(4 * cj + a1 + 1) * inv2,
-                          (float)(4 * ck + a2 + 1) * inv2};
-    // pass 1: T2 (and the position attaining it) over the whole parent list
-    float t2 = INFINITY;
-    int t2pos = 0;
-    for (int i = q; i < total; i += 4) {
-        const float4 cc = col[lst[i]];
-        const float d = (ax_max2(cc.x, blo[0], bhi[0]) + ax_max2(cc.y, blo[1], bhi[1])) +
-                        ax_max2(cc.z, blo[2], bhi[2]);
-        if (d < t2) { t2 = d; t2pos = i; }
-    }
-#pragma unroll
-    for (int mm = 1; mm <= 2; mm <<= 1) {
-        const float o = __shfl_xor(t2, mm, 64);
-        const int op = __shfl_xor(t2pos, mm, 64);
-        if (o < t2 || (o == t2 && op < t2pos)) { t2 = o; t2pos = op; }
-    }
-    const float thr = t2 * HQ_CAND_MARGIN;
-    const int bstar = total > 0 ? (int)lst[t2pos] : 0;
-    // pass 2, 32 positions at a time: candidate mask, ranks in list order
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
-    int n = 0;  // candidates so far (quad-uniform)
-    for (int b0 = 0; b0 < total && n <= kL2Cap; b0 += 32) {
-        uint32_t mine = 0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int i = b0 + q + 4 * j;
-            if (i < total) {
-                const float4 cc = col[lst[i]];
-                const float d = (ax_min2(cc.x, blo[0], bhi[0]) + ax_min2(cc.y, blo[1], bhi[1])) +
-                                ax_min2(cc.z, blo[2], bhi[2]);
-                if (d <= thr) mine |= 1u << (q + 4 * j);
-            }
-        }
-        uint32_t M = mine | (uint32_t)__shfl_xor((int)mine, 1, 64);
-        M |= (uint32_t)__shfl_xor((int)M, 2, 64);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int r = q + 4 * j;
-            if ((mine >> r) & 1u) {
-                const int pos = n + __popc(M & ((1u << r) - 1u)) + 1;  // byte in the entry
-                if (pos <= kL2Cap) w[pos >> 2] |= (uint32_t)lst[b0 + r] << (8 * (pos & 3));
-            }
-        }
-        n += __popc(M);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        w[k] |= (uint32_t)__shfl_xor((int)w[k], 1, 64);
-        w[k] |= (uint32_t)__shfl_xor((int)w[k], 2, 64);
-    }
-    if (!exh && n >= 2 && n <= kL2Cap) prune_dominated(w, n, col, bstar, blo, bhi, q);
-    if (q == 0) {
-        if (exh || n > kL2Cap) { w[0] = kOverflow; w[1] = w[2] = w[3] = 0; }
-        else w[0] |= (uint32_t)n;
-        const int ci2 = ci * 4 + a0, cj2 = cj * 4 + a1, ck2 = ck * 4 + a2;
-        uint8_t* l2e = a.lvl2 + lvl2_offset(a.lvl2_gstride, p, (int64_t)(ci2 * G2 + cj2) * G2 + ck2);
-        *reinterpret_cast<uint4*>(l2e) = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-}
-
-// ----------------------------------------------------------------------------
 // finalize: grid (P), block 1024.  Fixed-order fp64 sum of the tile partials
 // (thread_partial_sums) and the used bits -> out[p] = {sum, used[0..K-1]}.
 // ----------------------------------------------------------------------------
@@ -879,11 +744,8 @@ hipError_t launch_sa_step(const SaArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_build_grid(const GridArgs& a, int P, int variant, hipStream_t s) {
-    if (variant == 0)
-        HQ_LAUNCH(build_grid_kernel, dim3(a.G1 * a.G1 * a.G1, P), dim3(256), 0, s, a);
-    else
-        HQ_LAUNCH(build_grid_wave_kernel, dim3(a.G1 * a.G1 * a.G1, P), dim3(256), 0, s, a);
+hipError_t launch_build_grid(const GridArgs& a, int P, hipStream_t s) {
+    HQ_LAUNCH(build_grid_kernel, dim3(a.G1 * a.G1 * a.G1, P), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

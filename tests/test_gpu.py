@@ -278,9 +278,8 @@ def test_assign_group_sizes(ip, P):
         np.testing.assert_array_equal(used[p], ref_used)
 
 
-@pytest.mark.parametrize("gv", [1, 0])
 @pytest.mark.parametrize("grid", [64, 32, 16])
-def test_grid_margin_adversarial(ip, grid, gv):
+def test_grid_margin_adversarial(ip, grid):
     """build_grid's fp32 box bounds and its 1e-5 candidate margin (hq_search.hip)
     on the inputs that sit exactly on the decision boundaries: pixels on cell
     faces i/G2 (and on 0.0 / 1.0) and one ulp either side, palette colours on
@@ -322,7 +321,6 @@ def test_grid_margin_adversarial(ip, grid, gv):
     pals[3, :, :3] = (rng.integers(0, 256, (K, 3)) / 255.0).astype(np.float32)
     pals[3, ::7, 0] = rng.choice(faces, len(pals[3, ::7]))
     pals[3, 200:210] = pals[3, 3]
-    ip.setOption("grid_variant", gv)  # build_grid: wave form (default) or workgroup form
     ip.setImage(px.reshape(-1), np.zeros_like(px).reshape(-1), w, ip.illum)
     refs = [c_oracle.assign(px, pals[p]) for p in range(4)]
     for g in (grid, 0):
@@ -673,12 +671,7 @@ def test_full_size_properties(gpu, filt):
     c3 = m.computeQuantizationErrorPopulation(pals, 2.0)
     np.testing.assert_array_equal(m.getIndices(1), idx1)  # pruned == exhaustive argmin
     np.testing.assert_array_equal(c3, c1)
-    m.setOption("grid", 32)
-    m.setOption("grid_variant", 0)  # the workgroup-form grid builds the same lists
-    c3b = m.computeQuantizationErrorPopulation(pals, 2.0)
-    np.testing.assert_array_equal(m.getIndices(1), idx1)
-    np.testing.assert_array_equal(c3b, c1)
-    m.setOption("grid_variant", 1)
+
     m.setOption("grid", 64)
     m.setOption("cost_rows", 8)
     c8 = m.computeQuantizationErrorPopulation(pals, 2.0)
