@@ -372,6 +372,8 @@ void prof_add(hq_ctx* c, ProfSlot& s, hipEvent_t a, hipEvent_t b) {
     if (hipEventElapsedTime(&ms, a, b) == hipSuccess) {
         s.ms += ms;
         s.launches += 1;
+    } else {
+        (void)hipGetLastError();  // an event pair this evaluation never recorded: not a launch error
     }
 }
 
@@ -532,8 +534,8 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
 }
 
 // Add one evaluation's kernel times (its events have completed).
-void prof_accumulate(hq_ctx* c, const hipEvent_t* ev, bool finalize = true) {
-    if (c->G2 > 0) prof_add(c, c->prof_grid, ev[0], ev[1]);
+void prof_accumulate(hq_ctx* c, const hipEvent_t* ev, bool finalize = true, bool grid = true) {
+    if (grid && c->G2 > 0) prof_add(c, c->prof_grid, ev[0], ev[1]);
     prof_add(c, c->prof_assign, ev[2], ev[3]);
     prof_add(c, c->prof_cost, ev[4], ev[5]);
     if (finalize) prof_add(c, c->prof_finalize, ev[6], ev[7]);
@@ -557,7 +559,7 @@ int enqueue_eval(hq_ctx* c, int P, int K) {
     HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out.p, sizeof(double) * (size_t)P * (1 + K),
                               hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
-    if (ev) prof_accumulate(c, ev);
+    if (ev) prof_accumulate(c, ev, true, K <= kMaxK);  // (K > 256 builds no grid)
     return HQ_OK;
 }
 

@@ -381,6 +381,13 @@ def test_wide_palette_vs_oracle(gpu, filt, K):
         np.testing.assert_array_equal(m.getIndices32(p), parts["idx"].astype(np.uint32))
     with pytest.raises(hq.HQError):
         m.getIndices(0)  # u8 indices only exist for K <= 256
+    lib = hq.load()  # kernel timing on: the wide path records no grid events, and must not fail
+    lib.hq_profile_enable(m.ctx, 1)
+    c2 = m.computeQuantizationErrorPopulation(pals.reshape(2, -1), 2.0)
+    c3 = m.computeQuantizationErrorPopulation(pals.reshape(2, -1), 2.0)
+    lib.hq_profile_enable(m.ctx, 0)
+    np.testing.assert_array_equal(c2, costs)
+    np.testing.assert_array_equal(c3, costs)
     m.close()
 
 
