@@ -4,6 +4,17 @@
 #include "hq_device.h"
 #include "hq_launch.h"
 
+#ifndef HQ_ASSIGN_PF
+#define HQ_ASSIGN_PF 1
+#endif
+#ifndef HQ_ASSIGN_PRED
+#define HQ_ASSIGN_PRED 2
+#endif
+#ifndef HQ_ASSIGN_JOINT
+#define HQ_ASSIGN_JOINT 0  // 1: argmin_group over the whole group in lockstep (measured slower:
+                           // 0.218 vs 0.199 ms at C3 P=4, fewer waves and longer walks)
+#endif
+
 namespace hq {
 
 // Reference loop verbatim (CL:179-192) over a candidate list or all K colours.
@@ -21,19 +32,17 @@ __device__ __noinline__ int argmin_exact_slow(float r, float g, float b, uint4 L
     return bi;
 }
 
-// Exact argmin (CL:179-193 semantics) over the pixel's candidate list.
-// Candidates are ranked by d2; the reference ranks by sqrtf(d2), which can map
-// two different d2 onto one distance, and then keeps the lower index.  Equal
-// sqrtf values imply |d2a - d2b| < 2^-22 * d2, so lanes whose runner-up d2 lies
-// within 1e-6 relative of the best are re-resolved with the reference loop
-// (rare).
-__device__ __forceinline__ int argmin_from_entry(float r, float g, float b, uint4 L0, bool listed,
-                                                 const float4* s_pal, const uint8_t* lvl1p, int G2,
-                                                 int K) {
+// Re-resolution of one palette's pixel by the reference loop: the level-1 list
+// when the level-2 list overflowed (or all K colours when that overflowed too),
+// else the level-2 list itself (a near tie) or all K (no list: pixel outside
+// the unit cube, or a palette outside it).
+__device__ __noinline__ int argmin_resolve_slow(float r, float g, float b, uint4 L0, bool listed,
+                                                const float4* s_pal, const uint8_t* lvl1p, int G2,
+                                                int K) {
     uint4 L1 = make_uint4(0, 0, 0, 0);
     int cnt = listed ? (int)(L0.x & 0xff) : 0;
-    bool exh = !listed;
-    if (cnt == kOverflow) {  // level-2 overflow: the parent's level-1 list (rare)
+    bool all = !listed;
+    if (cnt == kOverflow) {
         const int G1 = G2 >> 2;
         const int ir = min((int)(r * (float)G2), G2 - 1) >> 2;
         const int ig = min((int)(g * (float)G2), G2 - 1) >> 2;
@@ -43,52 +52,115 @@ __device__ __forceinline__ int argmin_from_entry(float r, float g, float b, uint
         L0 = e[0];
         L1 = e[1];
         cnt = L0.x & 0xff;
-        if (cnt == kOverflow) { exh = true; cnt = 0; }
+        if (cnt == kOverflow) all = true;
     }
-    int bi = (L0.x >> 8) & 0xff;  // first candidate (lowest index)
-    bool near = false;
-    if (__any(cnt > 1)) {
-        const uint32_t words[8] = {L0.x, L0.y, L0.z, L0.w, L1.x, L1.y, L1.z, L1.w};
-        // Ranked by dist2_rank.  best2 <= second2 always, so the runner-up after a
-        // new value is the median of the three (v_med3_f32): 4 VALU per candidate
-        // to track best, runner-up and index (the compare-and-select form took 7).
-        // Slots past a lane's list (build_grid writes index 0 there) rank as +inf.
-        const f32x2 rg = {r, g};
-        float best2 = dist2_rank(r, g, b, s_pal[bi]);
-        float second2 = INFINITY;
-        // The next candidate's colour is read while this one is evaluated (the
-        // loop is unrolled, so the hand-over is register renaming, not a copy).
-        // Candidates are tracked by LDS byte offset (index x 16): one SDWA shift
-        // takes list byte j straight to the ds_read_b128 address.
-        const char* base = reinterpret_cast<const char*>(s_pal);
-        auto at = [&](uint32_t off) { return *reinterpret_cast<const float4*>(base + off); };
-        auto cand16 = [&](int i) { return byte_x16(words[(i + 1) >> 2], (i + 1) & 3); };
-        uint32_t ba = (uint32_t)bi << 4;
-        uint32_t an = cand16(1);
-        float4 cn = at(an);
+    return argmin_exact_slow(r, g, b, L0, L1, cnt, all, s_pal, K);
+}
+
+// Exact argmin (CL:179-193 semantics) of one pixel against the NG palettes of
+// its group over their level-2 candidate lists.  Candidates are ranked by d2;
+// the reference ranks by sqrtf(d2), which can map two different d2 onto one
+// distance, and then keeps the lower index.  Equal sqrtf values imply
+// |d2a - d2b| < 2^-22 * d2, so lanes whose runner-up d2 lies within 1e-6
+// relative of the best are re-resolved with the reference loop (rare), as are
+// lanes whose list overflowed the level-2 entry or that have no list.
+// NG > 1 walks the lists in lockstep (HQ_ASSIGN_JOINT): candidate i of every
+// palette in one loop step, NG independent LDS reads and compare chains in
+// flight; the step count is then the longest list over the wave's lanes and
+// the group's palettes.
+template <int NG>
+__device__ __forceinline__ void argmin_group(float r, float g, float b, const uint4 (&E)[NG], bool inside,
+                                             const bool (&exh_pal)[NG], const float4* s_pal,
+                                             const uint8_t* lvl1, int64_t lvl1_pitch, int p0, int G2,
+                                             int K, int (&out)[NG]) {
+    int cnt[NG];
+    bool slow[NG];
+    uint32_t ba[NG];
+    int maxc = 0;
 #pragma unroll
-        for (int i = 1; i < kL1Cap; ++i) {
-            if (!__any(i < cnt)) break;
-            const uint32_t ak = an;
-            const float4 c = cn;
-            if (i + 1 < kL1Cap) {
-                an = cand16(i + 1);
-                cn = at(an);
+    for (int q = 0; q < NG; ++q) {
+        const bool listed = inside && !exh_pal[q];
+        const int c = listed ? (int)(E[q].x & 0xff) : 0;
+        slow[q] = !listed || c == kOverflow;
+        cnt[q] = slow[q] ? 0 : c;
+        maxc = max(maxc, cnt[q]);
+        ba[q] = byte_x16(E[q].x, 1);
+    }
+    bool near[NG];
+#pragma unroll
+    for (int q = 0; q < NG; ++q) near[q] = false;
+    if (__any(maxc > 1)) {
+        const f32x2 rg = {r, g};
+        const char* base = reinterpret_cast<const char*>(s_pal);
+        auto at = [&](int q, uint32_t off) {
+            return *reinterpret_cast<const float4*>(base + q * (kMaxK * 16) + off);
+        };
+        auto cand16 = [&](int q, int i) {  // byte i + 1 of the entry, x16
+            const uint32_t w = (i + 1) < 4 ? E[q].x : (i + 1) < 8 ? E[q].y : (i + 1) < 12 ? E[q].z : E[q].w;
+            return byte_x16(w, (i + 1) & 3);
+        };
+        float best2[NG], second2[NG];
+        // candidate colours are read HQ_ASSIGN_PF steps ahead of their use
+        constexpr int PF = HQ_ASSIGN_PF;
+        uint32_t an[NG][PF];
+        float4 cn[NG][PF];
+#pragma unroll
+        for (int q = 0; q < NG; ++q) {
+            best2[q] = dist2_rank(r, g, b, at(q, ba[q]));
+            second2[q] = INFINITY;
+#pragma unroll
+            for (int d = 0; d < PF; ++d) {
+                an[q][d] = cand16(q, 1 + d);
+                cn[q][d] = at(q, an[q][d]);
             }
-            asm volatile("" ::"v"(c.w));  // keep .w: one ds_read_b128 (16-lane groups), not b96
-            const float d2 = i < cnt ? dist2_rank_pk(rg, b, c) : INFINITY;
-            const bool lt = d2 < best2;  // a select, not fminf (which canonicalises its inputs)
-            ba = lt ? ak : ba;
-            second2 = __builtin_amdgcn_fmed3f(best2, second2, d2);
-            best2 = lt ? d2 : best2;
         }
-        bi = (int)(ba >> 4);
-        near = second2 <= best2 * (1.0f + 1e-6f);
+#pragma unroll
+        for (int i = 1; i < kL2Cap; ++i) {
+            if (!__any(i < maxc)) break;
+#pragma unroll
+            for (int q = 0; q < NG; ++q) {
+                const uint32_t ak = an[q][0];
+                const float4 c = cn[q][0];
+#pragma unroll
+                for (int d = 0; d + 1 < PF; ++d) {
+                    an[q][d] = an[q][d + 1];
+                    cn[q][d] = cn[q][d + 1];
+                }
+                if (i + PF < kL2Cap) {
+                    an[q][PF - 1] = cand16(q, i + PF);
+#if HQ_ASSIGN_PRED == 1
+                    // only lanes whose list reaches that far read LDS (exec-masked):
+                    // the wave walks to its longest list, 6 steps for a mean of 2
+                    if (i + PF < cnt[q]) cn[q][PF - 1] = at(q, an[q][PF - 1]);
+#elif HQ_ASSIGN_PRED == 2
+                    // lanes past their list all read entry 0 (one broadcast address,
+                    // no bank conflicts): the wave walks to its longest list
+                    cn[q][PF - 1] = at(q, i + PF < cnt[q] ? an[q][PF - 1] : 0u);
+#else
+                    cn[q][PF - 1] = at(q, an[q][PF - 1]);
+#endif
+                }
+                asm volatile("" ::"v"(c.w));  // one ds_read_b128, not b96
+                const float d2 = i < cnt[q] ? dist2_rank_pk(rg, b, c) : INFINITY;
+                const bool lt = d2 < best2[q];
+                ba[q] = lt ? ak : ba[q];
+                second2[q] = __builtin_amdgcn_fmed3f(best2[q], second2[q], d2);
+                best2[q] = lt ? d2 : best2[q];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < NG; ++q) near[q] = second2[q] <= best2[q] * (1.0f + 1e-6f);
     }
-    if (__any(exh || near)) {
-        if (exh || near) bi = argmin_exact_slow(r, g, b, L0, L1, cnt, exh, s_pal, K);
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+        out[q] = (int)(ba[q] >> 4);
+        const bool s = slow[q] || near[q];
+        if (__any(s)) {
+            if (s)
+                out[q] = argmin_resolve_slow(r, g, b, E[q], inside && !exh_pal[q], s_pal + q * kMaxK,
+                                             lvl1 + (int64_t)(p0 + q) * lvl1_pitch, G2, K);
+        }
     }
-    return bi;
 }
 
 // ----------------------------------------------------------------------------
@@ -108,48 +180,78 @@ __device__ __forceinline__ int64_t quad_cell(float r, float g, float b, int G2) 
            min((int)(b * (float)G2), G2 - 1);
 }
 
-// NG = min(P, 4): the palettes a pixel pass can serve.  A population below 4
-// loads only its NG 16-B entries of each 64-B level-2 line (P = 1 issued four
-// dwordx4 lookups per pixel for one useful one) and keeps NG palette tables.
-template <int NG>
+// NG: the palettes of the group a pixel pass serves (4, or P mod 4 for the
+// last group, launched on its own): every palette slot is live, so the
+// resolve step has no data-dependent exits.  A group below 4 loads only its NG
+// 16-B entries of each 64-B level-2 line and keeps NG palette tables.
+// k/255 exactly as the host's float division makes it, from the byte k: the
+// product with RN(1/255) is off by one ulp for 126 of the 256 values; one FMA
+// residual step corrects all 256 (checked exhaustively, tests/test_assign_u8.py).
+__device__ __forceinline__ float u8_unit(uint32_t v, int j) {
+    const float k = (float)((v >> (8 * j)) & 0xffu);
+    const float c = 1.0f / 255.0f;
+    const float q = k * c;
+    const float r = __builtin_fmaf(-q, 255.0f, k);
+    return __builtin_fmaf(r, c, q);
+}
+
+// A pixel's colour while its load is in flight: three planar floats, or the
+// packed bytes of an 8-bit image (one dword, one register).
+template <bool U8> struct RawPx { float r, g, b; };
+template <> struct RawPx<true> { uint32_t v; };
+
+template <int NG, bool U8>
 #ifndef HQ_ASSIGN_WAVES
 #define HQ_ASSIGN_WAVES 1
 #endif
-__global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(AssignArgs a, int P) {
-    constexpr int PPT = kAssignPPT;  // pixels per thread per chunk (the pipeline runs across chunks)
+__global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(AssignArgs a, int grp0, int ngroups) {
     // [NG][kMaxK]: a fixed palette stride, so each palette's base folds into the
     // ds_read_b128 offset field and a candidate's address is its byte << 4
     __shared__ __attribute__((aligned(16))) float4 s_pal[NG * kMaxK];
     __shared__ uint32_t s_used[NG][8];
-    const int ngroups = (P + 3) / 4;
     const int w = xcd_remap(blockIdx.x, a.nblocks * ngroups);
-    const int grp = w % ngroups, blk = w / ngroups, tid = threadIdx.x;
-    const int p0 = 4 * grp, ng = min(NG, P - p0);
+    const int grp = grp0 + w % ngroups, blk = w / ngroups, tid = threadIdx.x;
+    const int p0 = 4 * grp;
     const uint8_t* lines = a.lvl2 + (int64_t)grp * a.lvl2_gstride;
     const int G2 = a.G2 > 0 ? a.G2 : 4;
-    // pixel sequence of this thread: chunk c (stride nblocks), slot j < PPT.
-    // Positions and byte offsets are 32-bit (the host keeps a shard's extended
-    // rows below 2^30 pixels), so loads and stores take the scalar-base form.
-    const uint32_t chunk = 256 * PPT, cstride = (uint32_t)a.nblocks * chunk;
-    const uint32_t qbase = (uint32_t)blk * chunk + (uint32_t)(tid >> 6) * 64 * PPT + (tid & 63);
-    auto qpos = [&](int i) {  // i-th pixel of this thread
-        return qbase + (uint32_t)(i / PPT) * cstride + 64u * (uint32_t)(i % PPT);
-    };
+    // pixel sequence of this thread: a grid stride.  Positions and byte offsets
+    // are 32-bit (the host keeps a shard's extended rows below 2^30 pixels), so
+    // loads and stores take the scalar-base form.
+    const uint32_t n_ext = (uint32_t)a.n_ext, qlast = n_ext - 1;
+    const uint32_t cstride = (uint32_t)a.nblocks * 256u;
+    const uint32_t qbase = (uint32_t)blk * 256u + (uint32_t)tid;
+    const int npx = qbase < n_ext ? (int)((n_ext - 1 - qbase) / cstride) + 1 : 0;
+    auto qpos = [&](int i) { return qbase + (uint32_t)i * cstride; };
     // Loads are unconditional (clamped addresses, results selected afterwards):
     // predicated loads sit behind branches, and the compiler's wait counting
     // then keeps at most one load in flight.
-    const uint32_t n_ext = (uint32_t)a.n_ext, qlast = n_ext - 1;
     auto at = [](const float* base, uint32_t q) {
         return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + (q << 2));
     };
-    auto load_rgb = [&](uint32_t q, float& r, float& g, float& b) {
+    auto load_rgb = [&](uint32_t q, RawPx<U8>& x) {
         const uint32_t qc = min(q, qlast);
-        r = at(a.R, qc);
-        g = at(a.G, qc);
-        b = at(a.B, qc);
+        if constexpr (U8) {
+            x.v = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(a.rgbx) + (qc << 2));
+        } else {
+            x.r = at(a.R, qc);
+            x.g = at(a.G, qc);
+            x.b = at(a.B, qc);
+        }
+    };
+    auto unpack = [&](const RawPx<U8>& x, float& r, float& g, float& b) {
+        if constexpr (U8) {
+            r = u8_unit(x.v, 0);
+            g = u8_unit(x.v, 1);
+            b = u8_unit(x.v, 2);
+        } else {
+            r = x.r;
+            g = x.g;
+            b = x.b;
+        }
     };
     auto lookup = [&](uint32_t q, float r, float g, float b, bool& inside, uint4 (&e)[NG]) {
-        inside = q < n_ext && r >= 0.f && r <= 1.f && g >= 0.f && g <= 1.f && b >= 0.f && b <= 1.f;
+        inside = U8 ? q < n_ext
+                    : q < n_ext && r >= 0.f && r <= 1.f && g >= 0.f && g <= 1.f && b >= 0.f && b <= 1.f;
         const uint4* line =
             reinterpret_cast<const uint4*>(lines + (inside ? (uint32_t)quad_cell(r, g, b, G2) : 0u) * 64u);
 #pragma unroll
@@ -160,39 +262,64 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
     // loop end serialised the whole pipeline behind an s_waitcnt vmcnt(0)).
     // Step i (parity h = i & 1): RGB(i+1) has landed -> its cell lookup goes out
     // into E[h^1] and its RGB moves to X[h^1]; RGB(i+3) goes out into the freed
-    // buffer; pixel i is resolved from E[h], X[h] while those loads fly.
-    float rb[2], gb[2], bb[2];        // RGB loads in flight: pixel i+1 / i+2 by parity
+    // buffer; pixel i is resolved from E[h], X[h] while those loads fly.  The
+    // step body loads nothing conditionally (the rare list overflows and near
+    // ties are re-resolved in a called function): a conditional load into a
+    // register that a later step overwrites made the compiler wait for every
+    // load in flight before that write.
+    RawPx<U8> rb[2];                  // RGB loads in flight: pixel i+1 / i+2 by parity
     float xr[2], xg[2], xb[2];        // RGB of pixels being looked up / resolved
     uint4 E[2][NG];
     bool in_[2];
     uint32_t qq[2];
-    load_rgb(qpos(0), xr[0], xg[0], xb[0]);
+    {
+        RawPx<U8> x0;
+        load_rgb(qpos(0), x0);
+        unpack(x0, xr[0], xg[0], xb[0]);
+    }
     qq[0] = qpos(0);
     lookup(qq[0], xr[0], xg[0], xb[0], in_[0], E[0]);
-    load_rgb(qpos(1), rb[1], gb[1], bb[1]);
-    load_rgb(qpos(2), rb[0], gb[0], bb[0]);
+    load_rgb(qpos(1), rb[1]);
+    load_rgb(qpos(2), rb[0]);
     // The palette table is filled while the first pixels' loads are in flight
     // (the fill used to come first: one more memory round trip per workgroup).
     static_assert(kMaxK == 256, "one table entry per thread and palette");
-    for (int pp = 0; pp < ng; ++pp)
-        if (tid < a.K) s_pal[pp * kMaxK + tid] = a.pal[(int64_t)(p0 + pp) * kMaxK + tid];
+    // (unconditional: entries past K hold a copy of colour K-1 and are never
+    // listed.  A fill skipped by some threads left the prologue's RGB loads in
+    // flight on that path, and the loop head's wait, which serves both paths,
+    // then drained every lookup in flight on each step.)
+#pragma unroll
+    for (int pp = 0; pp < NG; ++pp)
+        s_pal[pp * kMaxK + tid] = a.pal[(int64_t)(p0 + pp) * kMaxK + min(tid, a.K - 1)];
     if (tid < 8 * NG) s_used[tid >> 3][tid & 7] = 0;
     __syncthreads();
     uint8_t* idx_base[NG];  // each palette's index image
-#pragma unroll
-    for (int pp = 0; pp < NG; ++pp) idx_base[pp] = a.idx + (int64_t)(p0 + min(pp, ng - 1)) * a.idx_pitch;
     bool exh_pal[NG];
 #pragma unroll
-    for (int pp = 0; pp < NG; ++pp) exh_pal[pp] = pp >= ng || a.pflags[p0 + min(pp, ng - 1)] != 0 || a.G2 == 0;
+    for (int pp = 0; pp < NG; ++pp) {
+        idx_base[pp] = a.idx + (int64_t)(p0 + pp) * a.idx_pitch;
+        exh_pal[pp] = a.pflags[p0 + pp] != 0 || a.G2 == 0;
+    }
     auto resolve = [&](int h) {
         const uint32_t q = qq[h];
+        int kk[NG];
+#if HQ_ASSIGN_JOINT
+        argmin_group<NG>(xr[h], xg[h], xb[h], E[h], in_[h], exh_pal, s_pal, a.lvl1, a.lvl1_pitch, p0, G2,
+                         a.K, kk);
+#else
 #pragma unroll
         for (int pp = 0; pp < NG; ++pp) {
-            if (pp >= ng) break;
-            const int pq = p0 + pp;
-            const int k = argmin_from_entry(xr[h], xg[h], xb[h], E[h][pp], in_[h] && !exh_pal[pp],
-                                            s_pal + pp * kMaxK, a.lvl1 + (int64_t)pq * a.lvl1_pitch,
-                                            G2, a.K);
+            const uint4 e1[1] = {E[h][pp]};
+            const bool x1[1] = {exh_pal[pp]};
+            int k1[1];
+            argmin_group<1>(xr[h], xg[h], xb[h], e1, in_[h], x1, s_pal + pp * kMaxK, a.lvl1, a.lvl1_pitch,
+                            p0 + pp, G2, a.K, k1);
+            kk[pp] = k1[0];
+        }
+#endif
+#pragma unroll
+        for (int pp = 0; pp < NG; ++pp) {
+            const int k = kk[pp];
             // non-temporal: streamed out during the kernel rather than left dirty
             // in L2 for the kernel boundary to write back (67 MB per population;
             // ~0.5-1% per evaluation)
@@ -204,17 +331,17 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
     auto step = [&](int i, int h) {  // h == i & 1, a compile-time constant at each call
         const int n = h ^ 1;
         qq[n] = qpos(i + 1);
-        xr[n] = rb[n]; xg[n] = gb[n]; xb[n] = bb[n];  // RGB(i+1): landed, needed now anyway
+        unpack(rb[n], xr[n], xg[n], xb[n]);  // RGB(i+1): landed, needed now anyway
         lookup(qq[n], xr[n], xg[n], xb[n], in_[n], E[n]);
-        load_rgb(qpos(i + 3), rb[n], gb[n], bb[n]);
+        load_rgb(qpos(i + 3), rb[n]);
         resolve(h);
     };
-    for (int i = 0;; i += 2) {
-        if (qpos(i) >= n_ext) break;
+    int i = 0;
+    for (; i + 2 <= npx; i += 2) {
         step(i, 0);
-        if (qpos(i + 1) >= n_ext) break;
         step(i + 1, 1);
     }
+    if (i < npx) step(i, 0);
     __syncthreads();
     // the workgroup's used bits into the palette's 8 words (OR is order-free:
     // the result does not depend on which workgroup gets there first).  A
@@ -222,7 +349,7 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
     // after the first workgroups every colour of a 256-colour palette is
     // usually in, and 2,000-4,000 workgroups' atomics on the same 32 words
     // serialised at the end of a short (row-block shard) launch.
-    if (tid < 8 * ng) {
+    if (tid < 8 * NG) {
         const uint32_t m = s_used[tid >> 3][tid & 7];
         uint32_t* gw = &a.used_glob[(p0 + (tid >> 3)) * 8 + (tid & 7)];
         const uint32_t seen = __hip_atomic_load(gw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -231,17 +358,50 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
 }
 
 // ----------------------------------------------------------------------------
-// Launcher
+// Launcher: the full groups of 4 palettes in one launch, a last group of
+// P mod 4 in a second (the profiling events, when set, bracket both).
 // ----------------------------------------------------------------------------
-hipError_t launch_assign(const AssignArgs& a, int P, hipStream_t s) {
-    const unsigned grid = (unsigned)(a.nblocks * ((P + 3) / 4));
-    switch (P) {
-    case 1: HQ_LAUNCH(assign_pipe_kernel<1>, dim3(grid), dim3(256), 0, s, a, P); break;
-    case 2: HQ_LAUNCH(assign_pipe_kernel<2>, dim3(grid), dim3(256), 0, s, a, P); break;
-    case 3: HQ_LAUNCH(assign_pipe_kernel<3>, dim3(grid), dim3(256), 0, s, a, P); break;
-    default: HQ_LAUNCH(assign_pipe_kernel<4>, dim3(grid), dim3(256), 0, s, a, P); break;
+template <bool U8>
+void launch_assign_t(const AssignArgs& a, int P, hipStream_t s) {
+    const int full = P / 4, rest = P % 4;
+    const hipEvent_t ev0 = t_ev_start, ev1 = t_ev_stop;
+    if (full > 0) {
+        if (rest) t_ev_stop = nullptr;
+        HQ_LAUNCH((assign_pipe_kernel<4, U8>), dim3((unsigned)(a.nblocks * full)), dim3(256), 0, s, a, 0, full);
+        t_ev_stop = ev1;
+        if (rest) t_ev_start = nullptr;
     }
+    switch (rest) {
+    case 1: HQ_LAUNCH((assign_pipe_kernel<1, U8>), dim3((unsigned)a.nblocks), dim3(256), 0, s, a, full, 1); break;
+    case 2: HQ_LAUNCH((assign_pipe_kernel<2, U8>), dim3((unsigned)a.nblocks), dim3(256), 0, s, a, full, 1); break;
+    case 3: HQ_LAUNCH((assign_pipe_kernel<3, U8>), dim3((unsigned)a.nblocks), dim3(256), 0, s, a, full, 1); break;
+    default: break;
+    }
+    t_ev_start = ev0;
+}
+
+hipError_t launch_assign(const AssignArgs& a, int P, hipStream_t s) {
+    if (a.rgbx)
+        launch_assign_t<true>(a, P, s);
+    else
+        launch_assign_t<false>(a, P, s);
     return hipGetLastError();
+}
+
+// Resident workgroups per CU of assign_pipe_kernel<NG> (the auto size of one
+// grid-stride round; the packed and planar forms take the larger register
+// count); 0 if the query fails.
+int assign_residency(int NG) {
+    auto q = [](auto kern) {
+        int n = 0;
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, 256, 0) == hipSuccess ? n : 0;
+    };
+    switch (NG) {
+    case 1: return std::min(q(assign_pipe_kernel<1, false>), q(assign_pipe_kernel<1, true>));
+    case 2: return std::min(q(assign_pipe_kernel<2, false>), q(assign_pipe_kernel<2, true>));
+    case 3: return std::min(q(assign_pipe_kernel<3, false>), q(assign_pipe_kernel<3, true>));
+    default: return std::min(q(assign_pipe_kernel<4, false>), q(assign_pipe_kernel<4, true>));
+    }
 }
 
 }  // namespace hq

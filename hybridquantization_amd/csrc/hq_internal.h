@@ -47,14 +47,10 @@ struct PaletteArgs {
     int K;
 };
 
-#ifndef HQ_ASSIGN_PPT
-#define HQ_ASSIGN_PPT 1
-#endif
-constexpr int kAssignPPT = HQ_ASSIGN_PPT;  // assign: pixels per thread per 256-thread chunk.  1, with
-                                           // one resident round of workgroups (6 per CU), makes the
-                                           // pixel sequence a grid stride: every thread gets the same
-                                           // number of pixels +-1 (512-row shard 0.1306 -> 0.1261 ms per
-                                           // step vs 4 per chunk at 16 per CU; 4096^2 unchanged)
+// assign: one pixel per thread per 256-thread chunk, with one resident round
+// of workgroups, makes each thread's pixel sequence a grid stride: every thread
+// gets the same number of pixels +-1 (512-row shard 0.1306 -> 0.1261 ms per
+// step vs 4 pixels per chunk at 16 workgroups per CU; 4096^2 unchanged).
 constexpr int kSaMaxP = 64;       // device-resident SWASA: largest population
 constexpr int kFoldMaxP = 8;      // largest population whose accept step folds the finalize
 
@@ -111,6 +107,8 @@ struct AssignArgs {
     const float* R;         // planar, n_ext floats (extended rows)
     const float* G;
     const float* B;
+    const uint32_t* rgbx;   // packed 8-bit R,G,B (byte 0..2) of an image whose channels are all
+                            // k/255 (exactly, IM:100's int-RGB source), else null
     const float4* pal;      // [P][256]
     const int* pflags;
     const uint8_t* lvl1;

@@ -24,6 +24,7 @@ hipError_t launch_sa_step(const SaArgs&, hipStream_t);
 void set_launch_events(hipEvent_t start, hipEvent_t stop);
 hipError_t launch_build_grid(const GridArgs&, int P, hipStream_t);
 hipError_t launch_assign(const AssignArgs&, int P, hipStream_t);
+int assign_residency(int P);
 void fast_tile_dims(int W, int own_rows, int tile_rows, int* tiles_x, int* ntiles);
 void opp2xyz_over_illum(const float inv_illum[3], float m[9]);
 hipError_t launch_cost_fast(const CostArgs&, int P, int de, bool trim, int tile_rows, int HB, hipStream_t);
@@ -103,6 +104,8 @@ struct hq_ctx {
     Geom g{};
     float illum[3] = {0.95047f, 1.0f, 1.0883f};
     DevBuf d_R, d_G, d_B;          // planar, extended rows (n_ext, padded to 4)
+    DevBuf d_rgbx;                 // packed 8-bit copy of R,G,B when every channel is k/255
+    bool img_u8 = false;
     DevBuf d_labL, d_labA, d_labB;  // planar LabRef, owned rows, lab_pitch
 
     // population work buffers
@@ -120,9 +123,11 @@ struct hq_ctx {
     int G2 = 32;           // argmin grid resolution (0 = exhaustive)
     int cost_variant = 0;  // 0 tiled (default), 1 generic two-pass
     int cost_rows = 16;    // fast path tiles: 16 x 128 (cost16w_kernel) or 8 x 108 (cost_mfma_kernel)
-    int assign_blocks_per_cu = 0;  // 0 = auto: assign_pipe_kernel<NG>'s residency (NG = 4: 78 VGPRs,
-                                   // 6 waves per SIMD; NG = 3: 7; NG <= 2: 8), one round of
-                                   // workgroups, each thread a grid-stride pixel sequence
+    int assign_blocks_per_cu = 0;  // 0 = auto: assign_pipe_kernel<NG>'s residency (the occupancy
+                                   // query, assign_res[NG]), one round of workgroups, each
+                                   // thread a grid-stride pixel sequence
+    int assign_res[5] = {0, 0, 0, 0, 0};
+    int img_u8_path = 1;   // assign reads the packed 8-bit image when there is one (option 'img_u8')
     int shard_solo = 0;    // experiment: a sharded search without a communicator (per-rank timing)
     int sa_device = 1;     // hq_search_*: 1 = SWASA iterations resident on the device (no host
                            // round trip per iteration), 0 = host-driven (one eval call each)
@@ -278,6 +283,36 @@ int set_image_common(hq_ctx* c, const std::vector<float>& R, const std::vector<f
     HIP_TRY(c, hipMemcpyAsync(c->d_R.p, R.data(), plane, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, hipMemcpyAsync(c->d_G.p, G.data(), plane, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, hipMemcpyAsync(c->d_B.p, B.data(), plane, hipMemcpyHostToDevice, c->stream));
+    // An image whose channels are all exactly k/255 (the reference's int-RGB
+    // source, IM:100) is also kept as packed bytes: assign reads 4 B per pixel
+    // instead of 12 and rebuilds k/255 exactly (u8_unit, hq_assign.hip).
+    {
+        std::vector<uint32_t> px((size_t)round_up(g.n_ext, 4), 0u);
+        float unit[256];
+        for (int k = 0; k < 256; ++k) unit[k] = (float)k / 255.0f;
+        bool u8 = true;
+        const std::vector<float>* ch[3] = {&R, &G, &B};
+        for (int64_t i = 0; i < g.n_ext && u8; ++i) {
+            uint32_t v = 0;
+            for (int j = 0; j < 3; ++j) {
+                const float f = (*ch[j])[i];
+                if (!(f >= 0.f && f <= 1.f)) { u8 = false; break; }
+                const int k = (int)std::lround(f * 255.0f);
+                if (std::memcmp(&unit[k], &f, 4) != 0) { u8 = false; break; }
+                v |= (uint32_t)k << (8 * j);
+            }
+            px[i] = v;
+        }
+        c->img_u8 = u8;
+        if (u8) {
+            HIP_TRY(c, c->d_rgbx.ensure(sizeof(uint32_t) * px.size()));
+            HIP_TRY(c, hipMemcpyAsync(c->d_rgbx.p, px.data(), sizeof(uint32_t) * px.size(),
+                                      hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(c, hipStreamSynchronize(c->stream));
+        } else {
+            c->d_rgbx.release();
+        }
+    }
     if (illum) std::memcpy(c->illum, illum, sizeof c->illum);
     const int own = g.r1 - g.r0;
     const size_t lplane = sizeof(float) * (size_t)g.lab_pitch * std::max(own, 1);
@@ -320,15 +355,17 @@ int check_geom_args(hq_ctx* c, int w, int h, int r0, int r1) {
 }
 
 // Assign workgroups per palette group: assign_blocks_per_cu per CU, but no more
-// than pixel chunks (256 threads x kAssignPPT pixels): idle workgroups still fill LDS,
+// than pixel chunks (256 pixels, one per thread): idle workgroups still fill LDS,
 // and after the XCD relabelling they would all sit on the last XCDs (a 512-row
 // shard ran assign on half the chip: 0.071 vs 0.053 ms).  (Evening out the
 // chunks per workgroup instead -- 1064 workgroups of 2 for 2128 chunks -- was
 // slower than 2048 with 80 of them taking a second chunk.)
 int assign_blocks(const hq_ctx* c, int P) {
-    const int64_t chunk = 256 * kAssignPPT;
+    const int64_t chunk = 256;
     const int ng = std::min(P, 4);
-    const int per_cu = c->assign_blocks_per_cu > 0 ? c->assign_blocks_per_cu : (ng >= 4 ? 6 : ng == 3 ? 7 : 8);
+    const int per_cu = c->assign_blocks_per_cu > 0 ? c->assign_blocks_per_cu
+                       : c->assign_res[ng] > 0     ? c->assign_res[ng]
+                                                   : 4;
     const int64_t nblocks = (int64_t)c->num_cu * per_cu;
     return (int)std::max<int64_t>(1, std::min<int64_t>(nblocks, (c->g.n_ext + chunk - 1) / chunk));
 }
@@ -480,7 +517,8 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
         HIP_TRY(c, hipMemsetAsync(c->d_used_mask.p, 0, sizeof(uint32_t) * 8 * (size_t)P, s));
     }
     const int nblocks = assign_blocks(c, P);
-    const AssignArgs aa{c->d_R.as<float>(), c->d_G.as<float>(), c->d_B.as<float>(), c->d_pal.as<float4>(),
+    const AssignArgs aa{c->d_R.as<float>(), c->d_G.as<float>(), c->d_B.as<float>(),
+                        c->img_u8 && c->img_u8_path ? c->d_rgbx.as<uint32_t>() : nullptr, c->d_pal.as<float4>(),
                         c->d_pflags.as<int>(), c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(),
                         c->d_idx.as<uint8_t>(), c->d_used_mask.as<uint32_t>(), g.n_ext, g.idx_pitch,
                         ga.lvl1_pitch, ga.lvl2_gstride, K, c->G2, nblocks};
@@ -783,6 +821,7 @@ int hq_create(int device, int delta_e_type, hq_ctx** out) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         c->num_cu = prop.multiProcessorCount;
+    for (int ng = 1; ng <= 4; ++ng) c->assign_res[ng] = assign_residency(ng);
     for (auto& e : c->ev) (void)hipEventCreate(&e);
     *out = c;
     return HQ_OK;
@@ -793,7 +832,7 @@ void hq_destroy(hq_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) (void)ncclCommDestroy(c->comm);
-    for (DevBuf* b : {&c->d_k1, &c->d_k2, &c->d_k3, &c->d_absk3, &c->d_R, &c->d_G, &c->d_B,
+    for (DevBuf* b : {&c->d_k1, &c->d_k2, &c->d_k3, &c->d_absk3, &c->d_R, &c->d_G, &c->d_B, &c->d_rgbx,
                       &c->d_labL, &c->d_labA, &c->d_labB, &c->d_pal_in, &c->d_pal, &c->d_opp, &c->d_opp16,
                       &c->d_dup, &c->d_pflags, &c->d_lvl1, &c->d_lvl2, &c->d_idx,
                       &c->d_used_mask, &c->d_partial, &c->d_out, &c->d_gen_t, &c->d_taps,
@@ -1232,6 +1271,8 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
         c->sa_device = value != 0;
     } else if (!std::strcmp(name, "shard_solo")) {
         c->shard_solo = value != 0;
+    } else if (!std::strcmp(name, "img_u8")) {
+        c->img_u8_path = value != 0;
     } else if (!std::strcmp(name, "assign_blocks_per_cu")) {
         if (value < 0 || value > 64) return fail(c, HQ_ERR_ARG, "assign_blocks_per_cu in [0,64] (0 = auto)");
         c->assign_blocks_per_cu = value;

@@ -658,6 +658,39 @@ def test_assign_workgroup_count_invariance(gpu, filt, w, h, P):
     m.close()
 
 
+@pytest.mark.parametrize("off_lattice", [False, True])
+def test_packed_image_path(gpu, filt, off_lattice):
+    """An image whose channels are all k/255 (the reference's int-RGB source)
+    is also kept as packed bytes, and assign reads those (4 B per pixel instead
+    of 12, k/255 rebuilt by u8_unit); option img_u8 = 0 forces the planar floats.
+    Both give the same indices, used flags and costs, and the indices are the
+    exhaustive oracle argmin.  An image with one value off the k/255 lattice is
+    kept planar only (both settings then take the same path).  P = 5 runs a
+    group of 4 and a group of 1 (two assign launches)."""
+    w, h, K, P = 301, 203, 256, 5
+    R, G, B = o.synthetic_image(w, h, seed=31)
+    if off_lattice:
+        R = R.copy()
+        R[7] = np.float32(0.5)
+        G[1000] = np.nextafter(G[1000], np.float32(2))
+    m = _planar_ctx(gpu, R, G, B, w, h, filt.illum)
+    pals = np.stack([o.synthetic_palette(K, 60 + p) for p in range(P)])
+    pals[4, 17, :3] = [R[9], G[9], B[9]]  # a colour on a pixel
+    c1, used1 = m.computeQuantizationErrorPopulation(pals.reshape(P, -1), 2.0, return_used=True)
+    idx1 = [m.getIndices(p) for p in range(P)]
+    m.setOption("img_u8", 0)
+    c0, used0 = m.computeQuantizationErrorPopulation(pals.reshape(P, -1), 2.0, return_used=True)
+    np.testing.assert_array_equal(c0, c1)
+    np.testing.assert_array_equal(used0, used1)
+    px = np.stack([R, G, B, np.zeros_like(R)], 1)
+    for p in range(P):
+        np.testing.assert_array_equal(m.getIndices(p), idx1[p])
+        ref_idx, ref_used = c_oracle.assign(px, pals[p])
+        np.testing.assert_array_equal(idx1[p], ref_idx.astype(np.uint8), err_msg=f"palette {p}")
+        np.testing.assert_array_equal(used1[p], ref_used)
+    m.close()
+
+
 def test_full_size_properties(gpu, filt):
     w = h = 4096
     K = 256
