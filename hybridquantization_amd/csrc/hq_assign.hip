@@ -89,6 +89,9 @@ __device__ __forceinline__ void argmin_group(float r, float g, float b, const ui
     bool near[NG];
 #pragma unroll
     for (int q = 0; q < NG; ++q) near[q] = false;
+#ifdef HQ_ABL_NOLOOP  // timing ablation (wrong results): no candidate walk
+    maxc = 1;
+#endif
     if (__any(maxc > 1)) {
         const f32x2 rg = {r, g};
         const char* base = reinterpret_cast<const char*>(s_pal);
@@ -252,10 +255,19 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
     auto lookup = [&](uint32_t q, float r, float g, float b, bool& inside, uint4 (&e)[NG]) {
         inside = U8 ? q < n_ext
                     : q < n_ext && r >= 0.f && r <= 1.f && g >= 0.f && g <= 1.f && b >= 0.f && b <= 1.f;
+#ifdef HQ_ABL_HASHLOOKUP  // timing ablation (wrong results): a random line, independent of the RGB
+        const uint4* line = reinterpret_cast<const uint4*>(lines + ((q * 2654435761u) >> 17) * 64u);
+#else
         const uint4* line =
             reinterpret_cast<const uint4*>(lines + (inside ? (uint32_t)quad_cell(r, g, b, G2) : 0u) * 64u);
+#endif
 #pragma unroll
         for (int pp = 0; pp < NG; ++pp) e[pp] = line[pp];  // selected by the `listed` flag at use
+#ifdef HQ_ABL_NOLOOKUP  // timing ablation (wrong results): one fixed entry, lists of 3-4
+#pragma unroll
+        for (int pp = 0; pp < NG; ++pp)
+            e[pp] = make_uint4(0x03020103u + (q & 1u), 0x07060504u, 0x0b0a0908u, 0x0f0e0d0cu);
+#endif
     };
     // Pipeline, unrolled by two so every buffer has a fixed register set (a
     // register copy of an in-flight load waits for it: rotating buffers at the

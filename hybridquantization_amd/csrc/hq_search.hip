@@ -174,7 +174,11 @@ __device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared
     double fold_acc[kFoldMaxP];
     uint32_t fold_word = 0u;
     if (a.accept && a.fold) {  // the finalize's work, folded (P <= kFoldMaxP)
-        if (tid < P) s.err_in[tid] = a.err_in[tid];
+        // the small inputs are loaded first and stored to LDS after the partials'
+        // loads are out: an LDS store of a just-loaded value waits for it, and
+        // the wait (in-order counters) held back every partial load behind it
+        const double ein = tid < P ? a.err_in[tid] : 0.0;
+        if (tid < 8 * P) fold_word = a.used_glob[tid];
         if (P <= 4) {
             double acc4[4];
             thread_partial_sums<4, 8>(a.partial, a.ntiles, P, acc4);
@@ -183,7 +187,7 @@ __device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared
         } else {
             thread_partial_sums<kFoldMaxP, 4>(a.partial, a.ntiles, P, fold_acc);
         }
-        if (tid < 8 * P) fold_word = a.used_glob[tid];
+        if (tid < P) s.err_in[tid] = ein;
     } else if (a.accept) {
         if (tid < P) {
             s.sum[tid] = a.out[(int64_t)tid * (1 + K)];
