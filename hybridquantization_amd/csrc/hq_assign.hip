@@ -213,7 +213,11 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
     __shared__ __attribute__((aligned(16))) float4 s_pal[NG * kMaxK];
     __shared__ uint32_t s_used[NG][8];
     const int w = xcd_remap(blockIdx.x, a.nblocks * ngroups);
-    const int grp = grp0 + w % ngroups, blk = w / ngroups, tid = threadIdx.x;
+    // group-major: after the relabelling an XCD's contiguous range of
+    // workgroups covers one or two groups, so its L2 holds those groups' level-2
+    // tables (2 MiB each at G2 = 32) rather than every group's (P = 64: 32 MiB
+    // against a 4 MiB L2; the lookups then came from the Infinity Cache)
+    const int grp = grp0 + w / a.nblocks, blk = w % a.nblocks, tid = threadIdx.x;
     const int p0 = 4 * grp;
     const uint8_t* lines = a.lvl2 + (int64_t)grp * a.lvl2_gstride;
     const int G2 = a.G2 > 0 ? a.G2 : 4;
