@@ -218,6 +218,10 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
     // tables (2 MiB each at G2 = 32) rather than every group's (P = 64: 32 MiB
     // against a 4 MiB L2; the lookups then came from the Infinity Cache)
     const int grp = grp0 + w / a.nblocks, blk = w % a.nblocks, tid = threadIdx.x;
+#ifdef HQ_ASSIGN_TIMING  // diagnostic build: per-workgroup stamps (wall_clock64, 100 MHz)
+    const uint64_t t_start = wall_clock64();
+    uint64_t t_fill = 0, t_loop = 0;
+#endif
     const int p0 = 4 * grp;
     const uint8_t* lines = a.lvl2 + (int64_t)grp * a.lvl2_gstride;
     const int G2 = a.G2 > 0 ? a.G2 : 4;
@@ -309,6 +313,9 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
         s_pal[pp * kMaxK + tid] = a.pal[(int64_t)(p0 + pp) * kMaxK + min(tid, a.K - 1)];
     if (tid < 8 * NG) s_used[tid >> 3][tid & 7] = 0;
     __syncthreads();
+#ifdef HQ_ASSIGN_TIMING
+    t_fill = wall_clock64();
+#endif
     uint8_t* idx_base[NG];  // each palette's index image
     bool exh_pal[NG];
 #pragma unroll
@@ -358,6 +365,9 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
         step(i + 1, 1);
     }
     if (i < npx) step(i, 0);
+#ifdef HQ_ASSIGN_TIMING
+    t_loop = wall_clock64();
+#endif
     __syncthreads();
     // the workgroup's used bits into the palette's 8 words (OR is order-free:
     // the result does not depend on which workgroup gets there first).  A
@@ -371,6 +381,11 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
         const uint32_t seen = __hip_atomic_load(gw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (m & ~seen) atomicOr(gw, m);
     }
+#ifdef HQ_ASSIGN_TIMING
+    if (tid == 0)
+        printf("ASG_T %d %d %llu %llu %llu %llu\n", grp, blk, (unsigned long long)t_start,
+               (unsigned long long)t_fill, (unsigned long long)t_loop, (unsigned long long)wall_clock64());
+#endif
 }
 
 // ----------------------------------------------------------------------------
