@@ -203,6 +203,12 @@ __device__ __forceinline__ float u8_unit(uint32_t v, int j) {
 template <bool U8> struct RawPx { float r, g, b; };
 template <> struct RawPx<true> { uint32_t v; };
 
+#ifdef HQ_ASSIGN_TIMING
+constexpr int kAsgStamps = 16384;
+// per workgroup: start, fill barrier, end, then each wave's loop end
+__device__ unsigned long long g_asg_t[kAsgStamps][8];
+#endif
+
 template <int NG, bool U8>
 #ifndef HQ_ASSIGN_WAVES
 #define HQ_ASSIGN_WAVES 1
@@ -382,9 +388,12 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
         if (m & ~seen) atomicOr(gw, m);
     }
 #ifdef HQ_ASSIGN_TIMING
-    if (tid == 0)
-        printf("ASG_T %d %d %llu %llu %llu %llu\n", grp, blk, (unsigned long long)t_start,
-               (unsigned long long)t_fill, (unsigned long long)t_loop, (unsigned long long)wall_clock64());
+    if ((tid & 63) == 0 && w < kAsgStamps) g_asg_t[w][4 + (tid >> 6)] = t_loop;
+    if (tid == 0 && w < kAsgStamps) {
+        g_asg_t[w][0] = t_start;
+        g_asg_t[w][1] = t_fill;
+        g_asg_t[w][2] = wall_clock64();
+    }
 #endif
 }
 
@@ -436,3 +445,11 @@ int assign_residency(int NG) {
 }
 
 }  // namespace hq
+
+#ifdef HQ_ASSIGN_TIMING
+// diagnostic build only: the last assign launch's workgroup stamps (wall_clock64 ticks)
+extern "C" int hq_debug_assign_stamps(unsigned long long* out, int n) {
+    n = n < hq::kAsgStamps ? n : hq::kAsgStamps;
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(hq::g_asg_t), sizeof(unsigned long long) * 8 * (size_t)n);
+}
+#endif

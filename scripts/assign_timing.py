@@ -1,7 +1,8 @@
 """Diagnostic: per-workgroup stamps of assign_pipe_kernel (a library built with
--DHQ_ASSIGN_TIMING, HQ_LIB_PATH) over a few evaluations at GT_SIZE^2 (rows
-GT_ROWS of it, default all), K = 256, P = GT_P: the dispatch spread, the time
-to the table fill barrier, the pixel loop and the end, of the last evaluation."""
+-DHQ_ASSIGN_TIMING, HQ_LIB_PATH; stamps kept in device memory, read back by
+hq_debug_assign_stamps) over a few evaluations at GT_SIZE^2 (rows GT_ROWS of
+it, default all), K = 256, P = GT_P: the dispatch spread, the time to the table
+fill barrier, the pixel loop and the end, of the last evaluation."""
 import os
 import subprocess
 import sys
@@ -9,6 +10,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if len(sys.argv) > 1 and sys.argv[1] == "run":
     sys.path.insert(0, ROOT)
+    import ctypes as C
     import numpy as np
     import bench
     import hybridquantization_amd as hq
@@ -26,13 +28,22 @@ if len(sys.argv) > 1 and sys.argv[1] == "run":
     for it in range(3):
         pal = rng.random((P, 256, 4), dtype=np.float32)
         pal[..., 3] = 0
-        print("EVAL", it, flush=True)
         m.computeQuantizationErrorPopulation(pal.reshape(P, -1), 2.0)
+    buf = np.zeros((16384, 8), np.uint64)
+    lib.hq_debug_assign_stamps.argtypes = [C.c_void_p, C.c_int]
+    lib.hq_debug_assign_stamps(buf.ctypes.data, 16384)
     m.close()
+    n = int((buf[:, 2] > 0).sum())
+    for r in buf[:n]:
+        print("ASG_T 0 0 " + " ".join(str(int(x)) for x in r))
     sys.exit(0)
-out = subprocess.run([sys.executable, __file__, "run"], capture_output=True, text=True, timeout=300).stdout
-last = [l.split() for l in out.split("EVAL")[-1].splitlines() if l.startswith("ASG_T")]
-st, fi, lo, en = ([int(x[k]) for x in last] for k in (3, 4, 5, 6))
+res = subprocess.run([sys.executable, __file__, "run"], capture_output=True, text=True, timeout=300)
+last = [l.split() for l in res.stdout.splitlines() if l.startswith("ASG_T")]
+if not last:
+    sys.exit("no stamps:\n" + res.stderr[-2000:])
+st, fi, en = ([int(x[k]) for x in last] for k in (3, 4, 5))
+wr = [[int(x[k]) for k in (6, 7, 8, 9)] for x in last]  # each wave's loop end (0: not stamped)
+wl = [[y for y in w if y] for w in wr]
 t0 = min(st)
 
 
@@ -42,8 +53,21 @@ def q(v):
 
 
 print(f"{len(last)} workgroups; end of the last {(max(en) - t0) / 100:.2f} us after the first start")
-print("start     ", q([(s - t0) / 100 for s in st]))
-print("to fill   ", q([(f - s) / 100 for s, f in zip(st, fi)]))
-print("loop      ", q([(l - f) / 100 for f, l in zip(fi, lo)]))
-print("flush     ", q([(e - l) / 100 for l, e in zip(lo, en)]))
-print("end       ", q([(e - t0) / 100 for e in en]))
+print("start            ", q([(s - t0) / 100 for s in st]))
+print("to fill          ", q([(f - s) / 100 for s, f in zip(st, fi)]))
+print("wave loops       ", q([(x - f) / 100 for f, w in zip(fi, wl) for x in w]))
+print("wave spread in wg", q([(max(w) - min(w)) / 100 for w in wl if w]))
+print("end              ", q([(e - t0) / 100 for e in en]))
+n = len(last)
+per_x = n // 8
+for x in range(8):  # XCD x holds workgroups [x n/8, (x+1) n/8) after xcd_remap
+    sl = range(x * per_x, (x + 1) * per_x)
+    print(f"xcd {x}: wave loops", q([(y - fi[i]) / 100 for i in sl for y in wl[i]]),
+          " end", q([(en[i] - t0) / 100 for i in sl]))
+for k in range(4):  # wave index in the workgroup
+    v = [(wr[i][k] - fi[i]) / 100 for i in range(n) if wr[i][k]]
+    print(f"wave {k}: {len(v)} stamped", q(v) if v else "")
+# by dispatch order within an XCD (position s of the workgroup in its XCD's range)
+for part in range(4):
+    sl = [i for i in range(n) if (i % per_x) * 4 // per_x == part]
+    print(f"dispatch quarter {part}:", q([(y - fi[i]) / 100 for i in sl for y in wl[i]]))
