@@ -381,9 +381,14 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
     // after the first workgroups every colour of a 256-colour palette is
     // usually in, and 2,000-4,000 workgroups' atomics on the same 32 words
     // serialised at the end of a short (row-block shard) launch.
+#ifdef HQ_ABL_NOUSED  // timing ablation (wrong results): no used-bit flush
+    if (false) {
+#else
     if (tid < 8 * NG) {
+#endif
         const uint32_t m = s_used[tid >> 3][tid & 7];
-        uint32_t* gw = &a.used_glob[(p0 + (tid >> 3)) * 8 + (tid & 7)];
+        uint32_t* gw = &a.used_glob[(blockIdx.x & (kUsedSlots - 1)) * a.used_stride + (p0 + (tid >> 3)) * 8 +
+                                    (tid & 7)];
         const uint32_t seen = __hip_atomic_load(gw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (m & ~seen) atomicOr(gw, m);
     }

@@ -51,7 +51,13 @@ struct PaletteArgs {
 // of workgroups, makes each thread's pixel sequence a grid stride: every thread
 // gets the same number of pixels +-1 (512-row shard 0.1306 -> 0.1261 ms per
 // step vs 4 pixels per chunk at 16 workgroups per CU; 4096^2 unchanged).
-constexpr int kSaMaxP = 64;       // device-resident SWASA: largest population
+constexpr int kSaMaxP = 64;
+// Used-colour bits are kept in kUsedSlots copies, used_stride(P) words apart
+// (256-B multiples): assign's workgroups OR theirs into copy blockIdx & 7, the
+// readers OR the copies.  One copy took every workgroup's atomic at the end of
+// the launch (C2, P = 1: 2048 workgroups on one 32-B word set, +14 us).
+constexpr int kUsedSlots = 8;
+inline int used_stride(int P) { return (P * 8 + 63) / 64 * 64; }       // device-resident SWASA: largest population
 constexpr int kFoldMaxP = 8;      // largest population whose accept step folds the finalize
 
 // sa_step_kernel: one accept + generate step of the device-resident SWASA search.
@@ -74,7 +80,8 @@ struct SaArgs {
     // kernel's partials and the used bits itself (finalize's order), so no
     // finalize launch sits between the cost kernel and this step
     const double* partial;  // [P][ntiles]
-    const uint32_t* used_glob;  // [P][8]
+    const uint32_t* used_glob;  // [kUsedSlots][used_stride]: [P][8] per slot
+    int used_stride;
     int ntiles;
     int fold;
     double n_total;         // pixels of the whole image
@@ -96,7 +103,8 @@ struct GridArgs {
     const int* pflags;
     uint8_t* lvl1;          // [P][G1^3][32]
     uint8_t* lvl2;          // [ceil(P/4)][G2^3][4][16]: 4 palettes' entries per 64-B line
-    uint32_t* used_glob;    // [P][8] used-colour bits, zeroed here for the assign that follows
+    uint32_t* used_glob;    // [kUsedSlots][used_stride] used-colour bits, zeroed here for the assign
+    int used_stride;        // that follows
     int K;
     int G1;                 // level-1 resolution (G2 / 4)
     int64_t lvl1_pitch;     // bytes per palette
@@ -114,7 +122,8 @@ struct AssignArgs {
     const uint8_t* lvl1;
     const uint8_t* lvl2;
     uint8_t* idx;           // [P][idx_pitch]
-    uint32_t* used_glob;    // [P][8] used-colour bits: every workgroup ORs its own in (atomics)
+    uint32_t* used_glob;    // [kUsedSlots][used_stride]: [P][8] used-colour bits per slot, every
+    int used_stride;        // workgroup ORs its own into slot blockIdx & 7 (atomics)
     int64_t n_ext;
     int64_t idx_pitch;
     int64_t lvl1_pitch;     // bytes per palette
@@ -143,7 +152,8 @@ struct CostArgs {
 
 struct FinalizeArgs {
     const double* partial;  // [P][ntiles]
-    const uint32_t* used_glob;  // [P][8] used-colour bits (assign)
+    const uint32_t* used_glob;  // [kUsedSlots][used_stride] used-colour bits (assign)
+    int used_stride;
     double* out;            // [P][1+K]
     int ntiles;
     int K;

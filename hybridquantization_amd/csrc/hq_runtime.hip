@@ -360,8 +360,16 @@ int check_geom_args(hq_ctx* c, int w, int h, int r0, int r1) {
 // shard ran assign on half the chip: 0.071 vs 0.053 ms).  (Evening out the
 // chunks per workgroup instead -- 1064 workgroups of 2 for 2128 chunks -- was
 // slower than 2048 with 80 of them taking a second chunk.)
+#ifndef HQ_ASSIGN_MINPX
+#define HQ_ASSIGN_MINPX 6
+#endif
 int assign_blocks(const hq_ctx* c, int P) {
-    const int64_t chunk = 256;
+    // at least HQ_ASSIGN_MINPX pixels per thread: a launch's fixed part (table
+    // fill, pipeline start, the used-bit flush) is paid per workgroup (C2,
+    // 1024^2 P = 1: 2048 workgroups of 2 pixels per thread took 14 us, 1045 of 4
+    // took 12.3, 523 of 8 took 8.5; the 512-row shard, 5.5 per thread at 1536
+    // workgroups, slowed from 43 to 46 us at 8)
+    const int64_t chunk = 256 * HQ_ASSIGN_MINPX;
     const int ng = std::min(P, 4);
     const int per_cu = c->assign_blocks_per_cu > 0 ? c->assign_blocks_per_cu
                        : c->assign_res[ng] > 0     ? c->assign_res[ng]
@@ -398,7 +406,7 @@ int ensure_population(hq_ctx* c, int P, int K) {
     // bytes past a region's last column (past the buffer on the last palette's
     // last row when idx_pitch has no padding)
     HIP_TRY(c, c->d_idx.ensure((size_t)P * g.idx_pitch + 256));
-    HIP_TRY(c, c->d_used_mask.ensure(sizeof(uint32_t) * 8 * (size_t)P));
+    HIP_TRY(c, c->d_used_mask.ensure(sizeof(uint32_t) * kUsedSlots * (size_t)used_stride(P)));
     HIP_TRY(c, c->d_partial.ensure(sizeof(double) * (size_t)P * nparts));
     HIP_TRY(c, c->d_out.ensure(sizeof(double) * (size_t)P * (1 + K)));
     return ensure_pinned(c, sizeof(float) * 4 * (size_t)P * K, sizeof(double) * (size_t)P * (1 + K));
@@ -424,11 +432,12 @@ PaletteArgs prep_args(hq_ctx* c, int K) {
 // flags), all-reduced if a comm is set.  ev (8 events, or null): start/stop of
 // the grid, assign, cost and finalize launches, carried by the launches
 // themselves (set_launch_events).
-GridArgs grid_args(hq_ctx* c, int K) {
+GridArgs grid_args(hq_ctx* c, int P, int K) {
     const int G2 = c->G2 > 0 ? c->G2 : 4;
     const int G1 = G2 / 4;
     return GridArgs{c->d_pal.as<float4>(), c->d_dup.as<uint8_t>(), c->d_pflags.as<int>(),
-                    c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(), c->d_used_mask.as<uint32_t>(), K, G1,
+                    c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(), c->d_used_mask.as<uint32_t>(),
+                    used_stride(P), K, G1,
                     round_up((int64_t)G1 * G1 * G1 * 32, 256), round_up((int64_t)G2 * G2 * G2 * 64, 256)};
 }
 
@@ -487,7 +496,7 @@ int enqueue_wide(hq_ctx* c, int P, int K, const hipEvent_t* ev) {
     int nparts = 0;
     int rc = enqueue_generic_cost(c, P, c->d_idx32.p, true, K, ev, &nparts);
     if (rc) return rc;
-    FinalizeArgs fa{c->d_partial.as<double>(), nullptr, c->d_out.as<double>(), nparts, K,
+    FinalizeArgs fa{c->d_partial.as<double>(), nullptr, 0, c->d_out.as<double>(), nparts, K,
                     c->d_used32.as<uint32_t>()};
     if (ev) set_launch_events(ev[6], ev[7]);
     const hipError_t ef = launch_finalize(fa, P, s);
@@ -503,7 +512,7 @@ int enqueue_wide(hq_ctx* c, int P, int K, const hipEvent_t* ev) {
 int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = false) {
     const Geom& g = c->g;
     hipStream_t s = c->stream;
-    const GridArgs ga = grid_args(c, K);
+    const GridArgs ga = grid_args(c, P, K);
     auto timed = [&](int slot) {
         if (ev) set_launch_events(ev[2 * slot], ev[2 * slot + 1]);
     };
@@ -514,13 +523,13 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
         untimed();
         HIP_TRY(c, e);
     } else {
-        HIP_TRY(c, hipMemsetAsync(c->d_used_mask.p, 0, sizeof(uint32_t) * 8 * (size_t)P, s));
+        HIP_TRY(c, hipMemsetAsync(c->d_used_mask.p, 0, sizeof(uint32_t) * kUsedSlots * (size_t)used_stride(P), s));
     }
     const int nblocks = assign_blocks(c, P);
     const AssignArgs aa{c->d_R.as<float>(), c->d_G.as<float>(), c->d_B.as<float>(),
                         c->img_u8 && c->img_u8_path ? c->d_rgbx.as<uint32_t>() : nullptr, c->d_pal.as<float4>(),
                         c->d_pflags.as<int>(), c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(),
-                        c->d_idx.as<uint8_t>(), c->d_used_mask.as<uint32_t>(), g.n_ext, g.idx_pitch,
+                        c->d_idx.as<uint8_t>(), c->d_used_mask.as<uint32_t>(), used_stride(P), g.n_ext, g.idx_pitch,
                         ga.lvl1_pitch, ga.lvl2_gstride, K, c->G2, nblocks};
     timed(1);
     hipError_t e = launch_assign(aa, P, s);
@@ -555,7 +564,7 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
     }
     c->last_nparts = nparts;
     if (!fold) {  // (a folding search's accept step reduces the partials itself)
-        FinalizeArgs fa{c->d_partial.as<double>(), c->d_used_mask.as<uint32_t>(), c->d_out.as<double>(),
+        FinalizeArgs fa{c->d_partial.as<double>(), c->d_used_mask.as<uint32_t>(), used_stride(P), c->d_out.as<double>(),
                         nparts, K, nullptr};
         timed(3);
         const hipError_t ef = launch_finalize(fa, P, s);
@@ -677,6 +686,7 @@ int enqueue_sa_step(hq_search* s, bool accept, bool init, bool generate, bool ra
     a.convergence = s->prm.convergence;
     a.partial = c->d_partial.as<double>();
     a.used_glob = c->d_used_mask.as<uint32_t>();
+    a.used_stride = used_stride(a.P);
     a.ntiles = c->last_nparts;
     a.fold = s->fold;
     HIP_TRY(c, launch_sa_step(a, c->stream));

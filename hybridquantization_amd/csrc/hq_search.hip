@@ -178,7 +178,13 @@ __device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared
         // loads are out: an LDS store of a just-loaded value waits for it, and
         // the wait (in-order counters) held back every partial load behind it
         const double ein = tid < P ? a.err_in[tid] : 0.0;
-        if (tid < 8 * P) fold_word = a.used_glob[tid];
+        if (tid < 8 * P) {
+            uint32_t wv[kUsedSlots];
+#pragma unroll
+            for (int sl = 0; sl < kUsedSlots; ++sl) wv[sl] = a.used_glob[sl * a.used_stride + tid];
+#pragma unroll
+            for (int sl = 0; sl < kUsedSlots; ++sl) fold_word |= wv[sl];
+        }
         if (P <= 4) {
             double acc4[4];
             thread_partial_sums<4, 8>(a.partial, a.ntiles, P, acc4);
@@ -685,7 +691,8 @@ __global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
 #ifdef HQ_GRID_TIMING  // diagnostic build: per-workgroup start / end (wall_clock64, 100 MHz)
     const uint64_t t_start = wall_clock64();
 #endif
-    if (blockIdx.x == 0 && tid < 8) a.used_glob[p * 8 + tid] = 0u;  // for the assign that follows
+    if (blockIdx.x == 0 && tid < 8 * kUsedSlots)  // for the assign that follows
+        a.used_glob[(tid >> 3) * a.used_stride + p * 8 + (tid & 7)] = 0u;
     const bool exh = a.pflags[p] != 0;
     bool valid = false;
     float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -725,7 +732,12 @@ __global__ __launch_bounds__(1024) void finalize_kernel(FinalizeArgs a) {
         for (int k = tid; k < a.K; k += NT) out[1 + k] = u[k] != 0u ? 1.0 : 0.0;
     } else {
         const uint32_t* u = a.used_glob + (int64_t)p * 8;
-        for (int k = tid; k < a.K; k += NT) out[1 + k] = (u[k >> 5] >> (k & 31)) & 1u ? 1.0 : 0.0;
+        for (int k = tid; k < a.K; k += NT) {
+            uint32_t w = 0u;
+#pragma unroll
+            for (int sl = 0; sl < kUsedSlots; ++sl) w |= u[sl * a.used_stride + (k >> 5)];
+            out[1 + k] = (w >> (k & 31)) & 1u ? 1.0 : 0.0;
+        }
     }
 }
 
