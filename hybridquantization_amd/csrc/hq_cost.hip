@@ -10,6 +10,13 @@
 #include <cstring>
 #include <vector>
 
+#ifndef HQ_CHW
+#define HQ_CHW 8  // horizontal taps per chunk at HB = 15, 24
+#endif
+#ifndef HQ_CH19
+#define HQ_CH19 6  // horizontal taps per chunk at HB = 19 (8 spilled 40 B per lane at 3 waves/SIMD, 6 spills 12)
+#endif
+
 namespace hq {
 
 // ----------------------------------------------------------------------------
@@ -511,7 +518,7 @@ template <int HB, int TLO = 0, int THI = 2 * HB, int WH = 80>
 __device__ __forceinline__ void hpass_wide(const f32x4* src, int j, TapsPtr<HB> taps, int f,
                                            int plane, int pstride, f32x2 (&acc)[4]) {
     constexpr int HR = 4;
-    constexpr int CH = HB <= 10 ? 2 * HB + 1 : 8;  // taps per chunk
+    constexpr int CH = HB <= 10 ? 2 * HB + 1 : HB == 19 ? HQ_CH19 : HQ_CHW;  // taps per chunk
     const f32x4* row = src + plane * pstride + j;
 #pragma unroll
     for (int t0 = TLO; t0 <= THI; t0 += CH) {
