@@ -17,6 +17,13 @@
 
 namespace hq {
 
+#ifdef HQ_ASSIGN_TIMING
+__device__ unsigned int g_asg_slow[2];
+constexpr int kAsgStamps = 16384;
+// per workgroup: start, fill barrier, end, then each wave's loop end
+__device__ unsigned long long g_asg_t[kAsgStamps][8];
+#endif
+
 // Reference loop verbatim (CL:179-192) over a candidate list or all K colours.
 __device__ __noinline__ int argmin_exact_slow(float r, float g, float b, uint4 L0, uint4 L1,
                                               int cnt, bool all, const float4* s_pal, int K) {
@@ -55,6 +62,58 @@ __device__ __noinline__ int argmin_resolve_slow(float r, float g, float b, uint4
         if (cnt == kOverflow) all = true;
     }
     return argmin_exact_slow(r, g, b, L0, L1, cnt, all, s_pal, K);
+}
+
+// The reference loop (CL:179-192) for the few lanes of a wave that need it
+// (mask sm), the whole wave working on one lane's pixel at a time: lane l
+// takes colours l, l + 64, ... in ascending order (strict <, so the first
+// minimum within the lane), then a butterfly picks the least (distance,
+// index) -- the reference's first minimum.  A NaN distance never wins unless
+// colour 0's is NaN, which the reference keeps (nothing compares below NaN).
+// One rare near tie or list overflow used to cost its wave a 256-colour loop
+// on one lane (3-4 times the wave's other work): the launch waited for those
+// waves (assign_timing.py: the slowest waves 67 us against 20 at the median
+// on a 512-row shard).  Call with every lane active.
+constexpr int kCoopMax = 16;
+__device__ __forceinline__ int argmin_fix(float r, float g, float b, bool s, int cur, uint4 L0, bool listed,
+                                       const float4* s_pal, const uint8_t* lvl1p, int G2, int K) {
+    uint64_t sm = __ballot(s);
+    if (__popcll(sm) > kCoopMax)  // many (a palette with a non-finite colour): each lane its own loop
+        return s ? argmin_resolve_slow(r, g, b, L0, listed, s_pal, lvl1p, G2, K) : cur;
+    const int lane = (int)__lane_id();
+    int result = cur;
+    while (sm) {
+        const int L = __builtin_ctzll(sm);
+        sm &= sm - 1;
+        const float pr = __shfl(r, L, 64), pg = __shfl(g, L, 64), pb = __shfl(b, L, 64);
+        // (distance, key): a NaN distance counts as +inf with key bit 16 set, so a
+        // number (+inf included) beats it; equal distances: the lower index
+        float bd = INFINITY;
+        uint32_t bkey = 0xffffffffu;  // no colour yet
+        for (int k = lane; k < K; k += 64) {
+            const float d = sqrtf(dist2(pr, pg, pb, s_pal[k]));
+            const bool nan = d != d;
+            const float dv = nan ? INFINITY : d;
+            const uint32_t key = (nan ? 0x10000u : 0u) | (uint32_t)k;
+            if (dv < bd || (dv == bd && key < bkey)) {
+                bd = dv;
+                bkey = key;
+            }
+        }
+#pragma unroll
+        for (int m = 1; m < 64; m <<= 1) {
+            const float od = __shfl_xor(bd, m, 64);
+            const uint32_t ok = (uint32_t)__shfl_xor((int)bkey, m, 64);
+            if (od < bd || (od == bd && ok < bkey)) {
+                bd = od;
+                bkey = ok;
+            }
+        }
+        const int bk = (int)(bkey & 0xffffu);
+        const float d0 = sqrtf(dist2(pr, pg, pb, s_pal[0]));
+        if (lane == L) result = d0 != d0 ? 0 : bk;
+    }
+    return result;
 }
 
 // Exact argmin (CL:179-193 semantics) of one pixel against the NG palettes of
@@ -157,12 +216,18 @@ __device__ __forceinline__ void argmin_group(float r, float g, float b, const ui
 #pragma unroll
     for (int q = 0; q < NG; ++q) {
         out[q] = (int)(ba[q] >> 4);
+#ifdef HQ_ABL_NOSLOW  // timing ablation (wrong results): no re-resolution
+        const bool s = false;
+#else
         const bool s = slow[q] || near[q];
-        if (__any(s)) {
-            if (s)
-                out[q] = argmin_resolve_slow(r, g, b, E[q], inside && !exh_pal[q], s_pal + q * kMaxK,
-                                             lvl1 + (int64_t)(p0 + q) * lvl1_pitch, G2, K);
-        }
+#endif
+#ifdef HQ_ASSIGN_TIMING  // diagnostic: lanes re-resolved (near ties, overflows / no list)
+        if (near[q]) atomicAdd(&g_asg_slow[0], 1u);
+        if (slow[q]) atomicAdd(&g_asg_slow[1], 1u);
+#endif
+        if (__any(s))
+            out[q] = argmin_fix(r, g, b, s, out[q], E[q], inside && !exh_pal[q], s_pal + q * kMaxK,
+                                lvl1 + (int64_t)(p0 + q) * lvl1_pitch, G2, K);
     }
 }
 
@@ -203,11 +268,6 @@ __device__ __forceinline__ float u8_unit(uint32_t v, int j) {
 template <bool U8> struct RawPx { float r, g, b; };
 template <> struct RawPx<true> { uint32_t v; };
 
-#ifdef HQ_ASSIGN_TIMING
-constexpr int kAsgStamps = 16384;
-// per workgroup: start, fill barrier, end, then each wave's loop end
-__device__ unsigned long long g_asg_t[kAsgStamps][8];
-#endif
 
 template <int NG, bool U8>
 #ifndef HQ_ASSIGN_WAVES
@@ -453,6 +513,12 @@ int assign_residency(int NG) {
 
 #ifdef HQ_ASSIGN_TIMING
 // diagnostic build only: the last assign launch's workgroup stamps (wall_clock64 ticks)
+extern "C" int hq_debug_assign_slow(unsigned int* out) {  // and resets the counts
+    const int e = (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(hq::g_asg_slow), 2 * sizeof(unsigned int));
+    const unsigned int z[2] = {0u, 0u};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(hq::g_asg_slow), z, sizeof z);
+    return e;
+}
 extern "C" int hq_debug_assign_stamps(unsigned long long* out, int n) {
     n = n < hq::kAsgStamps ? n : hq::kAsgStamps;
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(hq::g_asg_t), sizeof(unsigned long long) * 8 * (size_t)n);

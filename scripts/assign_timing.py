@@ -28,7 +28,16 @@ if len(sys.argv) > 1 and sys.argv[1] == "run":
     for it in range(3):
         pal = rng.random((P, 256, 4), dtype=np.float32)
         pal[..., 3] = 0
-        m.computeQuantizationErrorPopulation(pal.reshape(P, -1), 2.0)
+        if rows < W:  # a row-block shard: the partial evaluation (no communicator)
+            part = np.zeros(P * 257, np.float64)
+            _lib.check(lib.hq_eval_population_partial(m.ctx, _lib.fptr(pal.reshape(-1)), P, 256,
+                                                      _lib.dptr(part)), m.ctx)
+        else:
+            m.computeQuantizationErrorPopulation(pal.reshape(P, -1), 2.0)
+    slow = np.zeros(2, np.uint32)
+    lib.hq_debug_assign_slow.argtypes = [C.c_void_p]
+    lib.hq_debug_assign_slow(slow.ctypes.data)
+    print("SLOW %d %d" % (int(slow[0]), int(slow[1])))
     buf = np.zeros((16384, 8), np.uint64)
     lib.hq_debug_assign_stamps.argtypes = [C.c_void_p, C.c_int]
     lib.hq_debug_assign_stamps(buf.ctypes.data, 16384)
@@ -52,6 +61,9 @@ def q(v):
     return "min %.2f med %.2f p90 %.2f max %.2f" % (v[0], v[len(v) // 2], v[int(len(v) * 0.9)], v[-1])
 
 
+sl = [l for l in res.stdout.splitlines() if l.startswith("SLOW")]
+if sl:
+    print("lanes re-resolved over the 3 evaluations: near ties %s, overflow or no list %s" % tuple(sl[0].split()[1:]))
 print(f"{len(last)} workgroups; end of the last {(max(en) - t0) / 100:.2f} us after the first start")
 print("start            ", q([(s - t0) / 100 for s in st]))
 print("to fill          ", q([(f - s) / 100 for s, f in zip(st, fi)]))
