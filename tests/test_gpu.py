@@ -233,6 +233,36 @@ def test_assign_random_and_near_ties(ip, K):
         np.testing.assert_array_equal(used[1], rev_used)
 
 
+@pytest.mark.parametrize("grid", [32, 64, 0])
+def test_assign_sparse_special_pixels(ip, grid):
+    """Lanes that need the reference loop (CL:179-192) -- pixels outside [0, 1],
+    NaN or infinite channels, colours equal to a pixel or one ulp apart -- are
+    re-resolved by their whole wave when they are few (argmin_coop: the loop
+    split over 64 lanes and a (distance, index) butterfly, NaN distances never
+    winning unless colour 0's is NaN), by each lane otherwise (a wave of
+    specials).  Both must give the oracle's indices and used flags."""
+    rng = np.random.default_rng(21)
+    w, h = 256, 64
+    px = np.zeros((w * h, 4), np.float32)
+    px[:, :3] = (rng.integers(0, 256, (w * h, 3)) / 255.0).astype(np.float32)
+    specials = [np.nan, np.inf, -np.inf, -0.5, 1.5, 2.0, -0.0]
+    for j, i in enumerate(range(0, w * h, 97)):  # sparse: ~one per wave
+        px[i, j % 3] = specials[j % len(specials)]
+    px[640:704, 0] = np.nan  # a whole wave of NaN pixels: the per-lane path
+    px[704:720, 1] = 3.0     # 16 outside pixels in one wave: the cooperative path's limit
+    pal = o.synthetic_palette(256, 5)
+    pal[7, :3] = px[3, :3]
+    pal[8, :3] = np.nextafter(pal[7, :3], np.float32(2))
+    pal[100, :3] = pal[9, :3]
+    ip.setOption("grid", grid)
+    ip.setImage(px.reshape(-1), np.zeros_like(px).reshape(-1), w, ip.illum)
+    for p in (pal, pal[::-1].copy()):
+        _, used = ip.computeQuantizationErrorPopulation([p.reshape(-1)], 2.0, return_used=True)
+        ref_idx, ref_used = c_oracle.assign(px, p)
+        np.testing.assert_array_equal(ip.getIndices(0), ref_idx.astype(np.uint8))
+        np.testing.assert_array_equal(used[0], ref_used)
+
+
 @pytest.mark.parametrize("grid", [64, 32, 0])
 def test_assign_signed_zero_and_mass_duplicates(ip, grid):
     """Duplicate flags (prep_palette's hash of first occurrences): +0/-0 channels
