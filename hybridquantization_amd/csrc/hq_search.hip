@@ -686,6 +686,11 @@ __device__ __forceinline__ void grid_cell_body(const GridArgs& a, int p, int cel
     }
 }
 
+#ifdef HQ_GRID_TIMING
+constexpr int kGridStamps = 65536;
+__device__ unsigned long long g_grid_t[kGridStamps][2];  // per workgroup: start, end (wall_clock64 ticks)
+#endif
+
 __global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
     const int p = blockIdx.y, tid = threadIdx.x;
 #ifdef HQ_GRID_TIMING  // diagnostic build: per-workgroup start / end (wall_clock64, 100 MHz)
@@ -703,9 +708,10 @@ __global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
     grid_cell_body(a, p, blockIdx.x, c, valid, exh);
 #ifdef HQ_GRID_TIMING
     __syncthreads();
-    if (tid == 0)
-        printf("GRID_T %d %d %llu %llu\n", p, (int)blockIdx.x, (unsigned long long)t_start,
-               (unsigned long long)wall_clock64());
+    if (tid == 0 && p * (int)gridDim.x + (int)blockIdx.x < kGridStamps) {
+        g_grid_t[p * gridDim.x + blockIdx.x][0] = t_start;
+        g_grid_t[p * gridDim.x + blockIdx.x][1] = wall_clock64();
+    }
 #endif
 }
 // ----------------------------------------------------------------------------
@@ -771,3 +777,11 @@ hipError_t launch_finalize(const FinalizeArgs& a, int P, hipStream_t s) {
 }
 
 }  // namespace hq
+
+#ifdef HQ_GRID_TIMING
+// diagnostic build only: the last build_grid launch's workgroup stamps
+extern "C" int hq_debug_grid_stamps(unsigned long long* out, int n) {
+    n = n < hq::kGridStamps ? n : hq::kGridStamps;
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(hq::g_grid_t), sizeof(unsigned long long) * 2 * (size_t)n);
+}
+#endif

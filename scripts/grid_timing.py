@@ -1,6 +1,7 @@
 """Diagnostic: per-workgroup start/end stamps of build_grid (a library built with
--DHQ_GRID_TIMING, HQ_LIB_PATH) over a few 4096^2 / K=256 / P=4 evaluations;
-prints the dispatch spread and the workgroup durations of the last one."""
+-DHQ_GRID_TIMING, HQ_LIB_PATH; stamps kept in device memory, read back by
+hq_debug_grid_stamps) over a few 4096^2 / K=256 / P=4 evaluations; prints the
+dispatch spread and the workgroup durations of the last one."""
 import os
 import subprocess
 import sys
@@ -23,13 +24,20 @@ if len(sys.argv) > 1 and sys.argv[1] == "run":
     for it in range(3):
         pal = rng.random((4, 256, 4), dtype=np.float32)
         pal[..., 3] = 0
-        print("EVAL", it, flush=True)
         m.computeQuantizationErrorPopulation(pal.reshape(4, -1), 2.0)
+    import ctypes as C
+    n = 4 * 512
+    buf = np.zeros((n, 2), np.uint64)
+    lib.hq_debug_grid_stamps.argtypes = [C.c_void_p, C.c_int]
+    lib.hq_debug_grid_stamps(buf.ctypes.data, n)
     m.close()
+    for i, r in enumerate(buf):
+        print("GRID_T %d %d %d %d" % (i // 512, i % 512, int(r[0]), int(r[1])))
     sys.exit(0)
-out = subprocess.run([sys.executable, __file__, "run"], capture_output=True, text=True, timeout=300).stdout
-evals = out.split("EVAL")
-last = [l.split() for l in evals[-1].splitlines() if l.startswith("GRID_T")]
+res = subprocess.run([sys.executable, __file__, "run"], capture_output=True, text=True, timeout=300)
+last = [l.split() for l in res.stdout.splitlines() if l.startswith("GRID_T")]
+if not last:
+    sys.exit("no stamps:\n" + res.stderr[-2000:])
 st = [int(x[3]) for x in last]
 en = [int(x[4]) for x in last]
 t0 = min(st)
