@@ -188,12 +188,15 @@ int hq_profile_reset(hq_ctx *ctx);
  * every evaluation sizes the context's work buffers for the options and image
  * in force when it is enqueued.
  *   "grid"         argmin pruning resolution G2: 0 = exhaustive, 16, 32 (default), 64
- *   "cost_variant" 0 = fast tiled path (default; 21-tap filters), 1 = generic
+ *   "cost_variant" 0 = fast tiled path (default; filters up to halfSize 24), 1 = generic
  *                  two-pass path (any filter length; the fast path's cross-check)
  *   "cost_rows"    fast path tiles: 16 (16 x 128 outputs, default) or 8 (8 x 108)
  *   "trim"         1 = skip the narrow k1 filters' taps below 1e-9 of their peak
  *                  (default; only when the filters allow it), 0 = all taps
- *   "assign_blocks_per_cu" workgroups per CU of the assign grid (default 16)
+ *   "assign_blocks_per_cu" workgroups per CU of the assign grid (0 = default: one
+ *                  resident round, at least 6 pixels per thread)
+ *   "img_u8"       1 (default) = assign reads the packed 8-bit copy of an image whose
+ *                  channels are all k/255; 0 = the planar floats
  *   "sa_device"    hq_search_*: 1 (default) = the SWASA iterations run on the device
  *                  (accept/generate kernel, no host round trip per iteration; needs
  *                  population <= 64), 0 = host-driven, one evaluation call each
