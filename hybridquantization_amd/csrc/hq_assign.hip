@@ -1,6 +1,8 @@
 // hq_assign.hip -- per-pixel palette index (CL:179-193 argmin, bit-exact)
 // and used-colour bitmask (CL:193) for a population of palettes, through the
 // exact candidate lists of build_grid (hq_search.hip).
+#include <type_traits>
+
 #include "hq_device.h"
 #include "hq_launch.h"
 
@@ -16,6 +18,17 @@
 #endif
 
 namespace hq {
+
+// A level-2 entry in registers: count + kL2Cap indices (hq_internal.h).
+using L2E = std::conditional_t<kL2Bytes == 16, uint4, uint2>;
+__device__ __forceinline__ uint32_t l2_word(const uint2& e, int k) { return k == 0 ? e.x : e.y; }
+__device__ __forceinline__ uint32_t l2_word(const uint4& e, int k) {
+    return k == 0 ? e.x : k == 1 ? e.y : k == 2 ? e.z : e.w;
+}
+__device__ __forceinline__ uint4 l2_u4(const uint2& e) { return make_uint4(e.x, e.y, 0u, 0u); }
+__device__ __forceinline__ uint4 l2_u4(const uint4& e) { return e; }
+__device__ __forceinline__ void l2_set(uint2& e, uint32_t x, uint32_t y) { e = make_uint2(x, y); }
+__device__ __forceinline__ void l2_set(uint4& e, uint32_t x, uint32_t y) { e = make_uint4(x, y, 0u, 0u); }
 
 #ifdef HQ_ASSIGN_TIMING
 __device__ unsigned int g_asg_slow[2];
@@ -75,11 +88,11 @@ __device__ __noinline__ int argmin_resolve_slow(float r, float g, float b, uint4
 // waves (assign_timing.py: the slowest waves 67 us against 20 at the median
 // on a 512-row shard).  Call with every lane active.
 constexpr int kCoopMax = 16;
-__device__ __forceinline__ int argmin_fix(float r, float g, float b, bool s, int cur, uint4 L0, bool listed,
+__device__ __forceinline__ int argmin_fix(float r, float g, float b, bool s, int cur, L2E L0, bool listed,
                                        const float4* s_pal, const uint8_t* lvl1p, int G2, int K) {
     uint64_t sm = __ballot(s);
     if (__popcll(sm) > kCoopMax)  // many (a palette with a non-finite colour): each lane its own loop
-        return s ? argmin_resolve_slow(r, g, b, L0, listed, s_pal, lvl1p, G2, K) : cur;
+        return s ? argmin_resolve_slow(r, g, b, l2_u4(L0), listed, s_pal, lvl1p, G2, K) : cur;
     const int lane = (int)__lane_id();
     int result = cur;
     while (sm) {
@@ -128,7 +141,7 @@ __device__ __forceinline__ int argmin_fix(float r, float g, float b, bool s, int
 // flight; the step count is then the longest list over the wave's lanes and
 // the group's palettes.
 template <int NG>
-__device__ __forceinline__ void argmin_group(float r, float g, float b, const uint4 (&E)[NG], bool inside,
+__device__ __forceinline__ void argmin_group(float r, float g, float b, const L2E (&E)[NG], bool inside,
                                              const bool (&exh_pal)[NG], const float4* s_pal,
                                              const uint8_t* lvl1, int64_t lvl1_pitch, int p0, int G2,
                                              int K, int (&out)[NG]) {
@@ -158,7 +171,7 @@ __device__ __forceinline__ void argmin_group(float r, float g, float b, const ui
             return *reinterpret_cast<const float4*>(base + q * (kMaxK * 16) + off);
         };
         auto cand16 = [&](int q, int i) {  // byte i + 1 of the entry, x16
-            const uint32_t w = (i + 1) < 4 ? E[q].x : (i + 1) < 8 ? E[q].y : (i + 1) < 12 ? E[q].z : E[q].w;
+            const uint32_t w = l2_word(E[q], (i + 1) >> 2);
             return byte_x16(w, (i + 1) & 3);
         };
         float best2[NG], second2[NG];
@@ -297,7 +310,12 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
     const uint32_t n_ext = (uint32_t)a.n_ext, qlast = n_ext - 1;
     const uint32_t cstride = (uint32_t)a.nblocks * 256u;
     const uint32_t qbase = (uint32_t)blk * 256u + (uint32_t)tid;
-    const int npx = qbase < n_ext ? (int)((n_ext - 1 - qbase) / cstride) + 1 : 0;
+    // Every lane of a wave runs its lane 0's step count (the largest: qbase
+    // grows with the lane): argmin_fix's cooperative loop and butterfly need
+    // the whole wave active.  Steps past the image resolve the clamped last
+    // pixel again and store nothing.
+    const int npx0 = qbase < n_ext ? (int)((n_ext - 1 - qbase) / cstride) + 1 : 0;
+    const int npx = __builtin_amdgcn_readfirstlane(npx0);
     auto qpos = [&](int i) { return qbase + (uint32_t)i * cstride; };
     // Loads are unconditional (clamped addresses, results selected afterwards):
     // predicated loads sit behind branches, and the compiler's wait counting
@@ -326,21 +344,35 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
             b = x.b;
         }
     };
-    auto lookup = [&](uint32_t q, float r, float g, float b, bool& inside, uint4 (&e)[NG]) {
-        inside = U8 ? q < n_ext
-                    : q < n_ext && r >= 0.f && r <= 1.f && g >= 0.f && g <= 1.f && b >= 0.f && b <= 1.f;
+    auto lookup = [&](uint32_t q, float r, float g, float b, bool& inside, L2E (&e)[NG]) {
+        // (q past the image: the clamped last pixel, resolved but not stored)
+        inside = U8 ? true : r >= 0.f && r <= 1.f && g >= 0.f && g <= 1.f && b >= 0.f && b <= 1.f;
 #ifdef HQ_ABL_HASHLOOKUP  // timing ablation (wrong results): a random line, independent of the RGB
-        const uint4* line = reinterpret_cast<const uint4*>(lines + ((q * 2654435761u) >> 17) * 64u);
+        const uint8_t* lb = lines + ((q * 2654435761u) >> 17) * (uint32_t)kL2Line;
 #else
-        const uint4* line =
-            reinterpret_cast<const uint4*>(lines + (inside ? (uint32_t)quad_cell(r, g, b, G2) : 0u) * 64u);
+        const uint8_t* lb = lines + (inside ? (uint32_t)quad_cell(r, g, b, G2) : 0u) * (uint32_t)kL2Line;
 #endif
+        // selected by the `listed` flag at use.  8-B entries: two palettes per
+        // 16-B load (the L1 access count per pixel, not the bytes, is the cost)
+        const uint4* line = reinterpret_cast<const uint4*>(lb);
+        if constexpr (kL2Bytes == 16) {
 #pragma unroll
-        for (int pp = 0; pp < NG; ++pp) e[pp] = line[pp];  // selected by the `listed` flag at use
+            for (int pp = 0; pp < NG; ++pp) e[pp] = line[pp];
+        } else {
+#pragma unroll
+            for (int pp = 0; pp + 1 < NG; pp += 2) {
+                const uint4 v = line[pp >> 1];
+                l2_set(e[pp], v.x, v.y);
+                l2_set(e[pp + 1], v.z, v.w);
+            }
+            if constexpr (NG & 1) e[NG - 1] = reinterpret_cast<const L2E*>(lb)[NG - 1];
+        }
 #ifdef HQ_ABL_NOLOOKUP  // timing ablation (wrong results): one fixed entry, lists of 3-4
 #pragma unroll
-        for (int pp = 0; pp < NG; ++pp)
-            e[pp] = make_uint4(0x03020103u + (q & 1u), 0x07060504u, 0x0b0a0908u, 0x0f0e0d0cu);
+        for (int pp = 0; pp < NG; ++pp) {
+            const uint4 f = make_uint4(0x03020103u + (q & 1u), 0x07060504u, 0x0b0a0908u, 0x0f0e0d0cu);
+            l2_set(e[pp], f.x, f.y);  // counts 3-4: words 0-1
+        }
 #endif
     };
     // Pipeline, unrolled by two so every buffer has a fixed register set (a
@@ -355,7 +387,7 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
     // load in flight before that write.
     RawPx<U8> rb[2];                  // RGB loads in flight: pixel i+1 / i+2 by parity
     float xr[2], xg[2], xb[2];        // RGB of pixels being looked up / resolved
-    uint4 E[2][NG];
+    L2E E[2][NG];
     bool in_[2];
     uint32_t qq[2];
     {
@@ -398,7 +430,7 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
 #else
 #pragma unroll
         for (int pp = 0; pp < NG; ++pp) {
-            const uint4 e1[1] = {E[h][pp]};
+            const L2E e1[1] = {E[h][pp]};
             const bool x1[1] = {exh_pal[pp]};
             int k1[1];
             argmin_group<1>(xr[h], xg[h], xb[h], e1, in_[h], x1, s_pal + pp * kMaxK, a.lvl1, a.lvl1_pitch,
@@ -412,9 +444,11 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
             // non-temporal: streamed out during the kernel rather than left dirty
             // in L2 for the kernel boundary to write back (67 MB per population;
             // ~0.5-1% per evaluation)
-            __builtin_nontemporal_store((uint8_t)k, idx_base[pp] + q);
-            const uint32_t bit = 1u << (k & 31);
-            if (!(s_used[pp][k >> 5] & bit)) atomicOr(&s_used[pp][k >> 5], bit);
+            if (q < n_ext) {
+                __builtin_nontemporal_store((uint8_t)k, idx_base[pp] + q);
+                const uint32_t bit = 1u << (k & 31);
+                if (!(s_used[pp][k >> 5] & bit)) atomicOr(&s_used[pp][k >> 5], bit);
+            }
         }
     };
     auto step = [&](int i, int h) {  // h == i & 1, a compile-time constant at each call

@@ -12,7 +12,13 @@ constexpr int kMaxKWide = 1 << 24;  // K > 256: 32-bit indices (the plugin's lim
 constexpr int kMaxTaps = 255;     // generic path limit (2*half+1)
 constexpr int kNumFilt = 7;       // separable filter pairs of the S-CIELAB stencil
 constexpr int kL1Cap = 31;        // level-1 candidate list capacity (32-B entry)
-constexpr int kL2Cap = 15;        // level-2 candidate list capacity (16-B entry)
+#ifndef HQ_L2B
+#define HQ_L2B 16  // bytes per level-2 entry: 16 (count + 15 indices) or 8 (count + 7; slower)
+#endif
+constexpr int kL2Bytes = HQ_L2B;
+constexpr int kL2Cap = kL2Bytes - 1;  // level-2 candidate list capacity (stored)
+constexpr int kL2Build = 15;          // list length build_grid tracks before pruning
+constexpr int kL2Line = 4 * kL2Bytes;  // one cell's entries of a group of 4 palettes
 constexpr uint8_t kOverflow = 255;
 
 // The 7 separable (vertical, horizontal) filter pairs of the candidate stencil,
@@ -102,13 +108,13 @@ struct GridArgs {
     const uint8_t* dup;
     const int* pflags;
     uint8_t* lvl1;          // [P][G1^3][32]
-    uint8_t* lvl2;          // [ceil(P/4)][G2^3][4][16]: 4 palettes' entries per 64-B line
+    uint8_t* lvl2;          // [ceil(P/4)][G2^3][4][kL2Bytes]: a group's 4 entries of a cell side by side
     uint32_t* used_glob;    // [kUsedSlots][used_stride] used-colour bits, zeroed here for the assign
     int used_stride;        // that follows
     int K;
     int G1;                 // level-1 resolution (G2 / 4)
     int64_t lvl1_pitch;     // bytes per palette
-    int64_t lvl2_gstride;   // bytes per group of 4 palettes (G2^3 * 64)
+    int64_t lvl2_gstride;   // bytes per group of 4 palettes (G2^3 * kL2Line)
 };
 
 struct AssignArgs {
@@ -127,7 +133,7 @@ struct AssignArgs {
     int64_t n_ext;
     int64_t idx_pitch;
     int64_t lvl1_pitch;     // bytes per palette
-    int64_t lvl2_gstride;   // bytes per group of 4 palettes (G2^3 * 64)
+    int64_t lvl2_gstride;   // bytes per group of 4 palettes (G2^3 * kL2Line)
     int K;
     int G2;                 // 0 = exhaustive
     int nblocks;            // workgroups per palette group

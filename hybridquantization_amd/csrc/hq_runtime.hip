@@ -384,7 +384,7 @@ int ensure_population(hq_ctx* c, int P, int K) {
     const int G2 = c->G2 > 0 ? c->G2 : 4;
     const int G1 = G2 / 4;
     const int64_t l1p = round_up((int64_t)G1 * G1 * G1 * 32, 256);
-    const int64_t l2g = round_up((int64_t)G2 * G2 * G2 * 64, 256);  // per group of 4 palettes
+    const int64_t l2g = round_up((int64_t)G2 * G2 * G2 * kL2Line, 256);  // per group of 4 palettes
     int tiles_x, ntiles;
     fast_tile_dims(g.W, g.r1 - g.r0, 8, &tiles_x, &ntiles);  // the most tiles of any config
     const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
@@ -438,7 +438,7 @@ GridArgs grid_args(hq_ctx* c, int P, int K) {
     return GridArgs{c->d_pal.as<float4>(), c->d_dup.as<uint8_t>(), c->d_pflags.as<int>(),
                     c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(), c->d_used_mask.as<uint32_t>(),
                     used_stride(P), K, G1,
-                    round_up((int64_t)G1 * G1 * G1 * 32, 256), round_up((int64_t)G2 * G2 * G2 * 64, 256)};
+                    round_up((int64_t)G1 * G1 * G1 * 32, 256), round_up((int64_t)G2 * G2 * G2 * kL2Line, 256)};
 }
 
 // The generic two-pass cost (CL:234-306 per pixel, any half-width) of P

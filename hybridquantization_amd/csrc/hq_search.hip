@@ -454,11 +454,14 @@ __device__ __forceinline__ float ax_max2(float c, float lo, float hi) {
 #define HQ_CAND_MARGIN (1.0f + 1e-5f)
 
 // Level-2 entries are interleaved by groups of 4 palettes: the 4 entries of one
-// cell share a 64-byte line, so a pixel evaluated under the 4 palettes of a
-// group fetches one line instead of 4 (random 16-B lookups are bound by the
-// line fetches they cause, not by their bytes).
+// cell sit side by side (32 B at 8 B per entry), so a pixel evaluated under the
+// 4 palettes of a group fetches one line instead of 4, in two 16-B loads per
+// lane (random lookups are bound by the L1 accesses they cause, not by their
+// bytes).  An 8-B entry holds count + 7 indices: after the dominance pruning
+// ~0.2% of cells list more (uniform noise, K = 256, G2 = 32); those overflow
+// into the reference loop (assign's argmin_fix).
 __host__ __device__ __forceinline__ int64_t lvl2_offset(int64_t gstride, int p, int64_t cell) {
-    return (int64_t)(p >> 2) * gstride + cell * 64 + (p & 3) * 16;
+    return (int64_t)(p >> 2) * gstride + cell * kL2Line + (p & 3) * kL2Bytes;
 }
 
 // Per-axis child terms of the level-2 pass: s_ax[axis][j][i] = the bound of
@@ -526,7 +529,7 @@ __device__ __forceinline__ void prune_dominated(uint32_t (&w)[4], int& n, const 
         uint32_t x0 = 0u, x1 = 0u, x2 = 0u, x3 = 0u;
         int kept = 0;
 #pragma unroll
-        for (int i = kL2Cap - 1; i >= 0; --i) {
+        for (int i = kL2Build - 1; i >= 0; --i) {
             if (i < n && !((drop >> i) & 1u)) {
                 x3 = (x3 << 8) | (x2 >> 24);
                 x2 = (x2 << 8) | (x1 >> 24);
@@ -626,7 +629,7 @@ __device__ __forceinline__ void grid_cell_body(const GridArgs& a, int p, int cel
     // pass 2, 32 positions at a time: candidate mask, ranks in list order
     uint32_t w[4] = {0u, 0u, 0u, 0u};
     int n = 0;  // candidates so far (quad-uniform)
-    for (int b0 = 0; b0 < total && n <= kL2Cap; b0 += 32) {
+    for (int b0 = 0; b0 < total && n <= kL2Build; b0 += 32) {
         uint32_t mine = 0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -643,7 +646,7 @@ __device__ __forceinline__ void grid_cell_body(const GridArgs& a, int p, int cel
             const int r = q + 4 * j;
             if ((mine >> r) & 1u) {
                 const int pos = n + __popc(M & ((1u << r) - 1u)) + 1;  // byte in the entry
-                if (pos <= kL2Cap) w[pos >> 2] |= (uint32_t)s_list[b0 + r] << (8 * (pos & 3));
+                if (pos <= kL2Build) w[pos >> 2] |= (uint32_t)s_list[b0 + r] << (8 * (pos & 3));
             }
         }
         n += __popc(M);
@@ -670,7 +673,7 @@ __device__ __forceinline__ void grid_cell_body(const GridArgs& a, int p, int cel
     // instead of b* only: 2.0 / 5.2, at O(n^2) build cost), and with them
     // assign's candidate loop, which runs each wave's longest list.
 #ifndef HQ_NO_DOMINANCE
-    if (!exh && n >= 2 && n <= kL2Cap) {
+    if (!exh && n >= 2 && n <= kL2Build) {
         const float blo[3] = {(float)(4 * ci + a0) * inv2, (float)(4 * cj + a1) * inv2,
                               (float)(4 * ck + a2) * inv2};
         const float bhi[3] = {blo[0] + inv2, blo[1] + inv2, blo[2] + inv2};
@@ -678,11 +681,15 @@ __device__ __forceinline__ void grid_cell_body(const GridArgs& a, int p, int cel
     }
 #endif
     if (q == 0) {
+#ifdef HQ_ABL_TRUNC  // timing ablation (wrong results): long lists truncated, never overflow
+        if (!exh && n > kL2Cap && n <= kL2Build) n = kL2Cap;
+#endif
         if (exh || n > kL2Cap) { w[0] = kOverflow; w[1] = w[2] = w[3] = 0; }
         else w[0] |= (uint32_t)n;
         const int ci2 = ci * 4 + a0, cj2 = cj * 4 + a1, ck2 = ck * 4 + a2;
         uint8_t* l2e = a.lvl2 + lvl2_offset(a.lvl2_gstride, p, (int64_t)(ci2 * G2 + cj2) * G2 + ck2);
-        *reinterpret_cast<uint4*>(l2e) = make_uint4(w[0], w[1], w[2], w[3]);
+        if constexpr (kL2Bytes == 16) *reinterpret_cast<uint4*>(l2e) = make_uint4(w[0], w[1], w[2], w[3]);
+        else *reinterpret_cast<uint2*>(l2e) = make_uint2(w[0], w[1]);
     }
 }
 
