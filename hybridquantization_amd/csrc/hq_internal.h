@@ -13,7 +13,7 @@ constexpr int kMaxTaps = 255;     // generic path limit (2*half+1)
 constexpr int kNumFilt = 7;       // separable filter pairs of the S-CIELAB stencil
 constexpr int kL1Cap = 31;        // level-1 candidate list capacity (32-B entry)
 #ifndef HQ_L2B
-#define HQ_L2B 16  // bytes per level-2 entry: 16 (count + 15 indices) or 8 (count + 7; slower)
+#define HQ_L2B 8  // bytes per level-2 entry: 8 (count + 7 indices) or 16 (count + 15)
 #endif
 constexpr int kL2Bytes = HQ_L2B;
 constexpr int kL2Cap = kL2Bytes - 1;  // level-2 candidate list capacity (stored)

@@ -491,6 +491,8 @@ __device__ __forceinline__ void axis_terms(float (*s_ax)[4][kAxPitch], const flo
     }
 }
 
+__device__ __forceinline__ void drop_positions(uint32_t (&w)[4], int& n, uint32_t drop);
+
 // Dominance pruning (exact) of one child entry (w[4], n candidates, quad lane
 // q): see the comment in grid_cell_body.
 __device__ __forceinline__ void prune_dominated(uint32_t (&w)[4], int& n, const float4* col, int bstar,
@@ -523,6 +525,66 @@ __device__ __forceinline__ void prune_dominated(uint32_t (&w)[4], int& n, const 
         }
         if (fmin > 1e-5f * S) drop |= 1u << i;
     }
+    drop_positions(w, n, drop);
+}
+
+// Dominance test of prune_dominated for colour a (bound dmax2a over the box)
+// against colour b.
+__device__ __forceinline__ bool dominated_by(const float (&va)[3], float dmax2a, const float (&vb)[3],
+                                             const float (&blo)[3], const float (&bhi)[3]) {
+    const float na = (va[0] * va[0] + va[1] * va[1]) + va[2] * va[2];
+    const float nb = (vb[0] * vb[0] + vb[1] * vb[1]) + vb[2] * vb[2];
+    float fmin = na - nb, S = na + nb + dmax2a;
+#pragma unroll
+    for (int ax = 0; ax < 3; ++ax) {
+        const float cc = 2.0f * (vb[ax] - va[ax]);
+        const float tl = cc * blo[ax], th = cc * bhi[ax];
+        fmin += fminf(tl, th);
+        S += fmaxf(fabsf(tl), fabsf(th));
+    }
+    return fmin > 1e-5f * S;
+}
+
+// Lists still longer than a stored entry holds (kL2Cap) after prune_dominated
+// (~0.2% of cells on uniform noise, K = 256, G2 = 32, 8-B entries): every
+// candidate is tested against every other one of its list (the same exact
+// test; a colour dominated by any listed colour never wins, and two colours
+// cannot dominate each other), which leaves ~1/7 of them overflowing.  The
+// quads of such children post their lists (slot: entry words, count, child);
+// a wave then takes one list at a time, its lanes testing the n (n - 1)
+// ordered pairs (<= 4 per lane), and ORs the drops into the slot.  (One quad
+// testing its own pairs held the workgroup: build_grid 13.3 -> 18.2 us.)
+struct LongLists {
+    uint32_t ent[64][4];
+    uint32_t drop[64];
+    uint8_t n[64], ch[64];
+    int count;
+};
+
+__device__ __forceinline__ void prune_long_lists(LongLists& L, const float4* col, int nl, int ci, int cj,
+                                                 int ck, float inv2) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int it = wave; it < nl; it += 4) {
+        const int chl = L.ch[it], nn = L.n[it];
+        const float blo[3] = {(float)(4 * ci + (chl >> 4)) * inv2, (float)(4 * cj + ((chl >> 2) & 3)) * inv2,
+                              (float)(4 * ck + (chl & 3)) * inv2};
+        const float bhi[3] = {blo[0] + inv2, blo[1] + inv2, blo[2] + inv2};
+        const uint8_t* keys = reinterpret_cast<const uint8_t*>(L.ent[it]) + 1;
+        for (int pi = lane; pi < nn * nn; pi += 64) {
+            const int ia = pi / nn, ib = pi - ia * nn;
+            if (ia == ib) continue;
+            const float4 ca = col[keys[ia]], cb = col[keys[ib]];
+            const float va[3] = {ca.x, ca.y, ca.z}, vb[3] = {cb.x, cb.y, cb.z};
+            const float dm = (ax_max2(va[0], blo[0], bhi[0]) + ax_max2(va[1], blo[1], bhi[1])) +
+                             ax_max2(va[2], blo[2], bhi[2]);
+            if (dominated_by(va, dm, vb, blo, bhi)) atomicOr(&L.drop[it], 1u << ia);
+        }
+    }
+}
+
+// The drop masks of a quad (OR-combined) applied to its entry: kept positions
+// move down in ascending order, count byte below them.
+__device__ __forceinline__ void drop_positions(uint32_t (&w)[4], int& n, uint32_t drop) {
     drop |= (uint32_t)__shfl_xor((int)drop, 1, 64);
     drop |= (uint32_t)__shfl_xor((int)drop, 2, 64);
     if (drop) {  // rebuild the entry from the kept positions, ascending
@@ -562,6 +624,8 @@ __device__ __forceinline__ void grid_cell_body(const GridArgs& a, int p, int cel
     __shared__ float s_ax[3][4][kAxPitch];
 
     s_col[tid] = c;
+    __shared__ LongLists s_long;  // (8-B entries only)
+    if (kL2Cap < kL2Build && tid == 0) s_long.count = 0;
     const float inv1 = 1.0f / (float)G1;
     const float lo0 = ci * inv1, hi0 = (ci + 1) * inv1;
     const float lo1 = cj * inv1, hi1 = (cj + 1) * inv1;
@@ -678,6 +742,26 @@ __device__ __forceinline__ void grid_cell_body(const GridArgs& a, int p, int cel
                               (float)(4 * ck + a2) * inv2};
         const float bhi[3] = {blo[0] + inv2, blo[1] + inv2, blo[2] + inv2};
         prune_dominated(w, n, s_col, bstar, blo, bhi, q);
+    }
+    if constexpr (kL2Cap < kL2Build) {
+        const bool lng = !exh && n > kL2Cap && n <= kL2Build;  // quad-uniform
+        int slot = 0;
+        if (lng && q == 0) {
+            slot = atomicAdd(&s_long.count, 1);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) s_long.ent[slot][k] = w[k];
+            s_long.drop[slot] = 0u;
+            s_long.n[slot] = (uint8_t)n;
+            s_long.ch[slot] = (uint8_t)ch;
+        }
+        __syncthreads();
+        const int nl = s_long.count;
+        if (nl > 0) {  // workgroup-uniform
+            prune_long_lists(s_long, s_col, nl, ci, cj, ck, inv2);
+            __syncthreads();
+            slot = __shfl(slot, (int)(threadIdx.x & 60), 64);
+            if (lng) drop_positions(w, n, s_long.drop[slot]);
+        }
     }
 #endif
     if (q == 0) {
