@@ -97,18 +97,19 @@ __device__ __forceinline__ TileItem tile_item(const CostArgs& a, int w, int P) {
 // Every load is issued before the first wait: vmcnt retires in order, so a
 // load -> wait -> store loop pays one memory round trip per trip (4 for the
 // interior index rows, 14 for the byte gathers of edge tiles).
-// Interior rows are read as DW = RW / 4 dword pairs: the first 32 dword columns
-// by a (row, column) = (tid / 32 + 8q, tid % 32) map (shifts and masks, row
-// offsets one multiply-add), the DW - 32 tail columns (cost16w's 148-byte rows:
-// 5) by a second, short pass.
-template <int HALF, int RW, int TH>
+// Interior rows are read as DW = RW / 4 dword pairs: the first DM = NTH / 8
+// dword columns by a (row, column) = (tid / DM + 8q, tid % DM) map (shifts and
+// masks, row offsets one multiply-add), the DW - DM tail columns (cost16w's
+// 148-byte rows: 5 of 37; the 276-byte rows of 256-column tiles: 5 of 69) by a
+// second, short pass.  NTH = threads of the workgroup.
+template <int HALF, int RW, int TH, int NTH = 256>
 struct TileFill {
-    static constexpr int TW = RW - 2 * HALF, RH = TH + 2 * HALF, DW = RW / 4;
-    static constexpr int DWT = DW - 32;                                   // tail dword columns
+    static constexpr int TW = RW - 2 * HALF, RH = TH + 2 * HALF, DW = RW / 4, DM = NTH / 8;
+    static constexpr int DWT = DW - DM;                                   // tail dword columns
     static constexpr int DWTD = DWT > 0 ? DWT : 1;                        // its divisor (no tail: unused)
-    static constexpr int NM = (RH * 32 + 255) / 256, NT = (RH * DWT + 255) / 256;
-    static constexpr int NFD = NM + NT, NFB = (RH * RW + 255) / 256;
-    static_assert(RW % 4 == 0 && DW >= 32 && DWT < 32, "whole dwords per region row, 32 <= DW < 64");
+    static constexpr int NM = (RH * DM + NTH - 1) / NTH, NT = (RH * DWT + NTH - 1) / NTH;
+    static constexpr int NFD = NM + NT, NFB = (RH * RW + NTH - 1) / NTH;
+    static_assert(RW % 4 == 0 && DW >= DM && DWT < DM, "whole dwords per region row, DM <= DW < 2 DM");
     uint32_t lo[NFD], hi[NFD];  // interior tiles: aligned dword pairs of the index rows
     uint32_t roff[NFD];         // their rows' byte offsets (alignment for commit)
     uint4 ov;  // the palette's split opponent entry tid (zeros past K)
@@ -131,7 +132,7 @@ struct TileFill {
     // use 32-bit unsigned offsets from the palette's base (saddr form); the host
     // keeps a shard's index image below 2^31 bytes.
     __device__ __forceinline__ void issue(const CostArgs& a, const TileItem& ti, int tid) {
-        static_assert(kMaxK == 256, "one opponent-table entry per thread");
+        static_assert(kMaxK <= NTH, "one opponent-table entry per thread");
         const Geom& g = a.g;
         t = ti;
         const uint8_t* idx = a.idx + (int64_t)t.p * g.idx_pitch;
@@ -149,11 +150,11 @@ struct TileFill {
                 hi[q] = src[1];
             };
 #pragma unroll
-            for (int q = 0; q < NM; ++q) load(q, min((tid >> 5) + 8 * q, RH - 1), tid & 31);
+            for (int q = 0; q < NM; ++q) load(q, min(tid / DM + 8 * q, RH - 1), tid % DM);
 #pragma unroll
             for (int q = 0; q < NT; ++q) {
-                const int e = min(tid + 256 * q, RH * DWT - 1);
-                load(NM + q, e / DWTD, 32 + e % DWTD);
+                const int e = min(tid + NTH * q, RH * DWT - 1);
+                load(NM + q, e / DWTD, DM + e % DWTD);
             }
         }
     }
@@ -166,15 +167,15 @@ struct TileFill {
             uint32_t* s32 = reinterpret_cast<uint32_t*>(s_idx);
 #pragma unroll
             for (int q = 0; q < NM; ++q) {
-                const int i = (tid >> 5) + 8 * q;
+                const int i = tid / DM + 8 * q;
                 if (i < RH)
-                    s32[i * (IDXP / 4) + (tid & 31)] = __builtin_amdgcn_alignbyte(hi[q], lo[q], roff[q] & 3u);
+                    s32[i * (IDXP / 4) + tid % DM] = __builtin_amdgcn_alignbyte(hi[q], lo[q], roff[q] & 3u);
             }
 #pragma unroll
             for (int q = 0; q < NT; ++q) {
-                const int e = tid + 256 * q;
+                const int e = tid + NTH * q;
                 if (e < RH * DWT)
-                    s32[(e / DWTD) * (IDXP / 4) + 32 + e % DWTD] =
+                    s32[(e / DWTD) * (IDXP / 4) + DM + e % DWTD] =
                         __builtin_amdgcn_alignbyte(hi[NM + q], lo[NM + q], roff[NM + q] & 3u);
             }
         } else {
@@ -182,7 +183,7 @@ struct TileFill {
             uint32_t b[NFB];
 #pragma unroll
             for (int q = 0; q < NFB; ++q) {  // all loads first: one round trip
-                const int e = min(tid + 256 * q, RH * RW - 1);
+                const int e = min(tid + NTH * q, RH * RW - 1);
                 const int i = e / RW, j = e % RW;
                 int gy = reflect_clamp(t.y0 - HALF + i, g.H);
                 gy = min(max(gy, g.e0), g.e1 - 1);
@@ -191,7 +192,7 @@ struct TileFill {
             }
 #pragma unroll
             for (int q = 0; q < NFB; ++q) {
-                const int e = tid + 256 * q;
+                const int e = tid + NTH * q;
                 if (e < RH * RW) s_idx[(e / RW) * IDXP + e % RW] = (uint8_t)b[q];
             }
         }
@@ -469,20 +470,20 @@ __global__ __launch_bounds__(256, 6) void cost_mfma_kernel(CostArgs a, int P_) {
 // ----------------------------------------------------------------------------
 constexpr int kTH16 = 16;
 
-template <int HB>
+template <int HB, int NW = 4>
 struct Tile16 {
-    static constexpr int TH = kTH16, TW = 128, HR = 4;
+    static constexpr int TH = kTH16, TW = 32 * NW, HR = 4;  // NW waves: 4 (16 x 128) or 8 (16 x 256)
     static constexpr int RWL = (TW + 2 * HB + 3) / 4 * 4;  // region columns read (whole dwords)
     static constexpr int RW = (RWL + 31) / 32 * 32;    // LDS pitch: whole 32-column ranges
     static constexpr int RH = TH + 2 * HB;             // region rows
     static constexpr int NBLK = RW / 16;               // vertical-pass column blocks
-    static constexpr int NSET = (NBLK + 3) / 4;        // blocks per wave (at most)
+    static constexpr int NSET = (NBLK + NW - 1) / NW;  // blocks per wave (at most)
     static constexpr int WH = RW / 2;                  // float2 per half of a permuted row-pair row
     static constexpr int S = (8 + 2 * HB + 31) / 32;   // K steps of 32 rows per output-row half
     static constexpr int NJ = 8 * S + 2;               // K slots (rows 4 n + g) a lane gathers
     static constexpr int PLANE4 = (TH / 2) * RW / 2;   // f32x4 per filter plane
     static constexpr int NQ = (HR + 2 * HB) / 2;       // horizontal window reads per filter
-    static_assert(RWL % 4 == 0 && RWL / 4 >= 32 && RWL / 4 < 64, "TileFill: 32 <= dwords per row < 64");
+    static_assert(RWL % 4 == 0 && RWL / 4 >= 8 * NW && RWL / 4 < 16 * NW, "TileFill: 8 NW <= dwords per row < 16 NW");
     static_assert(NSET <= 3, "three blocks per wave at most");
 };
 
@@ -553,10 +554,10 @@ __device__ __forceinline__ f32x2* vstack_base(float* s_v, int plane, int lk, int
     constexpr int PAIRS = kTH16 / 2, ROW = 2 * WH;
     return reinterpret_cast<f32x2*>(s_v) + (plane * PAIRS + 2 * (lk & 1)) * ROW + wide_pos<WH>(col0);
 }
-template <int WH>
+template <int WH, int NW = 4>
 __device__ __forceinline__ void store_vstack_at(f32x2* base, const f32x4v& d, int i, int half) {
     constexpr int ROW = 2 * WH;
-    f32x2* v = base + 4 * half * ROW + 32 * i;
+    f32x2* v = base + 4 * half * ROW + 8 * NW * i;  // block set i + 1: 16 NW columns on
     v[0] = f32x2{d[0], d[1]};
     v[ROW] = f32x2{d[2], d[3]};
 }
@@ -607,19 +608,20 @@ __device__ __forceinline__ void vblock(const uint32_t (&w)[8 * S + 2], const uin
 template <int HB>
 constexpr int cost16w_waves() { return HB == 10 ? 4 : HB == 15 ? 3 : HB == 19 ? HQ_LB19 : 2; }
 
-template <int HB, int DE, bool TRIM>
-__global__ __launch_bounds__(256, cost16w_waves<HB>()) void cost16w_kernel(CostArgs a, int P_) {
-    using Gm = Tile16<HB>;
+template <int HB, int DE, bool TRIM, int NW>
+__global__ __launch_bounds__(64 * NW, cost16w_waves<HB>()) void cost16w_kernel(CostArgs a, int P_) {
+    using Gm = Tile16<HB, NW>;
+    constexpr int NTH = 64 * NW, IPR = 8 * NW;  // threads; horizontal items per row pair
     constexpr int TH = kTH16, HR = 4, T2 = 2 * HB, TW = Gm::TW, RWL = Gm::RWL, RW = Gm::RW;
     constexpr int RH = Gm::RH, WH = Gm::WH, NBLK = Gm::NBLK, NSET = Gm::NSET, S = Gm::S, NJ = Gm::NJ;
     constexpr int ROW = 2 * WH, PLANE4 = Gm::PLANE4;
     constexpr int L0 = HB - trim_w(HB, 0), L1 = HB - trim_w(HB, 1), L2 = HB - trim_w(HB, 2);
-    static_assert(TW / HR == 32, "tile");
+    static_assert(TW / HR == IPR && 8 * IPR == NTH, "one horizontal item per thread");
     __shared__ f32x4 s_vq[3 * PLANE4];
     __shared__ uint32_t s_ox[kMaxK];  // opponent x 2^14 as (hi, lo) f16 pairs: channel 0
     __shared__ uint2 s_oyz[kMaxK];     // channels 1, 2
     __shared__ __attribute__((aligned(16))) uint8_t s_idx[RH * RW];
-    __shared__ double s_red[4];
+    __shared__ double s_red[NW];
     float* s_v = reinterpret_cast<float*>(s_vq);
     const int tid = threadIdx.x;
     const Geom& g = a.g;
@@ -630,7 +632,7 @@ __global__ __launch_bounds__(256, cost16w_waves<HB>()) void cost16w_kernel(CostA
     const uint4* frag = a.vfrag16 + (TRIM ? 2 * S * 4 * 2 * 64 : 0) + lane;
     auto F = [&](int half, int s, int st, int hl) { return frag[(((half * S + s) * 4 + st) * 2 + hl) * 64]; };
 
-    TileFill<HB, RWL, TH> fill;
+    TileFill<HB, RWL, TH, NTH> fill;
     fill.issue(a, cur, tid);
     uint4 A[2][2][S][2];  // channel 0's stacks (f0, f1), (f2, -); then channels 1-2's
 #pragma unroll
@@ -644,11 +646,13 @@ __global__ __launch_bounds__(256, cost16w_waves<HB>()) void cost16w_kernel(CostA
             }
     // every entry (zeros for tid >= K): zero-weight rows and the columns past
     // the region gather arbitrary indices, and 0 x NaN would be NaN
-    s_ox[tid] = fill.ov.x;
-    s_oyz[tid] = make_uint2(fill.ov.y, fill.ov.z);
+    if (NTH == kMaxK || tid < kMaxK) {
+        s_ox[tid] = fill.ov.x;
+        s_oyz[tid] = make_uint2(fill.ov.y, fill.ov.z);
+    }
     fill.template commit_idx<RW>(a, s_idx, tid);
     // H item: row pair m, output columns 4j .. 4j+3 (every thread has one)
-    const int m = tid >> 5, jr = tid & 31;
+    const int m = tid / IPR, jr = tid % IPR;
     const int gy0 = cur.y0 + 2 * m, gx0 = cur.x0 + HR * jr;
     const f32x4* hsrc = &s_vq[(m * ROW) / 2];
     f32x2 acc0[HR], acc1[HR], acc2[HR];
@@ -656,11 +660,12 @@ __global__ __launch_bounds__(256, cost16w_waves<HB>()) void cost16w_kernel(CostA
     for (int xo = 0; xo < HR; ++xo) acc0[xo] = acc1[xo] = acc2[xo] = f32x2{0.f, 0.f};
     __syncthreads();
 
-    // Block b = wset + 4i covers the 16 columns of parity half b & 1 of range
-    // b >> 1.  With 10 blocks, sets 0 and 1 hold 3 blocks and sets 2 and 3 hold
-    // 2: the sets rotate with the workgroup, so the extra blocks do not land on
-    // the same SIMDs in every workgroup.
-    const int wset = (wv + (int)blockIdx.x) & 3;
+    // Block b = wset + NW i covers the 16 columns of parity half b & 1 of range
+    // b >> 1.  With 10 blocks over 4 waves, sets 0 and 1 hold 3 blocks and sets
+    // 2 and 3 hold 2 (18 over 8: sets 0, 1 hold 3): the sets rotate with the
+    // workgroup, so the extra blocks do not land on the same SIMDs in every
+    // workgroup.
+    const int wset = (wv + (int)blockIdx.x) & (NW - 1);
     const int col0 = 32 * (wset >> 1) + 4 * (lc >> 1) + (lc & 1) + 2 * (wset & 1);
     f32x2* const st01 = vstack_base<WH>(s_v, lk < 2 ? 0 : 1, lk, col0);  // stacks -> planes 0, 1
     f32x2* const st2 = vstack_base<WH>(s_v, 2, lk, col0);                // (f2, -) -> plane 2
@@ -674,19 +679,19 @@ __global__ __launch_bounds__(256, cost16w_waves<HB>()) void cost16w_kernel(CostA
     // ---- channel 0: stacks (f0, f1) -> planes 0, 1 and (f2, -) -> plane 2 ----
 #pragma unroll
     for (int i = 0; i < NSET; ++i) {
-        const int b = wset + 4 * i;
+        const int b = wset + NW * i;
         if (b >= NBLK) break;
-        const int col = col0 + 64 * i;
+        const int col = col0 + 16 * NW * i;
         uint32_t w[NJ];
 #pragma unroll
         for (int n = 0; n < NJ; ++n) w[n] = 4 * n < RH ? s_ox[s_idx[gather_row(n, col)]] : 0u;
         f32x4v d[2][2];
         vblock<S, 2>(w, A, d);
-        store_vstack_at<WH>(st01, d[0][0], i, 0);
-        store_vstack_at<WH>(st01, d[0][1], i, 1);
+        store_vstack_at<WH, NW>(st01, d[0][0], i, 0);
+        store_vstack_at<WH, NW>(st01, d[0][1], i, 1);
         if (lk < 2) {  // the (f2, -) stack's second filter slot is empty
-            store_vstack_at<WH>(st2, d[1][0], i, 0);
-            store_vstack_at<WH>(st2, d[1][1], i, 1);
+            store_vstack_at<WH, NW>(st2, d[1][0], i, 0);
+            store_vstack_at<WH, NW>(st2, d[1][1], i, 1);
         }
     }
     // channel 1-2 stacks: in flight during channel 0's horizontal pass with one
@@ -717,9 +722,9 @@ __global__ __launch_bounds__(256, cost16w_waves<HB>()) void cost16w_kernel(CostA
     f32x4v d5[NSET][2];
 #pragma unroll
     for (int i = 0; i < NSET; ++i) {
-        const int b = wset + 4 * i;
+        const int b = wset + NW * i;
         if (b >= NBLK) break;
-        const int col = col0 + 64 * i;
+        const int col = col0 + 16 * NW * i;
         uint32_t wy[NJ], wz[NJ];
 #pragma unroll
         for (int n = 0; n < NJ; ++n) {
@@ -734,8 +739,8 @@ __global__ __launch_bounds__(256, cost16w_waves<HB>()) void cost16w_kernel(CostA
             const uint4(&Ay)[1][2][S][2] = *reinterpret_cast<const uint4(*)[1][2][S][2]>(&A[0]);
             f32x4v d[1][2];
             vblock<S, 1>(wy, Ay, d);
-            store_vstack_at<WH>(st01, d[0][0], i, 0);
-            store_vstack_at<WH>(st01, d[0][1], i, 1);
+            store_vstack_at<WH, NW>(st01, d[0][0], i, 0);
+            store_vstack_at<WH, NW>(st01, d[0][1], i, 1);
         }
         {
             const uint4(&Az)[1][2][S][2] = *reinterpret_cast<const uint4(*)[1][2][S][2]>(&A[1]);
@@ -754,10 +759,10 @@ __global__ __launch_bounds__(256, cost16w_waves<HB>()) void cost16w_kernel(CostA
     // ---- channel 2: stack (f5, f6) -> planes 0, 1 ----
 #pragma unroll
     for (int i = 0; i < NSET; ++i) {
-        const int b = wset + 4 * i;
+        const int b = wset + NW * i;
         if (b >= NBLK) break;
-        store_vstack_at<WH>(st01, d5[i][0], i, 0);
-        store_vstack_at<WH>(st01, d5[i][1], i, 1);
+        store_vstack_at<WH, NW>(st01, d5[i][0], i, 0);
+        store_vstack_at<WH, NW>(st01, d5[i][1], i, 1);
     }
     // LabRef of the item's 2 x 4 pixels, in flight across the barrier
     float4 lab[2][3];
@@ -805,8 +810,11 @@ __global__ __launch_bounds__(256, cost16w_waves<HB>()) void cost16w_kernel(CostA
     double sum = wave_sum_to_lane63((double)part);
     if ((tid & 63) == 63) s_red[tid >> 6] = sum;
     __syncthreads();
-    if (tid == 0)
-        a.partial[(int64_t)cur.p * a.ntiles + cur.tile] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+    if (tid == 0) {
+        double t = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+        if constexpr (NW == 8) t += (s_red[4] + s_red[5]) + (s_red[6] + s_red[7]);
+        a.partial[(int64_t)cur.p * a.ntiles + cur.tile] = t;
+    }
 }
 
 // ----------------------------------------------------------------------------
@@ -1015,37 +1023,44 @@ void build_fast_taps(int HB, int H, const float* k1, const float* k2, const floa
     }
 }
 
-// tile_rows: 8 (cost_mfma_kernel, 8 x 108 tiles) or 16 (cost16w_kernel, 16 x 128 tiles)
-void fast_tile_dims(int W, int own_rows, int tile_rows, int* tiles_x, int* ntiles) {
-    const int tw = tile_rows == kTH16 ? 128 : kFastTW;
+// tile_rows: 8 (cost_mfma_kernel, 8 x 108 tiles) or 16 (cost16w_kernel, 16 x
+// tile_w tiles, tile_w = 128 or 256)
+void fast_tile_dims(int W, int own_rows, int tile_rows, int tile_w, int* tiles_x, int* ntiles) {
+    const int tw = tile_rows == kTH16 ? tile_w : kFastTW;
     *tiles_x = (W + tw - 1) / tw;
     *ntiles = *tiles_x * ((own_rows + tile_rows - 1) / tile_rows);
 }
 
 // a.taps = the two CostTaps<HB> of build_fast_taps; [1] carries the vertical
 // pass's 2^30 scale in its horizontal taps.  8-row tiles: HB = 10 only.
-template <int HB>
+template <int HB, int NW>
 static void launch_cost16w(const CostArgs& a0, int P, int de, bool trim, hipStream_t s) {
     CostArgs a = a0;
     a.taps = static_cast<const char*>(a0.taps) + sizeof(CostTaps<HB>);
-    const dim3 grid((unsigned)(a.ntiles * P));
+    const dim3 grid((unsigned)(a.ntiles * P)), block(64 * NW);
     if (de == 0) {
-        if (trim) HQ_LAUNCH((cost16w_kernel<HB, 0, true>), grid, dim3(256), 0, s, a, P);
-        else HQ_LAUNCH((cost16w_kernel<HB, 0, false>), grid, dim3(256), 0, s, a, P);
+        if (trim) HQ_LAUNCH((cost16w_kernel<HB, 0, true, NW>), grid, block, 0, s, a, P);
+        else HQ_LAUNCH((cost16w_kernel<HB, 0, false, NW>), grid, block, 0, s, a, P);
     } else {
-        if (trim) HQ_LAUNCH((cost16w_kernel<HB, 1, true>), grid, dim3(256), 0, s, a, P);
-        else HQ_LAUNCH((cost16w_kernel<HB, 1, false>), grid, dim3(256), 0, s, a, P);
+        if (trim) HQ_LAUNCH((cost16w_kernel<HB, 1, true, NW>), grid, block, 0, s, a, P);
+        else HQ_LAUNCH((cost16w_kernel<HB, 1, false, NW>), grid, block, 0, s, a, P);
     }
 }
 
-hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, bool trim, int tile_rows, int HB,
+// 256-column tiles (8 waves, 69 KB of LDS at HB = 10): HB = 10 only.
+hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, bool trim, int tile_rows, int tile_w, int HB,
                             hipStream_t s) {
     if (tile_rows == kTH16) {
+        if (tile_w == 256) {
+            if (HB != 10) return hipErrorInvalidValue;
+            launch_cost16w<10, 8>(a0, P, de, trim, s);
+            return hipGetLastError();
+        }
         switch (HB) {
-        case 10: launch_cost16w<10>(a0, P, de, trim, s); break;
-        case 15: launch_cost16w<15>(a0, P, de, trim, s); break;
-        case 19: launch_cost16w<19>(a0, P, de, trim, s); break;
-        case 24: launch_cost16w<24>(a0, P, de, trim, s); break;
+        case 10: launch_cost16w<10, 4>(a0, P, de, trim, s); break;
+        case 15: launch_cost16w<15, 4>(a0, P, de, trim, s); break;
+        case 19: launch_cost16w<19, 4>(a0, P, de, trim, s); break;
+        case 24: launch_cost16w<24, 4>(a0, P, de, trim, s); break;
         default: return hipErrorInvalidValue;
         }
         return hipGetLastError();

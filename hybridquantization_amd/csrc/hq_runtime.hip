@@ -17,6 +17,10 @@
 #include "hq_internal.h"
 #include "hq_swasa.h"
 
+#ifndef HQ_COST_TW
+#define HQ_COST_TW 128
+#endif
+
 namespace hq {
 // launchers from hq_kernels.hip
 hipError_t launch_prep_palette(const PaletteArgs&, int P, hipStream_t);
@@ -25,9 +29,10 @@ void set_launch_events(hipEvent_t start, hipEvent_t stop);
 hipError_t launch_build_grid(const GridArgs&, int P, hipStream_t);
 hipError_t launch_assign(const AssignArgs&, int P, hipStream_t);
 int assign_residency(int P);
-void fast_tile_dims(int W, int own_rows, int tile_rows, int* tiles_x, int* ntiles);
+void fast_tile_dims(int W, int own_rows, int tile_rows, int tile_w, int* tiles_x, int* ntiles);
 void opp2xyz_over_illum(const float inv_illum[3], float m[9]);
-hipError_t launch_cost_fast(const CostArgs&, int P, int de, bool trim, int tile_rows, int HB, hipStream_t);
+hipError_t launch_cost_fast(const CostArgs&, int P, int de, bool trim, int tile_rows, int tile_w, int HB,
+                            hipStream_t);
 int fast_bucket(int half);
 size_t vpass_f16_stack_fragment_halves(int HB);
 void build_vpass_f16_stack_fragments(int HB, int H, const float* k1, const float* k2, const float* k3,
@@ -123,6 +128,7 @@ struct hq_ctx {
     int G2 = 32;           // argmin grid resolution (0 = exhaustive)
     int cost_variant = 0;  // 0 tiled (default), 1 generic two-pass
     int cost_rows = 16;    // fast path tiles: 16 x 128 (cost16w_kernel) or 8 x 108 (cost_mfma_kernel)
+    int cost_tw = HQ_COST_TW;  // 16-row tiles at HB = 10: 128 (4 waves) or 256 columns (8 waves; slower)
     int assign_blocks_per_cu = 0;  // 0 = auto: assign_pipe_kernel<NG>'s residency (the occupancy
                                    // query, assign_res[NG]), one round of workgroups, each
                                    // thread a grid-stride pixel sequence
@@ -386,7 +392,7 @@ int ensure_population(hq_ctx* c, int P, int K) {
     const int64_t l1p = round_up((int64_t)G1 * G1 * G1 * 32, 256);
     const int64_t l2g = round_up((int64_t)G2 * G2 * G2 * kL2Line, 256);  // per group of 4 palettes
     int tiles_x, ntiles;
-    fast_tile_dims(g.W, g.r1 - g.r0, 8, &tiles_x, &ntiles);  // the most tiles of any config
+    fast_tile_dims(g.W, g.r1 - g.r0, 8, 128, &tiles_x, &ntiles);  // the most tiles of any config
     const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
     const int64_t gen_blocks = (n_own + 255) / 256;
     const int64_t nparts = std::max<int64_t>(ntiles, gen_blocks);
@@ -540,6 +546,7 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
     if (c->cost_variant != 1 && c->fast_hb > 0 && !c->pal_generic) {
         // 8-row tiles (cost_mfma_kernel) exist for the 21-tap bucket only
         const int rows = c->fast_hb == 10 ? c->cost_rows : 16;
+        const int tw = c->fast_hb == 10 ? c->cost_tw : 128;  // 256-column tiles: HB = 10 only
         CostArgs ca{};
         ca.idx = c->d_idx.as<uint8_t>();
         ca.opp16 = c->d_opp16.as<uint4>();
@@ -551,10 +558,10 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
         ca.partial = c->d_partial.as<double>();
         ca.g = g;
         ca.K = K;
-        fast_tile_dims(g.W, g.r1 - g.r0, rows, &ca.tiles_x, &ca.ntiles);
+        fast_tile_dims(g.W, g.r1 - g.r0, rows, tw, &ca.tiles_x, &ca.ntiles);
         opp2xyz_over_illum(inv, ca.m_lab);
         timed(2);
-        e = launch_cost_fast(ca, P, c->de_type, c->trim && c->trim_ok, rows, c->fast_hb, s);
+        e = launch_cost_fast(ca, P, c->de_type, c->trim && c->trim_ok, rows, tw, c->fast_hb, s);
         untimed();
         HIP_TRY(c, e);
         nparts = ca.ntiles;
@@ -1276,6 +1283,9 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
     } else if (!std::strcmp(name, "cost_rows")) {
         if (value != 8 && value != 16) return fail(c, HQ_ERR_ARG, "cost_rows must be 8 or 16");
         c->cost_rows = value;
+    } else if (!std::strcmp(name, "cost_tw")) {
+        if (value != 128 && value != 256) return fail(c, HQ_ERR_ARG, "cost_tw must be 128 or 256");
+        c->cost_tw = value;
 
     } else if (!std::strcmp(name, "sa_device")) {
         c->sa_device = value != 0;

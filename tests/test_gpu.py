@@ -74,19 +74,20 @@ def test_labref_256_checksum(ip):
 # Candidate evaluation (IM:620-727): golden fixtures
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("grid", [64, 32, 16, 0])
-@pytest.mark.parametrize("variant", [(0, 16), (0, 8), (1, 16)])
+@pytest.mark.parametrize("variant", [(0, 16, 256), (0, 16, 128), (0, 8, 128), (1, 16, 256)])
 @pytest.mark.parametrize("name", ["case_64x48_k16", "case_97x53_k64"])
 def test_eval_golden(ip, name, grid, variant):
-    """(cost_variant, cost_rows): 0 = the fast tiled path (vertical passes on the
-    matrix cores in split f16, horizontal pass on VALU) on 16 x 128 tiles
-    (cost16w_kernel, default) or 8 x 108 tiles (cost_mfma_kernel), 1 = the
-    generic two-pass path; argmin through candidate grids of 64^3, 32^3, 16^3
+    """(cost_variant, cost_rows, cost_tw): 0 = the fast tiled path (vertical
+    passes on the matrix cores in split f16, horizontal pass on VALU) on 16 x 128
+    tiles (cost16w_kernel, 4 waves, default), 16 x 256 (8 waves) or 8 x 108 tiles
+    (cost_mfma_kernel), 1 = the generic two-pass path; argmin through candidate grids of 64^3, 32^3, 16^3
     cells or exhaustive."""
     g, R, G, B = load_case(name)
     w = int(g["w"])
     ip.setOption("grid", grid)
     ip.setOption("cost_variant", variant[0])
     ip.setOption("cost_rows", variant[1])
+    ip.setOption("cost_tw", variant[2])
     ip.setImage(o.inline_rgba(R, G, B).reshape(-1), g["lab"].reshape(-1), w, ip.illum)
     pals = g["palettes"]
     costs, used = ip.computeQuantizationErrorPopulation(pals.reshape(len(pals), -1), 2.0,
@@ -122,15 +123,15 @@ def test_eval_config2_1024_k64(ip, filt):
     assert abs(cost - ref) <= COST_RTOL * abs(ref) * 0.1
 
 
-@pytest.mark.parametrize("rows", [16, 8])
+@pytest.mark.parametrize("rows,tw", [(16, 256), (16, 128), (8, 128)])
 @pytest.mark.parametrize("de", [hq.deltaETypes.CIE76, hq.deltaETypes.CIE94])
 @pytest.mark.parametrize("trim", [1, 0])
-def test_fast_path_matches_generic(gpu, de, trim, rows):
+def test_fast_path_matches_generic(gpu, de, trim, rows, tw):
     """The fast path (split-f16 vertical products, hi.hi + hi.lo + lo.hi with ~2^-22
     relative per product dropped; trimmed narrow filters) agrees with the generic
     fp32 two-pass path to 1e-6 relative (the bar is 1e-4) on interior, edge and
-    partial tiles."""
-    w, h = (300, 77) if rows == 8 else (290, 93)
+    partial tiles (800 columns: two interior 256-column tiles)."""
+    w, h = (300, 77) if rows == 8 else (290, 93) if tw == 128 else (800, 93)
     R, G, B = o.synthetic_image(w, h, seed=5)
     m = hq.ImageManipulation(de, device=gpu)
     sp = hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
@@ -138,6 +139,7 @@ def test_fast_path_matches_generic(gpu, de, trim, rows):
     pals = [o.synthetic_palette(K, 7 + K) for K in (16, 64, 256)]
     m.setOption("trim", trim)
     m.setOption("cost_rows", rows)
+    m.setOption("cost_tw", tw)
     out = {}
     for variant in (0, 1):
         m.setOption("cost_variant", variant)
@@ -747,6 +749,11 @@ def test_full_size_properties(gpu, filt):
     c8 = m.computeQuantizationErrorPopulation(pals, 2.0)
     np.testing.assert_allclose(c8, c1, rtol=1e-6)  # 8-row tiles == 16-row tiles
     m.setOption("cost_rows", 16)
+    m.setOption("cost_tw", 256)
+    c256 = m.computeQuantizationErrorPopulation(pals, 2.0)
+    np.testing.assert_allclose(c256, c1, rtol=1e-6)  # 256-column tiles == 128-column tiles
+    m.setOption("cost_tw", 128)
+    m.setOption("cost_rows", 16)
     m.setOption("cost_variant", 1)
     c4 = m.computeQuantizationErrorPopulation(pals, 2.0)
     np.testing.assert_allclose(c4, c1, rtol=1e-6)  # generic two-pass == fast path
@@ -758,8 +765,8 @@ def test_full_size_properties(gpu, filt):
     m.close()
 
 
-@pytest.mark.parametrize("rows", [16, 8])
-def test_alternating_populations_bitwise(gpu, filt, rows):
+@pytest.mark.parametrize("rows,tw", [(16, 256), (16, 128), (8, 128)])
+def test_alternating_populations_bitwise(gpu, filt, rows, tw):
     """Two different populations evaluated alternately give, every time,
     bitwise the costs and used flags of their first evaluation (no state of one
     evaluation -- partials, used masks, level-2 lines -- leaks into the next),
@@ -769,6 +776,7 @@ def test_alternating_populations_bitwise(gpu, filt, rows):
     R, G, B = o.synthetic_image(w, h, seed=3)
     m = _planar_ctx(gpu, R, G, B, w, h, filt.illum)
     m.setOption("cost_rows", rows)
+    m.setOption("cost_tw", tw)
     pops = [np.stack([o.synthetic_palette(K, 40 + 10 * s + p) for p in range(P)]).reshape(P, -1)
             for s in range(2)]
     first = [m.computeQuantizationErrorPopulation(pp, 2.0, return_used=True) for pp in pops]
