@@ -293,6 +293,33 @@ def test_assign_signed_zero_and_mass_duplicates(ip, grid):
         np.testing.assert_array_equal(ip.getIndices(0), ref_idx.astype(np.uint8))
 
 
+@pytest.mark.parametrize("grid", [64, 32, 16])
+def test_assign_clustered_palettes_long_lists(ip, grid):
+    """Palettes of a few tight colour clusters: many cells list more colours than
+    an 8-B level-2 entry holds, so build_grid's pairwise pass (prune_long_lists)
+    and the overflow re-resolution (argmin_fix, cooperative and per-lane) both
+    run; indices and used flags equal the oracle's argmin.  P = 4 (one group)."""
+    rng = np.random.default_rng(31 + grid)
+    w, h, K, P = 256, 192, 256, 4
+    px = np.zeros((w * h, 4), np.float32)
+    px[:, :3] = (rng.integers(0, 256, (w * h, 3)) / 255.0).astype(np.float32)
+    pals = []
+    for p in range(P):
+        centres = rng.random((2 + 2 * p, 3), dtype=np.float32)
+        pal = np.zeros((K, 4), np.float32)
+        pal[:, :3] = np.clip(centres[rng.integers(0, len(centres), K)] +
+                             rng.normal(0, 0.02 * (p + 1), (K, 3)), 0, 1)
+        pals.append(pal)
+    pals = np.stack(pals)
+    ip.setOption("grid", grid)
+    ip.setImage(px.reshape(-1), np.zeros_like(px).reshape(-1), w, ip.illum)
+    _, used = ip.computeQuantizationErrorPopulation(pals.reshape(P, -1), 2.0, return_used=True)
+    for p in range(P):
+        ref_idx, ref_used = c_oracle.assign(px, pals[p])
+        np.testing.assert_array_equal(ip.getIndices(p), ref_idx.astype(np.uint8), err_msg=f"palette {p}")
+        np.testing.assert_array_equal(used[p], ref_used, err_msg=f"palette {p}")
+
+
 @pytest.mark.parametrize("P", [1, 2, 3, 5, 6, 8])
 def test_assign_group_sizes(ip, P):
     """Groups of 1-4 palettes per pixel pass (P = 5: a full group and a group of
@@ -817,15 +844,15 @@ def test_config3_4096_k256_p4_vs_oracle(gpu, filt):
     """C3 (4096x4096, K = 256, P = 4 per launch, the bench's population): the
     device LabRef equals the oracle's to 2e-4; every palette's cost is within
     1e-4 relative of the oracle's end to end (oracle LabRef on the oracle side,
-    device LabRef on the device side); indices of palettes 0 and 3 and all used
-    flags bit-exact."""
+    device LabRef on the device side); every palette's indices and used flags
+    bit-exact."""
     w = h = 4096
     K, P = 256, 4
     R, G, B = o.synthetic_image(w, h, seed=1)
     m = _planar_ctx(gpu, R, G, B, w, h, filt.illum)
     pals = np.stack([o.synthetic_palette(K, 2 + p) for p in range(P)])
     costs, used = m.computeQuantizationErrorPopulation(pals.reshape(P, -1), 2.0, return_used=True)
-    idx = {p: m.getIndices(p) for p in (0, 3)}
+    idx = {p: m.getIndices(p) for p in range(P)}
     lab_dev = m.getLabRef().reshape(-1, 4)
     m.close()
     nt = _threads()

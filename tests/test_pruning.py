@@ -3,7 +3,9 @@
 
 - the box-bound candidate test dmin^2(B, k) <= T(B) (1 + 1e-5), T = min_j dmax^2;
 - the dominance pruning: a is dropped when f_min = min over the box of
-  |p - a|^2 - |p - b*|^2 exceeds 1e-5 (dmax^2(B, a) + S).
+  |p - a|^2 - |p - b*|^2 exceeds 1e-5 (dmax^2(B, a) + S);
+- for lists still longer than an 8-B level-2 entry holds (7), the same test
+  against every other listed colour (build_grid's prune_long_lists).
 
 Each is checked against the reference's own argmin (CL:179-192: sqrtf of the
 unfused fp32 d^2, first minimum in ascending index) over dense pixel sets
@@ -74,7 +76,7 @@ def ref_argmin(px, pal):
     return np.argmin(d, axis=1)  # first minimum
 
 
-def check_palette(pal, G2, rng, cells=60):
+def check_palette(pal, G2, rng, cells=60, long_cap=7):
     pal = pal.astype(np.float32)
     inv = f32(1) / f32(G2)
     kept_total = dropped_total = 0
@@ -87,6 +89,8 @@ def check_palette(pal, G2, rng, cells=60):
         cand = np.nonzero(dmin <= T * f32(1 + 1e-5))[0]
         bstar = cand[np.argmin(dmax[cand])]
         keep = [k for k in cand if k == bstar or not dominated(pal[k], pal[bstar], lo, hi)]
+        if len(keep) > long_cap:  # build_grid's second pass (prune_long_lists): every pair
+            keep = [k for k in keep if not any(j != k and dominated(pal[k], pal[j], lo, hi) for j in keep)]
         kept_total += len(keep)
         dropped_total += len(cand) - len(keep)
         win = np.unique(ref_argmin(box_pixels(lo, hi, rng), pal))
@@ -102,6 +106,18 @@ def test_pruning_never_drops_a_winner_random():
         kept, d = check_palette(pal, G2, rng)
         dropped += d
     assert dropped > 0  # the test does prune on random palettes
+
+
+def test_pairwise_pruning_of_long_lists_never_drops_a_winner():
+    """The pairwise pass on every list (long_cap 0), clustered palettes whose
+    cells list many colours: a colour dominated by any listed colour never wins."""
+    rng = np.random.default_rng(21)
+    for G2 in (16, 32):
+        centres = rng.random((8, 3), dtype=np.float32)
+        pal = (centres[rng.integers(0, 8, 256)] + rng.normal(0, 0.03, (256, 3))).astype(np.float32)
+        pal = np.clip(pal, 0, 1)
+        kept, dropped = check_palette(pal, G2, rng, cells=40, long_cap=0)
+        assert dropped > 0
 
 
 def test_pruning_never_drops_a_winner_adversarial():
