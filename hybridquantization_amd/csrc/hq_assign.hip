@@ -12,6 +12,9 @@
 #ifndef HQ_ASSIGN_PRED
 #define HQ_ASSIGN_PRED 2
 #endif
+#ifndef HQ_ASSIGN_DEPTH
+#define HQ_ASSIGN_DEPTH 1  // pixels the level-2 lookups run ahead of the resolve (1 or 2)
+#endif
 #ifndef HQ_ASSIGN_JOINT
 #define HQ_ASSIGN_JOINT 0  // 1: argmin_group over the whole group in lockstep (measured slower:
                            // 0.218 vs 0.199 ms at C3 P=4, fewer waves and longer walks)
@@ -349,6 +352,8 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
         inside = U8 ? true : r >= 0.f && r <= 1.f && g >= 0.f && g <= 1.f && b >= 0.f && b <= 1.f;
 #ifdef HQ_ABL_HASHLOOKUP  // timing ablation (wrong results): a random line, independent of the RGB
         const uint8_t* lb = lines + ((q * 2654435761u) >> 17) * (uint32_t)kL2Line;
+#elif defined(HQ_ABL_COHERENT)  // timing ablation (wrong results): runs of 256 consecutive pixels share a cell
+        const uint8_t* lb = lines + (((q >> 8) * 40503u) & (uint32_t)(G2 * G2 * G2 - 1)) * (uint32_t)kL2Line;
 #else
         const uint8_t* lb = lines + (inside ? (uint32_t)quad_cell(r, g, b, G2) : 0u) * (uint32_t)kL2Line;
 #endif
@@ -385,20 +390,34 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
     // ties are re-resolved in a called function): a conditional load into a
     // register that a later step overwrites made the compiler wait for every
     // load in flight before that write.
-    RawPx<U8> rb[2];                  // RGB loads in flight: pixel i+1 / i+2 by parity
-    float xr[2], xg[2], xb[2];        // RGB of pixels being looked up / resolved
-    L2E E[2][NG];
-    bool in_[2];
-    uint32_t qq[2];
-    {
+#if HQ_ASSIGN_DEPTH == 2
+    // Lookups two pixels ahead (HQ_ASSIGN_DEPTH 2): three buffer sets by i % 3;
+    // at step i, E[i%3] and E[(i+1)%3] are in flight, RGB(i+2) and RGB(i+3)
+    // too (rb[(i+2)%3], rb[i%3]).
+    constexpr int NB = 3;
+#else
+    constexpr int NB = 2;
+#endif
+    RawPx<U8> rb[NB];                 // RGB loads in flight
+    float xr[NB], xg[NB], xb[NB];     // RGB of pixels being looked up / resolved
+    L2E E[NB][NG];
+    bool in_[NB];
+    uint32_t qq[NB];
+#pragma unroll
+    for (int j = 0; j < NB - 1; ++j) {
         RawPx<U8> x0;
-        load_rgb(qpos(0), x0);
-        unpack(x0, xr[0], xg[0], xb[0]);
+        load_rgb(qpos(j), x0);
+        unpack(x0, xr[j], xg[j], xb[j]);
+        qq[j] = qpos(j);
+        lookup(qq[j], xr[j], xg[j], xb[j], in_[j], E[j]);
     }
-    qq[0] = qpos(0);
-    lookup(qq[0], xr[0], xg[0], xb[0], in_[0], E[0]);
+#if HQ_ASSIGN_DEPTH == 2
+    load_rgb(qpos(2), rb[2]);
+    load_rgb(qpos(3), rb[0]);
+#else
     load_rgb(qpos(1), rb[1]);
     load_rgb(qpos(2), rb[0]);
+#endif
     // The palette table is filled while the first pixels' loads are in flight
     // (the fill used to come first: one more memory round trip per workgroup).
     static_assert(kMaxK == 256, "one table entry per thread and palette");
@@ -451,6 +470,24 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
             }
         }
     };
+#if HQ_ASSIGN_DEPTH == 2
+    auto step = [&](int i, int h) {  // h == i % 3, a compile-time constant at each call
+        const int a = (h + 2) % 3, f = (h + 1) % 3;
+        qq[a] = qpos(i + 2);
+        unpack(rb[a], xr[a], xg[a], xb[a]);  // RGB(i+2): landed
+        lookup(qq[a], xr[a], xg[a], xb[a], in_[a], E[a]);
+        load_rgb(qpos(i + 4), rb[f]);        // rb[f] held RGB(i+1), unpacked a step ago
+        resolve(h);
+    };
+    int i = 0;
+    for (; i + 3 <= npx; i += 3) {
+        step(i, 0);
+        step(i + 1, 1);
+        step(i + 2, 2);
+    }
+    if (i < npx) step(i, 0);
+    if (i + 1 < npx) step(i + 1, 1);
+#else
     auto step = [&](int i, int h) {  // h == i & 1, a compile-time constant at each call
         const int n = h ^ 1;
         qq[n] = qpos(i + 1);
@@ -465,6 +502,7 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
         step(i + 1, 1);
     }
     if (i < npx) step(i, 0);
+#endif
 #ifdef HQ_ASSIGN_TIMING
     t_loop = wall_clock64();
 #endif
