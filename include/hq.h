@@ -191,6 +191,8 @@ int hq_profile_reset(hq_ctx *ctx);
  *   "cost_variant" 0 = fast tiled path (default; filters up to halfSize 24), 1 = generic
  *                  two-pass path (any filter length; the fast path's cross-check)
  *   "cost_rows"    fast path tiles: 16 (16 x 128 outputs, default) or 8 (8 x 108)
+ *   "cost_tw"      16-row tiles at the default filter width: 128 columns (4 waves,
+ *                  default) or 256 (8 waves per workgroup)
  *   "trim"         1 = skip the narrow k1 filters' taps below 1e-9 of their peak
  *                  (default; only when the filters allow it), 0 = all taps
  *   "assign_blocks_per_cu" workgroups per CU of the assign grid (0 = default: one
