@@ -268,16 +268,7 @@ __device__ __forceinline__ int64_t quad_cell(float r, float g, float b, int G2) 
 // last group, launched on its own): every palette slot is live, so the
 // resolve step has no data-dependent exits.  A group below 4 loads only its NG
 // 16-B entries of each 64-B level-2 line and keeps NG palette tables.
-// k/255 exactly as the host's float division makes it, from the byte k: the
-// product with RN(1/255) is off by one ulp for 126 of the 256 values; one FMA
-// residual step corrects all 256 (checked exhaustively, tests/test_assign_u8.py).
-__device__ __forceinline__ float u8_unit(uint32_t v, int j) {
-    const float k = (float)((v >> (8 * j)) & 0xffu);
-    const float c = 1.0f / 255.0f;
-    const float q = k * c;
-    const float r = __builtin_fmaf(-q, 255.0f, k);
-    return __builtin_fmaf(r, c, q);
-}
+// (u8_unit, hq_device.h: k/255 bit-exactly from the byte k)
 
 // A pixel's colour while its load is in flight: three planar floats, or the
 // packed bytes of an 8-bit image (one dword, one register).
@@ -472,11 +463,11 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
     };
 #if HQ_ASSIGN_DEPTH == 2
     auto step = [&](int i, int h) {  // h == i % 3, a compile-time constant at each call
-        const int a = (h + 2) % 3, f = (h + 1) % 3;
-        qq[a] = qpos(i + 2);
-        unpack(rb[a], xr[a], xg[a], xb[a]);  // RGB(i+2): landed
-        lookup(qq[a], xr[a], xg[a], xb[a], in_[a], E[a]);
-        load_rgb(qpos(i + 4), rb[f]);        // rb[f] held RGB(i+1), unpacked a step ago
+        const int ia = (h + 2) % 3, fi = (h + 1) % 3;  // (not `a`: the kernel's AssignArgs)
+        qq[ia] = qpos(i + 2);
+        unpack(rb[ia], xr[ia], xg[ia], xb[ia]);  // RGB(i+2): landed
+        lookup(qq[ia], xr[ia], xg[ia], xb[ia], in_[ia], E[ia]);
+        load_rgb(qpos(i + 4), rb[fi]);           // rb[fi] held RGB(i+1), unpacked a step ago
         resolve(h);
     };
     int i = 0;

@@ -207,6 +207,17 @@ __device__ __forceinline__ double wave_sum_to_lane63(double v) {
     return v;
 }
 
+// k/255 exactly as the host's float division makes it, from byte j of v: the
+// product with RN(1/255) is off by one ulp for 126 of the 256 values; one FMA
+// residual step corrects all 256 (checked exhaustively, tests/test_assign_u8.py).
+__device__ __forceinline__ float u8_unit(uint32_t v, int j) {
+    const float k = (float)((v >> (8 * j)) & 0xffu);
+    const float c = 1.0f / 255.0f;
+    const float q = k * c;
+    const float r = __builtin_fmaf(-q, 255.0f, k);
+    return __builtin_fmaf(r, c, q);
+}
+
 // ----------------------------------------------------------------------------
 // XCD-aware relabelling of a 1-D grid of N workgroups.  Workgroups are placed
 // round-robin over the 8 XCDs (b % 8), so XCD x is given the contiguous work

@@ -57,13 +57,14 @@ struct PaletteArgs {
 // of workgroups, makes each thread's pixel sequence a grid stride: every thread
 // gets the same number of pixels +-1 (512-row shard 0.1306 -> 0.1261 ms per
 // step vs 4 pixels per chunk at 16 workgroups per CU; 4096^2 unchanged).
-constexpr int kSaMaxP = 64;
+constexpr int kSaMaxP = 64;        // device-resident SWASA: largest population
 // Used-colour bits are kept in kUsedSlots copies, used_stride(P) words apart
 // (256-B multiples): assign's workgroups OR theirs into copy blockIdx & 7, the
 // readers OR the copies.  One copy took every workgroup's atomic at the end of
 // the launch (C2, P = 1: 2048 workgroups on one 32-B word set, +14 us).
 constexpr int kUsedSlots = 8;
-inline int used_stride(int P) { return (P * 8 + 63) / 64 * 64; }       // device-resident SWASA: largest population
+// words per used-bit copy: P palettes x 8 words, rounded up to 64 words (256 B)
+inline int used_stride(int P) { return (P * 8 + 63) / 64 * 64; }
 constexpr int kFoldMaxP = 8;      // largest population whose accept step folds the finalize
 
 // sa_step_kernel: one accept + generate step of the device-resident SWASA search.

@@ -46,6 +46,7 @@ hipError_t launch_cost_generic(const GenArgs&, int de, bool idx32, hipStream_t);
 hipError_t launch_prep_wide(const WideArgs&, int P, hipStream_t);
 hipError_t launch_assign_wide(const WideArgs&, int P, hipStream_t);
 hipError_t launch_finalize(const FinalizeArgs&, int P, hipStream_t);
+hipError_t launch_pack_u8(const float*, const float*, const float*, uint32_t*, int*, int64_t, hipStream_t);
 hipError_t launch_labref_opp(const float*, const float*, const float*, float4*, int64_t, hipStream_t);
 hipError_t launch_xyz_to_opp(const float4*, float4*, int64_t, hipStream_t);
 hipError_t launch_rgb_to_xyz(const float*, const float*, const float*, float4*, int64_t, hipStream_t);
@@ -291,33 +292,21 @@ int set_image_common(hq_ctx* c, const std::vector<float>& R, const std::vector<f
     HIP_TRY(c, hipMemcpyAsync(c->d_B.p, B.data(), plane, hipMemcpyHostToDevice, c->stream));
     // An image whose channels are all exactly k/255 (the reference's int-RGB
     // source, IM:100) is also kept as packed bytes: assign reads 4 B per pixel
-    // instead of 12 and rebuilds k/255 exactly (u8_unit, hq_assign.hip).
+    // instead of 12 and rebuilds k/255 exactly (u8_unit).  The check and the
+    // packing run on the device (pack_u8_kernel); only a 4-byte flag returns.
     {
-        std::vector<uint32_t> px((size_t)round_up(g.n_ext, 4), 0u);
-        float unit[256];
-        for (int k = 0; k < 256; ++k) unit[k] = (float)k / 255.0f;
-        bool u8 = true;
-        const std::vector<float>* ch[3] = {&R, &G, &B};
-        for (int64_t i = 0; i < g.n_ext && u8; ++i) {
-            uint32_t v = 0;
-            for (int j = 0; j < 3; ++j) {
-                const float f = (*ch[j])[i];
-                if (!(f >= 0.f && f <= 1.f)) { u8 = false; break; }
-                const int k = (int)std::lround(f * 255.0f);
-                if (std::memcmp(&unit[k], &f, 4) != 0) { u8 = false; break; }
-                v |= (uint32_t)k << (8 * j);
-            }
-            px[i] = v;
-        }
-        c->img_u8 = u8;
-        if (u8) {
-            HIP_TRY(c, c->d_rgbx.ensure(sizeof(uint32_t) * px.size()));
-            HIP_TRY(c, hipMemcpyAsync(c->d_rgbx.p, px.data(), sizeof(uint32_t) * px.size(),
-                                      hipMemcpyHostToDevice, c->stream));
-            HIP_TRY(c, hipStreamSynchronize(c->stream));
-        } else {
-            c->d_rgbx.release();
-        }
+        HIP_TRY(c, c->d_rgbx.ensure(sizeof(uint32_t) * (size_t)round_up(g.n_ext, 4)));
+        DevBuf flag;
+        HIP_TRY(c, flag.ensure(sizeof(int)));
+        HIP_TRY(c, hipMemsetAsync(flag.p, 0, sizeof(int), c->stream));
+        HIP_TRY(c, launch_pack_u8(c->d_R.as<float>(), c->d_G.as<float>(), c->d_B.as<float>(),
+                                  c->d_rgbx.as<uint32_t>(), flag.as<int>(), g.n_ext, c->stream));
+        int not_u8 = 1;
+        HIP_TRY(c, hipMemcpyAsync(&not_u8, flag.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        flag.release();
+        c->img_u8 = not_u8 == 0;
+        if (!c->img_u8) c->d_rgbx.release();
     }
     if (illum) std::memcpy(c->illum, illum, sizeof c->illum);
     const int own = g.r1 - g.r0;

@@ -8,6 +8,32 @@
 namespace hq {
 
 // ----------------------------------------------------------------------------
+// Packed 8-bit copy of the image (assign's U8 path): pixel q -> R | G << 8 |
+// B << 16 when every channel is exactly k/255 (IM:100's int-RGB source, bit
+// for bit: u8_unit); any other value (off the lattice, outside [0, 1], -0,
+// NaN) sets *not_u8, and the host then drops the copy.  One pass on the
+// device instead of a host scan of every pixel.
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void pack_u8_kernel(const float* R, const float* G, const float* B,
+                                                      uint32_t* out, int* not_u8, int64_t n) {
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    bool bad = false;
+    if (q < n) {
+        const float f[3] = {R[q], G[q], B[q]};
+        uint32_t v = 0;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const bool in = f[j] >= 0.f && f[j] <= 1.f;
+            const uint32_t k = in ? (uint32_t)__builtin_rintf(f[j] * 255.0f) : 0u;
+            bad |= !in || __float_as_uint(u8_unit(k, 0)) != __float_as_uint(f[j]);
+            v |= k << (8 * j);
+        }
+        out[q] = v;
+    }
+    if (__ballot(bad) && __lane_id() == 0) *not_u8 = 1;  // idempotent plain store
+}
+
+// ----------------------------------------------------------------------------
 // LabRef (setup, once per search): IM:100-153 + IM:285-370 on the device.
 // ----------------------------------------------------------------------------
 // planar R,G,B -> Opp float4 (CL:79-90 then CL:111-116)
@@ -164,6 +190,12 @@ __global__ __launch_bounds__(256) void error_image_kernel(const float4* orig, co
 // ----------------------------------------------------------------------------
 // Launchers
 // ----------------------------------------------------------------------------
+hipError_t launch_pack_u8(const float* R, const float* G, const float* B, uint32_t* out, int* not_u8,
+                          int64_t n, hipStream_t s) {
+    HQ_LAUNCH(pack_u8_kernel, dim3(blocks_for(n)), dim3(256), 0, s, R, G, B, out, not_u8, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_labref_opp(const float* R, const float* G, const float* B, float4* opp,
                              int64_t n, hipStream_t s) {
     hipLaunchKernelGGL(labref_opp_kernel, dim3(blocks_for(n)), dim3(256), 0, s, R, G, B, opp, n);

@@ -697,10 +697,12 @@ def test_device_search_with_single_rank_comm(gpu, filt):
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("w,h,P", [(1003, 517, 4), (1003, 517, 3), (37, 29, 5)])
 def test_assign_workgroup_count_invariance(gpu, filt, w, h, P):
-    """The assign grid (option assign_blocks_per_cu: 1 workgroup per CU up to 64,
-    default 16) only changes which workgroup takes which pixel chunk: indices,
-    used flags and costs are bitwise the same for every count, also when an
-    image has fewer chunks than workgroups (37 x 29)."""
+    """The assign grid (option assign_blocks_per_cu: 1 to 64 workgroups per CU)
+    only changes which workgroup takes which pixels.  The reference run uses
+    the default, 0 = auto (one resident round from the occupancy query, at
+    least HQ_ASSIGN_MINPX pixels per thread); indices, used flags and costs at
+    every listed count must equal it bit for bit, also when an image has
+    fewer pixel chunks than workgroups (37 x 29)."""
     K = 256
     R, G, B = o.synthetic_image(w, h, seed=11)
     m = _planar_ctx(gpu, R, G, B, w, h, filt.illum)
