@@ -42,9 +42,10 @@ def synthetic_planes(w, h, seed=1):
     return [((z >> np.uint64(8 * c)) & np.uint64(0xFF)).astype(np.float32) / s for c in range(3)]
 
 
-def measured_traffic(size, K, P, grid, world, kernel):
+def measured_traffic(size, K, P, grid, world, kernel, dpi=72, distance=45.0):
     """HBM bytes per launch of `kernel` from the newest committed PMC passes
-    (profiles/rNN_hbm_traffic.json), or None when none matches this config."""
+    (profiles/rNN_hbm_traffic.json), or None when none matches this config
+    (image size, K, P, grid and viewing geometry)."""
     import glob
 
     paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_hbm_traffic.json")))
@@ -55,6 +56,8 @@ def measured_traffic(size, K, P, grid, world, kernel):
             continue
         c = d.get("config", {})
         if world != 1 or (c.get("size"), c.get("K"), c.get("P"), c.get("grid")) != (size, K, P, grid):
+            continue
+        if (c.get("dpi", 72), float(c.get("distance", 45.0))) != (dpi, float(distance)):
             continue
         for name, v in d.get("kernels", {}).items():
             if name.startswith("hq::" + kernel):
@@ -298,20 +301,35 @@ def main():
     # Dominant kernel: the cost kernel (S-CIELAB stencil + Opp->Lab + dE76).  With P > 1
     # palettes per launch its HBM bytes (LabRef once + P index images) amortise
     # and FP32 VALU bounds it.  Algorithmic flops per pixel-eval: the
-    # reference's stencil, 7 separable filters x 2 passes x 21 taps x 2 flops = 588,
-    # + Opp->Lab / dE76 ~ 40 (nominal 628); the kernel executes 2 x 111 significant
-    # taps (the narrow k1 filters trimmed) + Lab / dE = 484 (DESIGN.md "Roofline").
+    # reference's stencil, 7 separable filters x 2 passes x (2 half + 1) taps x 2
+    # flops (588 at the default half 10), + Opp->Lab / dE76 ~ 40.  Executed: the
+    # fast path runs the filters centred in its tap bucket HB (2 HB + 1 taps), the
+    # narrow k1 filters over their trimmed windows only (2 trim_w + 1 taps,
+    # hq_cost.hip trim_w); the generic path runs the filters as designed.
+    half = m.halfSize
+    rows = int(opts.get("cost_rows", 16))
+    variant = int(opts.get("cost_variant", 0))
+    hb = next((b for b in (10, 15, 19, 24) if half <= b), 0)
+    generic = variant == 1 or hb == 0 or args.K > 256
+    trim_w = {10: (3, 4, 5), 15: (4, 5, 7), 19: (5, 7, 9), 24: (6, 9, 12)}
+    if generic:
+        kernel = "gen_hpass_kernel+gen_vpass_kernel"
+        taps_exec = 7 * (2 * half + 1)
+    else:
+        kernel = "cost_mfma_kernel" if rows == 8 and hb == 10 else "cost16w_kernel"
+        trim = int(opts.get("trim", 1)) != 0
+        taps_exec = 4 * (2 * hb + 1) + (sum(2 * t + 1 for t in trim_w[hb]) if trim else 3 * (2 * hb + 1))
     cost_ms = prof["cost"][0]
-    alg_flops = n_own * P * (588 + 40)
-    exec_flops = n_own * P * (2 * 2 * 111 + 40)
+    flops_nominal = 7 * 2 * (2 * half + 1) * 2 + 40
+    flops_exec = 2 * 2 * taps_exec + 40
+    alg_flops = n_own * P * flops_nominal
+    exec_flops = n_own * P * flops_exec
     achieved_tf = alg_flops / (cost_ms * 1e-3) / 1e12 if cost_ms > 0 else 0.0
     exec_tf = exec_flops / (cost_ms * 1e-3) / 1e12 if cost_ms > 0 else 0.0
-    alg_bytes = n_own * (12 + P)
+    alg_bytes = n_own * (12 + P * (4 if args.K > 256 else 1))
     hbm_gbs = alg_bytes / (cost_ms * 1e-3) / 1e9 if cost_ms > 0 else 0.0
-    rows = int(opts.get("cost_rows", 16))
-    kernel = ("gen_vpass_kernel" if int(opts.get("cost_variant", 0)) == 1
-              else "cost_mfma_kernel" if rows == 8 else "cost16w_kernel")
-    traffic = measured_traffic(W, args.K, P, args.grid, world, kernel)
+    traffic = measured_traffic(W, args.K, P, args.grid, world, kernel.split("+")[0],
+                               args.dpi, args.distance)
     # whole-evaluation view: the metric's 24 B/px-eval HBM-read roofline
     eval_roof_mpx = HBM_PEAK_GBS * 1e9 / 24.0 / 1e6 * world
     out = {
@@ -340,6 +358,8 @@ def main():
                      "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4),
                      "traffic": traffic,
                      "kernel": kernel, "kernel_avg_ms": round(cost_ms, 4),
+                     "flops_per_px_eval": flops_nominal, "exec_flops_per_px_eval": flops_exec,
+                     "half": half, "tap_bucket": None if generic else hb,
                      "alg_flops_per_launch": alg_flops, "exec_flops_per_launch": exec_flops,
                      "frac_executed_taps": round(exec_tf / FP32_PEAK_TFLOPS, 4),
                      "alg_bytes_per_launch": alg_bytes, "hbm_GBs_alg": round(hbm_gbs, 1),
@@ -347,10 +367,10 @@ def main():
                      "note": "fp32-accurate stencil: vertical taps on the matrix cores as split-f16 "
                              "products (hi*hi+hi*lo+lo*hi, fp32 accumulate), horizontal taps, Lab and dE on "
                              "FP32 VALU.  bound valu: the compute roof is the FP32 vector peak, 157.3 TFLOP/s "
-                             "(the f32 MFMA peak is the same number on gfx950); achieved = the nominal 628 "
-                             "flop/px-eval of the reference's stencil + Lab/dE over the kernel time; "
-                             "frac_executed_taps = the 484 flop/px-eval the kernel executes (trimmed narrow "
-                             "filters); hbm_frac = the kernel's algorithmic bytes (LabRef 12 B + P index bytes "
+                             "(the f32 MFMA peak is the same number on gfx950); achieved = the nominal "
+                             "7*2*(2 half+1)*2 + 40 flop/px-eval of the reference's stencil + Lab/dE (628 at "
+                             "half 10) over the kernel time (all P palettes' launches); frac_executed_taps = "
+                             "the flops the kernel executes (bucket taps, trimmed narrow filters); hbm_frac = the kernel's algorithmic bytes (LabRef 12 B + P index bytes "
                              "per pixel) over its time against 8 TB/s; traffic = HBM bytes/launch from the "
                              "committed rocprofv3 FETCH_SIZE(x2)+WRITE_SIZE passes when their config matches; "
                              "kernel_avg_ms: HIP events carried by the launches on the context stream over a "

@@ -63,6 +63,7 @@ SIGNATURES = {
     "hq_eval_population_partial": (C.c_int, [_ctx, _f, C.c_int, C.c_int, _d]),
     "hq_get_indices": (C.c_int, [_ctx, C.c_int, _u8]),
     "hq_get_indices32": (C.c_int, [_ctx, C.c_int, C.POINTER(C.c_uint32)]),
+    "hq_get_pixel_errors": (C.c_int, [_ctx, C.c_int, _f]),
     "hq_quantize": (C.c_int, [_ctx, _f, C.c_int64, _f, C.c_int, _f, _i32]),
     "hq_compute_error": (C.c_int, [_ctx, _f, _f, C.c_int64, _f, _d]),
     "hq_comm_unique_id": (C.c_int, [C.POINTER(C.c_ubyte)]),

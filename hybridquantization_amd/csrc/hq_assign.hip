@@ -526,44 +526,208 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
 }
 
 // ----------------------------------------------------------------------------
+// assign_quad: the same argmin, pipeline and grid as assign_pipe_kernel, but a
+// lane owns 4 consecutive pixels ("quads", a grid stride of quads): their
+// packed colours arrive in one 16-B load, and each palette's 4 index bytes
+// leave in one dword store, so a wave writes 256 contiguous bytes per palette
+// (whole 128-B lines) instead of 64 single bytes (half a line; write traffic
+// 1.27x the index bytes in r03_hbm_traffic.json).  Quad data is loaded 4 pixel
+// steps ahead of its first lookup.  Pixels past the image (the last quad's
+// padding, quads past the grid stride) are resolved but never stored or
+// counted as used; the last quad's padding bytes land in the index image's
+// slack (idx_pitch >= n_ext + 4), which no reader uses.
+// ----------------------------------------------------------------------------
+template <bool U8> struct RawQuad { float4 r, g, b; };
+template <> struct RawQuad<true> { uint4 v; };
+
+__device__ __forceinline__ uint32_t u4_at(const uint4& v, int u) {
+    return u == 0 ? v.x : u == 1 ? v.y : u == 2 ? v.z : v.w;
+}
+__device__ __forceinline__ float f4_at(const float4& v, int u) {
+    return u == 0 ? v.x : u == 1 ? v.y : u == 2 ? v.z : v.w;
+}
+
+template <int NG, bool U8>
+__global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_quad_kernel(AssignArgs a, int grp0, int ngroups) {
+    __shared__ __attribute__((aligned(16))) float4 s_pal[NG * kMaxK];
+    __shared__ uint32_t s_used[NG][8];
+    const int w = xcd_remap(blockIdx.x, a.nblocks * ngroups);
+    const int grp = grp0 + w / a.nblocks, blk = w % a.nblocks, tid = threadIdx.x;
+    const int p0 = 4 * grp;
+    const uint8_t* lines = a.lvl2 + (int64_t)grp * a.lvl2_gstride;
+    const int G2 = a.G2 > 0 ? a.G2 : 4;
+    const uint32_t n_ext = (uint32_t)a.n_ext;
+    const uint32_t nquad = (n_ext + 3u) >> 2, dlast = nquad - 1u;
+    const uint32_t cstride = (uint32_t)a.nblocks * 256u;  // quads
+    const uint32_t dbase = (uint32_t)blk * 256u + (uint32_t)tid;
+    // every lane runs lane 0's quad count (argmin_fix needs the whole wave)
+    const int nq0 = dbase < nquad ? (int)((nquad - 1u - dbase) / cstride) + 1 : 0;
+    const int nq = __builtin_amdgcn_readfirstlane(nq0);
+    auto dpos = [&](int i) { return dbase + (uint32_t)i * cstride; };
+    auto load_quad = [&](uint32_t d, RawQuad<U8>& x) {
+        const uint32_t dc = min(d, dlast) << 4;  // byte offset of the quad (16 B per channel)
+        if constexpr (U8) {
+            x.v = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.rgbx) + dc);
+        } else {
+            x.r = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(a.R) + dc);
+            x.g = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(a.G) + dc);
+            x.b = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(a.B) + dc);
+        }
+    };
+    auto px_of = [&](const RawQuad<U8>& x, int u, float& r, float& g, float& b) {
+        if constexpr (U8) {
+            const uint32_t v = u4_at(x.v, u);
+            r = u8_unit(v, 0);
+            g = u8_unit(v, 1);
+            b = u8_unit(v, 2);
+        } else {
+            r = f4_at(x.r, u);
+            g = f4_at(x.g, u);
+            b = f4_at(x.b, u);
+        }
+    };
+    auto lookup = [&](float r, float g, float b, bool& inside, L2E (&e)[NG]) {
+        inside = U8 ? true : r >= 0.f && r <= 1.f && g >= 0.f && g <= 1.f && b >= 0.f && b <= 1.f;
+        const uint8_t* lb = lines + (inside ? (uint32_t)quad_cell(r, g, b, G2) : 0u) * (uint32_t)kL2Line;
+        const uint4* line = reinterpret_cast<const uint4*>(lb);
+        if constexpr (kL2Bytes == 16) {
+#pragma unroll
+            for (int pp = 0; pp < NG; ++pp) e[pp] = line[pp];
+        } else {
+#pragma unroll
+            for (int pp = 0; pp + 1 < NG; pp += 2) {
+                const uint4 v = line[pp >> 1];
+                l2_set(e[pp], v.x, v.y);
+                l2_set(e[pp + 1], v.z, v.w);
+            }
+            if constexpr (NG & 1) e[NG - 1] = reinterpret_cast<const L2E*>(lb)[NG - 1];
+        }
+    };
+    RawQuad<U8> xq[2];            // quads: i & 1
+    float xr[2], xg[2], xb[2];    // pixels being looked up / resolved: step parity
+    L2E E[2][NG];
+    bool in_[2];
+    uint32_t acc[NG];             // index bytes of the current quad, per palette
+    load_quad(dpos(0), xq[0]);
+    px_of(xq[0], 0, xr[0], xg[0], xb[0]);
+    lookup(xr[0], xg[0], xb[0], in_[0], E[0]);
+    load_quad(dpos(1), xq[1]);
+    static_assert(kMaxK == 256, "one table entry per thread and palette");
+#pragma unroll
+    for (int pp = 0; pp < NG; ++pp)
+        s_pal[pp * kMaxK + tid] = a.pal[(int64_t)(p0 + pp) * kMaxK + min(tid, a.K - 1)];
+    if (tid < 8 * NG) s_used[tid >> 3][tid & 7] = 0;
+    __syncthreads();
+    uint32_t* idx_base[NG];
+    bool exh_pal[NG];
+#pragma unroll
+    for (int pp = 0; pp < NG; ++pp) {
+        idx_base[pp] = reinterpret_cast<uint32_t*>(a.idx + (int64_t)(p0 + pp) * a.idx_pitch);
+        exh_pal[pp] = a.pflags[p0 + pp] != 0 || a.G2 == 0;
+        acc[pp] = 0u;
+    }
+    // step (quad i, pixel u): quad parity qp = i & 1 and u are compile-time
+    auto step = [&](int i, int qp, int u) {
+        const int h = u & 1, n = h ^ 1;
+        if (u < 3) px_of(xq[qp], u + 1, xr[n], xg[n], xb[n]);
+        else px_of(xq[qp ^ 1], 0, xr[n], xg[n], xb[n]);
+        lookup(xr[n], xg[n], xb[n], in_[n], E[n]);
+        if (u == 3) load_quad(dpos(i + 2), xq[qp]);  // this quad's buffer is free now
+        const uint32_t d = dpos(i);
+        const uint32_t q = (d << 2) + (uint32_t)u;
+#pragma unroll
+        for (int pp = 0; pp < NG; ++pp) {
+            const L2E e1[1] = {E[h][pp]};
+            const bool x1[1] = {exh_pal[pp]};
+            int k1[1];
+            argmin_group<1>(xr[h], xg[h], xb[h], e1, in_[h], x1, s_pal + pp * kMaxK, a.lvl1, a.lvl1_pitch,
+                            p0 + pp, G2, a.K, k1);
+            const int k = k1[0];
+            acc[pp] = u == 0 ? (uint32_t)k : acc[pp] | ((uint32_t)k << (8 * u));
+            if (q < n_ext) {
+                const uint32_t bit = 1u << (k & 31);
+                if (!(s_used[pp][k >> 5] & bit)) atomicOr(&s_used[pp][k >> 5], bit);
+            }
+        }
+        if (u == 3 && (d << 2) < n_ext) {
+#pragma unroll
+            for (int pp = 0; pp < NG; ++pp) __builtin_nontemporal_store(acc[pp], idx_base[pp] + d);
+        }
+    };
+    int i = 0;
+    for (; i + 2 <= nq; i += 2) {
+        step(i, 0, 0); step(i, 0, 1); step(i, 0, 2); step(i, 0, 3);
+        step(i + 1, 1, 0); step(i + 1, 1, 1); step(i + 1, 1, 2); step(i + 1, 1, 3);
+    }
+    if (i < nq) { step(i, 0, 0); step(i, 0, 1); step(i, 0, 2); step(i, 0, 3); }
+    __syncthreads();
+    if (tid < 8 * NG) {
+        const uint32_t m = s_used[tid >> 3][tid & 7];
+        uint32_t* gw = &a.used_glob[(blockIdx.x & (kUsedSlots - 1)) * a.used_stride + (p0 + (tid >> 3)) * 8 +
+                                    (tid & 7)];
+        const uint32_t seen = __hip_atomic_load(gw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (m & ~seen) atomicOr(gw, m);
+    }
+}
+
+// ----------------------------------------------------------------------------
 // Launcher: the full groups of 4 palettes in one launch, a last group of
 // P mod 4 in a second (the profiling events, when set, bracket both).
 // ----------------------------------------------------------------------------
-template <bool U8>
+template <bool U8, bool QUAD>
 void launch_assign_t(const AssignArgs& a, int P, hipStream_t s) {
     const int full = P / 4, rest = P % 4;
     const hipEvent_t ev0 = t_ev_start, ev1 = t_ev_stop;
+#define HQ_ASG(NG, NB, G0, NGR)                                                                         \
+    do {                                                                                                \
+        if (QUAD) HQ_LAUNCH((assign_quad_kernel<NG, U8>), dim3((unsigned)(NB)), dim3(256), 0, s, a, G0, NGR); \
+        else HQ_LAUNCH((assign_pipe_kernel<NG, U8>), dim3((unsigned)(NB)), dim3(256), 0, s, a, G0, NGR);      \
+    } while (0)
     if (full > 0) {
         if (rest) t_ev_stop = nullptr;
-        HQ_LAUNCH((assign_pipe_kernel<4, U8>), dim3((unsigned)(a.nblocks * full)), dim3(256), 0, s, a, 0, full);
+        HQ_ASG(4, a.nblocks * full, 0, full);
         t_ev_stop = ev1;
         if (rest) t_ev_start = nullptr;
     }
     switch (rest) {
-    case 1: HQ_LAUNCH((assign_pipe_kernel<1, U8>), dim3((unsigned)a.nblocks), dim3(256), 0, s, a, full, 1); break;
-    case 2: HQ_LAUNCH((assign_pipe_kernel<2, U8>), dim3((unsigned)a.nblocks), dim3(256), 0, s, a, full, 1); break;
-    case 3: HQ_LAUNCH((assign_pipe_kernel<3, U8>), dim3((unsigned)a.nblocks), dim3(256), 0, s, a, full, 1); break;
+    case 1: HQ_ASG(1, a.nblocks, full, 1); break;
+    case 2: HQ_ASG(2, a.nblocks, full, 1); break;
+    case 3: HQ_ASG(3, a.nblocks, full, 1); break;
     default: break;
     }
+#undef HQ_ASG
     t_ev_start = ev0;
 }
 
-hipError_t launch_assign(const AssignArgs& a, int P, hipStream_t s) {
-    if (a.rgbx)
-        launch_assign_t<true>(a, P, s);
-    else
-        launch_assign_t<false>(a, P, s);
+// quad: 1 = assign_quad_kernel (4 consecutive pixels per lane, dword index
+// stores), 0 = assign_pipe_kernel (one pixel per lane and step, byte stores)
+hipError_t launch_assign(const AssignArgs& a, int P, hipStream_t s, bool quad) {
+    if (a.rgbx) {
+        if (quad) launch_assign_t<true, true>(a, P, s);
+        else launch_assign_t<true, false>(a, P, s);
+    } else {
+        if (quad) launch_assign_t<false, true>(a, P, s);
+        else launch_assign_t<false, false>(a, P, s);
+    }
     return hipGetLastError();
 }
 
 // Resident workgroups per CU of assign_pipe_kernel<NG> (the auto size of one
 // grid-stride round; the packed and planar forms take the larger register
 // count); 0 if the query fails.
-int assign_residency(int NG) {
+int assign_residency(int NG, bool quad) {
     auto q = [](auto kern) {
         int n = 0;
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, 256, 0) == hipSuccess ? n : 0;
     };
+    if (quad) {
+        switch (NG) {
+        case 1: return std::min(q(assign_quad_kernel<1, false>), q(assign_quad_kernel<1, true>));
+        case 2: return std::min(q(assign_quad_kernel<2, false>), q(assign_quad_kernel<2, true>));
+        case 3: return std::min(q(assign_quad_kernel<3, false>), q(assign_quad_kernel<3, true>));
+        default: return std::min(q(assign_quad_kernel<4, false>), q(assign_quad_kernel<4, true>));
+        }
+    }
     switch (NG) {
     case 1: return std::min(q(assign_pipe_kernel<1, false>), q(assign_pipe_kernel<1, true>));
     case 2: return std::min(q(assign_pipe_kernel<2, false>), q(assign_pipe_kernel<2, true>));

@@ -421,9 +421,12 @@ __global__ __launch_bounds__(256, 6) void cost_mfma_kernel(CostArgs a, int P_) {
         for (int r = 0; r < 2; ++r) {
 #pragma unroll
             for (int xo = 0; xo < HR; ++xo) {
-                const float3 g3 = opp2g_fast(acc0[xo][r], acc1[xo][r], acc2[xo][r], a.m_lab);
-                const float e = delta_e_g<DE>(labv[r][0][xo], labv[r][1][xo], labv[r][2][xo], g3);
-                part += (gy0 + r < g.r1 && gx0 + xo < g.W) ? e : 0.f;
+                const float3 lf = opp2f_fast(acc0[xo][r], acc1[xo][r], acc2[xo][r], a.m_lab);
+                const float e = delta_e_f<DE>(labv[r][0][xo], labv[r][1][xo], labv[r][2][xo], lf);
+                const bool in = gy0 + r < g.r1 && gx0 + xo < g.W;
+                part += in ? e : 0.f;
+                if (a.pix_err && in)  // test option: the per-pixel dE (CL:201-209's error image)
+                    a.pix_err[(int64_t)cur.p * a.pix_pitch + (int64_t)(gy0 + r - g.r0) * g.W + gx0 + xo] = e;
             }
         }
         sum = (double)part;
@@ -789,9 +792,18 @@ __global__ __launch_bounds__(64 * NW, cost16w_waves<HB>()) void cost16w_kernel(C
         const float Bs[4] = {lab[r][2].x, lab[r][2].y, lab[r][2].z, lab[r][2].w};
 #pragma unroll
         for (int xo = 0; xo < HR; ++xo) {
-            const float3 g3 = opp2g_fast(acc0[xo][r], acc1[xo][r], acc2[xo][r], a.m_lab);
-            e[r][xo] = delta_e_g<DE>(Ls[xo], As[xo], Bs[xo], g3);
+            const float3 lf = opp2f_fast(acc0[xo][r], acc1[xo][r], acc2[xo][r], a.m_lab);
+            e[r][xo] = delta_e_f<DE>(Ls[xo], As[xo], Bs[xo], lf);
         }
+    }
+    if (a.pix_err) {  // test option: the per-pixel dE (CL:201-209's error image)
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int xo = 0; xo < HR; ++xo)
+                if (gy0 + r < g.r1 && gx0 + xo < g.W)
+                    a.pix_err[(int64_t)cur.p * a.pix_pitch + (int64_t)(gy0 + r - g.r0) * g.W + gx0 + xo] =
+                        e[r][xo];
     }
     // tiles inside the image and shard (all but the last tile column and row)
     // sum without per-pixel masks
@@ -864,9 +876,11 @@ __global__ __launch_bounds__(256) void gen_vpass_kernel(GenArgs a) {
             oz = fmaf(a.t[2 * n + s], a.k1[4 * t + 2], fmaf(a.t[5 * n + s], a.k2[4 * t + 2], oz));
             ox = fmaf(a.t[6 * n + s], a.absk3[t], ox);
         }
-        const float3 g3 = opp2g_fast(ox, oy, oz, a.m_lab);
+        const float3 lf = opp2f_fast(ox, oy, oz, a.m_lab);
         const int64_t off = (int64_t)(y - a.g.r0) * a.g.lab_pitch + x;
-        e = (double)delta_e_g<DE>(a.labL[off], a.labA[off], a.labB[off], g3);
+        const float ef = delta_e_f<DE>(a.labL[off], a.labA[off], a.labB[off], lf);
+        if (a.pix_err) a.pix_err[q] = ef;  // test option: the per-pixel dE
+        e = (double)ef;
     }
     e = wave_sum(e);
     if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = e;
@@ -877,11 +891,11 @@ __global__ __launch_bounds__(256) void gen_vpass_kernel(GenArgs a) {
 // ----------------------------------------------------------------------------
 // Host side: tap tables, MFMA fragments, launchers
 // ----------------------------------------------------------------------------
-// Opp->XYZ (CL:118) with row r divided by the illuminant's component r and
-// scaled by 116^3 (lab_g_fast works on t' = 116^3 t).
+// Opp->XYZ (CL:118) with row r divided by the illuminant's component r
+// (lab_f_fast works on t = X/Xn, Y/Yn, Z/Zn).
 void opp2xyz_over_illum(const float inv_illum[3], float m[9]) {
     static const float opp2xyz[9] = HQ_OPP2XYZ;
-    for (int i = 0; i < 9; ++i) m[i] = (float)((double)opp2xyz[i] * inv_illum[i / 3] * 1560896.0);
+    for (int i = 0; i < 9; ++i) m[i] = (float)((double)opp2xyz[i] * inv_illum[i / 3]);
 }
 
 // The fast path's tap bucket for a filter half-width H (halfSize, IM:408): the
@@ -1077,13 +1091,19 @@ hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, bool trim, int ti
 }
 
 hipError_t launch_cost_generic(const GenArgs& a, int de, bool idx32, hipStream_t s) {
+    // profiling events (when set) bracket both launches: start on the first, stop on the second
+    const hipEvent_t ev0 = t_ev_start, ev1 = t_ev_stop;
+    t_ev_stop = nullptr;
     if (idx32) HQ_LAUNCH(gen_hpass_kernel<uint32_t>, dim3(blocks_for(a.g.n_ext)), dim3(256), 0, s, a);
     else HQ_LAUNCH(gen_hpass_kernel<uint8_t>, dim3(blocks_for(a.g.n_ext)), dim3(256), 0, s, a);
+    t_ev_start = nullptr;
+    t_ev_stop = ev1;
     const int64_t n_own = (int64_t)a.g.W * (a.g.r1 - a.g.r0);
     if (de == 0)
         HQ_LAUNCH(gen_vpass_kernel<0>, dim3(blocks_for(n_own)), dim3(256), 0, s, a);
     else
         HQ_LAUNCH(gen_vpass_kernel<1>, dim3(blocks_for(n_own)), dim3(256), 0, s, a);
+    t_ev_start = ev0;
     return hipGetLastError();
 }
 

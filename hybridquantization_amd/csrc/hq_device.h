@@ -40,26 +40,25 @@ __device__ __forceinline__ float lab_f(float t) {  // CL:137
     return t > LAB_DELTA3 ? cbrtf(t) : fmaf(LAB_KAPPA, t, 16.0f) * (1.0f / 116.0f);
 }
 
-// The hot path's Opp->Lab (CL:124-145) works on t' = 116^3 t: m = Opp->XYZ with
-// row r divided by the illuminant's component r and multiplied by 116^3
-// (opp2xyz_over_illum), so g(t') = 116 f(t) needs no scaling of its own:
-// cube root as exp2(log2(t')/3) (v_log_f32 / v_exp_f32, about 3 ulp; no Newton
-// step -- the cost tolerance is 1e-4 relative and this moves the mean dE by
-// ~1e-7), the linear segment fma(kappa / 116^3, t', 16), selected branch-free.
-#define LAB_G3 1560896.0f  // 116^3
-__device__ __forceinline__ float lab_g_fast(float t) {
-    constexpr float thr = LAB_DELTA3 * LAB_G3;  // t > delta^3 <=> t' > delta^3 116^3
-    // y is only selected for t' > thr > 0 (for t' <= 0 it is 0 or NaN, discarded)
+// The hot path's Opp->Lab (CL:124-145): m = Opp->XYZ with row r divided by the
+// illuminant's component r (opp2xyz_over_illum), so t = X/Xn etc. is one dot
+// product; cube root as exp2(log2(t)/3) (v_log_f32 / v_exp_f32; ~1 ulp over
+// t in (delta^3, ~1.1]: log2 t stays small, so its fp32 rounding moves the
+// root by ~2e-8 relative on average -- round 3 worked on t' = 116^3 t, whose
+// log2 near 20 carried 6x that), the linear segment fma(kappa / 116, t,
+// 16 / 116), selected branch-free.
+__device__ __forceinline__ float lab_f_fast(float t) {
+    // y is only selected for t > delta^3 > 0 (for t <= 0 it is 0 or NaN, discarded)
     const float y = __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(t) * (1.0f / 3.0f));
-    const float lin = fmaf(LAB_KAPPA / LAB_G3, t, 16.0f);
-    return t > thr ? y : lin;
+    const float lin = fmaf(LAB_KAPPA / 116.0f, t, 16.0f / 116.0f);
+    return t > LAB_DELTA3 ? y : lin;
 }
 
-// 116 (f(X/Xn), f(Y/Yn), f(Z/Zn)) of an opponent colour: L = g.y - 16,
-// a = (500/116)(g.x - g.y), b = (200/116)(g.y - g.z).
-__device__ __forceinline__ float3 opp2g_fast(float o0, float o1, float o2, const float* m) {
-    return make_float3(lab_g_fast(dot3(o0, o1, o2, m + 0)), lab_g_fast(dot3(o0, o1, o2, m + 3)),
-                       lab_g_fast(dot3(o0, o1, o2, m + 6)));
+// (f(X/Xn), f(Y/Yn), f(Z/Zn)) of an opponent colour: L = 116 f.y - 16,
+// a = 500 (f.x - f.y), b = 200 (f.y - f.z).
+__device__ __forceinline__ float3 opp2f_fast(float o0, float o1, float o2, const float* m) {
+    return make_float3(lab_f_fast(dot3(o0, o1, o2, m + 0)), lab_f_fast(dot3(o0, o1, o2, m + 3)),
+                       lab_f_fast(dot3(o0, o1, o2, m + 6)));
 }
 
 // CL:124-145 with true division (setup paths: LabRef, quantize/error image).
@@ -94,18 +93,17 @@ __device__ __forceinline__ float delta_e(float L1, float a1, float b1, float L2,
     }
 }
 
-// dE (CL:201-226) between a reference Lab and the Lab of g = opp2g_fast(...):
-// for dE76 the 500/116 and 200/116 scalings fold into one fma per channel.
+// dE (CL:201-226) between a reference Lab and the Lab of f = opp2f_fast(...):
+// for dE76 each channel's difference is one fma.
 template <int DE>
-__device__ __forceinline__ float delta_e_g(float Lr, float Ar, float Br, float3 g) {
+__device__ __forceinline__ float delta_e_f(float Lr, float Ar, float Br, float3 f) {
     if constexpr (DE == 0) {
-        const float dl = (Lr + 16.0f) - g.y;
-        const float da = fmaf(-500.0f / 116.0f, g.x - g.y, Ar);
-        const float db = fmaf(-200.0f / 116.0f, g.y - g.z, Br);
+        const float dl = fmaf(-116.0f, f.y, Lr + 16.0f);
+        const float da = fmaf(-500.0f, f.x - f.y, Ar);
+        const float db = fmaf(-200.0f, f.y - f.z, Br);
         return hw_sqrt((dl * dl + da * da) + db * db);
     } else {
-        return delta_e<DE>(Lr, Ar, Br, g.y - 16.0f, (500.0f / 116.0f) * (g.x - g.y),
-                           (200.0f / 116.0f) * (g.y - g.z));
+        return delta_e<DE>(Lr, Ar, Br, fmaf(116.0f, f.y, -16.0f), 500.0f * (f.x - f.y), 200.0f * (f.y - f.z));
     }
 }
 

@@ -154,7 +154,9 @@ struct CostArgs {
     int K;
     int tiles_x;
     int ntiles;      // tiles of the shard (partial pitch per palette)
-    float m_lab[9];  // Opp->XYZ rows / illuminant x 116^3 (CL:124-131), opp2xyz_over_illum()
+    float m_lab[9];  // Opp->XYZ rows / illuminant (CL:124-131), opp2xyz_over_illum()
+    float* pix_err;  // test option "pixel_err": [P][pix_pitch] per-pixel dE of the owned rows
+    int64_t pix_pitch;  // (null: not written)
 };
 
 struct FinalizeArgs {
@@ -198,7 +200,8 @@ struct GenArgs {
     double* partial;         // [nblocks]
     Geom g;
     int half;
-    float m_lab[9];  // Opp->XYZ rows / illuminant x 116^3 (CL:124-131), opp2xyz_over_illum()
+    float m_lab[9];  // Opp->XYZ rows / illuminant (CL:124-131), opp2xyz_over_illum()
+    float* pix_err;  // this palette's per-pixel dE of the owned rows (test option), or null
 };
 
 }  // namespace hq

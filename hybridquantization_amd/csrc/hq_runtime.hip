@@ -27,8 +27,8 @@ hipError_t launch_prep_palette(const PaletteArgs&, int P, hipStream_t);
 hipError_t launch_sa_step(const SaArgs&, hipStream_t);
 void set_launch_events(hipEvent_t start, hipEvent_t stop);
 hipError_t launch_build_grid(const GridArgs&, int P, hipStream_t);
-hipError_t launch_assign(const AssignArgs&, int P, hipStream_t);
-int assign_residency(int P);
+hipError_t launch_assign(const AssignArgs&, int P, hipStream_t, bool quad);
+int assign_residency(int NG, bool quad);
 void fast_tile_dims(int W, int own_rows, int tile_rows, int tile_w, int* tiles_x, int* ntiles);
 void opp2xyz_over_illum(const float inv_illum[3], float m[9]);
 hipError_t launch_cost_fast(const CostArgs&, int P, int de, bool trim, int tile_rows, int tile_w, int HB,
@@ -118,6 +118,7 @@ struct hq_ctx {
     int P_cap = 0, K_cur = 0;
     DevBuf d_pal_in, d_pal, d_opp, d_opp16, d_dup, d_pflags, d_lvl1, d_lvl2, d_idx, d_used_mask,
         d_partial, d_out, d_gen_t;
+    DevBuf d_pixerr;           // option "pixel_err": [P][n_own] per-pixel dE of the last evaluation
     DevBuf d_idx32, d_used32;  // K > 256 (hq_wide.hip): 32-bit index images, per-colour used flags
     float* h_pal = nullptr;   // pinned [P][K][4]
     double* h_out = nullptr;  // pinned [P][1+K]
@@ -133,11 +134,13 @@ struct hq_ctx {
     int assign_blocks_per_cu = 0;  // 0 = auto: assign_pipe_kernel<NG>'s residency (the occupancy
                                    // query, assign_res[NG]), one round of workgroups, each
                                    // thread a grid-stride pixel sequence
-    int assign_res[5] = {0, 0, 0, 0, 0};
+    int assign_res[2][5] = {};  // [quad][NG]
+    int assign_quad = 1;   // assign_quad_kernel (dword index stores); 0 = assign_pipe_kernel
     int img_u8_path = 1;   // assign reads the packed 8-bit image when there is one (option 'img_u8')
     int shard_solo = 0;    // experiment: a sharded search without a communicator (per-rank timing)
     int sa_device = 1;     // hq_search_*: 1 = SWASA iterations resident on the device (no host
                            // round trip per iteration), 0 = host-driven (one eval call each)
+    int pixel_err = 0;     // test option: the cost kernels also write the per-pixel dE
     int trim = 1;          // skip taps < 1e-9 of the peak of the narrow k1 filters
     bool trim_ok = false;  // set by hq_set_filters (the bucket's narrow-filter windows hold)
     bool pal_generic = false;  // this population needs the generic cost path (palette_fits_fast)
@@ -367,7 +370,7 @@ int assign_blocks(const hq_ctx* c, int P) {
     const int64_t chunk = 256 * HQ_ASSIGN_MINPX;
     const int ng = std::min(P, 4);
     const int per_cu = c->assign_blocks_per_cu > 0 ? c->assign_blocks_per_cu
-                       : c->assign_res[ng] > 0     ? c->assign_res[ng]
+                       : c->assign_res[c->assign_quad][ng] > 0 ? c->assign_res[c->assign_quad][ng]
                                                    : 4;
     const int64_t nblocks = (int64_t)c->num_cu * per_cu;
     return (int)std::max<int64_t>(1, std::min<int64_t>(nblocks, (c->g.n_ext + chunk - 1) / chunk));
@@ -404,6 +407,7 @@ int ensure_population(hq_ctx* c, int P, int K) {
     HIP_TRY(c, c->d_used_mask.ensure(sizeof(uint32_t) * kUsedSlots * (size_t)used_stride(P)));
     HIP_TRY(c, c->d_partial.ensure(sizeof(double) * (size_t)P * nparts));
     HIP_TRY(c, c->d_out.ensure(sizeof(double) * (size_t)P * (1 + K)));
+    if (c->pixel_err) HIP_TRY(c, c->d_pixerr.ensure(sizeof(float) * (size_t)P * std::max<int64_t>(n_own, 1)));
     return ensure_pinned(c, sizeof(float) * 4 * (size_t)P * K, sizeof(double) * (size_t)P * (1 + K));
 }
 
@@ -439,7 +443,7 @@ GridArgs grid_args(hq_ctx* c, int P, int K) {
 // The generic two-pass cost (CL:234-306 per pixel, any half-width) of P
 // palettes, one launch pair each: index images at idx_base (u8, or u32 when
 // idx32) with c->g.idx_pitch elements per palette, opponent tables of
-// opp_stride entries per palette in d_opp.  Times the first palette's pair.
+// opp_stride entries per palette in d_opp.  The cost events time all P pairs.
 int enqueue_generic_cost(hq_ctx* c, int P, const void* idx_base, bool idx32, int opp_stride,
                          const hipEvent_t* ev, int* nparts_out) {
     const Geom& g = c->g;
@@ -463,8 +467,10 @@ int enqueue_generic_cost(hq_ctx* c, int P, const void* idx_base, bool idx32, int
         gn.partial = c->d_partial.as<double>() + (int64_t)p * nparts;
         gn.g = g;
         gn.half = c->half;
+        gn.pix_err = c->pixel_err ? c->d_pixerr.as<float>() + (int64_t)p * n_own : nullptr;
         opp2xyz_over_illum(inv, gn.m_lab);
-        if (p == 0 && ev) set_launch_events(ev[4], ev[5]);  // the first palette's two launches
+        // the events span every palette's launch pair: start on the first, stop on the last
+        if (ev) set_launch_events(p == 0 ? ev[4] : nullptr, p == P - 1 ? ev[5] : nullptr);
         const hipError_t e = launch_cost_generic(gn, c->de_type, idx32, s);
         set_launch_events(nullptr, nullptr);
         HIP_TRY(c, e);
@@ -527,7 +533,7 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
                         c->d_idx.as<uint8_t>(), c->d_used_mask.as<uint32_t>(), used_stride(P), g.n_ext, g.idx_pitch,
                         ga.lvl1_pitch, ga.lvl2_gstride, K, c->G2, nblocks};
     timed(1);
-    hipError_t e = launch_assign(aa, P, s);
+    hipError_t e = launch_assign(aa, P, s, c->assign_quad != 0);
     untimed();
     HIP_TRY(c, e);
     const float inv[3] = {1.0f / c->illum[0], 1.0f / c->illum[1], 1.0f / c->illum[2]};
@@ -549,6 +555,8 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
         ca.K = K;
         fast_tile_dims(g.W, g.r1 - g.r0, rows, tw, &ca.tiles_x, &ca.ntiles);
         opp2xyz_over_illum(inv, ca.m_lab);
+        ca.pix_err = c->pixel_err ? c->d_pixerr.as<float>() : nullptr;
+        ca.pix_pitch = (int64_t)g.W * (g.r1 - g.r0);
         timed(2);
         e = launch_cost_fast(ca, P, c->de_type, c->trim && c->trim_ok, rows, tw, c->fast_hb, s);
         untimed();
@@ -827,7 +835,8 @@ int hq_create(int device, int delta_e_type, hq_ctx** out) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         c->num_cu = prop.multiProcessorCount;
-    for (int ng = 1; ng <= 4; ++ng) c->assign_res[ng] = assign_residency(ng);
+    for (int qd = 0; qd < 2; ++qd)
+        for (int ng = 1; ng <= 4; ++ng) c->assign_res[qd][ng] = assign_residency(ng, qd != 0);
     for (auto& e : c->ev) (void)hipEventCreate(&e);
     *out = c;
     return HQ_OK;
@@ -842,7 +851,7 @@ void hq_destroy(hq_ctx* c) {
                       &c->d_labL, &c->d_labA, &c->d_labB, &c->d_pal_in, &c->d_pal, &c->d_opp, &c->d_opp16,
                       &c->d_dup, &c->d_pflags, &c->d_lvl1, &c->d_lvl2, &c->d_idx,
                       &c->d_used_mask, &c->d_partial, &c->d_out, &c->d_gen_t, &c->d_taps,
-                      &c->d_vfrag16, &c->d_idx32, &c->d_used32})
+                      &c->d_vfrag16, &c->d_idx32, &c->d_used32, &c->d_pixerr})
         b->release();
     if (c->h_pal) (void)hipHostFree(c->h_pal);
     if (c->h_out) (void)hipHostFree(c->h_out);
@@ -1017,6 +1026,20 @@ int hq_get_indices32(hq_ctx* c, int p, uint32_t* idx) {
     HIP_TRY(c, hipMemcpy(b.data(), c->d_idx.as<uint8_t>() + (int64_t)p * g.idx_pitch + off, n_own,
                          hipMemcpyDeviceToHost));
     for (int64_t i = 0; i < n_own; ++i) idx[i] = b[i];
+    return HQ_OK;
+}
+
+int hq_get_pixel_errors(hq_ctx* c, int p, float* err) {
+    if (!c || !err) return HQ_ERR_ARG;
+    if (!c->pixel_err) return fail(c, HQ_ERR_STATE, "option pixel_err is off");
+    if (p < 0 || p >= c->last_P) return fail(c, HQ_ERR_ARG, "palette %d not in last population", p);
+    if (c->d_pixerr.bytes < sizeof(float) * (size_t)c->last_P * (size_t)c->g.W * (c->g.r1 - c->g.r0))
+        return fail(c, HQ_ERR_STATE, "pixel_err was set after the last evaluation");
+    int rc = bind(c);
+    if (rc) return rc;
+    const int64_t n_own = (int64_t)c->g.W * (c->g.r1 - c->g.r0);
+    HIP_TRY(c, hipMemcpy(err, c->d_pixerr.as<float>() + (int64_t)p * n_own, sizeof(float) * n_own,
+                         hipMemcpyDeviceToHost));
     return HQ_OK;
 }
 
@@ -1280,6 +1303,10 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
         c->sa_device = value != 0;
     } else if (!std::strcmp(name, "shard_solo")) {
         c->shard_solo = value != 0;
+    } else if (!std::strcmp(name, "assign_quad")) {
+        c->assign_quad = value != 0;
+    } else if (!std::strcmp(name, "pixel_err")) {
+        c->pixel_err = value != 0;
     } else if (!std::strcmp(name, "img_u8")) {
         c->img_u8_path = value != 0;
     } else if (!std::strcmp(name, "assign_blocks_per_cu")) {

@@ -150,6 +150,14 @@ class ImageManipulation:
         check(self._lib.hq_get_indices(ctx, int(p), out.ctypes.data_as(_lib._u8)), ctx)
         return out
 
+    def getPixelErrors(self, p: int = 0):
+        """Per-pixel dE of palette p of the last population over the owned rows (the
+        error image of IM:663-667); needs setOption("pixel_err", 1) before it."""
+        ctx = self._require()
+        out = np.zeros(self.w * self.h, np.float32)
+        check(self._lib.hq_get_pixel_errors(ctx, int(p), fptr(out)), ctx)
+        return out
+
     def getIndices32(self, p: int = 0):
         """32-bit palette index per pixel of palette p of the last population (any K,
         the int index of CL:172-193)."""

@@ -124,6 +124,12 @@ int hq_get_indices(hq_ctx *ctx, int p, uint8_t *idx);
 /* The same for any K (1 .. 2^24, HQ:192): 32-bit indices, w*(row_end-row_begin)
  * of them -- the reference's int index of CL:172-193. */
 int hq_get_indices32(hq_ctx *ctx, int p, uint32_t *idx);
+/* Test surface: the per-pixel dE of palette p of the last evaluation over the
+ * owned rows (w*(row_end-row_begin) floats) -- the error image the reference
+ * reads back per member (IM:663-667, CL:201-209).  Needs option "pixel_err" = 1
+ * before that evaluation (the cost kernels then also store it); HQ_ERR_STATE
+ * otherwise. */
+int hq_get_pixel_errors(hq_ctx *ctx, int p, float *err);
 
 /* IM:770 quantize(inlineImageRGB, colors): chosen colour per pixel (CL:147-170).
  * used (K ints) may be NULL. */
@@ -203,7 +209,9 @@ int hq_profile_reset(hq_ctx *ctx);
  *                  (accept/generate kernel, no host round trip per iteration; needs
  *                  population <= 64), 0 = host-driven, one evaluation call each
  *   "shard_solo"   experiment only: let a row-block shard run hq_search_* without a
- *                  communicator (its own partial costs; per-rank timing at N GPUs) */
+ *                  communicator (its own partial costs; per-rank timing at N GPUs)
+ *   "pixel_err"    test only: 1 = the cost kernels also write the per-pixel dE
+ *                  (hq_get_pixel_errors) */
 int hq_set_option(hq_ctx *ctx, const char *name, int value);
 
 #ifdef __cplusplus
