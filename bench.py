@@ -310,7 +310,12 @@ def main():
     rows = int(opts.get("cost_rows", 16))
     variant = int(opts.get("cost_variant", 0))
     hb = next((b for b in (10, 15, 19, 24) if half <= b), 0)
-    generic = variant == 1 or hb == 0 or args.K > 256
+    # K <= 256: u8 indices; 256 < K <= 4096: chunked palettes, 16-bit indices, the
+    # tiled kernel at HB = 10 with 16 x 128 tiles only; above: 32-bit indices
+    chunked = 256 < args.K <= 4096 and int(opts.get("chunked", 1)) != 0 and args.grid > 0
+    tw_opt = int(opts.get("cost_tw", 128))
+    generic = (variant == 1 or hb == 0 or (args.K > 256 and not chunked)
+               or (chunked and (hb != 10 or rows != 16 or tw_opt != 128)))
     trim_w = {10: (3, 4, 5), 15: (4, 5, 7), 19: (5, 7, 9), 24: (6, 9, 12)}
     if generic:
         kernel = "gen_hpass_kernel+gen_vpass_kernel"
@@ -326,7 +331,7 @@ def main():
     exec_flops = n_own * P * flops_exec
     achieved_tf = alg_flops / (cost_ms * 1e-3) / 1e12 if cost_ms > 0 else 0.0
     exec_tf = exec_flops / (cost_ms * 1e-3) / 1e12 if cost_ms > 0 else 0.0
-    alg_bytes = n_own * (12 + P * (4 if args.K > 256 else 1))
+    alg_bytes = n_own * (12 + P * (1 if args.K <= 256 else 2 if chunked else 4))
     hbm_gbs = alg_bytes / (cost_ms * 1e-3) / 1e9 if cost_ms > 0 else 0.0
     traffic = measured_traffic(W, args.K, P, args.grid, world, kernel.split("+")[0],
                                args.dpi, args.distance)

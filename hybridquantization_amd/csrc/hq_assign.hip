@@ -276,11 +276,25 @@ template <bool U8> struct RawPx { float r, g, b; };
 template <> struct RawPx<true> { uint32_t v; };
 
 
-template <int NG, bool U8>
+// Chunked palettes (256 < K <= 4096; AssignArgs::nch > 1): a palette of K colours
+// is nch sub-palettes of 256 (colours 256 c .. 256 c + 255, the last ones padded
+// with copies of colour 0), each with its own grid, and the argmin over K is
+// the argmin over the chunks' own argmins: each chunk's winner is its first
+// minimum (CL:179-193), and the reference distance of each winner, compared
+// in ascending chunk order with a strict <, picks the first chunk that
+// attains the global minimum -- the reference's first minimum over all K
+// (a padding colour ties colour 0, which chunk 0 holds, and never wins).
+// CMB consecutive sub-palettes of a group combine into one 16-bit index per
+// pixel.  nch > 4 runs nch / 4 passes over the groups (PASS 1 first, 2 middle,
+// 3 last), each comparing its group's winner with the best so far in the
+// distance scratch; PASS 0 is a single pass (nch <= 4) and the only one that
+// records used bits (nch > 4: used_idx16_kernel from the final indices).
+template <int NG, bool U8, int CMB = 1, int PASS = 0>
 #ifndef HQ_ASSIGN_WAVES
 #define HQ_ASSIGN_WAVES 1
 #endif
 __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(AssignArgs a, int grp0, int ngroups) {
+    static_assert(NG % CMB == 0 && (CMB == 4 || PASS == 0), "combine sets inside the group; passes: 4 chunks");
     // [NG][kMaxK]: a fixed palette stride, so each palette's base folds into the
     // ds_read_b128 offset field and a candidate's address is its byte << 4
     __shared__ __attribute__((aligned(16))) float4 s_pal[NG * kMaxK];
@@ -290,7 +304,7 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
     // workgroups covers one or two groups, so its L2 holds those groups' level-2
     // tables (2 MiB each at G2 = 32) rather than every group's (P = 64: 32 MiB
     // against a 4 MiB L2; the lookups then came from the Infinity Cache)
-    const int grp = grp0 + w / a.nblocks, blk = w % a.nblocks, tid = threadIdx.x;
+    const int grp = grp0 + (w / a.nblocks) * a.gstep, blk = w % a.nblocks, tid = threadIdx.x;
 #ifdef HQ_ASSIGN_TIMING  // diagnostic build: per-workgroup stamps (wall_clock64, 100 MHz)
     const uint64_t t_start = wall_clock64();
     uint64_t t_fill = 0, t_loop = 0;
@@ -317,8 +331,13 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
     auto at = [](const float* base, uint32_t q) {
         return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + (q << 2));
     };
-    auto load_rgb = [&](uint32_t q, RawPx<U8>& x) {
+    // PASS >= 2: the best reference distance of the earlier passes, per pixel of
+    // the group's palette (loaded with the pixel's RGB)
+    const float* dist_in = PASS >= 2 ? a.dist + (int64_t)((4 * grp) >> a.lg_nch) * a.idx_pitch : nullptr;
+    float pdl[3], pdv[3];  // [NB]: loads in flight, values of pixels being resolved
+    auto load_rgb = [&](uint32_t q, RawPx<U8>& x, float& pd) {
         const uint32_t qc = min(q, qlast);
+        if constexpr (PASS >= 2) pd = at(dist_in, qc);
         if constexpr (U8) {
             x.v = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(a.rgbx) + (qc << 2));
         } else {
@@ -397,17 +416,17 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
 #pragma unroll
     for (int j = 0; j < NB - 1; ++j) {
         RawPx<U8> x0;
-        load_rgb(qpos(j), x0);
+        load_rgb(qpos(j), x0, pdv[j]);
         unpack(x0, xr[j], xg[j], xb[j]);
         qq[j] = qpos(j);
         lookup(qq[j], xr[j], xg[j], xb[j], in_[j], E[j]);
     }
 #if HQ_ASSIGN_DEPTH == 2
-    load_rgb(qpos(2), rb[2]);
-    load_rgb(qpos(3), rb[0]);
+    load_rgb(qpos(2), rb[2], pdl[2]);
+    load_rgb(qpos(3), rb[0], pdl[0]);
 #else
-    load_rgb(qpos(1), rb[1]);
-    load_rgb(qpos(2), rb[0]);
+    load_rgb(qpos(1), rb[1], pdl[1]);
+    load_rgb(qpos(2), rb[0], pdl[0]);
 #endif
     // The palette table is filled while the first pixels' loads are in flight
     // (the fill used to come first: one more memory round trip per workgroup).
@@ -448,16 +467,48 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
             kk[pp] = k1[0];
         }
 #endif
+        if constexpr (CMB == 1) {
 #pragma unroll
-        for (int pp = 0; pp < NG; ++pp) {
-            const int k = kk[pp];
-            // non-temporal: streamed out during the kernel rather than left dirty
-            // in L2 for the kernel boundary to write back (67 MB per population;
-            // ~0.5-1% per evaluation)
-            if (q < n_ext) {
-                __builtin_nontemporal_store((uint8_t)k, idx_base[pp] + q);
-                const uint32_t bit = 1u << (k & 31);
-                if (!(s_used[pp][k >> 5] & bit)) atomicOr(&s_used[pp][k >> 5], bit);
+            for (int pp = 0; pp < NG; ++pp) {
+                const int k = kk[pp];
+                // non-temporal: streamed out during the kernel rather than left dirty
+                // in L2 for the kernel boundary to write back (67 MB per population;
+                // ~0.5-1% per evaluation)
+                if (q < n_ext) {
+                    __builtin_nontemporal_store((uint8_t)k, idx_base[pp] + q);
+                    const uint32_t bit = 1u << (k & 31);
+                    if (!(s_used[pp][k >> 5] & bit)) atomicOr(&s_used[pp][k >> 5], bit);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int s0 = 0; s0 < NG; s0 += CMB) {
+                // the chunks' winners in ascending chunk order, by the reference's
+                // distance (sqrtf of the unfused d^2, CL:186): strict <
+                float best = sqrtf(dist2(xr[h], xg[h], xb[h], s_pal[s0 * kMaxK + kk[s0]]));
+                int bc = 0, k = kk[s0];
+#pragma unroll
+                for (int c = 1; c < CMB; ++c) {
+                    const float d = sqrtf(dist2(xr[h], xg[h], xb[h], s_pal[(s0 + c) * kMaxK + kk[s0 + c]]));
+                    const bool lt = d < best;
+                    best = lt ? d : best;
+                    bc = lt ? c : bc;
+                    k = lt ? kk[s0 + c] : k;
+                }
+                const int sp = p0 + s0 + bc;  // the winning sub-palette
+                const uint16_t gidx = (uint16_t)(((sp & (a.nch - 1)) << 8) | k);
+                const int64_t pal = (int64_t)((p0 + s0) >> a.lg_nch);
+                if (q < n_ext) {
+                    bool win = true;
+                    if constexpr (PASS >= 2) win = best < pdv[h];  // earlier chunks first: strict <
+                    if (win) __builtin_nontemporal_store(gidx, a.idx16 + pal * a.idx_pitch + q);
+                    if constexpr (PASS == 1 || PASS == 2)
+                        if (win) a.dist[pal * a.idx_pitch + q] = best;
+                    if constexpr (PASS == 0) {
+                        const uint32_t bit = 1u << (k & 31);
+                        if (!(s_used[s0 + bc][k >> 5] & bit)) atomicOr(&s_used[s0 + bc][k >> 5], bit);
+                    }
+                }
             }
         }
     };
@@ -466,8 +517,9 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
         const int ia = (h + 2) % 3, fi = (h + 1) % 3;  // (not `a`: the kernel's AssignArgs)
         qq[ia] = qpos(i + 2);
         unpack(rb[ia], xr[ia], xg[ia], xb[ia]);  // RGB(i+2): landed
+        pdv[ia] = pdl[ia];
         lookup(qq[ia], xr[ia], xg[ia], xb[ia], in_[ia], E[ia]);
-        load_rgb(qpos(i + 4), rb[fi]);           // rb[fi] held RGB(i+1), unpacked a step ago
+        load_rgb(qpos(i + 4), rb[fi], pdl[fi]);  // rb[fi] held RGB(i+1), unpacked a step ago
         resolve(h);
     };
     int i = 0;
@@ -483,8 +535,9 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
         const int n = h ^ 1;
         qq[n] = qpos(i + 1);
         unpack(rb[n], xr[n], xg[n], xb[n]);  // RGB(i+1): landed, needed now anyway
+        pdv[n] = pdl[n];
         lookup(qq[n], xr[n], xg[n], xb[n], in_[n], E[n]);
-        load_rgb(qpos(i + 3), rb[n]);
+        load_rgb(qpos(i + 3), rb[n], pdl[n]);
         resolve(h);
     };
     int i = 0;
@@ -507,7 +560,7 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
 #ifdef HQ_ABL_NOUSED  // timing ablation (wrong results): no used-bit flush
     if (false) {
 #else
-    if (tid < 8 * NG) {
+    if (PASS == 0 && tid < 8 * NG) {
 #endif
         const uint32_t m = s_used[tid >> 3][tid & 7];
         uint32_t* gw = &a.used_glob[(blockIdx.x & (kUsedSlots - 1)) * a.used_stride + (p0 + (tid >> 3)) * 8 +
@@ -526,214 +579,114 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
 }
 
 // ----------------------------------------------------------------------------
-// assign_quad: the same argmin, pipeline and grid as assign_pipe_kernel, but a
-// lane owns 4 consecutive pixels ("quads", a grid stride of quads): their
-// packed colours arrive in one 16-B load, and each palette's 4 index bytes
-// leave in one dword store, so a wave writes 256 contiguous bytes per palette
-// (whole 128-B lines) instead of 64 single bytes (half a line; write traffic
-// 1.27x the index bytes in r03_hbm_traffic.json).  Quad data is loaded 4 pixel
-// steps ahead of its first lookup.  Pixels past the image (the last quad's
-// padding, quads past the grid stride) are resolved but never stored or
-// counted as used; the last quad's padding bytes land in the index image's
-// slack (idx_pitch >= n_ext + 4), which no reader uses.
+// used_idx16: grid (blocks, P), block 256 (nch > 4 only: the passes leave the
+// used bits to this kernel).  Used bits of palette p from its final 16-bit
+// indices (CL:193): an LDS bitmap per workgroup, OR'ed into used copy
+// blockIdx.x & 7 at words p * 8 nch ...
 // ----------------------------------------------------------------------------
-template <bool U8> struct RawQuad { float4 r, g, b; };
-template <> struct RawQuad<true> { uint4 v; };
-
-__device__ __forceinline__ uint32_t u4_at(const uint4& v, int u) {
-    return u == 0 ? v.x : u == 1 ? v.y : u == 2 ? v.z : v.w;
-}
-__device__ __forceinline__ float f4_at(const float4& v, int u) {
-    return u == 0 ? v.x : u == 1 ? v.y : u == 2 ? v.z : v.w;
-}
-
-template <int NG, bool U8>
-__global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_quad_kernel(AssignArgs a, int grp0, int ngroups) {
-    __shared__ __attribute__((aligned(16))) float4 s_pal[NG * kMaxK];
-    __shared__ uint32_t s_used[NG][8];
-    const int w = xcd_remap(blockIdx.x, a.nblocks * ngroups);
-    const int grp = grp0 + w / a.nblocks, blk = w % a.nblocks, tid = threadIdx.x;
-    const int p0 = 4 * grp;
-    const uint8_t* lines = a.lvl2 + (int64_t)grp * a.lvl2_gstride;
-    const int G2 = a.G2 > 0 ? a.G2 : 4;
-    const uint32_t n_ext = (uint32_t)a.n_ext;
-    const uint32_t nquad = (n_ext + 3u) >> 2, dlast = nquad - 1u;
-    const uint32_t cstride = (uint32_t)a.nblocks * 256u;  // quads
-    const uint32_t dbase = (uint32_t)blk * 256u + (uint32_t)tid;
-    // every lane runs lane 0's quad count (argmin_fix needs the whole wave)
-    const int nq0 = dbase < nquad ? (int)((nquad - 1u - dbase) / cstride) + 1 : 0;
-    const int nq = __builtin_amdgcn_readfirstlane(nq0);
-    auto dpos = [&](int i) { return dbase + (uint32_t)i * cstride; };
-    auto load_quad = [&](uint32_t d, RawQuad<U8>& x) {
-        const uint32_t dc = min(d, dlast) << 4;  // byte offset of the quad (16 B per channel)
-        if constexpr (U8) {
-            x.v = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.rgbx) + dc);
-        } else {
-            x.r = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(a.R) + dc);
-            x.g = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(a.G) + dc);
-            x.b = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(a.B) + dc);
-        }
-    };
-    auto px_of = [&](const RawQuad<U8>& x, int u, float& r, float& g, float& b) {
-        if constexpr (U8) {
-            const uint32_t v = u4_at(x.v, u);
-            r = u8_unit(v, 0);
-            g = u8_unit(v, 1);
-            b = u8_unit(v, 2);
-        } else {
-            r = f4_at(x.r, u);
-            g = f4_at(x.g, u);
-            b = f4_at(x.b, u);
-        }
-    };
-    auto lookup = [&](float r, float g, float b, bool& inside, L2E (&e)[NG]) {
-        inside = U8 ? true : r >= 0.f && r <= 1.f && g >= 0.f && g <= 1.f && b >= 0.f && b <= 1.f;
-        const uint8_t* lb = lines + (inside ? (uint32_t)quad_cell(r, g, b, G2) : 0u) * (uint32_t)kL2Line;
-        const uint4* line = reinterpret_cast<const uint4*>(lb);
-        if constexpr (kL2Bytes == 16) {
-#pragma unroll
-            for (int pp = 0; pp < NG; ++pp) e[pp] = line[pp];
-        } else {
-#pragma unroll
-            for (int pp = 0; pp + 1 < NG; pp += 2) {
-                const uint4 v = line[pp >> 1];
-                l2_set(e[pp], v.x, v.y);
-                l2_set(e[pp + 1], v.z, v.w);
-            }
-            if constexpr (NG & 1) e[NG - 1] = reinterpret_cast<const L2E*>(lb)[NG - 1];
-        }
-    };
-    RawQuad<U8> xq[2];            // quads: i & 1
-    float xr[2], xg[2], xb[2];    // pixels being looked up / resolved: step parity
-    L2E E[2][NG];
-    bool in_[2];
-    uint32_t acc[NG];             // index bytes of the current quad, per palette
-    load_quad(dpos(0), xq[0]);
-    px_of(xq[0], 0, xr[0], xg[0], xb[0]);
-    lookup(xr[0], xg[0], xb[0], in_[0], E[0]);
-    load_quad(dpos(1), xq[1]);
-    static_assert(kMaxK == 256, "one table entry per thread and palette");
-#pragma unroll
-    for (int pp = 0; pp < NG; ++pp)
-        s_pal[pp * kMaxK + tid] = a.pal[(int64_t)(p0 + pp) * kMaxK + min(tid, a.K - 1)];
-    if (tid < 8 * NG) s_used[tid >> 3][tid & 7] = 0;
+__global__ __launch_bounds__(256) void used_idx16_kernel(AssignArgs a) {
+    __shared__ uint32_t s_bits[kMaxKChunked / 32];
+    const int p = blockIdx.y, tid = threadIdx.x, wpp = 8 * a.nch;
+    for (int i = tid; i < wpp; i += 256) s_bits[i] = 0u;
     __syncthreads();
-    uint32_t* idx_base[NG];
-    bool exh_pal[NG];
-#pragma unroll
-    for (int pp = 0; pp < NG; ++pp) {
-        idx_base[pp] = reinterpret_cast<uint32_t*>(a.idx + (int64_t)(p0 + pp) * a.idx_pitch);
-        exh_pal[pp] = a.pflags[p0 + pp] != 0 || a.G2 == 0;
-        acc[pp] = 0u;
+    const uint16_t* idx = a.idx16 + (int64_t)p * a.idx_pitch;
+    for (int64_t q = (int64_t)blockIdx.x * 256 + tid; q < a.n_ext; q += (int64_t)gridDim.x * 256) {
+        const uint32_t k = idx[q], bit = 1u << (k & 31);
+        if (!(s_bits[k >> 5] & bit)) atomicOr(&s_bits[k >> 5], bit);
     }
-    // step (quad i, pixel u): quad parity qp = i & 1 and u are compile-time
-    auto step = [&](int i, int qp, int u) {
-        const int h = u & 1, n = h ^ 1;
-        if (u < 3) px_of(xq[qp], u + 1, xr[n], xg[n], xb[n]);
-        else px_of(xq[qp ^ 1], 0, xr[n], xg[n], xb[n]);
-        lookup(xr[n], xg[n], xb[n], in_[n], E[n]);
-        if (u == 3) load_quad(dpos(i + 2), xq[qp]);  // this quad's buffer is free now
-        const uint32_t d = dpos(i);
-        const uint32_t q = (d << 2) + (uint32_t)u;
-#pragma unroll
-        for (int pp = 0; pp < NG; ++pp) {
-            const L2E e1[1] = {E[h][pp]};
-            const bool x1[1] = {exh_pal[pp]};
-            int k1[1];
-            argmin_group<1>(xr[h], xg[h], xb[h], e1, in_[h], x1, s_pal + pp * kMaxK, a.lvl1, a.lvl1_pitch,
-                            p0 + pp, G2, a.K, k1);
-            const int k = k1[0];
-            acc[pp] = u == 0 ? (uint32_t)k : acc[pp] | ((uint32_t)k << (8 * u));
-            if (q < n_ext) {
-                const uint32_t bit = 1u << (k & 31);
-                if (!(s_used[pp][k >> 5] & bit)) atomicOr(&s_used[pp][k >> 5], bit);
-            }
-        }
-        if (u == 3 && (d << 2) < n_ext) {
-#pragma unroll
-            for (int pp = 0; pp < NG; ++pp) __builtin_nontemporal_store(acc[pp], idx_base[pp] + d);
-        }
-    };
-    int i = 0;
-    for (; i + 2 <= nq; i += 2) {
-        step(i, 0, 0); step(i, 0, 1); step(i, 0, 2); step(i, 0, 3);
-        step(i + 1, 1, 0); step(i + 1, 1, 1); step(i + 1, 1, 2); step(i + 1, 1, 3);
-    }
-    if (i < nq) { step(i, 0, 0); step(i, 0, 1); step(i, 0, 2); step(i, 0, 3); }
     __syncthreads();
-    if (tid < 8 * NG) {
-        const uint32_t m = s_used[tid >> 3][tid & 7];
-        uint32_t* gw = &a.used_glob[(blockIdx.x & (kUsedSlots - 1)) * a.used_stride + (p0 + (tid >> 3)) * 8 +
-                                    (tid & 7)];
-        const uint32_t seen = __hip_atomic_load(gw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (m & ~seen) atomicOr(gw, m);
+    for (int i = tid; i < wpp; i += 256) {
+        const uint32_t m = s_bits[i];
+        if (m) atomicOr(&a.used_glob[(blockIdx.x & (kUsedSlots - 1)) * a.used_stride + p * wpp + i], m);
     }
 }
 
 // ----------------------------------------------------------------------------
 // Launcher: the full groups of 4 palettes in one launch, a last group of
 // P mod 4 in a second (the profiling events, when set, bracket both).
+// Chunked palettes (a.nch > 1; P = sub-palettes): nch = 2 combines pairs, 4
+// whole groups; nch = 8, 16 run nch / 4 passes (groups j, j + nch / 4, ...),
+// then used_idx16.
 // ----------------------------------------------------------------------------
-template <bool U8, bool QUAD>
-void launch_assign_t(const AssignArgs& a, int P, hipStream_t s) {
-    const int full = P / 4, rest = P % 4;
+template <bool U8>
+void launch_assign_t(const AssignArgs& a0, int P, hipStream_t s) {
     const hipEvent_t ev0 = t_ev_start, ev1 = t_ev_stop;
-#define HQ_ASG(NG, NB, G0, NGR)                                                                         \
-    do {                                                                                                \
-        if (QUAD) HQ_LAUNCH((assign_quad_kernel<NG, U8>), dim3((unsigned)(NB)), dim3(256), 0, s, a, G0, NGR); \
-        else HQ_LAUNCH((assign_pipe_kernel<NG, U8>), dim3((unsigned)(NB)), dim3(256), 0, s, a, G0, NGR);      \
-    } while (0)
+    AssignArgs a = a0;
+    a.gstep = 1;
+    if (a.nch > 4) {
+        const int npass = a.nch / 4, npal = P / a.nch;
+        a.gstep = npass;
+        for (int j = 0; j < npass; ++j) {
+            t_ev_start = j == 0 ? ev0 : nullptr;
+            t_ev_stop = nullptr;
+            const dim3 grid((unsigned)(a.nblocks * npal));
+            if (j == 0) HQ_LAUNCH((assign_pipe_kernel<4, U8, 4, 1>), grid, dim3(256), 0, s, a, j, npal);
+            else if (j + 1 < npass) HQ_LAUNCH((assign_pipe_kernel<4, U8, 4, 2>), grid, dim3(256), 0, s, a, j, npal);
+            else HQ_LAUNCH((assign_pipe_kernel<4, U8, 4, 3>), grid, dim3(256), 0, s, a, j, npal);
+        }
+        t_ev_start = nullptr;
+        t_ev_stop = ev1;
+        const unsigned ub = (unsigned)std::min<int64_t>(512, (a.n_ext + 4095) / 4096);
+        HQ_LAUNCH(used_idx16_kernel, dim3(ub, (unsigned)npal), dim3(256), 0, s, a);
+        t_ev_start = ev0;
+        return;
+    }
+    const int full = P / 4, rest = P % 4;
+#define HQ_ASG(NG, CMB, NB, G0, NGR) \
+    HQ_LAUNCH((assign_pipe_kernel<NG, U8, CMB>), dim3((unsigned)(NB)), dim3(256), 0, s, a, G0, NGR)
     if (full > 0) {
         if (rest) t_ev_stop = nullptr;
-        HQ_ASG(4, a.nblocks * full, 0, full);
+        if (a.nch == 4) HQ_ASG(4, 4, a.nblocks * full, 0, full);
+        else if (a.nch == 2) HQ_ASG(4, 2, a.nblocks * full, 0, full);
+        else HQ_ASG(4, 1, a.nblocks * full, 0, full);
         t_ev_stop = ev1;
         if (rest) t_ev_start = nullptr;
     }
-    switch (rest) {
-    case 1: HQ_ASG(1, a.nblocks, full, 1); break;
-    case 2: HQ_ASG(2, a.nblocks, full, 1); break;
-    case 3: HQ_ASG(3, a.nblocks, full, 1); break;
+    switch (rest) {  // (nch = 2: rest is 0 or 2; nch = 4: 0)
+    case 1: HQ_ASG(1, 1, a.nblocks, full, 1); break;
+    case 2:
+        if (a.nch == 2) HQ_ASG(2, 2, a.nblocks, full, 1);
+        else HQ_ASG(2, 1, a.nblocks, full, 1);
+        break;
+    case 3: HQ_ASG(3, 1, a.nblocks, full, 1); break;
     default: break;
     }
 #undef HQ_ASG
     t_ev_start = ev0;
 }
 
-// quad: 1 = assign_quad_kernel (4 consecutive pixels per lane, dword index
-// stores), 0 = assign_pipe_kernel (one pixel per lane and step, byte stores)
-hipError_t launch_assign(const AssignArgs& a, int P, hipStream_t s, bool quad) {
-    if (a.rgbx) {
-        if (quad) launch_assign_t<true, true>(a, P, s);
-        else launch_assign_t<true, false>(a, P, s);
-    } else {
-        if (quad) launch_assign_t<false, true>(a, P, s);
-        else launch_assign_t<false, false>(a, P, s);
-    }
+hipError_t launch_assign(const AssignArgs& a, int P, hipStream_t s) {
+    if (a.rgbx) launch_assign_t<true>(a, P, s);
+    else launch_assign_t<false>(a, P, s);
     return hipGetLastError();
 }
 
 // Resident workgroups per CU of assign_pipe_kernel<NG> (the auto size of one
-// grid-stride round; the packed and planar forms take the larger register
-// count); 0 if the query fails.
-int assign_residency(int NG, bool quad) {
+// grid-stride round; the packed and planar forms and, for NG = 4, the chunk
+// combining forms take the larger register count); 0 if the query fails.
+int assign_residency(int NG) {
     auto q = [](auto kern) {
         int n = 0;
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, 256, 0) == hipSuccess ? n : 0;
     };
-    if (quad) {
-        switch (NG) {
-        case 1: return std::min(q(assign_quad_kernel<1, false>), q(assign_quad_kernel<1, true>));
-        case 2: return std::min(q(assign_quad_kernel<2, false>), q(assign_quad_kernel<2, true>));
-        case 3: return std::min(q(assign_quad_kernel<3, false>), q(assign_quad_kernel<3, true>));
-        default: return std::min(q(assign_quad_kernel<4, false>), q(assign_quad_kernel<4, true>));
-        }
-    }
     switch (NG) {
     case 1: return std::min(q(assign_pipe_kernel<1, false>), q(assign_pipe_kernel<1, true>));
     case 2: return std::min(q(assign_pipe_kernel<2, false>), q(assign_pipe_kernel<2, true>));
     case 3: return std::min(q(assign_pipe_kernel<3, false>), q(assign_pipe_kernel<3, true>));
     default: return std::min(q(assign_pipe_kernel<4, false>), q(assign_pipe_kernel<4, true>));
     }
+}
+
+// The same for the chunk-combining forms (chunked palettes, nch = 2 .. 16).
+int assign_residency_chunked() {
+    auto q = [](auto kern) {
+        int n = 0;
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, 256, 0) == hipSuccess ? n : 0;
+    };
+    int r = std::min(q(assign_pipe_kernel<4, false, 2>), q(assign_pipe_kernel<4, true, 2>));
+    r = std::min(r, std::min(q(assign_pipe_kernel<4, false, 4>), q(assign_pipe_kernel<4, true, 4>)));
+    r = std::min(r, std::min(q(assign_pipe_kernel<4, false, 4, 2>), q(assign_pipe_kernel<4, true, 4, 2>)));
+    return r;
 }
 
 }  // namespace hq

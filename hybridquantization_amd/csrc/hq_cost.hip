@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <type_traits>
 #include <cstring>
 #include <vector>
 
@@ -194,6 +195,69 @@ struct TileFill {
             for (int q = 0; q < NFB; ++q) {
                 const int e = tid + NTH * q;
                 if (e < RH * RW) s_idx[(e / RW) * IDXP + e % RW] = (uint8_t)b[q];
+            }
+        }
+    }
+};
+
+// The 16-bit index rows of a chunked palette's tile (256 < K <= 4096): region
+// row i = RWL indices from column x0 - HALF into s_idx row i (pitch RW
+// elements; columns RWL .. RW - 1, read by the vertical pass's last block but
+// never used, are zeroed so they index the table).  Tiles whose rows all start
+// on a dword (interior tiles of an even-width image at an even HALF) load
+// dwords of two indices; the others gather element by element with reflection.
+template <int HALF, int RWL, int RW, int TH, int NTH = 256>
+struct TileFill16 {
+    static constexpr int RH = TH + 2 * HALF, DW = RWL / 2, NL = (RH * DW + NTH - 1) / NTH;
+    static constexpr int NE = (RH * RW + NTH - 1) / NTH, NZ = RH * (RW - RWL) / 2;
+    static_assert(RWL % 2 == 0 && RW % 2 == 0, "whole dwords");
+    uint32_t v[NL];
+    TileItem t;
+    bool fast;
+
+    __device__ __forceinline__ void issue(const CostArgs& a, const TileItem& ti, int tid) {
+        const Geom& g = a.g;
+        t = ti;
+        const uint16_t* idx = reinterpret_cast<const uint16_t*>(a.idx) + (int64_t)t.p * g.idx_pitch;
+        fast = t.x0 - HALF >= 0 && t.x0 + RWL - HALF <= g.W && (g.W & 1) == 0 && ((t.x0 - HALF) & 1) == 0;
+        if (fast) {
+#pragma unroll
+            for (int q = 0; q < NL; ++q) {
+                const int e = min(tid + NTH * q, RH * DW - 1), i = e / DW, c = e - i * DW;
+                const int roff = TileFill<HALF, RWL, TH, NTH>::row_base(g, t, i);  // even: dword aligned
+                v[q] = *reinterpret_cast<const uint32_t*>(idx + roff + 2 * c);
+            }
+        }
+    }
+
+    __device__ __forceinline__ void commit(const CostArgs& a, uint16_t* s_idx, int tid) const {
+        const Geom& g = a.g;
+        uint32_t* s32 = reinterpret_cast<uint32_t*>(s_idx);
+        if (fast) {
+#pragma unroll
+            for (int q = 0; q < NL; ++q) {
+                const int e = tid + NTH * q, i = e / DW, c = e - i * DW;
+                if (e < RH * DW) s32[i * (RW / 2) + c] = v[q];
+            }
+            for (int e = tid; e < NZ; e += NTH) {
+                const int i = e / ((RW - RWL) / 2), c = e - i * ((RW - RWL) / 2);
+                s32[i * (RW / 2) + RWL / 2 + c] = 0u;
+            }
+        } else {
+            const uint16_t* idx = reinterpret_cast<const uint16_t*>(a.idx) + (int64_t)t.p * g.idx_pitch;
+            uint32_t b[NE];
+#pragma unroll
+            for (int q = 0; q < NE; ++q) {  // all loads first: one round trip
+                const int e = min(tid + NTH * q, RH * RW - 1), i = e / RW, j = e - i * RW;
+                int gy = reflect_clamp(t.y0 - HALF + i, g.H);
+                gy = min(max(gy, g.e0), g.e1 - 1);
+                const int gx = reflect_clamp(t.x0 - HALF + min(j, RWL - 1), g.W);
+                b[q] = idx[(uint32_t)((gy - g.e0) * g.W + gx)];
+            }
+#pragma unroll
+            for (int q = 0; q < NE; ++q) {
+                const int e = tid + NTH * q, i = e / RW, j = e - i * RW;
+                if (e < RH * RW) s_idx[i * RW + j] = j < RWL ? (uint16_t)b[q] : (uint16_t)0;
             }
         }
     }
@@ -607,12 +671,21 @@ __device__ __forceinline__ void vblock(const uint32_t (&w)[8 * S + 2], const uin
 #ifndef HQ_LB19
 #define HQ_LB19 3  // waves per SIMD of the 19-tap bucket
 #endif
-// occupancy per bucket: LDS allows 4 workgroups per CU at HB = 10, 3 above
-template <int HB>
-constexpr int cost16w_waves() { return HB == 10 ? 4 : HB == 15 ? 3 : HB == 19 ? HQ_LB19 : 2; }
+// occupancy per bucket: LDS allows 4 workgroups per CU at HB = 10, 3 above;
+// chunked palettes (NCH > 1: 16-bit indices, a table of 256 NCH entries): 3 up
+// to 1,024 colours, 2 above
+template <int HB, int NCH = 1>
+constexpr int cost16w_waves() {
+    return NCH > 4 ? 2 : NCH > 1 ? 3 : HB == 10 ? 4 : HB == 15 ? 3 : HB == 19 ? HQ_LB19 : 2;
+}
 
-template <int HB, int DE, bool TRIM, int NW>
-__global__ __launch_bounds__(64 * NW, cost16w_waves<HB>()) void cost16w_kernel(CostArgs a, int P_) {
+// NCH > 1 (chunked palettes, 256 < K <= 256 NCH; HB = 10): the index image is
+// 16-bit and the split opponent table has KT = 256 NCH entries, in dynamic LDS
+// (8 KT bytes): channel 0's x words first, then -- loaded from global memory
+// during channel 0's horizontal pass, once its gathers are done -- the (y, z)
+// pairs in the same bytes.
+template <int HB, int DE, bool TRIM, int NW, int NCH = 1>
+__global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_kernel(CostArgs a, int P_) {
     using Gm = Tile16<HB, NW>;
     constexpr int NTH = 64 * NW, IPR = 8 * NW;  // threads; horizontal items per row pair
     constexpr int TH = kTH16, HR = 4, T2 = 2 * HB, TW = Gm::TW, RWL = Gm::RWL, RW = Gm::RW;
@@ -620,11 +693,17 @@ __global__ __launch_bounds__(64 * NW, cost16w_waves<HB>()) void cost16w_kernel(C
     constexpr int ROW = 2 * WH, PLANE4 = Gm::PLANE4;
     constexpr int L0 = HB - trim_w(HB, 0), L1 = HB - trim_w(HB, 1), L2 = HB - trim_w(HB, 2);
     static_assert(TW / HR == IPR && 8 * IPR == NTH, "one horizontal item per thread");
+    constexpr bool W16 = NCH > 1;
+    constexpr int KT = kMaxK * NCH, NTE = KT / NTH;  // table entries (per thread)
+    using IT = std::conditional_t<W16, uint16_t, uint8_t>;
     __shared__ f32x4 s_vq[3 * PLANE4];
-    __shared__ uint32_t s_ox[kMaxK];  // opponent x 2^14 as (hi, lo) f16 pairs: channel 0
-    __shared__ uint2 s_oyz[kMaxK];     // channels 1, 2
-    __shared__ __attribute__((aligned(16))) uint8_t s_idx[RH * RW];
+    __shared__ uint32_t s_ox8[W16 ? 1 : kMaxK];  // opponent x 2^14 as (hi, lo) f16 pairs: channel 0
+    __shared__ uint2 s_oyz8[W16 ? 1 : kMaxK];    // channels 1, 2
+    __shared__ __attribute__((aligned(16))) IT s_idx[RH * RW];
     __shared__ double s_red[NW];
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];  // W16: 8 KT bytes
+    uint32_t* const s_ox = W16 ? s_tab : s_ox8;
+    uint2* const s_oyz = W16 ? reinterpret_cast<uint2*>(s_tab) : s_oyz8;
     float* s_v = reinterpret_cast<float*>(s_vq);
     const int tid = threadIdx.x;
     const Geom& g = a.g;
@@ -635,8 +714,13 @@ __global__ __launch_bounds__(64 * NW, cost16w_waves<HB>()) void cost16w_kernel(C
     const uint4* frag = a.vfrag16 + (TRIM ? 2 * S * 4 * 2 * 64 : 0) + lane;
     auto F = [&](int half, int s, int st, int hl) { return frag[(((half * S + s) * 4 + st) * 2 + hl) * 64]; };
 
-    TileFill<HB, RWL, TH, NTH> fill;
+    std::conditional_t<W16, TileFill16<HB, RWL, RW, TH, NTH>, TileFill<HB, RWL, TH, NTH>> fill;
     fill.issue(a, cur, tid);
+    uint32_t tx[W16 ? NTE : 1];  // W16: this thread's x words of the table (entries tid + NTH j)
+    if constexpr (W16) {
+#pragma unroll
+        for (int j = 0; j < NTE; ++j) tx[j] = a.opp16[(int64_t)cur.p * KT + tid + NTH * j].x;
+    }
     uint4 A[2][2][S][2];  // channel 0's stacks (f0, f1), (f2, -); then channels 1-2's
 #pragma unroll
     for (int st = 0; st < 2; ++st)
@@ -649,11 +733,17 @@ __global__ __launch_bounds__(64 * NW, cost16w_waves<HB>()) void cost16w_kernel(C
             }
     // every entry (zeros for tid >= K): zero-weight rows and the columns past
     // the region gather arbitrary indices, and 0 x NaN would be NaN
-    if (NTH == kMaxK || tid < kMaxK) {
-        s_ox[tid] = fill.ov.x;
-        s_oyz[tid] = make_uint2(fill.ov.y, fill.ov.z);
+    if constexpr (W16) {
+#pragma unroll
+        for (int j = 0; j < NTE; ++j) s_ox[tid + NTH * j] = tx[j];
+        fill.commit(a, s_idx, tid);
+    } else {
+        if (NTH == kMaxK || tid < kMaxK) {
+            s_ox[tid] = fill.ov.x;
+            s_oyz[tid] = make_uint2(fill.ov.y, fill.ov.z);
+        }
+        fill.template commit_idx<RW>(a, s_idx, tid);
     }
-    fill.template commit_idx<RW>(a, s_idx, tid);
     // H item: row pair m, output columns 4j .. 4j+3 (every thread has one)
     const int m = tid / IPR, jr = tid % IPR;
     const int gy0 = cur.y0 + 2 * m, gx0 = cur.x0 + HR * jr;
@@ -712,10 +802,22 @@ __global__ __launch_bounds__(64 * NW, cost16w_waves<HB>()) void cost16w_kernel(C
     };
     if constexpr (S == 1) load_a12();
     __syncthreads();
+    uint2 tyz[W16 ? NTE : 1];  // W16: the (y, z) words, in flight through channel 0's horizontal pass
+    if constexpr (W16) {
+#pragma unroll
+        for (int j = 0; j < NTE; ++j) {
+            const uint4 e = a.opp16[(int64_t)cur.p * KT + tid + NTH * j];
+            tyz[j] = make_uint2(e.y, e.z);
+        }
+    }
     if constexpr (TRIM) hpass_wide<HB, L0, T2 - L0, WH>(hsrc, jr, taps, 0, 0, PLANE4, acc0);
     else hpass_wide<HB, 0, T2, WH>(hsrc, jr, taps, 0, 0, PLANE4, acc0);
     hpass_wide<HB, 0, T2, WH>(hsrc, jr, taps, 1, 1, PLANE4, acc0);
     hpass_wide<HB, 0, T2, WH>(hsrc, jr, taps, 2, 2, PLANE4, acc0);
+    if constexpr (W16) {  // (the x words' last reads were the gathers before the barrier)
+#pragma unroll
+        for (int j = 0; j < NTE; ++j) s_oyz[tid + NTH * j] = tyz[j];
+    }
     __syncthreads();
 
     // ---- channels 1, 2: one gather of (y, z) per region row; stack (f3, f4)
@@ -1061,6 +1163,43 @@ static void launch_cost16w(const CostArgs& a0, int P, int de, bool trim, hipStre
     }
 }
 
+// Chunked palettes (nch = 2 .. 16 chunks of 256 colours, 16-bit indices): HB =
+// 10, 16 x 128 tiles; the table takes 8 * 256 nch bytes of dynamic LDS.
+template <int NCH>
+static void launch_cost16w_chunked(const CostArgs& a0, int P, int de, bool trim, hipStream_t s) {
+    CostArgs a = a0;
+    a.taps = static_cast<const char*>(a0.taps) + sizeof(CostTaps<10>);
+    const dim3 grid((unsigned)(a.ntiles * P)), block(256);
+    const size_t dyn = 8 * (size_t)kMaxK * NCH;
+    auto go = [&](auto kern) {
+        static bool attr = false;  // LDS above 64 KB in all (NCH 16: 74 KB)
+        if (!attr) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+            attr = true;
+        }
+        HQ_LAUNCH(kern, grid, block, dyn, s, a, P);
+    };
+    if (de == 0) {
+        if (trim) go(cost16w_kernel<10, 0, true, 4, NCH>);
+        else go(cost16w_kernel<10, 0, false, 4, NCH>);
+    } else {
+        if (trim) go(cost16w_kernel<10, 1, true, 4, NCH>);
+        else go(cost16w_kernel<10, 1, false, 4, NCH>);
+    }
+}
+
+hipError_t launch_cost_chunked(const CostArgs& a, int P, int nch, int de, bool trim, hipStream_t s) {
+    switch (nch) {
+    case 2: launch_cost16w_chunked<2>(a, P, de, trim, s); break;
+    case 4: launch_cost16w_chunked<4>(a, P, de, trim, s); break;
+    case 8: launch_cost16w_chunked<8>(a, P, de, trim, s); break;
+    case 16: launch_cost16w_chunked<16>(a, P, de, trim, s); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 // 256-column tiles (8 waves, 69 KB of LDS at HB = 10): HB = 10 only.
 hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, bool trim, int tile_rows, int tile_w, int HB,
                             hipStream_t s) {
@@ -1090,11 +1229,13 @@ hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, bool trim, int ti
     return hipGetLastError();
 }
 
-hipError_t launch_cost_generic(const GenArgs& a, int de, bool idx32, hipStream_t s) {
+// idx_bytes: 1, 2 (chunked palettes) or 4 (K > 4096)
+hipError_t launch_cost_generic(const GenArgs& a, int de, int idx_bytes, hipStream_t s) {
     // profiling events (when set) bracket both launches: start on the first, stop on the second
     const hipEvent_t ev0 = t_ev_start, ev1 = t_ev_stop;
     t_ev_stop = nullptr;
-    if (idx32) HQ_LAUNCH(gen_hpass_kernel<uint32_t>, dim3(blocks_for(a.g.n_ext)), dim3(256), 0, s, a);
+    if (idx_bytes == 4) HQ_LAUNCH(gen_hpass_kernel<uint32_t>, dim3(blocks_for(a.g.n_ext)), dim3(256), 0, s, a);
+    else if (idx_bytes == 2) HQ_LAUNCH(gen_hpass_kernel<uint16_t>, dim3(blocks_for(a.g.n_ext)), dim3(256), 0, s, a);
     else HQ_LAUNCH(gen_hpass_kernel<uint8_t>, dim3(blocks_for(a.g.n_ext)), dim3(256), 0, s, a);
     t_ev_start = nullptr;
     t_ev_stop = ev1;

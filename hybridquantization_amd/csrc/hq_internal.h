@@ -9,6 +9,13 @@ namespace hq {
 
 constexpr int kMaxK = 256;        // u8 palette indices (K <= 256 on the tiled path)
 constexpr int kMaxKWide = 1 << 24;  // K > 256: 32-bit indices (the plugin's limit, HQ:192)
+constexpr int kMaxKChunked = 4096;  // 256 < K <= 4096: palettes as 256-colour chunks, 16-bit indices
+// chunks of a palette of K colours on the chunked path: a power of two (2 .. 16)
+inline int chunk_count(int K) {
+    int n = 1;
+    while (256 * n < K) n <<= 1;
+    return n;
+}
 constexpr int kMaxTaps = 255;     // generic path limit (2*half+1)
 constexpr int kNumFilt = 7;       // separable filter pairs of the S-CIELAB stencil
 constexpr int kL1Cap = 31;        // level-1 candidate list capacity (32-B entry)
@@ -102,6 +109,7 @@ struct SaArgs {
     int generate;           // 1: generate the next candidates (and prep them)
     int random;             // generate SW:40-52 random colours instead of neighbours
     int convergence;
+    int nch;                // chunked palettes: chunks per palette (P nch workgroups), else 1
 };
 
 struct GridArgs {
@@ -138,6 +146,12 @@ struct AssignArgs {
     int K;
     int G2;                 // 0 = exhaustive
     int nblocks;            // workgroups per palette group
+    // chunked palettes (256 < K <= 4096): the P above are sub-palettes, nch per
+    // palette (chunk_count), combined into 16-bit indices (hq_assign.hip)
+    uint16_t* idx16;        // [P / nch][idx_pitch]
+    float* dist;            // [P / nch][idx_pitch] best reference distance (nch > 4 passes)
+    int nch = 1, lg_nch = 0;
+    int gstep = 1;          // (set by the launcher)
 };
 
 struct CostArgs {
@@ -166,7 +180,8 @@ struct FinalizeArgs {
     double* out;            // [P][1+K]
     int ntiles;
     int K;
-    const uint32_t* used32; // K > 256: [P][K] used flags (assign_wide), replaces used_mask
+    const uint32_t* used32; // K > 4096: [P][K] used flags (assign_wide), replaces used_mask
+    int wpp;                // used words per palette in used_glob (8; 8 nch for chunked palettes)
 };
 
 // Palettes of K > 256 colours (hq_wide.hip).

@@ -27,8 +27,10 @@ hipError_t launch_prep_palette(const PaletteArgs&, int P, hipStream_t);
 hipError_t launch_sa_step(const SaArgs&, hipStream_t);
 void set_launch_events(hipEvent_t start, hipEvent_t stop);
 hipError_t launch_build_grid(const GridArgs&, int P, hipStream_t);
-hipError_t launch_assign(const AssignArgs&, int P, hipStream_t, bool quad);
-int assign_residency(int NG, bool quad);
+hipError_t launch_assign(const AssignArgs&, int P, hipStream_t);
+int assign_residency(int NG);
+int assign_residency_chunked();
+hipError_t launch_cost_chunked(const CostArgs&, int P, int nch, int de, bool trim, hipStream_t);
 void fast_tile_dims(int W, int own_rows, int tile_rows, int tile_w, int* tiles_x, int* ntiles);
 void opp2xyz_over_illum(const float inv_illum[3], float m[9]);
 hipError_t launch_cost_fast(const CostArgs&, int P, int de, bool trim, int tile_rows, int tile_w, int HB,
@@ -42,7 +44,7 @@ void build_fast_taps(int HB, int H, const float* k1, const float* k2, const floa
                      void* out);
 bool trim_window_ok(const float* k1, int H, int HB);
 
-hipError_t launch_cost_generic(const GenArgs&, int de, bool idx32, hipStream_t);
+hipError_t launch_cost_generic(const GenArgs&, int de, int idx_bytes, hipStream_t);
 hipError_t launch_prep_wide(const WideArgs&, int P, hipStream_t);
 hipError_t launch_assign_wide(const WideArgs&, int P, hipStream_t);
 hipError_t launch_finalize(const FinalizeArgs&, int P, hipStream_t);
@@ -119,7 +121,10 @@ struct hq_ctx {
     DevBuf d_pal_in, d_pal, d_opp, d_opp16, d_dup, d_pflags, d_lvl1, d_lvl2, d_idx, d_used_mask,
         d_partial, d_out, d_gen_t;
     DevBuf d_pixerr;           // option "pixel_err": [P][n_own] per-pixel dE of the last evaluation
-    DevBuf d_idx32, d_used32;  // K > 256 (hq_wide.hip): 32-bit index images, per-colour used flags
+    DevBuf d_idx32, d_used32;  // K > 4096 (hq_wide.hip): 32-bit index images, per-colour used flags
+    DevBuf d_idx16, d_dist;    // 256 < K <= 4096 (chunked): 16-bit index images, pass distances
+    int nch_cur = 1;           // chunks per palette of the population being enqueued (1: K <= 256)
+    int last_nch = 1;          // ... of the last evaluation (its index image: u16 when > 1)
     float* h_pal = nullptr;   // pinned [P][K][4]
     double* h_out = nullptr;  // pinned [P][1+K]
     size_t h_pal_bytes = 0, h_out_bytes = 0;
@@ -134,8 +139,10 @@ struct hq_ctx {
     int assign_blocks_per_cu = 0;  // 0 = auto: assign_pipe_kernel<NG>'s residency (the occupancy
                                    // query, assign_res[NG]), one round of workgroups, each
                                    // thread a grid-stride pixel sequence
-    int assign_res[2][5] = {};  // [quad][NG]
-    int assign_quad = 1;   // assign_quad_kernel (dword index stores); 0 = assign_pipe_kernel
+    int assign_res[5] = {};   // [NG]
+    int assign_res_chunked = 0;  // the chunk-combining forms (NG = 4)
+    int chunked = 1;       // 256 < K <= 4096: palettes as 256-colour chunks through the grid and
+                           // tiled kernels (option "chunked"; 0 = the exhaustive K > 256 path)
     int img_u8_path = 1;   // assign reads the packed 8-bit image when there is one (option 'img_u8')
     int shard_solo = 0;    // experiment: a sharded search without a communicator (per-rank timing)
     int sa_device = 1;     // hq_search_*: 1 = SWASA iterations resident on the device (no host
@@ -167,6 +174,7 @@ struct hq_search {
     Swasa* pol = nullptr;
     hq_swasa_params prm{};
     int P = 0, ite = 0, st = 0, cd = 0;  // state and candidate buffer parities
+    int nch = 1;                         // chunked palettes (256 < K <= 4096): chunks per palette
     bool fold = false;                   // accept steps reduce the partials (no finalize launch)
     float t_acc = 0.f;                   // temperature / threshold of the iteration
     double keep_acc = 0.0;               // whose population awaits acceptance
@@ -369,9 +377,8 @@ int assign_blocks(const hq_ctx* c, int P) {
     // workgroups, slowed from 43 to 46 us at 8)
     const int64_t chunk = 256 * HQ_ASSIGN_MINPX;
     const int ng = std::min(P, 4);
-    const int per_cu = c->assign_blocks_per_cu > 0 ? c->assign_blocks_per_cu
-                       : c->assign_res[c->assign_quad][ng] > 0 ? c->assign_res[c->assign_quad][ng]
-                                                   : 4;
+    const int res = c->nch_cur > 1 ? c->assign_res_chunked : c->assign_res[ng];
+    const int per_cu = c->assign_blocks_per_cu > 0 ? c->assign_blocks_per_cu : res > 0 ? res : 4;
     const int64_t nblocks = (int64_t)c->num_cu * per_cu;
     return (int)std::max<int64_t>(1, std::min<int64_t>(nblocks, (c->g.n_ext + chunk - 1) / chunk));
 }
@@ -379,6 +386,12 @@ int assign_blocks(const hq_ctx* c, int P) {
 // Ensure population buffers for P palettes of K colours.
 int ensure_population(hq_ctx* c, int P, int K) {
     const Geom& g = c->g;
+    if (c->nch_cur > 1) {  // chunked palettes: 16-bit indices, then P nch sub-palettes of 256
+        HIP_TRY(c, c->d_idx16.ensure(sizeof(uint16_t) * (size_t)P * g.idx_pitch + 256));
+        if (c->nch_cur > 4) HIP_TRY(c, c->d_dist.ensure(sizeof(float) * (size_t)P * g.idx_pitch));
+        P *= c->nch_cur;  // (d_out, h_out: P nch (1 + 256) >= P (1 + K) doubles)
+        K = kMaxK;
+    }
     const int G2 = c->G2 > 0 ? c->G2 : 4;
     const int G1 = G2 / 4;
     const int64_t l1p = round_up((int64_t)G1 * G1 * G1 * 32, 256);
@@ -442,9 +455,9 @@ GridArgs grid_args(hq_ctx* c, int P, int K) {
 
 // The generic two-pass cost (CL:234-306 per pixel, any half-width) of P
 // palettes, one launch pair each: index images at idx_base (u8, or u32 when
-// idx32) with c->g.idx_pitch elements per palette, opponent tables of
+// u16 (chunked palettes) or u32, idx_bytes) with c->g.idx_pitch elements per palette, opponent tables of
 // opp_stride entries per palette in d_opp.  The cost events time all P pairs.
-int enqueue_generic_cost(hq_ctx* c, int P, const void* idx_base, bool idx32, int opp_stride,
+int enqueue_generic_cost(hq_ctx* c, int P, const void* idx_base, int idx_bytes, int opp_stride,
                          const hipEvent_t* ev, int* nparts_out) {
     const Geom& g = c->g;
     hipStream_t s = c->stream;
@@ -454,7 +467,7 @@ int enqueue_generic_cost(hq_ctx* c, int P, const void* idx_base, bool idx32, int
     const float inv[3] = {1.0f / c->illum[0], 1.0f / c->illum[1], 1.0f / c->illum[2]};
     for (int p = 0; p < P; ++p) {
         GenArgs gn{};
-        gn.idx = static_cast<const char*>(idx_base) + (int64_t)p * g.idx_pitch * (idx32 ? 4 : 1);
+        gn.idx = static_cast<const char*>(idx_base) + (int64_t)p * g.idx_pitch * idx_bytes;
         gn.opp = c->d_opp.as<float4>() + (int64_t)p * opp_stride;
         gn.k1 = c->d_k1.as<float>();
         gn.k2 = c->d_k2.as<float>();
@@ -471,7 +484,7 @@ int enqueue_generic_cost(hq_ctx* c, int P, const void* idx_base, bool idx32, int
         opp2xyz_over_illum(inv, gn.m_lab);
         // the events span every palette's launch pair: start on the first, stop on the last
         if (ev) set_launch_events(p == 0 ? ev[4] : nullptr, p == P - 1 ? ev[5] : nullptr);
-        const hipError_t e = launch_cost_generic(gn, c->de_type, idx32, s);
+        const hipError_t e = launch_cost_generic(gn, c->de_type, idx_bytes, s);
         set_launch_events(nullptr, nullptr);
         HIP_TRY(c, e);
     }
@@ -495,10 +508,10 @@ int enqueue_wide(hq_ctx* c, int P, int K, const hipEvent_t* ev) {
     set_launch_events(nullptr, nullptr);
     HIP_TRY(c, e);
     int nparts = 0;
-    int rc = enqueue_generic_cost(c, P, c->d_idx32.p, true, K, ev, &nparts);
+    int rc = enqueue_generic_cost(c, P, c->d_idx32.p, 4, K, ev, &nparts);
     if (rc) return rc;
     FinalizeArgs fa{c->d_partial.as<double>(), nullptr, 0, c->d_out.as<double>(), nparts, K,
-                    c->d_used32.as<uint32_t>()};
+                    c->d_used32.as<uint32_t>(), 8};
     if (ev) set_launch_events(ev[6], ev[7]);
     const hipError_t ef = launch_finalize(fa, P, s);
     set_launch_events(nullptr, nullptr);
@@ -507,43 +520,58 @@ int enqueue_wide(hq_ctx* c, int P, int K, const hipEvent_t* ev) {
         NCCL_TRY(c, ncclAllReduce(c->d_out.p, c->d_out.p, (size_t)P * (1 + K), ncclFloat64, ncclSum, c->comm, s));
     c->last_P = P;
     c->K_cur = K;
+    c->last_nch = 1;
     return HQ_OK;
 }
 
+// P palettes of K colours.  Chunked palettes (c->nch_cur = nch > 1, 256 < K <=
+// 256 nch): the grid and assign run on P nch sub-palettes of 256 colours (d_pal
+// etc. hold them, prep_palette made them), assign combines them into 16-bit
+// indices, the cost kernel reads those with a 256 nch-entry table.
 int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = false) {
     const Geom& g = c->g;
     hipStream_t s = c->stream;
-    const GridArgs ga = grid_args(c, P, K);
+    const int nch = c->nch_cur, Ps = P * nch, Ks = nch > 1 ? kMaxK : K;
+    const GridArgs ga = grid_args(c, Ps, Ks);
     auto timed = [&](int slot) {
         if (ev) set_launch_events(ev[2 * slot], ev[2 * slot + 1]);
     };
     auto untimed = [&]() { set_launch_events(nullptr, nullptr); };
     if (c->G2 > 0) {  // (build_grid also zeroes the used bits)
         timed(0);
-        const hipError_t e = launch_build_grid(ga, P, s);
+        const hipError_t e = launch_build_grid(ga, Ps, s);
         untimed();
         HIP_TRY(c, e);
     } else {
-        HIP_TRY(c, hipMemsetAsync(c->d_used_mask.p, 0, sizeof(uint32_t) * kUsedSlots * (size_t)used_stride(P), s));
+        HIP_TRY(c, hipMemsetAsync(c->d_used_mask.p, 0, sizeof(uint32_t) * kUsedSlots * (size_t)used_stride(Ps), s));
     }
-    const int nblocks = assign_blocks(c, P);
-    const AssignArgs aa{c->d_R.as<float>(), c->d_G.as<float>(), c->d_B.as<float>(),
-                        c->img_u8 && c->img_u8_path ? c->d_rgbx.as<uint32_t>() : nullptr, c->d_pal.as<float4>(),
-                        c->d_pflags.as<int>(), c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(),
-                        c->d_idx.as<uint8_t>(), c->d_used_mask.as<uint32_t>(), used_stride(P), g.n_ext, g.idx_pitch,
-                        ga.lvl1_pitch, ga.lvl2_gstride, K, c->G2, nblocks};
+    const int nblocks = assign_blocks(c, Ps);
+    AssignArgs aa{c->d_R.as<float>(), c->d_G.as<float>(), c->d_B.as<float>(),
+                  c->img_u8 && c->img_u8_path ? c->d_rgbx.as<uint32_t>() : nullptr, c->d_pal.as<float4>(),
+                  c->d_pflags.as<int>(), c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(),
+                  c->d_idx.as<uint8_t>(), c->d_used_mask.as<uint32_t>(), used_stride(Ps), g.n_ext, g.idx_pitch,
+                  ga.lvl1_pitch, ga.lvl2_gstride, Ks, c->G2, nblocks};
+    if (nch > 1) {
+        aa.idx16 = c->d_idx16.as<uint16_t>();
+        aa.dist = nch > 4 ? c->d_dist.as<float>() : nullptr;
+        aa.nch = nch;
+        while ((1 << aa.lg_nch) < nch) ++aa.lg_nch;
+    }
     timed(1);
-    hipError_t e = launch_assign(aa, P, s, c->assign_quad != 0);
+    hipError_t e = launch_assign(aa, Ps, s);
     untimed();
     HIP_TRY(c, e);
     const float inv[3] = {1.0f / c->illum[0], 1.0f / c->illum[1], 1.0f / c->illum[2]};
     int nparts;
-    if (c->cost_variant != 1 && c->fast_hb > 0 && !c->pal_generic) {
+    // chunked palettes: the 16 x 128 tiles at HB = 10 (else the generic path)
+    const bool fast = c->cost_variant != 1 && c->fast_hb > 0 && !c->pal_generic &&
+                      (nch == 1 || (c->fast_hb == 10 && c->cost_rows == 16 && c->cost_tw == 128));
+    if (fast) {
         // 8-row tiles (cost_mfma_kernel) exist for the 21-tap bucket only
         const int rows = c->fast_hb == 10 ? c->cost_rows : 16;
         const int tw = c->fast_hb == 10 ? c->cost_tw : 128;  // 256-column tiles: HB = 10 only
         CostArgs ca{};
-        ca.idx = c->d_idx.as<uint8_t>();
+        ca.idx = nch > 1 ? c->d_idx16.as<uint8_t>() : c->d_idx.as<uint8_t>();
         ca.opp16 = c->d_opp16.as<uint4>();
         ca.taps = c->d_taps.p;
         ca.vfrag16 = c->d_vfrag16.as<uint4>();
@@ -558,18 +586,20 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
         ca.pix_err = c->pixel_err ? c->d_pixerr.as<float>() : nullptr;
         ca.pix_pitch = (int64_t)g.W * (g.r1 - g.r0);
         timed(2);
-        e = launch_cost_fast(ca, P, c->de_type, c->trim && c->trim_ok, rows, tw, c->fast_hb, s);
+        e = nch > 1 ? launch_cost_chunked(ca, P, nch, c->de_type, c->trim && c->trim_ok, s)
+                    : launch_cost_fast(ca, P, c->de_type, c->trim && c->trim_ok, rows, tw, c->fast_hb, s);
         untimed();
         HIP_TRY(c, e);
         nparts = ca.ntiles;
     } else {
-        int rc = enqueue_generic_cost(c, P, c->d_idx.p, false, kMaxK, ev, &nparts);
+        int rc = nch > 1 ? enqueue_generic_cost(c, P, c->d_idx16.p, 2, nch * kMaxK, ev, &nparts)
+                         : enqueue_generic_cost(c, P, c->d_idx.p, 1, kMaxK, ev, &nparts);
         if (rc) return rc;
     }
     c->last_nparts = nparts;
     if (!fold) {  // (a folding search's accept step reduces the partials itself)
-        FinalizeArgs fa{c->d_partial.as<double>(), c->d_used_mask.as<uint32_t>(), used_stride(P), c->d_out.as<double>(),
-                        nparts, K, nullptr};
+        FinalizeArgs fa{c->d_partial.as<double>(), c->d_used_mask.as<uint32_t>(), used_stride(Ps),
+                        c->d_out.as<double>(), nparts, K, nullptr, 8 * nch};
         timed(3);
         const hipError_t ef = launch_finalize(fa, P, s);
         untimed();
@@ -581,6 +611,7 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
     }
     c->last_P = P;
     c->K_cur = K;
+    c->last_nch = nch;
     return HQ_OK;
 }
 
@@ -596,11 +627,14 @@ void prof_accumulate(hq_ctx* c, const hipEvent_t* ev, bool finalize = true, bool
 // read back d_out into h_out.
 int enqueue_eval(hq_ctx* c, int P, int K) {
     hipStream_t s = c->stream;
-    HIP_TRY(c, hipMemcpyAsync(c->d_pal_in.p, c->h_pal, sizeof(float) * 4 * (size_t)P * K,
-                              hipMemcpyHostToDevice, s));
+    const size_t n_in = c->nch_cur > 1 ? (size_t)P * c->nch_cur * kMaxK : (size_t)P * K;
+    HIP_TRY(c, hipMemcpyAsync(c->d_pal_in.p, c->h_pal, sizeof(float4) * n_in, hipMemcpyHostToDevice, s));
     const hipEvent_t* ev = c->prof ? c->ev : nullptr;
     int rc;
-    if (K > kMaxK) {
+    if (c->nch_cur > 1) {  // h_pal holds P nch sub-palettes of 256 (pack_chunks)
+        HIP_TRY(c, launch_prep_palette(prep_args(c, kMaxK), P * c->nch_cur, s));
+        rc = enqueue_core(c, P, K, ev);
+    } else if (K > kMaxK) {
         rc = enqueue_wide(c, P, K, ev);
     } else {
         HIP_TRY(c, launch_prep_palette(prep_args(c, K), P, s));
@@ -610,7 +644,7 @@ int enqueue_eval(hq_ctx* c, int P, int K) {
     HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out.p, sizeof(double) * (size_t)P * (1 + K),
                               hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
-    if (ev) prof_accumulate(c, ev, true, K <= kMaxK);  // (K > 256 builds no grid)
+    if (ev) prof_accumulate(c, ev, true, K <= kMaxK || c->nch_cur > 1);  // (the wide path builds no grid)
     return HQ_OK;
 }
 
@@ -632,6 +666,19 @@ int check_eval_args(hq_ctx* c, const float* palettes, int P, int K) {
 // above).  Colours outside [-32, 1.9] -- never produced by the SA, which
 // clamps to [0, 1] (SW:103-106), but accepted by hq_eval_population -- and
 // non-finite colours send the population to the generic fp32 path.
+// [P][K] palettes -> P nch sub-palettes of 256 colours: sub-palette p nch + c
+// holds colours 256 c .. 256 c + 255 of palette p, and copies of colour 0 past
+// K (a copy of colour 0 ties it and never wins the chunk combine, which keeps
+// the first chunk at equal distance; hq_assign.hip).
+void pack_chunks(const float* pal, int P, int K, int nch, float* out) {
+    for (int p = 0; p < P; ++p)
+        for (int k = 0; k < nch * kMaxK; ++k) {
+            const float* src = pal + 4 * ((size_t)p * K + (k < K ? k : 0));
+            float* dst = out + 4 * ((size_t)p * nch * kMaxK + k);
+            dst[0] = src[0]; dst[1] = src[1]; dst[2] = src[2]; dst[3] = src[3];
+        }
+}
+
 bool palette_fits_fast(const float* pal, int P, int K) {
     for (size_t i = 0, n = (size_t)P * K; i < n; ++i)
         for (int ch = 0; ch < 3; ++ch) {
@@ -645,17 +692,32 @@ int eval_partial_into_hout(hq_ctx* c, const float* palettes, int P, int K) {
     int rc = check_eval_args(c, palettes, P, K);
     if (rc) return rc;
     if ((rc = bind(c))) return rc;
+    const bool fits = palette_fits_fast(palettes, P, K);
+    // 256 < K <= 4096: chunks of 256 colours through the grid, assign and tiled
+    // cost kernels.  Palettes outside the fast range (non-finite colours among
+    // them) take the exhaustive K > 256 path instead, which keeps the
+    // reference's NaN semantics across all K colours.
+    c->nch_cur = c->chunked && fits && c->G2 > 0 && K > kMaxK && K <= kMaxKChunked ? chunk_count(K) : 1;
     if ((rc = ensure_population(c, P, K))) return rc;
-    std::memcpy(c->h_pal, palettes, sizeof(float) * 4 * (size_t)P * K);
-    c->pal_generic = !palette_fits_fast(palettes, P, K);
+    if (c->nch_cur > 1) pack_chunks(palettes, P, K, c->nch_cur, c->h_pal);
+    else std::memcpy(c->h_pal, palettes, sizeof(float) * 4 * (size_t)P * K);
+    c->pal_generic = !fits;
     rc = enqueue_eval(c, P, K);
     c->pal_generic = false;  // device-resident searches generate clamped palettes
+    c->nch_cur = 1;
     return rc;
 }
 
 }  // namespace
 
 namespace {
+
+// The chunk count of the population being enqueued, for one search call.
+struct NchScope {
+    hq_ctx* c;
+    NchScope(hq_ctx* cc, int nch) : c(cc) { c->nch_cur = nch; }
+    ~NchScope() { c->nch_cur = 1; }
+};
 
 // One sa_step launch: accept the population in cand[cd] (if `accept`), then
 // generate the next candidates into cand[1 - cd] (if `generate`).
@@ -675,7 +737,8 @@ int enqueue_sa_step(hq_search* s, bool accept, bool init, bool generate, bool ra
     a.best_colors = s->best_colors.as<float>();
     a.jump_A = s->jA.as<uint64_t>();
     a.jump_C = s->jC.as<uint64_t>();
-    a.prep = prep_args(c, s->K);
+    a.prep = prep_args(c, s->nch > 1 ? kMaxK : s->K);
+    a.nch = s->nch;
     a.n_total = (double)c->g.W * (double)c->g.H;
     a.keep_threshold = s->keep_acc;
     a.temperature = s->t_acc;
@@ -690,7 +753,7 @@ int enqueue_sa_step(hq_search* s, bool accept, bool init, bool generate, bool ra
     a.convergence = s->prm.convergence;
     a.partial = c->d_partial.as<double>();
     a.used_glob = c->d_used_mask.as<uint32_t>();
-    a.used_stride = used_stride(a.P);
+    a.used_stride = used_stride(a.P * s->nch);
     a.ntiles = c->last_nparts;
     a.fold = s->fold;
     HIP_TRY(c, launch_sa_step(a, c->stream));
@@ -716,6 +779,7 @@ int device_search_create(hq_ctx* c, const hq_swasa_params* params, int K, uint64
     // step reduces the partials itself (one launch less per iteration)
     s->fold = !c->comm && P <= kFoldMaxP;
     s->pol = new Swasa(*params, seed);
+    const NchScope scope(c, s->nch);
     int rc = ensure_population(c, P, K);
     if (rc) return rc;
     const size_t n4 = (size_t)P * 4 * K;
@@ -764,6 +828,7 @@ int device_search_run(hq_search* s, int iterations, int* ran) {
     if (!c->have_image) return fail(c, HQ_ERR_STATE, "no image set (hq_set_image)");
     if (c->de_type == HQ_DE_CIEDE2000)
         return fail(c, HQ_ERR_UNSUPPORTED, "CIEDE2000 is unimplemented in the reference (CL:227-230)");
+    const NchScope scope(c, s->nch);
     if ((rc = ensure_population(c, s->P, s->K))) return rc;
     if (s->fold && c->comm)
         return fail(c, HQ_ERR_STATE, "communicator set after hq_search_create: recreate the search");
@@ -835,8 +900,8 @@ int hq_create(int device, int delta_e_type, hq_ctx** out) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         c->num_cu = prop.multiProcessorCount;
-    for (int qd = 0; qd < 2; ++qd)
-        for (int ng = 1; ng <= 4; ++ng) c->assign_res[qd][ng] = assign_residency(ng, qd != 0);
+    for (int ng = 1; ng <= 4; ++ng) c->assign_res[ng] = assign_residency(ng);
+    c->assign_res_chunked = assign_residency_chunked();
     for (auto& e : c->ev) (void)hipEventCreate(&e);
     *out = c;
     return HQ_OK;
@@ -851,7 +916,7 @@ void hq_destroy(hq_ctx* c) {
                       &c->d_labL, &c->d_labA, &c->d_labB, &c->d_pal_in, &c->d_pal, &c->d_opp, &c->d_opp16,
                       &c->d_dup, &c->d_pflags, &c->d_lvl1, &c->d_lvl2, &c->d_idx,
                       &c->d_used_mask, &c->d_partial, &c->d_out, &c->d_gen_t, &c->d_taps,
-                      &c->d_vfrag16, &c->d_idx32, &c->d_used32, &c->d_pixerr})
+                      &c->d_vfrag16, &c->d_idx32, &c->d_used32, &c->d_pixerr, &c->d_idx16, &c->d_dist})
         b->release();
     if (c->h_pal) (void)hipHostFree(c->h_pal);
     if (c->h_out) (void)hipHostFree(c->h_out);
@@ -1017,6 +1082,13 @@ int hq_get_indices32(hq_ctx* c, int p, uint32_t* idx) {
     const Geom& g = c->g;
     const int64_t off = (int64_t)(g.r0 - g.e0) * g.W;
     const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
+    if (c->last_nch > 1) {  // chunked palettes: 16-bit indices
+        std::vector<uint16_t> b((size_t)n_own);
+        HIP_TRY(c, hipMemcpy(b.data(), c->d_idx16.as<uint16_t>() + (int64_t)p * g.idx_pitch + off,
+                             sizeof(uint16_t) * n_own, hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < n_own; ++i) idx[i] = b[i];
+        return HQ_OK;
+    }
     if (c->K_cur > kMaxK) {
         HIP_TRY(c, hipMemcpy(idx, c->d_idx32.as<uint32_t>() + (int64_t)p * g.idx_pitch + off,
                              sizeof(uint32_t) * n_own, hipMemcpyDeviceToHost));
@@ -1179,7 +1251,10 @@ int hq_search_create(hq_ctx* c, const hq_swasa_params* params, int K, uint64_t s
     *out = nullptr;
     if (params->population < 1 || params->imax < 1 || params->iTc < 1 || K < 1)
         return fail(c, HQ_ERR_ARG, "bad SWASA parameters");
-    const bool device = c->sa_device && params->population <= kSaMaxP && K <= kMaxK;
+    // device-resident: K <= 256, or chunked palettes (256 < K <= 4096) of at most
+    // kSaMaxP sub-palettes in all
+    const int nch = K > kMaxK && K <= kMaxKChunked && c->chunked && c->G2 > 0 ? chunk_count(K) : 1;
+    const bool device = c->sa_device && params->population * nch <= kSaMaxP && (K <= kMaxK || nch > 1);
     hq_search* s = new hq_search{c, nullptr, K};
     int rc;
     if (device) {
@@ -1196,6 +1271,7 @@ int hq_search_create(hq_ctx* c, const hq_swasa_params* params, int K, uint64_t s
             hq_search_destroy(s);
             return fail(c, HQ_ERR_STATE, "sharded context without a communicator");
         }
+        s->nch = nch;
         rc = device_search_create(c, params, K, seed, s);
     } else {
         const float delta = params->delta;
@@ -1303,8 +1379,8 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
         c->sa_device = value != 0;
     } else if (!std::strcmp(name, "shard_solo")) {
         c->shard_solo = value != 0;
-    } else if (!std::strcmp(name, "assign_quad")) {
-        c->assign_quad = value != 0;
+    } else if (!std::strcmp(name, "chunked")) {
+        c->chunked = value != 0;
     } else if (!std::strcmp(name, "pixel_err")) {
         c->pixel_err = value != 0;
     } else if (!std::strcmp(name, "img_u8")) {

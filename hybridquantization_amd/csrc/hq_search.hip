@@ -168,6 +168,7 @@ struct SaShared {
 __device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared& s) {
 #pragma clang fp contract(off)
     const int tid = threadIdx.x, nt = blockDim.x, P = a.P, K = a.K;
+    const int wpp = 8 * a.nch;  // used words per palette (chunked palettes: 8 per chunk)
     constexpr int MAXF = 16;  // used flags per thread held in registers
     const int nf = (P * K + nt - 1) / nt;
     double fv[MAXF];
@@ -178,7 +179,7 @@ __device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared
         // loads are out: an LDS store of a just-loaded value waits for it, and
         // the wait (in-order counters) held back every partial load behind it
         const double ein = tid < P ? a.err_in[tid] : 0.0;
-        if (tid < 8 * P) {
+        if (tid < wpp * P) {
             uint32_t wv[kUsedSlots];
 #pragma unroll
             for (int sl = 0; sl < kUsedSlots; ++sl) wv[sl] = a.used_glob[sl * a.used_stride + tid];
@@ -226,11 +227,11 @@ __device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared
             const double w = wave_sum_to_lane63(fold_acc[p]);
             if ((tid & 63) == 63) s.fold_red[p][tid >> 6] = w;
         }
-        if (tid < 8 * P) {  // unused colours: clear bits below K
-            const int nbits = min(max(K - 32 * (tid & 7), 0), 32);
+        if (tid < wpp * P) {  // unused colours: clear bits below K
+            const int nbits = min(max(K - 32 * (tid % wpp), 0), 32);
             const uint32_t valid = nbits >= 32 ? ~0u : ((1u << nbits) - 1u);
             const int clear = nbits - __popc(fold_word & valid);
-            if (clear) atomicAdd(&s.unused[tid >> 3], clear);
+            if (clear) atomicAdd(&s.unused[tid / wpp], clear);
         }
     } else if (a.accept) {
         if (nf <= MAXF) {
@@ -314,55 +315,69 @@ __device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared
     __syncthreads();
 }
 
-// Member p's accepted palette into s_from (LDS, 4K floats); `lead` also copies
-// it to colors_out (and, for p = 0, a new best to best_colors).  The two likely
+// Member p's accepted palette into s_from (LDS, 4K floats; chunked palettes:
+// elements e0 .. e0 + 1023 of it, chunk c = e0 / 1024); `lead` also copies it
+// to colors_out (and, for p = 0, a new best to best_colors).  The two likely
 // sources -- member p's candidate and its kept palette -- are read before the
-// acceptance (pf_cand, pf_col: element tid); only a convergence copy from
+// acceptance (pf_cand, pf_col: element e0 + tid); only a convergence copy from
 // another member's candidate reads after it.
-__device__ __forceinline__ void sa_keep(const SaArgs& a, int p, bool lead, const SaShared& s,
+__device__ __forceinline__ void sa_keep(const SaArgs& a, int p, int e0, bool lead, const SaShared& s,
                                         float pf_cand, float pf_col, float* s_from) {
     const int n4 = 4 * a.K, tid = threadIdx.x, nt = blockDim.x;
+    const int ne = a.nch > 1 ? min(4 * kMaxK, n4 - e0) : n4;
     const int src = s.src[p];
-    for (int e = tid; e < n4; e += nt) {
+    for (int i = tid; i < ne; i += nt) {
+        const int e = e0 + i;
         float v;
-        if (e == tid && src == p) v = pf_cand;
-        else if (e == tid && src < 0) v = pf_col;
+        if (i == tid && src == p) v = pf_cand;
+        else if (i == tid && src < 0) v = pf_col;
         else v = src >= 0 ? a.cand_in[(int64_t)src * n4 + e] : a.colors_in[(int64_t)p * n4 + e];
-        s_from[e] = v;
+        s_from[i] = v;
         if (lead) a.colors_out[(int64_t)p * n4 + e] = v;
     }
     if (lead && p == 0 && s.best >= 0)  // IM:533-536: the best palette so far
-        for (int e = tid; e < n4; e += nt) a.best_colors[e] = a.cand_in[(int64_t)s.best * n4 + e];
+        for (int i = tid; i < ne; i += nt) a.best_colors[e0 + i] = a.cand_in[(int64_t)s.best * n4 + e0 + i];
     __syncthreads();
 }
 
 // Candidate p into s_cand (.w = 0; cand_out too when `lead`): draw t = 3i + c of
 // this palette's block (SW:91-101 neighbours of s_from, or SW:40-52 random).
-// jA/jC: this thread's prefetched jump to its first draw (t = tid).
-__device__ __forceinline__ void sa_generate(const SaArgs& a, int p, const float* s_from, uint64_t seed,
-                                            float4* s_cand, bool lead, uint64_t jA, uint64_t jC,
-                                            uint64_t bA, uint64_t bC) {
+// jA/jC: this thread's prefetched jump to its first draw (t = t0 + tid).
+// Chunked palettes: chunk ch = colours 256 ch .. (draws t0 = 768 ch ..), and
+// the chunk's colours past K are copies of candidate colour 0 (pack_chunks'
+// padding), drawn again here from its source colour `src0`.
+__device__ __forceinline__ float sa_draw(const SaArgs& a, uint64_t st, float from) {
 #pragma clang fp contract(off)
+    const float u = (float)(int32_t)(st >> 24) / (float)(1 << 24);
+    if (a.random) return u;
+    const float step = (u * 2 - 1) * a.amax;
+    const float x = from + step;
+    return x > 0.f ? (x > 1.f ? 1.f : x) : 0.f;  // clampf_java (SW:103-106)
+}
+
+__device__ __forceinline__ void sa_generate(const SaArgs& a, int p, int ch, const float* s_from,
+                                            const float* src0, uint64_t seed, float4* s_cand, bool lead,
+                                            uint64_t jA, uint64_t jC, uint64_t bA, uint64_t bC) {
     const int K = a.K, n4 = 4 * K, tid = threadIdx.x, nt = blockDim.x;
+    const int k0 = a.nch > 1 ? kMaxK * ch : 0, kn = a.nch > 1 ? min(kMaxK, K - k0) : K;  // real colours
+    const int t0 = 3 * k0;
     const uint64_t base = lcg_jump(seed, bA, bC);  // bA, bC: jump_A/C[3Kp], prefetched
-    for (int t = tid; t < 3 * K; t += nt) {
-        const int i = t / 3, c = t - 3 * i;
-        const uint64_t st = t == tid ? lcg_jump(base, jA, jC) : lcg_jump(base, a.jump_A[t + 1], a.jump_C[t + 1]);
-        const float u = (float)(int32_t)(st >> 24) / (float)(1 << 24);
-        float v;
-        if (a.random) {
-            v = u;
-        } else {
-            const float step = (u * 2 - 1) * a.amax;
-            const float x = s_from[4 * i + c] + step;
-            v = x > 0.f ? (x > 1.f ? 1.f : x) : 0.f;  // clampf_java (SW:103-106)
-        }
+    for (int tt = tid; tt < 3 * kn; tt += nt) {
+        const int t = t0 + tt, i = tt / 3, c = tt - 3 * i;
+        const uint64_t st = tt == tid ? lcg_jump(base, jA, jC) : lcg_jump(base, a.jump_A[t + 1], a.jump_C[t + 1]);
+        const float v = sa_draw(a, st, s_from[4 * i + c]);
         reinterpret_cast<float*>(s_cand)[4 * i + c] = v;
-        if (lead) a.cand_out[(int64_t)p * n4 + 4 * i + c] = v;
+        if (lead) a.cand_out[(int64_t)p * n4 + 4 * (k0 + i) + c] = v;
     }
-    for (int k = tid; k < K; k += nt) {
+    for (int k = tid; k < kn; k += nt) {
         reinterpret_cast<float*>(s_cand)[4 * k + 3] = 0.f;
-        if (lead) a.cand_out[(int64_t)p * n4 + 4 * k + 3] = 0.f;
+        if (lead) a.cand_out[(int64_t)p * n4 + 4 * (k0 + k) + 3] = 0.f;
+    }
+    if (a.nch > 1 && kn < kMaxK) {  // padding: candidate colour 0 (draws 0, 1, 2)
+        __shared__ float s_c0[3];
+        if (tid < 3) s_c0[tid] = sa_draw(a, lcg_jump(base, a.jump_A[tid + 1], a.jump_C[tid + 1]), src0[tid]);
+        __syncthreads();
+        for (int k = kn + tid; k < kMaxK; k += nt) s_cand[k] = make_float4(s_c0[0], s_c0[1], s_c0[2], 0.f);
     }
     __syncthreads();
 }
@@ -372,15 +387,18 @@ __device__ __forceinline__ void sa_generate(const SaArgs& a, int p, const float*
 struct SaPf {
     float cand = 0.f, col = 0.f;
     uint64_t jA = 0, jC = 0, bA = 0, bC = 0;
-    __device__ __forceinline__ void load(const SaArgs& a, int p) {
+    __device__ __forceinline__ void load(const SaArgs& a, int p, int ch) {
         const int n4 = 4 * a.K, tid = threadIdx.x;
-        if (tid < n4) {
-            if (a.accept) cand = a.cand_in[(int64_t)p * n4 + tid];
-            col = a.colors_in[(int64_t)p * n4 + tid];
+        const int e = a.nch > 1 ? 4 * kMaxK * ch + tid : tid, t = a.nch > 1 ? 3 * kMaxK * ch + tid : tid;
+        if (e < n4 && (a.nch == 1 || tid < 4 * kMaxK)) {
+            if (a.accept) cand = a.cand_in[(int64_t)p * n4 + e];
+            col = a.colors_in[(int64_t)p * n4 + e];
         }
-        if (a.generate && tid < 3 * a.K) {
-            jA = a.jump_A[tid + 1];
-            jC = a.jump_C[tid + 1];
+        if (a.generate && t < 3 * a.K && (a.nch == 1 || tid < 3 * kMaxK)) {
+            jA = a.jump_A[t + 1];
+            jC = a.jump_C[t + 1];
+        }
+        if (a.generate) {
             bA = a.jump_A[3 * a.K * p];
             bC = a.jump_C[3 * a.K * p];
         }
@@ -389,8 +407,12 @@ struct SaPf {
 
 // Build with -DHQ_SA_TIMING to print block 0's phase times (accept, keep,
 // generate, prep; wall_clock64 ticks of 10 ns) per launch.
+// Chunked palettes (a.nch > 1): workgroup p nch + ch keeps, generates and
+// preps chunk ch of member p (sub-palette p nch + ch); every workgroup runs the
+// acceptance itself.
 __global__ __launch_bounds__(1024) void sa_step_kernel(SaArgs a) {
-    const int p = blockIdx.x, K = a.K;
+    const int p = blockIdx.x / a.nch, ch = blockIdx.x % a.nch;
+    const int K = a.nch > 1 ? kMaxK : a.K;  // colours prepped by this workgroup
     __shared__ SaShared s;
     __shared__ float s_from[4 * kMaxK];
     __shared__ float4 s_cand[kMaxK];
@@ -398,22 +420,30 @@ __global__ __launch_bounds__(1024) void sa_step_kernel(SaArgs a) {
     const uint64_t t0 = wall_clock64();
 #endif
     SaPf pf;
-    pf.load(a, p);
-    sa_accept(a, p == 0, s);
+    pf.load(a, p, ch);
+    sa_accept(a, blockIdx.x == 0, s);
 #ifdef HQ_SA_TIMING
     const uint64_t t1 = wall_clock64();
 #endif
-    sa_keep(a, p, true, s, pf.cand, pf.col, s_from);
+    const int e0 = 4 * kMaxK * ch;
+    sa_keep(a, p, e0, true, s, pf.cand, pf.col, s_from);
 #ifdef HQ_SA_TIMING
     const uint64_t t2 = wall_clock64();
 #endif
     if (!a.generate) return;
-    sa_generate(a, p, s_from, s.seed, s_cand, true, pf.jA, pf.jC, pf.bA, pf.bC);
+    // chunks past colour 0's: its source colour (the member's accepted colour 0)
+    __shared__ float s_src0[3];
+    if (a.nch > 1 && ch > 0 && threadIdx.x < 3) {
+        const int src = s.src[p], n4 = 4 * a.K;
+        s_src0[threadIdx.x] = src >= 0 ? a.cand_in[(int64_t)src * n4 + threadIdx.x]
+                                       : a.colors_in[(int64_t)p * n4 + threadIdx.x];
+    }
+    sa_generate(a, p, ch, s_from, ch > 0 ? s_src0 : s_from, s.seed, s_cand, true, pf.jA, pf.jC, pf.bA, pf.bC);
 #ifdef HQ_SA_TIMING
     const uint64_t t3 = wall_clock64();
 #endif
     const int k = threadIdx.x;
-    prep_palette_body(a.prep, p, k < K ? s_cand[k] : make_float4(0.f, 0.f, 0.f, 0.f));
+    prep_palette_body(a.prep, blockIdx.x, k < K ? s_cand[k] : make_float4(0.f, 0.f, 0.f, 0.f));
 #ifdef HQ_SA_TIMING
     __syncthreads();
     if (threadIdx.x == 0 && p == 0)
@@ -828,7 +858,7 @@ __global__ __launch_bounds__(1024) void finalize_kernel(FinalizeArgs a) {
         const uint32_t* u = a.used32 + (int64_t)p * a.K;
         for (int k = tid; k < a.K; k += NT) out[1 + k] = u[k] != 0u ? 1.0 : 0.0;
     } else {
-        const uint32_t* u = a.used_glob + (int64_t)p * 8;
+        const uint32_t* u = a.used_glob + (int64_t)p * a.wpp;
         for (int k = tid; k < a.K; k += NT) {
             uint32_t w = 0u;
 #pragma unroll
@@ -853,7 +883,7 @@ hipError_t launch_prep_palette(const PaletteArgs& a, int P, hipStream_t s) {
 }
 
 hipError_t launch_sa_step(const SaArgs& a, hipStream_t s) {
-    HQ_LAUNCH(sa_step_kernel, dim3(a.P), dim3(1024), 0, s, a);
+    HQ_LAUNCH(sa_step_kernel, dim3(a.P * a.nch), dim3(1024), 0, s, a);
     return hipGetLastError();
 }
 

@@ -14,6 +14,7 @@ for cfg in "" "--dpi 96 --distance 60" "--size 1024 --K 1024 --steps 10 --warmup
 done
 timeout -k 10 300 python bench.py --no-cpu-baseline --no-full-search --shard-of 8 > $O/shard8.json 2> $O/shard8.err || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --no-cpu-baseline --no-full-search --steps 50 > $O/bench_rocprof.json 2> $O/bench_rocprof.err || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof8 -o run -- python3 bench.py --no-cpu-baseline --no-full-search --shard-of 8 --steps 100 > $O/shard8_rocprof.json 2> $O/shard8_rocprof.err || exit $?
 timeout -k 10 120 ./scripts/mbs > $O/mbs.txt || exit $?
 python3 -c "
 import json

@@ -411,14 +411,16 @@ def test_out_of_range_palette_takes_generic_path(ip, filt):
         np.testing.assert_array_equal(ip.getIndices(p), parts["idx"].astype(np.uint8))
 
 
-@pytest.mark.parametrize("K", [257, 1024, 4096])
-def test_wide_palette_vs_oracle(gpu, filt, K):
-    """K > 256 (the plugin allows up to 2^24, HybridQuantization.java:192):
-    32-bit indices from the exhaustive argmin (hq_wide.hip) and the generic
-    stencil path.  Indices and used flags bit-exact against the oracle's
-    argmin (CL:172-193), costs within 1e-5 relative (the bar is 1e-4), on a
-    256 x 256 image with duplicate colours, colours one ulp apart and colours
-    equal to pixels (exact ties)."""
+@pytest.mark.parametrize("K,P", [(257, 2), (300, 3), (600, 2), (1024, 2), (1500, 1), (4096, 2)])
+def test_wide_palette_vs_oracle(gpu, filt, K, P):
+    """K > 256 (the plugin allows up to 2^24, HybridQuantization.java:192).  Up
+    to K = 4096 the palettes run as 256-colour chunks through the grid, assign
+    (16-bit indices, chunk winners combined by the reference distance) and the
+    tiled cost kernel; nch = 2 with P odd leaves a group of two sub-palettes,
+    nch = 8 and 16 run assign in passes.  Indices and used flags bit-exact
+    against the oracle's argmin (CL:172-193), costs within 1e-5 relative (the
+    bar is 1e-4), on a 256 x 256 image with duplicate colours (also across
+    chunks), colours one ulp apart and colours equal to pixels (exact ties)."""
     w = h = 256
     R, G, B = o.synthetic_image(w, h, seed=K)
     rgba = o.inline_rgba(R, G, B)
@@ -426,14 +428,14 @@ def test_wide_palette_vs_oracle(gpu, filt, K):
     hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
     m.setImage(rgba.reshape(-1), None, w, filt.illum)
     lab = m.getLabRef().reshape(-1, 4)
-    pals = np.stack([o.synthetic_palette(K, 900 + p) for p in range(2)])
+    pals = np.stack([o.synthetic_palette(K, 900 + p) for p in range(P)])
     pals[0, K // 2, :3] = np.nextafter(pals[0, 3, :3], np.float32(1))
     pals[0, K - 1] = pals[0, 7]
-    pals[1, 100:110, :3] = rgba[1000:1010, :3]
-    pals[1, K - 5:, :3] = rgba[1000:1005, :3]  # same colours again at higher indices
-    costs, used = m.computeQuantizationErrorPopulation(pals.reshape(2, -1), 2.0, return_used=True)
+    pals[-1, 100:110, :3] = rgba[1000:1010, :3]
+    pals[-1, K - 5:, :3] = rgba[1000:1005, :3]  # same colours again at higher indices
+    costs, used = m.computeQuantizationErrorPopulation(pals.reshape(P, -1), 2.0, return_used=True)
     nt = _threads()
-    for p in range(2):
+    for p in range(P):
         ref, parts = c_oracle.eval_palette(rgba, lab, pals[p], filt, w, nthreads=nt, return_parts=True)
         assert abs(costs[p] - ref) <= 1e-5 * abs(ref), (p, costs[p], ref)
         np.testing.assert_array_equal(used[p], parts["used"])
@@ -442,11 +444,47 @@ def test_wide_palette_vs_oracle(gpu, filt, K):
         m.getIndices(0)  # u8 indices only exist for K <= 256
     lib = hq.load()  # kernel timing on: the wide path records no grid events, and must not fail
     lib.hq_profile_enable(m.ctx, 1)
-    c2 = m.computeQuantizationErrorPopulation(pals.reshape(2, -1), 2.0)
-    c3 = m.computeQuantizationErrorPopulation(pals.reshape(2, -1), 2.0)
+    c2 = m.computeQuantizationErrorPopulation(pals.reshape(P, -1), 2.0)
+    c3 = m.computeQuantizationErrorPopulation(pals.reshape(P, -1), 2.0)
     lib.hq_profile_enable(m.ctx, 0)
     np.testing.assert_array_equal(c2, costs)
     np.testing.assert_array_equal(c3, costs)
+    m.close()
+
+
+@pytest.mark.parametrize("K", [512, 1024, 2048])
+def test_chunked_palettes_match_exhaustive(gpu, filt, K):
+    """The chunked K > 256 path (grid per 256-colour chunk, winners combined by
+    the reference distance, hq_assign.hip) against the exhaustive one (option
+    chunked 0, hq_wide.hip) on a 512 x 384 image: indices bit for bit, used
+    flags equal, costs within 1e-6 relative -- with the ties a chunk boundary
+    can split: colours of chunk 0 repeated at the same position of every other
+    chunk, a colour one ulp from one in another chunk, pixels equal to palette
+    colours, and near-black / near-white colours."""
+    w, h = 512, 384
+    R, G, B = o.synthetic_image(w, h, seed=K + 7)
+    rgba = o.inline_rgba(R, G, B)
+    pal = o.synthetic_palette(K, 4242).copy()
+    for c in range(1, K // 256):
+        pal[256 * c + 5] = pal[5]                     # exact duplicates across chunks
+        pal[256 * c + 9, :3] = np.nextafter(pal[9, :3], np.float32(2))
+    pal[K - 20:K - 10, :3] = rgba[5000:5010, :3]      # pixel colours in the last chunk
+    pal[30:40, :3] = rgba[5000:5010, :3]              # ... and in chunk 0 (ties: chunk 0 wins)
+    pal[K - 3, :3] = 0.0
+    pal[K - 2, :3] = 1.0
+    pals = np.stack([pal, o.synthetic_palette(K, 77)])
+    m = hq.ImageManipulation(device=gpu)
+    hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
+    m.setImage(rgba.reshape(-1), None, w, filt.illum)
+    res = {}
+    for chunked in (1, 0):
+        m.setOption("chunked", chunked)
+        costs, used = m.computeQuantizationErrorPopulation(pals.reshape(2, -1), 2.0, return_used=True)
+        res[chunked] = (costs, used, [m.getIndices32(p) for p in range(2)])
+    for p in range(2):
+        np.testing.assert_array_equal(res[1][2][p], res[0][2][p])
+        np.testing.assert_array_equal(res[1][1][p], res[0][1][p])
+    np.testing.assert_allclose(res[1][0], res[0][0], rtol=1e-6)
     m.close()
 
 
@@ -503,17 +541,23 @@ def test_used_flags_from_sparse_pixels(gpu, filt, P):
         assert 50 < ref_used.sum() < 200
 
 
-def test_nonfinite_palette_falls_back_exactly(ip):
+@pytest.mark.parametrize("K", [16, 600])
+def test_nonfinite_palette_falls_back_exactly(ip, K):
+    """Non-finite colours: the reference loop verbatim (K <= 256), or the
+    exhaustive K > 256 path instead of the chunked one (a NaN colour 0 of a
+    later chunk would stop that chunk's own loop, CL:186, not the reference's)."""
     w = h = 32
     px = np.zeros((w * h, 4), np.float32)
     px[:, :3] = np.random.default_rng(3).random((w * h, 3), dtype=np.float32)
-    pal = o.synthetic_palette(16, 5)
+    pal = o.synthetic_palette(K, 5)
     pal[3, 1] = np.nan
     pal[7, 0] = np.inf
+    if K > 256:
+        pal[256, 2] = np.nan  # colour 0 of chunk 1
     ip.setImage(px.reshape(-1), np.zeros_like(px).reshape(-1), w, ip.illum)
     ip.computeQuantizationErrorPopulation([pal.reshape(-1)], 2.0)
     ref_idx, _ = c_oracle.assign(px, pal)
-    np.testing.assert_array_equal(ip.getIndices(0), ref_idx.astype(np.uint8))
+    np.testing.assert_array_equal(ip.getIndices32(0), ref_idx.astype(np.uint32))
 
 
 # ---------------------------------------------------------------------------
@@ -621,14 +665,16 @@ def test_search_matches_host_driver_on_oracle_costs(ip, filt):
     np.testing.assert_array_equal(best, hbest)
 
 
-@pytest.mark.parametrize("P", [1, 3, 4])
-def test_device_search_matches_host_driven(gpu, filt, P):
+@pytest.mark.parametrize("P,K", [(1, 16), (3, 16), (4, 16), (2, 600), (3, 1500)])
+def test_device_search_matches_host_driven(gpu, filt, P, K):
     """The device-resident SWASA loop (sa_step_kernel: acceptance, convergence,
     java.util.Random draws by jump table, neighbour generation) follows the
     host-driven driver's trajectory exactly on the same GPU costs, across
-    resumed run() calls and up to imax."""
+    resumed run() calls and up to imax.  K = 600 and 1500: chunked palettes
+    (one workgroup per chunk keeps, draws and preps its colours; the padding
+    of the last chunks is candidate colour 0, drawn again)."""
     import ctypes as C
-    w, h, K = 96, 64, 16
+    w, h = 96, 64
     R, G, B = o.synthetic_image(w, h, seed=9)
     m = hq.ImageManipulation(device=gpu)
     hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
@@ -1084,22 +1130,19 @@ def test_pixel_errors_vs_oracle(gpu, case, variant):
         # ulp of f (1.2e-7 near 1) into 6e-5 of dE, so two fp32 orders of the same
         # sums cannot agree to 2e-5: the oracle alone is up to ~1e-4 (mean ~1.3e-5)
         # from the float64 value.  Both fp32 paths are therefore measured against
-        # the float64 evaluation of the same inputs.  The fast path's vertical
-        # products are split f16 (hi*hi + hi*lo + lo*hi of 11 + 11 mantissa bits,
-        # the dropped lo*lo ~2^-22 relative) and its cube root exp2(log2 t / 3)
-        # is ~3 ulp, so its per-pixel error runs ~4x the oracle's (first GPU run:
-        # max 2.3e-4, mean 5.1e-5 against 6.2e-5 / 1.3e-5 on case_64x48_k16); the
-        # bound is 6x the oracle's worst pixel and 6x its mean, and every pixel
-        # within 5e-4 of the oracle's (4e-6 of the largest dE here; the summed
-        # cost's bar is 1e-4 relative).
+        # the float64 evaluation of the same inputs: the GPU's per-pixel error may
+        # be at most 2x the oracle's worst pixel and 1.5x its mean (measured: at
+        # most 1.56x and 1.23x over these cases; 4x before the cube root moved to
+        # unscaled t, hq_device.h lab_f_fast), and every pixel within 2e-4 of
+        # the oracle's.
         ex = exact_pixel_err(parts["idx"], pal, lab, f, w, h)
         e_gpu, e_orc = np.abs(err - ex), np.abs(parts["err"] - ex)
         stats = (f"{case} K={K} variant {variant}: |gpu-exact| max {e_gpu.max():.3g} mean {e_gpu.mean():.3g}; "
                  f"|oracle-exact| max {e_orc.max():.3g} mean {e_orc.mean():.3g}")
         print(stats)
-        np.testing.assert_allclose(err, parts["err"], rtol=0, atol=5e-4, err_msg=stats)
-        assert e_gpu.max() <= 6 * e_orc.max(), stats
-        assert e_gpu.mean() <= 6 * e_orc.mean(), stats
+        np.testing.assert_allclose(err, parts["err"], rtol=0, atol=2e-4, err_msg=stats)
+        assert e_gpu.max() <= 2 * e_orc.max(), stats
+        assert e_gpu.mean() <= 1.5 * e_orc.mean(), stats
         dark_lin += int(np.count_nonzero(parts["idx"] >= K // 2)) if not case.startswith("case_") else 0
     if not case.startswith("case_"):
         assert dark_lin > 1000  # the near-black colours were chosen (linear-segment Lab)
