@@ -283,7 +283,7 @@ def main():
         elapsed = hqd.max_over_ranks(dist, elapsed)
 
     prof = {}
-    for k in ("grid", "assign", "cost", "finalize"):
+    for k in ("sa_step", "grid", "assign", "cost", "finalize"):
         ms = C.c_double()
         n = C.c_int64()
         lib.hq_profile_get(m.ctx, k.encode(), C.byref(ms), C.byref(n))

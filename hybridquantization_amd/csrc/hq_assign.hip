@@ -274,6 +274,21 @@ __device__ __forceinline__ int64_t quad_cell(float r, float g, float b, int G2) 
 // packed bytes of an 8-bit image (one dword, one register).
 template <bool U8> struct RawPx { float r, g, b; };
 template <> struct RawPx<true> { uint32_t v; };
+__device__ __forceinline__ uint32_t raw_of(const RawPx<false>&) { return 0u; }
+__device__ __forceinline__ uint32_t raw_of(const RawPx<true>& x) { return x.v; }
+
+// Level-2 cell of a packed 8-bit pixel (G2 = 2^lg, lg <= 6): quad_cell's
+// min((int)(RN(k/255) G2), G2 - 1) per channel is k >> (8 - lg) for every
+// byte k.  Proof: the rounding of k/255 moves k G2/255 by at most 2^-19 while
+// a non-integer k G2/255 lies at least 1/255 from an integer (255 is odd,
+// G2 a power of two: only k = 0, 255 give integers, and 255 G2/255 = G2 is
+// clamped to G2 - 1); floor(k G2/255) = floor(k G2/256) unless some integer j
+// has 255 j <= k G2 < 256 j, which needs (-255 j) mod G2 = j < j for j < G2.
+__device__ __forceinline__ uint32_t cell_u8(uint32_t v, int lg) {
+    const int sh = 8 - lg;
+    const uint32_t m = (1u << lg) - 1u;
+    return ((((v >> sh) & m) << lg | ((v >> (8 + sh)) & m)) << lg) | ((v >> (16 + sh)) & m);
+}
 
 
 // Chunked palettes (256 < K <= 4096; AssignArgs::nch > 1): a palette of K colours
@@ -312,6 +327,9 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
     const int p0 = 4 * grp;
     const uint8_t* lines = a.lvl2 + (int64_t)grp * a.lvl2_gstride;
     const int G2 = a.G2 > 0 ? a.G2 : 4;
+#ifdef HQ_CELL_INT
+    const int lg_g2 = 31 - __builtin_clz(G2);  // (a power of two, hq_set_option "grid")
+#endif
     // pixel sequence of this thread: a grid stride.  Positions and byte offsets
     // are 32-bit (the host keeps a shard's extended rows below 2^30 pixels), so
     // loads and stores take the scalar-base form.
@@ -357,7 +375,7 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
             b = x.b;
         }
     };
-    auto lookup = [&](uint32_t q, float r, float g, float b, bool& inside, L2E (&e)[NG]) {
+    auto lookup = [&](uint32_t q, float r, float g, float b, bool& inside, L2E (&e)[NG], uint32_t raw) {
         // (q past the image: the clamped last pixel, resolved but not stored)
         inside = U8 ? true : r >= 0.f && r <= 1.f && g >= 0.f && g <= 1.f && b >= 0.f && b <= 1.f;
 #ifdef HQ_ABL_HASHLOOKUP  // timing ablation (wrong results): a random line, independent of the RGB
@@ -365,7 +383,12 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
 #elif defined(HQ_ABL_COHERENT)  // timing ablation (wrong results): runs of 256 consecutive pixels share a cell
         const uint8_t* lb = lines + (((q >> 8) * 40503u) & (uint32_t)(G2 * G2 * G2 - 1)) * (uint32_t)kL2Line;
 #else
+#ifdef HQ_CELL_INT
+        const uint8_t* lb = lines + (U8 ? cell_u8(raw, lg_g2) : inside ? (uint32_t)quad_cell(r, g, b, G2) : 0u) *
+                                        (uint32_t)kL2Line;
+#else
         const uint8_t* lb = lines + (inside ? (uint32_t)quad_cell(r, g, b, G2) : 0u) * (uint32_t)kL2Line;
+#endif
 #endif
         // selected by the `listed` flag at use.  8-B entries: two palettes per
         // 16-B load (the L1 access count per pixel, not the bytes, is the cost)
@@ -419,7 +442,7 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
         load_rgb(qpos(j), x0, pdv[j]);
         unpack(x0, xr[j], xg[j], xb[j]);
         qq[j] = qpos(j);
-        lookup(qq[j], xr[j], xg[j], xb[j], in_[j], E[j]);
+        lookup(qq[j], xr[j], xg[j], xb[j], in_[j], E[j], raw_of(x0));
     }
 #if HQ_ASSIGN_DEPTH == 2
     load_rgb(qpos(2), rb[2], pdl[2]);
@@ -518,7 +541,7 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
         qq[ia] = qpos(i + 2);
         unpack(rb[ia], xr[ia], xg[ia], xb[ia]);  // RGB(i+2): landed
         pdv[ia] = pdl[ia];
-        lookup(qq[ia], xr[ia], xg[ia], xb[ia], in_[ia], E[ia]);
+        lookup(qq[ia], xr[ia], xg[ia], xb[ia], in_[ia], E[ia], raw_of(rb[ia]));
         load_rgb(qpos(i + 4), rb[fi], pdl[fi]);  // rb[fi] held RGB(i+1), unpacked a step ago
         resolve(h);
     };
@@ -536,7 +559,7 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
         qq[n] = qpos(i + 1);
         unpack(rb[n], xr[n], xg[n], xb[n]);  // RGB(i+1): landed, needed now anyway
         pdv[n] = pdl[n];
-        lookup(qq[n], xr[n], xg[n], xb[n], in_[n], E[n]);
+        lookup(qq[n], xr[n], xg[n], xb[n], in_[n], E[n], raw_of(rb[n]));
         load_rgb(qpos(i + 3), rb[n], pdl[n]);
         resolve(h);
     };

@@ -499,7 +499,7 @@ __global__ __launch_bounds__(256, 6) void cost_mfma_kernel(CostArgs a, int P_) {
     if ((tid & 63) == 63) s_red[tid >> 6] = sum;
     __syncthreads();
     if (tid == 0)
-        a.partial[(int64_t)cur.p * a.ntiles + cur.tile] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+        acc_add(a.acc, P_, cur.p, cur.tile, (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]));
 }
 
 // ----------------------------------------------------------------------------
@@ -604,8 +604,14 @@ __device__ __forceinline__ void hpass_wide(const f32x4* src, int j, TapsPtr<HB> 
             const float k = taps->h[f][t];
             const f32x2 kk = {k, k};
 #pragma unroll
-            for (int xo = 0; xo < HR; ++xo)
+            for (int xo = 0; xo < HR; ++xo) {
+#ifdef HQ_HPASS_SCALAR  // experiment: two v_fma_f32 per row pair instead of one v_pk_fma_f32
+                acc[xo].x = __builtin_fmaf(in[xo + t - 2 * q0].x, k, acc[xo].x);
+                acc[xo].y = __builtin_fmaf(in[xo + t - 2 * q0].y, k, acc[xo].y);
+#else
                 acc[xo] = __builtin_elementwise_fma(in[xo + t - 2 * q0], kk, acc[xo]);
+#endif
+            }
         }
     }
 }
@@ -927,7 +933,7 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
     if (tid == 0) {
         double t = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
         if constexpr (NW == 8) t += (s_red[4] + s_red[5]) + (s_red[6] + s_red[7]);
-        a.partial[(int64_t)cur.p * a.ntiles + cur.tile] = t;
+        acc_add(a.acc, P_, cur.p, cur.tile, t);
     }
 }
 
@@ -987,7 +993,7 @@ __global__ __launch_bounds__(256) void gen_vpass_kernel(GenArgs a) {
     e = wave_sum(e);
     if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = e;
     __syncthreads();
-    if (threadIdx.x == 0) a.partial[blockIdx.x] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+    if (threadIdx.x == 0) acc_add(a.acc, a.P, a.p, blockIdx.x, (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]));
 }
 
 // ----------------------------------------------------------------------------

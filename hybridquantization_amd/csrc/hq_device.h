@@ -217,6 +217,45 @@ __device__ __forceinline__ float u8_unit(uint32_t v, int j) {
 }
 
 // ----------------------------------------------------------------------------
+// The dE sum of a palette (IM:736-768) as a fixed-point integer sum: each
+// workgroup's fp64 partial x (a tile, or 256 pixels of the generic path) adds
+// v = RN(x 2^20) to kAccSlots slot counters of 64 bits (slot = its tile mod
+// kAccSlots, which spreads the atomics), split as v mod 2^32 into `lo` and
+// v >> 32 into `hi` so neither can overflow (2^32 partials of < 2^43).
+// Integer addition is associative: the total is the same bits whatever order
+// the workgroups finish in, so no partial array and no ordered fold are needed
+// (round 3 stored [P][tiles] partials and summed them in a fixed order in
+// finalize or the SA step).  Resolution 2^-20 per partial: < 1e-10 relative at
+// 4096^2.  A partial that is not a finite number in [0, 2^43) (a NaN pixel,
+// an absurd palette) counts in `bad` and makes the sum NaN.
+// Layout: [kAccSlots][P][4] u64: lo, hi, bad, (pad).
+// ----------------------------------------------------------------------------
+constexpr double kAccScale = 1048576.0;  // 2^20
+__device__ __forceinline__ void acc_add(uint64_t* acc, int P, int p, int slot, double x) {
+    uint64_t* a = acc + ((int64_t)(slot & (kAccSlots - 1)) * P + p) * 4;
+    if (x >= 0.0 && x < 8796093022208.0) {  // 2^43 (NaN fails the test)
+        const uint64_t v = (uint64_t)__double2ull_rn(x * kAccScale);
+        atomicAdd((unsigned long long*)(a + 0), (unsigned long long)(v & 0xffffffffull));
+        if (v >> 32) atomicAdd((unsigned long long*)(a + 1), (unsigned long long)(v >> 32));
+    } else {
+        atomicAdd((unsigned long long*)(a + 2), 1ull);
+    }
+}
+// The total of palette p (any thread; kAccSlots x 3 loads, issued together).
+__device__ __forceinline__ double acc_total(const uint64_t* acc, int P, int p) {
+    uint64_t lo = 0, hi = 0, bad = 0;
+#pragma unroll
+    for (int sl = 0; sl < kAccSlots; ++sl) {
+        const uint64_t* a = acc + ((int64_t)sl * P + p) * 4;
+        lo += a[0];
+        hi += a[1];
+        bad += a[2];
+    }
+    // hi 2^12 and lo 2^-20 are exact doubles (hi < 2^41, lo < 2^53): one rounding
+    return bad ? __builtin_nan("") : (double)hi * 4096.0 + (double)lo * (1.0 / kAccScale);
+}
+
+// ----------------------------------------------------------------------------
 // XCD-aware relabelling of a 1-D grid of N workgroups.  Workgroups are placed
 // round-robin over the 8 XCDs (b % 8), so XCD x is given the contiguous work
 // range starting at x*(N/8) + min(x, N%8): neighbouring work items (the P

@@ -72,7 +72,11 @@ constexpr int kSaMaxP = 64;        // device-resident SWASA: largest population
 constexpr int kUsedSlots = 8;
 // words per used-bit copy: P palettes x 8 words, rounded up to 64 words (256 B)
 inline int used_stride(int P) { return (P * 8 + 63) / 64 * 64; }
-constexpr int kFoldMaxP = 8;      // largest population whose accept step folds the finalize
+// fixed-point dE sums (hq_device.h acc_add): slot counters per palette, and two
+// sets used alternately by consecutive evaluations (a set is zeroed by the
+// kernel before the evaluation's cost kernel, while the previous set is read)
+constexpr int kAccSlots = 16;
+inline size_t acc_words(int P) { return (size_t)kAccSlots * P * 4; }
 
 // sa_step_kernel: one accept + generate step of the device-resident SWASA search.
 struct SaArgs {
@@ -85,18 +89,18 @@ struct SaArgs {
     double* err_out;
     const uint64_t* seed_in;  // java.util.Random state
     uint64_t* seed_out;
-    double* best_err;       // [1]
+    const double* best_err_in;  // best error so far (ping-ponged like the state: the
+    double* best_err_out;       // writer updates it while other workgroups read it)
     float* best_colors;     // [4K]
     const uint64_t* jump_A; // LCG jumps: n steps = A_n s + C_n mod 2^48, n = 0 .. 3K*P
     const uint64_t* jump_C;
     PaletteArgs prep;       // outputs of the palette prep of the next candidates
-    // fold (no communicator, P <= kFoldMaxP): the accept step reduces the cost
-    // kernel's partials and the used bits itself (finalize's order), so no
-    // finalize launch sits between the cost kernel and this step
-    const double* partial;  // [P][ntiles]
-    const uint32_t* used_glob;  // [kUsedSlots][used_stride]: [P][8] per slot
+    // fold (no communicator): the accept step reads the fixed-point sums and the
+    // used bits itself, so no finalize launch sits between the cost kernel and
+    // this step
+    const uint64_t* acc;    // [kAccSlots][P][4] (acc_total)
+    const uint32_t* used_glob;  // [kUsedSlots][used_stride]: [P][8 nch] per slot
     int used_stride;
-    int ntiles;
     int fold;
     double n_total;         // pixels of the whole image
     double keep_threshold;  // SW:59-62 -(tanh(num/den))/2 + 0.5 at the accepted iteration
@@ -124,6 +128,9 @@ struct GridArgs {
     int G1;                 // level-1 resolution (G2 / 4)
     int64_t lvl1_pitch;     // bytes per palette
     int64_t lvl2_gstride;   // bytes per group of 4 palettes (G2^3 * kL2Line)
+    uint64_t* acc_zero;     // the fixed-point sums the following cost kernel adds to, zeroed here
+    int P_acc;              // their palettes (P above / nch)
+    int nch;                // sub-palettes per palette (chunked palettes), else 1
 };
 
 struct AssignArgs {
@@ -163,7 +170,7 @@ struct CostArgs {
     const float* labL;      // planar LabRef, owned rows, pitch lab_pitch
     const float* labA;
     const float* labB;
-    double* partial;        // [P][ntiles]
+    uint64_t* acc;          // fixed-point dE sums [kAccSlots][P][4] (acc_add)
     Geom g;
     int K;
     int tiles_x;
@@ -174,11 +181,11 @@ struct CostArgs {
 };
 
 struct FinalizeArgs {
-    const double* partial;  // [P][ntiles]
+    const uint64_t* acc;    // fixed-point dE sums [kAccSlots][P][4]
     const uint32_t* used_glob;  // [kUsedSlots][used_stride] used-colour bits (assign)
     int used_stride;
     double* out;            // [P][1+K]
-    int ntiles;
+    int P;
     int K;
     const uint32_t* used32; // K > 4096: [P][K] used flags (assign_wide), replaces used_mask
     int wpp;                // used words per palette in used_glob (8; 8 nch for chunked palettes)
@@ -212,7 +219,8 @@ struct GenArgs {
     const float* labL;
     const float* labA;
     const float* labB;
-    double* partial;         // [nblocks]
+    uint64_t* acc;           // fixed-point dE sums [kAccSlots][P][4] (acc_add), palette p
+    int p, P;
     Geom g;
     int half;
     float m_lab[9];  // Opp->XYZ rows / illuminant (CL:124-131), opp2xyz_over_illum()

@@ -119,7 +119,10 @@ struct hq_ctx {
     // population work buffers
     int P_cap = 0, K_cur = 0;
     DevBuf d_pal_in, d_pal, d_opp, d_opp16, d_dup, d_pflags, d_lvl1, d_lvl2, d_idx, d_used_mask,
-        d_partial, d_out, d_gen_t;
+        d_acc, d_out, d_gen_t;
+    // d_acc: two sets of fixed-point dE sums [kAccSlots][P][4] u64 (acc_add), d_used_mask two
+    // sets of used bits [kUsedSlots][used_stride]; evaluation n fills set acc_par = n & 1
+    int acc_par = 0;
     DevBuf d_pixerr;           // option "pixel_err": [P][n_own] per-pixel dE of the last evaluation
     DevBuf d_idx32, d_used32;  // K > 4096 (hq_wide.hip): 32-bit index images, per-colour used flags
     DevBuf d_idx16, d_dist;    // 256 < K <= 4096 (chunked): 16-bit index images, pass distances
@@ -129,7 +132,6 @@ struct hq_ctx {
     double* h_out = nullptr;  // pinned [P][1+K]
     size_t h_pal_bytes = 0, h_out_bytes = 0;
     int last_P = 0;
-    int last_nparts = 0;  // cost partials per palette of the last evaluation
 
     // options
     int G2 = 32;           // argmin grid resolution (0 = exhaustive)
@@ -158,7 +160,7 @@ struct hq_ctx {
 
     // profiling
     bool prof = false;
-    ProfSlot prof_assign, prof_cost, prof_grid, prof_finalize;
+    ProfSlot prof_assign, prof_cost, prof_grid, prof_finalize, prof_sa;
     hipEvent_t ev[8] = {};  // profiling: start/stop of grid, assign, cost, finalize
     int num_cu = 256;
 };
@@ -178,7 +180,7 @@ struct hq_search {
     bool fold = false;                   // accept steps reduce the partials (no finalize launch)
     float t_acc = 0.f;                   // temperature / threshold of the iteration
     double keep_acc = 0.0;               // whose population awaits acceptance
-    DevBuf colors[2], cand[2], err[2], seed[2], best_err, best_colors, jA, jC;
+    DevBuf colors[2], cand[2], err[2], seed[2], best_err[2], best_colors, jA, jC;
     std::vector<hipEvent_t> pev;         // profiling: 8 events per iteration of a run
 };
 
@@ -396,11 +398,7 @@ int ensure_population(hq_ctx* c, int P, int K) {
     const int G1 = G2 / 4;
     const int64_t l1p = round_up((int64_t)G1 * G1 * G1 * 32, 256);
     const int64_t l2g = round_up((int64_t)G2 * G2 * G2 * kL2Line, 256);  // per group of 4 palettes
-    int tiles_x, ntiles;
-    fast_tile_dims(g.W, g.r1 - g.r0, 8, 128, &tiles_x, &ntiles);  // the most tiles of any config
     const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
-    const int64_t gen_blocks = (n_own + 255) / 256;
-    const int64_t nparts = std::max<int64_t>(ntiles, gen_blocks);
     HIP_TRY(c, c->d_pal_in.ensure(sizeof(float4) * (size_t)P * K));
     HIP_TRY(c, c->d_pal.ensure(sizeof(float4) * (size_t)P * std::max(K, kMaxK)));
     HIP_TRY(c, c->d_opp.ensure(sizeof(float4) * (size_t)P * std::max(K, kMaxK)));
@@ -417,8 +415,8 @@ int ensure_population(hq_ctx* c, int P, int K) {
     // bytes past a region's last column (past the buffer on the last palette's
     // last row when idx_pitch has no padding)
     HIP_TRY(c, c->d_idx.ensure((size_t)P * g.idx_pitch + 256));
-    HIP_TRY(c, c->d_used_mask.ensure(sizeof(uint32_t) * kUsedSlots * (size_t)used_stride(P)));
-    HIP_TRY(c, c->d_partial.ensure(sizeof(double) * (size_t)P * nparts));
+    HIP_TRY(c, c->d_used_mask.ensure(2 * sizeof(uint32_t) * kUsedSlots * (size_t)used_stride(P)));
+    HIP_TRY(c, c->d_acc.ensure(2 * sizeof(uint64_t) * acc_words(P)));
     HIP_TRY(c, c->d_out.ensure(sizeof(double) * (size_t)P * (1 + K)));
     if (c->pixel_err) HIP_TRY(c, c->d_pixerr.ensure(sizeof(float) * (size_t)P * std::max<int64_t>(n_own, 1)));
     return ensure_pinned(c, sizeof(float) * 4 * (size_t)P * K, sizeof(double) * (size_t)P * (1 + K));
@@ -444,13 +442,22 @@ PaletteArgs prep_args(hq_ctx* c, int K) {
 // flags), all-reduced if a comm is set.  ev (8 events, or null): start/stop of
 // the grid, assign, cost and finalize launches, carried by the launches
 // themselves (set_launch_events).
+// Counter set `par` of an evaluation of P palettes (P nch sub-palettes Ps).
+uint64_t* acc_set(hq_ctx* c, int par, int P) { return c->d_acc.as<uint64_t>() + (size_t)par * acc_words(P); }
+uint32_t* used_set(hq_ctx* c, int par, int Ps) {
+    return c->d_used_mask.as<uint32_t>() + (size_t)par * kUsedSlots * used_stride(Ps);
+}
+
 GridArgs grid_args(hq_ctx* c, int P, int K) {
     const int G2 = c->G2 > 0 ? c->G2 : 4;
     const int G1 = G2 / 4;
+    // (P = sub-palettes; the counters of set c->acc_par)
+    const int nch = c->nch_cur;
     return GridArgs{c->d_pal.as<float4>(), c->d_dup.as<uint8_t>(), c->d_pflags.as<int>(),
-                    c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(), c->d_used_mask.as<uint32_t>(),
+                    c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(), used_set(c, c->acc_par, P),
                     used_stride(P), K, G1,
-                    round_up((int64_t)G1 * G1 * G1 * 32, 256), round_up((int64_t)G2 * G2 * G2 * kL2Line, 256)};
+                    round_up((int64_t)G1 * G1 * G1 * 32, 256), round_up((int64_t)G2 * G2 * G2 * kL2Line, 256),
+                    acc_set(c, c->acc_par, P / nch), P / nch, nch};
 }
 
 // The generic two-pass cost (CL:234-306 per pixel, any half-width) of P
@@ -458,12 +465,11 @@ GridArgs grid_args(hq_ctx* c, int P, int K) {
 // u16 (chunked palettes) or u32, idx_bytes) with c->g.idx_pitch elements per palette, opponent tables of
 // opp_stride entries per palette in d_opp.  The cost events time all P pairs.
 int enqueue_generic_cost(hq_ctx* c, int P, const void* idx_base, int idx_bytes, int opp_stride,
-                         const hipEvent_t* ev, int* nparts_out) {
+                         const hipEvent_t* ev) {
     const Geom& g = c->g;
     hipStream_t s = c->stream;
     HIP_TRY(c, c->d_gen_t.ensure(sizeof(float) * 7 * (size_t)g.n_ext));
     const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
-    const int nparts = (int)((n_own + 255) / 256);
     const float inv[3] = {1.0f / c->illum[0], 1.0f / c->illum[1], 1.0f / c->illum[2]};
     for (int p = 0; p < P; ++p) {
         GenArgs gn{};
@@ -477,7 +483,9 @@ int enqueue_generic_cost(hq_ctx* c, int P, const void* idx_base, int idx_bytes, 
         gn.labL = c->d_labL.as<float>();
         gn.labA = c->d_labA.as<float>();
         gn.labB = c->d_labB.as<float>();
-        gn.partial = c->d_partial.as<double>() + (int64_t)p * nparts;
+        gn.acc = acc_set(c, c->acc_par, P);
+        gn.p = p;
+        gn.P = P;
         gn.g = g;
         gn.half = c->half;
         gn.pix_err = c->pixel_err ? c->d_pixerr.as<float>() + (int64_t)p * n_own : nullptr;
@@ -488,7 +496,6 @@ int enqueue_generic_cost(hq_ctx* c, int P, const void* idx_base, int idx_bytes, 
         set_launch_events(nullptr, nullptr);
         HIP_TRY(c, e);
     }
-    *nparts_out = nparts;
     return HQ_OK;
 }
 
@@ -500,6 +507,8 @@ int enqueue_wide(hq_ctx* c, int P, int K, const hipEvent_t* ev) {
     WideArgs wa{c->d_pal_in.as<float4>(), c->d_pal.as<float4>(), c->d_opp.as<float4>(), c->d_pflags.as<int>(),
                 c->d_R.as<float>(), c->d_G.as<float>(), c->d_B.as<float>(), c->d_idx32.as<uint32_t>(),
                 c->d_used32.as<uint32_t>(), g.n_ext, g.idx_pitch, K};
+    c->acc_par ^= 1;
+    HIP_TRY(c, hipMemsetAsync(acc_set(c, c->acc_par, P), 0, sizeof(uint64_t) * acc_words(P), s));
     HIP_TRY(c, hipMemsetAsync(c->d_pflags.p, 0, sizeof(int) * (size_t)P, s));
     HIP_TRY(c, launch_prep_wide(wa, P, s));
     HIP_TRY(c, hipMemsetAsync(c->d_used32.p, 0, sizeof(uint32_t) * (size_t)P * K, s));
@@ -507,10 +516,9 @@ int enqueue_wide(hq_ctx* c, int P, int K, const hipEvent_t* ev) {
     const hipError_t e = launch_assign_wide(wa, P, s);
     set_launch_events(nullptr, nullptr);
     HIP_TRY(c, e);
-    int nparts = 0;
-    int rc = enqueue_generic_cost(c, P, c->d_idx32.p, 4, K, ev, &nparts);
+    int rc = enqueue_generic_cost(c, P, c->d_idx32.p, 4, K, ev);
     if (rc) return rc;
-    FinalizeArgs fa{c->d_partial.as<double>(), nullptr, 0, c->d_out.as<double>(), nparts, K,
+    FinalizeArgs fa{acc_set(c, c->acc_par, P), nullptr, 0, c->d_out.as<double>(), P, K,
                     c->d_used32.as<uint32_t>(), 8};
     if (ev) set_launch_events(ev[6], ev[7]);
     const hipError_t ef = launch_finalize(fa, P, s);
@@ -528,28 +536,32 @@ int enqueue_wide(hq_ctx* c, int P, int K, const hipEvent_t* ev) {
 // 256 nch): the grid and assign run on P nch sub-palettes of 256 colours (d_pal
 // etc. hold them, prep_palette made them), assign combines them into 16-bit
 // indices, the cost kernel reads those with a 256 nch-entry table.
+// Each evaluation takes the other counter set than the last one (build_grid
+// zeroes it), so an accept step can read the last set while the next is filled.
 int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = false) {
     const Geom& g = c->g;
     hipStream_t s = c->stream;
     const int nch = c->nch_cur, Ps = P * nch, Ks = nch > 1 ? kMaxK : K;
+    c->acc_par ^= 1;
     const GridArgs ga = grid_args(c, Ps, Ks);
     auto timed = [&](int slot) {
         if (ev) set_launch_events(ev[2 * slot], ev[2 * slot + 1]);
     };
     auto untimed = [&]() { set_launch_events(nullptr, nullptr); };
-    if (c->G2 > 0) {  // (build_grid also zeroes the used bits)
+    if (c->G2 > 0) {  // (build_grid also zeroes the used bits and the sums)
         timed(0);
         const hipError_t e = launch_build_grid(ga, Ps, s);
         untimed();
         HIP_TRY(c, e);
     } else {
-        HIP_TRY(c, hipMemsetAsync(c->d_used_mask.p, 0, sizeof(uint32_t) * kUsedSlots * (size_t)used_stride(Ps), s));
+        HIP_TRY(c, hipMemsetAsync(ga.used_glob, 0, sizeof(uint32_t) * kUsedSlots * (size_t)used_stride(Ps), s));
+        HIP_TRY(c, hipMemsetAsync(ga.acc_zero, 0, sizeof(uint64_t) * acc_words(P), s));
     }
     const int nblocks = assign_blocks(c, Ps);
     AssignArgs aa{c->d_R.as<float>(), c->d_G.as<float>(), c->d_B.as<float>(),
                   c->img_u8 && c->img_u8_path ? c->d_rgbx.as<uint32_t>() : nullptr, c->d_pal.as<float4>(),
                   c->d_pflags.as<int>(), c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(),
-                  c->d_idx.as<uint8_t>(), c->d_used_mask.as<uint32_t>(), used_stride(Ps), g.n_ext, g.idx_pitch,
+                  c->d_idx.as<uint8_t>(), ga.used_glob, used_stride(Ps), g.n_ext, g.idx_pitch,
                   ga.lvl1_pitch, ga.lvl2_gstride, Ks, c->G2, nblocks};
     if (nch > 1) {
         aa.idx16 = c->d_idx16.as<uint16_t>();
@@ -562,7 +574,6 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
     untimed();
     HIP_TRY(c, e);
     const float inv[3] = {1.0f / c->illum[0], 1.0f / c->illum[1], 1.0f / c->illum[2]};
-    int nparts;
     // chunked palettes: the 16 x 128 tiles at HB = 10 (else the generic path)
     const bool fast = c->cost_variant != 1 && c->fast_hb > 0 && !c->pal_generic &&
                       (nch == 1 || (c->fast_hb == 10 && c->cost_rows == 16 && c->cost_tw == 128));
@@ -578,7 +589,7 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
         ca.labL = c->d_labL.as<float>();
         ca.labA = c->d_labA.as<float>();
         ca.labB = c->d_labB.as<float>();
-        ca.partial = c->d_partial.as<double>();
+        ca.acc = ga.acc_zero;
         ca.g = g;
         ca.K = K;
         fast_tile_dims(g.W, g.r1 - g.r0, rows, tw, &ca.tiles_x, &ca.ntiles);
@@ -590,16 +601,13 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
                     : launch_cost_fast(ca, P, c->de_type, c->trim && c->trim_ok, rows, tw, c->fast_hb, s);
         untimed();
         HIP_TRY(c, e);
-        nparts = ca.ntiles;
     } else {
-        int rc = nch > 1 ? enqueue_generic_cost(c, P, c->d_idx16.p, 2, nch * kMaxK, ev, &nparts)
-                         : enqueue_generic_cost(c, P, c->d_idx.p, 1, kMaxK, ev, &nparts);
+        int rc = nch > 1 ? enqueue_generic_cost(c, P, c->d_idx16.p, 2, nch * kMaxK, ev)
+                         : enqueue_generic_cost(c, P, c->d_idx.p, 1, kMaxK, ev);
         if (rc) return rc;
     }
-    c->last_nparts = nparts;
-    if (!fold) {  // (a folding search's accept step reduces the partials itself)
-        FinalizeArgs fa{c->d_partial.as<double>(), c->d_used_mask.as<uint32_t>(), used_stride(Ps),
-                        c->d_out.as<double>(), nparts, K, nullptr, 8 * nch};
+    if (!fold) {  // (a folding search's accept step reads the sums itself)
+        FinalizeArgs fa{ga.acc_zero, ga.used_glob, used_stride(Ps), c->d_out.as<double>(), P, K, nullptr, 8 * nch};
         timed(3);
         const hipError_t ef = launch_finalize(fa, P, s);
         untimed();
@@ -621,6 +629,11 @@ void prof_accumulate(hq_ctx* c, const hipEvent_t* ev, bool finalize = true, bool
     prof_add(c, c->prof_assign, ev[2], ev[3]);
     prof_add(c, c->prof_cost, ev[4], ev[5]);
     if (finalize) prof_add(c, c->prof_finalize, ev[6], ev[7]);
+}
+
+// ... and the SA step that generated it (device-resident search: events 8, 9).
+void prof_accumulate_sa(hq_ctx* c, const hipEvent_t* ev) {
+    prof_add(c, c->prof_sa, ev[8], ev[9]);
 }
 
 // Host-driven evaluation of the P palettes in h_pal: upload, prep, enqueue_core,
@@ -719,9 +732,10 @@ struct NchScope {
     ~NchScope() { c->nch_cur = 1; }
 };
 
-// One sa_step launch: accept the population in cand[cd] (if `accept`), then
-// generate the next candidates into cand[1 - cd] (if `generate`).
-int enqueue_sa_step(hq_search* s, bool accept, bool init, bool generate, bool random, float amax) {
+// The arguments of an SA step: accept the population in cand[cd] (if `accept`,
+// its counters in set c->acc_par), then generate the next candidates into
+// cand[1 - cd] (if `generate`).
+SaArgs sa_args(hq_search* s, bool accept, bool init, bool generate, bool random, float amax) {
     hq_ctx* c = s->ctx;
     SaArgs a{};
     a.out = c->d_out.as<double>();
@@ -733,7 +747,8 @@ int enqueue_sa_step(hq_search* s, bool accept, bool init, bool generate, bool ra
     a.err_out = s->err[1 - s->st].as<double>();
     a.seed_in = s->seed[s->st].as<uint64_t>();
     a.seed_out = s->seed[1 - s->st].as<uint64_t>();
-    a.best_err = s->best_err.as<double>();
+    a.best_err_in = s->best_err[s->st].as<double>();
+    a.best_err_out = s->best_err[1 - s->st].as<double>();
     a.best_colors = s->best_colors.as<float>();
     a.jump_A = s->jA.as<uint64_t>();
     a.jump_C = s->jC.as<uint64_t>();
@@ -751,14 +766,28 @@ int enqueue_sa_step(hq_search* s, bool accept, bool init, bool generate, bool ra
     a.generate = generate;
     a.random = random;
     a.convergence = s->prm.convergence;
-    a.partial = c->d_partial.as<double>();
-    a.used_glob = c->d_used_mask.as<uint32_t>();
+    a.acc = acc_set(c, c->acc_par, a.P);
+    a.used_glob = used_set(c, c->acc_par, a.P * s->nch);
     a.used_stride = used_stride(a.P * s->nch);
-    a.ntiles = c->last_nparts;
     a.fold = s->fold;
-    HIP_TRY(c, launch_sa_step(a, c->stream));
+    return a;
+}
+
+void sa_advance(hq_search* s, bool generate) {
     s->st = 1 - s->st;
     if (generate) s->cd = 1 - s->cd;
+}
+
+// One sa_step launch (sa_args).
+int enqueue_sa_step(hq_search* s, bool accept, bool init, bool generate, bool random, float amax,
+                    const hipEvent_t* ev = nullptr) {
+    hq_ctx* c = s->ctx;
+    const SaArgs a = sa_args(s, accept, init, generate, random, amax);
+    if (ev) set_launch_events(ev[0], ev[1]);
+    const hipError_t e = launch_sa_step(a, c->stream);
+    set_launch_events(nullptr, nullptr);
+    HIP_TRY(c, e);
+    sa_advance(s, generate);
     return HQ_OK;
 }
 
@@ -776,8 +805,8 @@ int device_search_create(hq_ctx* c, const hq_swasa_params* params, int K, uint64
     s->prm = *params;
     s->P = P;
     // no communicator: nothing has to see the finalized sums, so the accept
-    // step reduces the partials itself (one launch less per iteration)
-    s->fold = !c->comm && P <= kFoldMaxP;
+    // step reads the fixed-point sums itself (one launch less per iteration)
+    s->fold = !c->comm;
     s->pol = new Swasa(*params, seed);
     const NchScope scope(c, s->nch);
     int rc = ensure_population(c, P, K);
@@ -789,7 +818,7 @@ int device_search_create(hq_ctx* c, const hq_swasa_params* params, int K, uint64
         HIP_TRY(c, s->err[i].ensure(sizeof(double) * P));
         HIP_TRY(c, s->seed[i].ensure(sizeof(uint64_t)));
     }
-    HIP_TRY(c, s->best_err.ensure(sizeof(double)));
+    for (int i = 0; i < 2; ++i) HIP_TRY(c, s->best_err[i].ensure(sizeof(double)));
     HIP_TRY(c, s->best_colors.ensure(sizeof(float) * 4 * K));
     // java.util.Random jumps: n steps = A_n s + C_n (mod 2^48), n = 0 .. 3KP
     const size_t nj = (size_t)3 * K * P + 1;
@@ -808,6 +837,7 @@ int device_search_create(hq_ctx* c, const hq_swasa_params* params, int K, uint64
     const uint64_t s0 = (seed ^ mult) & mask;  // JavaRandom::set_seed
     HIP_TRY(c, hipMemcpy(s->seed[0].p, &s0, sizeof s0, hipMemcpyHostToDevice));
     HIP_TRY(c, hipMemset(s->err[0].p, 0, sizeof(double) * P));
+    for (int i = 0; i < 2; ++i) HIP_TRY(c, hipMemset(s->best_err[i].p, 0, sizeof(double)));
     s->st = s->cd = 0;
     // IM:385-493: random population (SW:40-52), its evaluation, argmin
     if ((rc = enqueue_sa_step(s, false, false, true, true, 0.f))) return rc;
@@ -833,21 +863,24 @@ int device_search_run(hq_search* s, int iterations, int* ran) {
     if (s->fold && c->comm)
         return fail(c, HQ_ERR_STATE, "communicator set after hq_search_create: recreate the search");
     const bool prof = c->prof;
-    if (prof && (rc = ensure_events(s, (size_t)8 * iterations))) return rc;
+    if (prof && (rc = ensure_events(s, (size_t)10 * iterations))) return rc;
     for (; done < iterations && s->ite < s->prm.imax; ++done) {
         const int ite = ++s->ite;
         s->pol->reduce_temperature_if_necessary(ite);                  // IM:507
         const float amax = s->pol->max_step_width(ite) / 256.0f;       // SW:91-101
-        const hipEvent_t* ev = prof ? &s->pev[(size_t)8 * done] : nullptr;
+        const hipEvent_t* ev = prof ? &s->pev[(size_t)10 * done] : nullptr;
         // accept the previous iteration's population (none at the first of a run)
-        if ((rc = enqueue_sa_step(s, done > 0, false, true, false, amax))) return rc;
+        if ((rc = enqueue_sa_step(s, done > 0, false, true, false, amax, ev ? ev + 8 : nullptr))) return rc;
         if ((rc = enqueue_core(c, s->P, s->K, ev, s->fold))) return rc;
         s->t_acc = s->pol->temperature();     // SW:54-57 at this iteration
         s->keep_acc = s->pol->keep_threshold(ite);
     }
     if (done > 0 && (rc = enqueue_sa_step(s, true, false, false, false, 0.f))) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    for (int i = 0; prof && i < done; ++i) prof_accumulate(c, &s->pev[(size_t)8 * i], !s->fold);
+    for (int i = 0; prof && i < done; ++i) {
+        prof_accumulate(c, &s->pev[(size_t)10 * i], !s->fold);
+        prof_accumulate_sa(c, &s->pev[(size_t)10 * i]);
+    }
     if (ran) *ran = done;
     return HQ_OK;
 }
@@ -915,7 +948,7 @@ void hq_destroy(hq_ctx* c) {
     for (DevBuf* b : {&c->d_k1, &c->d_k2, &c->d_k3, &c->d_absk3, &c->d_R, &c->d_G, &c->d_B, &c->d_rgbx,
                       &c->d_labL, &c->d_labA, &c->d_labB, &c->d_pal_in, &c->d_pal, &c->d_opp, &c->d_opp16,
                       &c->d_dup, &c->d_pflags, &c->d_lvl1, &c->d_lvl2, &c->d_idx,
-                      &c->d_used_mask, &c->d_partial, &c->d_out, &c->d_gen_t, &c->d_taps,
+                      &c->d_used_mask, &c->d_acc, &c->d_out, &c->d_gen_t, &c->d_taps,
                       &c->d_vfrag16, &c->d_idx32, &c->d_used32, &c->d_pixerr, &c->d_idx16, &c->d_dist})
         b->release();
     if (c->h_pal) (void)hipHostFree(c->h_pal);
@@ -1306,7 +1339,8 @@ int hq_search_best(const hq_search* s, float* colors, double* best_error, int* i
         if (rc) return rc;
         if (colors)
             HIP_TRY(c, hipMemcpy(colors, s->best_colors.p, sizeof(float) * 4 * s->K, hipMemcpyDeviceToHost));
-        if (best_error) HIP_TRY(c, hipMemcpy(best_error, s->best_err.p, sizeof(double), hipMemcpyDeviceToHost));
+        if (best_error)
+            HIP_TRY(c, hipMemcpy(best_error, s->best_err[s->st].p, sizeof(double), hipMemcpyDeviceToHost));
         if (iteration) *iteration = s->ite;
         return HQ_OK;
     }
@@ -1324,7 +1358,7 @@ void hq_search_destroy(hq_search* s) {
     }
     for (hipEvent_t e : s->pev) (void)hipEventDestroy(e);
     for (DevBuf* b : {&s->colors[0], &s->colors[1], &s->cand[0], &s->cand[1], &s->err[0], &s->err[1],
-                      &s->seed[0], &s->seed[1], &s->best_err, &s->best_colors, &s->jA,
+                      &s->seed[0], &s->seed[1], &s->best_err[0], &s->best_err[1], &s->best_colors, &s->jA,
                       &s->jC})
         b->release();
     delete s->pol;
@@ -1340,7 +1374,7 @@ int hq_profile_enable(hq_ctx* c, int on) {
 
 int hq_profile_reset(hq_ctx* c) {
     if (!c) return HQ_ERR_ARG;
-    c->prof_assign = c->prof_cost = c->prof_grid = c->prof_finalize = ProfSlot{};
+    c->prof_assign = c->prof_cost = c->prof_grid = c->prof_finalize = c->prof_sa = ProfSlot{};
     return HQ_OK;
 }
 
@@ -1351,6 +1385,7 @@ int hq_profile_get(hq_ctx* c, const char* kernel, double* total_ms, int64_t* lau
     else if (!std::strcmp(kernel, "cost")) s = &c->prof_cost;
     else if (!std::strcmp(kernel, "grid")) s = &c->prof_grid;
     else if (!std::strcmp(kernel, "finalize")) s = &c->prof_finalize;
+    else if (!std::strcmp(kernel, "sa_step")) s = &c->prof_sa;
     else return fail(c, HQ_ERR_ARG, "unknown kernel '%s'", kernel);
     if (total_ms) *total_ms = s->ms;
     if (launches) *launches = s->launches;

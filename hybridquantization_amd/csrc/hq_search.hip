@@ -32,15 +32,27 @@ __device__ __forceinline__ uint32_t dup_hash(float4 c) {
     return (h ^ (h >> 15)) & (kDupSlots - 1);
 }
 
-__device__ __forceinline__ void prep_palette_body(const PaletteArgs& a, int p, float4 c) {
+// LDS of the prep besides the colour table (the caller's: its own, or the SA
+// step's candidate table, which the colours already sit in).
+struct PrepLds {
+    uint32_t tab[kDupSlots], mn[kDupSlots];
+    float lin[3 * kMaxK];
+    int nonfinite;
+};
+
+// Returns colour k's duplicate flag; `nonfinite` = the palette has a colour
+// that is not finite.  write: store the outputs (pal, opp, opp16, dup, pflags)
+// of palette p (sa_grid_kernel: one workgroup per palette stores, the others
+// only use the flags).
+__device__ __forceinline__ bool prep_palette_body(const PaletteArgs& a, int p, float4 c, float4* s, PrepLds& L,
+                                                  bool write, bool& nonfinite) {
     // threads 0..K-1 handle colour k = tid; any block size >= K.
     const int tid = threadIdx.x, k = tid;
-    __shared__ float4 s[kMaxK];
-    __shared__ uint32_t s_tab[kDupSlots], s_min[kDupSlots];
-    __shared__ int s_nonfinite;
-    __shared__ float s_lin[3 * kMaxK];
+    uint32_t* s_tab = L.tab;
+    uint32_t* s_min = L.mn;
+    float* s_lin = L.lin;
     for (int i = tid; i < kDupSlots; i += blockDim.x) { s_tab[i] = ~0u; s_min[i] = ~0u; }
-    if (tid == 0) s_nonfinite = 0;
+    if (tid == 0) L.nonfinite = 0;
     const bool own = k < a.K;
     if (own) c.w = 0.f;  // SW:49: palettes carry .w = 0
     else c = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -55,7 +67,7 @@ __device__ __forceinline__ void prep_palette_body(const PaletteArgs& a, int p, f
     }
     uint32_t slot = 0;
     if (own) {
-        if (!(isfinite(c.x) && isfinite(c.y) && isfinite(c.z))) atomicOr(&s_nonfinite, 1);
+        if (!(isfinite(c.x) && isfinite(c.y) && isfinite(c.z))) atomicOr(&L.nonfinite, 1);
         slot = dup_hash(c);
         for (;;) {
             const uint32_t r = atomicCAS(&s_tab[slot], ~0u, (uint32_t)k);
@@ -67,7 +79,9 @@ __device__ __forceinline__ void prep_palette_body(const PaletteArgs& a, int p, f
         atomicMin(&s_min[slot], (uint32_t)k);
     }
     __syncthreads();
-    if (own) {
+    const bool dup = own && s_min[slot] < (uint32_t)k;
+    nonfinite = L.nonfinite != 0;
+    if (own && write) {
         const float lr = s_lin[3 * k], lg = s_lin[3 * k + 1], lb = s_lin[3 * k + 2];
         const float4 opp = make_float4(dot3(lr, lg, lb, c_RGB2Opp + 0),
                                        dot3(lr, lg, lb, c_RGB2Opp + 3),
@@ -75,15 +89,19 @@ __device__ __forceinline__ void prep_palette_body(const PaletteArgs& a, int p, f
         a.pal[(int64_t)p * kMaxK + k] = c;
         a.opp[(int64_t)p * kMaxK + k] = opp;
         a.opp16[(int64_t)p * kMaxK + k] = make_uint4(split_f16(opp.x), split_f16(opp.y), split_f16(opp.z), 0u);
-        a.dup[(int64_t)p * kMaxK + k] = s_min[slot] < (uint32_t)k ? 1u : 0u;
+        a.dup[(int64_t)p * kMaxK + k] = dup ? 1u : 0u;
     }
-    if (tid == 0) a.pflags[p] = s_nonfinite;
+    if (tid == 0 && write) a.pflags[p] = nonfinite;
+    return dup;
 }
 
 __global__ __launch_bounds__(1024) void prep_palette_kernel(PaletteArgs a) {
     const int p = blockIdx.x, k = threadIdx.x;
+    __shared__ float4 s[kMaxK];
+    __shared__ PrepLds L;
     const float4 c = k < a.K ? a.pal_in[(int64_t)p * a.K + k] : make_float4(0.f, 0.f, 0.f, 0.f);
-    prep_palette_body(a, p, c);
+    bool nf;
+    (void)prep_palette_body(a, p, c, s, L, true, nf);
 }
 
 // ----------------------------------------------------------------------------
@@ -118,43 +136,12 @@ __device__ __forceinline__ uint64_t lcg_jump(uint64_t s, uint64_t A, uint64_t C)
     return (A * s + C) & kLcgMask;
 }
 
-// Fixed-order sums of the cost kernel's per-tile partials by a 1024-thread
-// block (IM:736-768's fp64 sum, in an order of our own that never changes):
-// thread t adds partials t, t + 1024, t + 2048, ... of palette p in that order
-// into acc[p]; the caller then folds the lanes with wave_sum_to_lane63 and the
-// 16 wave sums in ascending order.  finalize_kernel and sa_step's fold both
-// use it, so a search that folds the finalize into its accept step gets the
-// host-driven evaluation's sums bit for bit.  NL loads per palette in flight.
-template <int MAXP, int NL>
-__device__ __forceinline__ void thread_partial_sums(const double* part, int ntiles, int P,
-                                                    double (&acc)[MAXP]) {
-    constexpr int NT = 1024;
-    const int tid = threadIdx.x;
-#pragma unroll
-    for (int p = 0; p < MAXP; ++p) acc[p] = 0.0;
-    for (int t0 = 0; t0 < ntiles; t0 += NT * NL) {
-        double v[MAXP][NL];
-#pragma unroll
-        for (int p = 0; p < MAXP; ++p)
-#pragma unroll
-            for (int u = 0; u < NL; ++u) {
-                const int t = t0 + u * NT + tid;
-                v[p][u] = p < P && t < ntiles ? part[(int64_t)p * ntiles + t] : 0.0;
-            }
-#pragma unroll
-        for (int p = 0; p < MAXP; ++p)
-#pragma unroll
-            for (int u = 0; u < NL; ++u) acc[p] += v[p][u];
-    }
-}
-
 // Block-shared SA state of one step (thread 0 runs the sequential logic).
 struct SaShared {
     int unused[kSaMaxP];
     int src[kSaMaxP];  // >= 0: member p continues from candidate src; -1: keeps its palette
     double cur[kSaMaxP], err[kSaMaxP], ex[kSaMaxP];  // ex: exp(-(err - cur) / T), lanes in parallel
     double sum[kSaMaxP], err_in[kSaMaxP];  // prefetched inputs of the sequential part
-    double fold_red[kFoldMaxP][16];  // fold: per-wave partial sums of each palette
     uint64_t seed;     // java.util.Random state (prefetched, then after the acceptance draws)
     double best_in;
     int best;          // candidate that set a new best (-1: none)
@@ -165,34 +152,51 @@ struct SaShared {
 // global input is loaded before the first barrier, in parallel, so the
 // sequential part on thread 0 works from LDS (a chain of dependent global
 // loads on one thread was most of this kernel's ~13 us).
+// MAXF: used flags per thread held in registers (the communicator path).
+template <int MAXF>
 __device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared& s) {
 #pragma clang fp contract(off)
     const int tid = threadIdx.x, nt = blockDim.x, P = a.P, K = a.K;
     const int wpp = 8 * a.nch;  // used words per palette (chunked palettes: 8 per chunk)
-    constexpr int MAXF = 16;  // used flags per thread held in registers
     const int nf = (P * K + nt - 1) / nt;
     double fv[MAXF];
-    double fold_acc[kFoldMaxP];
-    uint32_t fold_word = 0u;
-    if (a.accept && a.fold) {  // the finalize's work, folded (P <= kFoldMaxP)
-        // the small inputs are loaded first and stored to LDS after the partials'
-        // loads are out: an LDS store of a just-loaded value waits for it, and
-        // the wait (in-order counters) held back every partial load behind it
+    constexpr int MAXW = 4;  // used words per thread (wpp P <= 4 nt)
+    uint32_t fold_word[MAXW] = {0u, 0u, 0u, 0u};
+    if (a.accept && a.fold) {  // the finalize's work, folded: the fixed-point sums, the used bits
+        // (all loads issued before the first LDS store: in-order counters)
         const double ein = tid < P ? a.err_in[tid] : 0.0;
-        if (tid < wpp * P) {
-            uint32_t wv[kUsedSlots];
 #pragma unroll
-            for (int sl = 0; sl < kUsedSlots; ++sl) wv[sl] = a.used_glob[sl * a.used_stride + tid];
+        for (int j = 0; j < MAXW; ++j) {
+            const int e = tid + nt * j;
+            if (e < wpp * P) {
+                uint32_t wv[kUsedSlots];
 #pragma unroll
-            for (int sl = 0; sl < kUsedSlots; ++sl) fold_word |= wv[sl];
+                for (int sl = 0; sl < kUsedSlots; ++sl) wv[sl] = a.used_glob[sl * a.used_stride + e];
+#pragma unroll
+                for (int sl = 0; sl < kUsedSlots; ++sl) fold_word[j] |= wv[sl];
+            }
         }
-        if (P <= 4) {
-            double acc4[4];
-            thread_partial_sums<4, 8>(a.partial, a.ntiles, P, acc4);
+        // palette pp's sum: lanes 16 pp .. 16 pp + 15 load its kAccSlots slot
+        // counters and add them across the lanes (integers: in any order,
+        // acc_total's value)
+        static_assert(kAccSlots == 16, "one 16-lane group per palette");
+        for (int e0 = 0; e0 < P * kAccSlots; e0 += nt) {
+            const int e = e0 + tid, pp = e >> 4, sl = e & 15;
+            unsigned long long lo = 0, hi = 0, bad = 0;
+            if (e < P * kAccSlots) {
+                const uint64_t* q = a.acc + ((int64_t)sl * P + pp) * 4;
+                lo = q[0];
+                hi = q[1];
+                bad = q[2];
+            }
 #pragma unroll
-            for (int p = 0; p < kFoldMaxP; ++p) fold_acc[p] = p < 4 ? acc4[p] : 0.0;
-        } else {
-            thread_partial_sums<kFoldMaxP, 4>(a.partial, a.ntiles, P, fold_acc);
+            for (int m = 8; m >= 1; m >>= 1) {
+                lo += __shfl_xor(lo, m, 64);
+                hi += __shfl_xor(hi, m, 64);
+                bad += __shfl_xor(bad, m, 64);
+            }
+            if (sl == 0 && e < P * kAccSlots)
+                s.sum[pp] = bad ? __builtin_nan("") : (double)hi * 4096.0 + (double)lo * (1.0 / kAccScale);
         }
         if (tid < P) s.err_in[tid] = ein;
     } else if (a.accept) {
@@ -215,23 +219,21 @@ __device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared
     uint64_t jA = 0, jC = 0;  // the writer's jump past this step's draws
     if (tid == 0) {
         s.seed = *a.seed_in;
-        s.best_in = a.accept && !a.init ? *a.best_err : 0.0;
+        s.best_in = a.init ? 0.0 : *a.best_err_in;
         if (writer && a.generate) { jA = a.jump_A[K * 3 * P]; jC = a.jump_C[K * 3 * P]; }
     }
     if (tid < P) s.unused[tid] = 0;
     __syncthreads();
     if (a.accept && a.fold) {
 #pragma unroll
-        for (int p = 0; p < kFoldMaxP; ++p) {
-            if (p >= P) break;
-            const double w = wave_sum_to_lane63(fold_acc[p]);
-            if ((tid & 63) == 63) s.fold_red[p][tid >> 6] = w;
-        }
-        if (tid < wpp * P) {  // unused colours: clear bits below K
-            const int nbits = min(max(K - 32 * (tid % wpp), 0), 32);
-            const uint32_t valid = nbits >= 32 ? ~0u : ((1u << nbits) - 1u);
-            const int clear = nbits - __popc(fold_word & valid);
-            if (clear) atomicAdd(&s.unused[tid / wpp], clear);
+        for (int j = 0; j < MAXW; ++j) {
+            const int e = tid + nt * j;
+            if (e < wpp * P) {  // unused colours: clear bits below K
+                const int nbits = min(max(K - 32 * (e % wpp), 0), 32);
+                const uint32_t valid = nbits >= 32 ? ~0u : ((1u << nbits) - 1u);
+                const int clear = nbits - __popc(fold_word[j] & valid);
+                if (clear) atomicAdd(&s.unused[e / wpp], clear);
+            }
         }
     } else if (a.accept) {
         if (nf <= MAXF) {
@@ -254,11 +256,6 @@ __device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared
     if (a.accept) {
         __syncthreads();
         if (tid < P) {  // per member, in parallel: error, current, acceptance probability
-            if (a.fold) {  // finalize's order: the 16 wave sums ascending
-                double tot = 0.0;
-                for (int i = 0; i < 16; ++i) tot += s.fold_red[tid][i];
-                s.sum[tid] = tot;
-            }
             const double e = s.sum[tid] / a.n_total + (double)s.unused[tid] * (double)a.delta;
             const double c = a.init ? e : s.err_in[tid];
             s.err[tid] = e;
@@ -300,7 +297,7 @@ __device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared
             s.best = best_src;
             if (writer) {
                 for (int i = 0; i < P; ++i) a.err_out[i] = cur[i];
-                *a.best_err = best;
+                *a.best_err_out = best;
                 *a.seed_out = a.generate ? lcg_jump(seed, jA, jC) : seed;
             }
         }
@@ -309,31 +306,68 @@ __device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared
         for (int i = 0; i < P; ++i) s.src[i] = -1;
         if (writer) {
             for (int i = 0; i < P; ++i) a.err_out[i] = a.err_in[i];
+            *a.best_err_out = s.best_in;
             *a.seed_out = a.generate ? lcg_jump(s.seed, a.jump_A[K * 3 * P], a.jump_C[K * 3 * P]) : s.seed;
         }
     }
     __syncthreads();
 }
 
+// Prefetches of a step, issued before the acceptance: member p's candidate and
+// kept palette (elements e0 + tid + nt j of its colours, chunk ch's 1,024 floats
+// at most) and this thread's jumps to draws t0 + tid + nt j (768 at most), nt =
+// 1024 / NPF threads.
+template <int NPF>
+struct SaPf {
+    float cand[NPF], col[NPF];
+    uint64_t jA[NPF], jC[NPF], bA = 0, bC = 0;
+    __device__ __forceinline__ void load(const SaArgs& a, int p, int ch) {
+        const int n4 = 4 * a.K, tid = threadIdx.x, nt = 1024 / NPF;
+        const int e0 = a.nch > 1 ? 4 * kMaxK * ch : 0, t0 = a.nch > 1 ? 3 * kMaxK * ch : 0;
+#pragma unroll
+        for (int j = 0; j < NPF; ++j) {
+            const int e = e0 + tid + nt * j, t = t0 + tid + nt * j;
+            cand[j] = col[j] = 0.f;
+            jA[j] = jC[j] = 0;
+            if (e < n4 && tid + nt * j < 4 * kMaxK) {
+                if (a.accept) cand[j] = a.cand_in[(int64_t)p * n4 + e];
+                col[j] = a.colors_in[(int64_t)p * n4 + e];
+            }
+            if (a.generate && t < 3 * a.K && tid + nt * j < 3 * kMaxK) {
+                jA[j] = a.jump_A[t + 1];
+                jC[j] = a.jump_C[t + 1];
+            }
+        }
+        if (a.generate) {
+            bA = a.jump_A[3 * a.K * p];
+            bC = a.jump_C[3 * a.K * p];
+        }
+    }
+};
+
 // Member p's accepted palette into s_from (LDS, 4K floats; chunked palettes:
 // elements e0 .. e0 + 1023 of it, chunk c = e0 / 1024); `lead` also copies it
 // to colors_out (and, for p = 0, a new best to best_colors).  The two likely
-// sources -- member p's candidate and its kept palette -- are read before the
-// acceptance (pf_cand, pf_col: element e0 + tid); only a convergence copy from
-// another member's candidate reads after it.
+// sources -- member p's candidate and its kept palette -- were read before the
+// acceptance (pf); only a convergence copy from another member's candidate
+// reads after it.
+template <int NPF>
 __device__ __forceinline__ void sa_keep(const SaArgs& a, int p, int e0, bool lead, const SaShared& s,
-                                        float pf_cand, float pf_col, float* s_from) {
-    const int n4 = 4 * a.K, tid = threadIdx.x, nt = blockDim.x;
+                                        const SaPf<NPF>& pf, float* s_from) {
+    const int n4 = 4 * a.K, tid = threadIdx.x, nt = 1024 / NPF;
     const int ne = a.nch > 1 ? min(4 * kMaxK, n4 - e0) : n4;
     const int src = s.src[p];
-    for (int i = tid; i < ne; i += nt) {
-        const int e = e0 + i;
-        float v;
-        if (i == tid && src == p) v = pf_cand;
-        else if (i == tid && src < 0) v = pf_col;
-        else v = src >= 0 ? a.cand_in[(int64_t)src * n4 + e] : a.colors_in[(int64_t)p * n4 + e];
-        s_from[i] = v;
-        if (lead) a.colors_out[(int64_t)p * n4 + e] = v;
+#pragma unroll
+    for (int j = 0; j < NPF; ++j) {
+        const int i = tid + nt * j, e = e0 + i;
+        if (i < ne) {
+            float v;
+            if (src == p) v = pf.cand[j];
+            else if (src < 0) v = pf.col[j];
+            else v = a.cand_in[(int64_t)src * n4 + e];
+            s_from[i] = v;
+            if (lead) a.colors_out[(int64_t)p * n4 + e] = v;
+        }
     }
     if (lead && p == 0 && s.best >= 0)  // IM:533-536: the best palette so far
         for (int i = tid; i < ne; i += nt) a.best_colors[e0 + i] = a.cand_in[(int64_t)s.best * n4 + e0 + i];
@@ -342,7 +376,6 @@ __device__ __forceinline__ void sa_keep(const SaArgs& a, int p, int e0, bool lea
 
 // Candidate p into s_cand (.w = 0; cand_out too when `lead`): draw t = 3i + c of
 // this palette's block (SW:91-101 neighbours of s_from, or SW:40-52 random).
-// jA/jC: this thread's prefetched jump to its first draw (t = t0 + tid).
 // Chunked palettes: chunk ch = colours 256 ch .. (draws t0 = 768 ch ..), and
 // the chunk's colours past K are copies of candidate colour 0 (pack_chunks'
 // padding), drawn again here from its source colour `src0`.
@@ -355,19 +388,21 @@ __device__ __forceinline__ float sa_draw(const SaArgs& a, uint64_t st, float fro
     return x > 0.f ? (x > 1.f ? 1.f : x) : 0.f;  // clampf_java (SW:103-106)
 }
 
+template <int NPF>
 __device__ __forceinline__ void sa_generate(const SaArgs& a, int p, int ch, const float* s_from,
                                             const float* src0, uint64_t seed, float4* s_cand, bool lead,
-                                            uint64_t jA, uint64_t jC, uint64_t bA, uint64_t bC) {
-    const int K = a.K, n4 = 4 * K, tid = threadIdx.x, nt = blockDim.x;
+                                            const SaPf<NPF>& pf) {
+    const int K = a.K, n4 = 4 * K, tid = threadIdx.x, nt = 1024 / NPF;
     const int k0 = a.nch > 1 ? kMaxK * ch : 0, kn = a.nch > 1 ? min(kMaxK, K - k0) : K;  // real colours
-    const int t0 = 3 * k0;
-    const uint64_t base = lcg_jump(seed, bA, bC);  // bA, bC: jump_A/C[3Kp], prefetched
-    for (int tt = tid; tt < 3 * kn; tt += nt) {
-        const int t = t0 + tt, i = tt / 3, c = tt - 3 * i;
-        const uint64_t st = tt == tid ? lcg_jump(base, jA, jC) : lcg_jump(base, a.jump_A[t + 1], a.jump_C[t + 1]);
-        const float v = sa_draw(a, st, s_from[4 * i + c]);
-        reinterpret_cast<float*>(s_cand)[4 * i + c] = v;
-        if (lead) a.cand_out[(int64_t)p * n4 + 4 * (k0 + i) + c] = v;
+    const uint64_t base = lcg_jump(seed, pf.bA, pf.bC);  // jump_A/C[3Kp], prefetched
+#pragma unroll
+    for (int j = 0; j < NPF; ++j) {
+        const int tt = tid + nt * j, i = tt / 3, c = tt - 3 * i;
+        if (tt < 3 * kn) {
+            const float v = sa_draw(a, lcg_jump(base, pf.jA[j], pf.jC[j]), s_from[4 * i + c]);
+            reinterpret_cast<float*>(s_cand)[4 * i + c] = v;
+            if (lead) a.cand_out[(int64_t)p * n4 + 4 * (k0 + i) + c] = v;
+        }
     }
     for (int k = tid; k < kn; k += nt) {
         reinterpret_cast<float*>(s_cand)[4 * k + 3] = 0.f;
@@ -381,29 +416,6 @@ __device__ __forceinline__ void sa_generate(const SaArgs& a, int p, int ch, cons
     }
     __syncthreads();
 }
-
-// Prefetches of a step, issued before the acceptance: member p's candidate and
-// kept palette (element tid) and this thread's jump to draw tid.
-struct SaPf {
-    float cand = 0.f, col = 0.f;
-    uint64_t jA = 0, jC = 0, bA = 0, bC = 0;
-    __device__ __forceinline__ void load(const SaArgs& a, int p, int ch) {
-        const int n4 = 4 * a.K, tid = threadIdx.x;
-        const int e = a.nch > 1 ? 4 * kMaxK * ch + tid : tid, t = a.nch > 1 ? 3 * kMaxK * ch + tid : tid;
-        if (e < n4 && (a.nch == 1 || tid < 4 * kMaxK)) {
-            if (a.accept) cand = a.cand_in[(int64_t)p * n4 + e];
-            col = a.colors_in[(int64_t)p * n4 + e];
-        }
-        if (a.generate && t < 3 * a.K && (a.nch == 1 || tid < 3 * kMaxK)) {
-            jA = a.jump_A[t + 1];
-            jC = a.jump_C[t + 1];
-        }
-        if (a.generate) {
-            bA = a.jump_A[3 * a.K * p];
-            bC = a.jump_C[3 * a.K * p];
-        }
-    }
-};
 
 // Build with -DHQ_SA_TIMING to print block 0's phase times (accept, keep,
 // generate, prep; wall_clock64 ticks of 10 ns) per launch.
@@ -419,14 +431,14 @@ __global__ __launch_bounds__(1024) void sa_step_kernel(SaArgs a) {
 #ifdef HQ_SA_TIMING
     const uint64_t t0 = wall_clock64();
 #endif
-    SaPf pf;
+    SaPf<1> pf;
     pf.load(a, p, ch);
-    sa_accept(a, blockIdx.x == 0, s);
+    sa_accept<16>(a, blockIdx.x == 0, s);
 #ifdef HQ_SA_TIMING
     const uint64_t t1 = wall_clock64();
 #endif
     const int e0 = 4 * kMaxK * ch;
-    sa_keep(a, p, e0, true, s, pf.cand, pf.col, s_from);
+    sa_keep(a, p, e0, true, s, pf, s_from);
 #ifdef HQ_SA_TIMING
     const uint64_t t2 = wall_clock64();
 #endif
@@ -438,12 +450,15 @@ __global__ __launch_bounds__(1024) void sa_step_kernel(SaArgs a) {
         s_src0[threadIdx.x] = src >= 0 ? a.cand_in[(int64_t)src * n4 + threadIdx.x]
                                        : a.colors_in[(int64_t)p * n4 + threadIdx.x];
     }
-    sa_generate(a, p, ch, s_from, ch > 0 ? s_src0 : s_from, s.seed, s_cand, true, pf.jA, pf.jC, pf.bA, pf.bC);
+    sa_generate(a, p, ch, s_from, ch > 0 ? s_src0 : s_from, s.seed, s_cand, true, pf);
 #ifdef HQ_SA_TIMING
     const uint64_t t3 = wall_clock64();
 #endif
     const int k = threadIdx.x;
-    prep_palette_body(a.prep, blockIdx.x, k < K ? s_cand[k] : make_float4(0.f, 0.f, 0.f, 0.f));
+    __shared__ PrepLds L;
+    bool nf;
+    (void)prep_palette_body(a.prep, blockIdx.x, k < K ? s_cand[k] : make_float4(0.f, 0.f, 0.f, 0.f), s_cand, L,
+                            true, nf);
 #ifdef HQ_SA_TIMING
     __syncthreads();
     if (threadIdx.x == 0 && p == 0)
@@ -639,22 +654,32 @@ __device__ __forceinline__ void drop_positions(uint32_t (&w)[4], int& n, uint32_
     }
 }
 
+// LDS of one level-1 cell's grid work.
+struct GridLds {
+    float4 col[kMaxK];
+    float ax[3][4][kAxPitch];
+    LongLists lng;  // (8-B entries only)
+    uint8_t list[kMaxK];
+    float mn[4];
+    int wcount[4];
+};
+
 // The grid work of level-1 cell `cell` of palette p; thread tid holds colour
 // tid (zeros past K) and whether it may be a candidate (prep_palette's
 // duplicate flags: an exact duplicate never wins the strict < of CL:186).
 __device__ __forceinline__ void grid_cell_body(const GridArgs& a, int p, int cell, float4 c,
-                                               bool valid, bool exh) {
+                                               bool valid, bool exh, GridLds& L) {
     const int tid = threadIdx.x;
     const int G1 = a.G1, G2 = 4 * G1;
     const int ci = cell / (G1 * G1), cj = (cell / G1) % G1, ck = cell % G1;
-    __shared__ float4 s_col[kMaxK];
-    __shared__ uint8_t s_list[kMaxK];
-    __shared__ float s_min[4];
-    __shared__ int s_wcount[4];
-    __shared__ float s_ax[3][4][kAxPitch];
+    float4* const s_col = L.col;
+    uint8_t* const s_list = L.list;
+    float* const s_min = L.mn;
+    int* const s_wcount = L.wcount;
+    float (*const s_ax)[4][kAxPitch] = L.ax;
+    LongLists& s_long = L.lng;
 
     s_col[tid] = c;
-    __shared__ LongLists s_long;  // (8-B entries only)
     if (kL2Cap < kL2Build && tid == 0) s_long.count = 0;
     const float inv1 = 1.0f / (float)G1;
     const float lo0 = ci * inv1, hi0 = (ci + 1) * inv1;
@@ -819,6 +844,8 @@ __global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
 #endif
     if (blockIdx.x == 0 && tid < 8 * kUsedSlots)  // for the assign that follows
         a.used_glob[(tid >> 3) * a.used_stride + p * 8 + (tid & 7)] = 0u;
+    if (blockIdx.x == 0 && p % a.nch == 0 && tid < 4 * kAccSlots)  // for the cost kernel
+        a.acc_zero[((int64_t)(tid >> 2) * a.P_acc + p / a.nch) * 4 + (tid & 3)] = 0ull;
     const bool exh = a.pflags[p] != 0;
     bool valid = false;
     float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -826,7 +853,8 @@ __global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
         c = a.pal[(int64_t)p * kMaxK + tid];
         valid = !exh && a.dup[(int64_t)p * kMaxK + tid] == 0;
     }
-    grid_cell_body(a, p, blockIdx.x, c, valid, exh);
+    __shared__ GridLds L;
+    grid_cell_body(a, p, blockIdx.x, c, valid, exh, L);
 #ifdef HQ_GRID_TIMING
     __syncthreads();
     if (tid == 0 && p * (int)gridDim.x + (int)blockIdx.x < kGridStamps) {
@@ -836,24 +864,14 @@ __global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
 #endif
 }
 // ----------------------------------------------------------------------------
-// finalize: grid (P), block 1024.  Fixed-order fp64 sum of the tile partials
-// (thread_partial_sums) and the used bits -> out[p] = {sum, used[0..K-1]}.
+// finalize: grid (P), block 1024.  The fixed-point dE sum (acc_total) and the
+// used bits -> out[p] = {sum, used[0..K-1]}.
 // ----------------------------------------------------------------------------
 __global__ __launch_bounds__(1024) void finalize_kernel(FinalizeArgs a) {
     constexpr int NT = 1024;
     const int p = blockIdx.x, tid = threadIdx.x;
-    __shared__ double s_red[NT / 64];
-    double acc[1];
-    thread_partial_sums<1, 24>(a.partial + (int64_t)p * a.ntiles, a.ntiles, 1, acc);
-    const double s = wave_sum_to_lane63(acc[0]);
-    if ((tid & 63) == 63) s_red[tid >> 6] = s;
-    __syncthreads();
     double* out = a.out + (int64_t)p * (1 + a.K);
-    if (tid == 0) {
-        double tot = 0.0;
-        for (int i = 0; i < NT / 64; ++i) tot += s_red[i];
-        out[0] = tot;
-    }
+    if (tid == 0) out[0] = acc_total(a.acc, a.P, p);
     if (a.used32) {  // K > 256: the reference's per-colour flags (assign_wide)
         const uint32_t* u = a.used32 + (int64_t)p * a.K;
         for (int k = tid; k < a.K; k += NT) out[1 + k] = u[k] != 0u ? 1.0 : 0.0;

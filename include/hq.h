@@ -185,7 +185,8 @@ int hq_swasa_search_host(const hq_swasa_params *params, int K, uint64_t seed, in
 /* Kernel timing of the dominant kernels, measured with HIP events on the
  * context stream while enabled (bench.py roofline). */
 int hq_profile_enable(hq_ctx *ctx, int on);
-/* names: "assign", "cost", "grid", "finalize"; returns total ms and launch count. */
+/* names: "assign", "cost", "grid", "finalize", "sa_step" (device-resident search); returns total
+ * ms and launch count. */
 int hq_profile_get(hq_ctx *ctx, const char *kernel, double *total_ms, int64_t *launches);
 int hq_profile_reset(hq_ctx *ctx);
 
