@@ -327,9 +327,7 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
     const int p0 = 4 * grp;
     const uint8_t* lines = a.lvl2 + (int64_t)grp * a.lvl2_gstride;
     const int G2 = a.G2 > 0 ? a.G2 : 4;
-#ifdef HQ_CELL_INT
     const int lg_g2 = 31 - __builtin_clz(G2);  // (a power of two, hq_set_option "grid")
-#endif
     // pixel sequence of this thread: a grid stride.  Positions and byte offsets
     // are 32-bit (the host keeps a shard's extended rows below 2^30 pixels), so
     // loads and stores take the scalar-base form.
@@ -383,12 +381,9 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
 #elif defined(HQ_ABL_COHERENT)  // timing ablation (wrong results): runs of 256 consecutive pixels share a cell
         const uint8_t* lb = lines + (((q >> 8) * 40503u) & (uint32_t)(G2 * G2 * G2 - 1)) * (uint32_t)kL2Line;
 #else
-#ifdef HQ_CELL_INT
+        // (packed pixels: the cell straight from the bytes, cell_u8)
         const uint8_t* lb = lines + (U8 ? cell_u8(raw, lg_g2) : inside ? (uint32_t)quad_cell(r, g, b, G2) : 0u) *
                                         (uint32_t)kL2Line;
-#else
-        const uint8_t* lb = lines + (inside ? (uint32_t)quad_cell(r, g, b, G2) : 0u) * (uint32_t)kL2Line;
-#endif
 #endif
         // selected by the `listed` flag at use.  8-B entries: two palettes per
         // 16-B load (the L1 access count per pixel, not the bytes, is the cost)

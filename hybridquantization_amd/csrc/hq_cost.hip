@@ -604,14 +604,8 @@ __device__ __forceinline__ void hpass_wide(const f32x4* src, int j, TapsPtr<HB> 
             const float k = taps->h[f][t];
             const f32x2 kk = {k, k};
 #pragma unroll
-            for (int xo = 0; xo < HR; ++xo) {
-#ifdef HQ_HPASS_SCALAR  // experiment: two v_fma_f32 per row pair instead of one v_pk_fma_f32
-                acc[xo].x = __builtin_fmaf(in[xo + t - 2 * q0].x, k, acc[xo].x);
-                acc[xo].y = __builtin_fmaf(in[xo + t - 2 * q0].y, k, acc[xo].y);
-#else
+            for (int xo = 0; xo < HR; ++xo)
                 acc[xo] = __builtin_elementwise_fma(in[xo + t - 2 * q0], kk, acc[xo]);
-#endif
-            }
         }
     }
 }
