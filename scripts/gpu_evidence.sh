@@ -31,7 +31,10 @@ done
 # (C5's 64-palette search would take ~1 min: 10 warm-up steps, ~0.1 s, instead)
 for cfg in "--size 1024 --K 64 --population 1" "--population 1" "" "--size 8192 --shard-of 8" "--population 64 --steps 20 --warmup 10 --no-full-search" \
            "--dpi 96 --distance 60 --no-full-search" "--dpi 150 --distance 30 --no-full-search" \
-           "--size 1024 --K 1024 --steps 10 --warmup 2 --no-full-search"; do
+           "--dpi 300 --distance 50 --steps 10 --warmup 2 --no-full-search" \
+           "--population 64 --shard-of 8 --steps 20 --warmup 5 --no-full-search" \
+           "--size 1024 --K 1024 --steps 50 --warmup 5 --no-full-search" \
+           "--size 1024 --K 4096 --steps 20 --warmup 3 --no-full-search"; do
   timeout -k 10 300 python bench.py --no-cpu-baseline $cfg >> $E/configs.jsonl 2>> $E/configs.err
   rc=$?; echo "config [$cfg] rc=$rc"; fatal $rc "config $cfg"
 done
