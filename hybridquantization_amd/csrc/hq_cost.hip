@@ -499,7 +499,7 @@ __global__ __launch_bounds__(256, 6) void cost_mfma_kernel(CostArgs a, int P_) {
     if ((tid & 63) == 63) s_red[tid >> 6] = sum;
     __syncthreads();
     if (tid == 0)
-        acc_add(a.acc, P_, cur.p, cur.tile, (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]));
+        acc_add(a.acc, a.acc_P, a.acc_p0 + cur.p, cur.tile, (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]));
 }
 
 // ----------------------------------------------------------------------------
@@ -800,7 +800,23 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
                     A[st][h][s][1] = F(h, s, 2 + st, 1);
                 }
     };
-    if constexpr (S == 1) load_a12();
+    // HB = 19: channels 1 and 2 gathered one after the other, so no vertical
+    // results wait in registers through a horizontal pass (the shared gather
+    // with channel 2 held in registers spilled 16 VGPRs; now 4)
+#ifndef HQ_SPLIT12
+#define HQ_SPLIT12 1
+#endif
+    constexpr bool SPLIT = HB == 19 && HQ_SPLIT12;  // (HB = 15: 5% slower split, r04_split12_ab.txt)
+    auto load_a_stack = [&](int stack) {  // one stack's fragments into A[0]
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                A[0][h][s][0] = F(h, s, stack, 0);
+                A[0][h][s][1] = F(h, s, stack, 1);
+            }
+    };
+    if constexpr (S == 1 && !SPLIT) load_a12();
     __syncthreads();
     uint2 tyz[W16 ? NTE : 1];  // W16: the (y, z) words, in flight through channel 0's horizontal pass
     if constexpr (W16) {
@@ -820,54 +836,91 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
     }
     __syncthreads();
 
-    // ---- channels 1, 2: one gather of (y, z) per region row; stack (f3, f4)
-    // -> planes 0, 1 now, stack (f5, f6)'s results held in registers until
-    // channel 1's horizontal pass has read the planes ----
-    if constexpr (S > 1) load_a12();
-    f32x4v d5[NSET][2];
+    // one column block's gather of channel `chn` (1: y, 2: z) and its stack -> planes 0, 1
+    auto vgather_one = [&](int chn) {
+        const uint4(&A1)[1][2][S][2] = *reinterpret_cast<const uint4(*)[1][2][S][2]>(&A[0]);
 #pragma unroll
-    for (int i = 0; i < NSET; ++i) {
-        const int b = wset + NW * i;
-        if (b >= NBLK) break;
-        const int col = col0 + 16 * NW * i;
-        uint32_t wy[NJ], wz[NJ];
+        for (int i = 0; i < NSET; ++i) {
+            const int b = wset + NW * i;
+            if (b >= NBLK) break;
+            const int col = col0 + 16 * NW * i;
+            uint32_t w[NJ];
 #pragma unroll
-        for (int n = 0; n < NJ; ++n) {
-            if (4 * n < RH) {
-                const uint2 e = s_oyz[s_idx[gather_row(n, col)]];
-                wy[n] = e.x; wz[n] = e.y;
-            } else {
-                wy[n] = wz[n] = 0u;
+            for (int n = 0; n < NJ; ++n) {
+                if (4 * n < RH) {
+                    const uint2 e = s_oyz[s_idx[gather_row(n, col)]];
+                    w[n] = chn == 1 ? e.x : e.y;
+                } else {
+                    w[n] = 0u;
+                }
             }
-        }
-        {
-            const uint4(&Ay)[1][2][S][2] = *reinterpret_cast<const uint4(*)[1][2][S][2]>(&A[0]);
             f32x4v d[1][2];
-            vblock<S, 1>(wy, Ay, d);
+            vblock<S, 1>(w, A1, d);
             store_vstack_at<WH, NW>(st01, d[0][0], i, 0);
             store_vstack_at<WH, NW>(st01, d[0][1], i, 1);
         }
-        {
-            const uint4(&Az)[1][2][S][2] = *reinterpret_cast<const uint4(*)[1][2][S][2]>(&A[1]);
-            f32x4v d[1][2];
-            vblock<S, 1>(wz, Az, d);
-            d5[i][0] = d[0][0];
-            d5[i][1] = d[0][1];
-        }
-    }
-    __syncthreads();
-    if constexpr (TRIM) hpass_wide<HB, L1, T2 - L1, WH>(hsrc, jr, taps, 3, 0, PLANE4, acc1);
-    else hpass_wide<HB, 0, T2, WH>(hsrc, jr, taps, 3, 0, PLANE4, acc1);
-    hpass_wide<HB, 0, T2, WH>(hsrc, jr, taps, 4, 1, PLANE4, acc1);
-    __syncthreads();
-
-    // ---- channel 2: stack (f5, f6) -> planes 0, 1 ----
+    };
+    if constexpr (SPLIT) {
+        // ---- channel 1: stack (f3, f4) -> planes 0, 1; then channel 2 ----
+        load_a_stack(2);
+        vgather_one(1);
+        __syncthreads();
+        load_a_stack(3);  // (in flight through channel 1's horizontal pass)
+        if constexpr (TRIM) hpass_wide<HB, L1, T2 - L1, WH>(hsrc, jr, taps, 3, 0, PLANE4, acc1);
+        else hpass_wide<HB, 0, T2, WH>(hsrc, jr, taps, 3, 0, PLANE4, acc1);
+        hpass_wide<HB, 0, T2, WH>(hsrc, jr, taps, 4, 1, PLANE4, acc1);
+        __syncthreads();
+        vgather_one(2);
+    } else {
+        // ---- channels 1, 2: one gather of (y, z) per region row; stack (f3, f4)
+        // -> planes 0, 1 now, stack (f5, f6)'s results held in registers until
+        // channel 1's horizontal pass has read the planes ----
+        if constexpr (S > 1) load_a12();
+        f32x4v d5[NSET][2];
 #pragma unroll
-    for (int i = 0; i < NSET; ++i) {
-        const int b = wset + NW * i;
-        if (b >= NBLK) break;
-        store_vstack_at<WH, NW>(st01, d5[i][0], i, 0);
-        store_vstack_at<WH, NW>(st01, d5[i][1], i, 1);
+        for (int i = 0; i < NSET; ++i) {
+            const int b = wset + NW * i;
+            if (b >= NBLK) break;
+            const int col = col0 + 16 * NW * i;
+            uint32_t wy[NJ], wz[NJ];
+#pragma unroll
+            for (int n = 0; n < NJ; ++n) {
+                if (4 * n < RH) {
+                    const uint2 e = s_oyz[s_idx[gather_row(n, col)]];
+                    wy[n] = e.x; wz[n] = e.y;
+                } else {
+                    wy[n] = wz[n] = 0u;
+                }
+            }
+            {
+                const uint4(&Ay)[1][2][S][2] = *reinterpret_cast<const uint4(*)[1][2][S][2]>(&A[0]);
+                f32x4v d[1][2];
+                vblock<S, 1>(wy, Ay, d);
+                store_vstack_at<WH, NW>(st01, d[0][0], i, 0);
+                store_vstack_at<WH, NW>(st01, d[0][1], i, 1);
+            }
+            {
+                const uint4(&Az)[1][2][S][2] = *reinterpret_cast<const uint4(*)[1][2][S][2]>(&A[1]);
+                f32x4v d[1][2];
+                vblock<S, 1>(wz, Az, d);
+                d5[i][0] = d[0][0];
+                d5[i][1] = d[0][1];
+            }
+        }
+        __syncthreads();
+        if constexpr (TRIM) hpass_wide<HB, L1, T2 - L1, WH>(hsrc, jr, taps, 3, 0, PLANE4, acc1);
+        else hpass_wide<HB, 0, T2, WH>(hsrc, jr, taps, 3, 0, PLANE4, acc1);
+        hpass_wide<HB, 0, T2, WH>(hsrc, jr, taps, 4, 1, PLANE4, acc1);
+        __syncthreads();
+
+        // ---- channel 2: stack (f5, f6) -> planes 0, 1 ----
+#pragma unroll
+        for (int i = 0; i < NSET; ++i) {
+            const int b = wset + NW * i;
+            if (b >= NBLK) break;
+            store_vstack_at<WH, NW>(st01, d5[i][0], i, 0);
+            store_vstack_at<WH, NW>(st01, d5[i][1], i, 1);
+        }
     }
     // LabRef of the item's 2 x 4 pixels, in flight across the barrier
     float4 lab[2][3];
@@ -927,7 +980,7 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
     if (tid == 0) {
         double t = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
         if constexpr (NW == 8) t += (s_red[4] + s_red[5]) + (s_red[6] + s_red[7]);
-        acc_add(a.acc, P_, cur.p, cur.tile, t);
+        acc_add(a.acc, a.acc_P, a.acc_p0 + cur.p, cur.tile, t);
     }
 }
 
@@ -988,6 +1041,126 @@ __global__ __launch_bounds__(256) void gen_vpass_kernel(GenArgs a) {
     if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = e;
     __syncthreads();
     if (threadIdx.x == 0) acc_add(a.acc, a.P, a.p, blockIdx.x, (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]));
+}
+
+// ----------------------------------------------------------------------------
+// Tiled generic path (any half-width; the default generic path since round 4,
+// and the one half > 24 -- e.g. 300 dpi at 50 cm, half 51 -- takes).  The same
+// two passes and the same [7][n_ext] scratch as gen_hpass / gen_vpass, staged
+// through LDS so each input feeds many outputs from LDS instead of L1/L2:
+// - gen_hrow: grid (ceil(W / 256), extended rows), block 256.  The opponent
+//   colours of the row segment x0 - half .. x0 + 255 + half (reflected,
+//   CL:256-263) land in LDS once (a float4 each); output x then reads one
+//   float4 per tap for its 7 FMAs, in the reference's tap order (CL:254-267).
+//   (gen_hpass gathered index and table entry per tap: 2 (2 half + 1) L1 reads.)
+// - gen_vtile: grid (64 x 64 output tiles of the owned rows), block 256.  For
+//   each filter (plane t1.xyz, t2.xyz, t3 with vertical taps k1.xyz, k2.xyz,
+//   |k3|), rows y0 - half .. y0 + 63 + half of the tile's 64 columns land in LDS;
+//   thread (column c, row block rb) owns output rows 16 rb .. 16 rb + 15 and runs
+//   the taps in chunks of 16: 32 window values from LDS and 16 taps (scalar
+//   loads, zero-padded to a multiple of 16) make 256 FMAs.  The filters are
+//   summed one after another (the reference interleaves them per tap): the
+//   fp32 rounding differs, as in the fast path (1e-6 relative on costs).  Then
+//   Opp->Lab, dE and the tile's fixed-point partial.  (gen_vpass read 7 (2 half
+//   + 1) floats per output from L2: 2.9 KB at half 51.)
+// ----------------------------------------------------------------------------
+template <typename IT>
+__global__ __launch_bounds__(256) void gen_hrow_kernel(GenArgs a) {
+    extern __shared__ float4 s_opp[];  // [256 + 2 half]
+    const int tid = threadIdx.x, half = a.half, W = a.g.W;
+    const int x0 = blockIdx.x * 256, ly = blockIdx.y;
+    const IT* row = static_cast<const IT*>(a.idx) + (int64_t)ly * W;
+    for (int e = tid; e < 256 + 2 * half; e += 256) {
+        const int x = min(x0 - half + e, W - 1 + half);  // (past the row end: reflected, unused)
+        s_opp[e] = a.opp[row[reflect_only(x, W)]];
+    }
+    __syncthreads();
+    const int x = x0 + tid;
+    if (x >= W) return;
+    float t1x = 0, t1y = 0, t1z = 0, t2x = 0, t2y = 0, t2z = 0, t3 = 0;
+    for (int t = 0; t <= 2 * half; ++t) {  // CL:254-267
+        const float4 in = s_opp[tid + t];
+        t1x = fmaf(in.x, a.k1[4 * t + 0], t1x);
+        t1y = fmaf(in.y, a.k1[4 * t + 1], t1y);
+        t1z = fmaf(in.z, a.k1[4 * t + 2], t1z);
+        t2x = fmaf(in.x, a.k2[4 * t + 0], t2x);
+        t2y = fmaf(in.y, a.k2[4 * t + 1], t2y);
+        t2z = fmaf(in.z, a.k2[4 * t + 2], t2z);
+        t3 = fmaf(in.x, a.k3[t], t3);
+    }
+    const int64_t n = a.g.n_ext, q = (int64_t)ly * W + x;
+    a.t[q] = t1x; a.t[n + q] = t1y; a.t[2 * n + q] = t1z;
+    a.t[3 * n + q] = t2x; a.t[4 * n + q] = t2y; a.t[5 * n + q] = t2z;
+    a.t[6 * n + q] = t3;
+}
+
+constexpr int kVtTile = 64, kVtRows = 16;  // gen_vtile: 64 x 64 tiles, 16 output rows per thread
+template <int DE>
+__global__ __launch_bounds__(256) void gen_vtile_kernel(GenArgs a, int tiles_x) {
+    extern __shared__ float s_win[];  // [64 + 2 half][64]
+    constexpr int TW = kVtTile, RB = kVtRows;
+    __shared__ double s_red[4];
+    const int tid = threadIdx.x, c = tid & (TW - 1), rb = tid >> 6;
+    const Geom& g = a.g;
+    const int x0 = (blockIdx.x % tiles_x) * TW, y0 = g.r0 + (blockIdx.x / tiles_x) * TW;
+    const int half = a.half, RH = TW + 2 * half, T = 2 * half + 1;
+    const int64_t n = g.n_ext;
+    float acc[3][RB];
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch)
+#pragma unroll
+        for (int j = 0; j < RB; ++j) acc[ch][j] = 0.f;
+    for (int f = 0; f < kNumFilt; ++f) {
+        const float* plane = a.t + (int64_t)f * n;
+        const float* vt = a.vtaps + f * a.vtap_pitch;  // zero-padded to a multiple of 16
+        __syncthreads();  // (the previous filter's window reads)
+        for (int e = tid; e < RH * TW; e += 256) {
+            const int i = e / TW, j = e % TW;
+            int gy = reflect_clamp(y0 - half + i, g.H);
+            gy = min(max(gy, g.e0), g.e1 - 1);
+            s_win[e] = plane[(int64_t)(gy - g.e0) * g.W + min(x0 + j, g.W - 1)];
+        }
+        __syncthreads();
+        float o[RB];
+#pragma unroll
+        for (int j = 0; j < RB; ++j) o[j] = 0.f;
+        for (int k0 = 0; k0 < T; k0 += 16) {
+            float v[RB + 16];
+#pragma unroll
+            for (int i = 0; i < RB + 16; ++i) v[i] = s_win[min(RB * rb + k0 + i, RH - 1) * TW + c];
+#pragma unroll
+            for (int kk = 0; kk < 16; ++kk) {
+                const float w = vt[k0 + kk];
+#pragma unroll
+                for (int j = 0; j < RB; ++j) o[j] = fmaf(v[j + kk], w, o[j]);
+            }
+        }
+        // planes: 0 t1.x, 1 t1.y, 2 t1.z, 3 t2.x, 4 t2.y, 5 t2.z, 6 t3 -> channels x y z x y z x
+        const int chp = f == 6 ? 0 : f % 3;
+#pragma unroll
+        for (int j = 0; j < RB; ++j) {
+            if (chp == 0) acc[0][j] += o[j];
+            else if (chp == 1) acc[1][j] += o[j];
+            else acc[2][j] += o[j];
+        }
+    }
+    double part = 0.0;
+    const int gx = x0 + c;
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+        const int y = y0 + RB * rb + j;
+        if (gx < g.W && y < g.r1) {
+            const float3 lf = opp2f_fast(acc[0][j], acc[1][j], acc[2][j], a.m_lab);
+            const int64_t off = (int64_t)(y - g.r0) * g.lab_pitch + gx;
+            const float ef = delta_e_f<DE>(a.labL[off], a.labA[off], a.labB[off], lf);
+            if (a.pix_err) a.pix_err[(int64_t)(y - g.r0) * g.W + gx] = ef;  // test option: the per-pixel dE
+            part += (double)ef;
+        }
+    }
+    part = wave_sum_to_lane63(part);
+    if ((tid & 63) == 63) s_red[tid >> 6] = part;
+    __syncthreads();
+    if (tid == 0) acc_add(a.acc, a.P, a.p, blockIdx.x, (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]));
 }
 
 // ----------------------------------------------------------------------------
@@ -1174,8 +1347,9 @@ static void launch_cost16w_chunked(const CostArgs& a0, int P, int de, bool trim,
     auto go = [&](auto kern) {
         static bool attr = false;  // LDS above 64 KB in all (NCH 16: 74 KB)
         if (!attr) {
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+            if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)dyn) != hipSuccess)
+                return;  // (the launch error is the caller's hipGetLastError)
             attr = true;
         }
         HQ_LAUNCH(kern, grid, block, dyn, s, a, P);
@@ -1226,6 +1400,36 @@ hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, bool trim, int ti
     if (de == 0) { if (trim) HQ_COST(cost_mfma_kernel, 0, true); else HQ_COST(cost_mfma_kernel, 0, false); }
     else { if (trim) HQ_COST(cost_mfma_kernel, 1, true); else HQ_COST(cost_mfma_kernel, 1, false); }
 #undef HQ_COST
+    return hipGetLastError();
+}
+
+// The tiled generic pair (gen_hrow + gen_vtile).  idx_bytes: 1, 2 (chunked
+// palettes) or 4 (K > 4096).
+hipError_t launch_cost_tiled_generic(const GenArgs& a, int de, int idx_bytes, hipStream_t s) {
+    const hipEvent_t ev0 = t_ev_start, ev1 = t_ev_stop;
+    t_ev_stop = nullptr;
+    const dim3 hg((unsigned)((a.g.W + 255) / 256), (unsigned)(a.g.e1 - a.g.e0));
+    const size_t hl = sizeof(float4) * (256 + 2 * (size_t)a.half);
+    if (idx_bytes == 4) HQ_LAUNCH(gen_hrow_kernel<uint32_t>, hg, dim3(256), hl, s, a);
+    else if (idx_bytes == 2) HQ_LAUNCH(gen_hrow_kernel<uint16_t>, hg, dim3(256), hl, s, a);
+    else HQ_LAUNCH(gen_hrow_kernel<uint8_t>, hg, dim3(256), hl, s, a);
+    t_ev_start = nullptr;
+    t_ev_stop = ev1;
+    const int tiles_x = (a.g.W + kVtTile - 1) / kVtTile, tiles_y = (a.g.r1 - a.g.r0 + kVtTile - 1) / kVtTile;
+    const size_t vl = sizeof(float) * kVtTile * (kVtTile + 2 * (size_t)a.half);
+    auto go = [&](auto kern) {
+        static size_t attr = 64 * 1024;  // window rows above 64 KB (half > 95): raise the limit
+        if (vl > attr) {
+            if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)vl) != hipSuccess)
+                return;  // (the launch error is the caller's hipGetLastError)
+            attr = vl;
+        }
+        HQ_LAUNCH(kern, dim3((unsigned)(tiles_x * tiles_y)), dim3(256), vl, s, a, tiles_x);
+    };
+    if (de == 0) go(gen_vtile_kernel<0>);
+    else go(gen_vtile_kernel<1>);
+    t_ev_start = ev0;
     return hipGetLastError();
 }
 

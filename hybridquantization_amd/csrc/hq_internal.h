@@ -170,7 +170,8 @@ struct CostArgs {
     const float* labL;      // planar LabRef, owned rows, pitch lab_pitch
     const float* labA;
     const float* labB;
-    uint64_t* acc;          // fixed-point dE sums [kAccSlots][P][4] (acc_add)
+    uint64_t* acc;          // fixed-point dE sums [kAccSlots][acc_P][4] (acc_add); this launch's
+    int acc_P, acc_p0;      // palettes are acc_p0 .. (a group of a larger population: acc_p0 > 0)
     Geom g;
     int K;
     int tiles_x;
@@ -225,6 +226,8 @@ struct GenArgs {
     int half;
     float m_lab[9];  // Opp->XYZ rows / illuminant (CL:124-131), opp2xyz_over_illum()
     float* pix_err;  // this palette's per-pixel dE of the owned rows (test option), or null
+    const float* vtaps;  // tiled path: [7][vtap_pitch] vertical taps per plane, zero-padded
+    int vtap_pitch;      // (2 half + 1 rounded up to 16, + 16)
 };
 
 }  // namespace hq

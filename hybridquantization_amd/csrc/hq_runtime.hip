@@ -45,6 +45,7 @@ void build_fast_taps(int HB, int H, const float* k1, const float* k2, const floa
 bool trim_window_ok(const float* k1, int H, int HB);
 
 hipError_t launch_cost_generic(const GenArgs&, int de, int idx_bytes, hipStream_t);
+hipError_t launch_cost_tiled_generic(const GenArgs&, int de, int idx_bytes, hipStream_t);
 hipError_t launch_prep_wide(const WideArgs&, int P, hipStream_t);
 hipError_t launch_assign_wide(const WideArgs&, int P, hipStream_t);
 hipError_t launch_finalize(const FinalizeArgs&, int P, hipStream_t);
@@ -103,6 +104,8 @@ struct hq_ctx {
     int taps = 0, half = 0;
     std::vector<float> k1, k2, k3, absk3;
     DevBuf d_k1, d_k2, d_k3, d_absk3;
+    DevBuf d_vtaps;    // tiled generic path: [7][vtap_pitch] vertical taps per plane, zero-padded
+    int vtap_pitch = 0;
     int fast_hb = 0;   // fast path tap bucket (fast_bucket(half)); 0 = generic path only
     DevBuf d_taps;     // fast path taps, build_fast_taps (the filters centred in the bucket)
     DevBuf d_vfrag16;  // split-f16 MFMA A fragments of the stacked vertical taps
@@ -135,7 +138,8 @@ struct hq_ctx {
 
     // options
     int G2 = 32;           // argmin grid resolution (0 = exhaustive)
-    int cost_variant = 0;  // 0 tiled (default), 1 generic two-pass
+    int cost_variant = 0;  // 0 fast tiled (default), 1 generic two-pass (LDS-tiled), 2 the generic
+                           // pair per pixel in the reference's summation order
     int cost_rows = 16;    // fast path tiles: 16 x 128 (cost16w_kernel) or 8 x 108 (cost_mfma_kernel)
     int cost_tw = HQ_COST_TW;  // 16-row tiles at HB = 10: 128 (4 waves) or 256 columns (8 waves; slower)
     int assign_blocks_per_cu = 0;  // 0 = auto: assign_pipe_kernel<NG>'s residency (the occupancy
@@ -489,10 +493,14 @@ int enqueue_generic_cost(hq_ctx* c, int P, const void* idx_base, int idx_bytes, 
         gn.g = g;
         gn.half = c->half;
         gn.pix_err = c->pixel_err ? c->d_pixerr.as<float>() + (int64_t)p * n_own : nullptr;
+        gn.vtaps = c->d_vtaps.as<float>();
+        gn.vtap_pitch = c->vtap_pitch;
         opp2xyz_over_illum(inv, gn.m_lab);
         // the events span every palette's launch pair: start on the first, stop on the last
         if (ev) set_launch_events(p == 0 ? ev[4] : nullptr, p == P - 1 ? ev[5] : nullptr);
-        const hipError_t e = launch_cost_generic(gn, c->de_type, idx_bytes, s);
+        // cost_variant 2: the per-pixel pair in the reference's summation order
+        const hipError_t e = c->cost_variant == 2 ? launch_cost_generic(gn, c->de_type, idx_bytes, s)
+                                                  : launch_cost_tiled_generic(gn, c->de_type, idx_bytes, s);
         set_launch_events(nullptr, nullptr);
         HIP_TRY(c, e);
     }
@@ -569,19 +577,15 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
         aa.nch = nch;
         while ((1 << aa.lg_nch) < nch) ++aa.lg_nch;
     }
-    timed(1);
-    hipError_t e = launch_assign(aa, Ps, s);
-    untimed();
-    HIP_TRY(c, e);
     const float inv[3] = {1.0f / c->illum[0], 1.0f / c->illum[1], 1.0f / c->illum[2]};
     // chunked palettes: the 16 x 128 tiles at HB = 10 (else the generic path)
-    const bool fast = c->cost_variant != 1 && c->fast_hb > 0 && !c->pal_generic &&
+    const bool fast = c->cost_variant == 0 && c->fast_hb > 0 && !c->pal_generic &&
                       (nch == 1 || (c->fast_hb == 10 && c->cost_rows == 16 && c->cost_tw == 128));
+    // 8-row tiles (cost_mfma_kernel) exist for the 21-tap bucket only
+    const int rows = c->fast_hb == 10 ? c->cost_rows : 16;
+    const int tw = c->fast_hb == 10 ? c->cost_tw : 128;  // 256-column tiles: HB = 10 only
+    CostArgs ca{};
     if (fast) {
-        // 8-row tiles (cost_mfma_kernel) exist for the 21-tap bucket only
-        const int rows = c->fast_hb == 10 ? c->cost_rows : 16;
-        const int tw = c->fast_hb == 10 ? c->cost_tw : 128;  // 256-column tiles: HB = 10 only
-        CostArgs ca{};
         ca.idx = nch > 1 ? c->d_idx16.as<uint8_t>() : c->d_idx.as<uint8_t>();
         ca.opp16 = c->d_opp16.as<uint4>();
         ca.taps = c->d_taps.p;
@@ -590,12 +594,20 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
         ca.labA = c->d_labA.as<float>();
         ca.labB = c->d_labB.as<float>();
         ca.acc = ga.acc_zero;
+        ca.acc_P = P;
+        ca.acc_p0 = 0;
         ca.g = g;
         ca.K = K;
         fast_tile_dims(g.W, g.r1 - g.r0, rows, tw, &ca.tiles_x, &ca.ntiles);
         opp2xyz_over_illum(inv, ca.m_lab);
         ca.pix_err = c->pixel_err ? c->d_pixerr.as<float>() : nullptr;
         ca.pix_pitch = (int64_t)g.W * (g.r1 - g.r0);
+    }
+    timed(1);
+    hipError_t e = launch_assign(aa, Ps, s);
+    untimed();
+    HIP_TRY(c, e);
+    if (fast) {
         timed(2);
         e = nch > 1 ? launch_cost_chunked(ca, P, nch, c->de_type, c->trim && c->trim_ok, s)
                     : launch_cost_fast(ca, P, c->de_type, c->trim && c->trim_ok, rows, tw, c->fast_hb, s);
@@ -945,7 +957,7 @@ void hq_destroy(hq_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) (void)ncclCommDestroy(c->comm);
-    for (DevBuf* b : {&c->d_k1, &c->d_k2, &c->d_k3, &c->d_absk3, &c->d_R, &c->d_G, &c->d_B, &c->d_rgbx,
+    for (DevBuf* b : {&c->d_k1, &c->d_k2, &c->d_k3, &c->d_absk3, &c->d_vtaps, &c->d_R, &c->d_G, &c->d_B, &c->d_rgbx,
                       &c->d_labL, &c->d_labA, &c->d_labB, &c->d_pal_in, &c->d_pal, &c->d_opp, &c->d_opp16,
                       &c->d_dup, &c->d_pflags, &c->d_lvl1, &c->d_lvl2, &c->d_idx,
                       &c->d_used_mask, &c->d_acc, &c->d_out, &c->d_gen_t, &c->d_taps,
@@ -984,6 +996,19 @@ int hq_set_filters(hq_ctx* c, int taps, const float* k1, const float* k2, const 
     HIP_TRY(c, hipMemcpy(c->d_k2.p, k2, sizeof(float) * 4 * taps, hipMemcpyHostToDevice));
     HIP_TRY(c, hipMemcpy(c->d_k3.p, k3, sizeof(float) * taps, hipMemcpyHostToDevice));
     HIP_TRY(c, hipMemcpy(c->d_absk3.p, absk3, sizeof(float) * taps, hipMemcpyHostToDevice));
+    {  // the tiled generic path's vertical taps per plane (t1.xyz: k1, t2.xyz: k2, t3: |k3|)
+        c->vtap_pitch = (taps + 15) / 16 * 16 + 16;
+        std::vector<float> vt((size_t)kNumFilt * c->vtap_pitch, 0.f);
+        for (int t = 0; t < taps; ++t) {
+            for (int ch = 0; ch < 3; ++ch) {
+                vt[(size_t)ch * c->vtap_pitch + t] = k1[4 * t + ch];
+                vt[(size_t)(3 + ch) * c->vtap_pitch + t] = k2[4 * t + ch];
+            }
+            vt[(size_t)6 * c->vtap_pitch + t] = absk3[t];
+        }
+        HIP_TRY(c, c->d_vtaps.ensure(sizeof(float) * vt.size()));
+        HIP_TRY(c, hipMemcpy(c->d_vtaps.p, vt.data(), sizeof(float) * vt.size(), hipMemcpyHostToDevice));
+    }
     // fast path: the filters centred in the smallest tap bucket that holds them
     // (half-widths up to 24: every dpi / viewing distance of HQ:229-231 up to
     // ~200 dpi at 45 cm); longer filters take the generic path
@@ -1399,7 +1424,7 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
             return fail(c, HQ_ERR_ARG, "grid must be 0, 16, 32 or 64");
         c->G2 = value;
     } else if (!std::strcmp(name, "cost_variant")) {
-        if (value < 0 || value > 1) return fail(c, HQ_ERR_ARG, "cost_variant must be 0 or 1");
+        if (value < 0 || value > 2) return fail(c, HQ_ERR_ARG, "cost_variant must be 0, 1 or 2");
         c->cost_variant = value;
     } else if (!std::strcmp(name, "trim")) {
         c->trim = value != 0;

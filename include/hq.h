@@ -196,7 +196,8 @@ int hq_profile_reset(hq_ctx *ctx);
  * in force when it is enqueued.
  *   "grid"         argmin pruning resolution G2: 0 = exhaustive, 16, 32 (default), 64
  *   "cost_variant" 0 = fast tiled path (default; filters up to halfSize 24), 1 = generic
- *                  two-pass path (any filter length; the fast path's cross-check)
+ *                  two-pass path, LDS-tiled (any filter length; halfSize > 24 takes it),
+ *                  2 = the generic pair per pixel in the reference's summation order
  *   "cost_rows"    fast path tiles: 16 (16 x 128 outputs, default) or 8 (8 x 108)
  *   "cost_tw"      16-row tiles at the default filter width: 128 columns (4 waves,
  *                  default) or 256 (8 waves per workgroup)

@@ -162,7 +162,7 @@ def test_viewing_geometry_vs_oracle(gpu, dpi, vd, half):
     image: device LabRef within 2e-4, every cost within 1e-5 relative of the
     oracle (the bar is 1e-4), indices and used flags bit-exact; the fast path
     (bucketed taps, trimmed or not) equals the generic fp32 two-pass path to
-    1e-6 relative."""
+    1e-6 relative, and the LDS-tiled generic pair the per-pixel one."""
     f = o.design_filters(dpi, vd)
     assert f.half == half
     nt = _threads()
@@ -184,13 +184,15 @@ def test_viewing_geometry_vs_oracle(gpu, dpi, vd, half):
             np.testing.assert_array_equal(used[p], parts["used"])
             np.testing.assert_array_equal(m.getIndices(p), parts["idx"].astype(np.uint8))
         out = {}
-        for variant, trim in ((1, 1), (0, 0), (0, 1)):
+        for variant, trim in ((1, 1), (2, 1), (0, 0), (0, 1)):
             m.setOption("cost_variant", variant)
             m.setOption("trim", trim)
             out[(variant, trim)] = m.computeQuantizationErrorPopulation(pals.reshape(4, -1), 2.0)
         np.testing.assert_array_equal(out[(0, 1)], costs)
         np.testing.assert_allclose(out[(0, 0)], out[(1, 1)], rtol=1e-6)
         np.testing.assert_allclose(out[(0, 1)], out[(1, 1)], rtol=1e-6)
+        # the LDS-tiled generic pair against the per-pixel one (reference order)
+        np.testing.assert_allclose(out[(1, 1)], out[(2, 1)], rtol=1e-6)
         m.close()
 
 
@@ -1089,11 +1091,14 @@ def _pal_with_dark(K, seed):
     return pal
 
 
-@pytest.mark.parametrize("variant", [(0, 16), (0, 8), (1, 16)])
-@pytest.mark.parametrize("case", ["case_64x48_k16", "case_97x53_k64", "dark_256_9660", "dark_193x131_7245"])
+@pytest.mark.parametrize("variant", [(0, 16), (0, 8), (1, 16), (2, 16)])
+@pytest.mark.parametrize("case", ["case_64x48_k16", "case_97x53_k64", "dark_256_9660", "dark_193x131_7245",
+                                  "dark_256_30050"])
 def test_pixel_errors_vs_oracle(gpu, case, variant):
     """(cost_variant, cost_rows): the default 16 x 128 tiles (cost16w), the 8 x 108
-    tiles (cost_mfma) and the generic two-pass path.  Every pixel's dE -- border
+    tiles (cost_mfma), the LDS-tiled generic pair and the per-pixel generic pair
+    (the reference's summation order); 300 dpi / 50 cm (half 51) takes the
+    generic path whatever the variant.  Every pixel's dE -- border
     pixels (reflection, CL:256-263), pixels in the linear Lab segment, edge and
     partial tiles -- within 2e-5 absolute of the oracle's error image (same
     LabRef on both sides), and the indices bit-exact."""
@@ -1107,7 +1112,7 @@ def test_pixel_errors_vs_oracle(gpu, case, variant):
     else:
         dims, geo = case.split("_")[1], case.split("_")[2]
         w, h = (int(v) for v in dims.split("x")) if "x" in dims else (int(dims), int(dims))
-        dpi, vd = (96, 60.0) if geo == "9660" else (72, 45.0)
+        dpi, vd = {"9660": (96, 60.0), "7245": (72, 45.0), "30050": (300, 50.0)}[geo]
         f = o.design_filters(dpi, vd)
         R, G, B = _dark_case(w, h, seed=w + h)
         pals = [_pal_with_dark(64, 900 + w), _pal_with_dark(256, 901 + w)]
