@@ -180,6 +180,9 @@ def main():
     ap.add_argument("--shard-of", type=int, default=0, metavar="N",
                     help="experiment: run rank 0's row block of an N-way split on one GPU, "
                          "no collective (per-rank step time at N GPUs)")
+    ap.add_argument("--split", choices=["rows", "palettes"], default="rows",
+                    help="N > 1: row-block shards + one all-reduce (default), or each rank the whole "
+                         "image and P/N palettes + one all-gather (SURVEY 8e, large populations)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-full-search", action="store_true",
@@ -215,7 +218,10 @@ def main():
         m.setOption(k, int(v))
     sa_device = int(opts.get("sa_device", 1))
     R, G, B = synthetic_planes(W, H, seed=args.seed)
-    r0, r1 = hqd.shard_rows(H, args.shard_of if args.shard_of > 0 else world, rank)
+    psplit = args.split == "palettes" and world > 1
+    if psplit:
+        m.setOption("palette_split", 1)
+    r0, r1 = (0, H) if psplit else hqd.shard_rows(H, args.shard_of if args.shard_of > 0 else world, rank)
     _lib.check(lib.hq_set_image_planar_shard(m.ctx, _lib.fptr(R), _lib.fptr(G), _lib.fptr(B), W, H,
                                              _lib.fptr(sp.illuminant), r0, r1), m.ctx)
     del R, G, B
@@ -327,11 +333,12 @@ def main():
     cost_ms = prof["cost"][0]
     flops_nominal = 7 * 2 * (2 * half + 1) * 2 + 40
     flops_exec = 2 * 2 * taps_exec + 40
-    alg_flops = n_own * P * flops_nominal
-    exec_flops = n_own * P * flops_exec
+    P_dev = P // world if psplit else P  # palettes one device's cost kernel evaluates
+    alg_flops = n_own * P_dev * flops_nominal
+    exec_flops = n_own * P_dev * flops_exec
     achieved_tf = alg_flops / (cost_ms * 1e-3) / 1e12 if cost_ms > 0 else 0.0
     exec_tf = exec_flops / (cost_ms * 1e-3) / 1e12 if cost_ms > 0 else 0.0
-    alg_bytes = n_own * (12 + P * (1 if args.K <= 256 else 2 if chunked else 4))
+    alg_bytes = n_own * (12 + P_dev * (1 if args.K <= 256 else 2 if chunked else 4))
     hbm_gbs = alg_bytes / (cost_ms * 1e-3) / 1e9 if cost_ms > 0 else 0.0
     traffic = measured_traffic(W, args.K, P, args.grid, world, kernel.split("+")[0],
                                args.dpi, args.distance)
@@ -353,7 +360,8 @@ def main():
         "config": {"workload": f"SWASA search iteration, {W}x{H} RGB image, K={args.K}, "
                                f"population P={P} palettes per step ({cfg_name})",
                    "image": f"{W}x{H}", "K": args.K, "population": P,
-                   "parallelism": f"row-block x{world} + RCCL all-reduce" if world > 1 else "1 GPU",
+                   "parallelism": (f"palette split x{world} + RCCL all-gather" if psplit else
+                                   f"row-block x{world} + RCCL all-reduce" if world > 1 else "1 GPU"),
                    "argmin_grid": args.grid,
                    **({"dpi": args.dpi, "distance_cm": args.distance}
                       if (args.dpi, args.distance) != (72, 45.0) else {}),

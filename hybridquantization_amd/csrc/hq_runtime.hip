@@ -147,6 +147,11 @@ struct hq_ctx {
                                    // thread a grid-stride pixel sequence
     int assign_res[5] = {};   // [NG]
     int assign_res_chunked = 0;  // the chunk-combining forms (NG = 4)
+    int psplit = 0;        // with a communicator of N ranks and the whole image on every rank: rank r
+                           // evaluates palettes [r P/N, (r+1) P/N), then one all-gather (option
+                           // "palette_split"; SURVEY 8e's split of large populations)
+    int slice_ranks = 1, slice_rank = 0;  // test only: the same slice without a communicator
+    int slice_lo = 0, slice_n = 0;        // the last evaluation's palettes held on this device
     int chunked = 1;       // 256 < K <= 4096: palettes as 256-colour chunks through the grid and
                            // tiled kernels (option "chunked"; 0 = the exhaustive K > 256 path)
     int img_u8_path = 1;   // assign reads the packed 8-bit image when there is one (option 'img_u8')
@@ -452,13 +457,15 @@ uint32_t* used_set(hq_ctx* c, int par, int Ps) {
     return c->d_used_mask.as<uint32_t>() + (size_t)par * kUsedSlots * used_stride(Ps);
 }
 
-GridArgs grid_args(hq_ctx* c, int P, int K) {
+GridArgs grid_args(hq_ctx* c, int P, int K, int so = 0) {
     const int G2 = c->G2 > 0 ? c->G2 : 4;
     const int G1 = G2 / 4;
     // (P = sub-palettes; the counters of set c->acc_par)
     const int nch = c->nch_cur;
-    return GridArgs{c->d_pal.as<float4>(), c->d_dup.as<uint8_t>(), c->d_pflags.as<int>(),
-                    c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(), used_set(c, c->acc_par, P),
+    // (so: the first of the P sub-palettes in the prepared tables, a palette split's slice)
+    return GridArgs{c->d_pal.as<float4>() + (int64_t)so * kMaxK, c->d_dup.as<uint8_t>() + (int64_t)so * kMaxK,
+                    c->d_pflags.as<int>() + so, c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(),
+                    used_set(c, c->acc_par, P),
                     used_stride(P), K, G1,
                     round_up((int64_t)G1 * G1 * G1 * 32, 256), round_up((int64_t)G2 * G2 * G2 * kL2Line, 256),
                     acc_set(c, c->acc_par, P / nch), P / nch, nch};
@@ -469,7 +476,7 @@ GridArgs grid_args(hq_ctx* c, int P, int K) {
 // u16 (chunked palettes) or u32, idx_bytes) with c->g.idx_pitch elements per palette, opponent tables of
 // opp_stride entries per palette in d_opp.  The cost events time all P pairs.
 int enqueue_generic_cost(hq_ctx* c, int P, const void* idx_base, int idx_bytes, int opp_stride,
-                         const hipEvent_t* ev) {
+                         const hipEvent_t* ev, int p_off = 0) {
     const Geom& g = c->g;
     hipStream_t s = c->stream;
     HIP_TRY(c, c->d_gen_t.ensure(sizeof(float) * 7 * (size_t)g.n_ext));
@@ -478,7 +485,7 @@ int enqueue_generic_cost(hq_ctx* c, int P, const void* idx_base, int idx_bytes, 
     for (int p = 0; p < P; ++p) {
         GenArgs gn{};
         gn.idx = static_cast<const char*>(idx_base) + (int64_t)p * g.idx_pitch * idx_bytes;
-        gn.opp = c->d_opp.as<float4>() + (int64_t)p * opp_stride;
+        gn.opp = c->d_opp.as<float4>() + (int64_t)(p_off + p) * opp_stride;
         gn.k1 = c->d_k1.as<float>();
         gn.k2 = c->d_k2.as<float>();
         gn.k3 = c->d_k3.as<float>();
@@ -534,6 +541,8 @@ int enqueue_wide(hq_ctx* c, int P, int K, const hipEvent_t* ev) {
     HIP_TRY(c, ef);
     if (c->comm)
         NCCL_TRY(c, ncclAllReduce(c->d_out.p, c->d_out.p, (size_t)P * (1 + K), ncclFloat64, ncclSum, c->comm, s));
+    c->slice_lo = 0;
+    c->slice_n = P;
     c->last_P = P;
     c->K_cur = K;
     c->last_nch = 1;
@@ -544,14 +553,38 @@ int enqueue_wide(hq_ctx* c, int P, int K, const hipEvent_t* ev) {
 // 256 nch): the grid and assign run on P nch sub-palettes of 256 colours (d_pal
 // etc. hold them, prep_palette made them), assign combines them into 16-bit
 // indices, the cost kernel reads those with a 256 nch-entry table.
+// The palettes of a P-palette population this device evaluates: a palette
+// split (psplit with a communicator of N ranks, or the test-only slice options)
+// takes [r P/N, (r+1) P/N) on the whole image; anything else all P.
+int palette_slice(hq_ctx* c, int P, int* lo, int* n) {
+    int R = 1, r = 0;
+    if (c->psplit && c->comm) R = c->nranks, r = c->rank;
+    else if (c->slice_ranks > 1) R = c->slice_ranks, r = c->slice_rank;
+    *lo = 0;
+    *n = P;
+    if (R == 1) return HQ_OK;
+    if (P % R) return fail(c, HQ_ERR_ARG, "palette split: population %d not divisible by %d ranks", P, R);
+    if (c->g.r0 != 0 || c->g.r1 != c->g.H)
+        return fail(c, HQ_ERR_STATE, "palette split: every rank needs the whole image (hq_set_image)");
+    *n = P / R;
+    *lo = r * *n;
+    return HQ_OK;
+}
+
 // Each evaluation takes the other counter set than the last one (build_grid
 // zeroes it), so an accept step can read the last set while the next is filled.
 int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = false) {
     const Geom& g = c->g;
     hipStream_t s = c->stream;
-    const int nch = c->nch_cur, Ps = P * nch, Ks = nch > 1 ? kMaxK : K;
+    const int nch = c->nch_cur, Ks = nch > 1 ? kMaxK : K;
+    // the palettes this device evaluates: all, or a palette split's slice [lo, lo + Pl)
+    int lo = 0, Pl = P;
+    if (int rc = palette_slice(c, P, &lo, &Pl)) return rc;
+    const int Ps = Pl * nch, so = lo * nch;  // sub-palettes, the first one's index
+    if (Pl < P && !c->comm)  // test-only slice: the other palettes' rows read as zero
+        HIP_TRY(c, hipMemsetAsync(c->d_out.p, 0, sizeof(double) * (size_t)P * (1 + K), s));
     c->acc_par ^= 1;
-    const GridArgs ga = grid_args(c, Ps, Ks);
+    const GridArgs ga = grid_args(c, Ps, Ks, so);
     auto timed = [&](int slot) {
         if (ev) set_launch_events(ev[2 * slot], ev[2 * slot + 1]);
     };
@@ -563,12 +596,12 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
         HIP_TRY(c, e);
     } else {
         HIP_TRY(c, hipMemsetAsync(ga.used_glob, 0, sizeof(uint32_t) * kUsedSlots * (size_t)used_stride(Ps), s));
-        HIP_TRY(c, hipMemsetAsync(ga.acc_zero, 0, sizeof(uint64_t) * acc_words(P), s));
+        HIP_TRY(c, hipMemsetAsync(ga.acc_zero, 0, sizeof(uint64_t) * acc_words(Pl), s));
     }
     const int nblocks = assign_blocks(c, Ps);
     AssignArgs aa{c->d_R.as<float>(), c->d_G.as<float>(), c->d_B.as<float>(),
-                  c->img_u8 && c->img_u8_path ? c->d_rgbx.as<uint32_t>() : nullptr, c->d_pal.as<float4>(),
-                  c->d_pflags.as<int>(), c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(),
+                  c->img_u8 && c->img_u8_path ? c->d_rgbx.as<uint32_t>() : nullptr, ga.pal, ga.pflags,
+                  c->d_lvl1.as<uint8_t>(), c->d_lvl2.as<uint8_t>(),
                   c->d_idx.as<uint8_t>(), ga.used_glob, used_stride(Ps), g.n_ext, g.idx_pitch,
                   ga.lvl1_pitch, ga.lvl2_gstride, Ks, c->G2, nblocks};
     if (nch > 1) {
@@ -587,14 +620,14 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
     CostArgs ca{};
     if (fast) {
         ca.idx = nch > 1 ? c->d_idx16.as<uint8_t>() : c->d_idx.as<uint8_t>();
-        ca.opp16 = c->d_opp16.as<uint4>();
+        ca.opp16 = c->d_opp16.as<uint4>() + (int64_t)so * kMaxK;
         ca.taps = c->d_taps.p;
         ca.vfrag16 = c->d_vfrag16.as<uint4>();
         ca.labL = c->d_labL.as<float>();
         ca.labA = c->d_labA.as<float>();
         ca.labB = c->d_labB.as<float>();
         ca.acc = ga.acc_zero;
-        ca.acc_P = P;
+        ca.acc_P = Pl;
         ca.acc_p0 = 0;
         ca.g = g;
         ca.K = K;
@@ -609,26 +642,32 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
     HIP_TRY(c, e);
     if (fast) {
         timed(2);
-        e = nch > 1 ? launch_cost_chunked(ca, P, nch, c->de_type, c->trim && c->trim_ok, s)
-                    : launch_cost_fast(ca, P, c->de_type, c->trim && c->trim_ok, rows, tw, c->fast_hb, s);
+        e = nch > 1 ? launch_cost_chunked(ca, Pl, nch, c->de_type, c->trim && c->trim_ok, s)
+                    : launch_cost_fast(ca, Pl, c->de_type, c->trim && c->trim_ok, rows, tw, c->fast_hb, s);
         untimed();
         HIP_TRY(c, e);
     } else {
-        int rc = nch > 1 ? enqueue_generic_cost(c, P, c->d_idx16.p, 2, nch * kMaxK, ev)
-                         : enqueue_generic_cost(c, P, c->d_idx.p, 1, kMaxK, ev);
+        int rc = nch > 1 ? enqueue_generic_cost(c, Pl, c->d_idx16.p, 2, nch * kMaxK, ev, lo)
+                         : enqueue_generic_cost(c, Pl, c->d_idx.p, 1, kMaxK, ev, lo);
         if (rc) return rc;
     }
     if (!fold) {  // (a folding search's accept step reads the sums itself)
-        FinalizeArgs fa{ga.acc_zero, ga.used_glob, used_stride(Ps), c->d_out.as<double>(), P, K, nullptr, 8 * nch};
+        FinalizeArgs fa{ga.acc_zero, ga.used_glob, used_stride(Ps), c->d_out.as<double>() + (int64_t)lo * (1 + K),
+                        Pl, K, nullptr, 8 * nch};
         timed(3);
-        const hipError_t ef = launch_finalize(fa, P, s);
+        const hipError_t ef = launch_finalize(fa, Pl, s);
         untimed();
         HIP_TRY(c, ef);
     }
-    if (c->comm) {  // also with one rank (a no-op copy), so that path is exercised on one GPU
+    if (c->comm && c->psplit) {  // every rank's slice to every rank (in place; one rank: a no-op)
+        NCCL_TRY(c, ncclAllGather(c->d_out.as<double>() + (int64_t)lo * (1 + K), c->d_out.p, (size_t)Pl * (1 + K),
+                                  ncclFloat64, c->comm, s));
+    } else if (c->comm) {  // also with one rank (a no-op copy), so that path is exercised on one GPU
         NCCL_TRY(c, ncclAllReduce(c->d_out.p, c->d_out.p, (size_t)P * (1 + K), ncclFloat64, ncclSum,
                                   c->comm, s));
     }
+    c->slice_lo = lo;
+    c->slice_n = Pl;
     c->last_P = P;
     c->K_cur = K;
     c->last_nch = nch;
@@ -819,6 +858,8 @@ int device_search_create(hq_ctx* c, const hq_swasa_params* params, int K, uint64
     // no communicator: nothing has to see the finalized sums, so the accept
     // step reads the fixed-point sums itself (one launch less per iteration)
     s->fold = !c->comm;
+    if (c->slice_ranks > 1 && !c->comm)
+        return fail(c, HQ_ERR_STATE, "palette slice without a communicator (test option): no search");
     s->pol = new Swasa(*params, seed);
     const NchScope scope(c, s->nch);
     int rc = ensure_population(c, P, K);
@@ -1100,8 +1141,8 @@ int hq_eval_population(hq_ctx* c, const float* palettes, int P, int K, float del
     // IM:712: averageArray(error) + computePenalty(used).  After an all-reduce
     // the used entries count the ranks using colour k; unused <=> 0.
     const bool full = c->g.r0 == 0 && c->g.r1 == c->g.H;
-    if (!full && !(c->comm && c->nranks > 1))
-        return fail(c, HQ_ERR_STATE, "sharded context without a communicator: use "
+    if ((!full || c->slice_ranks > 1) && !(c->comm && c->nranks > 1))
+        return fail(c, HQ_ERR_STATE, "sharded context or palette slice without a communicator: use "
                                      "hq_eval_population_partial");
     const double n_total = (double)c->g.W * (double)c->g.H;
     for (int p = 0; p < P; ++p) {
@@ -1120,6 +1161,9 @@ int hq_eval_population(hq_ctx* c, const float* palettes, int P, int K, float del
 int hq_get_indices(hq_ctx* c, int p, uint8_t* idx) {
     if (!c || !idx) return HQ_ERR_ARG;
     if (p < 0 || p >= c->last_P) return fail(c, HQ_ERR_ARG, "palette %d not in last population", p);
+    if (p < c->slice_lo || p >= c->slice_lo + c->slice_n)
+        return fail(c, HQ_ERR_ARG, "palette %d was evaluated on another rank (palette split)", p);
+    p -= c->slice_lo;
     if (c->K_cur > kMaxK)
         return fail(c, HQ_ERR_STATE, "K=%d > 256: indices are 32-bit (hq_get_indices32)", c->K_cur);
     int rc = bind(c);
@@ -1135,6 +1179,9 @@ int hq_get_indices(hq_ctx* c, int p, uint8_t* idx) {
 int hq_get_indices32(hq_ctx* c, int p, uint32_t* idx) {
     if (!c || !idx) return HQ_ERR_ARG;
     if (p < 0 || p >= c->last_P) return fail(c, HQ_ERR_ARG, "palette %d not in last population", p);
+    if (p < c->slice_lo || p >= c->slice_lo + c->slice_n)
+        return fail(c, HQ_ERR_ARG, "palette %d was evaluated on another rank (palette split)", p);
+    p -= c->slice_lo;
     int rc = bind(c);
     if (rc) return rc;
     const Geom& g = c->g;
@@ -1163,6 +1210,9 @@ int hq_get_pixel_errors(hq_ctx* c, int p, float* err) {
     if (!c || !err) return HQ_ERR_ARG;
     if (!c->pixel_err) return fail(c, HQ_ERR_STATE, "option pixel_err is off");
     if (p < 0 || p >= c->last_P) return fail(c, HQ_ERR_ARG, "palette %d not in last population", p);
+    if (p < c->slice_lo || p >= c->slice_lo + c->slice_n)
+        return fail(c, HQ_ERR_ARG, "palette %d was evaluated on another rank (palette split)", p);
+    p -= c->slice_lo;
     if (c->d_pixerr.bytes < sizeof(float) * (size_t)c->last_P * (size_t)c->g.W * (c->g.r1 - c->g.r0))
         return fail(c, HQ_ERR_STATE, "pixel_err was set after the last evaluation");
     int rc = bind(c);
@@ -1439,6 +1489,13 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
         c->sa_device = value != 0;
     } else if (!std::strcmp(name, "shard_solo")) {
         c->shard_solo = value != 0;
+    } else if (!std::strcmp(name, "palette_split")) {
+        c->psplit = value != 0;
+    } else if (!std::strcmp(name, "slice_ranks")) {
+        if (value < 1) return fail(c, HQ_ERR_ARG, "slice_ranks must be >= 1");
+        c->slice_ranks = value;
+    } else if (!std::strcmp(name, "slice_rank")) {
+        c->slice_rank = value;
     } else if (!std::strcmp(name, "chunked")) {
         c->chunked = value != 0;
     } else if (!std::strcmp(name, "pixel_err")) {

@@ -213,7 +213,13 @@ int hq_profile_reset(hq_ctx *ctx);
  *   "shard_solo"   experiment only: let a row-block shard run hq_search_* without a
  *                  communicator (its own partial costs; per-rank timing at N GPUs)
  *   "pixel_err"    test only: 1 = the cost kernels also write the per-pixel dE
- *                  (hq_get_pixel_errors) */
+ *                  (hq_get_pixel_errors)
+ *   "palette_split" 1 = with a communicator of N ranks, each holding the whole image
+ *                  (hq_set_image): rank r evaluates palettes [r P/N, (r+1) P/N) and one
+ *                  all-gather gives every rank all P results (SURVEY 8e's split of large
+ *                  populations; P must divide by N); 0 (default) = row-block shards
+ *   "slice_ranks", "slice_rank"  test only: the same palette slice without a
+ *                  communicator (hq_eval_population_partial: other rows read 0) */
 int hq_set_option(hq_ctx *ctx, const char *name, int value);
 
 #ifdef __cplusplus

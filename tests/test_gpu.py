@@ -706,10 +706,12 @@ def test_device_search_matches_host_driven(gpu, filt, P, K):
     m.close()
 
 
-def test_device_search_with_single_rank_comm(gpu, filt):
+@pytest.mark.parametrize("split", [0, 1])
+def test_device_search_with_single_rank_comm(gpu, filt, split):
     """The multi-GPU search loop on one GPU: with libhq's RCCL communicator the
-    all-reduce sits between finalize and sa_step in every iteration; with one
-    rank the trajectory must be the one without a communicator."""
+    all-reduce (split 0: row blocks) or the all-gather (split 1: option
+    palette_split) sits between finalize and sa_step in every iteration; with
+    one rank the trajectory must be the one without a communicator."""
     import ctypes as C
     w, h, K, P = 80, 72, 24, 4
     R, G, B = o.synthetic_image(w, h, seed=12)
@@ -719,6 +721,7 @@ def test_device_search_with_single_rank_comm(gpu, filt):
         m = hq.ImageManipulation(device=gpu)
         hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
         m.setImage(o.inline_rgba(R, G, B).reshape(-1), None, w, filt.illum)
+        m.setOption("palette_split", split)
         if comm:
             m.initComm(1, 0, hq.ImageManipulation.commUniqueId())
         sw = hq.SWASA(population=P, imax=30, seed=21, t0=0.05)
@@ -737,6 +740,55 @@ def test_device_search_with_single_rank_comm(gpu, filt):
     assert res[0][2] == res[1][2] == 30
     assert res[0][1] == res[1][1]
     np.testing.assert_array_equal(res[0][0], res[1][0])
+
+
+@pytest.mark.parametrize("K,P,ranks", [(64, 8, 2), (64, 8, 4), (256, 12, 3), (600, 4, 2)])
+def test_palette_slices_sum_to_full(gpu, filt, K, P, ranks):
+    """The palette split (option palette_split with a communicator):
+    rank r evaluates palettes [r P/N, (r+1) P/N) of the whole image.  Here the
+    ranks are contexts on one GPU with the test-only slice options: each slice's
+    rows of hq_eval_population_partial equal the full evaluation's bit for bit
+    (sums and used flags; the other rows read 0), and so do the indices of the
+    slice's palettes; K = 600 runs chunked palettes."""
+    w, h = 160, 120
+    R, G, B = o.synthetic_image(w, h, seed=K + P)
+    rgba = o.inline_rgba(R, G, B).reshape(-1)
+    pals = np.stack([o.synthetic_palette(K, 40 + p) for p in range(P)]).reshape(P, -1)
+    lib = hq.load()
+
+    def run(slice_rank):
+        m = hq.ImageManipulation(device=gpu)
+        hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
+        m.setImage(rgba, None, w, filt.illum)
+        if slice_rank is not None:
+            m.setOption("slice_ranks", ranks)
+            m.setOption("slice_rank", slice_rank)
+        out = np.zeros(P * (1 + K))
+        hq._lib.check(lib.hq_eval_population_partial(m.ctx, hq._lib.fptr(np.ascontiguousarray(pals)), P, K,
+                                                     out.ctypes.data_as(hq._lib._d)), m.ctx)
+        idx = {}
+        n = P // ranks
+        lo = 0 if slice_rank is None else slice_rank * n
+        for p in range(P):
+            if slice_rank is None or lo <= p < lo + n:
+                idx[p] = m.getIndices32(p)
+            else:
+                with pytest.raises(hq.HQError):
+                    m.getIndices32(p)
+        m.close()
+        return out.reshape(P, 1 + K), idx
+
+    full, idx_full = run(None)
+    n = P // ranks
+    for r in range(ranks):
+        part, idx = run(r)
+        rows = slice(r * n, (r + 1) * n)
+        np.testing.assert_array_equal(part[rows], full[rows])
+        others = np.ones(P, bool)
+        others[rows] = False
+        assert not part[others].any()
+        for p, v in idx.items():
+            np.testing.assert_array_equal(v, idx_full[p])
 
 
 # ---------------------------------------------------------------------------
