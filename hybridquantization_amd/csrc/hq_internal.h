@@ -60,11 +60,7 @@ struct PaletteArgs {
     int K;
 };
 
-// assign: one pixel per thread per 256-thread chunk, with one resident round
-// of workgroups, makes each thread's pixel sequence a grid stride: every thread
-// gets the same number of pixels +-1 (512-row shard 0.1306 -> 0.1261 ms per
-// step vs 4 pixels per chunk at 16 workgroups per CU; 4096^2 unchanged).
-constexpr int kSaMaxP = 64;        // device-resident SWASA: largest population
+constexpr int kSaMaxP = 64;        // device-resident SWASA: largest population (sub-palettes)
 // Used-colour bits are kept in kUsedSlots copies, used_stride(P) words apart
 // (256-B multiples): assign's workgroups OR theirs into copy blockIdx & 7, the
 // readers OR the copies.  One copy took every workgroup's atomic at the end of
