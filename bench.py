@@ -220,6 +220,7 @@ def main():
     R, G, B = synthetic_planes(W, H, seed=args.seed)
     psplit = args.split == "palettes" and world > 1
     if psplit:
+        hqd.palette_slice(args.population, world, rank)  # (raises unless the population divides)
         m.setOption("palette_split", 1)
     r0, r1 = (0, H) if psplit else hqd.shard_rows(H, args.shard_of if args.shard_of > 0 else world, rank)
     _lib.check(lib.hq_set_image_planar_shard(m.ctx, _lib.fptr(R), _lib.fptr(G), _lib.fptr(B), W, H,
@@ -333,7 +334,7 @@ def main():
     cost_ms = prof["cost"][0]
     flops_nominal = 7 * 2 * (2 * half + 1) * 2 + 40
     flops_exec = 2 * 2 * taps_exec + 40
-    P_dev = P // world if psplit else P  # palettes one device's cost kernel evaluates
+    P_dev = hqd.palette_slice(P, world, rank)[1] if psplit else P  # palettes one device's cost kernel evaluates
     alg_flops = n_own * P_dev * flops_nominal
     exec_flops = n_own * P_dev * flops_exec
     achieved_tf = alg_flops / (cost_ms * 1e-3) / 1e12 if cost_ms > 0 else 0.0

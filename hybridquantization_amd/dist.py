@@ -1,10 +1,12 @@
-"""Control plane of the row-block sharded evaluation.
+"""Control plane of the sharded evaluation.
 
 One process per GPU.  torch.distributed (gloo) carries only control data:
 the 128-byte RCCL unique id from rank 0 to every rank, and the MAX of the
-ranks' timings.  The data path -- one fp64 all-reduce of P * (1 + K) partial
-sums per SWASA iteration -- runs inside libhq on its own RCCL communicator
-over xGMI.  bench.py and the multi-process tests call these same functions.
+ranks' timings.  The data path runs inside libhq on its own RCCL communicator
+over xGMI: per SWASA iteration either one fp64 all-reduce of P * (1 + K)
+partial sums (row-block split) or one all-gather of each rank's P / N result
+rows (palette split, option "palette_split").  bench.py and the
+multi-process tests call these same functions.
 """
 
 from __future__ import annotations
@@ -15,6 +17,31 @@ def shard_rows(H: int, world: int, rank: int) -> tuple[int, int]:
     if world < 1 or not 0 <= rank < world:
         raise ValueError(f"rank {rank} of world {world}")
     return rank * H // world, (rank + 1) * H // world
+
+
+def palette_slice(P: int, world: int, rank: int) -> tuple[int, int]:
+    """Palettes [lo, lo + n) that `rank` evaluates under the palette split
+    (hq_runtime.hip palette_slice): an equal slice of the population, every
+    rank holding the whole image; P must be a multiple of the world size."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"rank {rank} of world {world}")
+    if P % world:
+        raise ValueError(f"palette split: population {P} not divisible by {world} ranks")
+    n = P // world
+    return rank * n, n
+
+
+def allgather_rows(dist, rows, world: int):
+    """The palette split's exchange: every rank's [n, 1 + K] result rows,
+    concatenated in rank order ([P, 1 + K]) -- ncclAllGather in libhq, here
+    over gloo for tests."""
+    import numpy as np
+    import torch
+
+    t = torch.from_numpy(np.ascontiguousarray(rows, dtype=np.float64)).clone()
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return torch.cat(out).numpy()
 
 
 def broadcast_unique_id(dist, rank: int, make_id) -> bytes:

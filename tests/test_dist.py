@@ -1,8 +1,11 @@
-"""Multi-process (gloo, world size 2) test of the row-block sharded evaluation
- on CPU: each rank evaluates its shard with halo rows through the
-oracle's shard restatement, partials are all-reduced, and the result must equal
-the single-process full-image cost.  This is the same decomposition libhq's
-hq_eval_population_partial + RCCL all-reduce performs on the GPUs."""
+"""Multi-process (gloo, world size 2) tests of the two sharded evaluations
+ on CPU.  Row-block split: each rank evaluates its shard with halo
+rows through the oracle's shard restatement, partials are all-reduced, and the
+result must equal the single-process full-image cost -- the decomposition
+libhq's hq_eval_population_partial + RCCL all-reduce performs on the GPUs.
+Palette split (option "palette_split"): each rank evaluates its slice of the
+population on the whole image, the result rows are all-gathered in rank order,
+and must equal the full population's rows -- libhq's ncclAllGather."""
 
 import os
 import socket
@@ -84,6 +87,66 @@ def test_row_block_shards_allreduce_matches_full(world):
         # cost assembled like hq_eval_population: mean + delta * #unused
         c = red[p, 0] / (W * H) + 2.0 * np.count_nonzero(red[p, 1:] == 0)
         assert abs(c - cost) <= 1e-6 * abs(cost)
+
+
+def _palette_worker(rank, world, port, out):
+    import torch  # noqa: F401
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hybridquantization_amd import dist as hqd
+
+    f, rgb3, lab, pals = _inputs4()
+    rgba = o.inline_rgba(rgb3[:, 0], rgb3[:, 1], rgb3[:, 2])
+    lo, n = hqd.palette_slice(len(pals), world, rank)
+    rows = np.zeros((n, 1 + K))
+    for j in range(n):
+        _, parts = c_oracle.eval_palette(rgba, lab, pals[lo + j], f, W, return_parts=True)
+        rows[j, 0] = parts["err_sum"]
+        rows[j, 1:] = parts["used"]
+    full = hqd.allgather_rows(dist, rows, world)
+    if rank == 0:
+        out.put(full)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _inputs4():
+    f, rgb3, lab, _ = _inputs()
+    return f, rgb3, lab, [o.synthetic_palette(K, 80 + p) for p in range(4)]
+
+
+@pytest.mark.parametrize("world", [2])
+def test_palette_split_allgather_matches_full(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_palette_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    f, rgb3, lab, pals = _inputs4()
+    rgba = o.inline_rgba(rgb3[:, 0], rgb3[:, 1], rgb3[:, 2])
+    assert got.shape == (len(pals), 1 + K)
+    for p, pal in enumerate(pals):  # rank order = population order, bitwise
+        _, parts = c_oracle.eval_palette(rgba, lab, pal, f, W, return_parts=True)
+        assert got[p, 0] == parts["err_sum"]
+        np.testing.assert_array_equal(got[p, 1:], np.asarray(parts["used"], np.float64))
+
+
+def test_palette_slice_bounds():
+    from hybridquantization_amd.dist import palette_slice
+
+    assert [palette_slice(64, 8, r) for r in (0, 3, 7)] == [(0, 8), (24, 8), (56, 8)]
+    assert palette_slice(4, 1, 0) == (0, 4)
+    with pytest.raises(ValueError):
+        palette_slice(6, 4, 0)  # libhq: HQ_ERR_ARG, population not divisible
+    with pytest.raises(ValueError):
+        palette_slice(8, 2, 2)
 
 
 def test_shard_partial_single_process_identity():
