@@ -325,7 +325,8 @@ def main():
                or (chunked and (hb != 10 or rows != 16 or tw_opt != 128)))
     trim_w = {10: (3, 4, 5), 15: (4, 5, 7), 19: (5, 7, 9), 24: (6, 9, 12)}
     if generic:
-        kernel = "gen_hpass_kernel+gen_vpass_kernel"
+        # cost_variant 2: the per-pixel pair; otherwise the LDS-tiled pair
+        kernel = "gen_hpass_kernel+gen_vpass_kernel" if variant == 2 else "gen_hrow_kernel+gen_vtile_kernel"
         taps_exec = 7 * (2 * half + 1)
     else:
         kernel = "cost_mfma_kernel" if rows == 8 and hb == 10 else "cost16w_kernel"

@@ -167,7 +167,7 @@ __device__ __forceinline__ void argmin_group(float r, float g, float b, const L2
 #ifdef HQ_ABL_NOLOOP  // timing ablation (wrong results): no candidate walk
     maxc = 1;
 #endif
-    if (__any(maxc > 1)) {
+    if (__builtin_amdgcn_ballot_w64(maxc > 1)) {  // (no bool -> VGPR -> compare)
         const f32x2 rg = {r, g};
         const char* base = reinterpret_cast<const char*>(s_pal);
         auto at = [&](int q, uint32_t off) {
@@ -194,7 +194,7 @@ __device__ __forceinline__ void argmin_group(float r, float g, float b, const L2
         }
 #pragma unroll
         for (int i = 1; i < kL2Cap; ++i) {
-            if (!__any(i < maxc)) break;
+            if (!__builtin_amdgcn_ballot_w64(i < maxc)) break;
 #pragma unroll
             for (int q = 0; q < NG; ++q) {
                 const uint32_t ak = an[q][0];
@@ -241,7 +241,7 @@ __device__ __forceinline__ void argmin_group(float r, float g, float b, const L2
         if (near[q]) atomicAdd(&g_asg_slow[0], 1u);
         if (slow[q]) atomicAdd(&g_asg_slow[1], 1u);
 #endif
-        if (__any(s))
+        if (__builtin_amdgcn_ballot_w64(s))
             out[q] = argmin_fix(r, g, b, s, out[q], E[q], inside && !exh_pal[q], s_pal + q * kMaxK,
                                 lvl1 + (int64_t)(p0 + q) * lvl1_pitch, G2, K);
     }
@@ -313,7 +313,10 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
     // [NG][kMaxK]: a fixed palette stride, so each palette's base folds into the
     // ds_read_b128 offset field and a candidate's address is its byte << 4
     __shared__ __attribute__((aligned(16))) float4 s_pal[NG * kMaxK];
-    __shared__ uint32_t s_used[NG][8];
+    // used colours: one byte per colour, set by plain byte stores (a read-test-or
+    // of 32-bit words cost an LDS round trip and 5 VALU per pixel and palette;
+    // assign 0.1597 -> 0.1578 ms at C3); words by ballot at the flush
+    __shared__ __attribute__((aligned(16))) uint8_t s_usedb[NG][kMaxK];
     const int w = xcd_remap(blockIdx.x, a.nblocks * ngroups);
     // group-major: after the relabelling an XCD's contiguous range of
     // workgroups covers one or two groups, so its L2 holds those groups' level-2
@@ -456,7 +459,7 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
 #pragma unroll
     for (int pp = 0; pp < NG; ++pp)
         s_pal[pp * kMaxK + tid] = a.pal[(int64_t)(p0 + pp) * kMaxK + min(tid, a.K - 1)];
-    if (tid < 8 * NG) s_used[tid >> 3][tid & 7] = 0;
+    if (tid < 64 * NG) reinterpret_cast<uint32_t*>(&s_usedb[0][0])[tid] = 0u;
     __syncthreads();
 #ifdef HQ_ASSIGN_TIMING
     t_fill = wall_clock64();
@@ -494,8 +497,7 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
                 // ~0.5-1% per evaluation)
                 if (q < n_ext) {
                     __builtin_nontemporal_store((uint8_t)k, idx_base[pp] + q);
-                    const uint32_t bit = 1u << (k & 31);
-                    if (!(s_used[pp][k >> 5] & bit)) atomicOr(&s_used[pp][k >> 5], bit);
+                    s_usedb[pp][k] = 1;
                 }
             }
         } else {
@@ -523,8 +525,7 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
                     if constexpr (PASS == 1 || PASS == 2)
                         if (win) a.dist[pal * a.idx_pitch + q] = best;
                     if constexpr (PASS == 0) {
-                        const uint32_t bit = 1u << (k & 31);
-                        if (!(s_used[s0 + bc][k >> 5] & bit)) atomicOr(&s_used[s0 + bc][k >> 5], bit);
+                        s_usedb[s0 + bc][k] = 1;
                     }
                 }
             }
@@ -575,17 +576,24 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
     // after the first workgroups every colour of a 256-colour palette is
     // usually in, and 2,000-4,000 workgroups' atomics on the same 32 words
     // serialised at the end of a short (row-block shard) launch.
-#ifdef HQ_ABL_NOUSED  // timing ablation (wrong results): no used-bit flush
-    if (false) {
-#else
-    if (PASS == 0 && tid < 8 * NG) {
-#endif
-        const uint32_t m = s_used[tid >> 3][tid & 7];
-        uint32_t* gw = &a.used_glob[(blockIdx.x & (kUsedSlots - 1)) * a.used_stride + (p0 + (tid >> 3)) * 8 +
-                                    (tid & 7)];
-        const uint32_t seen = __hip_atomic_load(gw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (m & ~seen) atomicOr(gw, m);
+#ifndef HQ_ABL_NOUSED  // (timing ablation, wrong results: no used-bit flush)
+    if constexpr (PASS == 0) {
+        // colour tid of each palette: wave wv's ballot = words 2 wv, 2 wv + 1
+        static_assert(kMaxK == 256, "one colour per thread at the flush");
+        const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+        for (int pp = 0; pp < NG; ++pp) {
+            const uint64_t bits = __ballot(s_usedb[pp][tid] != 0);
+            if (lane < 2) {
+                const uint32_t m = lane ? (uint32_t)(bits >> 32) : (uint32_t)bits;
+                uint32_t* gw = &a.used_glob[(blockIdx.x & (kUsedSlots - 1)) * a.used_stride + (p0 + pp) * 8 +
+                                            2 * wv + lane];
+                const uint32_t seen = __hip_atomic_load(gw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (m & ~seen) atomicOr(gw, m);
+            }
+        }
     }
+#endif
 #ifdef HQ_ASSIGN_TIMING
     if ((tid & 63) == 0 && w < kAsgStamps) g_asg_t[w][4 + (tid >> 6)] = t_loop;
     if (tid == 0 && w < kAsgStamps) {
