@@ -137,6 +137,13 @@ struct TileFill {
         const Geom& g = a.g;
         t = ti;
         const uint8_t* idx = a.idx + (int64_t)t.p * g.idx_pitch;
+#ifdef HQ_ABL_NOFILL  // timing ablation (wrong results): no global loads for the fill
+        ov = make_uint4(tid, tid + 1, tid + 2, 0u);
+        interior = true;
+#pragma unroll
+        for (int q = 0; q < NFD; ++q) lo[q] = hi[q] = roff[q] = (uint32_t)(tid * 7 + q);
+        return;
+#endif
         ov = tid < a.K ? a.opp16[(int64_t)t.p * kMaxK + tid] : make_uint4(0u, 0u, 0u, 0u);
         interior = t.x0 - HALF >= 0 && t.x0 + TW + HALF <= g.W;
         if (interior) {
@@ -360,8 +367,10 @@ __device__ __forceinline__ void pack_b_halves(const uint32_t (&w)[10], u32x4& h,
 __device__ __forceinline__ f32x4v mfma3(const f16x8& ah, const f16x8& al, const f16x8& bh,
                                         const f16x8& bl) {
     f32x4v d = {0.f, 0.f, 0.f, 0.f};
+#ifndef HQ_ABL_MFMA1  // (timing ablation, wrong results: the hi.hi product only)
     d = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, d, 0, 0, 0);
     d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, d, 0, 0, 0);
+#endif
     d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, d, 0, 0, 0);
     return d;
 }
@@ -588,6 +597,14 @@ __device__ __forceinline__ void hpass_wide(const f32x4* src, int j, TapsPtr<HB> 
     constexpr int HR = 4;
     constexpr int CH = HB <= 10 ? 2 * HB + 1 : HB == 19 ? HQ_CH19 : HQ_CHW;  // taps per chunk
     const f32x4* row = src + plane * pstride + j;
+#ifdef HQ_ABL_NOHPASS  // timing ablation (wrong results): one window read, no taps
+    {
+        const f32x4 v = row[0];
+        acc[0] += v.xy;
+        acc[1] += v.zw;
+        return;
+    }
+#endif
 #pragma unroll
     for (int t0 = TLO; t0 <= THI; t0 += CH) {
         const int t1 = t0 + CH - 1 < THI ? t0 + CH - 1 : THI;
@@ -768,6 +785,15 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
         const int row = 4 * n + lk;
         return (4 * n + 3 < RH ? row : min(row, RH - 1)) * RW + col;
     };
+    // index of a gathered element (timing ablations, wrong results: HQ_ABL_NOIDX
+    // skips the index read, HQ_ABL_NOTAB the table read below)
+    auto gidx = [&](int n, int col) -> uint32_t {
+#ifdef HQ_ABL_NOIDX
+        return (uint32_t)(gather_row(n, col) & 255);
+#else
+        return s_idx[gather_row(n, col)];
+#endif
+    };
 
     // ---- channel 0: stacks (f0, f1) -> planes 0, 1 and (f2, -) -> plane 2 ----
 #pragma unroll
@@ -777,7 +803,11 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
         const int col = col0 + 16 * NW * i;
         uint32_t w[NJ];
 #pragma unroll
-        for (int n = 0; n < NJ; ++n) w[n] = 4 * n < RH ? s_ox[s_idx[gather_row(n, col)]] : 0u;
+#ifdef HQ_ABL_NOTAB
+        for (int n = 0; n < NJ; ++n) w[n] = 4 * n < RH ? gidx(n, col) * 0x00010001u : 0u;
+#else
+        for (int n = 0; n < NJ; ++n) w[n] = 4 * n < RH ? s_ox[gidx(n, col)] : 0u;
+#endif
         f32x4v d[2][2];
         vblock<S, 2>(w, A, d);
         store_vstack_at<WH, NW>(st01, d[0][0], i, 0);
@@ -886,7 +916,12 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
 #pragma unroll
             for (int n = 0; n < NJ; ++n) {
                 if (4 * n < RH) {
-                    const uint2 e = s_oyz[s_idx[gather_row(n, col)]];
+#ifdef HQ_ABL_NOTAB
+                    const uint32_t ix = gidx(n, col);
+                    const uint2 e = make_uint2(ix * 0x00010001u, ix * 0x00020002u);
+#else
+                    const uint2 e = s_oyz[gidx(n, col)];
+#endif
                     wy[n] = e.x; wz[n] = e.y;
                 } else {
                     wy[n] = wz[n] = 0u;
@@ -928,11 +963,16 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
     for (int r = 0; r < 2; ++r) {
         const bool ok = gy0 + r < g.r1 && gx0 < g.W;
         const uint32_t off = ok ? (uint32_t)((gy0 + r - g.r0) * g.lab_pitch + gx0) : 0u;
+#ifdef HQ_ABL_NOLABLD  // timing ablation (wrong results): no LabRef loads
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) lab[r][ch] = make_float4(off, off + 1, off + ch, r);
+#else
         const float* src3[3] = {a.labL, a.labA, a.labB};
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch)
             lab[r][ch] = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(src3[ch]) +
                                                           (off << 2));  // 32-bit byte offset
+#endif
     }
     __syncthreads();
     if constexpr (TRIM) hpass_wide<HB, L2, T2 - L2, WH>(hsrc, jr, taps, 5, 0, PLANE4, acc2);
@@ -947,8 +987,12 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
         const float Bs[4] = {lab[r][2].x, lab[r][2].y, lab[r][2].z, lab[r][2].w};
 #pragma unroll
         for (int xo = 0; xo < HR; ++xo) {
+#ifdef HQ_ABL_NOLAB  // timing ablation (wrong results): no Opp->Lab / dE
+            e[r][xo] = (acc0[xo][r] + acc1[xo][r]) + (acc2[xo][r] + (Ls[xo] + As[xo] + Bs[xo]));
+#else
             const float3 lf = opp2f_fast(acc0[xo][r], acc1[xo][r], acc2[xo][r], a.m_lab);
             e[r][xo] = delta_e_f<DE>(Ls[xo], As[xo], Bs[xo], lf);
+#endif
         }
     }
     if (a.pix_err) {  // test option: the per-pixel dE (CL:201-209's error image)
