@@ -15,6 +15,9 @@
 #ifndef HQ_ASSIGN_DEPTH
 #define HQ_ASSIGN_DEPTH 1  // pixels the level-2 lookups run ahead of the resolve (1 or 2)
 #endif
+// wave-uniform "any lane": the compare's lane mask itself (HIP's __any
+// materialised the predicate in a VGPR and compared it again)
+#define HQ_ANY(c) (__builtin_amdgcn_ballot_w64(c) != 0)
 #ifndef HQ_ASSIGN_JOINT
 #define HQ_ASSIGN_JOINT 0  // 1: argmin_group over the whole group in lockstep (measured slower:
                            // 0.218 vs 0.199 ms at C3 P=4, fewer waves and longer walks)
@@ -167,7 +170,7 @@ __device__ __forceinline__ void argmin_group(float r, float g, float b, const L2
 #ifdef HQ_ABL_NOLOOP  // timing ablation (wrong results): no candidate walk
     maxc = 1;
 #endif
-    if (__builtin_amdgcn_ballot_w64(maxc > 1)) {  // (no bool -> VGPR -> compare)
+    if (HQ_ANY(maxc > 1)) {
         const f32x2 rg = {r, g};
         const char* base = reinterpret_cast<const char*>(s_pal);
         auto at = [&](int q, uint32_t off) {
@@ -194,7 +197,7 @@ __device__ __forceinline__ void argmin_group(float r, float g, float b, const L2
         }
 #pragma unroll
         for (int i = 1; i < kL2Cap; ++i) {
-            if (!__builtin_amdgcn_ballot_w64(i < maxc)) break;
+            if (!HQ_ANY(i < maxc)) break;
 #pragma unroll
             for (int q = 0; q < NG; ++q) {
                 const uint32_t ak = an[q][0];
@@ -241,7 +244,7 @@ __device__ __forceinline__ void argmin_group(float r, float g, float b, const L2
         if (near[q]) atomicAdd(&g_asg_slow[0], 1u);
         if (slow[q]) atomicAdd(&g_asg_slow[1], 1u);
 #endif
-        if (__builtin_amdgcn_ballot_w64(s))
+        if (HQ_ANY(s))
             out[q] = argmin_fix(r, g, b, s, out[q], E[q], inside && !exh_pal[q], s_pal + q * kMaxK,
                                 lvl1 + (int64_t)(p0 + q) * lvl1_pitch, G2, K);
     }
@@ -578,19 +581,26 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
     // serialised at the end of a short (row-block shard) launch.
 #ifndef HQ_ABL_NOUSED  // (timing ablation, wrong results: no used-bit flush)
     if constexpr (PASS == 0) {
-        // colour tid of each palette: wave wv's ballot = words 2 wv, 2 wv + 1
+        // bytes -> words: colour tid of each palette, wave wv's ballot = words
+        // 2 wv, 2 wv + 1, staged in LDS so that one wave then flushes all 8 NG
+        // words with one load and one atomic instruction (each wave flushing its
+        // own words in NG dependent load / atomic round trips held the tail of
+        // short launches: shard-of-8 assign 28 -> 59 us)
         static_assert(kMaxK == 256, "one colour per thread at the flush");
+        __shared__ uint32_t s_words[NG][8];
         const int lane = tid & 63, wv = tid >> 6;
 #pragma unroll
         for (int pp = 0; pp < NG; ++pp) {
             const uint64_t bits = __ballot(s_usedb[pp][tid] != 0);
-            if (lane < 2) {
-                const uint32_t m = lane ? (uint32_t)(bits >> 32) : (uint32_t)bits;
-                uint32_t* gw = &a.used_glob[(blockIdx.x & (kUsedSlots - 1)) * a.used_stride + (p0 + pp) * 8 +
-                                            2 * wv + lane];
-                const uint32_t seen = __hip_atomic_load(gw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (m & ~seen) atomicOr(gw, m);
-            }
+            if (lane < 2) s_words[pp][2 * wv + lane] = lane ? (uint32_t)(bits >> 32) : (uint32_t)bits;
+        }
+        __syncthreads();
+        if (tid < 8 * NG) {
+            const uint32_t m = s_words[tid >> 3][tid & 7];
+            uint32_t* gw = &a.used_glob[(blockIdx.x & (kUsedSlots - 1)) * a.used_stride + (p0 + (tid >> 3)) * 8 +
+                                        (tid & 7)];
+            const uint32_t seen = __hip_atomic_load(gw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (m & ~seen) atomicOr(gw, m);
         }
     }
 #endif

@@ -545,6 +545,9 @@ __global__ __launch_bounds__(256, 6) void cost_mfma_kernel(CostArgs a, int P_) {
 //   channel 1's horizontal pass.  HB = 10: 39,584 B of LDS.
 // ----------------------------------------------------------------------------
 constexpr int kTH16 = 16;
+#ifndef HQ_LAB_NT
+#define HQ_LAB_NT 0  // 1: LabRef read with non-temporal loads (streamed past the caches)
+#endif
 
 template <int HB, int NW = 4>
 struct Tile16 {
@@ -969,9 +972,16 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
 #else
         const float* src3[3] = {a.labL, a.labA, a.labB};
 #pragma unroll
-        for (int ch = 0; ch < 3; ++ch)
-            lab[r][ch] = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(src3[ch]) +
-                                                          (off << 2));  // 32-bit byte offset
+        for (int ch = 0; ch < 3; ++ch) {
+            const float4* lp =
+                reinterpret_cast<const float4*>(reinterpret_cast<const char*>(src3[ch]) + (off << 2));  // 32-bit byte offset
+#if HQ_LAB_NT
+            const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(lp));
+            lab[r][ch] = make_float4(v.x, v.y, v.z, v.w);
+#else
+            lab[r][ch] = *lp;
+#endif
+        }
 #endif
     }
     __syncthreads();
