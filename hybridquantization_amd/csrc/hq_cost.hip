@@ -15,7 +15,8 @@
 #define HQ_CHW 8  // horizontal taps per chunk at HB = 15, 24
 #endif
 #ifndef HQ_CH19
-#define HQ_CH19 6  // horizontal taps per chunk at HB = 19 (8 spilled 40 B per lane at 3 waves/SIMD, 6 spills 12)
+#define HQ_CH19 6  // horizontal taps per chunk at HB = 19 (6, 8, 13: equal since the pair layout; with the
+                   // 32-row layout 8 spilled 40 B per lane at 3 waves/SIMD, 6 spilled 12)
 #endif
 
 namespace hq {
@@ -558,8 +559,14 @@ struct Tile16 {
     static constexpr int NBLK = RW / 16;               // vertical-pass column blocks
     static constexpr int NSET = (NBLK + NW - 1) / NW;  // blocks per wave (at most)
     static constexpr int WH = RW / 2;                  // float2 per half of a permuted row-pair row
-    static constexpr int S = (8 + 2 * HB + 31) / 32;   // K steps of 32 rows per output-row half
-    static constexpr int NJ = 8 * S + 2;               // K slots (rows 4 n + g) a lane gathers
+    // vertical pass: the (hi, lo) pair layout (vblock_pair) above the 21-tap
+    // bucket, the 32-row layout (vblock) at HB = 10 (same-box A/B: pair layout
+    // -3% cost at HB = 19, -1.5% at 15, +4% at 10, where it needs 4 MFMAs per
+    // half and stack instead of 3 and its overlapping B windows cost copies)
+    static constexpr bool PAIR = HB > 10;
+    static constexpr int S = PAIR ? (8 + 2 * HB + 15) / 16 : (8 + 2 * HB + 31) / 32;  // MFMA K steps per half
+    static constexpr int NJ = PAIR ? 4 * S + 2 : 8 * S + 2;  // rows 4 n + g a lane gathers
+    static constexpr int AH = PAIR ? 1 : 2;  // fragment sets per stack and step (the pair layout's halves share)
     static constexpr int PLANE4 = (TH / 2) * RW / 2;   // f32x4 per filter plane
     static constexpr int NQ = (HR + 2 * HB) / 2;       // horizontal window reads per filter
     static_assert(RWL % 4 == 0 && RWL / 4 >= 8 * NW && RWL / 4 < 16 * NW, "TileFill: 8 NW <= dwords per row < 16 NW");
@@ -644,6 +651,9 @@ __device__ __forceinline__ f32x2* vstack_base(float* s_v, int plane, int lk, int
 template <int WH, int NW = 4>
 __device__ __forceinline__ void store_vstack_at(f32x2* base, const f32x4v& d, int i, int half) {
     constexpr int ROW = 2 * WH;
+#ifdef HQ_ABL_NOVSTORE  // timing ablation (wrong results): vertical results not stored
+    if (d[0] != 12345.f) return;
+#endif
     f32x2* v = base + 4 * half * ROW + 8 * NW * i;  // block set i + 1: 16 NW columns on
     v[0] = f32x2{d[0], d[1]};
     v[ROW] = f32x2{d[2], d[3]};
@@ -667,6 +677,14 @@ __device__ __forceinline__ void vblock(const uint32_t (&w)[8 * S + 2], const uin
     auto B = [](const u32x4& u) { return __builtin_bit_cast(f16x8, u); };
 #pragma unroll
     for (int st = 0; st < NST; ++st) d[st][0] = d[st][1] = f32x4v{0.f, 0.f, 0.f, 0.f};
+#ifdef HQ_ABL_NOMFMA  // timing ablation (wrong results): no operand packing, no MFMA
+#pragma unroll
+    for (int st = 0; st < NST; ++st) {
+        d[st][0] = f32x4v{__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(A[st][0][0][0].x), 0.f};
+        d[st][1] = f32x4v{__uint_as_float(w[2]), __uint_as_float(w[3]), __uint_as_float(A[st][1][0][1].y), 0.f};
+    }
+    return;
+#endif
 #pragma unroll
     for (int s = 0; s < S; ++s) {
         u32x4 bh, bl;
@@ -686,6 +704,63 @@ __device__ __forceinline__ void vblock(const uint32_t (&w)[8 * S + 2], const uin
         for (int st = 0; st < NST; ++st)
             d[st][1] = mfma3_acc(H(A[st][1][s][0]), H(A[st][1][s][1]), B(bh), B(bl), d[st][1]);
     }
+}
+
+// One column block's vertical products in the (hi, lo) pair layout: w[n] =
+// the gathered dword of region row 4 n + g, its (hi, lo) f16 pair, used as
+// two K slots of the B operand as is (no repacking).  Step u of half 0 reads
+// w[4 u .. 4 u + 3] (rows 16 u .. 16 u + 15 over the four lane groups), half 1
+// the rows 8 further on, w[4 u + 2 .. 4 u + 5], with the same A fragments
+// A[stack][u][hi, lo] (each K-slot pair holds one tap part twice): hi taps x
+// (hi + lo) data, then lo taps x (hi + lo) data, fp32 accumulate -- the full
+// split product (the lo.lo term included), two MFMAs per 16 rows and no
+// v_perm (the 32-row layout needed ten per step to split hi and lo halves).
+template <int N>
+using u32xn = uint32_t __attribute__((ext_vector_type(N)));
+
+// dwords O .. O + 3 of the gathered rows as one B operand: a sub-register of
+// the rows' single wide register, so the overlapping windows of the two
+// halves need no copies
+template <int O, int N>
+__device__ __forceinline__ f16x8 pair_window(const u32xn<N>& v) {
+    return __builtin_bit_cast(f16x8, __builtin_shufflevector(v, v, O, O + 1, O + 2, O + 3));
+}
+
+template <int U, int S, int NST>
+__device__ __forceinline__ void vblock_pair_step(const u32xn<4 * S + 2>& v, const uint4 (&A)[NST][S][2],
+                                                 f32x4v (&d)[NST][2]) {
+    if constexpr (U < S) {
+        auto H = [](const uint4& u) { return __builtin_bit_cast(f16x8, u); };
+        const f16x8 b0 = pair_window<4 * U, 4 * S + 2>(v);
+        const f16x8 b1 = pair_window<4 * U + 2, 4 * S + 2>(v);
+#pragma unroll
+        for (int st = 0; st < NST; ++st) {
+            d[st][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(H(A[st][U][0]), b0, d[st][0], 0, 0, 0);
+            d[st][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(H(A[st][U][1]), b0, d[st][0], 0, 0, 0);
+            d[st][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(H(A[st][U][0]), b1, d[st][1], 0, 0, 0);
+            d[st][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(H(A[st][U][1]), b1, d[st][1], 0, 0, 0);
+        }
+        vblock_pair_step<U + 1, S, NST>(v, A, d);
+    }
+}
+
+template <int S, int NST>
+__device__ __forceinline__ void vblock_pair(const uint32_t (&w)[4 * S + 2], const uint4 (&A)[NST][S][2],
+                                            f32x4v (&d)[NST][2]) {
+    u32xn<4 * S + 2> v;
+#pragma unroll
+    for (int n = 0; n < 4 * S + 2; ++n) v[n] = w[n];
+#pragma unroll
+    for (int st = 0; st < NST; ++st) d[st][0] = d[st][1] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    vblock_pair_step<0, S, NST>(v, A, d);
+}
+
+// cost16w's vertical products in its bucket's layout (Tile16::PAIR)
+template <bool PAIR, int S, int NST, int AH, int NJ>
+__device__ __forceinline__ void vblock_any(const uint32_t (&w)[NJ], const uint4 (&A)[NST][AH][S][2],
+                                           f32x4v (&d)[NST][2]) {
+    if constexpr (PAIR) vblock_pair<S, NST>(w, *reinterpret_cast<const uint4(*)[NST][S][2]>(&A), d);
+    else vblock<S, NST>(w, A, d);
 }
 
 #ifndef HQ_LB19
@@ -710,6 +785,8 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
     constexpr int NTH = 64 * NW, IPR = 8 * NW;  // threads; horizontal items per row pair
     constexpr int TH = kTH16, HR = 4, T2 = 2 * HB, TW = Gm::TW, RWL = Gm::RWL, RW = Gm::RW;
     constexpr int RH = Gm::RH, WH = Gm::WH, NBLK = Gm::NBLK, NSET = Gm::NSET, S = Gm::S, NJ = Gm::NJ;
+    constexpr bool PAIR = Gm::PAIR;
+    constexpr int AH = Gm::AH;
     constexpr int ROW = 2 * WH, PLANE4 = Gm::PLANE4;
     constexpr int L0 = HB - trim_w(HB, 0), L1 = HB - trim_w(HB, 1), L2 = HB - trim_w(HB, 2);
     static_assert(TW / HR == IPR && 8 * IPR == NTH, "one horizontal item per thread");
@@ -730,8 +807,9 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
     const TileItem cur = tile_item<TW, TH>(a, xcd_remap(blockIdx.x, a.ntiles * P_), P_);
     const TapsPtr<HB> taps = (TapsPtr<HB>)(uintptr_t)a.taps;  // H taps x 2^-30
     const int lane = tid & 63, wv = tid >> 6, lc = lane & 15, lk = lane >> 4;
-    // [trim][half][step][stack][hi, lo][lane]
-    const uint4* frag = a.vfrag16 + (TRIM ? 2 * S * 4 * 2 * 64 : 0) + lane;
+    // pair layout: [trim][step][stack][hi, lo][lane] (build_vpass_f16_pair_fragments);
+    // else [trim][half][step][stack][hi, lo][lane] (build_vpass_f16_stack_fragments)
+    const uint4* frag = (PAIR ? a.vfrag16p : a.vfrag16) + (TRIM ? AH * S * 4 * 2 * 64 : 0) + lane;
     auto F = [&](int half, int s, int st, int hl) { return frag[(((half * S + s) * 4 + st) * 2 + hl) * 64]; };
 
     std::conditional_t<W16, TileFill16<HB, RWL, RW, TH, NTH>, TileFill<HB, RWL, TH, NTH>> fill;
@@ -741,11 +819,11 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
 #pragma unroll
         for (int j = 0; j < NTE; ++j) tx[j] = a.opp16[(int64_t)cur.p * KT + tid + NTH * j].x;
     }
-    uint4 A[2][2][S][2];  // channel 0's stacks (f0, f1), (f2, -); then channels 1-2's
+    uint4 A[2][AH][S][2];  // channel 0's stacks (f0, f1), (f2, -); then channels 1-2's
 #pragma unroll
     for (int st = 0; st < 2; ++st)
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < AH; ++h)
 #pragma unroll
             for (int s = 0; s < S; ++s) {
                 A[st][h][s][0] = F(h, s, st, 0);
@@ -812,7 +890,7 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
         for (int n = 0; n < NJ; ++n) w[n] = 4 * n < RH ? s_ox[gidx(n, col)] : 0u;
 #endif
         f32x4v d[2][2];
-        vblock<S, 2>(w, A, d);
+        vblock_any<PAIR>(w, A, d);
         store_vstack_at<WH, NW>(st01, d[0][0], i, 0);
         store_vstack_at<WH, NW>(st01, d[0][1], i, 1);
         if (lk < 2) {  // the (f2, -) stack's second filter slot is empty
@@ -826,30 +904,16 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
 #pragma unroll
         for (int st = 0; st < 2; ++st)
 #pragma unroll
-            for (int h = 0; h < 2; ++h)
+            for (int h = 0; h < AH; ++h)
 #pragma unroll
                 for (int s = 0; s < S; ++s) {
                     A[st][h][s][0] = F(h, s, 2 + st, 0);
                     A[st][h][s][1] = F(h, s, 2 + st, 1);
                 }
     };
-    // HB = 19: channels 1 and 2 gathered one after the other, so no vertical
-    // results wait in registers through a horizontal pass (the shared gather
-    // with channel 2 held in registers spilled 16 VGPRs; now 4)
-#ifndef HQ_SPLIT12
-#define HQ_SPLIT12 1
-#endif
-    constexpr bool SPLIT = HB == 19 && HQ_SPLIT12;  // (HB = 15: 5% slower split, r04_split12_ab.txt)
-    auto load_a_stack = [&](int stack) {  // one stack's fragments into A[0]
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int s = 0; s < S; ++s) {
-                A[0][h][s][0] = F(h, s, stack, 0);
-                A[0][h][s][1] = F(h, s, stack, 1);
-            }
-    };
-    if constexpr (S == 1 && !SPLIT) load_a12();
+    // (32 fragment VGPRs in flight at most)
+    constexpr bool A12_EARLY = AH * S <= 2;
+    if constexpr (A12_EARLY) load_a12();
     __syncthreads();
     uint2 tyz[W16 ? NTE : 1];  // W16: the (y, z) words, in flight through channel 0's horizontal pass
     if constexpr (W16) {
@@ -869,46 +933,11 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
     }
     __syncthreads();
 
-    // one column block's gather of channel `chn` (1: y, 2: z) and its stack -> planes 0, 1
-    auto vgather_one = [&](int chn) {
-        const uint4(&A1)[1][2][S][2] = *reinterpret_cast<const uint4(*)[1][2][S][2]>(&A[0]);
-#pragma unroll
-        for (int i = 0; i < NSET; ++i) {
-            const int b = wset + NW * i;
-            if (b >= NBLK) break;
-            const int col = col0 + 16 * NW * i;
-            uint32_t w[NJ];
-#pragma unroll
-            for (int n = 0; n < NJ; ++n) {
-                if (4 * n < RH) {
-                    const uint2 e = s_oyz[s_idx[gather_row(n, col)]];
-                    w[n] = chn == 1 ? e.x : e.y;
-                } else {
-                    w[n] = 0u;
-                }
-            }
-            f32x4v d[1][2];
-            vblock<S, 1>(w, A1, d);
-            store_vstack_at<WH, NW>(st01, d[0][0], i, 0);
-            store_vstack_at<WH, NW>(st01, d[0][1], i, 1);
-        }
-    };
-    if constexpr (SPLIT) {
-        // ---- channel 1: stack (f3, f4) -> planes 0, 1; then channel 2 ----
-        load_a_stack(2);
-        vgather_one(1);
-        __syncthreads();
-        load_a_stack(3);  // (in flight through channel 1's horizontal pass)
-        if constexpr (TRIM) hpass_wide<HB, L1, T2 - L1, WH>(hsrc, jr, taps, 3, 0, PLANE4, acc1);
-        else hpass_wide<HB, 0, T2, WH>(hsrc, jr, taps, 3, 0, PLANE4, acc1);
-        hpass_wide<HB, 0, T2, WH>(hsrc, jr, taps, 4, 1, PLANE4, acc1);
-        __syncthreads();
-        vgather_one(2);
-    } else {
+    {
         // ---- channels 1, 2: one gather of (y, z) per region row; stack (f3, f4)
         // -> planes 0, 1 now, stack (f5, f6)'s results held in registers until
         // channel 1's horizontal pass has read the planes ----
-        if constexpr (S > 1) load_a12();
+        if constexpr (!A12_EARLY) load_a12();
         f32x4v d5[NSET][2];
 #pragma unroll
         for (int i = 0; i < NSET; ++i) {
@@ -931,16 +960,16 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
                 }
             }
             {
-                const uint4(&Ay)[1][2][S][2] = *reinterpret_cast<const uint4(*)[1][2][S][2]>(&A[0]);
+                const uint4(&Ay)[1][AH][S][2] = *reinterpret_cast<const uint4(*)[1][AH][S][2]>(&A[0]);
                 f32x4v d[1][2];
-                vblock<S, 1>(wy, Ay, d);
+                vblock_any<PAIR>(wy, Ay, d);
                 store_vstack_at<WH, NW>(st01, d[0][0], i, 0);
                 store_vstack_at<WH, NW>(st01, d[0][1], i, 1);
             }
             {
-                const uint4(&Az)[1][2][S][2] = *reinterpret_cast<const uint4(*)[1][2][S][2]>(&A[1]);
+                const uint4(&Az)[1][AH][S][2] = *reinterpret_cast<const uint4(*)[1][AH][S][2]>(&A[1]);
                 f32x4v d[1][2];
-                vblock<S, 1>(wz, Az, d);
+                vblock_any<PAIR>(wz, Az, d);
                 d5[i][0] = d[0][0];
                 d5[i][1] = d[0][1];
             }
@@ -1028,6 +1057,9 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
 #pragma unroll
             for (int xo = 0; xo < HR; ++xo) part += (gy0 + r < g.r1 && gx0 + xo < g.W) ? e[r][xo] : 0.f;
     }
+#ifdef HQ_ABL_NORED  // timing ablation (wrong results): no reduction / accumulation
+    if (part == 12345.f) a.acc[tid] = 1;
+#else
     double sum = wave_sum_to_lane63((double)part);
     if ((tid & 63) == 63) s_red[tid >> 6] = sum;
     __syncthreads();
@@ -1036,6 +1068,7 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
         if constexpr (NW == 8) t += (s_red[4] + s_red[5]) + (s_red[6] + s_red[7]);
         acc_add(a.acc, a.acc_P, a.acc_p0 + cur.p, cur.tile, t);
     }
+#endif
 }
 
 // ----------------------------------------------------------------------------
@@ -1236,6 +1269,8 @@ int fast_bucket(int half) {
 }
 
 static int bucket_steps(int HB) { return (8 + 2 * HB + 31) / 32; }
+// MFMA K steps of 16 region rows per output-row half in the pair layout (cost16w)
+static int pair_steps(int HB) { return (8 + 2 * HB + 15) / 16; }
 
 // The 7 filters (f: 0 k1.x, 1 k2.x, 2 k3 (|k3| vertical), 3 k1.y, 4 k2.y,
 // 5 k1.z, 6 k2.z) of half-width H centred in 2 HB + 1 taps (zeros around):
@@ -1325,6 +1360,45 @@ void build_vpass_f16_stack_fragments(int HB, int H, const float* k1, const float
                             out[((base + 0 * 64) + l) * 8 + j] = hi;
                             out[((base + 1 * 64) + l) * 8 + j] = lo;
                         }
+}
+
+// cost16w's A fragments in the (hi, lo) pair layout (see vblock_pair):
+// [trim][u][stack][hi, lo][lane] x 8 halves.  Lane l holds A[i = l & 15][k =
+// 8 g + 2 j + e], g = l >> 4: K slots 2 j and 2 j + 1 both stand for region row
+// 4 (4 u + j) + g (the gathered dword of that row is its (hi, lo) f16 pair), so
+// both hold the same tap part -- the tap's hi half in fragment hl = 0, its lo
+// half in hl = 1 -- of filter stack[i >> 3] for output row i & 7: bucket tap d =
+// row - (i & 7), zero outside [0, 2 HB] (and outside the trimmed window).  Half
+// 1 (output rows 8-15) reads the rows 8 further on with the same fragments.
+size_t vpass_f16_pair_fragment_halves(int HB) { return (size_t)2 * pair_steps(HB) * 4 * 2 * 64 * 8; }
+
+void build_vpass_f16_pair_fragments(int HB, int H, const float* k1, const float* k2, const float* k3,
+                                    const float* absk3, uint16_t* out) {
+    std::vector<float> tv, th;
+    bucket_taps(k1, k2, k3, absk3, H, HB, tv, th);
+    const int T = 2 * HB + 1, U = pair_steps(HB);
+    const int stack[4][2] = {{0, 1}, {2, -1}, {3, 4}, {5, 6}};
+    for (int trim = 0; trim < 2; ++trim)
+        for (int u = 0; u < U; ++u)
+            for (int st = 0; st < 4; ++st)
+                for (int l = 0; l < 64; ++l)
+                    for (int kk = 0; kk < 8; ++kk) {
+                        const int i = l & 15, g = l >> 4, r = i & 7, f = stack[st][i >> 3];
+                        const int row = 4 * (4 * u + (kk >> 1)) + g;
+                        const int d = row - r;
+                        float w = 0.f;
+                        if (f >= 0 && d >= 0 && d < T) {
+                            w = tv[f * T + d];
+                            const int ch = f == 0 ? 0 : (f == 3 ? 1 : (f == 5 ? 2 : -1));
+                            if (trim && ch >= 0 && std::abs(d - HB) > trim_w(HB, ch)) w = 0.f;
+                        }
+                        w *= kVTapScale;
+                        const uint16_t hi = host_f16(w);
+                        const uint16_t lo = host_f16(w - host_f16_to_f32(hi));
+                        const size_t base = ((((size_t)trim * U + u) * 4 + st) * 2) * 64;
+                        out[((base + 0 * 64) + l) * 8 + kk] = hi;
+                        out[((base + 1 * 64) + l) * 8 + kk] = lo;
+                    }
 }
 
 // The narrow k1 filters' taps outside the bucket's trimmed windows are below

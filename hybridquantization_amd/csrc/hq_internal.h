@@ -162,7 +162,9 @@ struct CostArgs {
     const uint4* opp16;     // [P][256] split opponent table (PaletteArgs::opp16)
     const void* taps;       // CostTaps<10> x 2 in device memory (build_fast_taps)
     const uint4* vfrag16;   // [trim][4 stacks][hi, lo][64 lanes] f16x8 A fragments of the
-                            // vertical taps (build_vpass_f16_stack_fragments)
+                            // vertical taps (build_vpass_f16_stack_fragments; cost_mfma)
+    const uint4* vfrag16p;  // [trim][u][4 stacks][hi, lo][64 lanes]: the same taps in the (hi, lo)
+                            // pair layout of cost16w (build_vpass_f16_pair_fragments)
     const float* labL;      // planar LabRef, owned rows, pitch lab_pitch
     const float* labA;
     const float* labB;

@@ -37,6 +37,9 @@ hipError_t launch_cost_fast(const CostArgs&, int P, int de, bool trim, int tile_
                             hipStream_t);
 int fast_bucket(int half);
 size_t vpass_f16_stack_fragment_halves(int HB);
+void build_vpass_f16_pair_fragments(int HB, int H, const float* k1, const float* k2, const float* k3,
+                                    const float* absk3, uint16_t* out);
+size_t vpass_f16_pair_fragment_halves(int HB);
 void build_vpass_f16_stack_fragments(int HB, int H, const float* k1, const float* k2, const float* k3,
                                      const float* absk3, uint16_t* out);
 size_t fast_taps_bytes(int HB);
@@ -109,6 +112,7 @@ struct hq_ctx {
     int fast_hb = 0;   // fast path tap bucket (fast_bucket(half)); 0 = generic path only
     DevBuf d_taps;     // fast path taps, build_fast_taps (the filters centred in the bucket)
     DevBuf d_vfrag16;  // split-f16 MFMA A fragments of the stacked vertical taps
+    DevBuf d_vfrag16p; // the same in cost16w's (hi, lo) pair layout
 
     // image
     bool have_image = false;
@@ -627,6 +631,7 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
         ca.opp16 = c->d_opp16.as<uint4>() + (int64_t)so * kMaxK;
         ca.taps = c->d_taps.p;
         ca.vfrag16 = c->d_vfrag16.as<uint4>();
+        ca.vfrag16p = c->d_vfrag16p.as<uint4>();
         ca.labL = c->d_labL.as<float>();
         ca.labA = c->d_labA.as<float>();
         ca.labB = c->d_labB.as<float>();
@@ -1006,7 +1011,7 @@ void hq_destroy(hq_ctx* c) {
                       &c->d_labL, &c->d_labA, &c->d_labB, &c->d_pal_in, &c->d_pal, &c->d_opp, &c->d_opp16,
                       &c->d_dup, &c->d_pflags, &c->d_lvl1, &c->d_lvl2, &c->d_idx,
                       &c->d_used_mask, &c->d_acc, &c->d_out, &c->d_gen_t, &c->d_taps,
-                      &c->d_vfrag16, &c->d_idx32, &c->d_used32, &c->d_pixerr, &c->d_idx16, &c->d_dist})
+                      &c->d_vfrag16, &c->d_vfrag16p, &c->d_idx32, &c->d_used32, &c->d_pixerr, &c->d_idx16, &c->d_dist})
         b->release();
     if (c->h_pal) (void)hipHostFree(c->h_pal);
     if (c->h_out) (void)hipHostFree(c->h_out);
@@ -1065,6 +1070,11 @@ int hq_set_filters(hq_ctx* c, int taps, const float* k1, const float* k2, const 
         build_vpass_f16_stack_fragments(HB, c->half, k1, k2, k3, absk3, f16s.data());
         HIP_TRY(c, c->d_vfrag16.ensure(f16s.size() * sizeof(uint16_t)));
         HIP_TRY(c, hipMemcpy(c->d_vfrag16.p, f16s.data(), f16s.size() * sizeof(uint16_t),
+                             hipMemcpyHostToDevice));
+        std::vector<uint16_t> f16p(vpass_f16_pair_fragment_halves(HB));
+        build_vpass_f16_pair_fragments(HB, c->half, k1, k2, k3, absk3, f16p.data());
+        HIP_TRY(c, c->d_vfrag16p.ensure(f16p.size() * sizeof(uint16_t)));
+        HIP_TRY(c, hipMemcpy(c->d_vfrag16p.p, f16p.data(), f16p.size() * sizeof(uint16_t),
                              hipMemcpyHostToDevice));
         std::vector<char> tb(fast_taps_bytes(HB));
         build_fast_taps(HB, c->half, k1, k2, k3, absk3, tb.data());
