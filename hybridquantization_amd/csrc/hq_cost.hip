@@ -546,9 +546,6 @@ __global__ __launch_bounds__(256, 6) void cost_mfma_kernel(CostArgs a, int P_) {
 //   channel 1's horizontal pass.  HB = 10: 39,584 B of LDS.
 // ----------------------------------------------------------------------------
 constexpr int kTH16 = 16;
-#ifndef HQ_TILE_SUM_LDS
-#define HQ_TILE_SUM_LDS 0  // 1: cost16w's tile total by LDS integer atomics, no closing barrier
-#endif
 #ifndef HQ_LAB_NT
 #define HQ_LAB_NT 0  // 1: LabRef read with non-temporal loads (streamed past the caches)
 #endif
@@ -767,10 +764,11 @@ __device__ __forceinline__ void vblock_any(const uint32_t (&w)[NJ], const uint4 
 }
 
 #ifndef HQ_LB15
-#define HQ_LB15 4  // waves per SIMD of the 15-tap bucket (126 VGPRs, no spill; LDS: OYZ_IN_PLANE)
+#define HQ_LB15 3  // waves per SIMD of the 15-tap bucket (4, with its (y, z) table moved into plane 2 to
+                   // fit 4 workgroups' LDS: no faster, 0.476 against 0.477 ms at 150/30)
 #endif
 #ifndef HQ_LB24
-#define HQ_LB24 2  // waves per SIMD of the 24-tap bucket
+#define HQ_LB24 2  // waves per SIMD of the 24-tap bucket (3: 92 B of spill, 0.823-0.826 against 0.820 ms)
 #endif
 #ifndef HQ_LB19
 #define HQ_LB19 3  // waves per SIMD of the 19-tap bucket
@@ -804,21 +802,12 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
     using IT = std::conditional_t<W16, uint16_t, uint8_t>;
     __shared__ f32x4 s_vq[3 * PLANE4];
     __shared__ uint32_t s_ox8[W16 ? 1 : kMaxK];  // opponent x 2^14 as (hi, lo) f16 pairs: channel 0
-    // channels 1, 2; HB = 15 keeps them in plane 2, unused from the end of channel
-    // 0's horizontal pass on (41,184 -> 39,136 B of LDS: 4 workgroups per CU)
-    constexpr bool OYZ_IN_PLANE = !W16 && HB == 15;
-    __shared__ uint2 s_oyz8[W16 || OYZ_IN_PLANE ? 1 : kMaxK];
+    __shared__ uint2 s_oyz8[W16 ? 1 : kMaxK];    // channels 1, 2
     __shared__ __attribute__((aligned(16))) IT s_idx[RH * RW];
-#if HQ_TILE_SUM_LDS
-    __shared__ unsigned long long s_tsum;  // the tile's fixed-point total, summed by the waves
-    __shared__ uint32_t s_tbad, s_tcnt;
-#else
     __shared__ double s_red[NW];
-#endif
     extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];  // W16: 8 KT bytes
     uint32_t* const s_ox = W16 ? s_tab : s_ox8;
-    uint2* const s_oyz = W16 ? reinterpret_cast<uint2*>(s_tab)
-                             : OYZ_IN_PLANE ? reinterpret_cast<uint2*>(s_vq + 2 * Gm::PLANE4) : s_oyz8;
+    uint2* const s_oyz = W16 ? reinterpret_cast<uint2*>(s_tab) : s_oyz8;
     float* s_v = reinterpret_cast<float*>(s_vq);
     const int tid = threadIdx.x;
     const Geom& g = a.g;
@@ -856,17 +845,10 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
     } else {
         if (NTH == kMaxK || tid < kMaxK) {
             s_ox[tid] = fill.ov.x;
-            if constexpr (!OYZ_IN_PLANE) s_oyz[tid] = make_uint2(fill.ov.y, fill.ov.z);
+            s_oyz[tid] = make_uint2(fill.ov.y, fill.ov.z);
         }
         fill.template commit_idx<RW>(a, s_idx, tid);
     }
-#if HQ_TILE_SUM_LDS
-    if (tid == 0) {
-        s_tsum = 0ull;
-        s_tbad = 0u;
-        s_tcnt = 0u;
-    }
-#endif
     // H item: row pair m, output columns 4j .. 4j+3 (every thread has one)
     const int m = tid / IPR, jr = tid % IPR;
     const int gy0 = cur.y0 + 2 * m, gx0 = cur.x0 + HR * jr;
@@ -955,10 +937,6 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
     if constexpr (W16) {  // (the x words' last reads were the gathers before the barrier)
 #pragma unroll
         for (int j = 0; j < NTE; ++j) s_oyz[tid + NTH * j] = tyz[j];
-    }
-    if constexpr (OYZ_IN_PLANE) {  // once every wave has read plane 2
-        __syncthreads();
-        if (NTH == kMaxK || tid < kMaxK) s_oyz[tid] = make_uint2(fill.ov.y, fill.ov.z);
     }
     __syncthreads();
 
@@ -1090,20 +1068,6 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
     if (part == 12345.f) a.acc[tid] = 1;
 #else
     double sum = wave_sum_to_lane63((double)part);
-#if HQ_TILE_SUM_LDS
-    // each wave's fixed-point partial into the tile's LDS total (integers: the
-    // order of the waves does not matter), no barrier; the last wave to arrive
-    // adds the total to the palette's slot counters
-    if ((tid & 63) == 63) {
-        uint64_t v = 0;
-        if (acc_fixed(sum, v)) __hip_atomic_fetch_add(&s_tsum, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        else __hip_atomic_fetch_add(&s_tbad, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (__hip_atomic_fetch_add(&s_tcnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == NW - 1)
-            acc_add_fixed(a.acc, a.acc_P, a.acc_p0 + cur.p, cur.tile,
-                          __hip_atomic_load(&s_tsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP),
-                          __hip_atomic_load(&s_tbad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-    }
-#else
     if ((tid & 63) == 63) s_red[tid >> 6] = sum;
     __syncthreads();
     if (tid == 0) {
@@ -1111,7 +1075,6 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
         if constexpr (NW == 8) t += (s_red[4] + s_red[5]) + (s_red[6] + s_red[7]);
         acc_add(a.acc, a.acc_P, a.acc_p0 + cur.p, cur.tile, t);
     }
-#endif
 #endif
 }
 

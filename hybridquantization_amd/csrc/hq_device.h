@@ -241,21 +241,6 @@ __device__ __forceinline__ void acc_add(uint64_t* acc, int P, int p, int slot, d
         atomicAdd((unsigned long long*)(a + 2), 1ull);
     }
 }
-// A wave's partial x as the fixed-point integer acc_add would add (RN(x 2^20)),
-// or false when x is not a number in [0, 2^43) (counted as `bad`).
-__device__ __forceinline__ bool acc_fixed(double x, uint64_t& v) {
-    if (!(x >= 0.0 && x < 8796093022208.0)) return false;
-    v = (uint64_t)__double2ull_rn(x * kAccScale);
-    return true;
-}
-// acc_add of an integer total v (already x 2^20) and `bad` counts.
-__device__ __forceinline__ void acc_add_fixed(uint64_t* acc, int P, int p, int slot, uint64_t v, uint32_t bad) {
-    uint64_t* a = acc + ((int64_t)(slot & (kAccSlots - 1)) * P + p) * 4;
-    if (v & 0xffffffffull) atomicAdd((unsigned long long*)(a + 0), (unsigned long long)(v & 0xffffffffull));
-    if (v >> 32) atomicAdd((unsigned long long*)(a + 1), (unsigned long long)(v >> 32));
-    if (bad) atomicAdd((unsigned long long*)(a + 2), (unsigned long long)bad);
-}
-
 // The total of palette p (any thread; kAccSlots x 3 loads, issued together).
 __device__ __forceinline__ double acc_total(const uint64_t* acc, int P, int p) {
     uint64_t lo = 0, hi = 0, bad = 0;
