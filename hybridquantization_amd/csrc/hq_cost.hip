@@ -527,6 +527,9 @@ __global__ __launch_bounds__(256, 6) void cost_mfma_kernel(CostArgs a, int P_) {
 //   replaced by the next step's dword 0: each lane gathers 8 S + 2 rows (the
 //   ones past the region are zero, not gathered) for 2 x 8 output rows, no
 //   divergence.  At HB = 10 (S = 1): 36 gathered rows per 16 output rows.
+//   Above HB = 10 the (hi, lo) pair layout instead (vblock_pair): steps of 16
+//   rows, the gathered dwords used as B operands as they are, 4 S + 2 rows per
+//   lane.
 //   RW / 16 blocks of 16 columns (ranges of 32) cover the region columns
 //   (+ unread ones): each block is the 16 columns of one parity half of a range
 //   (lane n -> column 4(n >> 1) + 2 (b & 1) + (n & 1)), so its stores fill 16
