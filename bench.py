@@ -180,9 +180,10 @@ def main():
     ap.add_argument("--shard-of", type=int, default=0, metavar="N",
                     help="experiment: run rank 0's row block of an N-way split on one GPU, "
                          "no collective (per-rank step time at N GPUs)")
-    ap.add_argument("--split", choices=["rows", "palettes"], default="rows",
-                    help="N > 1: row-block shards + one all-reduce (default), or each rank the whole "
-                         "image and P/N palettes + one all-gather (SURVEY 8e, large populations)")
+    ap.add_argument("--split", choices=["auto", "rows", "palettes"], default="auto",
+                    help="N > 1: row-block shards + one all-reduce, or each rank the whole image and P/N "
+                         "palettes + one all-gather (SURVEY 8e); auto: palettes when P >= 8 N and N "
+                         "divides P (C5: 1.23x faster per rank, DESIGN.md 5), else rows")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-full-search", action="store_true",
@@ -218,7 +219,8 @@ def main():
         m.setOption(k, int(v))
     sa_device = int(opts.get("sa_device", 1))
     R, G, B = synthetic_planes(W, H, seed=args.seed)
-    psplit = args.split == "palettes" and world > 1
+    auto_pal = args.population >= 8 * world and args.population % world == 0
+    psplit = world > 1 and (args.split == "palettes" or (args.split == "auto" and auto_pal))
     if psplit:
         hqd.palette_slice(args.population, world, rank)  # (raises unless the population divides)
         m.setOption("palette_split", 1)
