@@ -1145,7 +1145,7 @@ def _pal_with_dark(K, seed):
 
 @pytest.mark.parametrize("variant", [(0, 16), (0, 8), (1, 16), (2, 16)])
 @pytest.mark.parametrize("case", ["case_64x48_k16", "case_97x53_k64", "dark_256_9660", "dark_193x131_7245",
-                                  "dark_256_30050"])
+                                  "dark_256_30050", "dark_200x136_15030", "dark_160x144_20030"])
 def test_pixel_errors_vs_oracle(gpu, case, variant):
     """(cost_variant, cost_rows): the default 16 x 128 tiles (cost16w), the 8 x 108
     tiles (cost_mfma), the LDS-tiled generic pair and the per-pixel generic pair
@@ -1164,7 +1164,9 @@ def test_pixel_errors_vs_oracle(gpu, case, variant):
     else:
         dims, geo = case.split("_")[1], case.split("_")[2]
         w, h = (int(v) for v in dims.split("x")) if "x" in dims else (int(dims), int(dims))
-        dpi, vd = {"9660": (96, 60.0), "7245": (72, 45.0), "30050": (300, 50.0)}[geo]
+        # (96/60: tap bucket 19, 150/30: 15, 200/30: 24 -- the pair layout's 3 and 4 K steps)
+        dpi, vd = {"9660": (96, 60.0), "7245": (72, 45.0), "30050": (300, 50.0), "15030": (150, 30.0),
+                   "20030": (200, 30.0)}[geo]
         f = o.design_filters(dpi, vd)
         R, G, B = _dark_case(w, h, seed=w + h)
         pals = [_pal_with_dark(64, 900 + w), _pal_with_dark(256, 901 + w)]
