@@ -715,6 +715,9 @@ __device__ __forceinline__ void grid_cell_body(const GridArgs& a, int p, int cel
         else v = (!ovf1 && tid - 1 < total) ? s_list[tid - 1] : 0;
         l1[tid] = v;
     }
+#ifdef HQ_ABL_GRID_L1ONLY  // timing ablation (wrong results): no level-2 lists
+    return;
+#endif
     // Level 2: child ch = tid >> 2 of this cell at axis positions (a0, a1, a2),
     // its parent-list positions shared by the 4 threads of a quad (q = tid & 3
     // takes positions q, q+4, ...): T2 and the candidate mask are combined
