@@ -149,6 +149,27 @@ def test_fast_path_matches_generic(gpu, de, trim, rows, tw):
     m.close()
 
 
+@pytest.mark.parametrize("dpi,vd", [(150, 30.0), (96, 60.0), (200, 30.0)])
+@pytest.mark.parametrize("de", [hq.deltaETypes.CIE76, hq.deltaETypes.CIE94])
+def test_fast_path_matches_generic_wide_buckets(gpu, de, dpi, vd):
+    """The tap buckets 15, 19 and 24 (the vertical pass's (hi, lo) pair layout,
+    3 and 4 K steps) agree with the generic fp32 two-pass path to 1e-6 relative
+    for both dE formulas, on interior, edge and partial tiles."""
+    w, h = 290, 93
+    R, G, B = o.synthetic_image(w, h, seed=dpi)
+    m = hq.ImageManipulation(de, device=gpu)
+    sp = hq.ScielabProcessor(dpi, vd, hq.Whitepoint.D65, None, m)
+    m.setImage(o.inline_rgba(R, G, B).reshape(-1), None, w, sp.illuminant)
+    pals = [o.synthetic_palette(K, 11 + K) for K in (16, 256)]
+    out = {}
+    for variant in (0, 1):
+        m.setOption("cost_variant", variant)
+        out[variant] = np.array([m.computeQuantizationErrorPopulation([p.reshape(-1)], 2.0)[0]
+                                 for p in pals])
+    np.testing.assert_allclose(out[0], out[1], rtol=1e-6)
+    m.close()
+
+
 # ---------------------------------------------------------------------------
 # Viewing geometry (HQ:229-231 dpi / distance -> SP:80-102 tap count -> IM:408
 # halfSize): the fast path runs the filters centred in a tap bucket of
