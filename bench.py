@@ -65,6 +65,44 @@ def measured_traffic(size, K, P, grid, world, kernel, dpi=72, distance=45.0):
     return None
 
 
+def cost_accounting(half, K, grid, opts):
+    """The cost kernel that runs for a geometry / palette size / options, and its
+    flops per pixel-evaluation: nominal = the reference's stencil, 7 separable
+    filters x 2 passes x (2 half + 1) taps x 2 flops, + Opp->Lab / dE76 ~ 40 (628 at
+    the default half 10); executed = the fast path's filters centred in its tap
+    bucket HB (2 HB + 1 taps), the narrow k1 filters over their trimmed windows
+    only (hq_cost.hip trim_w); the generic path runs the filters as designed.
+    Returns (kernel name, bucket HB or 0, chunked, nominal, executed)."""
+    rows = int(opts.get("cost_rows", 16))
+    variant = int(opts.get("cost_variant", 0))
+    hb = next((b for b in (10, 15, 19, 24) if half <= b), 0)
+    # K <= 256: u8 indices; 256 < K <= 4096: chunked palettes, 16-bit indices, the
+    # tiled kernel at HB = 10 with 16 x 128 tiles only; above: 32-bit indices
+    chunked = 256 < K <= 4096 and int(opts.get("chunked", 1)) != 0 and grid > 0
+    tw_opt = int(opts.get("cost_tw", 128))
+    generic = (variant != 0 or hb == 0 or (K > 256 and not chunked)
+               or (chunked and (hb != 10 or rows != 16 or tw_opt != 128)))
+    trim_w = {10: (3, 4, 5), 15: (4, 5, 7), 19: (5, 7, 9), 24: (6, 9, 12)}
+    if generic:
+        # cost_variant 2: the per-pixel pair; otherwise the LDS-tiled pair
+        kernel = "gen_hpass_kernel+gen_vpass_kernel" if variant == 2 else "gen_hrow_kernel+gen_vtile_kernel"
+        taps_exec = 7 * (2 * half + 1)
+    else:
+        kernel = "cost_mfma_kernel" if rows == 8 and hb == 10 else "cost16w_kernel"
+        trim = int(opts.get("trim", 1)) != 0
+        taps_exec = 4 * (2 * hb + 1) + (sum(2 * t + 1 for t in trim_w[hb]) if trim else 3 * (2 * hb + 1))
+    return kernel, (0 if generic else hb), chunked, 7 * 2 * (2 * half + 1) * 2 + 40, 2 * 2 * taps_exec + 40
+
+
+def use_palette_split(split, P, world):
+    """N > 1: the palette split (whole image, P / N palettes per rank, one
+    all-gather) when asked, or under 'auto' when P >= 8 N and N divides P (C5:
+    1.23x faster per rank than the row split); else row blocks."""
+    if world <= 1:
+        return False
+    return split == "palettes" or (split == "auto" and P >= 8 * world and P % world == 0)
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -219,8 +257,7 @@ def main():
         m.setOption(k, int(v))
     sa_device = int(opts.get("sa_device", 1))
     R, G, B = synthetic_planes(W, H, seed=args.seed)
-    auto_pal = args.population >= 8 * world and args.population % world == 0
-    psplit = world > 1 and (args.split == "palettes" or (args.split == "auto" and auto_pal))
+    psplit = use_palette_split(args.split, args.population, world)
     if psplit:
         hqd.palette_slice(args.population, world, rank)  # (raises unless the population divides)
         m.setOption("palette_split", 1)
@@ -309,34 +346,10 @@ def main():
         value = n_own * P * args.steps / elapsed / 1e6
     # Dominant kernel: the cost kernel (S-CIELAB stencil + Opp->Lab + dE76).  With P > 1
     # palettes per launch its HBM bytes (LabRef once + P index images) amortise
-    # and FP32 VALU bounds it.  Algorithmic flops per pixel-eval: the
-    # reference's stencil, 7 separable filters x 2 passes x (2 half + 1) taps x 2
-    # flops (588 at the default half 10), + Opp->Lab / dE76 ~ 40.  Executed: the
-    # fast path runs the filters centred in its tap bucket HB (2 HB + 1 taps), the
-    # narrow k1 filters over their trimmed windows only (2 trim_w + 1 taps,
-    # hq_cost.hip trim_w); the generic path runs the filters as designed.
+    # and FP32 VALU bounds it; its flops: cost_accounting.
     half = m.halfSize
-    rows = int(opts.get("cost_rows", 16))
-    variant = int(opts.get("cost_variant", 0))
-    hb = next((b for b in (10, 15, 19, 24) if half <= b), 0)
-    # K <= 256: u8 indices; 256 < K <= 4096: chunked palettes, 16-bit indices, the
-    # tiled kernel at HB = 10 with 16 x 128 tiles only; above: 32-bit indices
-    chunked = 256 < args.K <= 4096 and int(opts.get("chunked", 1)) != 0 and args.grid > 0
-    tw_opt = int(opts.get("cost_tw", 128))
-    generic = (variant == 1 or hb == 0 or (args.K > 256 and not chunked)
-               or (chunked and (hb != 10 or rows != 16 or tw_opt != 128)))
-    trim_w = {10: (3, 4, 5), 15: (4, 5, 7), 19: (5, 7, 9), 24: (6, 9, 12)}
-    if generic:
-        # cost_variant 2: the per-pixel pair; otherwise the LDS-tiled pair
-        kernel = "gen_hpass_kernel+gen_vpass_kernel" if variant == 2 else "gen_hrow_kernel+gen_vtile_kernel"
-        taps_exec = 7 * (2 * half + 1)
-    else:
-        kernel = "cost_mfma_kernel" if rows == 8 and hb == 10 else "cost16w_kernel"
-        trim = int(opts.get("trim", 1)) != 0
-        taps_exec = 4 * (2 * hb + 1) + (sum(2 * t + 1 for t in trim_w[hb]) if trim else 3 * (2 * hb + 1))
+    kernel, hb, chunked, flops_nominal, flops_exec = cost_accounting(half, args.K, args.grid, opts)
     cost_ms = prof["cost"][0]
-    flops_nominal = 7 * 2 * (2 * half + 1) * 2 + 40
-    flops_exec = 2 * 2 * taps_exec + 40
     P_dev = hqd.palette_slice(P, world, rank)[1] if psplit else P  # palettes one device's cost kernel evaluates
     alg_flops = n_own * P_dev * flops_nominal
     exec_flops = n_own * P_dev * flops_exec
@@ -376,7 +389,7 @@ def main():
                      "traffic": traffic,
                      "kernel": kernel, "kernel_avg_ms": round(cost_ms, 4),
                      "flops_per_px_eval": flops_nominal, "exec_flops_per_px_eval": flops_exec,
-                     "half": half, "tap_bucket": None if generic else hb,
+                     "half": half, "tap_bucket": hb or None,
                      "alg_flops_per_launch": alg_flops, "exec_flops_per_launch": exec_flops,
                      "frac_executed_taps": round(exec_tf / FP32_PEAK_TFLOPS, 4),
                      "alg_bytes_per_launch": alg_bytes, "hbm_GBs_alg": round(hbm_gbs, 1),
