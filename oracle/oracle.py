@@ -277,6 +277,37 @@ def ciede94(lab1, lab2):
     return np.sqrt(dL * dL + (dC / sc) ** 2 + (dH / sh) ** 2).astype(f32)
 
 
+def _fma32(a, b, c):
+    """fp32 fma(a, b, c): the product is exact in float64, the sum rounds once
+    there and once more to fp32 (a double rounding that differs from one fused
+    rounding only on rare ties)."""
+    return (np.asarray(a, np.float64) * np.asarray(b, np.float64) + np.asarray(c, np.float64)).astype(f32)
+
+
+def ciede94_f32(lab1, lab2):
+    """CL:217-226 statement by statement in fp32: fma as one rounding, sc and sh
+    from double literals (1 + 0.045 c1 in double, stored as float), and no clamp
+    before sqrt(fma(da, da, db db) - dC dC) -- the reference returns NaN where
+    rounding makes dH^2 negative (the hue difference below ~1e-4 of the chroma
+    difference), and so does this restatement (`ciede94` clamps at 0)."""
+    p1 = np.asarray(lab1, f32)
+    p2 = np.asarray(lab2, f32)
+    L1, a1, b1 = p1[..., 0], p1[..., 1], p1[..., 2]
+    L2, a2, b2 = p2[..., 0], p2[..., 1], p2[..., 2]
+    with np.errstate(invalid="ignore"):
+        dL = (L1 - L2).astype(f32)
+        c1 = np.sqrt(_fma32(a1, a1, (b1 * b1).astype(f32)))
+        dC = (c1 - np.sqrt(_fma32(a2, a2, (b2 * b2).astype(f32)))).astype(f32)
+        da = (a1 - a2).astype(f32)
+        db = (b1 - b2).astype(f32)
+        dH = np.sqrt((_fma32(da, da, (db * db).astype(f32)) - (dC * dC).astype(f32)).astype(f32))
+        sc = (1 + 0.045 * c1.astype(np.float64)).astype(f32)
+        sh = (1 + 0.015 * c1.astype(np.float64)).astype(f32)
+        dcs = (dC / sc).astype(f32)
+        dhs = (dH / sh).astype(f32)
+        return np.sqrt(_fma32(dL, dL, _fma32(dcs, dcs, (dhs * dhs).astype(f32)))).astype(f32)
+
+
 # --------------------------------------------------------------------------
 # Separable stencil helpers (reflection CL:256-263)
 # --------------------------------------------------------------------------

@@ -123,6 +123,34 @@ def test_eval_config2_1024_k64(ip, filt):
     assert abs(cost - ref) <= COST_RTOL * abs(ref) * 0.1
 
 
+def _compare_fast_generic(m, pals, de):
+    """Costs and per-pixel dE of the fast path (cost_variant 0) and the generic
+    fp32 two-pass path (1) for each palette.  dE76: no NaN, costs to 1e-6
+    relative.  dE94: the reference's unclamped dH (CL:217-226) is NaN on the
+    rare hue-aligned pixels where fp32 rounding makes dH^2 negative, and which
+    pixels depends on the Lab's last bits: the finite pixels must agree, NaNs
+    stay below 2e-3 of the pixels, a cost is NaN exactly when one of its pixels
+    is, and finite costs agree to 1e-6 (NaN == NaN alone would pass vacuously)."""
+    m.setOption("pixel_err", 1)
+    for p in pals:
+        cost, err = {}, {}
+        for variant in (0, 1):
+            m.setOption("cost_variant", variant)
+            cost[variant] = m.computeQuantizationErrorPopulation([p.reshape(-1)], 2.0)[0]
+            err[variant] = m.getPixelErrors(0)
+        nan0, nan1 = np.isnan(err[0]), np.isnan(err[1])
+        if de == hq.deltaETypes.CIE76:
+            assert not nan0.any() and not nan1.any()
+        assert nan0.mean() < 2e-3 and nan1.mean() < 2e-3
+        ok = ~(nan0 | nan1)
+        np.testing.assert_allclose(err[0][ok], err[1][ok], rtol=0, atol=2e-4)
+        for v, nan in ((0, nan0), (1, nan1)):
+            assert np.isnan(cost[v]) == bool(nan.any())
+        if not (nan0.any() or nan1.any()):
+            np.testing.assert_allclose(cost[0], cost[1], rtol=1e-6)
+    m.setOption("pixel_err", 0)
+
+
 @pytest.mark.parametrize("rows,tw", [(16, 256), (16, 128), (8, 128)])
 @pytest.mark.parametrize("de", [hq.deltaETypes.CIE76, hq.deltaETypes.CIE94])
 @pytest.mark.parametrize("trim", [1, 0])
@@ -140,12 +168,7 @@ def test_fast_path_matches_generic(gpu, de, trim, rows, tw):
     m.setOption("trim", trim)
     m.setOption("cost_rows", rows)
     m.setOption("cost_tw", tw)
-    out = {}
-    for variant in (0, 1):
-        m.setOption("cost_variant", variant)
-        out[variant] = np.array([m.computeQuantizationErrorPopulation([p.reshape(-1)], 2.0)[0]
-                                 for p in pals])
-    np.testing.assert_allclose(out[0], out[1], rtol=1e-6)
+    _compare_fast_generic(m, pals, de)
     m.close()
 
 
@@ -161,12 +184,7 @@ def test_fast_path_matches_generic_wide_buckets(gpu, de, dpi, vd):
     sp = hq.ScielabProcessor(dpi, vd, hq.Whitepoint.D65, None, m)
     m.setImage(o.inline_rgba(R, G, B).reshape(-1), None, w, sp.illuminant)
     pals = [o.synthetic_palette(K, 11 + K) for K in (16, 256)]
-    out = {}
-    for variant in (0, 1):
-        m.setOption("cost_variant", variant)
-        out[variant] = np.array([m.computeQuantizationErrorPopulation([p.reshape(-1)], 2.0)[0]
-                                 for p in pals])
-    np.testing.assert_allclose(out[0], out[1], rtol=1e-6)
+    _compare_fast_generic(m, pals, de)
     m.close()
 
 
@@ -1125,12 +1143,13 @@ def _dark_case(w, h, seed):
     return R, G, B
 
 
-def exact_pixel_err(idx, pal, lab_ref, f, w, h):
+def exact_pixel_err(idx, pal, lab_ref, f, w, h, lab_only=False):
     """The per-pixel dE of CL:194-198 (palette -> opponent), CL:234-306 (both
     stencil passes, reflection CL:256-263), CL:118-145 (Opp->Lab) and CL:201-209
     (dE76), evaluated in float64 from the same fp32 inputs (palette, taps,
     LabRef): the exact value that both fp32 paths -- the reference's order in
-    the oracle and the GPU's -- approximate."""
+    the oracle and the GPU's -- approximate.  lab_only: the candidate's float64
+    Lab (n x 3) instead of dE76."""
     d = np.float64
     p = pal[:, :3].astype(d)
     lin = np.where(p <= 0.04045, p / 12.92, ((p + 0.055) / 1.055) ** float(np.float32(2.4)))
@@ -1154,6 +1173,8 @@ def exact_pixel_err(idx, pal, lab_ref, f, w, h):
     lin_seg = (d(o.KAPPA) * xyz + 16.0) / 116.0
     fx = np.where(xyz > d(o.LABDELTA3), np.cbrt(xyz), lin_seg)
     lab = np.stack([116.0 * fx[:, 1] - 16.0, 500.0 * (fx[:, 0] - fx[:, 1]), 200.0 * (fx[:, 1] - fx[:, 2])], -1)
+    if lab_only:
+        return lab
     return np.sqrt(((np.asarray(lab_ref, d).reshape(-1, 4)[:, :3] - lab) ** 2).sum(-1))
 
 
@@ -1226,4 +1247,83 @@ def test_pixel_errors_vs_oracle(gpu, case, variant):
         dark_lin += int(np.count_nonzero(parts["idx"] >= K // 2)) if not case.startswith("case_") else 0
     if not case.startswith("case_"):
         assert dark_lin > 1000  # the near-black colours were chosen (linear-segment Lab)
+    m.close()
+
+
+def _de94_exact(lab_ref, lab):
+    """CL:217-226 in float64 on float64 Lab; also returns dH^2 and da^2 + db^2."""
+    p1 = np.asarray(lab_ref, np.float64).reshape(-1, 4)[:, :3]
+    L1, a1, b1 = p1[:, 0], p1[:, 1], p1[:, 2]
+    L2, a2, b2 = lab[:, 0], lab[:, 1], lab[:, 2]
+    c1 = np.hypot(a1, b1)
+    dC = c1 - np.hypot(a2, b2)
+    dab2 = (a1 - a2) ** 2 + (b1 - b2) ** 2
+    dH2 = dab2 - dC * dC
+    e = np.sqrt((L1 - L2) ** 2 + (dC / (1 + 0.045 * c1)) ** 2 + np.maximum(dH2, 0) / (1 + 0.015 * c1) ** 2)
+    return e, dH2, dab2
+
+
+@pytest.mark.parametrize("variant", [(0, 16), (0, 8), (1, 16), (2, 16)])
+@pytest.mark.parametrize("case", ["case_97x53_k64", "dark_193x131_7245", "dark_256_9660", "dark_200x136_15030",
+                                  "dark_160x144_20030"])
+def test_pixel_errors_de94_vs_oracle(gpu, case, variant):
+    """dE94 (CL:217-226) per pixel against the oracle's fp32 statement of it
+    (oracle.ciede94_f32 on the oracle's candidate Lab) and a float64 evaluation.
+    The reference's dH = sqrt(fma(da, da, db db) - dC dC) has no clamp: where
+    fp32 rounding makes the argument negative (the hue difference ~1e-4 of the
+    colour difference or less; ~3e-4 of the pixels of a synthetic image) it is
+    NaN, the pixel's dE is NaN, and so is the mean (IM:736-768).  The GPU keeps
+    that: a NaN pixel on either side must have a float64 dH^2 within rounding of
+    0, the cost is NaN exactly when a pixel is, and every finite pixel meets
+    dE76's bars (2x the oracle's worst distance from float64, 1.5x its mean)."""
+    if case.startswith("case_"):
+        g, R, G, B = load_case(case)
+        w, h = int(g["w"]), int(g["h"])
+        f = o.design_filters()
+        dpi, vd = 72, 45.0
+        pals = [p for p in g["palettes"]]
+        lab = g["lab"].astype(np.float32)
+    else:
+        dims, geo = case.split("_")[1], case.split("_")[2]
+        w, h = (int(v) for v in dims.split("x")) if "x" in dims else (int(dims), int(dims))
+        dpi, vd = {"9660": (96, 60.0), "7245": (72, 45.0), "15030": (150, 30.0), "20030": (200, 30.0)}[geo]
+        f = o.design_filters(dpi, vd)
+        R, G, B = _dark_case(w, h, seed=w + h)
+        pals = [_pal_with_dark(64, 900 + w), _pal_with_dark(256, 901 + w)]
+        lab = c_oracle.srgb_to_scielab(R, G, B, f, w, nthreads=_threads())
+    rgba = o.inline_rgba(R, G, B)
+    m = hq.ImageManipulation(hq.deltaETypes.CIE94, device=gpu)
+    sp = hq.ScielabProcessor(dpi, vd, hq.Whitepoint.D65, None, m)
+    m.setOption("pixel_err", 1)
+    m.setOption("cost_variant", variant[0])
+    m.setOption("cost_rows", variant[1])
+    m.setImage(rgba.reshape(-1), lab.reshape(-1), w, sp.illuminant)
+    for pal in pals:
+        K = pal.shape[0]
+        cost = m.computeQuantizationErrorPopulation([pal.reshape(-1)], 2.0)[0]
+        _, parts = c_oracle.eval_palette(rgba, lab, pal, f, w, nthreads=_threads(), return_parts=True)
+        np.testing.assert_array_equal(m.getIndices(0), parts["idx"].astype(np.uint8))
+        err = m.getPixelErrors(0)
+        e_orc = o.ciede94_f32(lab, o.candidate_scielab(parts["idx"], pal, f, w, h))
+        ex, dH2, dab2 = _de94_exact(lab, exact_pixel_err(parts["idx"], pal, lab, f, w, h, lab_only=True))
+        nan_g, nan_o = np.isnan(err), np.isnan(e_orc)
+        # a NaN needs dH^2 within rounding of 0: fp32 Lab is ~1e-4 from float64
+        # in a and b (the 500x and 200x of CL:143-145), moving dH^2 by ~2e-4 |dab|
+        near0 = np.abs(dH2) <= 1e-3 * (np.sqrt(dab2) + 1.0)
+        assert near0[nan_g].all() and near0[nan_o].all()
+        assert nan_g.mean() < 2e-3
+        ok = ~(nan_g | nan_o)
+        d_gpu, d_orc = np.abs(err[ok] - ex[ok]), np.abs(e_orc[ok] - ex[ok])
+        stats = (f"{case} K={K} variant {variant}: NaN px gpu {int(nan_g.sum())} oracle {int(nan_o.sum())}; "
+                 f"|gpu-exact| max {d_gpu.max():.3g} mean {d_gpu.mean():.3g}; "
+                 f"|oracle-exact| max {d_orc.max():.3g} mean {d_orc.mean():.3g}")
+        print(stats)
+        np.testing.assert_allclose(err[ok], e_orc[ok], rtol=0, atol=2e-4, err_msg=stats)
+        assert d_gpu.max() <= 2 * d_orc.max(), stats
+        assert d_gpu.mean() <= 1.5 * d_orc.mean(), stats
+        assert np.isnan(cost) == bool(nan_g.any()), stats
+        if not nan_g.any():  # the mean (IM:736-768) and the penalty
+            used = np.bincount(parts["idx"], minlength=K)[:K] > 0
+            ref = float(np.mean(ex)) + float(np.count_nonzero(~used)) * 2.0
+            assert abs(cost - ref) <= 1e-5 * ref, stats
     m.close()

@@ -164,3 +164,32 @@ def test_swasa_trace_golden():
     best, err = o.find_best_quantization(lambda ps: [cost(p) for p in ps], int(g["K"]), sw, trace=tr)
     np.testing.assert_array_equal(np.array([[t[3]] + t[1] for t in tr]), g["trace"])
     np.testing.assert_array_equal(best, g["best"])
+
+
+def test_ciede94_f32_statement():
+    """oracle.ciede94_f32 (CL:217-226 in fp32, no clamp) against the float64
+    form: within 1e-5 where finite (the cancellation in dH^2 costs a few fp32
+    ulp of |dab|^2, divided by 2 dE); NaN exactly where rounding
+    makes fma(da, da, db db) - dC dC negative -- a hue-aligned pair (here a
+    colour and the same colour scaled towards grey, dH = 0 exactly) is NaN in
+    the reference's arithmetic, and identical colours are 0."""
+    rng = np.random.default_rng(1)
+    n = 4000
+    f32 = np.float32
+    a, b = (rng.uniform(-60, 60, n).astype(f32) for _ in range(2))
+    lab1 = np.stack([rng.uniform(0, 100, n).astype(f32), a, b, np.zeros(n, f32)], -1)
+    lab2 = (lab1 + rng.normal(0, 3, lab1.shape)).astype(f32)
+    e32, e64 = o.ciede94_f32(lab1, lab2), o.ciede94(lab1, lab2)
+    ok = ~np.isnan(e32)
+    assert ok.mean() > 0.999
+    np.testing.assert_allclose(e32[ok], e64[ok], rtol=1e-6, atol=1e-5)
+    # known NaN (fp32 dH^2 = -7.6e-6 for this pair; the float64 form gives 10.36)
+    p1 = np.array([[50.0, 53.837933, -44.249878, 0.0]], f32)
+    p2 = np.array([[40.0, 45.146347, -37.106186, 0.0]], f32)
+    assert np.isnan(o.ciede94_f32(p1, p2)[0])
+    assert abs(float(o.ciede94(p1, p2)[0]) - 10.363361) < 1e-4
+    k = rng.uniform(0.3, 0.9, n)
+    scaled = lab1.copy()
+    scaled[:, 1:3] = (lab1[:, 1:3] * k[:, None]).astype(f32)
+    assert 0.1 < np.isnan(o.ciede94_f32(lab1, scaled)).mean() < 0.9
+    assert (o.ciede94_f32(lab1, lab1) == 0).all()
