@@ -745,6 +745,50 @@ def test_device_search_matches_host_driven(gpu, filt, P, K):
     m.close()
 
 
+@pytest.mark.parametrize("P", [1, 4])
+def test_device_search_de94_nan_costs(gpu, filt, P):
+    """dE94 costs of a realistic image are NaN (the reference's unclamped dH,
+    CL:222; see test_pixel_errors_de94_vs_oracle).  The reference's loop then
+    runs on IEEE comparisons: argmin (IM:843-855) keeps member 0, isAccepted
+    (SW:54-57) rejects a NaN difference after drawing its random number, a NaN
+    never beats the best (IM:529) and the convergence copy takes member 0 with
+    minerror = Double.MAX_VALUE (IM:518-545).  The device-resident loop and the
+    host-driven driver must follow that trajectory identically; while no
+    candidate has a finite cost, the best palette stays the initial member 0's
+    (its error NaN).  (A rare candidate with no NaN pixel is finite and then
+    becomes the best, as in the reference.)"""
+    import ctypes as C
+    w, h, K = 256, 128, 16
+    R, G, B = o.synthetic_image(w, h, seed=19)
+    m = hq.ImageManipulation(hq.deltaETypes.CIE94, device=gpu)
+    hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
+    m.setImage(o.inline_rgba(R, G, B).reshape(-1), None, w, filt.illum)
+    lib = hq.load()
+    res = {}
+    for dev in (0, 1):  # host-driven; device-resident
+        m.setOption("sa_device", dev)
+        sw = hq.SWASA(population=P, imax=30, seed=40 + P, t0=0.05)
+        params = sw.params()
+        handle = C.c_void_p()
+        hq._lib.check(lib.hq_search_create(m.ctx, C.byref(params), K, sw.seed, C.byref(handle)), m.ctx)
+        best = np.zeros((2, 4 * K), np.float32)
+        err = C.c_double()
+        it = C.c_int()
+        ran = C.c_int()
+        for j, chunk in enumerate((1, 29)):
+            hq._lib.check(lib.hq_search_run(handle, chunk, C.byref(ran)), m.ctx)
+            hq._lib.check(lib.hq_search_best(handle, hq._lib.fptr(best[j]), C.byref(err), C.byref(it)), m.ctx)
+        lib.hq_search_destroy(handle)
+        res[dev] = (best, err.value, it.value)
+    print(f"P={P}: best error host {res[0][1]!r} device {res[1][1]!r}")
+    assert res[0][2] == res[1][2] == 30
+    assert res[0][1] == res[1][1] or (np.isnan(res[0][1]) and np.isnan(res[1][1]))
+    np.testing.assert_array_equal(res[1][0], res[0][0])
+    if np.isnan(res[0][1]):  # no finite cost in the run: member 0's initial palette stays the best
+        np.testing.assert_array_equal(res[0][0][0], res[0][0][1])
+    m.close()
+
+
 @pytest.mark.parametrize("split", [0, 1])
 def test_device_search_with_single_rank_comm(gpu, filt, split):
     """The multi-GPU search loop on one GPU: with libhq's RCCL communicator the
