@@ -88,7 +88,10 @@ __device__ __forceinline__ float delta_e(float L1, float a1, float b1, float L2,
         const float dC = c1 - hw_sqrt(fmaf(a2, a2, b2 * b2));
         const float da = a1 - a2, db = b1 - b2;
         const float dH = hw_sqrt(fmaf(da, da, db * db) - dC * dC);
-        const float sc = 1.0f + 0.045f * c1, sh = 1.0f + 0.015f * c1;
+        // CL:223-224: double literals, so 1 + 0.045 c1 in double (not fused), stored as float
+        const double c1d = (double)c1;
+        const float sc = (float)__dadd_rn(1.0, __dmul_rn(0.045, c1d));
+        const float sh = (float)__dadd_rn(1.0, __dmul_rn(0.015, c1d));
         return hw_sqrt(fmaf(dL, dL, fmaf(dC / sc, dC / sc, (dH / sh) * (dH / sh))));
     }
 }
