@@ -221,8 +221,9 @@ __device__ __forceinline__ float u8_unit(uint32_t v, int j) {
 
 // ----------------------------------------------------------------------------
 // The dE sum of a palette (IM:736-768) as a fixed-point integer sum: each
-// workgroup's fp64 partial x (a tile, or 256 pixels of the generic path) adds
-// v = RN(x 2^20) to kAccSlots slot counters of 64 bits (slot = its tile mod
+// fp64 partial x (a wave's part of a cost16w tile, a tile of the other tiled
+// kernels, or 256 pixels of the generic path) adds
+// v = RN(x 2^20) to kAccSlots slot counters of 64 bits (slot = its index mod
 // kAccSlots, which spreads the atomics), split as v mod 2^32 into `lo` and
 // v >> 32 into `hi` so neither can overflow (2^32 partials of < 2^43).
 // Integer addition is associative: the total is the same bits whatever order
