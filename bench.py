@@ -42,27 +42,35 @@ def synthetic_planes(w, h, seed=1):
     return [((z >> np.uint64(8 * c)) & np.uint64(0xFF)).astype(np.float32) / s for c in range(3)]
 
 
-def measured_traffic(size, K, P, grid, world, kernel, dpi=72, distance=45.0):
+def measured_traffic(size, K, P, grid, world, kernel, dpi=72, distance=45.0, with_source=False):
     """HBM bytes per launch of `kernel` from the newest committed PMC passes
-    (profiles/rNN_hbm_traffic.json), or None when none matches this config
-    (image size, K, P, grid and viewing geometry)."""
+    whose config matches this run (image size, K, P, grid and viewing
+    geometry): any profiles/rNN*hbm_traffic.json, newest = the highest round,
+    then the latest `generated` stamp (scripts/pmc_traffic.py), then the name.
+    None when no file matches (a file with an empty config never does)."""
     import glob
+    import re
 
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_hbm_traffic.json")))
-    for path in reversed(paths):
+    cands = []
+    for path in glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]*hbm_traffic.json")):
         try:
             d = json.load(open(path))
         except (OSError, ValueError):
             continue
-        c = d.get("config", {})
+        c = d.get("config") or {}
         if world != 1 or (c.get("size"), c.get("K"), c.get("P"), c.get("grid")) != (size, K, P, grid):
             continue
         if (c.get("dpi", 72), float(c.get("distance", 45.0))) != (dpi, float(distance)):
             continue
-        for name, v in d.get("kernels", {}).items():
-            if name.startswith("hq::" + kernel):
-                return int(v["traffic_bytes"])
-    return None
+        hit = next((int(v["traffic_bytes"]) for name, v in sorted(d.get("kernels", {}).items())
+                    if name.startswith("hq::" + kernel)), None)
+        if hit is not None:
+            rnd = int(re.match(r"r(\d\d)", os.path.basename(path)).group(1))
+            cands.append(((rnd, str(d.get("generated", "")), os.path.basename(path)), hit))
+    if not cands:
+        return (None, None) if with_source else None
+    key, hit = max(cands)
+    return (hit, key[2]) if with_source else hit
 
 
 def cost_accounting(half, K, grid, opts):
@@ -101,6 +109,23 @@ def use_palette_split(split, P, world):
     if world <= 1:
         return False
     return split == "palettes" or (split == "auto" and P >= 8 * world and P % world == 0)
+
+
+def profiled_stages(world):
+    """hq_profile_get names of one search iteration: the kernels, and at N > 1
+    the collective ("comm": the RCCL all-reduce or all-gather, event-timed)."""
+    return ("sa_step", "grid", "assign", "cost", "finalize") + (("comm",) if world > 1 else ())
+
+
+def kernel_profile(prof, world, max_over_ranks=None):
+    """{stage: (avg ms, launches)} of this rank -> (kernel_avg_ms of this rank,
+    the MAX over ranks of each average or None at N = 1).  max_over_ranks maps
+    a {stage: ms} dict to the element-wise max over the process group."""
+    avg = {k: round(v[0], 4) for k, v in prof.items()}
+    if world <= 1 or max_over_ranks is None:
+        return avg, None
+    mx = max_over_ranks({k: v[0] for k, v in prof.items()})
+    return avg, {k: round(v, 4) for k, v in mx.items()}
 
 
 def _cpu_model():
@@ -329,11 +354,12 @@ def main():
         elapsed = hqd.max_over_ranks(dist, elapsed)
 
     prof = {}
-    for k in ("sa_step", "grid", "assign", "cost", "finalize"):
+    for k in profiled_stages(world):
         ms = C.c_double()
         n = C.c_int64()
         lib.hq_profile_get(m.ctx, k.encode(), C.byref(ms), C.byref(n))
         prof[k] = (ms.value / max(n.value, 1), n.value)
+    kernel_avg, kernel_max = kernel_profile(prof, world, dist and (lambda v: hqd.max_each_over_ranks(dist, v)))
     best = np.zeros(4 * args.K, np.float32)
     berr = C.c_double()
     it = C.c_int()
@@ -357,8 +383,8 @@ def main():
     exec_tf = exec_flops / (cost_ms * 1e-3) / 1e12 if cost_ms > 0 else 0.0
     alg_bytes = n_own * (12 + P_dev * (1 if args.K <= 256 else 2 if chunked else 4))
     hbm_gbs = alg_bytes / (cost_ms * 1e-3) / 1e9 if cost_ms > 0 else 0.0
-    traffic = measured_traffic(W, args.K, P, args.grid, world, kernel.split("+")[0],
-                               args.dpi, args.distance)
+    traffic, traffic_src = measured_traffic(W, args.K, P, args.grid, world, kernel.split("+")[0],
+                                            args.dpi, args.distance, with_source=True)
     # whole-evaluation view: the metric's 24 B/px-eval HBM-read roofline
     eval_roof_mpx = HBM_PEAK_GBS * 1e9 / 24.0 / 1e6 * world
     out = {
@@ -386,7 +412,7 @@ def main():
                    **({"options": args.opt} if args.opt else {})},
         "roofline": {"bound": "valu", "achieved": round(achieved_tf, 2), "peak": FP32_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4),
-                     "traffic": traffic,
+                     "traffic": traffic, "traffic_source": traffic_src and f"profiles/{traffic_src}",
                      "kernel": kernel, "kernel_avg_ms": round(cost_ms, 4),
                      "flops_per_px_eval": flops_nominal, "exec_flops_per_px_eval": flops_exec,
                      "half": half, "tap_bucket": hb or None,
@@ -407,7 +433,8 @@ def main():
                              "second pass of the same steps, right after the timed one (events idle the GPU "
                              "~5-10 us each, so the timed pass has none)"},
         "metric_hbm_roofline_frac": round(value / eval_roof_mpx, 4),
-        "kernel_avg_ms": {k: round(v[0], 4) for k, v in prof.items()},
+        "kernel_avg_ms": kernel_avg,
+        **({"kernel_avg_ms_max_over_ranks": kernel_max} if kernel_max is not None else {}),
         "best_error": berr.value,
     }
     if search_line is not None and rank == 0:

@@ -9,6 +9,8 @@
 #include <cmath>
 #include <type_traits>
 #include <cstring>
+#include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #ifndef HQ_CHW
@@ -1418,6 +1420,20 @@ bool trim_window_ok(const float* k1, int H, int HB) {
     return true;
 }
 
+// Dynamic LDS of `bytes` for kernel `fn` (static + dynamic may pass 64 KB): raised once per kernel
+// (each template instance is its own function; the largest size asked so far
+// is kept per function pointer).  False if the runtime refused it.
+static bool allow_dyn_lds(const void* fn, size_t bytes) {
+    static std::mutex mu;
+    static std::unordered_map<const void*, size_t> granted;
+    const std::lock_guard<std::mutex> lock(mu);
+    size_t& g = granted[fn];
+    if (bytes <= g) return true;
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess) return false;
+    g = bytes;
+    return true;
+}
+
 template <int HB>
 static size_t taps_bytes() { return 2 * sizeof(CostTaps<HB>); }
 
@@ -1478,13 +1494,8 @@ static void launch_cost16w_chunked(const CostArgs& a0, int P, int de, bool trim,
     const dim3 grid((unsigned)(a.ntiles * P)), block(256);
     const size_t dyn = 8 * (size_t)kMaxK * NCH;
     auto go = [&](auto kern) {
-        static bool attr = false;  // LDS above 64 KB in all (NCH 16: 74 KB)
-        if (!attr) {
-            if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)dyn) != hipSuccess)
-                return;  // (the launch error is the caller's hipGetLastError)
-            attr = true;
-        }
+        // LDS above 64 KB in all (NCH 16: 74 KB)
+        if (!allow_dyn_lds(reinterpret_cast<const void*>(kern), dyn)) return;  // (the caller's hipGetLastError)
         HQ_LAUNCH(kern, grid, block, dyn, s, a, P);
     };
     if (de == 0) {
@@ -1551,13 +1562,8 @@ hipError_t launch_cost_tiled_generic(const GenArgs& a, int de, int idx_bytes, hi
     const int tiles_x = (a.g.W + kVtTile - 1) / kVtTile, tiles_y = (a.g.r1 - a.g.r0 + kVtTile - 1) / kVtTile;
     const size_t vl = sizeof(float) * kVtTile * (kVtTile + 2 * (size_t)a.half);
     auto go = [&](auto kern) {
-        static size_t attr = 64 * 1024;  // window rows above 64 KB (half > 95): raise the limit
-        if (vl > attr) {
-            if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)vl) != hipSuccess)
-                return;  // (the launch error is the caller's hipGetLastError)
-            attr = vl;
-        }
+        // window rows above 64 KB (half > 95): raise the limit
+        if (!allow_dyn_lds(reinterpret_cast<const void*>(kern), vl)) return;  // (the caller's hipGetLastError)
         HQ_LAUNCH(kern, dim3((unsigned)(tiles_x * tiles_y)), dim3(256), vl, s, a, tiles_x);
     };
     if (de == 0) go(gen_vtile_kernel<0>);

@@ -4,6 +4,21 @@
 // relabelling.  Included by every .hip translation unit of the library.
 #pragma once
 
+// HQ_ABL_* switches are timing ablations: they drop work and give wrong
+// results.  A build that sets one must say so with HQ_ABLATION_BUILD, so a
+// stray -D can never produce a library that silently returns wrong costs
+// (such a library says so on stderr at every hq_create; tests/test_capi.py
+// checks that every HQ_ABL_ name in the sources is listed here).
+#if !defined(HQ_ABLATION_BUILD) &&                                                                    \
+    (defined(HQ_ABL_NOLOOP) || defined(HQ_ABL_NOSLOW) || defined(HQ_ABL_HASHLOOKUP) ||                \
+     defined(HQ_ABL_COHERENT) || defined(HQ_ABL_NOLOOKUP) || defined(HQ_ABL_NOUSED) ||                \
+     defined(HQ_ABL_GRID_L1ONLY) || defined(HQ_ABL_TRUNC) || defined(HQ_ABL_NOFILL) ||                \
+     defined(HQ_ABL_MFMA1) || defined(HQ_ABL_NOHPASS) || defined(HQ_ABL_NOVSTORE) ||                  \
+     defined(HQ_ABL_NOMFMA) || defined(HQ_ABL_NOIDX) || defined(HQ_ABL_NOTAB) ||                      \
+     defined(HQ_ABL_NOLABLD) || defined(HQ_ABL_NOLAB) || defined(HQ_ABL_NORED))
+#error "HQ_ABL_* ablations give wrong results: define HQ_ABLATION_BUILD as well to build one"
+#endif
+
 #include "hq_internal.h"
 
 #include <hip/hip_ext.h>

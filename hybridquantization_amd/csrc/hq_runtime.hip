@@ -95,6 +95,11 @@ struct ProfSlot {
     int64_t launches = 0;
 };
 
+// Profiling events per evaluation / search iteration: start, stop of grid (0,
+// 1), assign (2, 3), cost (4, 5), finalize (6, 7), sa_step (8, 9) and the
+// collective (10, 11).
+constexpr int kProfEvents = 12;
+
 }  // namespace
 
 struct hq_ctx {
@@ -173,8 +178,9 @@ struct hq_ctx {
 
     // profiling
     bool prof = false;
-    ProfSlot prof_assign, prof_cost, prof_grid, prof_finalize, prof_sa;
-    hipEvent_t ev[8] = {};  // profiling: start/stop of grid, assign, cost, finalize
+    ProfSlot prof_assign, prof_cost, prof_grid, prof_finalize, prof_sa, prof_comm;
+    // profiling: start/stop of grid, assign, cost, finalize, [sa_step], the collective
+    hipEvent_t ev[kProfEvents] = {};
     int num_cu = 256;
 };
 
@@ -522,35 +528,57 @@ int enqueue_generic_cost(hq_ctx* c, int P, const void* idx_base, int idx_bytes, 
     return HQ_OK;
 }
 
+int palette_slice(hq_ctx* c, int P, int* lo, int* n);
+
 // K > 256 (hq_wide.hip): prep, exhaustive argmin into 32-bit indices and
-// per-colour used flags, the generic cost, finalize, [all-reduce].
+// per-colour used flags, the generic cost, finalize, [all-reduce or, under a
+// palette split, all-gather].  A palette split takes the same slice
+// [lo, lo + Pl) as enqueue_core: the other ranks' palettes are prepped here
+// too (cheap) but neither assigned nor costed, so no rank counts them.
 int enqueue_wide(hq_ctx* c, int P, int K, const hipEvent_t* ev) {
     const Geom& g = c->g;
     hipStream_t s = c->stream;
+    int lo = 0, Pl = P;
+    if (int rc = palette_slice(c, P, &lo, &Pl)) return rc;
     WideArgs wa{c->d_pal_in.as<float4>(), c->d_pal.as<float4>(), c->d_opp.as<float4>(), c->d_pflags.as<int>(),
                 c->d_R.as<float>(), c->d_G.as<float>(), c->d_B.as<float>(), c->d_idx32.as<uint32_t>(),
                 c->d_used32.as<uint32_t>(), g.n_ext, g.idx_pitch, K};
     c->acc_par ^= 1;
-    HIP_TRY(c, hipMemsetAsync(acc_set(c, c->acc_par, P), 0, sizeof(uint64_t) * acc_words(P), s));
+    if (Pl < P && !c->comm)  // test-only slice: the other palettes' rows read as zero
+        HIP_TRY(c, hipMemsetAsync(c->d_out.p, 0, sizeof(double) * (size_t)P * (1 + K), s));
+    HIP_TRY(c, hipMemsetAsync(acc_set(c, c->acc_par, Pl), 0, sizeof(uint64_t) * acc_words(Pl), s));
     HIP_TRY(c, hipMemsetAsync(c->d_pflags.p, 0, sizeof(int) * (size_t)P, s));
     HIP_TRY(c, launch_prep_wide(wa, P, s));
-    HIP_TRY(c, hipMemsetAsync(c->d_used32.p, 0, sizeof(uint32_t) * (size_t)P * K, s));
+    HIP_TRY(c, hipMemsetAsync(c->d_used32.p, 0, sizeof(uint32_t) * (size_t)Pl * K, s));
+    // the slice's palettes: indices and used flags in rows 0 .. Pl - 1
+    WideArgs ws = wa;
+    ws.pal += (int64_t)lo * K;
+    ws.opp += (int64_t)lo * K;
+    ws.pflags += lo;
     if (ev) set_launch_events(ev[2], ev[3]);
-    const hipError_t e = launch_assign_wide(wa, P, s);
+    const hipError_t e = launch_assign_wide(ws, Pl, s);
     set_launch_events(nullptr, nullptr);
     HIP_TRY(c, e);
-    int rc = enqueue_generic_cost(c, P, c->d_idx32.p, 4, K, ev);
+    int rc = enqueue_generic_cost(c, Pl, c->d_idx32.p, 4, K, ev, lo);
     if (rc) return rc;
-    FinalizeArgs fa{acc_set(c, c->acc_par, P), nullptr, 0, c->d_out.as<double>(), P, K,
+    FinalizeArgs fa{acc_set(c, c->acc_par, Pl), nullptr, 0, c->d_out.as<double>() + (int64_t)lo * (1 + K), Pl, K,
                     c->d_used32.as<uint32_t>(), 8};
     if (ev) set_launch_events(ev[6], ev[7]);
-    const hipError_t ef = launch_finalize(fa, P, s);
+    const hipError_t ef = launch_finalize(fa, Pl, s);
     set_launch_events(nullptr, nullptr);
     HIP_TRY(c, ef);
-    if (c->comm)
-        NCCL_TRY(c, ncclAllReduce(c->d_out.p, c->d_out.p, (size_t)P * (1 + K), ncclFloat64, ncclSum, c->comm, s));
-    c->slice_lo = 0;
-    c->slice_n = P;
+    if (c->comm) {
+        if (ev) HIP_TRY(c, hipEventRecord(ev[10], s));
+        if (c->psplit)
+            NCCL_TRY(c, ncclAllGather(c->d_out.as<double>() + (int64_t)lo * (1 + K), c->d_out.p,
+                                      (size_t)Pl * (1 + K), ncclFloat64, c->comm, s));
+        else
+            NCCL_TRY(c, ncclAllReduce(c->d_out.p, c->d_out.p, (size_t)P * (1 + K), ncclFloat64, ncclSum,
+                                      c->comm, s));
+        if (ev) HIP_TRY(c, hipEventRecord(ev[11], s));
+    }
+    c->slice_lo = lo;
+    c->slice_n = Pl;
     c->last_P = P;
     c->K_cur = K;
     c->last_nch = 1;
@@ -571,6 +599,7 @@ int palette_slice(hq_ctx* c, int P, int* lo, int* n) {
     *lo = 0;
     *n = P;
     if (R == 1) return HQ_OK;
+    if (r < 0 || r >= R) return fail(c, HQ_ERR_ARG, "palette split: rank %d outside [0, %d)", r, R);
     if (P % R) return fail(c, HQ_ERR_ARG, "palette split: population %d not divisible by %d ranks", P, R);
     if (c->g.r0 != 0 || c->g.r1 != c->g.H)
         return fail(c, HQ_ERR_STATE, "palette split: every rank needs the whole image (hq_set_image)");
@@ -668,12 +697,18 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
         untimed();
         HIP_TRY(c, ef);
     }
-    if (c->comm && c->psplit) {  // every rank's slice to every rank (in place; one rank: a no-op)
-        NCCL_TRY(c, ncclAllGather(c->d_out.as<double>() + (int64_t)lo * (1 + K), c->d_out.p, (size_t)Pl * (1 + K),
-                                  ncclFloat64, c->comm, s));
-    } else if (c->comm) {  // also with one rank (a no-op copy), so that path is exercised on one GPU
-        NCCL_TRY(c, ncclAllReduce(c->d_out.p, c->d_out.p, (size_t)P * (1 + K), ncclFloat64, ncclSum,
-                                  c->comm, s));
+    if (c->comm) {
+        // the collective's time (profiling only: an event record between launches
+        // idles the GPU a few us, so the timed pass of bench.py records none)
+        if (ev) HIP_TRY(c, hipEventRecord(ev[10], s));
+        if (c->psplit) {  // every rank's slice to every rank (in place; one rank: a no-op)
+            NCCL_TRY(c, ncclAllGather(c->d_out.as<double>() + (int64_t)lo * (1 + K), c->d_out.p,
+                                      (size_t)Pl * (1 + K), ncclFloat64, c->comm, s));
+        } else {  // also with one rank (a no-op copy), so that path is exercised on one GPU
+            NCCL_TRY(c, ncclAllReduce(c->d_out.p, c->d_out.p, (size_t)P * (1 + K), ncclFloat64, ncclSum,
+                                      c->comm, s));
+        }
+        if (ev) HIP_TRY(c, hipEventRecord(ev[11], s));
     }
     c->slice_lo = lo;
     c->slice_n = Pl;
@@ -689,6 +724,7 @@ void prof_accumulate(hq_ctx* c, const hipEvent_t* ev, bool finalize = true, bool
     prof_add(c, c->prof_assign, ev[2], ev[3]);
     prof_add(c, c->prof_cost, ev[4], ev[5]);
     if (finalize) prof_add(c, c->prof_finalize, ev[6], ev[7]);
+    if (c->comm) prof_add(c, c->prof_comm, ev[10], ev[11]);
 }
 
 // ... and the SA step that generated it (device-resident search: events 8, 9).
@@ -925,12 +961,12 @@ int device_search_run(hq_search* s, int iterations, int* ran) {
     if (s->fold && c->comm)
         return fail(c, HQ_ERR_STATE, "communicator set after hq_search_create: recreate the search");
     const bool prof = c->prof;
-    if (prof && (rc = ensure_events(s, (size_t)10 * iterations))) return rc;
+    if (prof && (rc = ensure_events(s, (size_t)kProfEvents * iterations))) return rc;
     for (; done < iterations && s->ite < s->prm.imax; ++done) {
         const int ite = ++s->ite;
         s->pol->reduce_temperature_if_necessary(ite);                  // IM:507
         const float amax = s->pol->max_step_width(ite) / 256.0f;       // SW:91-101
-        const hipEvent_t* ev = prof ? &s->pev[(size_t)10 * done] : nullptr;
+        const hipEvent_t* ev = prof ? &s->pev[(size_t)kProfEvents * done] : nullptr;
         // accept the previous iteration's population (none at the first of a run)
         if ((rc = enqueue_sa_step(s, done > 0, false, true, false, amax, ev ? ev + 8 : nullptr))) return rc;
         if ((rc = enqueue_core(c, s->P, s->K, ev, s->fold))) return rc;
@@ -940,8 +976,8 @@ int device_search_run(hq_search* s, int iterations, int* ran) {
     if (done > 0 && (rc = enqueue_sa_step(s, true, false, false, false, 0.f))) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     for (int i = 0; prof && i < done; ++i) {
-        prof_accumulate(c, &s->pev[(size_t)10 * i], !s->fold);
-        prof_accumulate_sa(c, &s->pev[(size_t)10 * i]);
+        prof_accumulate(c, &s->pev[(size_t)kProfEvents * i], !s->fold);
+        prof_accumulate_sa(c, &s->pev[(size_t)kProfEvents * i]);
     }
     if (ran) *ran = done;
     return HQ_OK;
@@ -980,6 +1016,9 @@ int hq_device_count(int* count) {
 int hq_create(int device, int delta_e_type, hq_ctx** out) {
     if (!out) return HQ_ERR_ARG;
     *out = nullptr;
+#ifdef HQ_ABLATION_BUILD
+    std::fprintf(stderr, "libhq: ABLATION BUILD (HQ_ABL_*): costs and indices are wrong by design\n");
+#endif
     if (delta_e_type < HQ_DE_CIE76 || delta_e_type > HQ_DE_CIEDE2000) return HQ_ERR_ARG;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device < 0 || device >= n)
@@ -1463,7 +1502,7 @@ int hq_profile_enable(hq_ctx* c, int on) {
 
 int hq_profile_reset(hq_ctx* c) {
     if (!c) return HQ_ERR_ARG;
-    c->prof_assign = c->prof_cost = c->prof_grid = c->prof_finalize = c->prof_sa = ProfSlot{};
+    c->prof_assign = c->prof_cost = c->prof_grid = c->prof_finalize = c->prof_sa = c->prof_comm = ProfSlot{};
     return HQ_OK;
 }
 
@@ -1475,6 +1514,7 @@ int hq_profile_get(hq_ctx* c, const char* kernel, double* total_ms, int64_t* lau
     else if (!std::strcmp(kernel, "grid")) s = &c->prof_grid;
     else if (!std::strcmp(kernel, "finalize")) s = &c->prof_finalize;
     else if (!std::strcmp(kernel, "sa_step")) s = &c->prof_sa;
+    else if (!std::strcmp(kernel, "comm")) s = &c->prof_comm;
     else return fail(c, HQ_ERR_ARG, "unknown kernel '%s'", kernel);
     if (total_ms) *total_ms = s->ms;
     if (launches) *launches = s->launches;
@@ -1509,6 +1549,8 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
         if (value < 1) return fail(c, HQ_ERR_ARG, "slice_ranks must be >= 1");
         c->slice_ranks = value;
     } else if (!std::strcmp(name, "slice_rank")) {
+        // (checked against slice_ranks again at each evaluation: the options may come in either order)
+        if (value < 0) return fail(c, HQ_ERR_ARG, "slice_rank must be >= 0");
         c->slice_rank = value;
     } else if (!std::strcmp(name, "chunked")) {
         c->chunked = value != 0;

@@ -393,7 +393,8 @@ __device__ __forceinline__ void sa_generate(const SaArgs& a, int p, int ch, cons
                                             const float* src0, uint64_t seed, float4* s_cand, bool lead,
                                             const SaPf<NPF>& pf) {
     const int K = a.K, n4 = 4 * K, tid = threadIdx.x, nt = 1024 / NPF;
-    const int k0 = a.nch > 1 ? kMaxK * ch : 0, kn = a.nch > 1 ? min(kMaxK, K - k0) : K;  // real colours
+    // real colours of this chunk: none when the chunk lies wholly past K (K = 600, chunk 3)
+    const int k0 = a.nch > 1 ? kMaxK * ch : 0, kn = a.nch > 1 ? max(0, min(kMaxK, K - k0)) : K;
     const uint64_t base = lcg_jump(seed, pf.bA, pf.bC);  // jump_A/C[3Kp], prefetched
 #pragma unroll
     for (int j = 0; j < NPF; ++j) {

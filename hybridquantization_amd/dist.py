@@ -75,6 +75,17 @@ def max_over_ranks(dist, value: float) -> float:
     return float(t.item())
 
 
+def max_each_over_ranks(dist, values: dict) -> dict:
+    """Element-wise MAX of a per-rank {name: float} (the same keys on every rank,
+    e.g. bench.py's per-kernel averages) over the process group."""
+    import torch
+
+    keys = sorted(values)
+    t = torch.tensor([float(values[k]) for k in keys], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return {k: float(v) for k, v in zip(keys, t.tolist())}
+
+
 def allreduce_partials(dist, partial):
     """Sum of the ranks' hq_eval_population_partial outputs (numpy fp64 [P*(1+K)])
     over the process group: the exchange libhq does with ncclAllReduce, here over

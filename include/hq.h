@@ -105,8 +105,13 @@ int hq_set_image_planar_shard(hq_ctx *ctx, const float *R, const float *G, const
 int hq_get_labref(hq_ctx *ctx, float *lab4);
 
 /* IM:620 computeQuantizationErrorPopulation for P palettes of K colours
- * (K in [1, 2^24] as the plugin allows, HQ:192; K > 256 runs the exhaustive
- * argmin with 32-bit indices and the generic stencil path):
+ * (K in [1, 2^24] as the plugin allows, HQ:192).  K <= 256: the pruned grid
+ * argmin and the tiled fast stencil.  256 < K <= 4096: chunked palettes (nch
+ * sub-palettes of 256 through the same grid, assign and fast stencil, 16-bit
+ * indices; option "chunked").  K > 4096, palettes with non-finite colours or
+ * outside the fast path's range, option "chunked" 0 or "grid" 0: the exhaustive
+ * argmin with 32-bit indices and the generic stencil path.  All give the same
+ * indices and used flags (bit-exact) and the same cost (1e-6 relative):
  * costs[p] = mean dE76 + delta * #unused (IM:712, SW:74-82); used[p*K+k] in
  * {0,1} (CL:193), may be NULL.  On a sharded context with a communicator the
  * partial sums are all-reduced over RCCL first. */
@@ -185,8 +190,9 @@ int hq_swasa_search_host(const hq_swasa_params *params, int K, uint64_t seed, in
 /* Kernel timing of the dominant kernels, measured with HIP events on the
  * context stream while enabled (bench.py roofline). */
 int hq_profile_enable(hq_ctx *ctx, int on);
-/* names: "assign", "cost", "grid", "finalize", "sa_step" (device-resident search); returns total
- * ms and launch count. */
+/* names: "assign", "cost", "grid", "finalize", "sa_step" (device-resident search), "comm" (the
+ * per-evaluation RCCL all-reduce or all-gather, with a communicator); returns total ms and launch
+ * count (HIP events on the context stream). */
 int hq_profile_get(hq_ctx *ctx, const char *kernel, double *total_ms, int64_t *launches);
 int hq_profile_reset(hq_ctx *ctx);
 

@@ -1,6 +1,10 @@
 """HBM bytes per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes.
 
-    python scripts/pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json [config-json]
+    python scripts/pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json CONFIG_JSON
+
+CONFIG_JSON names the profiled run ({"size": 4096, "K": 256, "P": 4, "grid": 32},
+plus "dpi"/"distance" off the default geometry): bench.py's roofline.traffic
+takes the newest file whose config matches its own run, so it is required.
 
 FETCH_DIR / WRITE_DIR are the -d directories of two separate
 `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE` passes
@@ -15,6 +19,7 @@ import csv
 import glob
 import json
 import sys
+import time
 
 
 def per_kernel(d, counter):
@@ -30,10 +35,16 @@ def per_kernel(d, counter):
 
 def main():
     fdir, wdir, out = sys.argv[1:4]
-    cfg = json.loads(sys.argv[4]) if len(sys.argv) > 4 else {}
+    if len(sys.argv) < 5:
+        sys.exit("pmc_traffic.py: the config JSON is required (bench.py matches on it)")
+    cfg = json.loads(sys.argv[4])
+    for key in ("size", "K", "P", "grid"):
+        if key not in cfg:
+            sys.exit(f"pmc_traffic.py: config needs '{key}'")
     fetch = per_kernel(fdir, "FETCH_SIZE")
     write = per_kernel(wdir, "WRITE_SIZE")
-    res = {"config": cfg, "unit": "bytes per launch",
+    res = {"config": cfg, "generated": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
+           "unit": "bytes per launch",
            "correction": "fetch_bytes = 2 x FETCH_SIZE (gfx950 wide-read tally); write as reported",
            "kernels": {}}
     for k in sorted(set(fetch) | set(write)):

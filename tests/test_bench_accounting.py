@@ -39,3 +39,37 @@ def test_measured_traffic_lookup():
     assert t is not None and 2.5e8 < t < 3.0e8  # the committed PMC passes (~271 MB per launch)
     assert bench.measured_traffic(4096, 256, 4, 32, 2, "cost16w_kernel") is None  # multi-GPU: none
     assert bench.measured_traffic(4096, 256, 4, 32, 1, "cost16w_kernel", dpi=96, distance=60.0) is None
+
+
+def test_measured_traffic_takes_the_newest_matching_file(tmp_path, monkeypatch):
+    """Any rNN*hbm_traffic.json counts; the newest round wins, then the latest
+    `generated` stamp; an empty config never matches."""
+    import json
+    import os
+
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    cfg = {"size": 4096, "K": 256, "P": 4, "grid": 32}
+
+    def put(name, traffic, config, generated=None):
+        d = {"config": config, "kernels": {"hq::cost16w_kernel<10, 0, true, 4, 1>": {"traffic_bytes": traffic}}}
+        if generated:
+            d["generated"] = generated
+        (prof / name).write_text(json.dumps(d))
+
+    put("r04_hbm_traffic.json", 100, cfg)
+    put("r04_wave_acc_hbm_traffic.json", 200, {})  # no config: never matches
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    assert bench.measured_traffic(4096, 256, 4, 32, 1, "cost16w_kernel") == 100
+    put("r05_a_hbm_traffic.json", 300, cfg, "2026-10-18T10:00:00Z")
+    put("r05_b_hbm_traffic.json", 400, cfg, "2026-10-18T09:00:00Z")
+    assert bench.measured_traffic(4096, 256, 4, 32, 1, "cost16w_kernel", with_source=True) == \
+        (300, "r05_a_hbm_traffic.json")
+    assert bench.measured_traffic(4096, 256, 8, 32, 1, "cost16w_kernel") is None
+    assert os.path.basename(str(tmp_path))  # (ROOT restored by monkeypatch)
+
+
+def test_profile_stages_and_single_rank_line():
+    assert "comm" not in bench.profiled_stages(1) and bench.profiled_stages(2)[-1] == "comm"
+    avg, mx = bench.kernel_profile({"cost": (0.35, 100), "assign": (0.15, 100)}, 1)
+    assert avg == {"cost": 0.35, "assign": 0.15} and mx is None

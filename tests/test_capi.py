@@ -122,3 +122,34 @@ def test_pack_filters_matches_im800():
     np.testing.assert_array_equal(k2, f.k2)
     np.testing.assert_array_equal(k3, f.k3)
     np.testing.assert_array_equal(ak3, f.absk3)
+
+
+CSRC = os.path.join(ROOT, "hybridquantization_amd", "csrc")
+
+
+def test_every_ablation_switch_is_guarded():
+    """Every HQ_ABL_* name used in the kernel sources is in hq_device.h's
+    #error guard, so no ablation (wrong results by design) builds by accident."""
+    guard = open(os.path.join(CSRC, "hq_device.h")).read()
+    guard = guard[guard.index("#if !defined(HQ_ABLATION_BUILD)"):guard.index("#error")]
+    listed = set(re.findall(r"defined\((HQ_ABL_\w+)\)", guard))
+    used = set()
+    for f in os.listdir(CSRC):
+        if f.endswith((".hip", ".h", ".cpp")) and f != "hq_device.h":
+            used |= set(re.findall(r"\b(HQ_ABL_\w+)", open(os.path.join(CSRC, f)).read()))
+    assert used, "no ablation switches found (the scan is broken)"
+    assert used <= listed, sorted(used - listed)
+
+
+def test_ablation_define_without_opt_in_fails_to_compile():
+    """A stray -DHQ_ABL_* (without HQ_ABLATION_BUILD) stops the build."""
+    import shutil
+    import subprocess
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("no hipcc")
+    cmd = [hipcc, "--offload-arch=gfx950", "-std=c++17", "-E", "-o", os.devnull, os.path.join(CSRC, "hq_wide.hip")]
+    assert subprocess.run(cmd, capture_output=True).returncode == 0
+    bad = subprocess.run(cmd + ["-DHQ_ABL_NOFILL"], capture_output=True, text=True)
+    assert bad.returncode != 0 and "HQ_ABLATION_BUILD" in bad.stderr
+    assert subprocess.run(cmd + ["-DHQ_ABL_NOFILL", "-DHQ_ABLATION_BUILD"], capture_output=True).returncode == 0

@@ -51,8 +51,15 @@ def _worker(rank, world, port, out):
 
     uid = hqd.broadcast_unique_id(dist, rank, lambda: bytes(range(128)))
     el = hqd.max_over_ranks(dist, 0.5 + rank)
+    # bench.py's N > 1 profile line: per-stage averages incl. the collective, max over ranks
+    import bench
+
+    stages = bench.profiled_stages(world)
+    prof = {k: (1.0 + i + (0.25 if (rank == 1) == (i % 2 == 0) else 0.0), 10) for i, k in enumerate(stages)}
+    avg, mx = bench.kernel_profile(prof, world, lambda v: hqd.max_each_over_ranks(dist, v))
     if rank == 0:
-        out.put((part.numpy(), uid, el, hqd.shard_rows(H, world, rank), hqd.shard_rows(H, world, 1)))
+        out.put((part.numpy(), uid, el, hqd.shard_rows(H, world, rank), hqd.shard_rows(H, world, 1),
+                 stages, avg, mx))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -71,11 +78,15 @@ def test_row_block_shards_allreduce_matches_full(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    red, uid, el, b0, b1 = q.get(timeout=240)
+    red, uid, el, b0, b1, stages, avg, mx = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     assert uid == bytes(range(128)) and el == 1.5
+    assert stages[-1] == "comm" and set(avg) == set(mx) == set(stages)
+    for i, k in enumerate(stages):  # rank 0's own averages; the max picks the larger rank's
+        assert avg[k] == 1.0 + i + (0.0 if i % 2 == 0 else 0.25)
+        assert mx[k] == 1.25 + i
     assert b0 == (0, H // 2) and b1 == (H // 2, H)
     f, rgb3, lab, pals = _inputs()
     rgba = o.inline_rgba(rgb3[:, 0], rgb3[:, 1], rgb3[:, 2])

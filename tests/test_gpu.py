@@ -794,7 +794,9 @@ def test_device_search_with_single_rank_comm(gpu, filt, split):
     """The multi-GPU search loop on one GPU: with libhq's RCCL communicator the
     all-reduce (split 0: row blocks) or the all-gather (split 1: option
     palette_split) sits between finalize and sa_step in every iteration; with
-    one rank the trajectory must be the one without a communicator."""
+    one rank the trajectory must be the one without a communicator.  The last
+    10 iterations run profiled: the collective is event-timed once per
+    iteration ("comm", bench.py's N > 1 line), and only with a communicator."""
     import ctypes as C
     w, h, K, P = 80, 72, 24, 4
     R, G, B = o.synthetic_image(w, h, seed=12)
@@ -807,32 +809,45 @@ def test_device_search_with_single_rank_comm(gpu, filt, split):
         m.setOption("palette_split", split)
         if comm:
             m.initComm(1, 0, hq.ImageManipulation.commUniqueId())
-        sw = hq.SWASA(population=P, imax=30, seed=21, t0=0.05)
+        sw = hq.SWASA(population=P, imax=40, seed=21, t0=0.05)
         params = sw.params()
         handle = C.c_void_p()
         hq._lib.check(lib.hq_search_create(m.ctx, C.byref(params), K, sw.seed, C.byref(handle)), m.ctx)
         ran = C.c_int()
         hq._lib.check(lib.hq_search_run(handle, 30, C.byref(ran)), m.ctx)
+        assert ran.value == 30
+        lib.hq_profile_reset(m.ctx)
+        lib.hq_profile_enable(m.ctx, 1)
+        hq._lib.check(lib.hq_search_run(handle, 10, C.byref(ran)), m.ctx)
+        lib.hq_profile_enable(m.ctx, 0)
+        for stage, want in (("comm", 10 if comm else 0), ("cost", 10), ("sa_step", 10)):
+            ms, n = C.c_double(), C.c_int64()
+            hq._lib.check(lib.hq_profile_get(m.ctx, stage.encode(), C.byref(ms), C.byref(n)), m.ctx)
+            assert n.value == want and (ms.value > 0) == (want > 0), (stage, comm, n.value, ms.value)
         best = np.zeros(4 * K, np.float32)
         err = C.c_double()
         it = C.c_int()
         hq._lib.check(lib.hq_search_best(handle, hq._lib.fptr(best), C.byref(err), C.byref(it)), m.ctx)
         lib.hq_search_destroy(handle)
         m.close()
-        res.append((best, err.value, ran.value))
-    assert res[0][2] == res[1][2] == 30
+        res.append((best, err.value, it.value))
+    assert res[0][2] == res[1][2] == 40
     assert res[0][1] == res[1][1]
     np.testing.assert_array_equal(res[0][0], res[1][0])
 
 
-@pytest.mark.parametrize("K,P,ranks", [(64, 8, 2), (64, 8, 4), (256, 12, 3), (600, 4, 2)])
-def test_palette_slices_sum_to_full(gpu, filt, K, P, ranks):
+@pytest.mark.parametrize("K,P,ranks,opts", [(64, 8, 2, {}), (64, 8, 4, {}), (256, 12, 3, {}), (600, 4, 2, {}),
+                                             (5000, 4, 2, {}), (600, 4, 2, {"chunked": 0}),
+                                             (300, 6, 3, {"grid": 0})])
+def test_palette_slices_sum_to_full(gpu, filt, K, P, ranks, opts):
     """The palette split (option palette_split with a communicator):
     rank r evaluates palettes [r P/N, (r+1) P/N) of the whole image.  Here the
     ranks are contexts on one GPU with the test-only slice options: each slice's
     rows of hq_eval_population_partial equal the full evaluation's bit for bit
     (sums and used flags; the other rows read 0), and so do the indices of the
-    slice's palettes; K = 600 runs chunked palettes."""
+    slice's palettes; K = 600 runs chunked palettes.  K = 5000, chunked 0 and
+    grid 0 run the wide (exhaustive K > 256) path, which must take the same
+    slice (a rank that evaluated every palette would count each N times)."""
     w, h = 160, 120
     R, G, B = o.synthetic_image(w, h, seed=K + P)
     rgba = o.inline_rgba(R, G, B).reshape(-1)
@@ -843,6 +858,8 @@ def test_palette_slices_sum_to_full(gpu, filt, K, P, ranks):
         m = hq.ImageManipulation(device=gpu)
         hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
         m.setImage(rgba, None, w, filt.illum)
+        for k, v in opts.items():
+            m.setOption(k, v)
         if slice_rank is not None:
             m.setOption("slice_ranks", ranks)
             m.setOption("slice_rank", slice_rank)
@@ -872,6 +889,29 @@ def test_palette_slices_sum_to_full(gpu, filt, K, P, ranks):
         assert not part[others].any()
         for p, v in idx.items():
             np.testing.assert_array_equal(v, idx_full[p])
+
+
+def test_palette_slice_rank_out_of_range(gpu, filt):
+    """slice_rank must lie in [0, slice_ranks): a rank past the last slice is
+    refused with HQ_ERR_ARG before anything is enqueued (it would address
+    palette rows past the population)."""
+    w, h, K, P = 64, 48, 16, 4
+    R, G, B = o.synthetic_image(w, h, seed=5)
+    rgba = o.inline_rgba(R, G, B).reshape(-1)
+    pals = np.stack([o.synthetic_palette(K, 2 + p) for p in range(P)]).reshape(P, -1)
+    m = hq.ImageManipulation(device=gpu)
+    hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
+    m.setImage(rgba, None, w, filt.illum)
+    with pytest.raises(hq.HQError):
+        m.setOption("slice_rank", -1)
+    m.setOption("slice_ranks", 2)
+    m.setOption("slice_rank", 2)
+    with pytest.raises(hq.HQError):
+        m.computeQuantizationErrorPopulation(pals, 2.0)
+    m.setOption("slice_rank", 1)
+    costs = m.computeQuantizationErrorPopulation(pals, 2.0)  # rows 0, 1 read 0 (the other slice)
+    assert np.isfinite(costs[2:]).all()
+    m.close()
 
 
 # ---------------------------------------------------------------------------
@@ -1238,8 +1278,10 @@ def test_pixel_errors_vs_oracle(gpu, case, variant):
     (the reference's summation order); 300 dpi / 50 cm (half 51) takes the
     generic path whatever the variant.  Every pixel's dE -- border
     pixels (reflection, CL:256-263), pixels in the linear Lab segment, edge and
-    partial tiles -- within 2e-5 absolute of the oracle's error image (same
-    LabRef on both sides), and the indices bit-exact."""
+    partial tiles -- within 2e-4 absolute of the oracle's error image (same
+    LabRef on both sides), at most 2x the oracle's own worst distance from a
+    float64 evaluation and 1.5x its mean (the comment below says why the bar is
+    relative to float64), and the indices bit-exact."""
     if case.startswith("case_"):
         g, R, G, B = load_case(case)
         w, h = int(g["w"]), int(g["h"])
