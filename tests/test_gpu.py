@@ -904,13 +904,20 @@ def test_palette_slice_rank_out_of_range(gpu, filt):
     m.setImage(rgba, None, w, filt.illum)
     with pytest.raises(hq.HQError):
         m.setOption("slice_rank", -1)
+    lib = hq.load()
+    out = np.zeros(P * (1 + K))
+
+    def partial():
+        return lib.hq_eval_population_partial(m.ctx, hq._lib.fptr(np.ascontiguousarray(pals)), P, K,
+                                              out.ctypes.data_as(hq._lib._d))
+
     m.setOption("slice_ranks", 2)
     m.setOption("slice_rank", 2)
-    with pytest.raises(hq.HQError):
-        m.computeQuantizationErrorPopulation(pals, 2.0)
+    assert partial() == hq._lib.HQ_ERR_ARG and "outside" in lib.hq_last_error(m.ctx).decode()
     m.setOption("slice_rank", 1)
-    costs = m.computeQuantizationErrorPopulation(pals, 2.0)  # rows 0, 1 read 0 (the other slice)
-    assert np.isfinite(costs[2:]).all()
+    assert partial() == 0
+    rows = out.reshape(P, 1 + K)
+    assert not rows[:2].any() and (rows[2:, 0] > 0).all()  # rows 0, 1: the other slice
     m.close()
 
 
