@@ -1,16 +1,18 @@
-# Same-box A/B of bench variants: each line of $VARIANTS (';'-separated option lists,
-# e.g. "cost_rows=8;cost_rows=16") runs bench.py twice, alternating; one JSON per run.
+# Same-box A/B of library builds and options, alternating, REPS rounds.
+#   VARIANTS="label=lib.so:opt=v,opt=v;label2=lib2.so:"  (libs under hybridquantization_amd/)
+#   BENCH_ARGS (default "--no-full-search --steps 200 --warmup 30"), REPS (default 2)
+# One JSON per run under gpurun_out/ab/, one summary line per run on stdout.
 set -u
 mkdir -p gpurun_out/ab
-i=0
-for rep in 1 2; do
-  IFS=';' read -ra VS <<< "$VARIANTS"
+IFS=';' read -ra VS <<< "$VARIANTS"
+for rep in $(seq 1 ${REPS:-2}); do
   for v in "${VS[@]}"; do
-    i=$((i+1)); opts=""
-    for kv in $v; do opts="$opts --opt $kv"; done
-    timeout -k 10 300 python bench.py --no-cpu-baseline --steps ${STEPS:-100} $opts ${BENCH_ARGS:-} > gpurun_out/ab/run$i.json 2> gpurun_out/ab/run$i.err
+    label=${v%%=*}; rest=${v#*=}; lib=${rest%%:*}; optstr=${rest#*:}
+    opts=""; IFS=',' read -ra OS <<< "$optstr"; for kv in "${OS[@]}"; do [ -n "$kv" ] && opts="$opts --opt $kv"; done
+    out=gpurun_out/ab/$label.$rep
+    HQ_LIB_PATH=hybridquantization_amd/$lib timeout -k 10 200 python bench.py --no-cpu-baseline ${BENCH_ARGS:---no-full-search --steps 200 --warmup 30} $opts > $out.json 2> $out.err
     rc=$?
-    python3 -c "import json,sys; d=json.load(open('gpurun_out/ab/run$i.json')); print('$v', d['value'], d['ms_per_step'], d['kernel_avg_ms'])" || { echo "rc=$rc"; tail -5 gpurun_out/ab/run$i.err; }
-    if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then exit $rc; fi
+    python3 -c "import json; d=json.load(open('$out.json')); k=d['kernel_avg_ms']; print('$label', '$rep', d['value'], d['ms_per_step'], 'cost', k['cost'], 'assign', k['assign'], 'grid', k['grid'], 'sa', k['sa_step'])" || { echo "$label rc=$rc"; tail -3 $out.err; }
+    if [ $rc -ne 0 ]; then exit $rc; fi
   done
 done
