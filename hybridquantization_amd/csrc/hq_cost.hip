@@ -551,6 +551,12 @@ __global__ __launch_bounds__(256, 6) void cost_mfma_kernel(CostArgs a, int P_) {
 //   channel 1's horizontal pass.  HB = 10: 39,584 B of LDS.
 // ----------------------------------------------------------------------------
 constexpr int kTH16 = 16;
+#ifndef HQ_HROW4
+#define HQ_HROW4 1  // tiled generic path: 4 outputs per thread in the horizontal pass (gen_hrow4)
+#endif
+#ifndef HQ_LAB_SKIPLIN
+#define HQ_LAB_SKIPLIN 1  // cost16w: skip the linear Lab segment when no pixel of the wave is in it
+#endif
 #ifndef HQ_LAB_NT
 #define HQ_LAB_NT 0  // 1: LabRef read with non-temporal loads (streamed past the caches)
 #endif
@@ -1030,6 +1036,35 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
     hpass_wide<HB, 0, T2, WH>(hsrc, jr, taps, 6, 1, PLANE4, acc2);
 
     float e[2][HR];
+#if HQ_LAB_SKIPLIN
+    // t = X/Xn, Y/Yn, Z/Zn of the item's 8 pixels; when no t of the wave is in
+    // the linear Lab segment (t <= delta^3: near-black filtered colours, rare),
+    // the cube roots alone (lab_f_root), else lab_f_fast's select (same values)
+    float3 tf[2][HR];
+    float tmin = INFINITY;
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int xo = 0; xo < HR; ++xo) {
+            const float o0 = acc0[xo][r], o1 = acc1[xo][r], o2 = acc2[xo][r];
+            tf[r][xo] = make_float3(dot3(o0, o1, o2, a.m_lab + 0), dot3(o0, o1, o2, a.m_lab + 3),
+                                    dot3(o0, o1, o2, a.m_lab + 6));
+            tmin = fminf(tmin, fminf(tf[r][xo].x, fminf(tf[r][xo].y, tf[r][xo].z)));  // (v_min3; a NaN t drops out)
+        }
+    if (__builtin_amdgcn_ballot_w64(!(tmin > LAB_DELTA3)) == 0) {
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int xo = 0; xo < HR; ++xo)
+                tf[r][xo] = make_float3(lab_f_root(tf[r][xo].x), lab_f_root(tf[r][xo].y), lab_f_root(tf[r][xo].z));
+    } else {
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int xo = 0; xo < HR; ++xo)
+                tf[r][xo] = make_float3(lab_f_fast(tf[r][xo].x), lab_f_fast(tf[r][xo].y), lab_f_fast(tf[r][xo].z));
+    }
+#endif
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
         const float Ls[4] = {lab[r][0].x, lab[r][0].y, lab[r][0].z, lab[r][0].w};
@@ -1039,6 +1074,8 @@ __global__ __launch_bounds__(64 * NW, (cost16w_waves<HB, NCH>())) void cost16w_k
         for (int xo = 0; xo < HR; ++xo) {
 #ifdef HQ_ABL_NOLAB  // timing ablation (wrong results): no Opp->Lab / dE
             e[r][xo] = (acc0[xo][r] + acc1[xo][r]) + (acc2[xo][r] + (Ls[xo] + As[xo] + Bs[xo]));
+#elif HQ_LAB_SKIPLIN
+            e[r][xo] = delta_e_f<DE>(Ls[xo], As[xo], Bs[xo], tf[r][xo]);
 #else
             const float3 lf = opp2f_fast(acc0[xo][r], acc1[xo][r], acc2[xo][r], a.m_lab);
             e[r][xo] = delta_e_f<DE>(Ls[xo], As[xo], Bs[xo], lf);
@@ -1186,6 +1223,71 @@ __global__ __launch_bounds__(256) void gen_hrow_kernel(GenArgs a) {
     a.t[q] = t1x; a.t[n + q] = t1y; a.t[2 * n + q] = t1z;
     a.t[3 * n + q] = t2x; a.t[4 * n + q] = t2y; a.t[5 * n + q] = t2z;
     a.t[6 * n + q] = t3;
+}
+
+// gen_hrow4: the same horizontal pass with 4 adjacent outputs per thread
+// (grid (ceil(W / 1024), rows), block 256): a thread slides a window of 7
+// colours over its taps in chunks of 4 -- 4 new ds_read_b128 per 4 taps and
+// 112 FMAs, against 4 reads per 28 FMAs above, which left gen_hrow bound by
+// the LDS reads at large half-widths.  The row segment sits in LDS permuted
+// (element e at slot (e & 3) Q + e / 4), so the 64 lanes of a read hit
+// consecutive slots.  Each output sums its taps in ascending order (CL:254-
+// 267), so the planes equal gen_hrow's bit for bit.
+constexpr int kHr4Seg = 1024;  // outputs per workgroup row segment
+template <typename IT>
+__global__ __launch_bounds__(256) void gen_hrow4_kernel(GenArgs a) {
+    extern __shared__ float4 s_opp[];  // [4][Q] permuted, Q = (kHr4Seg + 2 half + 7) / 4 + 1
+    const int tid = threadIdx.x, half = a.half, W = a.g.W, T = 2 * half + 1;
+    const int x0 = blockIdx.x * kHr4Seg, ly = blockIdx.y;
+    const int Q = (kHr4Seg + 2 * half + 7) / 4 + 1;
+    const IT* row = static_cast<const IT*>(a.idx) + (int64_t)ly * W;
+    for (int e = tid; e < 4 * Q; e += 256) {
+        const int x = min(x0 - half + e, W - 1 + half);  // (past the row end: reflected, unused)
+        s_opp[(e & 3) * Q + (e >> 2)] = a.opp[row[reflect_only(x, W)]];
+    }
+    __syncthreads();
+    float acc[7][4];
+#pragma unroll
+    for (int f = 0; f < 7; ++f)
+#pragma unroll
+        for (int xo = 0; xo < 4; ++xo) acc[f][xo] = 0.f;
+    // window w[i] = element 4 tid + t0 + i of the segment, i = 0 .. 6
+    auto rd = [&](int e) { return s_opp[(e & 3) * Q + (e >> 2)]; };
+    float4 w[7];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) w[i] = rd(4 * tid + i);
+    for (int t0 = 0; t0 < T; t0 += 4) {
+#pragma unroll
+        for (int i = 3; i < 7; ++i) w[i] = rd(4 * tid + t0 + i);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const int t = t0 + d;
+            if (t < T) {  // (uniform)
+                const float k1x = a.k1[4 * t + 0], k1y = a.k1[4 * t + 1], k1z = a.k1[4 * t + 2];
+                const float k2x = a.k2[4 * t + 0], k2y = a.k2[4 * t + 1], k2z = a.k2[4 * t + 2];
+                const float k3 = a.k3[t];
+#pragma unroll
+                for (int xo = 0; xo < 4; ++xo) {
+                    const float4 in = w[d + xo];
+                    acc[0][xo] = fmaf(in.x, k1x, acc[0][xo]);
+                    acc[1][xo] = fmaf(in.y, k1y, acc[1][xo]);
+                    acc[2][xo] = fmaf(in.z, k1z, acc[2][xo]);
+                    acc[3][xo] = fmaf(in.x, k2x, acc[3][xo]);
+                    acc[4][xo] = fmaf(in.y, k2y, acc[4][xo]);
+                    acc[5][xo] = fmaf(in.z, k2z, acc[5][xo]);
+                    acc[6][xo] = fmaf(in.x, k3, acc[6][xo]);
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) w[i] = w[i + 4];
+    }
+    const int64_t n = a.g.n_ext, q0 = (int64_t)ly * W + x0 + 4 * tid;
+#pragma unroll
+    for (int xo = 0; xo < 4; ++xo)
+        if (x0 + 4 * tid + xo < W)
+#pragma unroll
+            for (int f = 0; f < 7; ++f) a.t[f * n + q0 + xo] = acc[f][xo];
 }
 
 constexpr int kVtTile = 64, kVtRows = 16;  // gen_vtile: 64 x 64 tiles, 16 output rows per thread
@@ -1552,11 +1654,23 @@ hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, bool trim, int ti
 hipError_t launch_cost_tiled_generic(const GenArgs& a, int de, int idx_bytes, hipStream_t s) {
     const hipEvent_t ev0 = t_ev_start, ev1 = t_ev_stop;
     t_ev_stop = nullptr;
-    const dim3 hg((unsigned)((a.g.W + 255) / 256), (unsigned)(a.g.e1 - a.g.e0));
-    const size_t hl = sizeof(float4) * (256 + 2 * (size_t)a.half);
-    if (idx_bytes == 4) HQ_LAUNCH(gen_hrow_kernel<uint32_t>, hg, dim3(256), hl, s, a);
-    else if (idx_bytes == 2) HQ_LAUNCH(gen_hrow_kernel<uint16_t>, hg, dim3(256), hl, s, a);
-    else HQ_LAUNCH(gen_hrow_kernel<uint8_t>, hg, dim3(256), hl, s, a);
+    if (HQ_HROW4) {
+        const dim3 hg((unsigned)((a.g.W + kHr4Seg - 1) / kHr4Seg), (unsigned)(a.g.e1 - a.g.e0));
+        const size_t hl = sizeof(float4) * 4 * (size_t)((kHr4Seg + 2 * a.half + 7) / 4 + 1);
+        auto go = [&](auto kern) {
+            if (!allow_dyn_lds(reinterpret_cast<const void*>(kern), hl)) return;  // (the caller's hipGetLastError)
+            HQ_LAUNCH(kern, hg, dim3(256), hl, s, a);
+        };
+        if (idx_bytes == 4) go(gen_hrow4_kernel<uint32_t>);
+        else if (idx_bytes == 2) go(gen_hrow4_kernel<uint16_t>);
+        else go(gen_hrow4_kernel<uint8_t>);
+    } else {
+        const dim3 hg((unsigned)((a.g.W + 255) / 256), (unsigned)(a.g.e1 - a.g.e0));
+        const size_t hl = sizeof(float4) * (256 + 2 * (size_t)a.half);
+        if (idx_bytes == 4) HQ_LAUNCH(gen_hrow_kernel<uint32_t>, hg, dim3(256), hl, s, a);
+        else if (idx_bytes == 2) HQ_LAUNCH(gen_hrow_kernel<uint16_t>, hg, dim3(256), hl, s, a);
+        else HQ_LAUNCH(gen_hrow_kernel<uint8_t>, hg, dim3(256), hl, s, a);
+    }
     t_ev_start = nullptr;
     t_ev_stop = ev1;
     const int tiles_x = (a.g.W + kVtTile - 1) / kVtTile, tiles_y = (a.g.r1 - a.g.r0 + kVtTile - 1) / kVtTile;

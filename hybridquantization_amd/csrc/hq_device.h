@@ -69,6 +69,13 @@ __device__ __forceinline__ float lab_f_fast(float t) {
     return t > LAB_DELTA3 ? y : lin;
 }
 
+// lab_f_fast's cube-root branch alone: for a wave whose every t is above
+// delta^3 (the caller's ballot), the linear segment and the select are dead.
+// (A NaN t gives NaN either way.)
+__device__ __forceinline__ float lab_f_root(float t) {
+    return __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(t) * (1.0f / 3.0f));
+}
+
 // (f(X/Xn), f(Y/Yn), f(Z/Zn)) of an opponent colour: L = 116 f.y - 16,
 // a = 500 (f.x - f.y), b = 200 (f.y - f.z).
 __device__ __forceinline__ float3 opp2f_fast(float o0, float o1, float o2, const float* m) {
