@@ -551,9 +551,6 @@ __global__ __launch_bounds__(256, 6) void cost_mfma_kernel(CostArgs a, int P_) {
 //   channel 1's horizontal pass.  HB = 10: 39,584 B of LDS.
 // ----------------------------------------------------------------------------
 constexpr int kTH16 = 16;
-#ifndef HQ_HROW4
-#define HQ_HROW4 1  // tiled generic path: 4 outputs per thread in the horizontal pass (gen_hrow4)
-#endif
 #ifndef HQ_LAB_SKIPLIN
 #define HQ_LAB_SKIPLIN 1  // cost16w: skip the linear Lab segment when no pixel of the wave is in it
 #endif
@@ -1241,9 +1238,25 @@ __global__ __launch_bounds__(256) void gen_hrow4_kernel(GenArgs a) {
     const int x0 = blockIdx.x * kHr4Seg, ly = blockIdx.y;
     const int Q = (kHr4Seg + 2 * half + 7) / 4 + 1;
     const IT* row = static_cast<const IT*>(a.idx) + (int64_t)ly * W;
-    for (int e = tid; e < 4 * Q; e += 256) {
-        const int x = min(x0 - half + e, W - 1 + half);  // (past the row end: reflected, unused)
-        s_opp[(e & 3) * Q + (e >> 2)] = a.opp[row[reflect_only(x, W)]];
+    // the segment's colours, 8 per thread and batch: every index load of a batch
+    // first, then every table load, then the stores (one dependent pair of round
+    // trips per batch; a load -> load -> store loop paid two per element)
+    for (int e0 = 0; e0 < 4 * Q; e0 += 8 * 256) {
+        uint32_t ix[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int e = min(e0 + tid + 256 * u, 4 * Q - 1);
+            const int x = min(x0 - half + e, W - 1 + half);  // (past the row end: reflected, unused)
+            ix[u] = (uint32_t)row[reflect_only(x, W)];
+        }
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = a.opp[ix[u]];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int e = e0 + tid + 256 * u;
+            if (e < 4 * Q) s_opp[(e & 3) * Q + (e >> 2)] = v[u];
+        }
     }
     __syncthreads();
     float acc[7][4];
@@ -1310,11 +1323,22 @@ __global__ __launch_bounds__(256) void gen_vtile_kernel(GenArgs a, int tiles_x) 
         const float* plane = a.t + (int64_t)f * n;
         const float* vt = a.vtaps + f * a.vtap_pitch;  // zero-padded to a multiple of 16
         __syncthreads();  // (the previous filter's window reads)
-        for (int e = tid; e < RH * TW; e += 256) {
-            const int i = e / TW, j = e % TW;
-            int gy = reflect_clamp(y0 - half + i, g.H);
-            gy = min(max(gy, g.e0), g.e1 - 1);
-            s_win[e] = plane[(int64_t)(gy - g.e0) * g.W + min(x0 + j, g.W - 1)];
+        // the window rows, 16 loads per thread in flight per batch (a load ->
+        // store loop paid one memory round trip per element: ~42 per filter at
+        // half 51, most of the kernel's time)
+        const int jx = min(x0 + (tid & (TW - 1)), g.W - 1);
+        for (int e0 = 0; e0 < RH * TW; e0 += 16 * 256) {
+            float v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int i = min(e0 + tid + 256 * u, RH * TW - 1) / TW;  // (clamped: loaded, not stored)
+                int gy = reflect_clamp(y0 - half + i, g.H);
+                gy = min(max(gy, g.e0), g.e1 - 1);
+                v[u] = plane[(int64_t)(gy - g.e0) * g.W + jx];
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                if (e0 + tid + 256 * u < RH * TW) s_win[e0 + tid + 256 * u] = v[u];
         }
         __syncthreads();
         float o[RB];
@@ -1654,7 +1678,7 @@ hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, bool trim, int ti
 hipError_t launch_cost_tiled_generic(const GenArgs& a, int de, int idx_bytes, hipStream_t s) {
     const hipEvent_t ev0 = t_ev_start, ev1 = t_ev_stop;
     t_ev_stop = nullptr;
-    if (HQ_HROW4) {
+    if (a.hrow4) {  // (option gen_hrow4, default on; gen_hrow stays as its bitwise cross-check)
         const dim3 hg((unsigned)((a.g.W + kHr4Seg - 1) / kHr4Seg), (unsigned)(a.g.e1 - a.g.e0));
         const size_t hl = sizeof(float4) * 4 * (size_t)((kHr4Seg + 2 * a.half + 7) / 4 + 1);
         auto go = [&](auto kern) {

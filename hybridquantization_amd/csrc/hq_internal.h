@@ -226,6 +226,7 @@ struct GenArgs {
     float* pix_err;  // this palette's per-pixel dE of the owned rows (test option), or null
     const float* vtaps;  // tiled path: [7][vtap_pitch] vertical taps per plane, zero-padded
     int vtap_pitch;      // (2 half + 1 rounded up to 16, + 16)
+    int hrow4 = 1;       // tiled path: horizontal pass with 4 outputs per thread (gen_hrow4), else gen_hrow
 };
 
 }  // namespace hq

@@ -204,6 +204,9 @@ int hq_profile_reset(hq_ctx *ctx);
  *   "cost_variant" 0 = fast tiled path (default; filters up to halfSize 24), 1 = generic
  *                  two-pass path, LDS-tiled (any filter length; halfSize > 24 takes it),
  *                  2 = the generic pair per pixel in the reference's summation order
+ *   "gen_hrow4"    the LDS-tiled generic path's horizontal pass: 1 (default) = 4 adjacent
+ *                  outputs per thread over a sliding window, 0 = one output per thread
+ *                  (same planes bit for bit)
  *   "cost_rows"    fast path tiles: 16 (16 x 128 outputs, default) or 8 (8 x 108)
  *   "cost_tw"      16-row tiles at the default filter width: 128 columns (4 waves,
  *                  default) or 256 (8 waves per workgroup)

@@ -172,6 +172,37 @@ def test_fast_path_matches_generic(gpu, de, trim, rows, tw):
     m.close()
 
 
+@pytest.mark.parametrize("w,h,dpi,vd", [(300, 61, 300, 50.0), (1100, 60, 300, 50.0), (1029, 33, 72, 45.0),
+                                         (97, 53, 150, 30.0)])
+def test_generic_hrow4_bitwise(gpu, w, h, dpi, vd):
+    """The LDS-tiled generic path's horizontal pass with 4 adjacent outputs per
+    thread (option gen_hrow4, default) gives the one-output kernel's per-pixel
+    dE and sums bit for bit: both sum each output's taps in ascending order.
+    Segments of 1,024 outputs: 1,100 and 1,029 columns end in partial
+    segments; 300 dpi / 50 cm is 103 taps (half 51, not a multiple of 4)."""
+    R, G, B = o.synthetic_image(w, h, seed=w * h)
+    lib = hq.load()
+    m = hq.ImageManipulation(device=gpu)
+    sp = hq.ScielabProcessor(dpi, vd, hq.Whitepoint.D65, None, m)
+    m.setImage(o.inline_rgba(R, G, B).reshape(-1), None, w, sp.illuminant)
+    m.setOption("cost_variant", 1)
+    m.setOption("pixel_err", 1)
+    K, P = 64, 2
+    pals = np.stack([o.synthetic_palette(K, 9 + p) for p in range(P)]).reshape(P, -1)
+    res = []
+    for h4 in (0, 1):
+        m.setOption("gen_hrow4", h4)
+        out = np.zeros(P * (1 + K))
+        hq._lib.check(lib.hq_eval_population_partial(m.ctx, hq._lib.fptr(np.ascontiguousarray(pals)), P, K,
+                                                     out.ctypes.data_as(hq._lib._d)), m.ctx)
+        res.append((out, [m.getPixelErrors(p) for p in range(P)]))
+    m.close()
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    for p in range(P):
+        np.testing.assert_array_equal(res[0][1][p], res[1][1][p])
+    assert (res[1][0].reshape(P, 1 + K)[:, 0] > 0).all()
+
+
 @pytest.mark.parametrize("dpi,vd", [(150, 30.0), (96, 60.0), (200, 30.0)])
 @pytest.mark.parametrize("de", [hq.deltaETypes.CIE76, hq.deltaETypes.CIE94])
 def test_fast_path_matches_generic_wide_buckets(gpu, de, dpi, vd):
@@ -493,7 +524,7 @@ def test_wide_palette_vs_oracle(gpu, filt, K, P):
     m.close()
 
 
-@pytest.mark.parametrize("K", [512, 1024, 2048])
+@pytest.mark.parametrize("K", [512, 1024, 2048, 4096, 3000])
 def test_chunked_palettes_match_exhaustive(gpu, filt, K):
     """The chunked K > 256 path (grid per 256-colour chunk, winners combined by
     the reference distance, hq_assign.hip) against the exhaustive one (option
