@@ -1296,11 +1296,17 @@ __global__ __launch_bounds__(256) void gen_hrow4_kernel(GenArgs a) {
         for (int i = 0; i < 3; ++i) w[i] = w[i + 4];
     }
     const int64_t n = a.g.n_ext, q0 = (int64_t)ly * W + x0 + 4 * tid;
+    if ((W & 3) == 0 && x0 + 4 * tid + 3 < W) {  // (planes of n_ext = W rows floats: 16-B aligned)
 #pragma unroll
-    for (int xo = 0; xo < 4; ++xo)
-        if (x0 + 4 * tid + xo < W)
+        for (int f = 0; f < 7; ++f)
+            *reinterpret_cast<float4*>(a.t + f * n + q0) = make_float4(acc[f][0], acc[f][1], acc[f][2], acc[f][3]);
+    } else {
 #pragma unroll
-            for (int f = 0; f < 7; ++f) a.t[f * n + q0 + xo] = acc[f][xo];
+        for (int xo = 0; xo < 4; ++xo)
+            if (x0 + 4 * tid + xo < W)
+#pragma unroll
+                for (int f = 0; f < 7; ++f) a.t[f * n + q0 + xo] = acc[f][xo];
+    }
 }
 
 constexpr int kVtTile = 64, kVtRows = 16;  // gen_vtile: 64 x 64 tiles, 16 output rows per thread
@@ -1357,6 +1363,104 @@ __global__ __launch_bounds__(256) void gen_vtile_kernel(GenArgs a, int tiles_x) 
         }
         // planes: 0 t1.x, 1 t1.y, 2 t1.z, 3 t2.x, 4 t2.y, 5 t2.z, 6 t3 -> channels x y z x y z x
         const int chp = f == 6 ? 0 : f % 3;
+#pragma unroll
+        for (int j = 0; j < RB; ++j) {
+            if (chp == 0) acc[0][j] += o[j];
+            else if (chp == 1) acc[1][j] += o[j];
+            else acc[2][j] += o[j];
+        }
+    }
+    double part = 0.0;
+    const int gx = x0 + c;
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+        const int y = y0 + RB * rb + j;
+        if (gx < g.W && y < g.r1) {
+            const float3 lf = opp2f_fast(acc[0][j], acc[1][j], acc[2][j], a.m_lab);
+            const int64_t off = (int64_t)(y - g.r0) * g.lab_pitch + gx;
+            const float ef = delta_e_f<DE>(a.labL[off], a.labA[off], a.labB[off], lf);
+            if (a.pix_err) a.pix_err[(int64_t)(y - g.r0) * g.W + gx] = ef;  // test option: the per-pixel dE
+            part += (double)ef;
+        }
+    }
+    part = wave_sum_to_lane63(part);
+    if ((tid & 63) == 63) s_red[tid >> 6] = part;
+    __syncthreads();
+    if (tid == 0) acc_add(a.acc, a.P, a.p, blockIdx.x, (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]));
+}
+
+// gen_vtile2: the vertical pass on 32 x 64 output tiles (half <= kVt2MaxHalf)
+// with the filters' windows double-buffered in LDS and filled by LDS DMA
+// (global_load_lds_dword: no registers held): filter f + 1's window streams in
+// while filter f's taps run, so the fill's memory round trips hide behind the
+// FMAs (gen_vtile waits for each window between two barriers).  Thread
+// (column c = tid % 32, row block rb = tid / 32) owns output rows 8 rb .. 8 rb
+// + 7.  Element e of a window is row e / 32, column e % 32 -- a wave's DMA
+// instruction writes 64 consecutive LDS dwords, two window rows.  Same sums
+// in the same order as gen_vtile (filters one after another, each filter's
+// taps in chunks of 16), so every pixel's dE is bit-identical (the fixed-point
+// sums round per tile, and the tiles differ: 2^-20 per partial).
+constexpr int kVt2W = 32, kVt2MaxHalf = 64;
+#ifndef HQ_VT2_RB
+#define HQ_VT2_RB 8  // gen_vtile2: output rows per thread, tiles of 32 x 8 RB (16: 3.677 vs 3.619 ms at 300/50)
+#endif
+template <int DE, int RB>
+__global__ __launch_bounds__(256) void gen_vtile2_kernel(GenArgs a, int tiles_x) {
+    extern __shared__ float s_w2[];  // [2][8 RB + 2 half][32]
+    constexpr int TW = kVt2W, kVt2H = 8 * RB;
+    __shared__ double s_red[4];
+    const int tid = threadIdx.x, c = tid & (TW - 1), rb = tid >> 5;
+    const Geom& g = a.g;
+    const int x0 = (blockIdx.x % tiles_x) * TW, y0 = g.r0 + (blockIdx.x / tiles_x) * kVt2H;
+    const int half = a.half, RH = kVt2H + 2 * half, T = 2 * half + 1, NE = RH * TW;
+    const int64_t n = g.n_ext;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool rows_inside = y0 - half >= g.e0 && y0 - half >= 0 && y0 + kVt2H + half <= g.e1 && y0 + kVt2H + half <= g.H;
+    const int jx = min(x0 + c, g.W - 1);
+    auto issue = [&](int f, int b) {
+        const float* plane = a.t + (int64_t)f * n;
+        float* dst = s_w2 + b * NE;
+        for (int e0 = 0; e0 < NE; e0 += 256) {
+            const int e = e0 + tid;
+            if (e < NE) {
+                const int i = e >> 5;
+                int gy = y0 - half + i;
+                if (!rows_inside) {
+                    gy = reflect_clamp(gy, g.H);
+                    gy = min(max(gy, g.e0), g.e1 - 1);
+                }
+                const float* src = plane + (uint32_t)((gy - g.e0) * g.W + jx);
+                __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(dst + e0 + 64 * wv), 4, 0, 0);
+            }
+        }
+    };
+    float acc[3][RB];
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch)
+#pragma unroll
+        for (int j = 0; j < RB; ++j) acc[ch][j] = 0.f;
+    issue(0, 0);
+    for (int f = 0; f < kNumFilt; ++f) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's rows of window f have landed
+        __syncthreads();                     // every wave's rows; window f - 1's readers are done
+        if (f + 1 < kNumFilt) issue(f + 1, (f + 1) & 1);
+        const float* win = s_w2 + (f & 1) * NE;
+        const float* vt = a.vtaps + f * a.vtap_pitch;  // zero-padded to a multiple of 16
+        float o[RB];
+#pragma unroll
+        for (int j = 0; j < RB; ++j) o[j] = 0.f;
+        for (int k0 = 0; k0 < T; k0 += 16) {
+            float v[RB + 16];
+#pragma unroll
+            for (int i = 0; i < RB + 16; ++i) v[i] = win[min(RB * rb + k0 + i, RH - 1) * TW + c];
+#pragma unroll
+            for (int kk = 0; kk < 16; ++kk) {
+                const float w = vt[k0 + kk];
+#pragma unroll
+                for (int j = 0; j < RB; ++j) o[j] = fmaf(v[j + kk], w, o[j]);
+            }
+        }
+        const int chp = f == 6 ? 0 : f % 3;  // planes t1.xyz, t2.xyz, t3 -> channels x y z x y z x
 #pragma unroll
         for (int j = 0; j < RB; ++j) {
             if (chp == 0) acc[0][j] += o[j];
@@ -1697,6 +1801,19 @@ hipError_t launch_cost_tiled_generic(const GenArgs& a, int de, int idx_bytes, hi
     }
     t_ev_start = nullptr;
     t_ev_stop = ev1;
+    if (a.half <= kVt2MaxHalf && a.vtile2) {  // the double-buffered DMA form (option gen_vtile2)
+        constexpr int kVt2H = 8 * HQ_VT2_RB;
+        const int tx = (a.g.W + kVt2W - 1) / kVt2W, ty = (a.g.r1 - a.g.r0 + kVt2H - 1) / kVt2H;
+        const size_t l2 = sizeof(float) * 2 * kVt2W * (kVt2H + 2 * (size_t)a.half);
+        auto go2 = [&](auto kern) {
+            if (!allow_dyn_lds(reinterpret_cast<const void*>(kern), l2)) return;  // (the caller's hipGetLastError)
+            HQ_LAUNCH(kern, dim3((unsigned)(tx * ty)), dim3(256), l2, s, a, tx);
+        };
+        if (de == 0) go2(gen_vtile2_kernel<0, HQ_VT2_RB>);
+        else go2(gen_vtile2_kernel<1, HQ_VT2_RB>);
+        t_ev_start = ev0;
+        return hipGetLastError();
+    }
     const int tiles_x = (a.g.W + kVtTile - 1) / kVtTile, tiles_y = (a.g.r1 - a.g.r0 + kVtTile - 1) / kVtTile;
     const size_t vl = sizeof(float) * kVtTile * (kVtTile + 2 * (size_t)a.half);
     auto go = [&](auto kern) {

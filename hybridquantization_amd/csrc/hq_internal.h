@@ -227,6 +227,7 @@ struct GenArgs {
     const float* vtaps;  // tiled path: [7][vtap_pitch] vertical taps per plane, zero-padded
     int vtap_pitch;      // (2 half + 1 rounded up to 16, + 16)
     int hrow4 = 1;       // tiled path: horizontal pass with 4 outputs per thread (gen_hrow4), else gen_hrow
+    int vtile2 = 1;      // tiled path: double-buffered LDS-DMA vertical pass (gen_vtile2), else gen_vtile
 };
 
 }  // namespace hq

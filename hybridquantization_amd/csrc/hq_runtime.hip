@@ -152,6 +152,7 @@ struct hq_ctx {
     int cost_rows = 16;    // fast path tiles: 16 x 128 (cost16w_kernel) or 8 x 108 (cost_mfma_kernel)
     int cost_tw = HQ_COST_TW;  // 16-row tiles at HB = 10: 128 (4 waves) or 256 columns (8 waves; slower)
     int gen_hrow4 = 1;     // tiled generic path: 4 outputs per thread in the horizontal pass
+    int gen_vtile2 = 1;    // tiled generic path: double-buffered LDS-DMA vertical pass (half <= 64)
     int assign_blocks_per_cu = 0;  // 0 = auto: assign_pipe_kernel<NG>'s residency (the occupancy
                                    // query, assign_res[NG]), one round of workgroups, each
                                    // thread a grid-stride pixel sequence
@@ -518,6 +519,7 @@ int enqueue_generic_cost(hq_ctx* c, int P, const void* idx_base, int idx_bytes, 
         gn.vtaps = c->d_vtaps.as<float>();
         gn.vtap_pitch = c->vtap_pitch;
         gn.hrow4 = c->gen_hrow4;
+        gn.vtile2 = c->gen_vtile2;
         opp2xyz_over_illum(inv, gn.m_lab);
         // the events span every palette's launch pair: start on the first, stop on the last
         if (ev) set_launch_events(p == 0 ? ev[4] : nullptr, p == P - 1 ? ev[5] : nullptr);
@@ -1537,6 +1539,8 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
     } else if (!std::strcmp(name, "cost_rows")) {
         if (value != 8 && value != 16) return fail(c, HQ_ERR_ARG, "cost_rows must be 8 or 16");
         c->cost_rows = value;
+    } else if (!std::strcmp(name, "gen_vtile2")) {
+        c->gen_vtile2 = value != 0;
     } else if (!std::strcmp(name, "gen_hrow4")) {
         c->gen_hrow4 = value != 0;
     } else if (!std::strcmp(name, "cost_tw")) {

@@ -207,6 +207,9 @@ int hq_profile_reset(hq_ctx *ctx);
  *   "gen_hrow4"    the LDS-tiled generic path's horizontal pass: 1 (default) = 4 adjacent
  *                  outputs per thread over a sliding window, 0 = one output per thread
  *                  (same planes bit for bit)
+ *   "gen_vtile2"   the LDS-tiled generic path's vertical pass (halfSize <= 64): 1 (default) =
+ *                  32 x 64 tiles, windows double-buffered by LDS DMA; 0 = 64 x 64 tiles with
+ *                  one window at a time (same results bit for bit)
  *   "cost_rows"    fast path tiles: 16 (16 x 128 outputs, default) or 8 (8 x 108)
  *   "cost_tw"      16-row tiles at the default filter width: 128 columns (4 waves,
  *                  default) or 256 (8 waves per workgroup)

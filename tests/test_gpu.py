@@ -178,6 +178,8 @@ def test_generic_hrow4_bitwise(gpu, w, h, dpi, vd):
     """The LDS-tiled generic path's horizontal pass with 4 adjacent outputs per
     thread (option gen_hrow4, default) gives the one-output kernel's per-pixel
     dE and sums bit for bit: both sum each output's taps in ascending order.
+    The double-buffered vertical pass (gen_vtile2, default for half <= 64)
+    gives every pixel's dE bit for bit too.
     Segments of 1,024 outputs: 1,100 and 1,029 columns end in partial
     segments; 300 dpi / 50 cm is 103 taps (half 51, not a multiple of 4)."""
     R, G, B = o.synthetic_image(w, h, seed=w * h)
@@ -190,8 +192,9 @@ def test_generic_hrow4_bitwise(gpu, w, h, dpi, vd):
     K, P = 64, 2
     pals = np.stack([o.synthetic_palette(K, 9 + p) for p in range(P)]).reshape(P, -1)
     res = []
-    for h4 in (0, 1):
+    for h4, v2 in ((0, 0), (1, 0), (1, 1)):
         m.setOption("gen_hrow4", h4)
+        m.setOption("gen_vtile2", v2)
         out = np.zeros(P * (1 + K))
         hq._lib.check(lib.hq_eval_population_partial(m.ctx, hq._lib.fptr(np.ascontiguousarray(pals)), P, K,
                                                      out.ctypes.data_as(hq._lib._d)), m.ctx)
@@ -200,6 +203,9 @@ def test_generic_hrow4_bitwise(gpu, w, h, dpi, vd):
     np.testing.assert_array_equal(res[0][0], res[1][0])
     for p in range(P):
         np.testing.assert_array_equal(res[0][1][p], res[1][1][p])
+        np.testing.assert_array_equal(res[2][1][p], res[1][1][p])  # gen_vtile2: every pixel bit for bit
+    # (gen_vtile2's 32 x 64 tiles round their fixed-point partials per tile: 2^-20 each)
+    np.testing.assert_allclose(res[2][0], res[1][0], rtol=1e-9)
     assert (res[1][0].reshape(P, 1 + K)[:, 0] > 0).all()
 
 
