@@ -20,6 +20,9 @@
 #ifndef HQ_COST_TW
 #define HQ_COST_TW 128
 #endif
+#ifndef HQ_SA_GRAPH
+#define HQ_SA_GRAPH 0  // (measured slower: C3 0.528 -> 0.540 ms, shard-of-8 0.1035 -> 0.110 ms per step)
+#endif
 
 namespace hq {
 // launchers from hq_kernels.hip
@@ -153,6 +156,7 @@ struct hq_ctx {
     int cost_tw = HQ_COST_TW;  // 16-row tiles at HB = 10: 128 (4 waves) or 256 columns (8 waves; slower)
     int gen_hrow4 = 1;     // tiled generic path: 4 outputs per thread in the horizontal pass
     int gen_vtile2 = 1;    // tiled generic path: double-buffered LDS-DMA vertical pass (half <= 64)
+    int sa_graph = HQ_SA_GRAPH;  // device-resident search: each run's kernels as one hipGraph
     int assign_blocks_per_cu = 0;  // 0 = auto: assign_pipe_kernel<NG>'s residency (the occupancy
                                    // query, assign_res[NG]), one round of workgroups, each
                                    // thread a grid-stride pixel sequence
@@ -203,6 +207,8 @@ struct hq_search {
     double keep_acc = 0.0;               // whose population awaits acceptance
     DevBuf colors[2], cand[2], err[2], seed[2], best_err[2], best_colors, jA, jC;
     std::vector<hipEvent_t> pev;         // profiling: 8 events per iteration of a run
+    hipGraphExec_t gexec = nullptr;      // option sa_graph: the last run's iteration chain
+    int gexec_iters = 0;                 // (its iteration count: the topology an update must match)
 };
 
 namespace {
@@ -444,6 +450,11 @@ int ensure_population(hq_ctx* c, int P, int K) {
     HIP_TRY(c, c->d_acc.ensure(2 * sizeof(uint64_t) * acc_words(P)));
     HIP_TRY(c, c->d_out.ensure(sizeof(double) * (size_t)P * (1 + K)));
     if (c->pixel_err) HIP_TRY(c, c->d_pixerr.ensure(sizeof(float) * (size_t)P * std::max<int64_t>(n_own, 1)));
+    // the generic path's [7][n_ext] scratch, here rather than at its first launch: an
+    // allocation cannot happen while a search run is being captured into a graph
+    const bool fast = c->cost_variant == 0 && c->fast_hb > 0 &&
+                      (c->nch_cur == 1 || (c->fast_hb == 10 && c->cost_rows == 16 && c->cost_tw == 128));
+    if (!fast || K > kMaxK) HIP_TRY(c, c->d_gen_t.ensure(sizeof(float) * 7 * (size_t)g.n_ext));
     return ensure_pinned(c, sizeof(float) * 4 * (size_t)P * K, sizeof(double) * (size_t)P * (1 + K));
 }
 
@@ -966,18 +977,59 @@ int device_search_run(hq_search* s, int iterations, int* ran) {
         return fail(c, HQ_ERR_STATE, "communicator set after hq_search_create: recreate the search");
     const bool prof = c->prof;
     if (prof && (rc = ensure_events(s, (size_t)kProfEvents * iterations))) return rc;
+    // option sa_graph: the run's kernels go into one hipGraph (stream capture),
+    // replayed as a whole -- a chain of dependent kernels costs ~2.7 us per
+    // kernel from the stream and ~1.8 from a graph (profiles/r04_graph_gap_
+    // microbench.txt).  The previous run's executable graph is updated in place
+    // when the iteration count (the topology) is the same, else instantiated
+    // anew.  Not with profiling events (they ride on the launches).
+    const bool graph = c->sa_graph && !prof;
+    if (graph) HIP_TRY(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    auto abort_capture = [&](int rc0) {
+        if (graph) {
+            hipGraph_t gr = nullptr;
+            if (hipStreamEndCapture(c->stream, &gr) == hipSuccess && gr) (void)hipGraphDestroy(gr);
+        }
+        return rc0;
+    };
     for (; done < iterations && s->ite < s->prm.imax; ++done) {
         const int ite = ++s->ite;
         s->pol->reduce_temperature_if_necessary(ite);                  // IM:507
         const float amax = s->pol->max_step_width(ite) / 256.0f;       // SW:91-101
         const hipEvent_t* ev = prof ? &s->pev[(size_t)kProfEvents * done] : nullptr;
         // accept the previous iteration's population (none at the first of a run)
-        if ((rc = enqueue_sa_step(s, done > 0, false, true, false, amax, ev ? ev + 8 : nullptr))) return rc;
-        if ((rc = enqueue_core(c, s->P, s->K, ev, s->fold))) return rc;
+        if ((rc = enqueue_sa_step(s, done > 0, false, true, false, amax, ev ? ev + 8 : nullptr)))
+            return abort_capture(rc);
+        if ((rc = enqueue_core(c, s->P, s->K, ev, s->fold))) return abort_capture(rc);
         s->t_acc = s->pol->temperature();     // SW:54-57 at this iteration
         s->keep_acc = s->pol->keep_threshold(ite);
     }
-    if (done > 0 && (rc = enqueue_sa_step(s, true, false, false, false, 0.f))) return rc;
+    if (done > 0 && (rc = enqueue_sa_step(s, true, false, false, false, 0.f))) return abort_capture(rc);
+    if (graph) {
+        hipGraph_t gr = nullptr;
+        HIP_TRY(c, hipStreamEndCapture(c->stream, &gr));
+        bool updated = false;
+        if (s->gexec && s->gexec_iters == done) {
+            hipGraphNode_t err_node = nullptr;
+            hipGraphExecUpdateResult res = hipGraphExecUpdateError;
+            updated = hipGraphExecUpdate(s->gexec, gr, &err_node, &res) == hipSuccess &&
+                      res == hipGraphExecUpdateSuccess;
+            if (!updated) (void)hipGetLastError();
+        }
+        if (!updated) {
+            if (s->gexec) (void)hipGraphExecDestroy(s->gexec);
+            s->gexec = nullptr;
+            const hipError_t e = hipGraphInstantiate(&s->gexec, gr, nullptr, nullptr, 0);
+            if (e != hipSuccess) {
+                (void)hipGraphDestroy(gr);
+                s->gexec = nullptr;
+                HIP_TRY(c, e);
+            }
+            s->gexec_iters = done;
+        }
+        (void)hipGraphDestroy(gr);
+        HIP_TRY(c, hipGraphLaunch(s->gexec, c->stream));
+    }
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     for (int i = 0; prof && i < done; ++i) {
         prof_accumulate(c, &s->pev[(size_t)kProfEvents * i], !s->fold);
@@ -1489,6 +1541,7 @@ void hq_search_destroy(hq_search* s) {
         (void)hipStreamSynchronize(s->ctx->stream);
     }
     for (hipEvent_t e : s->pev) (void)hipEventDestroy(e);
+    if (s->gexec) (void)hipGraphExecDestroy(s->gexec);
     for (DevBuf* b : {&s->colors[0], &s->colors[1], &s->cand[0], &s->cand[1], &s->err[0], &s->err[1],
                       &s->seed[0], &s->seed[1], &s->best_err[0], &s->best_err[1], &s->best_colors, &s->jA,
                       &s->jC})
@@ -1539,6 +1592,8 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
     } else if (!std::strcmp(name, "cost_rows")) {
         if (value != 8 && value != 16) return fail(c, HQ_ERR_ARG, "cost_rows must be 8 or 16");
         c->cost_rows = value;
+    } else if (!std::strcmp(name, "sa_graph")) {
+        c->sa_graph = value != 0;
     } else if (!std::strcmp(name, "gen_vtile2")) {
         c->gen_vtile2 = value != 0;
     } else if (!std::strcmp(name, "gen_hrow4")) {

@@ -222,6 +222,8 @@ int hq_profile_reset(hq_ctx *ctx);
  *   "sa_device"    hq_search_*: 1 (default) = the SWASA iterations run on the device
  *                  (accept/generate kernel, no host round trip per iteration; needs
  *                  population <= 64), 0 = host-driven, one evaluation call each
+ *   "sa_graph"     hq_search_*: 1 = each run's kernels captured into one hipGraph and
+ *                  replayed (0, default: measured slower, 0.540 against 0.528 ms per C3 step)
  *   "shard_solo"   experiment only: let a row-block shard run hq_search_* without a
  *                  communicator (its own partial costs; per-rank timing at N GPUs)
  *   "pixel_err"    test only: 1 = the cost kernels also write the per-pixel dE
