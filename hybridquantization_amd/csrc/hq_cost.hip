@@ -1230,22 +1230,25 @@ __global__ __launch_bounds__(256) void gen_hrow_kernel(GenArgs a) {
 // (element e at slot (e & 3) Q + e / 4), so the 64 lanes of a read hit
 // consecutive slots.  Each output sums its taps in ascending order (CL:254-
 // 267), so the planes equal gen_hrow's bit for bit.
-constexpr int kHr4Seg = 1024;  // outputs per workgroup row segment
-template <typename IT>
+// NO adjacent outputs per thread (4 or 8: option gen_hrow_outputs), a row
+// segment of 256 NO outputs per workgroup; element e of the segment sits at
+// slot (e % NO) Q + e / NO, so a read's 64 lanes hit consecutive slots.
+template <typename IT, bool SPLIT, int NO>
 __global__ __launch_bounds__(256) void gen_hrow4_kernel(GenArgs a) {
-    extern __shared__ float4 s_opp[];  // [4][Q] permuted, Q = (kHr4Seg + 2 half + 7) / 4 + 1
+    extern __shared__ float4 s_opp[];  // [NO][Q] permuted
+    constexpr int SEG = 256 * NO, NW = NO + 3;  // window: NO outputs x a chunk of 4 taps
     const int tid = threadIdx.x, half = a.half, W = a.g.W, T = 2 * half + 1;
-    const int x0 = blockIdx.x * kHr4Seg, ly = blockIdx.y;
-    const int Q = (kHr4Seg + 2 * half + 7) / 4 + 1;
+    const int x0 = blockIdx.x * SEG, ly = blockIdx.y;
+    const int Q = (SEG + 2 * half + 3 + NO - 1) / NO;
     const IT* row = static_cast<const IT*>(a.idx) + (int64_t)ly * W;
     // the segment's colours, 8 per thread and batch: every index load of a batch
     // first, then every table load, then the stores (one dependent pair of round
     // trips per batch; a load -> load -> store loop paid two per element)
-    for (int e0 = 0; e0 < 4 * Q; e0 += 8 * 256) {
+    for (int e0 = 0; e0 < NO * Q; e0 += 8 * 256) {
         uint32_t ix[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const int e = min(e0 + tid + 256 * u, 4 * Q - 1);
+            const int e = min(e0 + tid + 256 * u, NO * Q - 1);
             const int x = min(x0 - half + e, W - 1 + half);  // (past the row end: reflected, unused)
             ix[u] = (uint32_t)row[reflect_only(x, W)];
         }
@@ -1255,55 +1258,84 @@ __global__ __launch_bounds__(256) void gen_hrow4_kernel(GenArgs a) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             const int e = e0 + tid + 256 * u;
-            if (e < 4 * Q) s_opp[(e & 3) * Q + (e >> 2)] = v[u];
+            if (e < NO * Q) s_opp[(e % NO) * Q + e / NO] = v[u];
         }
     }
     __syncthreads();
-    float acc[7][4];
+    float acc[7][NO];
 #pragma unroll
     for (int f = 0; f < 7; ++f)
 #pragma unroll
-        for (int xo = 0; xo < 4; ++xo) acc[f][xo] = 0.f;
-    // window w[i] = element 4 tid + t0 + i of the segment, i = 0 .. 6
-    auto rd = [&](int e) { return s_opp[(e & 3) * Q + (e >> 2)]; };
-    float4 w[7];
+        for (int xo = 0; xo < NO; ++xo) acc[f][xo] = 0.f;
+    // window w[i] = element NO tid + t0 + i of the segment, i = 0 .. NO + 2
+    auto rd = [&](int e) { return s_opp[(e % NO) * Q + e / NO]; };
+    float4 w[NW];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) w[i] = rd(4 * tid + i);
-    for (int t0 = 0; t0 < T; t0 += 4) {
+    for (int i = 0; i < NO - 1; ++i) w[i] = rd(NO * tid + i);
+    // taps t: ka = (k1.xyz, k3), kb = (k2.xyz, 0) (a.htaps, packed on the host: a
+    // chunk's 4 taps are 2 wide scalar loads, not 7 per tap)
+    auto taps_fma = [&](int d, float4 ka, float4 kb) {
 #pragma unroll
-        for (int i = 3; i < 7; ++i) w[i] = rd(4 * tid + t0 + i);
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-            const int t = t0 + d;
-            if (t < T) {  // (uniform)
-                const float k1x = a.k1[4 * t + 0], k1y = a.k1[4 * t + 1], k1z = a.k1[4 * t + 2];
-                const float k2x = a.k2[4 * t + 0], k2y = a.k2[4 * t + 1], k2z = a.k2[4 * t + 2];
-                const float k3 = a.k3[t];
-#pragma unroll
-                for (int xo = 0; xo < 4; ++xo) {
-                    const float4 in = w[d + xo];
-                    acc[0][xo] = fmaf(in.x, k1x, acc[0][xo]);
-                    acc[1][xo] = fmaf(in.y, k1y, acc[1][xo]);
-                    acc[2][xo] = fmaf(in.z, k1z, acc[2][xo]);
-                    acc[3][xo] = fmaf(in.x, k2x, acc[3][xo]);
-                    acc[4][xo] = fmaf(in.y, k2y, acc[4][xo]);
-                    acc[5][xo] = fmaf(in.z, k2z, acc[5][xo]);
-                    acc[6][xo] = fmaf(in.x, k3, acc[6][xo]);
-                }
-            }
+        for (int xo = 0; xo < NO; ++xo) {
+            const float4 in = w[d + xo];
+            acc[0][xo] = fmaf(in.x, ka.x, acc[0][xo]);
+            acc[1][xo] = fmaf(in.y, ka.y, acc[1][xo]);
+            acc[2][xo] = fmaf(in.z, ka.z, acc[2][xo]);
+            acc[3][xo] = fmaf(in.x, kb.x, acc[3][xo]);
+            acc[4][xo] = fmaf(in.y, kb.y, acc[4][xo]);
+            acc[5][xo] = fmaf(in.z, kb.z, acc[5][xo]);
+            acc[6][xo] = fmaf(in.x, ka.w, acc[6][xo]);
         }
+    };
+    const float4* tp = a.htaps;
+    int t0 = 0;
+    for (; t0 + 4 <= T; t0 += 4) {  // whole chunks
 #pragma unroll
-        for (int i = 0; i < 3; ++i) w[i] = w[i + 4];
+        for (int i = NO - 1; i < NW; ++i) w[i] = rd(NO * tid + t0 + i);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) taps_fma(d, tp[2 * (t0 + d)], tp[2 * (t0 + d) + 1]);
+#pragma unroll
+        for (int i = 0; i < NO - 1; ++i) w[i] = w[i + 4];
     }
-    const int64_t n = a.g.n_ext, q0 = (int64_t)ly * W + x0 + 4 * tid;
-    if ((W & 3) == 0 && x0 + 4 * tid + 3 < W) {  // (planes of n_ext = W rows floats: 16-B aligned)
+    if (t0 < T) {  // the last taps: guarded (a tap past T is not a zero product on a non-finite colour)
+#pragma unroll
+        for (int i = NO - 1; i < NW; ++i) w[i] = rd(NO * tid + t0 + i);
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+            if (t0 + d < T) taps_fma(d, tp[2 * (t0 + d)], tp[2 * (t0 + d) + 1]);
+    }
+    const int64_t n = a.g.n_ext, q0 = (int64_t)ly * W + x0 + NO * tid;
+    const bool whole = (W & 3) == 0 && x0 + NO * tid + NO - 1 < W;  // (planes of n_ext = W rows: 16-B aligned)
+    if constexpr (SPLIT) {  // planes of (hi, lo) f16 pairs of x 2^14 for the matrix-core vertical pass
+        uint32_t* t = reinterpret_cast<uint32_t*>(a.t);
+        if (whole) {
+#pragma unroll
+            for (int f = 0; f < 7; ++f)
+#pragma unroll
+                for (int v = 0; v < NO; v += 4)
+                    *reinterpret_cast<uint4*>(t + f * n + q0 + v) =
+                        make_uint4(split_f16(acc[f][v]), split_f16(acc[f][v + 1]), split_f16(acc[f][v + 2]),
+                                   split_f16(acc[f][v + 3]));
+        } else {
+#pragma unroll
+            for (int xo = 0; xo < NO; ++xo)
+                if (x0 + NO * tid + xo < W)
+#pragma unroll
+                    for (int f = 0; f < 7; ++f) t[f * n + q0 + xo] = split_f16(acc[f][xo]);
+        }
+        return;
+    }
+    if (whole) {
 #pragma unroll
         for (int f = 0; f < 7; ++f)
-            *reinterpret_cast<float4*>(a.t + f * n + q0) = make_float4(acc[f][0], acc[f][1], acc[f][2], acc[f][3]);
+#pragma unroll
+            for (int v = 0; v < NO; v += 4)
+                *reinterpret_cast<float4*>(a.t + f * n + q0 + v) =
+                    make_float4(acc[f][v], acc[f][v + 1], acc[f][v + 2], acc[f][v + 3]);
     } else {
 #pragma unroll
-        for (int xo = 0; xo < 4; ++xo)
-            if (x0 + 4 * tid + xo < W)
+        for (int xo = 0; xo < NO; ++xo)
+            if (x0 + NO * tid + xo < W)
 #pragma unroll
                 for (int f = 0; f < 7; ++f) a.t[f * n + q0 + xo] = acc[f][xo];
     }
@@ -1487,6 +1519,112 @@ __global__ __launch_bounds__(256) void gen_vtile2_kernel(GenArgs a, int tiles_x)
     if (tid == 0) acc_add(a.acc, a.P, a.p, blockIdx.x, (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]));
 }
 
+// gen_vmfma: the tiled generic path's vertical pass on the matrix cores
+// (half <= kVt2MaxHalf), the split-f16 (hi, lo) pair scheme of cost16w's wide
+// buckets: gen_hrow4<SPLIT> writes each plane value x as the dword (hi, lo) of
+// x 2^14 (split_f16), which is two K slots of the B operand as it stands; A
+// holds the vertical taps x 2^16 split on the host, each tap part in both
+// slots of a row (build_vtile_pair_fragments), the hi parts in one MFMA and
+// the lo parts in the next: (t_hi + t_lo)(x_hi + x_lo), every product exact in
+// the fp32 accumulator.  A 16 x 16 output block takes K steps of 16 window rows
+// (S = ceil((16 + 2 half) / 16)); K slot (g, 2 j + h) of step s is window row
+// 16 s + 4 g + j of the block, part h.  The windows are the 32 x (64 + 2 half)
+// dword planes of gen_vtile2, double-buffered by LDS DMA.  Wave w owns output
+// rows 16 w .. 16 w + 15 of the 64 x 32 tile, both 16-column blocks; a
+// channel's filters accumulate into its two D blocks (x 2^30, folded into the
+// Lab matrix).
+template <int DE>
+__global__ __launch_bounds__(256) void gen_vmfma_kernel(GenArgs a, int tiles_x) {
+    // [2][window (64 + 2 half) x 32 dwords, then the filter's A fragments S x 2 x 64 x 16 B]
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_wm[];
+    constexpr int TW = kVt2W, TH = 64;
+    __shared__ double s_red[4];
+    const int tid = threadIdx.x, lane = tid & 63, n = lane & 15, g = lane >> 4;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const Geom& gm = a.g;
+    const int x0 = (blockIdx.x % tiles_x) * TW, y0 = gm.r0 + (blockIdx.x / tiles_x) * TH;
+    const int half = a.half, RH = TH + 2 * half, NE = RH * TW, S = (16 + 2 * half + 15) / 16;
+    const int NF = S * 2 * 64 * 4, BUF = (NE + 3) / 4 * 4 + NF;  // fragment dwords; dwords per buffer
+    const int64_t np = gm.n_ext;
+    const bool rows_inside = y0 - half >= gm.e0 && y0 - half >= 0 && y0 + TH + half <= gm.e1 && y0 + TH + half <= gm.H;
+    const int jx = min(x0 + (tid & (TW - 1)), gm.W - 1);
+    auto issue = [&](int f, int b) {
+        const uint32_t* plane = reinterpret_cast<const uint32_t*>(a.t) + (int64_t)f * np;
+        uint32_t* dst = s_wm + b * BUF;
+        // the filter's A fragments, 1 KiB per wave instruction (16 B per lane)
+        uint32_t* fdst = dst + (NE + 3) / 4 * 4;
+        const uint4* fsrc = a.vfragm + (int64_t)f * S * 2 * 64;
+        for (int q = wv; q < 2 * S; q += 4)
+            __builtin_amdgcn_global_load_lds(fsrc + q * 64 + (tid & 63),
+                                             (__attribute__((address_space(3))) void*)(fdst + q * 256), 16, 0, 0);
+        for (int e0 = 0; e0 < NE; e0 += 256) {
+            const int e = e0 + tid;
+            if (e < NE) {
+                int gy = y0 - half + (e >> 5);
+                if (!rows_inside) {
+                    gy = reflect_clamp(gy, gm.H);
+                    gy = min(max(gy, gm.e0), gm.e1 - 1);
+                }
+                const uint32_t* src = plane + (uint32_t)((gy - gm.e0) * gm.W + jx);
+                __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(dst + e0 + 64 * wv), 4, 0, 0);
+            }
+        }
+    };
+    f32x4v D[3][2];
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) D[ch][0] = D[ch][1] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    issue(0, 0);
+    for (int f = 0; f < kNumFilt; ++f) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's rows of window f have landed
+        __syncthreads();                     // every wave's rows; window f - 1's readers are done
+        if (f + 1 < kNumFilt) issue(f + 1, (f + 1) & 1);
+        const uint32_t* win = s_wm + (f & 1) * BUF;
+        const uint4* fa = reinterpret_cast<const uint4*>(win + (NE + 3) / 4 * 4) + lane;  // [step][hi, lo][lane]
+        f32x4v e0 = {0.f, 0.f, 0.f, 0.f}, e1 = {0.f, 0.f, 0.f, 0.f};
+        for (int st = 0; st < S; ++st) {
+            const uint4 ch = fa[st * 128], cl = fa[st * 128 + 64];
+            const int r = 16 * wv + 16 * st + 4 * g;
+            u32x4 b0, b1;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int row = min(r + j, RH - 1);  // (rows past the window: zero taps, finite data)
+                b0[j] = win[row * TW + n];
+                b1[j] = win[row * TW + 16 + n];
+            }
+            const f16x8 B0 = __builtin_bit_cast(f16x8, b0), B1 = __builtin_bit_cast(f16x8, b1);
+            const f16x8 AH = __builtin_bit_cast(f16x8, ch), AL = __builtin_bit_cast(f16x8, cl);
+            e0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(AH, B0, e0, 0, 0, 0);
+            e1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(AH, B1, e1, 0, 0, 0);
+            e0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(AL, B0, e0, 0, 0, 0);
+            e1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(AL, B1, e1, 0, 0, 0);
+        }
+        const int chp = f == 6 ? 0 : f % 3;  // planes t1.xyz, t2.xyz, t3 -> channels x y z x y z x
+        if (chp == 0) { D[0][0] += e0; D[0][1] += e1; }
+        else if (chp == 1) { D[1][0] += e0; D[1][1] += e1; }
+        else { D[2][0] += e0; D[2][1] += e1; }
+    }
+    double part = 0.0;
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int y = y0 + 16 * wv + 4 * g + i, gx = x0 + 16 * cb + n;
+            if (gx < gm.W && y < gm.r1) {
+                // (x 2^-30: the data and tap scales, exactly)
+                const float3 lf = opp2f_fast(D[0][cb][i] * kVOutScale, D[1][cb][i] * kVOutScale,
+                                             D[2][cb][i] * kVOutScale, a.m_lab);
+                const int64_t off = (int64_t)(y - gm.r0) * gm.lab_pitch + gx;
+                const float ef = delta_e_f<DE>(a.labL[off], a.labA[off], a.labB[off], lf);
+                if (a.pix_err) a.pix_err[(int64_t)(y - gm.r0) * gm.W + gx] = ef;  // test option: the per-pixel dE
+                part += (double)ef;
+            }
+        }
+    part = wave_sum_to_lane63(part);
+    if ((tid & 63) == 63) s_red[tid >> 6] = part;
+    __syncthreads();
+    if (tid == 0) acc_add(a.acc, a.P, a.p, blockIdx.x, (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]));
+}
+
 // ----------------------------------------------------------------------------
 // Host side: tap tables, MFMA fragments, launchers
 // ----------------------------------------------------------------------------
@@ -1638,6 +1776,32 @@ void build_vpass_f16_pair_fragments(int HB, int H, const float* k1, const float*
                     }
 }
 
+// gen_vmfma's A fragments: [filter][step s][hi, lo][lane][8] f16, S steps of 16
+// window rows (S = vtile_pair_steps(H)).  Lane l: output row m = l & 15 of a
+// block, K slots 2 j + h of lane group g = l >> 4 hold tap t = 16 s + 4 g + j - m
+// (window row 16 s + 4 g + j), the same part in both slots of the row; zero
+// outside 0 .. 2 H.  Taps per plane: k1.xyz, k2.xyz, |k3| (the vertical taps of
+// t1.xyz, t2.xyz, t3), x 2^16.
+int vtile_pair_steps(int H) { return (16 + 2 * H + 15) / 16; }
+size_t vtile_pair_fragment_halves(int H) { return (size_t)kNumFilt * vtile_pair_steps(H) * 2 * 64 * 8; }
+void build_vtile_pair_fragments(int H, const float* k1, const float* k2, const float* absk3, uint16_t* out) {
+    const int S = vtile_pair_steps(H), T = 2 * H + 1;
+    for (int f = 0; f < kNumFilt; ++f)
+        for (int st = 0; st < S; ++st)
+            for (int l = 0; l < 64; ++l)
+                for (int kk = 0; kk < 8; ++kk) {
+                    const int m = l & 15, g = l >> 4, t = 16 * st + 4 * g + (kk >> 1) - m;
+                    float w = 0.f;
+                    if (t >= 0 && t < T) w = f < 3 ? k1[4 * t + f] : f < 6 ? k2[4 * t + f - 3] : absk3[t];
+                    w *= kVTapScale;
+                    const uint16_t hi = host_f16(w);
+                    const uint16_t lo = host_f16(w - host_f16_to_f32(hi));
+                    const size_t base = (((size_t)f * S + st) * 2) * 64;
+                    out[((base + 0 * 64) + l) * 8 + kk] = hi;
+                    out[((base + 1 * 64) + l) * 8 + kk] = lo;
+                }
+}
+
 // The narrow k1 filters' taps outside the bucket's trimmed windows are below
 // 1e-9 of their peak (then the fast path may skip them; else it runs all taps).
 bool trim_window_ok(const float* k1, int H, int HB) {
@@ -1777,21 +1941,50 @@ hipError_t launch_cost_fast(const CostArgs& a0, int P, int de, bool trim, int ti
     return hipGetLastError();
 }
 
+// gen_hrow4 with a.hrow_no outputs per thread (4 or 8)
+template <bool SPLIT, int NO>
+static void launch_hrow4_no(const GenArgs& a, int idx_bytes, hipStream_t s) {
+    constexpr int SEG = 256 * NO;
+    const dim3 hg((unsigned)((a.g.W + SEG - 1) / SEG), (unsigned)(a.g.e1 - a.g.e0));
+    const size_t hl = sizeof(float4) * NO * (size_t)((SEG + 2 * a.half + 3 + NO - 1) / NO);
+    auto go = [&](auto kern) {
+        if (!allow_dyn_lds(reinterpret_cast<const void*>(kern), hl)) return;  // (the caller's hipGetLastError)
+        HQ_LAUNCH(kern, hg, dim3(256), hl, s, a);
+    };
+    if (idx_bytes == 4) go(gen_hrow4_kernel<uint32_t, SPLIT, NO>);
+    else if (idx_bytes == 2) go(gen_hrow4_kernel<uint16_t, SPLIT, NO>);
+    else go(gen_hrow4_kernel<uint8_t, SPLIT, NO>);
+}
+template <bool SPLIT>
+static void launch_hrow4(const GenArgs& a, int idx_bytes, hipStream_t s) {
+    if (a.hrow_no == 8) launch_hrow4_no<SPLIT, 8>(a, idx_bytes, s);
+    else launch_hrow4_no<SPLIT, 4>(a, idx_bytes, s);
+}
+
 // The tiled generic pair (gen_hrow + gen_vtile).  idx_bytes: 1, 2 (chunked
 // palettes) or 4 (K > 4096).
 hipError_t launch_cost_tiled_generic(const GenArgs& a, int de, int idx_bytes, hipStream_t s) {
     const hipEvent_t ev0 = t_ev_start, ev1 = t_ev_stop;
     t_ev_stop = nullptr;
-    if (a.hrow4) {  // (option gen_hrow4, default on; gen_hrow stays as its bitwise cross-check)
-        const dim3 hg((unsigned)((a.g.W + kHr4Seg - 1) / kHr4Seg), (unsigned)(a.g.e1 - a.g.e0));
-        const size_t hl = sizeof(float4) * 4 * (size_t)((kHr4Seg + 2 * a.half + 7) / 4 + 1);
-        auto go = [&](auto kern) {
-            if (!allow_dyn_lds(reinterpret_cast<const void*>(kern), hl)) return;  // (the caller's hipGetLastError)
-            HQ_LAUNCH(kern, hg, dim3(256), hl, s, a);
+    const bool vm = a.vmfma && a.vfragm && a.half <= kVt2MaxHalf;  // the matrix-core vertical pass
+    if (vm) {
+        launch_hrow4<true>(a, idx_bytes, s);
+        t_ev_start = nullptr;
+        t_ev_stop = ev1;
+        const int tx = (a.g.W + kVt2W - 1) / kVt2W, ty = (a.g.r1 - a.g.r0 + 63) / 64;
+        const int S = (16 + 2 * a.half + 15) / 16, NE = kVt2W * (64 + 2 * a.half);
+        const size_t l2 = sizeof(uint32_t) * 2 * ((size_t)(NE + 3) / 4 * 4 + (size_t)S * 2 * 64 * 4);
+        auto gov = [&](auto kern) {
+            if (!allow_dyn_lds(reinterpret_cast<const void*>(kern), l2)) return;
+            HQ_LAUNCH(kern, dim3((unsigned)(tx * ty)), dim3(256), l2, s, a, tx);
         };
-        if (idx_bytes == 4) go(gen_hrow4_kernel<uint32_t>);
-        else if (idx_bytes == 2) go(gen_hrow4_kernel<uint16_t>);
-        else go(gen_hrow4_kernel<uint8_t>);
+        if (de == 0) gov(gen_vmfma_kernel<0>);
+        else gov(gen_vmfma_kernel<1>);
+        t_ev_start = ev0;
+        return hipGetLastError();
+    }
+    if (a.hrow4) {  // (option gen_hrow4, default on; gen_hrow stays as its bitwise cross-check)
+        launch_hrow4<false>(a, idx_bytes, s);
     } else {
         const dim3 hg((unsigned)((a.g.W + 255) / 256), (unsigned)(a.g.e1 - a.g.e0));
         const size_t hl = sizeof(float4) * (256 + 2 * (size_t)a.half);

@@ -227,7 +227,11 @@ struct GenArgs {
     const float* vtaps;  // tiled path: [7][vtap_pitch] vertical taps per plane, zero-padded
     int vtap_pitch;      // (2 half + 1 rounded up to 16, + 16)
     int hrow4 = 1;       // tiled path: horizontal pass with 4 outputs per thread (gen_hrow4), else gen_hrow
+    int hrow_no = 4;     // gen_hrow4's outputs per thread: 4 or 8
     int vtile2 = 1;      // tiled path: double-buffered LDS-DMA vertical pass (gen_vtile2), else gen_vtile
+    int vmfma = 1;       // tiled path: the vertical pass on the matrix cores (gen_vmfma, split f16)
+    const uint4* vfragm = nullptr;  // its A fragments [7][S][hi, lo][64] (build_vtile_pair_fragments)
+    const float4* htaps = nullptr;  // gen_hrow4: [T][2] (k1.xyz, k3), (k2.xyz, 0) horizontal taps
 };
 
 }  // namespace hq

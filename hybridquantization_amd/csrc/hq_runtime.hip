@@ -43,6 +43,8 @@ size_t vpass_f16_stack_fragment_halves(int HB);
 void build_vpass_f16_pair_fragments(int HB, int H, const float* k1, const float* k2, const float* k3,
                                     const float* absk3, uint16_t* out);
 size_t vpass_f16_pair_fragment_halves(int HB);
+size_t vtile_pair_fragment_halves(int H);
+void build_vtile_pair_fragments(int H, const float* k1, const float* k2, const float* absk3, uint16_t* out);
 void build_vpass_f16_stack_fragments(int HB, int H, const float* k1, const float* k2, const float* k3,
                                      const float* absk3, uint16_t* out);
 size_t fast_taps_bytes(int HB);
@@ -121,6 +123,8 @@ struct hq_ctx {
     DevBuf d_taps;     // fast path taps, build_fast_taps (the filters centred in the bucket)
     DevBuf d_vfrag16;  // split-f16 MFMA A fragments of the stacked vertical taps
     DevBuf d_vfrag16p; // the same in cost16w's (hi, lo) pair layout
+    DevBuf d_vfragm;   // the tiled generic path's matrix-core vertical taps (build_vtile_pair_fragments)
+    DevBuf d_htaps;    // gen_hrow4's packed horizontal taps [T][2] float4
 
     // image
     bool have_image = false;
@@ -156,6 +160,8 @@ struct hq_ctx {
     int cost_tw = HQ_COST_TW;  // 16-row tiles at HB = 10: 128 (4 waves) or 256 columns (8 waves; slower)
     int gen_hrow4 = 1;     // tiled generic path: 4 outputs per thread in the horizontal pass
     int gen_vtile2 = 1;    // tiled generic path: double-buffered LDS-DMA vertical pass (half <= 64)
+    int gen_vmfma = 1;     // tiled generic path: the vertical pass on the matrix cores (half <= 64)
+    int gen_hrow_no = 4;   // tiled generic path: horizontal outputs per thread (4 or 8)
     int sa_graph = HQ_SA_GRAPH;  // device-resident search: each run's kernels as one hipGraph
     int assign_blocks_per_cu = 0;  // 0 = auto: assign_pipe_kernel<NG>'s residency (the occupancy
                                    // query, assign_res[NG]), one round of workgroups, each
@@ -530,7 +536,11 @@ int enqueue_generic_cost(hq_ctx* c, int P, const void* idx_base, int idx_bytes, 
         gn.vtaps = c->d_vtaps.as<float>();
         gn.vtap_pitch = c->vtap_pitch;
         gn.hrow4 = c->gen_hrow4;
+        gn.hrow_no = c->gen_hrow_no;
         gn.vtile2 = c->gen_vtile2;
+        gn.vmfma = c->gen_vmfma;
+        gn.vfragm = c->d_vfragm.bytes ? c->d_vfragm.as<uint4>() : nullptr;
+        gn.htaps = c->d_htaps.as<float4>();
         opp2xyz_over_illum(inv, gn.m_lab);
         // the events span every palette's launch pair: start on the first, stop on the last
         if (ev) set_launch_events(p == 0 ? ev[4] : nullptr, p == P - 1 ? ev[5] : nullptr);
@@ -1106,7 +1116,7 @@ void hq_destroy(hq_ctx* c) {
                       &c->d_labL, &c->d_labA, &c->d_labB, &c->d_pal_in, &c->d_pal, &c->d_opp, &c->d_opp16,
                       &c->d_dup, &c->d_pflags, &c->d_lvl1, &c->d_lvl2, &c->d_idx,
                       &c->d_used_mask, &c->d_acc, &c->d_out, &c->d_gen_t, &c->d_taps,
-                      &c->d_vfrag16, &c->d_vfrag16p, &c->d_idx32, &c->d_used32, &c->d_pixerr, &c->d_idx16, &c->d_dist})
+                      &c->d_vfrag16, &c->d_vfrag16p, &c->d_vfragm, &c->d_htaps, &c->d_idx32, &c->d_used32, &c->d_pixerr, &c->d_idx16, &c->d_dist})
         b->release();
     if (c->h_pal) (void)hipHostFree(c->h_pal);
     if (c->h_out) (void)hipHostFree(c->h_out);
@@ -1153,6 +1163,17 @@ int hq_set_filters(hq_ctx* c, int taps, const float* k1, const float* k2, const 
         }
         HIP_TRY(c, c->d_vtaps.ensure(sizeof(float) * vt.size()));
         HIP_TRY(c, hipMemcpy(c->d_vtaps.p, vt.data(), sizeof(float) * vt.size(), hipMemcpyHostToDevice));
+        std::vector<float> ht((size_t)8 * taps);
+        for (int t = 0; t < taps; ++t) {
+            const float v[8] = {k1[4 * t], k1[4 * t + 1], k1[4 * t + 2], k3[t], k2[4 * t], k2[4 * t + 1], k2[4 * t + 2], 0.f};
+            std::copy(v, v + 8, ht.begin() + 8 * t);
+        }
+        HIP_TRY(c, c->d_htaps.ensure(sizeof(float) * ht.size()));
+        HIP_TRY(c, hipMemcpy(c->d_htaps.p, ht.data(), sizeof(float) * ht.size(), hipMemcpyHostToDevice));
+        std::vector<uint16_t> fm(vtile_pair_fragment_halves(c->half));
+        build_vtile_pair_fragments(c->half, k1, k2, absk3, fm.data());
+        HIP_TRY(c, c->d_vfragm.ensure(fm.size() * sizeof(uint16_t)));
+        HIP_TRY(c, hipMemcpy(c->d_vfragm.p, fm.data(), fm.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
     }
     // fast path: the filters centred in the smallest tap bucket that holds them
     // (half-widths up to 24: every dpi / viewing distance of HQ:229-231 up to
@@ -1594,6 +1615,11 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
         c->cost_rows = value;
     } else if (!std::strcmp(name, "sa_graph")) {
         c->sa_graph = value != 0;
+    } else if (!std::strcmp(name, "gen_hrow_outputs")) {
+        if (value != 4 && value != 8) return fail(c, HQ_ERR_ARG, "gen_hrow_outputs must be 4 or 8");
+        c->gen_hrow_no = value;
+    } else if (!std::strcmp(name, "gen_vmfma")) {
+        c->gen_vmfma = value != 0;
     } else if (!std::strcmp(name, "gen_vtile2")) {
         c->gen_vtile2 = value != 0;
     } else if (!std::strcmp(name, "gen_hrow4")) {

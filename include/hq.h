@@ -207,6 +207,8 @@ int hq_profile_reset(hq_ctx *ctx);
  *   "gen_hrow4"    the LDS-tiled generic path's horizontal pass: 1 (default) = 4 adjacent
  *                  outputs per thread over a sliding window, 0 = one output per thread
  *                  (same planes bit for bit)
+ *   "gen_vmfma"    the LDS-tiled generic path's vertical pass (halfSize <= 64) on the matrix
+ *                  cores in split f16 (as the fast path's; default 1), 0 = fp32 FMAs (gen_vtile2)
  *   "gen_vtile2"   the LDS-tiled generic path's vertical pass (halfSize <= 64): 1 (default) =
  *                  32 x 64 tiles, windows double-buffered by LDS DMA; 0 = 64 x 64 tiles with
  *                  one window at a time (same results bit for bit)

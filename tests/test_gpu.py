@@ -178,8 +178,9 @@ def test_generic_hrow4_bitwise(gpu, w, h, dpi, vd):
     """The LDS-tiled generic path's horizontal pass with 4 adjacent outputs per
     thread (option gen_hrow4, default) gives the one-output kernel's per-pixel
     dE and sums bit for bit: both sum each output's taps in ascending order.
-    The double-buffered vertical pass (gen_vtile2, default for half <= 64)
-    gives every pixel's dE bit for bit too.
+    The double-buffered vertical pass (gen_vtile2) gives every pixel's dE bit
+    for bit too; the matrix-core vertical pass (gen_vmfma, the default for
+    half <= 64) agrees within the fast path's bars.
     Segments of 1,024 outputs: 1,100 and 1,029 columns end in partial
     segments; 300 dpi / 50 cm is 103 taps (half 51, not a multiple of 4)."""
     R, G, B = o.synthetic_image(w, h, seed=w * h)
@@ -192,9 +193,11 @@ def test_generic_hrow4_bitwise(gpu, w, h, dpi, vd):
     K, P = 64, 2
     pals = np.stack([o.synthetic_palette(K, 9 + p) for p in range(P)]).reshape(P, -1)
     res = []
-    for h4, v2 in ((0, 0), (1, 0), (1, 1)):
+    for h4, v2, vm, no in ((0, 0, 0, 4), (1, 0, 0, 4), (1, 1, 0, 4), (1, 1, 1, 4), (1, 1, 0, 8)):
         m.setOption("gen_hrow4", h4)
         m.setOption("gen_vtile2", v2)
+        m.setOption("gen_vmfma", vm)
+        m.setOption("gen_hrow_outputs", no)
         out = np.zeros(P * (1 + K))
         hq._lib.check(lib.hq_eval_population_partial(m.ctx, hq._lib.fptr(np.ascontiguousarray(pals)), P, K,
                                                      out.ctypes.data_as(hq._lib._d)), m.ctx)
@@ -204,9 +207,17 @@ def test_generic_hrow4_bitwise(gpu, w, h, dpi, vd):
     for p in range(P):
         np.testing.assert_array_equal(res[0][1][p], res[1][1][p])
         np.testing.assert_array_equal(res[2][1][p], res[1][1][p])  # gen_vtile2: every pixel bit for bit
+        np.testing.assert_array_equal(res[4][1][p], res[2][1][p])  # 8 outputs per thread: the same sums
     # (gen_vtile2's 32 x 64 tiles round their fixed-point partials per tile: 2^-20 each)
     np.testing.assert_allclose(res[2][0], res[1][0], rtol=1e-9)
     assert (res[1][0].reshape(P, 1 + K)[:, 0] > 0).all()
+    # gen_vmfma (default): the vertical taps as split-f16 matrix-core products,
+    # the fast path's scheme -- the same bars as fast vs generic (per pixel 2e-4,
+    # sums 1e-6 relative)
+    for p in range(P):
+        np.testing.assert_allclose(res[3][1][p], res[2][1][p], rtol=0, atol=2e-4)
+    np.testing.assert_allclose(res[3][0].reshape(P, 1 + K)[:, 0], res[2][0].reshape(P, 1 + K)[:, 0], rtol=1e-6)
+    np.testing.assert_array_equal(res[3][0].reshape(P, 1 + K)[:, 1:], res[2][0].reshape(P, 1 + K)[:, 1:])
 
 
 @pytest.mark.parametrize("dpi,vd", [(150, 30.0), (96, 60.0), (200, 30.0)])
