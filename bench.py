@@ -84,16 +84,20 @@ def cost_accounting(half, K, grid, opts):
     rows = int(opts.get("cost_rows", 16))
     variant = int(opts.get("cost_variant", 0))
     hb = next((b for b in (10, 15, 19, 24) if half <= b), 0)
-    # K <= 256: u8 indices; 256 < K <= 4096: chunked palettes, 16-bit indices, the
-    # tiled kernel at HB = 10 with 16 x 128 tiles only; above: 32-bit indices
-    chunked = 256 < K <= 4096 and int(opts.get("chunked", 1)) != 0 and grid > 0
+    # K <= 256: u8 indices; 256 < K <= 16384: chunked palettes, 16-bit indices, the
+    # tiled kernel at HB = 10 with 16 x 128 tiles only, up to 16 chunks; above: 32-bit indices
+    chunked = 256 < K <= 16384 and int(opts.get("chunked", 1)) != 0 and grid > 0
+    nch = 1 << max(0, (K - 1).bit_length() - 8) if chunked else 1  # chunk_count: 256-colour chunks
     tw_opt = int(opts.get("cost_tw", 128))
     generic = (variant != 0 or hb == 0 or (K > 256 and not chunked)
-               or (chunked and (hb != 10 or rows != 16 or tw_opt != 128)))
+               or (chunked and (hb != 10 or rows != 16 or tw_opt != 128 or nch > 16)))
     trim_w = {10: (3, 4, 5), 15: (4, 5, 7), 19: (5, 7, 9), 24: (6, 9, 12)}
     if generic:
         # cost_variant 2: the per-pixel pair; otherwise the LDS-tiled pair
-        kernel = "gen_hpass_kernel+gen_vpass_kernel" if variant == 2 else "gen_hrow_kernel+gen_vtile_kernel"
+        # (variant 1, the LDS-tiled pair: the vertical pass on the matrix cores up to half 64)
+        kernel = ("gen_hpass_kernel+gen_vpass_kernel" if variant == 2 else
+                  "gen_hrow4_kernel+gen_vmfma_kernel" if half <= 64 and int(opts.get("gen_vmfma", 1)) else
+                  "gen_hrow4_kernel+gen_vtile2_kernel" if half <= 64 else "gen_hrow4_kernel+gen_vtile_kernel")
         taps_exec = 7 * (2 * half + 1)
     else:
         kernel = "cost_mfma_kernel" if rows == 8 and hb == 10 else "cost16w_kernel"

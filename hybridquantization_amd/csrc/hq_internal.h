@@ -9,8 +9,9 @@ namespace hq {
 
 constexpr int kMaxK = 256;        // u8 palette indices (K <= 256 on the tiled path)
 constexpr int kMaxKWide = 1 << 24;  // K > 256: 32-bit indices (the plugin's limit, HQ:192)
-constexpr int kMaxKChunked = 4096;  // 256 < K <= 4096: palettes as 256-colour chunks, 16-bit indices
-// chunks of a palette of K colours on the chunked path: a power of two (2 .. 16)
+constexpr int kMaxKChunked = 16384;  // 256 < K <= 16384: palettes as 256-colour chunks, 16-bit indices
+constexpr int kMaxNchFast = 16;      // chunked palettes of up to 16 chunks run the tiled cost kernel
+// chunks of a palette of K colours on the chunked path: a power of two (2 .. 64)
 inline int chunk_count(int K) {
     int n = 1;
     while (256 * n < K) n <<= 1;

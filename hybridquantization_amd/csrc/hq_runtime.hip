@@ -143,8 +143,8 @@ struct hq_ctx {
     // sets of used bits [kUsedSlots][used_stride]; evaluation n fills set acc_par = n & 1
     int acc_par = 0;
     DevBuf d_pixerr;           // option "pixel_err": [P][n_own] per-pixel dE of the last evaluation
-    DevBuf d_idx32, d_used32;  // K > 4096 (hq_wide.hip): 32-bit index images, per-colour used flags
-    DevBuf d_idx16, d_dist;    // 256 < K <= 4096 (chunked): 16-bit index images, pass distances
+    DevBuf d_idx32, d_used32;  // K > 16384 (hq_wide.hip): 32-bit index images, per-colour used flags
+    DevBuf d_idx16, d_dist;    // 256 < K <= 16384 (chunked): 16-bit index images, pass distances
     int nch_cur = 1;           // chunks per palette of the population being enqueued (1: K <= 256)
     int last_nch = 1;          // ... of the last evaluation (its index image: u16 when > 1)
     float* h_pal = nullptr;   // pinned [P][K][4]
@@ -173,7 +173,7 @@ struct hq_ctx {
                            // "palette_split"; SURVEY 8e's split of large populations)
     int slice_ranks = 1, slice_rank = 0;  // test only: the same slice without a communicator
     int slice_lo = 0, slice_n = 0;        // the last evaluation's palettes held on this device
-    int chunked = 1;       // 256 < K <= 4096: palettes as 256-colour chunks through the grid and
+    int chunked = 1;       // 256 < K <= 16384: palettes as 256-colour chunks through the grid and
                            // tiled kernels (option "chunked"; 0 = the exhaustive K > 256 path)
     int img_u8_path = 1;   // assign reads the packed 8-bit image when there is one (option 'img_u8')
     int shard_solo = 0;    // experiment: a sharded search without a communicator (per-rank timing)
@@ -207,7 +207,7 @@ struct hq_search {
     Swasa* pol = nullptr;
     hq_swasa_params prm{};
     int P = 0, ite = 0, st = 0, cd = 0;  // state and candidate buffer parities
-    int nch = 1;                         // chunked palettes (256 < K <= 4096): chunks per palette
+    int nch = 1;                         // chunked palettes (256 < K <= 16384): chunks per palette
     bool fold = false;                   // accept steps reduce the partials (no finalize launch)
     float t_acc = 0.f;                   // temperature / threshold of the iteration
     double keep_acc = 0.0;               // whose population awaits acceptance
@@ -459,7 +459,8 @@ int ensure_population(hq_ctx* c, int P, int K) {
     // the generic path's [7][n_ext] scratch, here rather than at its first launch: an
     // allocation cannot happen while a search run is being captured into a graph
     const bool fast = c->cost_variant == 0 && c->fast_hb > 0 &&
-                      (c->nch_cur == 1 || (c->fast_hb == 10 && c->cost_rows == 16 && c->cost_tw == 128));
+                      (c->nch_cur == 1 || (c->nch_cur <= kMaxNchFast && c->fast_hb == 10 && c->cost_rows == 16 &&
+                                           c->cost_tw == 128));
     if (!fast || K > kMaxK) HIP_TRY(c, c->d_gen_t.ensure(sizeof(float) * 7 * (size_t)g.n_ext));
     return ensure_pinned(c, sizeof(float) * 4 * (size_t)P * K, sizeof(double) * (size_t)P * (1 + K));
 }
@@ -675,7 +676,8 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
     const float inv[3] = {1.0f / c->illum[0], 1.0f / c->illum[1], 1.0f / c->illum[2]};
     // chunked palettes: the 16 x 128 tiles at HB = 10 (else the generic path)
     const bool fast = c->cost_variant == 0 && c->fast_hb > 0 && !c->pal_generic &&
-                      (nch == 1 || (c->fast_hb == 10 && c->cost_rows == 16 && c->cost_tw == 128));
+                      (nch == 1 || (nch <= kMaxNchFast && c->fast_hb == 10 && c->cost_rows == 16 &&
+                                    c->cost_tw == 128));
     // 8-row tiles (cost_mfma_kernel) exist for the 21-tap bucket only
     const int rows = c->fast_hb == 10 ? c->cost_rows : 16;
     const int tw = c->fast_hb == 10 ? c->cost_tw : 128;  // 256-column tiles: HB = 10 only
@@ -827,8 +829,9 @@ int eval_partial_into_hout(hq_ctx* c, const float* palettes, int P, int K) {
     if (rc) return rc;
     if ((rc = bind(c))) return rc;
     const bool fits = palette_fits_fast(palettes, P, K);
-    // 256 < K <= 4096: chunks of 256 colours through the grid, assign and tiled
-    // cost kernels.  Palettes outside the fast range (non-finite colours among
+    // 256 < K <= 16384: chunks of 256 colours through the grid and assign, and the
+    // tiled cost kernel up to 16 chunks (the generic pair above).  Palettes outside
+    // the fast range (non-finite colours among
     // them) take the exhaustive K > 256 path instead, which keeps the
     // reference's NaN semantics across all K colours.
     c->nch_cur = c->chunked && fits && c->G2 > 0 && K > kMaxK && K <= kMaxKChunked ? chunk_count(K) : 1;
@@ -1489,7 +1492,7 @@ int hq_search_create(hq_ctx* c, const hq_swasa_params* params, int K, uint64_t s
     *out = nullptr;
     if (params->population < 1 || params->imax < 1 || params->iTc < 1 || K < 1)
         return fail(c, HQ_ERR_ARG, "bad SWASA parameters");
-    // device-resident: K <= 256, or chunked palettes (256 < K <= 4096) of at most
+    // device-resident: K <= 256, or chunked palettes (256 < K <= 16384) of at most
     // kSaMaxP sub-palettes in all
     const int nch = K > kMaxK && K <= kMaxKChunked && c->chunked && c->G2 > 0 ? chunk_count(K) : 1;
     const bool device = c->sa_device && params->population * nch <= kSaMaxP && (K <= kMaxK || nch > 1);

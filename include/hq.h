@@ -106,9 +106,10 @@ int hq_get_labref(hq_ctx *ctx, float *lab4);
 
 /* IM:620 computeQuantizationErrorPopulation for P palettes of K colours
  * (K in [1, 2^24] as the plugin allows, HQ:192).  K <= 256: the pruned grid
- * argmin and the tiled fast stencil.  256 < K <= 4096: chunked palettes (nch
- * sub-palettes of 256 through the same grid, assign and fast stencil, 16-bit
- * indices; option "chunked").  K > 4096, palettes with non-finite colours or
+ * argmin and the tiled fast stencil.  256 < K <= 16384: chunked palettes (nch
+ * sub-palettes of 256 through the same grid and assign, 16-bit indices; the fast
+ * stencil up to K = 4096, the generic one above; option "chunked").  K > 16384,
+ * palettes with non-finite colours or
  * outside the fast path's range, option "chunked" 0 or "grid" 0: the exhaustive
  * argmin with 32-bit indices and the generic stencil path.  All give the same
  * indices and used flags (bit-exact) and the same cost (1e-6 relative):
