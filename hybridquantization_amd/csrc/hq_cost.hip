@@ -1432,6 +1432,47 @@ __global__ __launch_bounds__(256) void gen_vtile_kernel(GenArgs a, int tiles_x) 
 // in the same order as gen_vtile (filters one after another, each filter's
 // taps in chunks of 16), so every pixel's dE is bit-identical (the fixed-point
 // sums round per tile, and the tiles differ: 2^-20 per partial).
+// One filter's window (rows y0 - half .. of the tile's 32 columns, NE = RH x 32
+// dwords) from a [n_ext] plane into LDS by DMA.  An image width that is a
+// multiple of 4 makes every row segment 16-B aligned: global_load_lds_dwordx4,
+// 1 KiB per wave instruction (a lane's 4 dwords: row e4 / 8, columns 4 (e4 % 8)
+// .. + 3; the last tile column reads up to 31 elements past its row, which stay
+// inside the planes' 256-B tail pad and feed only masked output columns);
+// otherwise one dword per lane, columns clamped.  (Dword DMA is 4x the
+// instructions, and their issue held the vertical pass.)
+template <typename T>
+__device__ __forceinline__ void dma_window(const T* plane, T* dst, int NE, int tid, int wv, const Geom& g, int x0,
+                                           int y0, int half, bool rows_inside, bool wide) {
+    auto row_off = [&](int i) -> uint32_t {
+        int gy = y0 - half + i;
+        if (!rows_inside) {
+            gy = reflect_clamp(gy, g.H);
+            gy = min(max(gy, g.e0), g.e1 - 1);
+        }
+        return (uint32_t)((gy - g.e0) * g.W);
+    };
+    if (wide) {
+        const int NE4 = NE >> 2;
+        for (int e0 = 0; e0 < NE4; e0 += 256) {
+            const int e = e0 + tid;
+            if (e < NE4) {
+                const T* src = plane + row_off(e >> 3) + (uint32_t)(x0 + 4 * (e & 7));
+                __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(dst + 4 * (e0 + 64 * wv)),
+                                                 16, 0, 0);
+            }
+        }
+    } else {
+        const int jx = min(x0 + (tid & 31), g.W - 1);
+        for (int e0 = 0; e0 < NE; e0 += 256) {
+            const int e = e0 + tid;
+            if (e < NE) {
+                const T* src = plane + row_off(e >> 5) + (uint32_t)jx;
+                __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(dst + e0 + 64 * wv), 4, 0, 0);
+            }
+        }
+    }
+}
+
 constexpr int kVt2W = 32, kVt2MaxHalf = 64;
 #ifndef HQ_VT2_RB
 #define HQ_VT2_RB 8  // gen_vtile2: output rows per thread, tiles of 32 x 8 RB (16: 3.677 vs 3.619 ms at 300/50)
@@ -1448,23 +1489,9 @@ __global__ __launch_bounds__(256) void gen_vtile2_kernel(GenArgs a, int tiles_x)
     const int64_t n = g.n_ext;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool rows_inside = y0 - half >= g.e0 && y0 - half >= 0 && y0 + kVt2H + half <= g.e1 && y0 + kVt2H + half <= g.H;
-    const int jx = min(x0 + c, g.W - 1);
+    const bool wide = (g.W & 3) == 0;
     auto issue = [&](int f, int b) {
-        const float* plane = a.t + (int64_t)f * n;
-        float* dst = s_w2 + b * NE;
-        for (int e0 = 0; e0 < NE; e0 += 256) {
-            const int e = e0 + tid;
-            if (e < NE) {
-                const int i = e >> 5;
-                int gy = y0 - half + i;
-                if (!rows_inside) {
-                    gy = reflect_clamp(gy, g.H);
-                    gy = min(max(gy, g.e0), g.e1 - 1);
-                }
-                const float* src = plane + (uint32_t)((gy - g.e0) * g.W + jx);
-                __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(dst + e0 + 64 * wv), 4, 0, 0);
-            }
-        }
+        dma_window(a.t + (int64_t)f * n, s_w2 + b * NE, NE, tid, wv, g, x0, y0, half, rows_inside, wide);
     };
     float acc[3][RB];
 #pragma unroll
@@ -1524,7 +1551,7 @@ __global__ __launch_bounds__(256) void gen_vtile2_kernel(GenArgs a, int tiles_x)
 // buckets: gen_hrow4<SPLIT> writes each plane value x as the dword (hi, lo) of
 // x 2^14 (split_f16), which is two K slots of the B operand as it stands; A
 // holds the vertical taps x 2^16 split on the host, each tap part in both
-// slots of a row (build_vtile_pair_fragments), the hi parts in one MFMA and
+// slots of a row (build_vtile_dup_taps, read from LDS), the hi parts in one MFMA and
 // the lo parts in the next: (t_hi + t_lo)(x_hi + x_lo), every product exact in
 // the fp32 accumulator.  A 16 x 16 output block takes K steps of 16 window rows
 // (S = ceil((16 + 2 half) / 16)); K slot (g, 2 j + h) of step s is window row
@@ -1535,8 +1562,8 @@ __global__ __launch_bounds__(256) void gen_vtile2_kernel(GenArgs a, int tiles_x)
 // Lab matrix).
 template <int DE>
 __global__ __launch_bounds__(256) void gen_vmfma_kernel(GenArgs a, int tiles_x) {
-    // [2][window (64 + 2 half) x 32 dwords, then the filter's A fragments S x 2 x 64 x 16 B]
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_wm[];
+    // [2][64 + 2 half][32] windows, then the duplicated split taps [7][hi, lo][TP]
+    extern __shared__ uint32_t s_wm[];
     constexpr int TW = kVt2W, TH = 64;
     __shared__ double s_red[4];
     const int tid = threadIdx.x, lane = tid & 63, n = lane & 15, g = lane >> 4;
@@ -1544,31 +1571,16 @@ __global__ __launch_bounds__(256) void gen_vmfma_kernel(GenArgs a, int tiles_x) 
     const Geom& gm = a.g;
     const int x0 = (blockIdx.x % tiles_x) * TW, y0 = gm.r0 + (blockIdx.x / tiles_x) * TH;
     const int half = a.half, RH = TH + 2 * half, NE = RH * TW, S = (16 + 2 * half + 15) / 16;
-    const int NF = S * 2 * 64 * 4, BUF = (NE + 3) / 4 * 4 + NF;  // fragment dwords; dwords per buffer
+    const int BUF = NE, TP = 16 * S + 16;
+    uint32_t* s_tap = s_wm + 2 * BUF;
+    // the taps, once per workgroup (their first reads are after the first barrier)
+    for (int i = tid; i < kNumFilt * 2 * TP; i += 256) s_tap[i] = a.vtapd[i];
     const int64_t np = gm.n_ext;
     const bool rows_inside = y0 - half >= gm.e0 && y0 - half >= 0 && y0 + TH + half <= gm.e1 && y0 + TH + half <= gm.H;
-    const int jx = min(x0 + (tid & (TW - 1)), gm.W - 1);
+    const bool wide = (gm.W & 3) == 0;
     auto issue = [&](int f, int b) {
-        const uint32_t* plane = reinterpret_cast<const uint32_t*>(a.t) + (int64_t)f * np;
-        uint32_t* dst = s_wm + b * BUF;
-        // the filter's A fragments, 1 KiB per wave instruction (16 B per lane)
-        uint32_t* fdst = dst + (NE + 3) / 4 * 4;
-        const uint4* fsrc = a.vfragm + (int64_t)f * S * 2 * 64;
-        for (int q = wv; q < 2 * S; q += 4)
-            __builtin_amdgcn_global_load_lds(fsrc + q * 64 + (tid & 63),
-                                             (__attribute__((address_space(3))) void*)(fdst + q * 256), 16, 0, 0);
-        for (int e0 = 0; e0 < NE; e0 += 256) {
-            const int e = e0 + tid;
-            if (e < NE) {
-                int gy = y0 - half + (e >> 5);
-                if (!rows_inside) {
-                    gy = reflect_clamp(gy, gm.H);
-                    gy = min(max(gy, gm.e0), gm.e1 - 1);
-                }
-                const uint32_t* src = plane + (uint32_t)((gy - gm.e0) * gm.W + jx);
-                __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(dst + e0 + 64 * wv), 4, 0, 0);
-            }
-        }
+        dma_window(reinterpret_cast<const uint32_t*>(a.t) + (int64_t)f * np, s_wm + b * BUF, NE, tid, wv, gm, x0, y0,
+                   half, rows_inside, wide);
     };
     f32x4v D[3][2];
 #pragma unroll
@@ -1579,10 +1591,16 @@ __global__ __launch_bounds__(256) void gen_vmfma_kernel(GenArgs a, int tiles_x) 
         __syncthreads();                     // every wave's rows; window f - 1's readers are done
         if (f + 1 < kNumFilt) issue(f + 1, (f + 1) & 1);
         const uint32_t* win = s_wm + (f & 1) * BUF;
-        const uint4* fa = reinterpret_cast<const uint4*>(win + (NE + 3) / 4 * 4) + lane;  // [step][hi, lo][lane]
+        // A of step s: dwords 16 s + 4 g + j - m + 15 (j = 0 .. 3) of the filter's
+        // duplicated hi and lo tap rows -- a window sliding over the taps
+        // (fragments read from global memory left each filter waiting on L2)
+        const uint32_t* th = s_tap + f * 2 * TP + 4 * g - (lane & 15) + 15;
         f32x4v e0 = {0.f, 0.f, 0.f, 0.f}, e1 = {0.f, 0.f, 0.f, 0.f};
         for (int st = 0; st < S; ++st) {
-            const uint4 ch = fa[st * 128], cl = fa[st * 128 + 64];
+          {
+            uint4 ch, cl;
+            ch.x = th[16 * st]; ch.y = th[16 * st + 1]; ch.z = th[16 * st + 2]; ch.w = th[16 * st + 3];
+            cl.x = th[TP + 16 * st]; cl.y = th[TP + 16 * st + 1]; cl.z = th[TP + 16 * st + 2]; cl.w = th[TP + 16 * st + 3];
             const int r = 16 * wv + 16 * st + 4 * g;
             u32x4 b0, b1;
 #pragma unroll
@@ -1597,6 +1615,7 @@ __global__ __launch_bounds__(256) void gen_vmfma_kernel(GenArgs a, int tiles_x) 
             e1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(AH, B1, e1, 0, 0, 0);
             e0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(AL, B0, e0, 0, 0, 0);
             e1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(AL, B1, e1, 0, 0, 0);
+          }
         }
         const int chp = f == 6 ? 0 : f % 3;  // planes t1.xyz, t2.xyz, t3 -> channels x y z x y z x
         if (chp == 0) { D[0][0] += e0; D[0][1] += e1; }
@@ -1624,6 +1643,119 @@ __global__ __launch_bounds__(256) void gen_vmfma_kernel(GenArgs a, int tiles_x) 
     __syncthreads();
     if (tid == 0) acc_add(a.acc, a.P, a.p, blockIdx.x, (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]));
 }
+
+// gen_hmfma: the horizontal pass on the matrix cores as well (with gen_vmfma;
+// palettes in the fast range): gen_vmfma's pair scheme on its side.  D[m][n] =
+// sum_k A[m][k] B[k][n] with m an output column of a 16-column block, n a row
+// and k an input column: B of step s for lane (n, g) is columns 16 s + 4 g ..
+// + 3 of row n's segment (one ds_read_b128 of split dwords), A the
+// horizontal taps' duplicated rows (build_vtile_dup_taps with k3 signed: the
+// t3 plane's horizontal taps, CL:254-267).  D's lane holds 4 adjacent output
+// columns of one row: one 16-B store of split dwords per plane, which is
+// gen_vmfma's input as it stands.  A workgroup: 16 rows x 128 columns (4 waves
+// x 2 blocks of 16); its segment the 3 channels' split opponent colours,
+// [3][16][pitch] dwords, pitch = 8 mod 64 (ds_read_b128's lane groups then hit
+// 64 distinct banks).
+constexpr int kHmCB = 2, kHmCols = 64 * kHmCB;
+static int hmfma_seg_cols(int H) { return kHmCols - 16 + 16 * ((16 + 2 * H + 15) / 16); }
+static int hmfma_pitch(int H) { return (hmfma_seg_cols(H) - 8 + 63) / 64 * 64 + 8; }
+template <typename IT>
+__global__ __launch_bounds__(256) void gen_hmfma_kernel(GenArgs a, int pitch) {
+    extern __shared__ uint32_t s_hm[];  // [3][16][pitch] segment, then the taps [7][hi, lo][TP]
+    const int tid = threadIdx.x, lane = tid & 63, n = lane & 15, g = lane >> 4;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int half = a.half, W = a.g.W, rows = a.g.e1 - a.g.e0;
+    const int S = (16 + 2 * half + 15) / 16, TP = 16 * S + 16, SW = kHmCols - 16 + 16 * S;
+    const int x0 = blockIdx.x * kHmCols, y0 = blockIdx.y * 16;
+    uint32_t* s_tap = s_hm + 3 * 16 * pitch;
+    for (int i = tid; i < kNumFilt * 2 * TP; i += 256) s_tap[i] = a.htapd[i];
+    // the segment, column tid of every row (SW <= 256 for half <= 64): all 16
+    // index loads, then the colours, then the split stores
+    if (tid < SW) {
+        const int x = reflect_clamp(x0 - half + tid, W);  // (columns past the row end: finite, masked)
+        const IT* col = static_cast<const IT*>(a.idx) + x;
+#pragma unroll
+        for (int r0 = 0; r0 < 16; r0 += 8) {
+            uint32_t ix[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) ix[u] = (uint32_t)col[(int64_t)min(y0 + r0 + u, rows - 1) * W];
+            float4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = a.opp[ix[u]];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                uint32_t* d = s_hm + (r0 + u) * pitch + tid;
+                d[0] = split_f16(v[u].x);
+                d[16 * pitch] = split_f16(v[u].y);
+                d[32 * pitch] = split_f16(v[u].z);
+            }
+        }
+    }
+    __syncthreads();
+    f32x4v D[kNumFilt][kHmCB];
+#pragma unroll
+    for (int f = 0; f < kNumFilt; ++f)
+#pragma unroll
+        for (int cb = 0; cb < kHmCB; ++cb) D[f][cb] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    const uint32_t* sb = s_hm + n * pitch + 16 * kHmCB * wv + 4 * g;
+    const uint32_t* th = s_tap + 4 * g - n + 15;  // (m = lane & 15 = n)
+    for (int st = 0; st < S; ++st) {
+        f16x8 B[3][kHmCB];
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch)
+#pragma unroll
+            for (int cb = 0; cb < kHmCB; ++cb)
+                B[ch][cb] = __builtin_bit_cast(f16x8, *reinterpret_cast<const u32x4*>(sb + ch * 16 * pitch + 16 * cb + 16 * st));
+#pragma unroll
+        for (int f = 0; f < kNumFilt; ++f) {
+            const int ch = f == 6 ? 0 : f % 3;  // planes t1.xyz, t2.xyz, t3 -> channels x y z x y z x
+            const uint32_t* tf = th + f * 2 * TP + 16 * st;
+            uint4 ah, al;
+            ah.x = tf[0]; ah.y = tf[1]; ah.z = tf[2]; ah.w = tf[3];
+            al.x = tf[TP]; al.y = tf[TP + 1]; al.z = tf[TP + 2]; al.w = tf[TP + 3];
+            const f16x8 AH = __builtin_bit_cast(f16x8, ah), AL = __builtin_bit_cast(f16x8, al);
+#pragma unroll
+            for (int cb = 0; cb < kHmCB; ++cb) D[f][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(AH, B[ch][cb], D[f][cb], 0, 0, 0);
+#pragma unroll
+            for (int cb = 0; cb < kHmCB; ++cb) D[f][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(AL, B[ch][cb], D[f][cb], 0, 0, 0);
+        }
+    }
+    // lane (n, g): plane row y0 + n, columns 4 g .. 4 g + 3 of each block, x 2^-30
+    const int y = y0 + n;
+    if (y >= rows) return;
+    uint32_t* t = reinterpret_cast<uint32_t*>(a.t);
+    const int64_t np = a.g.n_ext;
+#pragma unroll
+    for (int cb = 0; cb < kHmCB; ++cb) {
+        const int x = x0 + 16 * (kHmCB * wv + cb) + 4 * g;
+        const int64_t q = (int64_t)y * W + x;
+        if ((W & 3) == 0 && x + 3 < W) {
+#pragma unroll
+            for (int f = 0; f < kNumFilt; ++f)
+                *reinterpret_cast<uint4*>(t + f * np + q) =
+                    make_uint4(split_f16(D[f][cb][0] * kVOutScale), split_f16(D[f][cb][1] * kVOutScale),
+                               split_f16(D[f][cb][2] * kVOutScale), split_f16(D[f][cb][3] * kVOutScale));
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (x + i < W)
+#pragma unroll
+                    for (int f = 0; f < kNumFilt; ++f) t[f * np + q + i] = split_f16(D[f][cb][i] * kVOutScale);
+        }
+    }
+}
+template __global__ void gen_hmfma_kernel<uint8_t>(GenArgs, int);
+template __global__ void gen_hmfma_kernel<uint16_t>(GenArgs, int);
+template __global__ void gen_hmfma_kernel<uint32_t>(GenArgs, int);
+
+// (explicit instantiations: taken only through a generic lambda, the dE94
+// kernels' host handles were left undefined by the host compile)
+template __global__ void gen_vmfma_kernel<0>(GenArgs, int);
+template __global__ void gen_vmfma_kernel<1>(GenArgs, int);
+template __global__ void gen_vtile2_kernel<0, HQ_VT2_RB>(GenArgs, int);
+template __global__ void gen_vtile2_kernel<1, HQ_VT2_RB>(GenArgs, int);
+template __global__ void gen_vtile_kernel<0>(GenArgs, int);
+template __global__ void gen_vtile_kernel<1>(GenArgs, int);
 
 // ----------------------------------------------------------------------------
 // Host side: tap tables, MFMA fragments, launchers
@@ -1776,30 +1908,26 @@ void build_vpass_f16_pair_fragments(int HB, int H, const float* k1, const float*
                     }
 }
 
-// gen_vmfma's A fragments: [filter][step s][hi, lo][lane][8] f16, S steps of 16
-// window rows (S = vtile_pair_steps(H)).  Lane l: output row m = l & 15 of a
-// block, K slots 2 j + h of lane group g = l >> 4 hold tap t = 16 s + 4 g + j - m
-// (window row 16 s + 4 g + j), the same part in both slots of the row; zero
-// outside 0 .. 2 H.  Taps per plane: k1.xyz, k2.xyz, |k3| (the vertical taps of
-// t1.xyz, t2.xyz, t3), x 2^16.
+// gen_vmfma's A operands come from duplicated tap rows (below): in the pair
+// layout lane l = (m = l & 15, g = l >> 4) needs, in K slots 2 j + h of step s,
+// part h of tap t = 16 s + 4 g + j - m -- a window sliding over the taps.
 int vtile_pair_steps(int H) { return (16 + 2 * H + 15) / 16; }
-size_t vtile_pair_fragment_halves(int H) { return (size_t)kNumFilt * vtile_pair_steps(H) * 2 * 64 * 8; }
-void build_vtile_pair_fragments(int H, const float* k1, const float* k2, const float* absk3, uint16_t* out) {
-    const int S = vtile_pair_steps(H), T = 2 * H + 1;
+// gen_vmfma's tap rows: [7][hi, lo][TP = 16 S + 16] dwords, entry i the part of
+// tap i - 15 x 2^16 in both halves (zero outside 0 .. 2 H): A of step s for
+// lane (m, g) is entries 16 s + 4 g - m + 15 .. + 3 of the filter's rows.
+size_t vtile_dup_tap_words(int H) { return (size_t)kNumFilt * 2 * (16 * vtile_pair_steps(H) + 16); }
+void build_vtile_dup_taps(int H, const float* k1, const float* k2, const float* absk3, uint32_t* out) {
+    const int TP = 16 * vtile_pair_steps(H) + 16, T = 2 * H + 1;
     for (int f = 0; f < kNumFilt; ++f)
-        for (int st = 0; st < S; ++st)
-            for (int l = 0; l < 64; ++l)
-                for (int kk = 0; kk < 8; ++kk) {
-                    const int m = l & 15, g = l >> 4, t = 16 * st + 4 * g + (kk >> 1) - m;
-                    float w = 0.f;
-                    if (t >= 0 && t < T) w = f < 3 ? k1[4 * t + f] : f < 6 ? k2[4 * t + f - 3] : absk3[t];
-                    w *= kVTapScale;
-                    const uint16_t hi = host_f16(w);
-                    const uint16_t lo = host_f16(w - host_f16_to_f32(hi));
-                    const size_t base = (((size_t)f * S + st) * 2) * 64;
-                    out[((base + 0 * 64) + l) * 8 + kk] = hi;
-                    out[((base + 1 * 64) + l) * 8 + kk] = lo;
-                }
+        for (int i = 0; i < TP; ++i) {
+            const int t = i - 15;
+            float w = 0.f;
+            if (t >= 0 && t < T) w = f < 3 ? k1[4 * t + f] : f < 6 ? k2[4 * t + f - 3] : absk3[t];
+            w *= kVTapScale;
+            const uint32_t hi = host_f16(w), lo = host_f16(w - host_f16_to_f32((uint16_t)hi));
+            out[((size_t)f * 2 + 0) * TP + i] = hi | (hi << 16);
+            out[((size_t)f * 2 + 1) * TP + i] = lo | (lo << 16);
+        }
 }
 
 // The narrow k1 filters' taps outside the bucket's trimmed windows are below
@@ -1966,14 +2094,27 @@ static void launch_hrow4(const GenArgs& a, int idx_bytes, hipStream_t s) {
 hipError_t launch_cost_tiled_generic(const GenArgs& a, int de, int idx_bytes, hipStream_t s) {
     const hipEvent_t ev0 = t_ev_start, ev1 = t_ev_stop;
     t_ev_stop = nullptr;
-    const bool vm = a.vmfma && a.vfragm && a.half <= kVt2MaxHalf;  // the matrix-core vertical pass
+    const bool vm = a.vmfma && a.vtapd && a.half <= kVt2MaxHalf;  // the matrix-core vertical pass
     if (vm) {
-        launch_hrow4<true>(a, idx_bytes, s);
+        if (a.hmfma && a.htapd) {  // both passes on the matrix cores
+            const int pitch = hmfma_pitch(a.half), S = (16 + 2 * a.half + 15) / 16;
+            const size_t hl = sizeof(uint32_t) * (3 * 16 * (size_t)pitch + (size_t)kNumFilt * 2 * (16 * S + 16));
+            const dim3 hg((unsigned)((a.g.W + kHmCols - 1) / kHmCols), (unsigned)((a.g.e1 - a.g.e0 + 15) / 16));
+            auto goh = [&](auto kern) {
+                if (!allow_dyn_lds(reinterpret_cast<const void*>(kern), hl)) return;
+                HQ_LAUNCH(kern, hg, dim3(256), hl, s, a, pitch);
+            };
+            if (idx_bytes == 4) goh(gen_hmfma_kernel<uint32_t>);
+            else if (idx_bytes == 2) goh(gen_hmfma_kernel<uint16_t>);
+            else goh(gen_hmfma_kernel<uint8_t>);
+        } else {
+            launch_hrow4<true>(a, idx_bytes, s);
+        }
         t_ev_start = nullptr;
         t_ev_stop = ev1;
         const int tx = (a.g.W + kVt2W - 1) / kVt2W, ty = (a.g.r1 - a.g.r0 + 63) / 64;
-        const int S = (16 + 2 * a.half + 15) / 16, NE = kVt2W * (64 + 2 * a.half);
-        const size_t l2 = sizeof(uint32_t) * 2 * ((size_t)(NE + 3) / 4 * 4 + (size_t)S * 2 * 64 * 4);
+        const int S = (16 + 2 * a.half + 15) / 16;
+        const size_t l2 = sizeof(uint32_t) * (2 * kVt2W * (64 + 2 * (size_t)a.half) + (size_t)kNumFilt * 2 * (16 * S + 16));
         auto gov = [&](auto kern) {
             if (!allow_dyn_lds(reinterpret_cast<const void*>(kern), l2)) return;
             HQ_LAUNCH(kern, dim3((unsigned)(tx * ty)), dim3(256), l2, s, a, tx);

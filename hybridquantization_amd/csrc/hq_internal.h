@@ -231,7 +231,9 @@ struct GenArgs {
     int hrow_no = 4;     // gen_hrow4's outputs per thread: 4 or 8
     int vtile2 = 1;      // tiled path: double-buffered LDS-DMA vertical pass (gen_vtile2), else gen_vtile
     int vmfma = 1;       // tiled path: the vertical pass on the matrix cores (gen_vmfma, split f16)
-    const uint4* vfragm = nullptr;  // its A fragments [7][S][hi, lo][64] (build_vtile_pair_fragments)
+    const uint32_t* vtapd = nullptr;  // its duplicated split taps [7][hi, lo][16 S + 16] (build_vtile_dup_taps)
+    int hmfma = 1;       // with vmfma: the horizontal pass on the matrix cores too (gen_hmfma)
+    const uint32_t* htapd = nullptr;  // its taps, the same layout (k3 signed: the horizontal t3 taps)
     const float4* htaps = nullptr;  // gen_hrow4: [T][2] (k1.xyz, k3), (k2.xyz, 0) horizontal taps
 };
 

@@ -43,8 +43,8 @@ size_t vpass_f16_stack_fragment_halves(int HB);
 void build_vpass_f16_pair_fragments(int HB, int H, const float* k1, const float* k2, const float* k3,
                                     const float* absk3, uint16_t* out);
 size_t vpass_f16_pair_fragment_halves(int HB);
-size_t vtile_pair_fragment_halves(int H);
-void build_vtile_pair_fragments(int H, const float* k1, const float* k2, const float* absk3, uint16_t* out);
+size_t vtile_dup_tap_words(int H);
+void build_vtile_dup_taps(int H, const float* k1, const float* k2, const float* absk3, uint32_t* out);
 void build_vpass_f16_stack_fragments(int HB, int H, const float* k1, const float* k2, const float* k3,
                                      const float* absk3, uint16_t* out);
 size_t fast_taps_bytes(int HB);
@@ -123,7 +123,7 @@ struct hq_ctx {
     DevBuf d_taps;     // fast path taps, build_fast_taps (the filters centred in the bucket)
     DevBuf d_vfrag16;  // split-f16 MFMA A fragments of the stacked vertical taps
     DevBuf d_vfrag16p; // the same in cost16w's (hi, lo) pair layout
-    DevBuf d_vfragm;   // the tiled generic path's matrix-core vertical taps (build_vtile_pair_fragments)
+    DevBuf d_vfragm;   // the tiled generic path's matrix-core vertical taps (build_vtile_dup_taps)
     DevBuf d_htaps;    // gen_hrow4's packed horizontal taps [T][2] float4
 
     // image
@@ -161,6 +161,7 @@ struct hq_ctx {
     int gen_hrow4 = 1;     // tiled generic path: 4 outputs per thread in the horizontal pass
     int gen_vtile2 = 1;    // tiled generic path: double-buffered LDS-DMA vertical pass (half <= 64)
     int gen_vmfma = 1;     // tiled generic path: the vertical pass on the matrix cores (half <= 64)
+    int gen_hmfma = 1;     // ... and the horizontal pass (gen_hmfma) with it
     int gen_hrow_no = 4;   // tiled generic path: horizontal outputs per thread (4 or 8)
     int sa_graph = HQ_SA_GRAPH;  // device-resident search: each run's kernels as one hipGraph
     int assign_blocks_per_cu = 0;  // 0 = auto: assign_pipe_kernel<NG>'s residency (the occupancy
@@ -461,7 +462,7 @@ int ensure_population(hq_ctx* c, int P, int K) {
     const bool fast = c->cost_variant == 0 && c->fast_hb > 0 &&
                       (c->nch_cur == 1 || (c->nch_cur <= kMaxNchFast && c->fast_hb == 10 && c->cost_rows == 16 &&
                                            c->cost_tw == 128));
-    if (!fast || K > kMaxK) HIP_TRY(c, c->d_gen_t.ensure(sizeof(float) * 7 * (size_t)g.n_ext));
+    if (!fast || K > kMaxK) HIP_TRY(c, c->d_gen_t.ensure(sizeof(float) * 7 * (size_t)g.n_ext + 256));
     return ensure_pinned(c, sizeof(float) * 4 * (size_t)P * K, sizeof(double) * (size_t)P * (1 + K));
 }
 
@@ -513,7 +514,7 @@ int enqueue_generic_cost(hq_ctx* c, int P, const void* idx_base, int idx_bytes, 
                          const hipEvent_t* ev, int p_off = 0) {
     const Geom& g = c->g;
     hipStream_t s = c->stream;
-    HIP_TRY(c, c->d_gen_t.ensure(sizeof(float) * 7 * (size_t)g.n_ext));
+    HIP_TRY(c, c->d_gen_t.ensure(sizeof(float) * 7 * (size_t)g.n_ext + 256));
     const int64_t n_own = (int64_t)g.W * (g.r1 - g.r0);
     const float inv[3] = {1.0f / c->illum[0], 1.0f / c->illum[1], 1.0f / c->illum[2]};
     for (int p = 0; p < P; ++p) {
@@ -539,8 +540,11 @@ int enqueue_generic_cost(hq_ctx* c, int P, const void* idx_base, int idx_bytes, 
         gn.hrow4 = c->gen_hrow4;
         gn.hrow_no = c->gen_hrow_no;
         gn.vtile2 = c->gen_vtile2;
-        gn.vmfma = c->gen_vmfma;
-        gn.vfragm = c->d_vfragm.bytes ? c->d_vfragm.as<uint4>() : nullptr;
+        // split-f16 planes hold |x| < 4 (x 2^14): palettes outside the fast range stay on fp32
+        gn.vmfma = c->gen_vmfma && !c->pal_generic;
+        gn.vtapd = c->d_vfragm.bytes ? c->d_vfragm.as<uint32_t>() : nullptr;
+        gn.hmfma = c->gen_hmfma;
+        gn.htapd = gn.vtapd ? gn.vtapd + vtile_dup_tap_words(c->half) : nullptr;
         gn.htaps = c->d_htaps.as<float4>();
         opp2xyz_over_illum(inv, gn.m_lab);
         // the events span every palette's launch pair: start on the first, stop on the last
@@ -1173,10 +1177,12 @@ int hq_set_filters(hq_ctx* c, int taps, const float* k1, const float* k2, const 
         }
         HIP_TRY(c, c->d_htaps.ensure(sizeof(float) * ht.size()));
         HIP_TRY(c, hipMemcpy(c->d_htaps.p, ht.data(), sizeof(float) * ht.size(), hipMemcpyHostToDevice));
-        std::vector<uint16_t> fm(vtile_pair_fragment_halves(c->half));
-        build_vtile_pair_fragments(c->half, k1, k2, absk3, fm.data());
-        HIP_TRY(c, c->d_vfragm.ensure(fm.size() * sizeof(uint16_t)));
-        HIP_TRY(c, hipMemcpy(c->d_vfragm.p, fm.data(), fm.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+        // gen_vmfma's vertical taps (t3: |k3|), then gen_hmfma's horizontal ones (t3: k3)
+        std::vector<uint32_t> fm(2 * vtile_dup_tap_words(c->half));
+        build_vtile_dup_taps(c->half, k1, k2, absk3, fm.data());
+        build_vtile_dup_taps(c->half, k1, k2, k3, fm.data() + vtile_dup_tap_words(c->half));
+        HIP_TRY(c, c->d_vfragm.ensure(fm.size() * sizeof(uint32_t)));
+        HIP_TRY(c, hipMemcpy(c->d_vfragm.p, fm.data(), fm.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     }
     // fast path: the filters centred in the smallest tap bucket that holds them
     // (half-widths up to 24: every dpi / viewing distance of HQ:229-231 up to
@@ -1623,6 +1629,8 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
         c->gen_hrow_no = value;
     } else if (!std::strcmp(name, "gen_vmfma")) {
         c->gen_vmfma = value != 0;
+    } else if (!std::strcmp(name, "gen_hmfma")) {
+        c->gen_hmfma = value != 0;
     } else if (!std::strcmp(name, "gen_vtile2")) {
         c->gen_vtile2 = value != 0;
     } else if (!std::strcmp(name, "gen_hrow4")) {

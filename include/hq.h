@@ -210,6 +210,8 @@ int hq_profile_reset(hq_ctx *ctx);
  *                  (same planes bit for bit)
  *   "gen_vmfma"    the LDS-tiled generic path's vertical pass (halfSize <= 64) on the matrix
  *                  cores in split f16 (as the fast path's; default 1), 0 = fp32 FMAs (gen_vtile2)
+ *   "gen_hmfma"    with gen_vmfma: the horizontal pass on the matrix cores too (default 1;
+ *                  palettes in the fast range), 0 = fp32 FMAs (gen_hrow4)
  *   "gen_vtile2"   the LDS-tiled generic path's vertical pass (halfSize <= 64): 1 (default) =
  *                  32 x 64 tiles, windows double-buffered by LDS DMA; 0 = 64 x 64 tiles with
  *                  one window at a time (same results bit for bit)

@@ -193,7 +193,9 @@ def test_generic_hrow4_bitwise(gpu, w, h, dpi, vd):
     K, P = 64, 2
     pals = np.stack([o.synthetic_palette(K, 9 + p) for p in range(P)]).reshape(P, -1)
     res = []
-    for h4, v2, vm, no in ((0, 0, 0, 4), (1, 0, 0, 4), (1, 1, 0, 4), (1, 1, 1, 4), (1, 1, 0, 8)):
+    for h4, v2, vm, no, hm in ((0, 0, 0, 4, 0), (1, 0, 0, 4, 0), (1, 1, 0, 4, 0), (1, 1, 1, 4, 0), (1, 1, 0, 8, 0),
+                               (1, 1, 1, 4, 1)):
+        m.setOption("gen_hmfma", hm)
         m.setOption("gen_hrow4", h4)
         m.setOption("gen_vtile2", v2)
         m.setOption("gen_vmfma", vm)
@@ -218,6 +220,11 @@ def test_generic_hrow4_bitwise(gpu, w, h, dpi, vd):
         np.testing.assert_allclose(res[3][1][p], res[2][1][p], rtol=0, atol=2e-4)
     np.testing.assert_allclose(res[3][0].reshape(P, 1 + K)[:, 0], res[2][0].reshape(P, 1 + K)[:, 0], rtol=1e-6)
     np.testing.assert_array_equal(res[3][0].reshape(P, 1 + K)[:, 1:], res[2][0].reshape(P, 1 + K)[:, 1:])
+    # gen_hmfma + gen_vmfma (the default): both passes on the matrix cores
+    for p in range(P):
+        np.testing.assert_allclose(res[5][1][p], res[2][1][p], rtol=0, atol=2e-4)
+    np.testing.assert_allclose(res[5][0].reshape(P, 1 + K)[:, 0], res[2][0].reshape(P, 1 + K)[:, 0], rtol=1e-6)
+    np.testing.assert_array_equal(res[5][0].reshape(P, 1 + K)[:, 1:], res[2][0].reshape(P, 1 + K)[:, 1:])
 
 
 @pytest.mark.parametrize("dpi,vd", [(150, 30.0), (96, 60.0), (200, 30.0)])
@@ -492,6 +499,26 @@ def test_out_of_range_palette_takes_generic_path(ip, filt):
     pal = g["palettes"][0].copy()
     pal[3, 1] = 2.5
     pal[5, 2] = -40.0
+    pals = np.stack([pal, g["palettes"][1]])
+    costs = ip.computeQuantizationErrorPopulation(pals.reshape(2, -1), 2.0)
+    for p in range(2):
+        ref, parts = c_oracle.eval_palette(rgba, g["lab"], pals[p], filt, w, return_parts=True)
+        assert np.isfinite(costs[p]) and abs(costs[p] - ref) <= 1e-6 * abs(ref), (p, costs[p], ref)
+        np.testing.assert_array_equal(ip.getIndices(p), parts["idx"].astype(np.uint8))
+
+
+def test_out_of_range_palette_every_pixel(ip, filt):
+    """Every colour of the palette beyond the split-f16 range (G + 2.2), so
+    every pixel's filtered error is out of the matrix-core range: the generic
+    path keeps both passes in fp32 (gn.vmfma off for such populations,
+    hq_runtime.hip) and the cost equals the oracle's."""
+    g, R, G, B = load_case("case_97x53_k64")
+    w = int(g["w"])
+    rgba = o.inline_rgba(R, G, B)
+    ip.setImage(rgba.reshape(-1), g["lab"].reshape(-1), w, ip.illum)
+    pal = g["palettes"][0].copy()
+    pal[:, 1] += 2.2
+    pal[:, 0] -= 0.5
     pals = np.stack([pal, g["palettes"][1]])
     costs = ip.computeQuantizationErrorPopulation(pals.reshape(2, -1), 2.0)
     for p in range(2):
