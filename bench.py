@@ -94,9 +94,11 @@ def cost_accounting(half, K, grid, opts):
     trim_w = {10: (3, 4, 5), 15: (4, 5, 7), 19: (5, 7, 9), 24: (6, 9, 12)}
     if generic:
         # cost_variant 2: the per-pixel pair; otherwise the LDS-tiled pair
-        # (variant 1, the LDS-tiled pair: the vertical pass on the matrix cores up to half 64)
+        # (variant 1, the LDS-tiled pair: both passes on the matrix cores up to half 64)
+        vm = half <= 64 and int(opts.get("gen_vmfma", 1))
         kernel = ("gen_hpass_kernel+gen_vpass_kernel" if variant == 2 else
-                  "gen_hrow4_kernel+gen_vmfma_kernel" if half <= 64 and int(opts.get("gen_vmfma", 1)) else
+                  "gen_hmfma_kernel+gen_vmfma_kernel" if vm and int(opts.get("gen_hmfma", 1)) else
+                  "gen_hrow4_kernel+gen_vmfma_kernel" if vm else
                   "gen_hrow4_kernel+gen_vtile2_kernel" if half <= 64 else "gen_hrow4_kernel+gen_vtile_kernel")
         taps_exec = 7 * (2 * half + 1)
     else:
