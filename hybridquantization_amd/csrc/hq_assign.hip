@@ -691,6 +691,11 @@ void launch_assign_t(const AssignArgs& a0, int P, hipStream_t s) {
     t_ev_start = ev0;
 }
 
+void launch_used_idx16(const AssignArgs& a, int P, hipStream_t s) {
+    const unsigned ub = (unsigned)std::min<int64_t>(512, (a.n_ext + 4095) / 4096);
+    HQ_LAUNCH(used_idx16_kernel, dim3(ub, (unsigned)P), dim3(256), 0, s, a);
+}
+
 hipError_t launch_assign(const AssignArgs& a, int P, hipStream_t s) {
     if (a.rgbx) launch_assign_t<true>(a, P, s);
     else launch_assign_t<false>(a, P, s);

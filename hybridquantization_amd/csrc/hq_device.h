@@ -281,6 +281,28 @@ __device__ __forceinline__ double acc_total(const uint64_t* acc, int P, int p) {
     return bad ? __builtin_nan("") : (double)hi * 4096.0 + (double)lo * (1.0 / kAccScale);
 }
 
+// Candidate-grid box bounds (build_grid, hq_search.hip; the 16-bit lists,
+// hq_lists16.hip).
+// Box bounds in fp32.  Box edges are multiples of 1/G (G a power of two):
+// exact.  Valid colours are finite (prep_palette routes non-finite palettes to
+// the exhaustive path), so every term is a correctly rounded difference,
+// squared and summed with non-negative terms: each bound is within 3 ulp
+// (2e-7 relative) of its exact value, and the 1e-5 margin covers that on
+// both sides of the test on top of the reference's own 1.1e-6.  An fp32
+// overflow (|colour| > 1e19) gives inf bounds: T = inf makes every colour a
+// candidate, which overflows the list into the exhaustive loop.  (fp64 was
+// ~570 VALU instructions per wave at half the fp32 rate.)
+__device__ __forceinline__ float ax_min2(float c, float lo, float hi) {
+    const float d = fmaxf(fmaxf(lo - c, c - hi), 0.f);
+    return d * d;
+}
+__device__ __forceinline__ float ax_max2(float c, float lo, float hi) {
+    const float d = fmaxf(c - lo, hi - c);
+    return d * d;
+}
+
+#define HQ_CAND_MARGIN (1.0f + 1e-5f)
+
 // ----------------------------------------------------------------------------
 // XCD-aware relabelling of a 1-D grid of N workgroups.  Workgroups are placed
 // round-robin over the 8 XCDs (b % 8), so XCD x is given the contiguous work

@@ -130,6 +130,28 @@ struct GridArgs {
     int nch;                // sub-palettes per palette (chunked palettes), else 1
 };
 
+// Native 16-bit candidate lists (hq_lists16.hip) for chunked palettes of 8 or
+// 16 chunks (1024 < K <= 4096): one grid over all K colours, level 1 at 16^3
+// cells (u16 count + 127 indices, 256 B), level 2 at 64^3 (u16 count + 15
+// indices, 32 B); count kN16Ovf = overflow.
+constexpr int kN16G1 = 16, kN16G2 = 64;
+constexpr int kN16L1Cap = 127, kN16L2Cap = 15;
+constexpr int kN16L1Words = kN16L1Cap + 1, kN16L2Words = kN16L2Cap + 1;  // u16 per entry
+constexpr uint16_t kN16Ovf = 0xffff;
+constexpr int kN16MinNch = 8;  // chunk counts that take the native lists (option "lists16")
+
+struct Lists16Args {
+    const float4* pal;      // [P][kpal] colours (the prepared sub-palettes, contiguous per palette)
+    const int* pflags;      // [P nch] sub-palette flags (non-finite colour: exhaustive)
+    uint16_t* lvl1;         // [P][16^3][kN16L1Words]
+    uint16_t* lvl2;         // [P][64^3][kN16L2Words]
+    uint32_t* used_glob;    // [kUsedSlots][used_stride]: [P][8 nch] used-colour bits, zeroed here
+    int used_stride;
+    uint64_t* acc_zero;     // the fixed-point sums of the cost kernel that follows, zeroed here
+    int P_acc;
+    int K, kpal, nch;
+};
+
 struct AssignArgs {
     const float* R;         // planar, n_ext floats (extended rows)
     const float* G;
@@ -156,6 +178,10 @@ struct AssignArgs {
     float* dist;            // [P / nch][idx_pitch] best reference distance (nch > 4 passes)
     int nch = 1, lg_nch = 0;
     int gstep = 1;          // (set by the launcher)
+    // native 16-bit lists (hq_lists16.hip): palette p's colours at pal + p kpal
+    const uint16_t* l1n = nullptr;
+    const uint16_t* l2n = nullptr;
+    int kpal = 0;
 };
 
 struct CostArgs {

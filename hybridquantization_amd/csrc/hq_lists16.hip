@@ -1,0 +1,427 @@
+// hq_lists16.hip -- native 16-bit candidate lists for chunked palettes of 8 or
+// 16 chunks (1024 < K <= 4096).  The chunked path (hq_assign.hip) runs one
+// grid per 256-colour chunk and nch / 4 assign passes that carry the best
+// distance so far through a scratch image: 16 lookups and list walks per pixel
+// at K = 4096.  Here one grid covers all K colours at a finer level 2 (64^3
+// cells of 1/64: about as many colours per cell as K = 256 has at 32^3) and
+// assign makes one lookup and one walk per pixel and palette, writing the
+// 16-bit index the chunked cost kernel reads (colour k = chunk k >> 8, entry
+// k & 255: the sub-palettes are the palette's colours in order).
+//
+// The lists are exact in the sense of build_grid (hq_search.hip): every
+// colour that can be the reference's argmin (CL:179-193: the first minimum of
+// sqrtf(d^2) in ascending index) for some pixel of a cell is listed.  A cell's
+// threshold T is the least upper bound of d^2 over the cell among the
+// colours; a colour whose lower bound exceeds T (1 + 1e-5) never wins there.
+// The walk ranks the candidates by d^2 and re-resolves a pixel whose runner-up
+// lies within 1e-6 relative (a possible tie of the reference's sqrtf) by the
+// least (sqrtf(d^2), index) over its list: the reference's first minimum.
+// Overflowing level-2 entries fall back to the pixel's level-1 list, an
+// overflowing level-1 list (or a pixel outside the unit cube, or a palette
+// with a non-finite colour) to all K colours, cooperatively by the wave.
+#include <mutex>
+#include <unordered_map>
+
+#include "hq_device.h"
+#include "hq_launch.h"
+
+namespace hq {
+
+// ----------------------------------------------------------------------------
+// The grid: one workgroup of 1024 threads per level-0 cell (side 1/4) and
+// palette, grid (64, P).  Level 0: the threshold over all K colours (read from
+// memory, 4 per thread) and the cell's candidates, compacted into LDS as
+// colours + indices.  Level 1: its 64 cells of side 1/16, 16 threads each, the
+// threshold and list over the level-0 candidates (positions into that LDS
+// array, and the colour indices to memory for assign's fallback).  Level 2:
+// the 4096 cells of side 1/64 below, one thread per cell (a wave's 64 threads
+// share a parent list: broadcast LDS reads), its entry written by that thread.
+// Each level's candidates are a superset of the colours that can win in its
+// cells: a pixel's winner w is within d(x, b) of it for every colour b, so
+// w passes the parent's test and then the child's over the parent's list.
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ float box_min2(float4 c, const float (&lo)[3], float w) {
+    return (ax_min2(c.x, lo[0], lo[0] + w) + ax_min2(c.y, lo[1], lo[1] + w)) + ax_min2(c.z, lo[2], lo[2] + w);
+}
+__device__ __forceinline__ float box_max2(float4 c, const float (&lo)[3], float w) {
+    return (ax_max2(c.x, lo[0], lo[0] + w) + ax_max2(c.y, lo[1], lo[1] + w)) + ax_max2(c.z, lo[2], lo[2] + w);
+}
+
+constexpr int kN16Threads = 1024;
+__global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
+    extern __shared__ float4 s_c0[];                               // [K] level-0 candidates
+    uint16_t* s_k0 = reinterpret_cast<uint16_t*>(s_c0 + a.K);       // [K] their colour indices
+    uint16_t* s_l1 = s_k0 + a.K;                                   // [64][kN16L1Words] positions in s_c0
+    __shared__ float s_red[kN16Threads / 64];
+    __shared__ int s_n0;
+    const int p = blockIdx.y, c0 = blockIdx.x, tid = threadIdx.x, K = a.K;
+    const int lane = tid & 63, wv = tid >> 6;
+    if (c0 == 0) {  // for the assign and cost kernels that follow
+        const int wpp = 8 * a.nch;
+        for (int i = tid; i < wpp * kUsedSlots; i += kN16Threads)
+            a.used_glob[(i / wpp) * a.used_stride + p * wpp + i % wpp] = 0u;
+        if (tid < 4 * kAccSlots) a.acc_zero[((int64_t)(tid >> 2) * a.P_acc + p) * 4 + (tid & 3)] = 0ull;
+    }
+    bool exh = false;
+    for (int j = 0; j < a.nch; ++j) exh |= a.pflags[p * a.nch + j] != 0;
+    const float4* pal = a.pal + (int64_t)p * a.kpal;
+    if (tid == 0) s_n0 = 0;
+    // level 0
+    const float lo0[3] = {(float)(c0 >> 4) * 0.25f, (float)((c0 >> 2) & 3) * 0.25f, (float)(c0 & 3) * 0.25f};
+    constexpr int U = 4096 / kN16Threads;
+    float4 cv[U];
+    float m = INFINITY;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int i = tid + kN16Threads * u;
+        cv[u] = pal[min(i, K - 1)];
+        if (i < K) m = fminf(m, box_max2(cv[u], lo0, 0.25f));
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fminf(m, __shfl_xor(m, off, 64));
+    if (lane == 0) s_red[wv] = m;
+    __syncthreads();
+    float t0 = s_red[0];
+#pragma unroll
+    for (int w = 1; w < kN16Threads / 64; ++w) t0 = fminf(t0, s_red[w]);
+    const float thr0 = t0 * HQ_CAND_MARGIN;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int i = tid + kN16Threads * u;
+        const bool cand = i < K && box_min2(cv[u], lo0, 0.25f) <= thr0;
+        const uint64_t bal = __ballot(cand);
+        int base = 0;
+        if (lane == 0 && bal) base = atomicAdd(&s_n0, __popcll(bal));
+        base = __shfl(base, 0, 64);
+        if (cand) {
+            const int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
+            s_c0[pos] = cv[u];
+            s_k0[pos] = (uint16_t)i;
+        }
+    }
+    __syncthreads();
+    const int n0 = s_n0;
+    // level 1: wave wv takes cells 4 wv .. 4 wv + 3, its lanes the level-0
+    // candidates (one LDS read per colour serves the 4 cells); lists in
+    // ascending position order by ballot
+    const float w1 = 1.0f / kN16G1;
+    {
+        float lo1[4][3], t1[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int ch = 4 * wv + c;
+            lo1[c][0] = (float)(4 * (c0 >> 4) + (ch >> 4)) * w1;
+            lo1[c][1] = (float)(4 * ((c0 >> 2) & 3) + ((ch >> 2) & 3)) * w1;
+            lo1[c][2] = (float)(4 * (c0 & 3) + (ch & 3)) * w1;
+            t1[c] = INFINITY;
+        }
+        for (int i = lane; i < n0; i += 64) {
+            const float4 cv = s_c0[i];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) t1[c] = fminf(t1[c], box_max2(cv, lo1[c], w1));
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) t1[c] = fminf(t1[c], __shfl_xor(t1[c], off, 64));
+            t1[c] *= HQ_CAND_MARGIN;
+        }
+        int cnt[4] = {0, 0, 0, 0};
+        const uint64_t below = (1ull << lane) - 1ull;
+        if (!exh) {
+            for (int i0 = 0; i0 < n0; i0 += 64) {
+                const int i = i0 + lane;
+                const float4 cv = s_c0[min(i, n0 - 1)];
+                const uint16_t kk = s_k0[min(i, n0 - 1)];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const bool cand = i < n0 && box_min2(cv, lo1[c], w1) <= t1[c];
+                    const uint64_t bal = __ballot(cand);
+                    const int pos = cnt[c] + __popcll(bal & below);
+                    if (cand && pos < kN16L1Cap) {
+                        const int ch = 4 * wv + c;
+                        const int I = 4 * (c0 >> 4) + (ch >> 4), J = 4 * ((c0 >> 2) & 3) + ((ch >> 2) & 3),
+                                  L = 4 * (c0 & 3) + (ch & 3);
+                        s_l1[ch * kN16L1Words + 1 + pos] = (uint16_t)i;
+                        a.lvl1[((int64_t)p * (kN16G1 * kN16G1 * kN16G1) + (I * kN16G1 + J) * kN16G1 + L) * kN16L1Words +
+                               1 + pos] = kk;
+                    }
+                    cnt[c] += __popcll(bal);
+                }
+            }
+        }
+        if (lane < 4) {
+            int total = cnt[0];
+#pragma unroll
+            for (int c = 1; c < 4; ++c) total = lane == c ? cnt[c] : total;
+            const int ch = 4 * wv + lane;
+            const int I = 4 * (c0 >> 4) + (ch >> 4), J = 4 * ((c0 >> 2) & 3) + ((ch >> 2) & 3), L = 4 * (c0 & 3) + (ch & 3);
+            const uint16_t h = exh || total > kN16L1Cap ? kN16Ovf : (uint16_t)total;
+            s_l1[ch * kN16L1Words] = h;
+            a.lvl1[((int64_t)p * (kN16G1 * kN16G1 * kN16G1) + (I * kN16G1 + J) * kN16G1 + L) * kN16L1Words] = h;
+        }
+    }
+    __syncthreads();
+    // level 2: wave wv takes parents wv + 16 j, its lane the child; the parent's
+    // list in registers (positions lane and lane + 64), each colour broadcast to
+    // the wave by readlane (no LDS in the loops)
+    const float w2 = 1.0f / kN16G2;
+    auto rl = [](float x, int i) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), i)); };
+    for (int j = 0; j < 4; ++j) {
+        const int ch = wv + 16 * j, sub = lane;
+        const int I2 = 16 * (c0 >> 4) + 4 * (ch >> 4) + (sub >> 4);
+        const int J2 = 16 * ((c0 >> 2) & 3) + 4 * ((ch >> 2) & 3) + ((sub >> 2) & 3);
+        const int L2 = 16 * (c0 & 3) + 4 * (ch & 3) + (sub & 3);
+        const float lo2[3] = {(float)I2 * w2, (float)J2 * w2, (float)L2 * w2};
+        uint16_t* out = a.lvl2 + ((int64_t)p * (kN16G2 * kN16G2 * kN16G2) + (I2 * kN16G2 + J2) * kN16G2 + L2) * kN16L2Words;
+        if (exh) {
+            out[0] = kN16Ovf;
+            continue;
+        }
+        const uint16_t* sl = s_l1 + ch * kN16L1Words;
+        const int c1 = __builtin_amdgcn_readfirstlane((int)sl[0]);
+        int cnt = 0;
+        if (c1 != kN16Ovf) {
+            const int pa = lane < c1 ? sl[1 + lane] : 0, pb = lane + 64 < c1 ? sl[65 + lane] : 0;
+            const float4 ca = s_c0[pa], cb = s_c0[pb];
+            const float ka = (float)s_k0[pa], kb = (float)s_k0[pb];  // (exact: < 2^24)
+            const int na = min(c1, 64);
+            float t2 = INFINITY;
+            for (int i = 0; i < na; ++i) t2 = fminf(t2, box_max2(make_float4(rl(ca.x, i), rl(ca.y, i), rl(ca.z, i), 0.f), lo2, w2));
+            for (int i = 64; i < c1; ++i)
+                t2 = fminf(t2, box_max2(make_float4(rl(cb.x, i - 64), rl(cb.y, i - 64), rl(cb.z, i - 64), 0.f), lo2, w2));
+            const float thr2 = t2 * HQ_CAND_MARGIN;
+            for (int i = 0; i < na; ++i)
+                if (box_min2(make_float4(rl(ca.x, i), rl(ca.y, i), rl(ca.z, i), 0.f), lo2, w2) <= thr2) {
+                    if (cnt < kN16L2Cap) out[1 + cnt] = (uint16_t)rl(ka, i);
+                    ++cnt;
+                }
+            for (int i = 64; i < c1; ++i)
+                if (box_min2(make_float4(rl(cb.x, i - 64), rl(cb.y, i - 64), rl(cb.z, i - 64), 0.f), lo2, w2) <= thr2) {
+                    if (cnt < kN16L2Cap) out[1 + cnt] = (uint16_t)rl(kb, i - 64);
+                    ++cnt;
+                }
+        } else {  // the parent list overflowed: every level-0 candidate (broadcast LDS reads)
+            float t2 = INFINITY;
+            for (int i = 0; i < n0; ++i) t2 = fminf(t2, box_max2(s_c0[i], lo2, w2));
+            const float thr2 = t2 * HQ_CAND_MARGIN;
+            for (int i = 0; i < n0; ++i)
+                if (box_min2(s_c0[i], lo2, w2) <= thr2) {
+                    if (cnt < kN16L2Cap) out[1 + cnt] = s_k0[i];
+                    ++cnt;
+                }
+        }
+        out[0] = cnt > kN16L2Cap ? kN16Ovf : (uint16_t)cnt;
+    }
+}
+
+// Dynamic LDS beyond the default 64 KiB for a kernel (raised once; 160 KiB per CU).
+static void allow_lds16(const void* fn, size_t bytes) {
+    static std::mutex mu;
+    static std::unordered_map<const void*, size_t> raised;
+    std::lock_guard<std::mutex> lk(mu);
+    size_t& r = raised[fn];
+    if (bytes > r) {
+        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        r = bytes;
+    }
+}
+
+hipError_t launch_lists16_grid(const Lists16Args& a, int P, hipStream_t s) {
+    const size_t lds = (sizeof(float4) + sizeof(uint16_t)) * (size_t)a.K + sizeof(uint16_t) * 64 * kN16L1Words;
+    allow_lds16(reinterpret_cast<const void*>(lists16_kernel), lds);
+    HQ_LAUNCH(lists16_kernel, dim3(64, (unsigned)P), dim3(kN16Threads), lds, s, a);
+    return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------
+// assign16: grid (nblocks * P), block 1024 (16 waves share the 64 KiB table:
+// 256-thread workgroups left one wave per SIMD), XCD-relabelled
+// palette-major; the palette in LDS.  A thread's pixels are a grid stride, resolved in batches of
+// kA16B: every RGB load of the batch, then every level-2 entry, then the walks.
+// ----------------------------------------------------------------------------
+constexpr int kA16B = 4;
+#define HQ_ANY16(c) (__builtin_amdgcn_ballot_w64(c) != 0)
+// level-2 cell (64^3) of a pixel in the unit cube; its level-1 cell (16^3) is
+// each coordinate >> 2 (floor(64 x) / 4 = floor(16 x): exact scalings)
+__device__ __forceinline__ uint32_t quad_cell16(float r, float g, float b) {
+    const int i = min((int)(r * (float)kN16G2), kN16G2 - 1), j = min((int)(g * (float)kN16G2), kN16G2 - 1),
+              k = min((int)(b * (float)kN16G2), kN16G2 - 1);
+    return (uint32_t)((i * kN16G2 + j) * kN16G2 + k);
+}
+
+// The reference loop (CL:179-192) for the lanes of a wave in mask s, the whole
+// wave on one lane's pixel at a time (as argmin_fix, hq_assign.hip): over its
+// level-1 list when it has one, else all K; least (distance, index), a NaN
+// distance never winning unless colour 0's is NaN.
+__device__ __noinline__ int argmin16_fix(float r, float g, float b, bool s, int cur, const uint16_t* l1,
+                                         const float4* s_pal, int K) {
+    uint64_t sm = __ballot(s);
+    const int lane = (int)__lane_id();
+    int result = cur;
+    while (sm) {
+        const int Ln = __builtin_ctzll(sm);
+        sm &= sm - 1;
+        const float pr = __shfl(r, Ln, 64), pg = __shfl(g, Ln, 64), pb = __shfl(b, Ln, 64);
+        const uint64_t lp = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uint64_t)l1 >> 32), Ln, 64) << 32) |
+                            (uint32_t)__shfl((int)(uint32_t)(uint64_t)l1, Ln, 64);
+        const uint16_t* list = reinterpret_cast<const uint16_t*>(lp);
+        const int n = list ? (int)list[0] : K;
+        float bd = INFINITY;
+        uint32_t bkey = 0xffffffffu;
+        for (int j = lane; j < n; j += 64) {
+            const int k = list ? (int)list[1 + j] : j;
+            const float d = sqrtf(dist2(pr, pg, pb, s_pal[k]));
+            const bool nan = d != d;
+            const float dv = nan ? INFINITY : d;
+            const uint32_t key = (nan ? 0x10000u : 0u) | (uint32_t)k;
+            if (dv < bd || (dv == bd && key < bkey)) {
+                bd = dv;
+                bkey = key;
+            }
+        }
+#pragma unroll
+        for (int m = 1; m < 64; m <<= 1) {
+            const float od = __shfl_xor(bd, m, 64);
+            const uint32_t ok = (uint32_t)__shfl_xor((int)bkey, m, 64);
+            if (od < bd || (od == bd && ok < bkey)) {
+                bd = od;
+                bkey = ok;
+            }
+        }
+        const int bk = (int)(bkey & 0xffffu);
+        const float d0 = sqrtf(dist2(pr, pg, pb, s_pal[0]));
+        if (lane == Ln) result = d0 != d0 ? 0 : bk;
+    }
+    return result;
+}
+
+__device__ __forceinline__ uint32_t u16_at(const uint4& a, const uint4& b, int j) {  // u16 j of the entry
+    const uint32_t w = j < 2 ? a.x : j < 4 ? a.y : j < 6 ? a.z : j < 8 ? a.w : j < 10 ? b.x : j < 12 ? b.y
+                                                                              : j < 14 ? b.z : b.w;
+    return (j & 1) ? w >> 16 : w & 0xffffu;
+}
+
+template <bool U8>
+__global__ __launch_bounds__(kN16Threads) void assign16_kernel(AssignArgs a, int P) {
+    extern __shared__ float4 s_pal[];  // [K]
+    const int w = xcd_remap(blockIdx.x, a.nblocks * P);
+    const int p = w / a.nblocks, blk = w % a.nblocks, tid = threadIdx.x, K = a.K;
+    const float4* pal = a.pal + (int64_t)p * a.kpal;
+    for (int i = tid; i < K; i += kN16Threads) s_pal[i] = pal[i];
+    bool exh = false;
+    for (int j = 0; j < a.nch; ++j) exh |= a.pflags[p * a.nch + j] != 0;
+    __syncthreads();
+    const uint4* l2 = reinterpret_cast<const uint4*>(a.l2n + (int64_t)p * (kN16G2 * kN16G2 * kN16G2) * kN16L2Words);
+    const uint16_t* l1 = a.l1n + (int64_t)p * (kN16G1 * kN16G1 * kN16G1) * kN16L1Words;
+    uint16_t* idx = a.idx16 + (int64_t)p * a.idx_pitch;
+    const uint32_t n_ext = (uint32_t)a.n_ext, qlast = n_ext - 1;
+    const uint32_t cstride = (uint32_t)a.nblocks * (uint32_t)kN16Threads;
+    const uint32_t qbase = (uint32_t)blk * (uint32_t)kN16Threads + (uint32_t)tid;
+    // every lane runs its lane 0's batch count (argmin16_fix needs the whole wave)
+    const int npx0 = qbase < n_ext ? (int)((n_ext - 1 - qbase) / cstride) + 1 : 0;
+    const int nb = __builtin_amdgcn_readfirstlane((npx0 + kA16B - 1) / kA16B);
+    for (int bi = 0; bi < nb; ++bi) {
+        float r[kA16B], g[kA16B], b[kA16B];
+        uint32_t q[kA16B];
+#pragma unroll
+        for (int u = 0; u < kA16B; ++u) {
+            q[u] = qbase + (uint32_t)(bi * kA16B + u) * cstride;
+            const uint32_t qc = min(q[u], qlast);
+            if constexpr (U8) {
+                const uint32_t v = a.rgbx[qc];
+                r[u] = u8_unit(v, 0);
+                g[u] = u8_unit(v, 1);
+                b[u] = u8_unit(v, 2);
+            } else {
+                r[u] = a.R[qc];
+                g[u] = a.G[qc];
+                b[u] = a.B[qc];
+            }
+        }
+        bool in_[kA16B];
+        uint4 e0[kA16B], e1[kA16B];
+#pragma unroll
+        for (int u = 0; u < kA16B; ++u) {
+            in_[u] = r[u] >= 0.f && r[u] <= 1.f && g[u] >= 0.f && g[u] <= 1.f && b[u] >= 0.f && b[u] <= 1.f;
+            const uint32_t cell = in_[u] ? (uint32_t)quad_cell16(r[u], g[u], b[u]) : 0u;
+            e0[u] = l2[2 * cell];
+            e1[u] = l2[2 * cell + 1];
+        }
+#pragma unroll
+        for (int u = 0; u < kA16B; ++u) {
+            const uint32_t c = e0[u].x & 0xffffu;
+            const bool slow = !in_[u] || exh || c == kN16Ovf || c == 0u;
+            const int cnt = slow ? 0 : (int)c;
+            // ranked by d^2 (dist2_rank: within 3 ulp of dist2); a runner-up within
+            // 1e-6 relative is a possible sqrtf tie: re-resolved over the list below
+            float best2 = INFINITY, second2 = INFINITY;
+            int bk = 0;
+#pragma unroll
+            for (int i = 0; i < kN16L2Cap; ++i) {
+                if (!HQ_ANY16(i < cnt)) break;
+                const int k = (int)u16_at(e0[u], e1[u], i + 1);
+                const float d2 = i < cnt ? dist2_rank(r[u], g[u], b[u], s_pal[i < cnt ? k : 0]) : INFINITY;
+                const bool lt = d2 < best2;
+                second2 = __builtin_amdgcn_fmed3f(best2, second2, d2);
+                bk = lt ? k : bk;
+                best2 = lt ? d2 : best2;
+            }
+            const bool near = !slow && second2 <= best2 * (1.0f + 1e-6f);
+            if (HQ_ANY16(near)) {
+                if (near) {  // the reference distance over the list: least (sqrtf(d^2), index)
+                    float bd = INFINITY;
+                    int bkk = 0x7fffffff;
+                    for (int i = 0; i < cnt; ++i) {
+                        const int k = (int)u16_at(e0[u], e1[u], i + 1);
+                        const float d = sqrtf(dist2(r[u], g[u], b[u], s_pal[k]));
+                        if (d < bd || (d == bd && k < bkk)) {
+                            bd = d;
+                            bkk = k;
+                        }
+                    }
+                    bk = bkk;
+                }
+            }
+            if (HQ_ANY16(slow)) {
+                // the level-1 list of the pixel's cell when it has one
+                const uint16_t* lst = nullptr;
+                if (in_[u] && !exh) {
+                    const int i1 = min((int)(r[u] * (float)kN16G1), kN16G1 - 1);
+                    const int j1 = min((int)(g[u] * (float)kN16G1), kN16G1 - 1);
+                    const int k1 = min((int)(b[u] * (float)kN16G1), kN16G1 - 1);
+                    const uint16_t* e = l1 + (int64_t)((i1 * kN16G1 + j1) * kN16G1 + k1) * kN16L1Words;
+                    if (e[0] != kN16Ovf) lst = e;
+                }
+                bk = argmin16_fix(r[u], g[u], b[u], slow, bk, lst, s_pal, K);
+            }
+            if (q[u] < n_ext) __builtin_nontemporal_store((uint16_t)bk, idx + q[u]);
+        }
+    }
+}
+
+void launch_used_idx16(const AssignArgs& a, int P, hipStream_t s);  // (hq_assign.hip)
+
+// assign16 then the used bits from the final indices; the profiling events
+// bracket both.
+hipError_t launch_assign16(const AssignArgs& a0, int P, hipStream_t s) {
+    const hipEvent_t ev0 = t_ev_start, ev1 = t_ev_stop;
+    AssignArgs a = a0;
+    t_ev_stop = nullptr;
+    const size_t lds = sizeof(float4) * (size_t)a.K;
+    allow_lds16(reinterpret_cast<const void*>(assign16_kernel<true>), lds);
+    allow_lds16(reinterpret_cast<const void*>(assign16_kernel<false>), lds);
+    const dim3 grid((unsigned)(a.nblocks * P));
+    if (a.rgbx) HQ_LAUNCH(assign16_kernel<true>, grid, dim3(kN16Threads), lds, s, a, P);
+    else HQ_LAUNCH(assign16_kernel<false>, grid, dim3(kN16Threads), lds, s, a, P);
+    t_ev_start = nullptr;
+    t_ev_stop = ev1;
+    launch_used_idx16(a, P, s);
+    t_ev_start = ev0;
+    return hipGetLastError();
+}
+
+template __global__ void assign16_kernel<true>(AssignArgs, int);
+template __global__ void assign16_kernel<false>(AssignArgs, int);
+
+}  // namespace hq

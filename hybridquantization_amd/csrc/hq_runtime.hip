@@ -31,6 +31,8 @@ hipError_t launch_sa_step(const SaArgs&, hipStream_t);
 void set_launch_events(hipEvent_t start, hipEvent_t stop);
 hipError_t launch_build_grid(const GridArgs&, int P, hipStream_t);
 hipError_t launch_assign(const AssignArgs&, int P, hipStream_t);
+hipError_t launch_lists16_grid(const Lists16Args&, int P, hipStream_t);
+hipError_t launch_assign16(const AssignArgs&, int P, hipStream_t);
 int assign_residency(int NG);
 int assign_residency_chunked();
 hipError_t launch_cost_chunked(const CostArgs&, int P, int nch, int de, bool trim, hipStream_t);
@@ -145,6 +147,7 @@ struct hq_ctx {
     DevBuf d_pixerr;           // option "pixel_err": [P][n_own] per-pixel dE of the last evaluation
     DevBuf d_idx32, d_used32;  // K > 16384 (hq_wide.hip): 32-bit index images, per-colour used flags
     DevBuf d_idx16, d_dist;    // 256 < K <= 16384 (chunked): 16-bit index images, pass distances
+    DevBuf d_l1n, d_l2n;       // the native 16-bit candidate lists (hq_lists16.hip)
     int nch_cur = 1;           // chunks per palette of the population being enqueued (1: K <= 256)
     int last_nch = 1;          // ... of the last evaluation (its index image: u16 when > 1)
     float* h_pal = nullptr;   // pinned [P][K][4]
@@ -174,6 +177,7 @@ struct hq_ctx {
                            // "palette_split"; SURVEY 8e's split of large populations)
     int slice_ranks = 1, slice_rank = 0;  // test only: the same slice without a communicator
     int slice_lo = 0, slice_n = 0;        // the last evaluation's palettes held on this device
+    int lists16 = 1;       // native 16-bit candidate lists: 1 = chunked palettes of 8 or 16 chunks, 2 = 2 .. 16
     int chunked = 1;       // 256 < K <= 16384: palettes as 256-colour chunks through the grid and
                            // tiled kernels (option "chunked"; 0 = the exhaustive K > 256 path)
     int img_u8_path = 1;   // assign reads the packed 8-bit image when there is one (option 'img_u8')
@@ -423,12 +427,22 @@ int assign_blocks(const hq_ctx* c, int P) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(nblocks, (c->g.n_ext + chunk - 1) / chunk));
 }
 
+// Chunked palettes of 8 or 16 chunks take the native 16-bit lists (option lists16).
+bool use_lists16(const hq_ctx* c) {
+    const int min_nch = c->lists16 >= 2 ? 2 : kN16MinNch;  // (2: also 2 and 4 chunks)
+    return c->lists16 > 0 && c->G2 > 0 && c->nch_cur >= min_nch && c->nch_cur <= kMaxNchFast;
+}
+
 // Ensure population buffers for P palettes of K colours.
 int ensure_population(hq_ctx* c, int P, int K) {
     const Geom& g = c->g;
     if (c->nch_cur > 1) {  // chunked palettes: 16-bit indices, then P nch sub-palettes of 256
         HIP_TRY(c, c->d_idx16.ensure(sizeof(uint16_t) * (size_t)P * g.idx_pitch + 256));
         if (c->nch_cur > 4) HIP_TRY(c, c->d_dist.ensure(sizeof(float) * (size_t)P * g.idx_pitch));
+        if (use_lists16(c)) {
+            HIP_TRY(c, c->d_l1n.ensure(sizeof(uint16_t) * kN16L1Words * (size_t)P * kN16G1 * kN16G1 * kN16G1));
+            HIP_TRY(c, c->d_l2n.ensure(sizeof(uint16_t) * kN16L2Words * (size_t)P * kN16G2 * kN16G2 * kN16G2));
+        }
         P *= c->nch_cur;  // (d_out, h_out: P nch (1 + 256) >= P (1 + K) doubles)
         K = kMaxK;
     }
@@ -656,9 +670,14 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
         if (ev) set_launch_events(ev[2 * slot], ev[2 * slot + 1]);
     };
     auto untimed = [&]() { set_launch_events(nullptr, nullptr); };
+    const bool n16 = use_lists16(c);
     if (c->G2 > 0) {  // (build_grid also zeroes the used bits and the sums)
         timed(0);
-        const hipError_t e = launch_build_grid(ga, Ps, s);
+        const hipError_t e =
+            n16 ? launch_lists16_grid(Lists16Args{ga.pal, ga.pflags, c->d_l1n.as<uint16_t>(), c->d_l2n.as<uint16_t>(),
+                                                  ga.used_glob, used_stride(Ps), ga.acc_zero, Pl, K, nch * kMaxK, nch},
+                                      Pl, s)
+                : launch_build_grid(ga, Ps, s);
         untimed();
         HIP_TRY(c, e);
     } else {
@@ -676,6 +695,15 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
         aa.dist = nch > 4 ? c->d_dist.as<float>() : nullptr;
         aa.nch = nch;
         while ((1 << aa.lg_nch) < nch) ++aa.lg_nch;
+    }
+    if (n16) {  // one palette of K colours per workgroup (its table in LDS)
+        aa.l1n = c->d_l1n.as<uint16_t>();
+        aa.l2n = c->d_l2n.as<uint16_t>();
+        aa.kpal = nch * kMaxK;
+        aa.K = K;
+        // one resident round of 1024-thread workgroups over the P palettes, >= 4 pixels per thread
+        aa.nblocks = (int)std::max<int64_t>(
+            1, std::min<int64_t>(std::max(1, c->num_cu / Pl), (g.n_ext + 4095) / 4096));
     }
     const float inv[3] = {1.0f / c->illum[0], 1.0f / c->illum[1], 1.0f / c->illum[2]};
     // chunked palettes: the 16 x 128 tiles at HB = 10 (else the generic path)
@@ -706,7 +734,7 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
         ca.pix_pitch = (int64_t)g.W * (g.r1 - g.r0);
     }
     timed(1);
-    hipError_t e = launch_assign(aa, Ps, s);
+    hipError_t e = n16 ? launch_assign16(aa, Pl, s) : launch_assign(aa, Ps, s);
     untimed();
     HIP_TRY(c, e);
     if (fast) {
@@ -1123,7 +1151,7 @@ void hq_destroy(hq_ctx* c) {
                       &c->d_labL, &c->d_labA, &c->d_labB, &c->d_pal_in, &c->d_pal, &c->d_opp, &c->d_opp16,
                       &c->d_dup, &c->d_pflags, &c->d_lvl1, &c->d_lvl2, &c->d_idx,
                       &c->d_used_mask, &c->d_acc, &c->d_out, &c->d_gen_t, &c->d_taps,
-                      &c->d_vfrag16, &c->d_vfrag16p, &c->d_vfragm, &c->d_htaps, &c->d_idx32, &c->d_used32, &c->d_pixerr, &c->d_idx16, &c->d_dist})
+                      &c->d_vfrag16, &c->d_vfrag16p, &c->d_vfragm, &c->d_htaps, &c->d_idx32, &c->d_used32, &c->d_pixerr, &c->d_idx16, &c->d_dist, &c->d_l1n, &c->d_l2n})
         b->release();
     if (c->h_pal) (void)hipHostFree(c->h_pal);
     if (c->h_out) (void)hipHostFree(c->h_out);
@@ -1652,6 +1680,9 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
         // (checked against slice_ranks again at each evaluation: the options may come in either order)
         if (value < 0) return fail(c, HQ_ERR_ARG, "slice_rank must be >= 0");
         c->slice_rank = value;
+    } else if (!std::strcmp(name, "lists16")) {
+        if (value < 0 || value > 2) return fail(c, HQ_ERR_ARG, "lists16: 0, 1 or 2");
+        c->lists16 = (int)value;
     } else if (!std::strcmp(name, "chunked")) {
         c->chunked = value != 0;
     } else if (!std::strcmp(name, "pixel_err")) {

@@ -479,25 +479,7 @@ __global__ __launch_bounds__(1024) void sa_step_kernel(SaArgs a) {
 // the child's T is attained inside it, so level 2 needs only the parent list.
 // Entries: byte0 = count (255 = overflow), then ascending indices.
 // ----------------------------------------------------------------------------
-// Box bounds in fp32.  Box edges are multiples of 1/G (G a power of two):
-// exact.  Valid colours are finite (prep_palette routes non-finite palettes to
-// the exhaustive path), so every term is a correctly rounded difference,
-// squared and summed with non-negative terms: each bound is within 3 ulp
-// (2e-7 relative) of its exact value, and the 1e-5 margin covers that on
-// both sides of the test on top of the reference's own 1.1e-6.  An fp32
-// overflow (|colour| > 1e19) gives inf bounds: T = inf makes every colour a
-// candidate, which overflows the list into the exhaustive loop.  (fp64 was
-// ~570 VALU instructions per wave at half the fp32 rate.)
-__device__ __forceinline__ float ax_min2(float c, float lo, float hi) {
-    const float d = fmaxf(fmaxf(lo - c, c - hi), 0.f);
-    return d * d;
-}
-__device__ __forceinline__ float ax_max2(float c, float lo, float hi) {
-    const float d = fmaxf(c - lo, hi - c);
-    return d * d;
-}
-
-#define HQ_CAND_MARGIN (1.0f + 1e-5f)
+// (box bounds ax_min2 / ax_max2 and HQ_CAND_MARGIN: hq_device.h)
 
 // Level-2 entries are interleaved by groups of 4 palettes: the 4 entries of one
 // cell sit side by side (32 B at 8 B per entry), so a pixel evaluated under the

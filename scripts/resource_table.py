@@ -7,7 +7,7 @@ import re
 import subprocess
 import sys
 
-SRC = ["hq_search.hip", "hq_assign.hip", "hq_cost.hip", "hq_setup.hip", "hq_wide.hip"]
+SRC = ["hq_search.hip", "hq_assign.hip", "hq_cost.hip", "hq_setup.hip", "hq_wide.hip", "hq_lists16.hip"]
 CSRC = "hybridquantization_amd/csrc"
 
 
