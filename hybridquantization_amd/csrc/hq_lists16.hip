@@ -186,18 +186,32 @@ __global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
             const float4 ca = s_c0[pa], cb = s_c0[pb];
             const float ka = (float)s_k0[pa], kb = (float)s_k0[pb];  // (exact: < 2^24)
             const int na = min(c1, 64);
+            // centre form of the bounds (3 VALU per axis): per axis |c - m| + h
+            // and max(|c - m| - h, 0), m the box centre (exact), h = 1/128.  Each
+            // is within 2 ulp of the exact term at the terms' sizes here, which
+            // the 1e-5 margin covers with T >= 3 h^2 (a colour at the centre)
+            const float h2 = 0.5f * w2;
+            const float m0 = lo2[0] + h2, m1 = lo2[1] + h2, m2 = lo2[2] + h2;
+            auto bmax = [&](float x, float y, float z) {
+                const float tx = fabsf(x - m0) + h2, ty = fabsf(y - m1) + h2, tz = fabsf(z - m2) + h2;
+                return fmaf(tz, tz, fmaf(ty, ty, tx * tx));
+            };
+            auto bmin = [&](float x, float y, float z) {
+                const float tx = fmaxf(fabsf(x - m0) - h2, 0.f), ty = fmaxf(fabsf(y - m1) - h2, 0.f),
+                            tz = fmaxf(fabsf(z - m2) - h2, 0.f);
+                return fmaf(tz, tz, fmaf(ty, ty, tx * tx));
+            };
             float t2 = INFINITY;
-            for (int i = 0; i < na; ++i) t2 = fminf(t2, box_max2(make_float4(rl(ca.x, i), rl(ca.y, i), rl(ca.z, i), 0.f), lo2, w2));
-            for (int i = 64; i < c1; ++i)
-                t2 = fminf(t2, box_max2(make_float4(rl(cb.x, i - 64), rl(cb.y, i - 64), rl(cb.z, i - 64), 0.f), lo2, w2));
+            for (int i = 0; i < na; ++i) t2 = fminf(t2, bmax(rl(ca.x, i), rl(ca.y, i), rl(ca.z, i)));
+            for (int i = 64; i < c1; ++i) t2 = fminf(t2, bmax(rl(cb.x, i - 64), rl(cb.y, i - 64), rl(cb.z, i - 64)));
             const float thr2 = t2 * HQ_CAND_MARGIN;
             for (int i = 0; i < na; ++i)
-                if (box_min2(make_float4(rl(ca.x, i), rl(ca.y, i), rl(ca.z, i), 0.f), lo2, w2) <= thr2) {
+                if (bmin(rl(ca.x, i), rl(ca.y, i), rl(ca.z, i)) <= thr2) {
                     if (cnt < kN16L2Cap) out[1 + cnt] = (uint16_t)rl(ka, i);
                     ++cnt;
                 }
             for (int i = 64; i < c1; ++i)
-                if (box_min2(make_float4(rl(cb.x, i - 64), rl(cb.y, i - 64), rl(cb.z, i - 64), 0.f), lo2, w2) <= thr2) {
+                if (bmin(rl(cb.x, i - 64), rl(cb.y, i - 64), rl(cb.z, i - 64)) <= thr2) {
                     if (cnt < kN16L2Cap) out[1 + cnt] = (uint16_t)rl(kb, i - 64);
                     ++cnt;
                 }
@@ -321,22 +335,38 @@ __global__ __launch_bounds__(kN16Threads) void assign16_kernel(AssignArgs a, int
     // every lane runs its lane 0's batch count (argmin16_fix needs the whole wave)
     const int npx0 = qbase < n_ext ? (int)((n_ext - 1 - qbase) / cstride) + 1 : 0;
     const int nb = __builtin_amdgcn_readfirstlane((npx0 + kA16B - 1) / kA16B);
+    // the next batch's pixels are loaded while this batch's entries are looked
+    // up and walked: one exposed memory round trip per batch, not two
+    uint32_t nv[kA16B];          // packed bytes (U8)
+    float nr[kA16B], ng[kA16B], nbl[kA16B];  // planar floats
+    auto load_batch = [&](int bi) {
+#pragma unroll
+        for (int u = 0; u < kA16B; ++u) {
+            const uint32_t qc = min(qbase + (uint32_t)(bi * kA16B + u) * cstride, qlast);
+            if constexpr (U8) {
+                nv[u] = a.rgbx[qc];
+            } else {
+                nr[u] = a.R[qc];
+                ng[u] = a.G[qc];
+                nbl[u] = a.B[qc];
+            }
+        }
+    };
+    if (nb > 0) load_batch(0);
     for (int bi = 0; bi < nb; ++bi) {
         float r[kA16B], g[kA16B], b[kA16B];
         uint32_t q[kA16B];
 #pragma unroll
         for (int u = 0; u < kA16B; ++u) {
             q[u] = qbase + (uint32_t)(bi * kA16B + u) * cstride;
-            const uint32_t qc = min(q[u], qlast);
             if constexpr (U8) {
-                const uint32_t v = a.rgbx[qc];
-                r[u] = u8_unit(v, 0);
-                g[u] = u8_unit(v, 1);
-                b[u] = u8_unit(v, 2);
+                r[u] = u8_unit(nv[u], 0);
+                g[u] = u8_unit(nv[u], 1);
+                b[u] = u8_unit(nv[u], 2);
             } else {
-                r[u] = a.R[qc];
-                g[u] = a.G[qc];
-                b[u] = a.B[qc];
+                r[u] = nr[u];
+                g[u] = ng[u];
+                b[u] = nbl[u];
             }
         }
         bool in_[kA16B];
@@ -348,6 +378,7 @@ __global__ __launch_bounds__(kN16Threads) void assign16_kernel(AssignArgs a, int
             e0[u] = l2[2 * cell];
             e1[u] = l2[2 * cell + 1];
         }
+        if (bi + 1 < nb) load_batch(bi + 1);
 #pragma unroll
         for (int u = 0; u < kA16B; ++u) {
             const uint32_t c = e0[u].x & 0xffffu;
