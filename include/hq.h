@@ -107,8 +107,10 @@ int hq_get_labref(hq_ctx *ctx, float *lab4);
 /* IM:620 computeQuantizationErrorPopulation for P palettes of K colours
  * (K in [1, 2^24] as the plugin allows, HQ:192).  K <= 256: the pruned grid
  * argmin and the tiled fast stencil.  256 < K <= 16384: chunked palettes (nch
- * sub-palettes of 256 through the same grid and assign, 16-bit indices; the fast
- * stencil up to K = 4096, the generic one above; option "chunked").  K > 16384,
+ * sub-palettes of 256, 16-bit indices; 1024 < K <= 4096: one grid of 16-bit
+ * candidate lists over all K colours, option "lists16", otherwise a grid and
+ * assign pass per chunk; the fast stencil up to K = 4096, the generic one
+ * above; option "chunked").  K > 16384,
  * palettes with non-finite colours or
  * outside the fast path's range, option "chunked" 0 or "grid" 0: the exhaustive
  * argmin with 32-bit indices and the generic stencil path.  All give the same
@@ -212,6 +214,9 @@ int hq_profile_reset(hq_ctx *ctx);
  *                  cores in split f16 (as the fast path's; default 1), 0 = fp32 FMAs (gen_vtile2)
  *   "gen_hmfma"    with gen_vmfma: the horizontal pass on the matrix cores too (default 1;
  *                  palettes in the fast range), 0 = fp32 FMAs (gen_hrow4)
+ *   "lists16"      chunked palettes: native 16-bit candidate lists (one grid over all K
+ *                  colours, one lookup per pixel): 1 (default) for 8 and 16 chunks, 2 for
+ *                  2 .. 16 chunks, 0 = a grid and assign pass per 256-colour chunk
  *   "gen_vtile2"   the LDS-tiled generic path's vertical pass (halfSize <= 64): 1 (default) =
  *                  32 x 64 tiles, windows double-buffered by LDS DMA; 0 = 64 x 64 tiles with
  *                  one window at a time (same results bit for bit)
