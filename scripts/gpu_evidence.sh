@@ -35,7 +35,8 @@ for cfg in "--size 1024 --K 64 --population 1" "--population 1" "" "--size 8192 
            "--population 64 --shard-of 8 --steps 20 --warmup 5 --no-full-search" \
            "--population 8 --steps 50 --warmup 5 --no-full-search" \
            "--size 1024 --K 1024 --steps 50 --warmup 5 --no-full-search" \
-           "--size 1024 --K 4096 --steps 20 --warmup 3 --no-full-search"; do
+           "--size 1024 --K 4096 --steps 20 --warmup 3 --no-full-search" \
+           "--size 1024 --K 8192 --steps 10 --warmup 2 --no-full-search"; do
   timeout -k 10 300 python bench.py --no-cpu-baseline $cfg >> $E/configs.jsonl 2>> $E/configs.err
   rc=$?; echo "config [$cfg] rc=$rc"; fatal $rc "config $cfg"
 done
