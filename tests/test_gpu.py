@@ -958,7 +958,7 @@ def test_device_search_with_single_rank_comm(gpu, filt, split):
 
 @pytest.mark.parametrize("K,P,ranks,opts", [(64, 8, 2, {}), (64, 8, 4, {}), (256, 12, 3, {}), (600, 4, 2, {}),
                                              (5000, 4, 2, {}), (600, 4, 2, {"chunked": 0}),
-                                             (300, 6, 3, {"grid": 0})])
+                                             (300, 6, 3, {"grid": 0}), (2048, 4, 2, {}), (600, 4, 2, {"lists16": 2})])
 def test_palette_slices_sum_to_full(gpu, filt, K, P, ranks, opts):
     """The palette split (option palette_split with a communicator):
     rank r evaluates palettes [r P/N, (r+1) P/N) of the whole image.  Here the
