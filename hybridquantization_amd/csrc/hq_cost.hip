@@ -1653,94 +1653,121 @@ __global__ __launch_bounds__(256) void gen_vmfma_kernel(GenArgs a, int tiles_x) 
 // t3 plane's horizontal taps, CL:254-267).  D's lane holds 4 adjacent output
 // columns of one row: one 16-B store of split dwords per plane, which is
 // gen_vmfma's input as it stands.  A workgroup: 16 rows x 128 columns (4 waves
-// x 2 blocks of 16); its segment the 3 channels' split opponent colours,
-// [3][16][pitch] dwords, pitch = 8 mod 64 (ds_read_b128's lane groups then hit
-// 64 distinct banks).
+// x 2 blocks of 16), kHmRpt such tiles down the image per workgroup; its
+// segment the 3 channels' split opponent colours, [3][16][pitch] dwords,
+// pitch = 8 mod 64 (ds_read_b128's lane groups then hit 64 distinct banks).
 constexpr int kHmCB = 2, kHmCols = 64 * kHmCB;
 static int hmfma_seg_cols(int H) { return kHmCols - 16 + 16 * ((16 + 2 * H + 15) / 16); }
 static int hmfma_pitch(int H) { return (hmfma_seg_cols(H) - 8 + 63) / 64 * 64 + 8; }
+#ifndef HQ_HM_RPT
+#define HQ_HM_RPT 4  // gen_hmfma: 16-row tiles per workgroup, the next one's colours loaded during this one's MFMAs
+#endif
+constexpr int kHmRpt = HQ_HM_RPT;
 template <typename IT>
-__global__ __launch_bounds__(256) void gen_hmfma_kernel(GenArgs a, int pitch) {
+__global__ __launch_bounds__(256, 2) void gen_hmfma_kernel(GenArgs a, int pitch) {  // (2 waves per SIMD: LDS allows 2 workgroups)
     extern __shared__ uint32_t s_hm[];  // [3][16][pitch] segment, then the taps [7][hi, lo][TP]
     const int tid = threadIdx.x, lane = tid & 63, n = lane & 15, g = lane >> 4;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int half = a.half, W = a.g.W, rows = a.g.e1 - a.g.e0;
     const int S = (16 + 2 * half + 15) / 16, TP = 16 * S + 16, SW = kHmCols - 16 + 16 * S;
-    const int x0 = blockIdx.x * kHmCols, y0 = blockIdx.y * 16;
+    const int x0 = blockIdx.x * kHmCols, yb = blockIdx.y * 16 * kHmRpt;
+    const int nt = min(kHmRpt, (rows - yb + 15) / 16);  // this workgroup's tiles
     uint32_t* s_tap = s_hm + 3 * 16 * pitch;
     for (int i = tid; i < kNumFilt * 2 * TP; i += 256) s_tap[i] = a.htapd[i];
-    // the segment, column tid of every row (SW <= 256 for half <= 64): all 16
-    // index loads, then the colours, then the split stores
-    if (tid < SW) {
-        const int x = reflect_clamp(x0 - half + tid, W);  // (columns past the row end: finite, masked)
-        const IT* col = static_cast<const IT*>(a.idx) + x;
+    // the segment of a tile: column tid of its 16 rows (SW <= 256 for half <= 64).
+    // Software pipeline over the tiles: tile t + 1's colours and tile t + 2's
+    // indices are in flight while tile t's MFMAs run (the fill's two dependent
+    // memory round trips were exposed once per 16 rows)
+    const bool act = tid < SW;
+    const IT* col = static_cast<const IT*>(a.idx) + reflect_clamp(x0 - half + tid, W);  // (past the row end: masked)
+    uint32_t ix[16];
+    float vx[16], vy[16], vz[16];  // (12 bytes each: the registers of two waves per SIMD)
+    auto load_ix = [&](int t) {
 #pragma unroll
-        for (int r0 = 0; r0 < 16; r0 += 8) {
-            uint32_t ix[8];
+        for (int u = 0; u < 16; ++u) ix[u] = act ? (uint32_t)col[(int64_t)min(yb + 16 * t + u, rows - 1) * W] : 0u;
+    };
+    auto gather = [&]() {
 #pragma unroll
-            for (int u = 0; u < 8; ++u) ix[u] = (uint32_t)col[(int64_t)min(y0 + r0 + u, rows - 1) * W];
-            float4 v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = a.opp[ix[u]];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                uint32_t* d = s_hm + (r0 + u) * pitch + tid;
-                d[0] = split_f16(v[u].x);
-                d[16 * pitch] = split_f16(v[u].y);
-                d[32 * pitch] = split_f16(v[u].z);
-            }
+        for (int u = 0; u < 16; ++u) {
+            const float* o = reinterpret_cast<const float*>(a.opp + ix[u]);
+            vx[u] = o[0];
+            vy[u] = o[1];
+            vz[u] = o[2];
         }
-    }
-    __syncthreads();
-    f32x4v D[kNumFilt][kHmCB];
-#pragma unroll
-    for (int f = 0; f < kNumFilt; ++f)
-#pragma unroll
-        for (int cb = 0; cb < kHmCB; ++cb) D[f][cb] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    };
+    load_ix(0);
+    gather();
+    if (nt > 1) load_ix(1);
     const uint32_t* sb = s_hm + n * pitch + 16 * kHmCB * wv + 4 * g;
     const uint32_t* th = s_tap + 4 * g - n + 15;  // (m = lane & 15 = n)
-    for (int st = 0; st < S; ++st) {
-        f16x8 B[3][kHmCB];
-#pragma unroll
-        for (int ch = 0; ch < 3; ++ch)
-#pragma unroll
-            for (int cb = 0; cb < kHmCB; ++cb)
-                B[ch][cb] = __builtin_bit_cast(f16x8, *reinterpret_cast<const u32x4*>(sb + ch * 16 * pitch + 16 * cb + 16 * st));
-#pragma unroll
-        for (int f = 0; f < kNumFilt; ++f) {
-            const int ch = f == 6 ? 0 : f % 3;  // planes t1.xyz, t2.xyz, t3 -> channels x y z x y z x
-            const uint32_t* tf = th + f * 2 * TP + 16 * st;
-            uint4 ah, al;
-            ah.x = tf[0]; ah.y = tf[1]; ah.z = tf[2]; ah.w = tf[3];
-            al.x = tf[TP]; al.y = tf[TP + 1]; al.z = tf[TP + 2]; al.w = tf[TP + 3];
-            const f16x8 AH = __builtin_bit_cast(f16x8, ah), AL = __builtin_bit_cast(f16x8, al);
-#pragma unroll
-            for (int cb = 0; cb < kHmCB; ++cb) D[f][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(AH, B[ch][cb], D[f][cb], 0, 0, 0);
-#pragma unroll
-            for (int cb = 0; cb < kHmCB; ++cb) D[f][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(AL, B[ch][cb], D[f][cb], 0, 0, 0);
-        }
-    }
-    // lane (n, g): plane row y0 + n, columns 4 g .. 4 g + 3 of each block, x 2^-30
-    const int y = y0 + n;
-    if (y >= rows) return;
-    uint32_t* t = reinterpret_cast<uint32_t*>(a.t);
+    uint32_t* tpl = reinterpret_cast<uint32_t*>(a.t);
     const int64_t np = a.g.n_ext;
+    for (int t = 0; t < nt; ++t) {
+        if (t) __syncthreads();  // tile t - 1's operand reads are done
+        if (act) {
 #pragma unroll
-    for (int cb = 0; cb < kHmCB; ++cb) {
-        const int x = x0 + 16 * (kHmCB * wv + cb) + 4 * g;
-        const int64_t q = (int64_t)y * W + x;
-        if ((W & 3) == 0 && x + 3 < W) {
+            for (int u = 0; u < 16; ++u) {
+                uint32_t* d = s_hm + u * pitch + tid;
+                d[0] = split_f16(vx[u]);
+                d[16 * pitch] = split_f16(vy[u]);
+                d[32 * pitch] = split_f16(vz[u]);
+            }
+        }
+        __syncthreads();
+        if (t + 1 < nt) {
+            gather();
+            if (t + 2 < nt) load_ix(t + 2);
+        }
+        f32x4v D[kNumFilt][kHmCB];
 #pragma unroll
-            for (int f = 0; f < kNumFilt; ++f)
-                *reinterpret_cast<uint4*>(t + f * np + q) =
-                    make_uint4(split_f16(D[f][cb][0] * kVOutScale), split_f16(D[f][cb][1] * kVOutScale),
-                               split_f16(D[f][cb][2] * kVOutScale), split_f16(D[f][cb][3] * kVOutScale));
-        } else {
+        for (int f = 0; f < kNumFilt; ++f)
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (x + i < W)
+            for (int cb = 0; cb < kHmCB; ++cb) D[f][cb] = f32x4v{0.f, 0.f, 0.f, 0.f};
+        for (int st = 0; st < S; ++st) {
+            f16x8 B[3][kHmCB];
 #pragma unroll
-                    for (int f = 0; f < kNumFilt; ++f) t[f * np + q + i] = split_f16(D[f][cb][i] * kVOutScale);
+            for (int ch = 0; ch < 3; ++ch)
+#pragma unroll
+                for (int cb = 0; cb < kHmCB; ++cb)
+                    B[ch][cb] =
+                        __builtin_bit_cast(f16x8, *reinterpret_cast<const u32x4*>(sb + ch * 16 * pitch + 16 * cb + 16 * st));
+#pragma unroll
+            for (int f = 0; f < kNumFilt; ++f) {
+                const int ch = f == 6 ? 0 : f % 3;  // planes t1.xyz, t2.xyz, t3 -> channels x y z x y z x
+                const uint32_t* tf = th + f * 2 * TP + 16 * st;
+                uint4 ah, al;
+                ah.x = tf[0]; ah.y = tf[1]; ah.z = tf[2]; ah.w = tf[3];
+                al.x = tf[TP]; al.y = tf[TP + 1]; al.z = tf[TP + 2]; al.w = tf[TP + 3];
+                const f16x8 AH = __builtin_bit_cast(f16x8, ah), AL = __builtin_bit_cast(f16x8, al);
+#pragma unroll
+                for (int cb = 0; cb < kHmCB; ++cb)
+                    D[f][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(AH, B[ch][cb], D[f][cb], 0, 0, 0);
+#pragma unroll
+                for (int cb = 0; cb < kHmCB; ++cb)
+                    D[f][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(AL, B[ch][cb], D[f][cb], 0, 0, 0);
+            }
+        }
+        // lane (n, g): plane row y0 + n, columns 4 g .. 4 g + 3 of each block, x 2^-30
+        const int y = yb + 16 * t + n;
+        if (y < rows) {
+#pragma unroll
+            for (int cb = 0; cb < kHmCB; ++cb) {
+                const int x = x0 + 16 * (kHmCB * wv + cb) + 4 * g;
+                const int64_t q = (int64_t)y * W + x;
+                if ((W & 3) == 0 && x + 3 < W) {
+#pragma unroll
+                    for (int f = 0; f < kNumFilt; ++f)
+                        *reinterpret_cast<uint4*>(tpl + f * np + q) =
+                            make_uint4(split_f16(D[f][cb][0] * kVOutScale), split_f16(D[f][cb][1] * kVOutScale),
+                                       split_f16(D[f][cb][2] * kVOutScale), split_f16(D[f][cb][3] * kVOutScale));
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (x + i < W)
+#pragma unroll
+                            for (int f = 0; f < kNumFilt; ++f) tpl[f * np + q + i] = split_f16(D[f][cb][i] * kVOutScale);
+                }
+            }
         }
     }
 }
@@ -2099,7 +2126,8 @@ hipError_t launch_cost_tiled_generic(const GenArgs& a, int de, int idx_bytes, hi
         if (a.hmfma && a.htapd) {  // both passes on the matrix cores
             const int pitch = hmfma_pitch(a.half), S = (16 + 2 * a.half + 15) / 16;
             const size_t hl = sizeof(uint32_t) * (3 * 16 * (size_t)pitch + (size_t)kNumFilt * 2 * (16 * S + 16));
-            const dim3 hg((unsigned)((a.g.W + kHmCols - 1) / kHmCols), (unsigned)((a.g.e1 - a.g.e0 + 15) / 16));
+            const dim3 hg((unsigned)((a.g.W + kHmCols - 1) / kHmCols),
+                          (unsigned)((a.g.e1 - a.g.e0 + 16 * kHmRpt - 1) / (16 * kHmRpt)));
             auto goh = [&](auto kern) {
                 if (!allow_dyn_lds(reinterpret_cast<const void*>(kern), hl)) return;
                 HQ_LAUNCH(kern, hg, dim3(256), hl, s, a, pitch);
