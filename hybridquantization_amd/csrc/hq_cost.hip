@@ -1560,11 +1560,20 @@ __global__ __launch_bounds__(256) void gen_vtile2_kernel(GenArgs a, int tiles_x)
 // rows 16 w .. 16 w + 15 of the 64 x 32 tile, both 16-column blocks; a
 // channel's filters accumulate into its two D blocks (x 2^30, folded into the
 // Lab matrix).
+#ifndef HQ_VM_NRB
+#define HQ_VM_NRB 2  // gen_vmfma: 16-row output blocks per wave (tiles of 64 NRB rows)
+#endif
+constexpr int kVmNrb = HQ_VM_NRB;
+// NRB = 2: wave w owns output rows 32 w .. 32 w + 31 of a 128 x 32 tile.  Block
+// 1's B operand of step s is block 0's of step s + 1 (the rows 16 further
+// down), so one window read feeds both blocks: D0 += A_b B_b, D1 += A_(b-1) B_b
+// over b = 0 .. S; and the (128 + 2 half)-row window re-reads 1.8x the tile's
+// rows at half 51 instead of 2.6x.
 template <int DE>
 __global__ __launch_bounds__(256) void gen_vmfma_kernel(GenArgs a, int tiles_x) {
-    // [2][64 + 2 half][32] windows, then the duplicated split taps [7][hi, lo][TP]
+    // [2][TH + 2 half][32] windows, then the duplicated split taps [7][hi, lo][TP]
     extern __shared__ uint32_t s_wm[];
-    constexpr int TW = kVt2W, TH = 64;
+    constexpr int TW = kVt2W, NRB = kVmNrb, TH = 64 * NRB;
     __shared__ double s_red[4];
     const int tid = threadIdx.x, lane = tid & 63, n = lane & 15, g = lane >> 4;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1582,9 +1591,11 @@ __global__ __launch_bounds__(256) void gen_vmfma_kernel(GenArgs a, int tiles_x) 
         dma_window(reinterpret_cast<const uint32_t*>(a.t) + (int64_t)f * np, s_wm + b * BUF, NE, tid, wv, gm, x0, y0,
                    half, rows_inside, wide);
     };
-    f32x4v D[3][2];
+    f32x4v D[3][NRB][2];
 #pragma unroll
-    for (int ch = 0; ch < 3; ++ch) D[ch][0] = D[ch][1] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    for (int ch = 0; ch < 3; ++ch)
+#pragma unroll
+        for (int rb = 0; rb < NRB; ++rb) D[ch][rb][0] = D[ch][rb][1] = f32x4v{0.f, 0.f, 0.f, 0.f};
     issue(0, 0);
     for (int f = 0; f < kNumFilt; ++f) {
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's rows of window f have landed
@@ -1595,13 +1606,12 @@ __global__ __launch_bounds__(256) void gen_vmfma_kernel(GenArgs a, int tiles_x) 
         // duplicated hi and lo tap rows -- a window sliding over the taps
         // (fragments read from global memory left each filter waiting on L2)
         const uint32_t* th = s_tap + f * 2 * TP + 4 * g - (lane & 15) + 15;
-        f32x4v e0 = {0.f, 0.f, 0.f, 0.f}, e1 = {0.f, 0.f, 0.f, 0.f};
-        for (int st = 0; st < S; ++st) {
-          {
-            uint4 ch, cl;
-            ch.x = th[16 * st]; ch.y = th[16 * st + 1]; ch.z = th[16 * st + 2]; ch.w = th[16 * st + 3];
-            cl.x = th[TP + 16 * st]; cl.y = th[TP + 16 * st + 1]; cl.z = th[TP + 16 * st + 2]; cl.w = th[TP + 16 * st + 3];
-            const int r = 16 * wv + 16 * st + 4 * g;
+        f32x4v e[NRB][2];
+#pragma unroll
+        for (int rb = 0; rb < NRB; ++rb) e[rb][0] = e[rb][1] = f32x4v{0.f, 0.f, 0.f, 0.f};
+        f16x8 PH = {}, PL = {};  // A of the previous step (block 1)
+        for (int bs = 0; bs < S + NRB - 1; ++bs) {
+            const int r = TH / 4 * wv + 16 * bs + 4 * g;
             u32x4 b0, b1;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -1610,34 +1620,55 @@ __global__ __launch_bounds__(256) void gen_vmfma_kernel(GenArgs a, int tiles_x) 
                 b1[j] = win[row * TW + 16 + n];
             }
             const f16x8 B0 = __builtin_bit_cast(f16x8, b0), B1 = __builtin_bit_cast(f16x8, b1);
-            const f16x8 AH = __builtin_bit_cast(f16x8, ch), AL = __builtin_bit_cast(f16x8, cl);
-            e0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(AH, B0, e0, 0, 0, 0);
-            e1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(AH, B1, e1, 0, 0, 0);
-            e0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(AL, B0, e0, 0, 0, 0);
-            e1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(AL, B1, e1, 0, 0, 0);
-          }
+            f16x8 AH = {}, AL = {};
+            if (bs < S) {
+                uint4 ch, cl;
+                ch.x = th[16 * bs]; ch.y = th[16 * bs + 1]; ch.z = th[16 * bs + 2]; ch.w = th[16 * bs + 3];
+                cl.x = th[TP + 16 * bs]; cl.y = th[TP + 16 * bs + 1]; cl.z = th[TP + 16 * bs + 2]; cl.w = th[TP + 16 * bs + 3];
+                AH = __builtin_bit_cast(f16x8, ch);
+                AL = __builtin_bit_cast(f16x8, cl);
+                e[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(AH, B0, e[0][0], 0, 0, 0);
+                e[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(AH, B1, e[0][1], 0, 0, 0);
+                e[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(AL, B0, e[0][0], 0, 0, 0);
+                e[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(AL, B1, e[0][1], 0, 0, 0);
+            }
+            if constexpr (NRB == 2) {
+                if (bs >= 1) {
+                    e[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(PH, B0, e[1][0], 0, 0, 0);
+                    e[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(PH, B1, e[1][1], 0, 0, 0);
+                    e[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(PL, B0, e[1][0], 0, 0, 0);
+                    e[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(PL, B1, e[1][1], 0, 0, 0);
+                }
+                PH = AH;
+                PL = AL;
+            }
         }
         const int chp = f == 6 ? 0 : f % 3;  // planes t1.xyz, t2.xyz, t3 -> channels x y z x y z x
-        if (chp == 0) { D[0][0] += e0; D[0][1] += e1; }
-        else if (chp == 1) { D[1][0] += e0; D[1][1] += e1; }
-        else { D[2][0] += e0; D[2][1] += e1; }
+#pragma unroll
+        for (int rb = 0; rb < NRB; ++rb) {
+            if (chp == 0) { D[0][rb][0] += e[rb][0]; D[0][rb][1] += e[rb][1]; }
+            else if (chp == 1) { D[1][rb][0] += e[rb][0]; D[1][rb][1] += e[rb][1]; }
+            else { D[2][rb][0] += e[rb][0]; D[2][rb][1] += e[rb][1]; }
+        }
     }
     double part = 0.0;
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
+    for (int rb = 0; rb < NRB; ++rb)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int y = y0 + 16 * wv + 4 * g + i, gx = x0 + 16 * cb + n;
-            if (gx < gm.W && y < gm.r1) {
-                // (x 2^-30: the data and tap scales, exactly)
-                const float3 lf = opp2f_fast(D[0][cb][i] * kVOutScale, D[1][cb][i] * kVOutScale,
-                                             D[2][cb][i] * kVOutScale, a.m_lab);
-                const int64_t off = (int64_t)(y - gm.r0) * gm.lab_pitch + gx;
-                const float ef = delta_e_f<DE>(a.labL[off], a.labA[off], a.labB[off], lf);
-                if (a.pix_err) a.pix_err[(int64_t)(y - gm.r0) * gm.W + gx] = ef;  // test option: the per-pixel dE
-                part += (double)ef;
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int y = y0 + TH / 4 * wv + 16 * rb + 4 * g + i, gx = x0 + 16 * cb + n;
+                if (gx < gm.W && y < gm.r1) {
+                    // (x 2^-30: the data and tap scales, exactly)
+                    const float3 lf = opp2f_fast(D[0][rb][cb][i] * kVOutScale, D[1][rb][cb][i] * kVOutScale,
+                                                 D[2][rb][cb][i] * kVOutScale, a.m_lab);
+                    const int64_t off = (int64_t)(y - gm.r0) * gm.lab_pitch + gx;
+                    const float ef = delta_e_f<DE>(a.labL[off], a.labA[off], a.labB[off], lf);
+                    if (a.pix_err) a.pix_err[(int64_t)(y - gm.r0) * gm.W + gx] = ef;  // test option: the per-pixel dE
+                    part += (double)ef;
+                }
             }
-        }
     part = wave_sum_to_lane63(part);
     if ((tid & 63) == 63) s_red[tid >> 6] = part;
     __syncthreads();
@@ -2140,9 +2171,10 @@ hipError_t launch_cost_tiled_generic(const GenArgs& a, int de, int idx_bytes, hi
         }
         t_ev_start = nullptr;
         t_ev_stop = ev1;
-        const int tx = (a.g.W + kVt2W - 1) / kVt2W, ty = (a.g.r1 - a.g.r0 + 63) / 64;
+        constexpr int vth = 64 * kVmNrb;
+        const int tx = (a.g.W + kVt2W - 1) / kVt2W, ty = (a.g.r1 - a.g.r0 + vth - 1) / vth;
         const int S = (16 + 2 * a.half + 15) / 16;
-        const size_t l2 = sizeof(uint32_t) * (2 * kVt2W * (64 + 2 * (size_t)a.half) + (size_t)kNumFilt * 2 * (16 * S + 16));
+        const size_t l2 = sizeof(uint32_t) * (2 * kVt2W * (vth + 2 * (size_t)a.half) + (size_t)kNumFilt * 2 * (16 * S + 16));
         auto gov = [&](auto kern) {
             if (!allow_dyn_lds(reinterpret_cast<const void*>(kern), l2)) return;
             HQ_LAUNCH(kern, dim3((unsigned)(tx * ty)), dim3(256), l2, s, a, tx);
