@@ -134,7 +134,7 @@ struct GridArgs {
 // 16 chunks (1024 < K <= 4096): one grid over all K colours, level 1 at 16^3
 // cells (u16 count + 127 indices, 256 B), level 2 at 64^3 (u16 count + 15
 // indices, 32 B); count kN16Ovf = overflow.
-constexpr int kN16G1 = 16, kN16G2 = 64;
+constexpr int kN16G2 = 64, kN16G1 = kN16G2 / 4, kN16G0 = kN16G1 / 4;
 constexpr int kN16L1Cap = 127, kN16L2Cap = 15;
 constexpr int kN16L1Words = kN16L1Cap + 1, kN16L2Words = kN16L2Cap + 1;  // u16 per entry
 constexpr uint16_t kN16Ovf = 0xffff;

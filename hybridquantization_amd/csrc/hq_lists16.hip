@@ -67,7 +67,10 @@ __global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
     const float4* pal = a.pal + (int64_t)p * a.kpal;
     if (tid == 0) s_n0 = 0;
     // level 0
-    const float lo0[3] = {(float)(c0 >> 4) * 0.25f, (float)((c0 >> 2) & 3) * 0.25f, (float)(c0 & 3) * 0.25f};
+    // level-0 cell (side 1 / kN16G0) coordinates
+    const int C0i = c0 / (kN16G0 * kN16G0), C0j = (c0 / kN16G0) % kN16G0, C0k = c0 % kN16G0;
+    const float w0 = 1.0f / kN16G0;
+    const float lo0[3] = {(float)C0i * w0, (float)C0j * w0, (float)C0k * w0};
     constexpr int U = 4096 / kN16Threads;
     float4 cv[U];
     float m = INFINITY;
@@ -75,7 +78,7 @@ __global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
     for (int u = 0; u < U; ++u) {
         const int i = tid + kN16Threads * u;
         cv[u] = pal[min(i, K - 1)];
-        if (i < K) m = fminf(m, box_max2(cv[u], lo0, 0.25f));
+        if (i < K) m = fminf(m, box_max2(cv[u], lo0, w0));
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) m = fminf(m, __shfl_xor(m, off, 64));
@@ -88,7 +91,7 @@ __global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const int i = tid + kN16Threads * u;
-        const bool cand = i < K && box_min2(cv[u], lo0, 0.25f) <= thr0;
+        const bool cand = i < K && box_min2(cv[u], lo0, w0) <= thr0;
         const uint64_t bal = __ballot(cand);
         int base = 0;
         if (lane == 0 && bal) base = atomicAdd(&s_n0, __popcll(bal));
@@ -110,9 +113,9 @@ __global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             const int ch = 4 * wv + c;
-            lo1[c][0] = (float)(4 * (c0 >> 4) + (ch >> 4)) * w1;
-            lo1[c][1] = (float)(4 * ((c0 >> 2) & 3) + ((ch >> 2) & 3)) * w1;
-            lo1[c][2] = (float)(4 * (c0 & 3) + (ch & 3)) * w1;
+            lo1[c][0] = (float)(4 * C0i + (ch >> 4)) * w1;
+            lo1[c][1] = (float)(4 * C0j + ((ch >> 2) & 3)) * w1;
+            lo1[c][2] = (float)(4 * C0k + (ch & 3)) * w1;
             t1[c] = INFINITY;
         }
         for (int i = lane; i < n0; i += 64) {
@@ -140,8 +143,7 @@ __global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
                     const int pos = cnt[c] + __popcll(bal & below);
                     if (cand && pos < kN16L1Cap) {
                         const int ch = 4 * wv + c;
-                        const int I = 4 * (c0 >> 4) + (ch >> 4), J = 4 * ((c0 >> 2) & 3) + ((ch >> 2) & 3),
-                                  L = 4 * (c0 & 3) + (ch & 3);
+                        const int I = 4 * C0i + (ch >> 4), J = 4 * C0j + ((ch >> 2) & 3), L = 4 * C0k + (ch & 3);
                         s_l1[ch * kN16L1Words + 1 + pos] = (uint16_t)i;
                         a.lvl1[((int64_t)p * (kN16G1 * kN16G1 * kN16G1) + (I * kN16G1 + J) * kN16G1 + L) * kN16L1Words +
                                1 + pos] = kk;
@@ -155,7 +157,7 @@ __global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
 #pragma unroll
             for (int c = 1; c < 4; ++c) total = lane == c ? cnt[c] : total;
             const int ch = 4 * wv + lane;
-            const int I = 4 * (c0 >> 4) + (ch >> 4), J = 4 * ((c0 >> 2) & 3) + ((ch >> 2) & 3), L = 4 * (c0 & 3) + (ch & 3);
+            const int I = 4 * C0i + (ch >> 4), J = 4 * C0j + ((ch >> 2) & 3), L = 4 * C0k + (ch & 3);
             const uint16_t h = exh || total > kN16L1Cap ? kN16Ovf : (uint16_t)total;
             s_l1[ch * kN16L1Words] = h;
             a.lvl1[((int64_t)p * (kN16G1 * kN16G1 * kN16G1) + (I * kN16G1 + J) * kN16G1 + L) * kN16L1Words] = h;
@@ -169,9 +171,9 @@ __global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
     auto rl = [](float x, int i) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), i)); };
     for (int j = 0; j < 4; ++j) {
         const int ch = wv + 16 * j, sub = lane;
-        const int I2 = 16 * (c0 >> 4) + 4 * (ch >> 4) + (sub >> 4);
-        const int J2 = 16 * ((c0 >> 2) & 3) + 4 * ((ch >> 2) & 3) + ((sub >> 2) & 3);
-        const int L2 = 16 * (c0 & 3) + 4 * (ch & 3) + (sub & 3);
+        const int I2 = 16 * C0i + 4 * (ch >> 4) + (sub >> 4);
+        const int J2 = 16 * C0j + 4 * ((ch >> 2) & 3) + ((sub >> 2) & 3);
+        const int L2 = 16 * C0k + 4 * (ch & 3) + (sub & 3);
         const float lo2[3] = {(float)I2 * w2, (float)J2 * w2, (float)L2 * w2};
         uint16_t* out = a.lvl2 + ((int64_t)p * (kN16G2 * kN16G2 * kN16G2) + (I2 * kN16G2 + J2) * kN16G2 + L2) * kN16L2Words;
         if (exh) {
@@ -182,14 +184,20 @@ __global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
         const int c1 = __builtin_amdgcn_readfirstlane((int)sl[0]);
         int cnt = 0;
         if (c1 != kN16Ovf) {
-            const int pa = lane < c1 ? sl[1 + lane] : 0, pb = lane + 64 < c1 ? sl[65 + lane] : 0;
-            const float4 ca = s_c0[pa], cb = s_c0[pb];
-            const float ka = (float)s_k0[pa], kb = (float)s_k0[pb];  // (exact: < 2^24)
-            const int na = min(c1, 64);
+            // the parent's list in registers: position 64 j + lane in slot j
+            constexpr int NSL = (kN16L1Cap + 1) / 64;
+            float4 cs[NSL];
+            float ks[NSL];
+#pragma unroll
+            for (int j = 0; j < NSL; ++j) {
+                const int pj = 64 * j + lane < c1 ? sl[1 + 64 * j + lane] : 0;
+                cs[j] = s_c0[pj];
+                ks[j] = (float)s_k0[pj];  // (exact: < 2^24)
+            }
             // centre form of the bounds (3 VALU per axis): per axis |c - m| + h
-            // and max(|c - m| - h, 0), m the box centre (exact), h = 1/128.  Each
-            // is within 2 ulp of the exact term at the terms' sizes here, which
-            // the 1e-5 margin covers with T >= 3 h^2 (a colour at the centre)
+            // and max(|c - m| - h, 0), m the box centre (exact), h = half a cell.
+            // Each is within 2 ulp of the exact term at the terms' sizes here,
+            // which the 1e-5 margin covers with T >= 3 h^2 (a colour at the centre)
             const float h2 = 0.5f * w2;
             const float m0 = lo2[0] + h2, m1 = lo2[1] + h2, m2 = lo2[2] + h2;
             auto bmax = [&](float x, float y, float z) {
@@ -202,19 +210,21 @@ __global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
                 return fmaf(tz, tz, fmaf(ty, ty, tx * tx));
             };
             float t2 = INFINITY;
-            for (int i = 0; i < na; ++i) t2 = fminf(t2, bmax(rl(ca.x, i), rl(ca.y, i), rl(ca.z, i)));
-            for (int i = 64; i < c1; ++i) t2 = fminf(t2, bmax(rl(cb.x, i - 64), rl(cb.y, i - 64), rl(cb.z, i - 64)));
+#pragma unroll
+            for (int j = 0; j < NSL; ++j) {
+                const int nj = min(c1 - 64 * j, 64);
+                for (int i = 0; i < nj; ++i) t2 = fminf(t2, bmax(rl(cs[j].x, i), rl(cs[j].y, i), rl(cs[j].z, i)));
+            }
             const float thr2 = t2 * HQ_CAND_MARGIN;
-            for (int i = 0; i < na; ++i)
-                if (bmin(rl(ca.x, i), rl(ca.y, i), rl(ca.z, i)) <= thr2) {
-                    if (cnt < kN16L2Cap) out[1 + cnt] = (uint16_t)rl(ka, i);
-                    ++cnt;
-                }
-            for (int i = 64; i < c1; ++i)
-                if (bmin(rl(cb.x, i - 64), rl(cb.y, i - 64), rl(cb.z, i - 64)) <= thr2) {
-                    if (cnt < kN16L2Cap) out[1 + cnt] = (uint16_t)rl(kb, i - 64);
-                    ++cnt;
-                }
+#pragma unroll
+            for (int j = 0; j < NSL; ++j) {
+                const int nj = min(c1 - 64 * j, 64);
+                for (int i = 0; i < nj; ++i)
+                    if (bmin(rl(cs[j].x, i), rl(cs[j].y, i), rl(cs[j].z, i)) <= thr2) {
+                        if (cnt < kN16L2Cap) out[1 + cnt] = (uint16_t)rl(ks[j], i);
+                        ++cnt;
+                    }
+            }
         } else {  // the parent list overflowed: every level-0 candidate (broadcast LDS reads)
             float t2 = INFINITY;
             for (int i = 0; i < n0; ++i) t2 = fminf(t2, box_max2(s_c0[i], lo2, w2));
@@ -244,7 +254,7 @@ static void allow_lds16(const void* fn, size_t bytes) {
 hipError_t launch_lists16_grid(const Lists16Args& a, int P, hipStream_t s) {
     const size_t lds = (sizeof(float4) + sizeof(uint16_t)) * (size_t)a.K + sizeof(uint16_t) * 64 * kN16L1Words;
     allow_lds16(reinterpret_cast<const void*>(lists16_kernel), lds);
-    HQ_LAUNCH(lists16_kernel, dim3(64, (unsigned)P), dim3(kN16Threads), lds, s, a);
+    HQ_LAUNCH(lists16_kernel, dim3(kN16G0 * kN16G0 * kN16G0, (unsigned)P), dim3(kN16Threads), lds, s, a);
     return hipGetLastError();
 }
 
@@ -310,10 +320,20 @@ __device__ __noinline__ int argmin16_fix(float r, float g, float b, bool s, int 
     return result;
 }
 
-__device__ __forceinline__ uint32_t u16_at(const uint4& a, const uint4& b, int j) {  // u16 j of the entry
-    const uint32_t w = j < 2 ? a.x : j < 4 ? a.y : j < 6 ? a.z : j < 8 ? a.w : j < 10 ? b.x : j < 12 ? b.y
-                                                                              : j < 14 ? b.z : b.w;
-    return (j & 1) ? w >> 16 : w & 0xffffu;
+// u16 j of the entry, by selects (a variable j must not index the register
+// array: that put the entries in scratch, assign 74 -> 103 us)
+template <int NQ>
+__device__ __forceinline__ uint32_t u16_at(const uint4 (&E)[NQ], int j) {
+    const int w = j >> 1;
+    uint32_t v = E[0].x;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        v = w == 4 * q ? E[q].x : v;
+        v = w == 4 * q + 1 ? E[q].y : v;
+        v = w == 4 * q + 2 ? E[q].z : v;
+        v = w == 4 * q + 3 ? E[q].w : v;
+    }
+    return (j & 1) ? v >> 16 : v & 0xffffu;
 }
 
 template <bool U8>
@@ -370,18 +390,19 @@ __global__ __launch_bounds__(kN16Threads) void assign16_kernel(AssignArgs a, int
             }
         }
         bool in_[kA16B];
-        uint4 e0[kA16B], e1[kA16B];
+        constexpr int NQ = kN16L2Words / 8;  // 16-B pieces per entry
+        uint4 E[kA16B][NQ];
 #pragma unroll
         for (int u = 0; u < kA16B; ++u) {
             in_[u] = r[u] >= 0.f && r[u] <= 1.f && g[u] >= 0.f && g[u] <= 1.f && b[u] >= 0.f && b[u] <= 1.f;
             const uint32_t cell = in_[u] ? (uint32_t)quad_cell16(r[u], g[u], b[u]) : 0u;
-            e0[u] = l2[2 * cell];
-            e1[u] = l2[2 * cell + 1];
+#pragma unroll
+            for (int qq = 0; qq < NQ; ++qq) E[u][qq] = l2[NQ * cell + qq];
         }
         if (bi + 1 < nb) load_batch(bi + 1);
 #pragma unroll
         for (int u = 0; u < kA16B; ++u) {
-            const uint32_t c = e0[u].x & 0xffffu;
+            const uint32_t c = E[u][0].x & 0xffffu;
             const bool slow = !in_[u] || exh || c == kN16Ovf || c == 0u;
             const int cnt = slow ? 0 : (int)c;
             // ranked by d^2 (dist2_rank: within 3 ulp of dist2); a runner-up within
@@ -391,7 +412,7 @@ __global__ __launch_bounds__(kN16Threads) void assign16_kernel(AssignArgs a, int
 #pragma unroll
             for (int i = 0; i < kN16L2Cap; ++i) {
                 if (!HQ_ANY16(i < cnt)) break;
-                const int k = (int)u16_at(e0[u], e1[u], i + 1);
+                const int k = (int)u16_at(E[u], i + 1);
                 const float d2 = i < cnt ? dist2_rank(r[u], g[u], b[u], s_pal[i < cnt ? k : 0]) : INFINITY;
                 const bool lt = d2 < best2;
                 second2 = __builtin_amdgcn_fmed3f(best2, second2, d2);
@@ -404,7 +425,7 @@ __global__ __launch_bounds__(kN16Threads) void assign16_kernel(AssignArgs a, int
                     float bd = INFINITY;
                     int bkk = 0x7fffffff;
                     for (int i = 0; i < cnt; ++i) {
-                        const int k = (int)u16_at(e0[u], e1[u], i + 1);
+                        const int k = (int)u16_at(E[u], i + 1);
                         const float d = sqrtf(dist2(r[u], g[u], b[u], s_pal[k]));
                         if (d < bd || (d == bd && k < bkk)) {
                             bd = d;
