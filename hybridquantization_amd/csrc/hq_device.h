@@ -254,11 +254,11 @@ __device__ __forceinline__ float u8_unit(uint32_t v, int j) {
 // finalize or the SA step).  Resolution 2^-20 per partial: < 1e-10 relative at
 // 4096^2.  A partial that is not a finite number in [0, 2^43) (a NaN pixel,
 // an absurd palette) counts in `bad` and makes the sum NaN.
-// Layout: [kAccSlots][P][4] u64: lo, hi, bad, (pad).
+// Layout: [kAccSlots][acc_pitch(P)][4] u64: lo, hi, bad, (pad).
 // ----------------------------------------------------------------------------
 constexpr double kAccScale = 1048576.0;  // 2^20
 __device__ __forceinline__ void acc_add(uint64_t* acc, int P, int p, int slot, double x) {
-    uint64_t* a = acc + ((int64_t)(slot & (kAccSlots - 1)) * P + p) * 4;
+    uint64_t* a = acc + ((int64_t)(slot & (kAccSlots - 1)) * acc_pitch(P) + p) * 4;
     if (x >= 0.0 && x < 8796093022208.0) {  // 2^43 (NaN fails the test)
         const uint64_t v = (uint64_t)__double2ull_rn(x * kAccScale);
         atomicAdd((unsigned long long*)(a + 0), (unsigned long long)(v & 0xffffffffull));
@@ -272,7 +272,7 @@ __device__ __forceinline__ double acc_total(const uint64_t* acc, int P, int p) {
     uint64_t lo = 0, hi = 0, bad = 0;
 #pragma unroll
     for (int sl = 0; sl < kAccSlots; ++sl) {
-        const uint64_t* a = acc + ((int64_t)sl * P + p) * 4;
+        const uint64_t* a = acc + ((int64_t)sl * acc_pitch(P) + p) * 4;
         lo += a[0];
         hi += a[1];
         bad += a[2];

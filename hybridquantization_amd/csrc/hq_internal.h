@@ -73,7 +73,11 @@ inline int used_stride(int P) { return (P * 8 + 63) / 64 * 64; }
 // sets used alternately by consecutive evaluations (a set is zeroed by the
 // kernel before the evaluation's cost kernel, while the previous set is read)
 constexpr int kAccSlots = 16;
-inline size_t acc_words(int P) { return (size_t)kAccSlots * P * 4; }
+// palettes per slot row, a multiple of 8: each slot's counters start a 256-B
+// row of their own, so the slots' atomics spread over the memory channels
+// rather than queueing on one (P = 1: sixteen 32-B slots shared 512 B)
+__host__ __device__ constexpr int acc_pitch(int P) { return (P + 7) & ~7; }
+inline size_t acc_words(int P) { return (size_t)kAccSlots * acc_pitch(P) * 4; }
 
 // sa_step_kernel: one accept + generate step of the device-resident SWASA search.
 struct SaArgs {

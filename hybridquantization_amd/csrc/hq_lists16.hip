@@ -60,7 +60,7 @@ __global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
         const int wpp = 8 * a.nch;
         for (int i = tid; i < wpp * kUsedSlots; i += kN16Threads)
             a.used_glob[(i / wpp) * a.used_stride + p * wpp + i % wpp] = 0u;
-        if (tid < 4 * kAccSlots) a.acc_zero[((int64_t)(tid >> 2) * a.P_acc + p) * 4 + (tid & 3)] = 0ull;
+        if (tid < 4 * kAccSlots) a.acc_zero[((int64_t)(tid >> 2) * acc_pitch(a.P_acc) + p) * 4 + (tid & 3)] = 0ull;
     }
     bool exh = false;
     for (int j = 0; j < a.nch; ++j) exh |= a.pflags[p * a.nch + j] != 0;

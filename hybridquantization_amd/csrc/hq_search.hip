@@ -184,7 +184,7 @@ __device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared
             const int e = e0 + tid, pp = e >> 4, sl = e & 15;
             unsigned long long lo = 0, hi = 0, bad = 0;
             if (e < P * kAccSlots) {
-                const uint64_t* q = a.acc + ((int64_t)sl * P + pp) * 4;
+                const uint64_t* q = a.acc + ((int64_t)sl * acc_pitch(P) + pp) * 4;
                 lo = q[0];
                 hi = q[1];
                 bad = q[2];
@@ -831,7 +831,7 @@ __global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
     if (blockIdx.x == 0 && tid < 8 * kUsedSlots)  // for the assign that follows
         a.used_glob[(tid >> 3) * a.used_stride + p * 8 + (tid & 7)] = 0u;
     if (blockIdx.x == 0 && p % a.nch == 0 && tid < 4 * kAccSlots)  // for the cost kernel
-        a.acc_zero[((int64_t)(tid >> 2) * a.P_acc + p / a.nch) * 4 + (tid & 3)] = 0ull;
+        a.acc_zero[((int64_t)(tid >> 2) * acc_pitch(a.P_acc) + p / a.nch) * 4 + (tid & 3)] = 0ull;
     const bool exh = a.pflags[p] != 0;
     bool valid = false;
     float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
