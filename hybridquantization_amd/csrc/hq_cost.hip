@@ -1560,20 +1560,16 @@ __global__ __launch_bounds__(256) void gen_vtile2_kernel(GenArgs a, int tiles_x)
 // rows 16 w .. 16 w + 15 of the 64 x 32 tile, both 16-column blocks; a
 // channel's filters accumulate into its two D blocks (x 2^30, folded into the
 // Lab matrix).
-#ifndef HQ_VM_NRB
-#define HQ_VM_NRB 2  // gen_vmfma: 16-row output blocks per wave (tiles of 64 NRB rows)
-#endif
-constexpr int kVmNrb = HQ_VM_NRB;
 // NRB = 2: wave w owns output rows 32 w .. 32 w + 31 of a 128 x 32 tile.  Block
 // 1's B operand of step s is block 0's of step s + 1 (the rows 16 further
 // down), so one window read feeds both blocks: D0 += A_b B_b, D1 += A_(b-1) B_b
 // over b = 0 .. S; and the (128 + 2 half)-row window re-reads 1.8x the tile's
 // rows at half 51 instead of 2.6x.
-template <int DE>
+template <int DE, int NRB>
 __global__ __launch_bounds__(256) void gen_vmfma_kernel(GenArgs a, int tiles_x) {
     // [2][TH + 2 half][32] windows, then the duplicated split taps [7][hi, lo][TP]
     extern __shared__ uint32_t s_wm[];
-    constexpr int TW = kVt2W, NRB = kVmNrb, TH = 64 * NRB;
+    constexpr int TW = kVt2W, TH = 64 * NRB;
     __shared__ double s_red[4];
     const int tid = threadIdx.x, lane = tid & 63, n = lane & 15, g = lane >> 4;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1684,25 +1680,21 @@ __global__ __launch_bounds__(256) void gen_vmfma_kernel(GenArgs a, int tiles_x) 
 // t3 plane's horizontal taps, CL:254-267).  D's lane holds 4 adjacent output
 // columns of one row: one 16-B store of split dwords per plane, which is
 // gen_vmfma's input as it stands.  A workgroup: 16 rows x 128 columns (4 waves
-// x 2 blocks of 16), kHmRpt such tiles down the image per workgroup; its
+// x 2 blocks of 16), rpt such tiles down the image per workgroup; its
 // segment the 3 channels' split opponent colours, [3][16][pitch] dwords,
 // pitch = 8 mod 64 (ds_read_b128's lane groups then hit 64 distinct banks).
 constexpr int kHmCB = 2, kHmCols = 64 * kHmCB;
 static int hmfma_seg_cols(int H) { return kHmCols - 16 + 16 * ((16 + 2 * H + 15) / 16); }
 static int hmfma_pitch(int H) { return (hmfma_seg_cols(H) - 8 + 63) / 64 * 64 + 8; }
-#ifndef HQ_HM_RPT
-#define HQ_HM_RPT 4  // gen_hmfma: 16-row tiles per workgroup, the next one's colours loaded during this one's MFMAs
-#endif
-constexpr int kHmRpt = HQ_HM_RPT;
 template <typename IT>
-__global__ __launch_bounds__(256, 2) void gen_hmfma_kernel(GenArgs a, int pitch) {  // (2 waves per SIMD: LDS allows 2 workgroups)
+__global__ __launch_bounds__(256, 2) void gen_hmfma_kernel(GenArgs a, int pitch, int rpt) {  // (2 waves per SIMD: LDS allows 2 workgroups)
     extern __shared__ uint32_t s_hm[];  // [3][16][pitch] segment, then the taps [7][hi, lo][TP]
     const int tid = threadIdx.x, lane = tid & 63, n = lane & 15, g = lane >> 4;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int half = a.half, W = a.g.W, rows = a.g.e1 - a.g.e0;
     const int S = (16 + 2 * half + 15) / 16, TP = 16 * S + 16, SW = kHmCols - 16 + 16 * S;
-    const int x0 = blockIdx.x * kHmCols, yb = blockIdx.y * 16 * kHmRpt;
-    const int nt = min(kHmRpt, (rows - yb + 15) / 16);  // this workgroup's tiles
+    const int x0 = blockIdx.x * kHmCols, yb = blockIdx.y * 16 * rpt;
+    const int nt = min(rpt, (rows - yb + 15) / 16);  // this workgroup's tiles
     uint32_t* s_tap = s_hm + 3 * 16 * pitch;
     for (int i = tid; i < kNumFilt * 2 * TP; i += 256) s_tap[i] = a.htapd[i];
     // the segment of a tile: column tid of its 16 rows (SW <= 256 for half <= 64).
@@ -1802,14 +1794,16 @@ __global__ __launch_bounds__(256, 2) void gen_hmfma_kernel(GenArgs a, int pitch)
         }
     }
 }
-template __global__ void gen_hmfma_kernel<uint8_t>(GenArgs, int);
-template __global__ void gen_hmfma_kernel<uint16_t>(GenArgs, int);
-template __global__ void gen_hmfma_kernel<uint32_t>(GenArgs, int);
+template __global__ void gen_hmfma_kernel<uint8_t>(GenArgs, int, int);
+template __global__ void gen_hmfma_kernel<uint16_t>(GenArgs, int, int);
+template __global__ void gen_hmfma_kernel<uint32_t>(GenArgs, int, int);
 
 // (explicit instantiations: taken only through a generic lambda, the dE94
 // kernels' host handles were left undefined by the host compile)
-template __global__ void gen_vmfma_kernel<0>(GenArgs, int);
-template __global__ void gen_vmfma_kernel<1>(GenArgs, int);
+template __global__ void gen_vmfma_kernel<0, 1>(GenArgs, int);
+template __global__ void gen_vmfma_kernel<1, 1>(GenArgs, int);
+template __global__ void gen_vmfma_kernel<0, 2>(GenArgs, int);
+template __global__ void gen_vmfma_kernel<1, 2>(GenArgs, int);
 template __global__ void gen_vtile2_kernel<0, HQ_VT2_RB>(GenArgs, int);
 template __global__ void gen_vtile2_kernel<1, HQ_VT2_RB>(GenArgs, int);
 template __global__ void gen_vtile_kernel<0>(GenArgs, int);
@@ -2154,14 +2148,27 @@ hipError_t launch_cost_tiled_generic(const GenArgs& a, int de, int idx_bytes, hi
     t_ev_stop = nullptr;
     const bool vm = a.vmfma && a.vtapd && a.half <= kVt2MaxHalf;  // the matrix-core vertical pass
     if (vm) {
+        // workgroup shapes by grid size: the taller forms only when they still
+        // give every CU two rounds of work (1024^2: 128-row tiles left 256
+        // workgroups, one per CU)
+        static const int cus = [] {
+            int d = 0, n = 0;
+            return hipGetDevice(&d) == hipSuccess &&
+                           hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && n > 0
+                       ? n
+                       : 256;
+        }();
+        const int rows = a.g.e1 - a.g.e0;
         if (a.hmfma && a.htapd) {  // both passes on the matrix cores
             const int pitch = hmfma_pitch(a.half), S = (16 + 2 * a.half + 15) / 16;
             const size_t hl = sizeof(uint32_t) * (3 * 16 * (size_t)pitch + (size_t)kNumFilt * 2 * (16 * S + 16));
-            const dim3 hg((unsigned)((a.g.W + kHmCols - 1) / kHmCols),
-                          (unsigned)((a.g.e1 - a.g.e0 + 16 * kHmRpt - 1) / (16 * kHmRpt)));
+            const int hx = (a.g.W + kHmCols - 1) / kHmCols, tiles = hx * ((rows + 15) / 16);
+            // 16-row tiles per workgroup (pipelined fills): 4 on large images
+            const int rpt = a.shape == 2 ? 4 : a.shape == 1 ? 1 : tiles >= 16 * cus ? 4 : tiles >= 8 * cus ? 2 : 1;
+            const dim3 hg((unsigned)hx, (unsigned)((rows + 16 * rpt - 1) / (16 * rpt)));
             auto goh = [&](auto kern) {
                 if (!allow_dyn_lds(reinterpret_cast<const void*>(kern), hl)) return;
-                HQ_LAUNCH(kern, hg, dim3(256), hl, s, a, pitch);
+                HQ_LAUNCH(kern, hg, dim3(256), hl, s, a, pitch, rpt);
             };
             if (idx_bytes == 4) goh(gen_hmfma_kernel<uint32_t>);
             else if (idx_bytes == 2) goh(gen_hmfma_kernel<uint16_t>);
@@ -2171,16 +2178,21 @@ hipError_t launch_cost_tiled_generic(const GenArgs& a, int de, int idx_bytes, hi
         }
         t_ev_start = nullptr;
         t_ev_stop = ev1;
-        constexpr int vth = 64 * kVmNrb;
-        const int tx = (a.g.W + kVt2W - 1) / kVt2W, ty = (a.g.r1 - a.g.r0 + vth - 1) / vth;
-        const int S = (16 + 2 * a.half + 15) / 16;
+        const int tx = (a.g.W + kVt2W - 1) / kVt2W, S = (16 + 2 * a.half + 15) / 16;
+        const bool two = a.shape == 2 || (a.shape == 0 && tx * ((a.g.r1 - a.g.r0 + 127) / 128) >= 4 * cus);  // 128-row tiles
+        const int vth = two ? 128 : 64, ty = (a.g.r1 - a.g.r0 + vth - 1) / vth;
         const size_t l2 = sizeof(uint32_t) * (2 * kVt2W * (vth + 2 * (size_t)a.half) + (size_t)kNumFilt * 2 * (16 * S + 16));
         auto gov = [&](auto kern) {
             if (!allow_dyn_lds(reinterpret_cast<const void*>(kern), l2)) return;
             HQ_LAUNCH(kern, dim3((unsigned)(tx * ty)), dim3(256), l2, s, a, tx);
         };
-        if (de == 0) gov(gen_vmfma_kernel<0>);
-        else gov(gen_vmfma_kernel<1>);
+        if (two) {
+            if (de == 0) gov(gen_vmfma_kernel<0, 2>);
+            else gov(gen_vmfma_kernel<1, 2>);
+        } else {
+            if (de == 0) gov(gen_vmfma_kernel<0, 1>);
+            else gov(gen_vmfma_kernel<1, 1>);
+        }
         t_ev_start = ev0;
         return hipGetLastError();
     }

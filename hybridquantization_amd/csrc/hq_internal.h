@@ -263,6 +263,7 @@ struct GenArgs {
     int vmfma = 1;       // tiled path: the vertical pass on the matrix cores (gen_vmfma, split f16)
     const uint32_t* vtapd = nullptr;  // its duplicated split taps [7][hi, lo][16 S + 16] (build_vtile_dup_taps)
     int hmfma = 1;       // with vmfma: the horizontal pass on the matrix cores too (gen_hmfma)
+    int shape = 0;       // matrix-core pair's tile shapes: 0 by grid size, 1 the short forms, 2 the tall ones
     const uint32_t* htapd = nullptr;  // its taps, the same layout (k3 signed: the horizontal t3 taps)
     const float4* htaps = nullptr;  // gen_hrow4: [T][2] (k1.xyz, k3), (k2.xyz, 0) horizontal taps
 };

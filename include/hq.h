@@ -214,6 +214,9 @@ int hq_profile_reset(hq_ctx *ctx);
  *                  cores in split f16 (as the fast path's; default 1), 0 = fp32 FMAs (gen_vtile2)
  *   "gen_hmfma"    with gen_vmfma: the horizontal pass on the matrix cores too (default 1;
  *                  palettes in the fast range), 0 = fp32 FMAs (gen_hrow4)
+ *   "gen_tile_shape" the matrix-core generic pair's workgroup shapes: 0 (default) by grid size
+ *                  (4 row tiles per gen_hmfma workgroup and 128-row gen_vmfma tiles on large
+ *                  images), 1 the short forms, 2 the tall forms (same results within the split bars)
  *   "lists16"      chunked palettes: native 16-bit candidate lists (one grid over all K
  *                  colours, one lookup per pixel): 1 (default) for 8 and 16 chunks, 2 for
  *                  2 .. 16 chunks, 0 = a grid and assign pass per 256-colour chunk

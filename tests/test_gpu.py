@@ -193,8 +193,9 @@ def test_generic_hrow4_bitwise(gpu, w, h, dpi, vd):
     K, P = 64, 2
     pals = np.stack([o.synthetic_palette(K, 9 + p) for p in range(P)]).reshape(P, -1)
     res = []
-    for h4, v2, vm, no, hm in ((0, 0, 0, 4, 0), (1, 0, 0, 4, 0), (1, 1, 0, 4, 0), (1, 1, 1, 4, 0), (1, 1, 0, 8, 0),
-                               (1, 1, 1, 4, 1)):
+    for h4, v2, vm, no, hm, shape in ((0, 0, 0, 4, 0, 0), (1, 0, 0, 4, 0, 0), (1, 1, 0, 4, 0, 0), (1, 1, 1, 4, 0, 0),
+                                      (1, 1, 0, 8, 0, 0), (1, 1, 1, 4, 1, 1), (1, 1, 1, 4, 1, 2)):
+        m.setOption("gen_tile_shape", shape)
         m.setOption("gen_hmfma", hm)
         m.setOption("gen_hrow4", h4)
         m.setOption("gen_vtile2", v2)
@@ -220,11 +221,14 @@ def test_generic_hrow4_bitwise(gpu, w, h, dpi, vd):
         np.testing.assert_allclose(res[3][1][p], res[2][1][p], rtol=0, atol=2e-4)
     np.testing.assert_allclose(res[3][0].reshape(P, 1 + K)[:, 0], res[2][0].reshape(P, 1 + K)[:, 0], rtol=1e-6)
     np.testing.assert_array_equal(res[3][0].reshape(P, 1 + K)[:, 1:], res[2][0].reshape(P, 1 + K)[:, 1:])
-    # gen_hmfma + gen_vmfma (the default): both passes on the matrix cores
-    for p in range(P):
-        np.testing.assert_allclose(res[5][1][p], res[2][1][p], rtol=0, atol=2e-4)
-    np.testing.assert_allclose(res[5][0].reshape(P, 1 + K)[:, 0], res[2][0].reshape(P, 1 + K)[:, 0], rtol=1e-6)
-    np.testing.assert_array_equal(res[5][0].reshape(P, 1 + K)[:, 1:], res[2][0].reshape(P, 1 + K)[:, 1:])
+    # gen_hmfma + gen_vmfma (the default): both passes on the matrix cores, in
+    # the short (one 16-row tile per gen_hmfma workgroup, 64-row gen_vmfma tiles)
+    # and the tall shapes (4 tiles, 128 rows: partial tiles at every size here)
+    for r in (5, 6):
+        for p in range(P):
+            np.testing.assert_allclose(res[r][1][p], res[2][1][p], rtol=0, atol=2e-4)
+        np.testing.assert_allclose(res[r][0].reshape(P, 1 + K)[:, 0], res[2][0].reshape(P, 1 + K)[:, 0], rtol=1e-6)
+        np.testing.assert_array_equal(res[r][0].reshape(P, 1 + K)[:, 1:], res[2][0].reshape(P, 1 + K)[:, 1:])
 
 
 @pytest.mark.parametrize("dpi,vd", [(150, 30.0), (96, 60.0), (200, 30.0)])
