@@ -572,7 +572,7 @@ def test_wide_palette_vs_oracle(gpu, filt, K, P):
     m.close()
 
 
-@pytest.mark.parametrize("K", [512, 1024, 2048, 4096, 3000, 8192, 5000])
+@pytest.mark.parametrize("K", [512, 1024, 2048, 4096, 3000, 8192, 5000, 16384, 10000])
 def test_chunked_palettes_match_exhaustive(gpu, filt, K):
     """The chunked K > 256 path (grid per 256-colour chunk, winners combined by
     the reference distance, hq_assign.hip) against the exhaustive one (option
