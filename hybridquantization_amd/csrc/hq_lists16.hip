@@ -31,11 +31,13 @@ namespace hq {
 // The grid: one workgroup of 1024 threads per level-0 cell (side 1/4) and
 // palette, grid (64, P).  Level 0: the threshold over all K colours (read from
 // memory, 4 per thread) and the cell's candidates, compacted into LDS as
-// colours + indices.  Level 1: its 64 cells of side 1/16, 16 threads each, the
-// threshold and list over the level-0 candidates (positions into that LDS
-// array, and the colour indices to memory for assign's fallback).  Level 2:
-// the 4096 cells of side 1/64 below, one thread per cell (a wave's 64 threads
-// share a parent list: broadcast LDS reads), its entry written by that thread.
+// colours + indices.  Level 1: its 64 cells of side 1/16, 4 per wave (the
+// wave's lanes over the level-0 candidates, one LDS read per colour for the 4
+// cells), the threshold and the list by ballot (positions into that LDS array,
+// and the colour indices to memory for assign's fallback).  Level 2: the 4096
+// cells of side 1/64 below, one thread per cell; a wave's 64 threads share a
+// parent, whose list sits in registers and is broadcast by readlane; each
+// entry is written by its thread.
 // Each level's candidates are a superset of the colours that can win in its
 // cells: a pixel's winner w is within d(x, b) of it for every colour b, so
 // w passes the parent's test and then the child's over the parent's list.
