@@ -61,7 +61,8 @@ struct PaletteArgs {
     int K;
 };
 
-constexpr int kSaMaxP = 64;        // device-resident SWASA: largest population (sub-palettes)
+constexpr int kSaMaxP = 64;        // device-resident SWASA: largest population
+constexpr int kSaMaxSub = 512;     // ... and sub-palettes (P nch; sa_step's fold: 8 P nch used words <= 4 x 1024)
 // Used-colour bits are kept in kUsedSlots copies, used_stride(P) words apart
 // (256-B multiples): assign's workgroups OR theirs into copy blockIdx & 7, the
 // readers OR the copies.  One copy took every workgroup's atomic at the end of
@@ -134,20 +135,25 @@ struct GridArgs {
     int nch;                // sub-palettes per palette (chunked palettes), else 1
 };
 
-// Native 16-bit candidate lists (hq_lists16.hip) for chunked palettes of 8 or
-// 16 chunks (1024 < K <= 4096): one grid over all K colours, level 1 at 16^3
-// cells (u16 count + 127 indices, 256 B), level 2 at 64^3 (u16 count + 15
+// Native 16-bit candidate lists (hq_lists16.hip) for chunked palettes of 8 to
+// 32 chunks (1024 < K <= 8192): one grid over all K colours, level 1 at 16^3
+// cells (u16 count + 127 or 255 indices), level 2 at 64^3 (u16 count + 15
 // indices, 32 B); count kN16Ovf = overflow.
 constexpr int kN16G2 = 64, kN16G1 = kN16G2 / 4, kN16G0 = kN16G1 / 4;
-constexpr int kN16L1Cap = 127, kN16L2Cap = 15;
-constexpr int kN16L1Words = kN16L1Cap + 1, kN16L2Words = kN16L2Cap + 1;  // u16 per entry
+// Level-1 entries: 128 u16 (count + 127) up to K = 4096, 256 above (lists at
+// K = 8192: mean ~66, a tail past 127); the buffer is sized for the larger.
+constexpr int kN16L2Cap = 15, kN16L2Words = kN16L2Cap + 1;  // u16 per entry
+constexpr int kN16L1WordsMax = 256;
+__host__ __device__ constexpr int n16_l1_words(int K) { return K > 4096 ? 256 : 128; }
 constexpr uint16_t kN16Ovf = 0xffff;
-constexpr int kN16MinNch = 8;  // chunk counts that take the native lists (option "lists16")
+constexpr int kN16MinNch = 8;   // chunk counts that take the native lists (option "lists16") ...
+constexpr int kN16MaxNch = 32;  // ... up to K = 8192: the palette's 128 KiB table in assign16's LDS
+constexpr int kN16MaxK = 256 * kN16MaxNch;
 
 struct Lists16Args {
     const float4* pal;      // [P][kpal] colours (the prepared sub-palettes, contiguous per palette)
     const int* pflags;      // [P nch] sub-palette flags (non-finite colour: exhaustive)
-    uint16_t* lvl1;         // [P][16^3][kN16L1Words]
+    uint16_t* lvl1;         // [P][16^3][n16_l1_words(K)]
     uint16_t* lvl2;         // [P][64^3][kN16L2Words]
     uint32_t* used_glob;    // [kUsedSlots][used_stride]: [P][8 nch] used-colour bits, zeroed here
     int used_stride;

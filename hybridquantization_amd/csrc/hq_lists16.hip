@@ -1,5 +1,5 @@
-// hq_lists16.hip -- native 16-bit candidate lists for chunked palettes of 8 or
-// 16 chunks (1024 < K <= 4096).  The chunked path (hq_assign.hip) runs one
+// hq_lists16.hip -- native 16-bit candidate lists for chunked palettes of 8 to
+// 32 chunks (1024 < K <= 8192).  The chunked path (hq_assign.hip) runs one
 // grid per 256-colour chunk and nch / 4 assign passes that carry the best
 // distance so far through a scratch image: 16 lookups and list walks per pixel
 // at K = 4096.  Here one grid covers all K colours at a finer level 2 (64^3
@@ -50,10 +50,26 @@ __device__ __forceinline__ float box_max2(float4 c, const float (&lo)[3], float 
 }
 
 constexpr int kN16Threads = 1024;
+// SOA: the level-0 candidates as three float planes (12 B per colour: K =
+// 8192 fits beside the lists), else float4 (one ds_read_b128 each; the planes
+// cost K = 4096 1.4 us)
+template <bool SOA>
 __global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
-    extern __shared__ float4 s_c0[];                               // [K] level-0 candidates
-    uint16_t* s_k0 = reinterpret_cast<uint16_t*>(s_c0 + a.K);       // [K] their colour indices
-    uint16_t* s_l1 = s_k0 + a.K;                                   // [64][kN16L1Words] positions in s_c0
+    constexpr int kN16L1Words = SOA ? 256 : 128, kN16L1Cap = kN16L1Words - 1;  // (n16_l1_words)
+    // [K] float4 or [3][K] floats, then the colour indices (declared float4: the
+    // b128 reads need the 16-B alignment known; a float array left them split)
+    extern __shared__ float4 s_cfv[];
+    float* const s_cf = reinterpret_cast<float*>(s_cfv);
+    float* const s_cx = s_cf;
+    float* const s_cy = s_cf + a.K;
+    float* const s_cz = s_cf + 2 * a.K;
+    float4* const s_c4 = s_cfv;
+    auto c0at = [&](int i) {
+        if constexpr (SOA) return make_float4(s_cx[i], s_cy[i], s_cz[i], 0.f);
+        else return s_c4[i];
+    };
+    uint16_t* s_k0 = reinterpret_cast<uint16_t*>(s_cf + (SOA ? 3 : 4) * a.K);  // [K] their colour indices
+    uint16_t* s_l1 = s_k0 + a.K;                                   // [64][kN16L1Words] positions in the level-0 planes
     __shared__ float s_red[kN16Threads / 64];
     __shared__ int s_n0;
     const int p = blockIdx.y, c0 = blockIdx.x, tid = threadIdx.x, K = a.K;
@@ -73,7 +89,7 @@ __global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
     const int C0i = c0 / (kN16G0 * kN16G0), C0j = (c0 / kN16G0) % kN16G0, C0k = c0 % kN16G0;
     const float w0 = 1.0f / kN16G0;
     const float lo0[3] = {(float)C0i * w0, (float)C0j * w0, (float)C0k * w0};
-    constexpr int U = 4096 / kN16Threads;
+    constexpr int U = (SOA ? kN16MaxK : 4096) / kN16Threads;  // colours per thread (K <= 4096 unless SOA)
     float4 cv[U];
     float m = INFINITY;
 #pragma unroll
@@ -100,7 +116,13 @@ __global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
         base = __shfl(base, 0, 64);
         if (cand) {
             const int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
-            s_c0[pos] = cv[u];
+            if constexpr (SOA) {
+                s_cx[pos] = cv[u].x;
+                s_cy[pos] = cv[u].y;
+                s_cz[pos] = cv[u].z;
+            } else {
+                s_c4[pos] = cv[u];
+            }
             s_k0[pos] = (uint16_t)i;
         }
     }
@@ -121,7 +143,7 @@ __global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
             t1[c] = INFINITY;
         }
         for (int i = lane; i < n0; i += 64) {
-            const float4 cv = s_c0[i];
+            const float4 cv = c0at(i);
 #pragma unroll
             for (int c = 0; c < 4; ++c) t1[c] = fminf(t1[c], box_max2(cv, lo1[c], w1));
         }
@@ -136,7 +158,7 @@ __global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
         if (!exh) {
             for (int i0 = 0; i0 < n0; i0 += 64) {
                 const int i = i0 + lane;
-                const float4 cv = s_c0[min(i, n0 - 1)];
+                const float4 cv = c0at(min(i, n0 - 1));
                 const uint16_t kk = s_k0[min(i, n0 - 1)];
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
@@ -193,7 +215,7 @@ __global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
 #pragma unroll
             for (int j = 0; j < NSL; ++j) {
                 const int pj = 64 * j + lane < c1 ? sl[1 + 64 * j + lane] : 0;
-                cs[j] = s_c0[pj];
+                cs[j] = c0at(pj);
                 ks[j] = (float)s_k0[pj];  // (exact: < 2^24)
             }
             // centre form of the bounds (3 VALU per axis): per axis |c - m| + h
@@ -229,10 +251,10 @@ __global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
             }
         } else {  // the parent list overflowed: every level-0 candidate (broadcast LDS reads)
             float t2 = INFINITY;
-            for (int i = 0; i < n0; ++i) t2 = fminf(t2, box_max2(s_c0[i], lo2, w2));
+            for (int i = 0; i < n0; ++i) t2 = fminf(t2, box_max2(c0at(i), lo2, w2));
             const float thr2 = t2 * HQ_CAND_MARGIN;
             for (int i = 0; i < n0; ++i)
-                if (box_min2(s_c0[i], lo2, w2) <= thr2) {
+                if (box_min2(c0at(i), lo2, w2) <= thr2) {
                     if (cnt < kN16L2Cap) out[1 + cnt] = s_k0[i];
                     ++cnt;
                 }
@@ -254,9 +276,17 @@ static void allow_lds16(const void* fn, size_t bytes) {
 }
 
 hipError_t launch_lists16_grid(const Lists16Args& a, int P, hipStream_t s) {
-    const size_t lds = (sizeof(float4) + sizeof(uint16_t)) * (size_t)a.K + sizeof(uint16_t) * 64 * kN16L1Words;
-    allow_lds16(reinterpret_cast<const void*>(lists16_kernel), lds);
-    HQ_LAUNCH(lists16_kernel, dim3(kN16G0 * kN16G0 * kN16G0, (unsigned)P), dim3(kN16Threads), lds, s, a);
+    const bool soa = a.K > 4096;
+    const size_t lds = ((soa ? 3 : 4) * sizeof(float) + sizeof(uint16_t)) * (size_t)a.K +
+                       sizeof(uint16_t) * 64 * n16_l1_words(a.K);
+    const dim3 grid(kN16G0 * kN16G0 * kN16G0, (unsigned)P);
+    if (soa) {
+        allow_lds16(reinterpret_cast<const void*>(lists16_kernel<true>), lds);
+        HQ_LAUNCH(lists16_kernel<true>, grid, dim3(kN16Threads), lds, s, a);
+    } else {
+        allow_lds16(reinterpret_cast<const void*>(lists16_kernel<false>), lds);
+        HQ_LAUNCH(lists16_kernel<false>, grid, dim3(kN16Threads), lds, s, a);
+    }
     return hipGetLastError();
 }
 
@@ -349,7 +379,8 @@ __global__ __launch_bounds__(kN16Threads) void assign16_kernel(AssignArgs a, int
     for (int j = 0; j < a.nch; ++j) exh |= a.pflags[p * a.nch + j] != 0;
     __syncthreads();
     const uint4* l2 = reinterpret_cast<const uint4*>(a.l2n + (int64_t)p * (kN16G2 * kN16G2 * kN16G2) * kN16L2Words);
-    const uint16_t* l1 = a.l1n + (int64_t)p * (kN16G1 * kN16G1 * kN16G1) * kN16L1Words;
+    const int l1w = n16_l1_words(K);
+    const uint16_t* l1 = a.l1n + (int64_t)p * (kN16G1 * kN16G1 * kN16G1) * l1w;
     uint16_t* idx = a.idx16 + (int64_t)p * a.idx_pitch;
     const uint32_t n_ext = (uint32_t)a.n_ext, qlast = n_ext - 1;
     const uint32_t cstride = (uint32_t)a.nblocks * (uint32_t)kN16Threads;
@@ -444,7 +475,7 @@ __global__ __launch_bounds__(kN16Threads) void assign16_kernel(AssignArgs a, int
                     const int i1 = min((int)(r[u] * (float)kN16G1), kN16G1 - 1);
                     const int j1 = min((int)(g[u] * (float)kN16G1), kN16G1 - 1);
                     const int k1 = min((int)(b[u] * (float)kN16G1), kN16G1 - 1);
-                    const uint16_t* e = l1 + (int64_t)((i1 * kN16G1 + j1) * kN16G1 + k1) * kN16L1Words;
+                    const uint16_t* e = l1 + (int64_t)((i1 * kN16G1 + j1) * kN16G1 + k1) * l1w;
                     if (e[0] != kN16Ovf) lst = e;
                 }
                 bk = argmin16_fix(r[u], g[u], b[u], slow, bk, lst, s_pal, K);
@@ -475,6 +506,8 @@ hipError_t launch_assign16(const AssignArgs& a0, int P, hipStream_t s) {
     return hipGetLastError();
 }
 
+template __global__ void lists16_kernel<true>(Lists16Args);
+template __global__ void lists16_kernel<false>(Lists16Args);
 template __global__ void assign16_kernel<true>(AssignArgs, int);
 template __global__ void assign16_kernel<false>(AssignArgs, int);
 

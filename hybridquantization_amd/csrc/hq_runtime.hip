@@ -428,10 +428,10 @@ int assign_blocks(const hq_ctx* c, int P) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(nblocks, (c->g.n_ext + chunk - 1) / chunk));
 }
 
-// Chunked palettes of 8 or 16 chunks take the native 16-bit lists (option lists16).
+// Chunked palettes of 8 to 32 chunks take the native 16-bit lists (option lists16).
 bool use_lists16(const hq_ctx* c) {
     const int min_nch = c->lists16 >= 2 ? 2 : kN16MinNch;  // (2: also 2 and 4 chunks)
-    return c->lists16 > 0 && c->G2 > 0 && c->nch_cur >= min_nch && c->nch_cur <= kMaxNchFast;
+    return c->lists16 > 0 && c->G2 > 0 && c->nch_cur >= min_nch && c->nch_cur <= kN16MaxNch;
 }
 
 // Ensure population buffers for P palettes of K colours.
@@ -441,7 +441,7 @@ int ensure_population(hq_ctx* c, int P, int K) {
         HIP_TRY(c, c->d_idx16.ensure(sizeof(uint16_t) * (size_t)P * g.idx_pitch + 256));
         if (c->nch_cur > 4) HIP_TRY(c, c->d_dist.ensure(sizeof(float) * (size_t)P * g.idx_pitch));
         if (use_lists16(c)) {
-            HIP_TRY(c, c->d_l1n.ensure(sizeof(uint16_t) * kN16L1Words * (size_t)P * kN16G1 * kN16G1 * kN16G1));
+            HIP_TRY(c, c->d_l1n.ensure(sizeof(uint16_t) * kN16L1WordsMax * (size_t)P * kN16G1 * kN16G1 * kN16G1));
             HIP_TRY(c, c->d_l2n.ensure(sizeof(uint16_t) * kN16L2Words * (size_t)P * kN16G2 * kN16G2 * kN16G2));
         }
         P *= c->nch_cur;  // (d_out, h_out: P nch (1 + 256) >= P (1 + K) doubles)
@@ -1528,10 +1528,12 @@ int hq_search_create(hq_ctx* c, const hq_swasa_params* params, int K, uint64_t s
     *out = nullptr;
     if (params->population < 1 || params->imax < 1 || params->iTc < 1 || K < 1)
         return fail(c, HQ_ERR_ARG, "bad SWASA parameters");
-    // device-resident: K <= 256, or chunked palettes (256 < K <= 16384) of at most
-    // kSaMaxP sub-palettes in all
+    // device-resident: K <= 256, or chunked palettes (256 < K <= 16384); at most
+    // kSaMaxP palettes (sa_step's per-palette tables) and kSaMaxSub sub-palettes
+    // (its fold reads 8 used words per sub-palette, at most 4 per thread)
     const int nch = K > kMaxK && K <= kMaxKChunked && c->chunked && c->G2 > 0 ? chunk_count(K) : 1;
-    const bool device = c->sa_device && params->population * nch <= kSaMaxP && (K <= kMaxK || nch > 1);
+    const bool device = c->sa_device && params->population <= kSaMaxP && params->population * nch <= kSaMaxSub &&
+                        (K <= kMaxK || nch > 1);
     hq_search* s = new hq_search{c, nullptr, K};
     int rc;
     if (device) {

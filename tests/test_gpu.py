@@ -608,7 +608,8 @@ def test_chunked_palettes_match_exhaustive(gpu, filt, K):
     m.close()
 
 
-@pytest.mark.parametrize("K,img_u8,mode", [(2048, 1, 1), (4096, 0, 1), (1500, 1, 1), (600, 1, 2), (300, 0, 2)])
+@pytest.mark.parametrize("K,img_u8,mode", [(2048, 1, 1), (4096, 0, 1), (1500, 1, 1), (600, 1, 2), (300, 0, 2),
+                                            (8192, 1, 1), (6000, 0, 1)])
 def test_lists16_match_chunked_and_exhaustive(gpu, filt, K, img_u8, mode):
     """The native 16-bit candidate lists (option lists16, default for 8 and 16
     chunks: one grid over all K colours, hq_lists16.hip) against the per-chunk
@@ -830,7 +831,7 @@ def test_search_matches_host_driver_on_oracle_costs(ip, filt):
     np.testing.assert_array_equal(best, hbest)
 
 
-@pytest.mark.parametrize("P,K", [(1, 16), (3, 16), (4, 16), (2, 600), (3, 1500)])
+@pytest.mark.parametrize("P,K", [(1, 16), (3, 16), (4, 16), (2, 600), (3, 1500), (4, 5000), (2, 8192)])
 def test_device_search_matches_host_driven(gpu, filt, P, K):
     """The device-resident SWASA loop (sa_step_kernel: acceptance, convergence,
     java.util.Random draws by jump table, neighbour generation) follows the
