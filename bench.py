@@ -85,12 +85,12 @@ def cost_accounting(half, K, grid, opts):
     variant = int(opts.get("cost_variant", 0))
     hb = next((b for b in (10, 15, 19, 24) if half <= b), 0)
     # K <= 256: u8 indices; 256 < K <= 16384: chunked palettes, 16-bit indices, the
-    # tiled kernel at HB = 10 with 16 x 128 tiles only, up to 16 chunks; above: 32-bit indices
+    # tiled kernel at HB = 10 with 16 x 128 tiles only, up to 32 chunks; above: 32-bit indices
     chunked = 256 < K <= 16384 and int(opts.get("chunked", 1)) != 0 and grid > 0
     nch = 1 << max(0, (K - 1).bit_length() - 8) if chunked else 1  # chunk_count: 256-colour chunks
     tw_opt = int(opts.get("cost_tw", 128))
     generic = (variant != 0 or hb == 0 or (K > 256 and not chunked)
-               or (chunked and (hb != 10 or rows != 16 or tw_opt != 128 or nch > 16)))
+               or (chunked and (hb != 10 or rows != 16 or tw_opt != 128 or nch > 32)))
     trim_w = {10: (3, 4, 5), 15: (4, 5, 7), 19: (5, 7, 9), 24: (6, 9, 12)}
     if generic:
         # cost_variant 2: the per-pixel pair; otherwise the LDS-tiled pair

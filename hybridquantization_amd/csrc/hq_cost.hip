@@ -783,10 +783,10 @@ __device__ __forceinline__ void vblock_any(const uint32_t (&w)[NJ], const uint4 
 #endif
 // occupancy per bucket: LDS allows 4 workgroups per CU at HB = 10, 3 above;
 // chunked palettes (NCH > 1: 16-bit indices, a table of 256 NCH entries): 3 up
-// to 1,024 colours, 2 above
+// to 1,024 colours, 2 up to 4,096, 1 above (the 64 KiB table at 8,192)
 template <int HB, int NCH = 1>
 constexpr int cost16w_waves() {
-    return NCH > 4 ? 2 : NCH > 1 ? 3 : HB == 10 ? 4 : HB == 15 ? HQ_LB15 : HB == 19 ? HQ_LB19 : HQ_LB24;
+    return NCH > 16 ? 1 : NCH > 4 ? 2 : NCH > 1 ? 3 : HB == 10 ? 4 : HB == 15 ? HQ_LB15 : HB == 19 ? HQ_LB19 : HQ_LB24;
 }
 
 // NCH > 1 (chunked palettes, 256 < K <= 256 NCH; HB = 10): the index image is
@@ -2087,6 +2087,7 @@ hipError_t launch_cost_chunked(const CostArgs& a, int P, int nch, int de, bool t
     case 4: launch_cost16w_chunked<4>(a, P, de, trim, s); break;
     case 8: launch_cost16w_chunked<8>(a, P, de, trim, s); break;
     case 16: launch_cost16w_chunked<16>(a, P, de, trim, s); break;
+    case 32: launch_cost16w_chunked<32>(a, P, de, trim, s); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -10,7 +10,10 @@ namespace hq {
 constexpr int kMaxK = 256;        // u8 palette indices (K <= 256 on the tiled path)
 constexpr int kMaxKWide = 1 << 24;  // K > 256: 32-bit indices (the plugin's limit, HQ:192)
 constexpr int kMaxKChunked = 16384;  // 256 < K <= 16384: palettes as 256-colour chunks, 16-bit indices
-constexpr int kMaxNchFast = 16;      // chunked palettes of up to 16 chunks run the tiled cost kernel
+#ifndef HQ_MAX_NCH_FAST
+#define HQ_MAX_NCH_FAST 32
+#endif
+constexpr int kMaxNchFast = HQ_MAX_NCH_FAST;  // chunked palettes of up to 32 chunks run the tiled cost kernel
 // chunks of a palette of K colours on the chunked path: a power of two (2 .. 64)
 inline int chunk_count(int K) {
     int n = 1;

@@ -178,7 +178,7 @@ struct hq_ctx {
                            // "palette_split"; SURVEY 8e's split of large populations)
     int slice_ranks = 1, slice_rank = 0;  // test only: the same slice without a communicator
     int slice_lo = 0, slice_n = 0;        // the last evaluation's palettes held on this device
-    int lists16 = 1;       // native 16-bit candidate lists: 1 = chunked palettes of 8 or 16 chunks, 2 = 2 .. 16
+    int lists16 = 1;       // native 16-bit candidate lists: 1 = chunked palettes of 8 to 32 chunks, 2 = 2 .. 32
     int chunked = 1;       // 256 < K <= 16384: palettes as 256-colour chunks through the grid and
                            // tiled kernels (option "chunked"; 0 = the exhaustive K > 256 path)
     int img_u8_path = 1;   // assign reads the packed 8-bit image when there is one (option 'img_u8')
@@ -864,7 +864,7 @@ int eval_partial_into_hout(hq_ctx* c, const float* palettes, int P, int K) {
     if ((rc = bind(c))) return rc;
     const bool fits = palette_fits_fast(palettes, P, K);
     // 256 < K <= 16384: chunks of 256 colours through the grid and assign, and the
-    // tiled cost kernel up to 16 chunks (the generic pair above).  Palettes outside
+    // tiled cost kernel up to 32 chunks (the generic pair above).  Palettes outside
     // the fast range (non-finite colours among
     // them) take the exhaustive K > 256 path instead, which keeps the
     // reference's NaN semantics across all K colours.

@@ -109,7 +109,7 @@ int hq_get_labref(hq_ctx *ctx, float *lab4);
  * argmin and the tiled fast stencil.  256 < K <= 16384: chunked palettes (nch
  * sub-palettes of 256, 16-bit indices; 1024 < K <= 8192: one grid of 16-bit
  * candidate lists over all K colours, option "lists16", otherwise a grid and
- * assign pass per chunk; the fast stencil up to K = 4096, the generic one
+ * assign pass per chunk; the fast stencil up to K = 8192, the generic one
  * above; option "chunked").  K > 16384,
  * palettes with non-finite colours or
  * outside the fast path's range, option "chunked" 0 or "grid" 0: the exhaustive

@@ -23,7 +23,8 @@ def test_viewing_geometries_and_palette_sizes():
     assert bench.cost_accounting(10, 256, 32, {"cost_rows": 8})[0] == "cost_mfma_kernel"
     assert bench.cost_accounting(10, 1024, 32, {})[:3] == ("cost16w_kernel", 10, True)  # chunked
     assert bench.cost_accounting(19, 1024, 32, {})[1] == 0  # chunked runs HB = 10 only
-    assert bench.cost_accounting(10, 5000, 32, {})[:3] == ("gen_hmfma_kernel+gen_vmfma_kernel", 0, True)  # 32 chunks
+    assert bench.cost_accounting(10, 5000, 32, {})[:3] == ("cost16w_kernel", 10, True)  # 32 chunks
+    assert bench.cost_accounting(10, 10000, 32, {})[:3] == ("gen_hmfma_kernel+gen_vmfma_kernel", 0, True)  # 64
     assert bench.cost_accounting(10, 20000, 32, {})[:3] == ("gen_hmfma_kernel+gen_vmfma_kernel", 0, False)
     assert bench.cost_accounting(70, 256, 32, {})[0] == "gen_hrow4_kernel+gen_vtile_kernel"  # half > 64
     assert bench.cost_accounting(51, 256, 32, {"gen_hmfma": 0})[0] == "gen_hrow4_kernel+gen_vmfma_kernel"
