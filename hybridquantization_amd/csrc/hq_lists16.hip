@@ -199,7 +199,12 @@ __global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
         const int J2 = 16 * C0j + 4 * ((ch >> 2) & 3) + ((sub >> 2) & 3);
         const int L2 = 16 * C0k + 4 * (ch & 3) + (sub & 3);
         const float lo2[3] = {(float)I2 * w2, (float)J2 * w2, (float)L2 * w2};
-        uint16_t* out = a.lvl2 + ((int64_t)p * (kN16G2 * kN16G2 * kN16G2) + (I2 * kN16G2 + J2) * kN16G2 + L2) * kN16L2Words;
+        // up to K = 4096 palette pairs interleaved per cell (one 64-B line holds
+        // both entries: assign16 takes two palettes per workgroup); above, a table
+        // per palette
+        const int64_t cell2 = (I2 * kN16G2 + J2) * kN16G2 + L2, n2 = kN16G2 * kN16G2 * kN16G2;
+        uint16_t* out = a.lvl2 + (a.K <= 4096 ? ((((int64_t)(p >> 1) * n2 + cell2) << 1) + (p & 1))
+                                              : (int64_t)p * n2 + cell2) * kN16L2Words;
         if (exh) {
             out[0] = kN16Ovf;
             continue;
@@ -368,34 +373,48 @@ __device__ __forceinline__ uint32_t u16_at(const uint4 (&E)[NQ], int j) {
     return (j & 1) ? v >> 16 : v & 0xffffu;
 }
 
-template <bool U8>
+// NPAL palettes per workgroup (2 up to K = 4096: both tables in LDS, one 64-B
+// level-2 line per pixel for both, the pixel read once), batches of 4 / NPAL
+// pixels per thread.
+template <bool U8, int NPAL>
 __global__ __launch_bounds__(kN16Threads) void assign16_kernel(AssignArgs a, int P) {
-    extern __shared__ float4 s_pal[];  // [K]
-    const int w = xcd_remap(blockIdx.x, a.nblocks * P);
-    const int p = w / a.nblocks, blk = w % a.nblocks, tid = threadIdx.x, K = a.K;
-    const float4* pal = a.pal + (int64_t)p * a.kpal;
-    for (int i = tid; i < K; i += kN16Threads) s_pal[i] = pal[i];
-    bool exh = false;
-    for (int j = 0; j < a.nch; ++j) exh |= a.pflags[p * a.nch + j] != 0;
+    extern __shared__ float4 s_pal[];  // [NPAL][K]
+    constexpr int KB = 4 / NPAL;
+    const int npr = (P + NPAL - 1) / NPAL;
+    const int w = xcd_remap(blockIdx.x, a.nblocks * npr);
+    const int pr = w / a.nblocks, blk = w % a.nblocks, tid = threadIdx.x, K = a.K;
+    const int p0 = NPAL * pr, np = min(NPAL, P - p0);
+    bool exh[NPAL];
+    uint16_t* idx[NPAL];
+#pragma unroll
+    for (int q = 0; q < NPAL; ++q) {
+        const int p = min(p0 + q, P - 1);
+        const float4* pal = a.pal + (int64_t)p * a.kpal;
+        for (int i = tid; i < K; i += kN16Threads) s_pal[q * K + i] = pal[i];
+        exh[q] = false;
+        for (int j = 0; j < a.nch; ++j) exh[q] |= a.pflags[p * a.nch + j] != 0;
+        idx[q] = a.idx16 + (int64_t)p * a.idx_pitch;
+    }
     __syncthreads();
-    const uint4* l2 = reinterpret_cast<const uint4*>(a.l2n + (int64_t)p * (kN16G2 * kN16G2 * kN16G2) * kN16L2Words);
+    // NPAL 2: the pair's level-2 lines (4 x 16 B per cell), palette p0 + q at
+    // uint4 2 q; NPAL 1: the palette's own table (2 x 16 B per cell)
+    const uint4* l2 = reinterpret_cast<const uint4*>(a.l2n) +
+                      (int64_t)(NPAL == 2 ? p0 >> 1 : p0) * (kN16G2 * kN16G2 * kN16G2) * (2 * NPAL);
     const int l1w = n16_l1_words(K);
-    const uint16_t* l1 = a.l1n + (int64_t)p * (kN16G1 * kN16G1 * kN16G1) * l1w;
-    uint16_t* idx = a.idx16 + (int64_t)p * a.idx_pitch;
     const uint32_t n_ext = (uint32_t)a.n_ext, qlast = n_ext - 1;
     const uint32_t cstride = (uint32_t)a.nblocks * (uint32_t)kN16Threads;
     const uint32_t qbase = (uint32_t)blk * (uint32_t)kN16Threads + (uint32_t)tid;
     // every lane runs its lane 0's batch count (argmin16_fix needs the whole wave)
     const int npx0 = qbase < n_ext ? (int)((n_ext - 1 - qbase) / cstride) + 1 : 0;
-    const int nb = __builtin_amdgcn_readfirstlane((npx0 + kA16B - 1) / kA16B);
+    const int nb = __builtin_amdgcn_readfirstlane((npx0 + KB - 1) / KB);
     // the next batch's pixels are loaded while this batch's entries are looked
     // up and walked: one exposed memory round trip per batch, not two
-    uint32_t nv[kA16B];          // packed bytes (U8)
-    float nr[kA16B], ng[kA16B], nbl[kA16B];  // planar floats
+    uint32_t nv[KB];          // packed bytes (U8)
+    float nr[KB], ng[KB], nbl[KB];  // planar floats
     auto load_batch = [&](int bi) {
 #pragma unroll
-        for (int u = 0; u < kA16B; ++u) {
-            const uint32_t qc = min(qbase + (uint32_t)(bi * kA16B + u) * cstride, qlast);
+        for (int u = 0; u < KB; ++u) {
+            const uint32_t qc = min(qbase + (uint32_t)(bi * KB + u) * cstride, qlast);
             if constexpr (U8) {
                 nv[u] = a.rgbx[qc];
             } else {
@@ -407,11 +426,11 @@ __global__ __launch_bounds__(kN16Threads) void assign16_kernel(AssignArgs a, int
     };
     if (nb > 0) load_batch(0);
     for (int bi = 0; bi < nb; ++bi) {
-        float r[kA16B], g[kA16B], b[kA16B];
-        uint32_t q[kA16B];
+        float r[KB], g[KB], b[KB];
+        uint32_t q[KB];
 #pragma unroll
-        for (int u = 0; u < kA16B; ++u) {
-            q[u] = qbase + (uint32_t)(bi * kA16B + u) * cstride;
+        for (int u = 0; u < KB; ++u) {
+            q[u] = qbase + (uint32_t)(bi * KB + u) * cstride;
             if constexpr (U8) {
                 r[u] = u8_unit(nv[u], 0);
                 g[u] = u8_unit(nv[u], 1);
@@ -422,21 +441,27 @@ __global__ __launch_bounds__(kN16Threads) void assign16_kernel(AssignArgs a, int
                 b[u] = nbl[u];
             }
         }
-        bool in_[kA16B];
+        bool in_[KB];
         constexpr int NQ = kN16L2Words / 8;  // 16-B pieces per entry
-        uint4 E[kA16B][NQ];
+        uint4 E[KB][NPAL][NQ];
 #pragma unroll
-        for (int u = 0; u < kA16B; ++u) {
+        for (int u = 0; u < KB; ++u) {
             in_[u] = r[u] >= 0.f && r[u] <= 1.f && g[u] >= 0.f && g[u] <= 1.f && b[u] >= 0.f && b[u] <= 1.f;
             const uint32_t cell = in_[u] ? (uint32_t)quad_cell16(r[u], g[u], b[u]) : 0u;
 #pragma unroll
-            for (int qq = 0; qq < NQ; ++qq) E[u][qq] = l2[NQ * cell + qq];
+            for (int pq = 0; pq < NPAL; ++pq)
+#pragma unroll
+                for (int qq = 0; qq < NQ; ++qq) E[u][pq][qq] = l2[2 * NPAL * cell + 2 * pq + qq];
         }
         if (bi + 1 < nb) load_batch(bi + 1);
 #pragma unroll
-        for (int u = 0; u < kA16B; ++u) {
-            const uint32_t c = E[u][0].x & 0xffffu;
-            const bool slow = !in_[u] || exh || c == kN16Ovf || c == 0u;
+        for (int u = 0; u < KB; ++u)
+#pragma unroll
+        for (int pq = 0; pq < NPAL; ++pq) {
+            if (pq >= np) break;  // (workgroup-uniform: the last pair of an odd population)
+            const float4* sp = s_pal + pq * K;
+            const uint32_t c = E[u][pq][0].x & 0xffffu;
+            const bool slow = !in_[u] || exh[pq] || c == kN16Ovf || c == 0u;
             const int cnt = slow ? 0 : (int)c;
             // ranked by d^2 (dist2_rank: within 3 ulp of dist2); a runner-up within
             // 1e-6 relative is a possible sqrtf tie: re-resolved over the list below
@@ -445,8 +470,8 @@ __global__ __launch_bounds__(kN16Threads) void assign16_kernel(AssignArgs a, int
 #pragma unroll
             for (int i = 0; i < kN16L2Cap; ++i) {
                 if (!HQ_ANY16(i < cnt)) break;
-                const int k = (int)u16_at(E[u], i + 1);
-                const float d2 = i < cnt ? dist2_rank(r[u], g[u], b[u], s_pal[i < cnt ? k : 0]) : INFINITY;
+                const int k = (int)u16_at(E[u][pq], i + 1);
+                const float d2 = i < cnt ? dist2_rank(r[u], g[u], b[u], sp[i < cnt ? k : 0]) : INFINITY;
                 const bool lt = d2 < best2;
                 second2 = __builtin_amdgcn_fmed3f(best2, second2, d2);
                 bk = lt ? k : bk;
@@ -458,8 +483,8 @@ __global__ __launch_bounds__(kN16Threads) void assign16_kernel(AssignArgs a, int
                     float bd = INFINITY;
                     int bkk = 0x7fffffff;
                     for (int i = 0; i < cnt; ++i) {
-                        const int k = (int)u16_at(E[u], i + 1);
-                        const float d = sqrtf(dist2(r[u], g[u], b[u], s_pal[k]));
+                        const int k = (int)u16_at(E[u][pq], i + 1);
+                        const float d = sqrtf(dist2(r[u], g[u], b[u], sp[k]));
                         if (d < bd || (d == bd && k < bkk)) {
                             bd = d;
                             bkk = k;
@@ -471,16 +496,17 @@ __global__ __launch_bounds__(kN16Threads) void assign16_kernel(AssignArgs a, int
             if (HQ_ANY16(slow)) {
                 // the level-1 list of the pixel's cell when it has one
                 const uint16_t* lst = nullptr;
-                if (in_[u] && !exh) {
+                if (in_[u] && !exh[pq]) {
                     const int i1 = min((int)(r[u] * (float)kN16G1), kN16G1 - 1);
                     const int j1 = min((int)(g[u] * (float)kN16G1), kN16G1 - 1);
                     const int k1 = min((int)(b[u] * (float)kN16G1), kN16G1 - 1);
-                    const uint16_t* e = l1 + (int64_t)((i1 * kN16G1 + j1) * kN16G1 + k1) * l1w;
+                    const uint16_t* e = a.l1n + ((int64_t)(p0 + pq) * (kN16G1 * kN16G1 * kN16G1) +
+                                                 (i1 * kN16G1 + j1) * kN16G1 + k1) * l1w;
                     if (e[0] != kN16Ovf) lst = e;
                 }
-                bk = argmin16_fix(r[u], g[u], b[u], slow, bk, lst, s_pal, K);
+                bk = argmin16_fix(r[u], g[u], b[u], slow, bk, lst, sp, K);
             }
-            if (q[u] < n_ext) __builtin_nontemporal_store((uint16_t)bk, idx + q[u]);
+            if (q[u] < n_ext) __builtin_nontemporal_store((uint16_t)bk, idx[pq] + q[u]);
         }
     }
 }
@@ -493,12 +519,20 @@ hipError_t launch_assign16(const AssignArgs& a0, int P, hipStream_t s) {
     const hipEvent_t ev0 = t_ev_start, ev1 = t_ev_stop;
     AssignArgs a = a0;
     t_ev_stop = nullptr;
-    const size_t lds = sizeof(float4) * (size_t)a.K;
-    allow_lds16(reinterpret_cast<const void*>(assign16_kernel<true>), lds);
-    allow_lds16(reinterpret_cast<const void*>(assign16_kernel<false>), lds);
-    const dim3 grid((unsigned)(a.nblocks * P));
-    if (a.rgbx) HQ_LAUNCH(assign16_kernel<true>, grid, dim3(kN16Threads), lds, s, a, P);
-    else HQ_LAUNCH(assign16_kernel<false>, grid, dim3(kN16Threads), lds, s, a, P);
+    const int npal = a.K <= 4096 ? 2 : 1;  // two 64 KiB tables fit one workgroup up to K = 4096
+    const size_t lds = sizeof(float4) * (size_t)a.K * npal;
+    const dim3 grid((unsigned)(a.nblocks * ((P + npal - 1) / npal)));
+    auto go = [&](auto kern) {
+        allow_lds16(reinterpret_cast<const void*>(kern), lds);
+        HQ_LAUNCH(kern, grid, dim3(kN16Threads), lds, s, a, P);
+    };
+    if (npal == 2) {
+        if (a.rgbx) go(assign16_kernel<true, 2>);
+        else go(assign16_kernel<false, 2>);
+    } else {
+        if (a.rgbx) go(assign16_kernel<true, 1>);
+        else go(assign16_kernel<false, 1>);
+    }
     t_ev_start = nullptr;
     t_ev_stop = ev1;
     launch_used_idx16(a, P, s);
@@ -508,7 +542,9 @@ hipError_t launch_assign16(const AssignArgs& a0, int P, hipStream_t s) {
 
 template __global__ void lists16_kernel<true>(Lists16Args);
 template __global__ void lists16_kernel<false>(Lists16Args);
-template __global__ void assign16_kernel<true>(AssignArgs, int);
-template __global__ void assign16_kernel<false>(AssignArgs, int);
+template __global__ void assign16_kernel<true, 1>(AssignArgs, int);
+template __global__ void assign16_kernel<false, 1>(AssignArgs, int);
+template __global__ void assign16_kernel<true, 2>(AssignArgs, int);
+template __global__ void assign16_kernel<false, 2>(AssignArgs, int);
 
 }  // namespace hq

@@ -442,7 +442,8 @@ int ensure_population(hq_ctx* c, int P, int K) {
         if (c->nch_cur > 4) HIP_TRY(c, c->d_dist.ensure(sizeof(float) * (size_t)P * g.idx_pitch));
         if (use_lists16(c)) {
             HIP_TRY(c, c->d_l1n.ensure(sizeof(uint16_t) * kN16L1WordsMax * (size_t)P * kN16G1 * kN16G1 * kN16G1));
-            HIP_TRY(c, c->d_l2n.ensure(sizeof(uint16_t) * kN16L2Words * (size_t)P * kN16G2 * kN16G2 * kN16G2));
+            // (palette pairs interleaved: an odd population's last pair half empty)
+            HIP_TRY(c, c->d_l2n.ensure(sizeof(uint16_t) * kN16L2Words * (size_t)(P + 1) / 2 * 2 * kN16G2 * kN16G2 * kN16G2));
         }
         P *= c->nch_cur;  // (d_out, h_out: P nch (1 + 256) >= P (1 + K) doubles)
         K = kMaxK;
@@ -704,8 +705,9 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
         aa.kpal = nch * kMaxK;
         aa.K = K;
         // one resident round of 1024-thread workgroups over the P palettes, >= 4 pixels per thread
+        const int ngr = K <= 4096 ? (Pl + 1) / 2 : Pl;  // workgroup groups: palette pairs up to K = 4096
         aa.nblocks = (int)std::max<int64_t>(
-            1, std::min<int64_t>(std::max(1, c->num_cu / Pl), (g.n_ext + 4095) / 4096));
+            1, std::min<int64_t>(std::max(1, c->num_cu / ngr), (g.n_ext + 4095) / 4096));
     }
     const float inv[3] = {1.0f / c->illum[0], 1.0f / c->illum[1], 1.0f / c->illum[2]};
     // chunked palettes: the 16 x 128 tiles at HB = 10 (else the generic path)
