@@ -138,8 +138,8 @@ struct GridArgs {
     int nch;                // sub-palettes per palette (chunked palettes), else 1
 };
 
-// Native 16-bit candidate lists (hq_lists16.hip) for chunked palettes of 8 to
-// 32 chunks (1024 < K <= 8192): one grid over all K colours, level 1 at 16^3
+// Native 16-bit candidate lists (hq_lists16.hip) for chunked palettes of 4 to
+// 32 chunks (512 < K <= 8192): one grid over all K colours, level 1 at 16^3
 // cells (u16 count + 127 or 255 indices), level 2 at 64^3 (u16 count + 15
 // indices, 32 B); count kN16Ovf = overflow.
 constexpr int kN16G2 = 64, kN16G1 = kN16G2 / 4, kN16G0 = kN16G1 / 4;
@@ -149,7 +149,7 @@ constexpr int kN16L2Cap = 15, kN16L2Words = kN16L2Cap + 1;  // u16 per entry
 constexpr int kN16L1WordsMax = 256;
 __host__ __device__ constexpr int n16_l1_words(int K) { return K > 4096 ? 256 : 128; }
 constexpr uint16_t kN16Ovf = 0xffff;
-constexpr int kN16MinNch = 8;   // chunk counts that take the native lists (option "lists16") ...
+constexpr int kN16MinNch = 4;   // chunk counts that take the native lists (option "lists16") ...
 constexpr int kN16MaxNch = 32;  // ... up to K = 8192: the palette's 128 KiB table in assign16's LDS
 constexpr int kN16MaxK = 256 * kN16MaxNch;
 

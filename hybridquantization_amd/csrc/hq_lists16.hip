@@ -1,5 +1,5 @@
-// hq_lists16.hip -- native 16-bit candidate lists for chunked palettes of 8 to
-// 32 chunks (1024 < K <= 8192).  The chunked path (hq_assign.hip) runs one
+// hq_lists16.hip -- native 16-bit candidate lists for chunked palettes of 4 to
+// 32 chunks (512 < K <= 8192).  The chunked path (hq_assign.hip) runs one
 // grid per 256-colour chunk and nch / 4 assign passes that carry the best
 // distance so far through a scratch image: 16 lookups and list walks per pixel
 // at K = 4096.  Here one grid covers all K colours at a finer level 2 (64^3

@@ -178,7 +178,7 @@ struct hq_ctx {
                            // "palette_split"; SURVEY 8e's split of large populations)
     int slice_ranks = 1, slice_rank = 0;  // test only: the same slice without a communicator
     int slice_lo = 0, slice_n = 0;        // the last evaluation's palettes held on this device
-    int lists16 = 1;       // native 16-bit candidate lists: 1 = chunked palettes of 8 to 32 chunks, 2 = 2 .. 32
+    int lists16 = 1;       // native 16-bit candidate lists: 1 = chunked palettes of 4 to 32 chunks, 2 = 2 .. 32
     int chunked = 1;       // 256 < K <= 16384: palettes as 256-colour chunks through the grid and
                            // tiled kernels (option "chunked"; 0 = the exhaustive K > 256 path)
     int img_u8_path = 1;   // assign reads the packed 8-bit image when there is one (option 'img_u8')
@@ -428,7 +428,7 @@ int assign_blocks(const hq_ctx* c, int P) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(nblocks, (c->g.n_ext + chunk - 1) / chunk));
 }
 
-// Chunked palettes of 8 to 32 chunks take the native 16-bit lists (option lists16).
+// Chunked palettes of 4 to 32 chunks take the native 16-bit lists (option lists16).
 bool use_lists16(const hq_ctx* c) {
     const int min_nch = c->lists16 >= 2 ? 2 : kN16MinNch;  // (2: also 2 and 4 chunks)
     return c->lists16 > 0 && c->G2 > 0 && c->nch_cur >= min_nch && c->nch_cur <= kN16MaxNch;

@@ -107,7 +107,7 @@ int hq_get_labref(hq_ctx *ctx, float *lab4);
 /* IM:620 computeQuantizationErrorPopulation for P palettes of K colours
  * (K in [1, 2^24] as the plugin allows, HQ:192).  K <= 256: the pruned grid
  * argmin and the tiled fast stencil.  256 < K <= 16384: chunked palettes (nch
- * sub-palettes of 256, 16-bit indices; 1024 < K <= 8192: one grid of 16-bit
+ * sub-palettes of 256, 16-bit indices; 512 < K <= 8192: one grid of 16-bit
  * candidate lists over all K colours, option "lists16", otherwise a grid and
  * assign pass per chunk; the fast stencil up to K = 8192, the generic one
  * above; option "chunked").  K > 16384,
@@ -218,7 +218,7 @@ int hq_profile_reset(hq_ctx *ctx);
  *                  (4 row tiles per gen_hmfma workgroup and 128-row gen_vmfma tiles on large
  *                  images), 1 the short forms, 2 the tall forms (same results within the split bars)
  *   "lists16"      chunked palettes: native 16-bit candidate lists (one grid over all K
- *                  colours, one lookup per pixel): 1 (default) for 8 to 32 chunks (1024 < K
+ *                  colours, one lookup per pixel): 1 (default) for 4 to 32 chunks (512 < K
  *                  <= 8192), 2 for 2 .. 32 chunks, 0 = a grid and assign pass per chunk
  *   "gen_vtile2"   the LDS-tiled generic path's vertical pass (halfSize <= 64): 1 (default) =
  *                  32 x 64 tiles, windows double-buffered by LDS DMA; 0 = 64 x 64 tiles with
