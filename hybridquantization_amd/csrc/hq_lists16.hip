@@ -233,18 +233,24 @@ __global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
                 const float tx = fabsf(x - m0) + h2, ty = fabsf(y - m1) + h2, tz = fabsf(z - m2) + h2;
                 return fmaf(tz, tz, fmaf(ty, ty, tx * tx));
             };
+            // (the clamp to [0, 1] is the add's clamp bit, not a v_max; a term
+            // above 1 -- a colour outside the unit cube -- only lowers the bound)
             auto bmin = [&](float x, float y, float z) {
-                const float tx = fmaxf(fabsf(x - m0) - h2, 0.f), ty = fmaxf(fabsf(y - m1) - h2, 0.f),
-                            tz = fmaxf(fabsf(z - m2) - h2, 0.f);
+                const float tx = __builtin_amdgcn_fmed3f(fabsf(x - m0) - h2, 0.f, 1.f),
+                            ty = __builtin_amdgcn_fmed3f(fabsf(y - m1) - h2, 0.f, 1.f),
+                            tz = __builtin_amdgcn_fmed3f(fabsf(z - m2) - h2, 0.f, 1.f);
                 return fmaf(tz, tz, fmaf(ty, ty, tx * tx));
             };
-            float t2 = INFINITY;
+            // the least bmax as an unsigned min of the bit patterns (bmax >= +0,
+            // finite): fminf canonicalised the running minimum every iteration
+            uint32_t t2u = 0x7f800000u;
 #pragma unroll
             for (int j = 0; j < NSL; ++j) {
                 const int nj = min(c1 - 64 * j, 64);
-                for (int i = 0; i < nj; ++i) t2 = fminf(t2, bmax(rl(cs[j].x, i), rl(cs[j].y, i), rl(cs[j].z, i)));
+                for (int i = 0; i < nj; ++i)
+                    t2u = min(t2u, __builtin_bit_cast(uint32_t, bmax(rl(cs[j].x, i), rl(cs[j].y, i), rl(cs[j].z, i))));
             }
-            const float thr2 = t2 * HQ_CAND_MARGIN;
+            const float thr2 = __builtin_bit_cast(float, t2u) * HQ_CAND_MARGIN;
 #pragma unroll
             for (int j = 0; j < NSL; ++j) {
                 const int nj = min(c1 - 64 * j, 64);
@@ -299,9 +305,8 @@ hipError_t launch_lists16_grid(const Lists16Args& a, int P, hipStream_t s) {
 // assign16: grid (nblocks * P), block 1024 (16 waves share the 64 KiB table:
 // 256-thread workgroups left one wave per SIMD), XCD-relabelled
 // palette-major; the palette in LDS.  A thread's pixels are a grid stride, resolved in batches of
-// kA16B: every RGB load of the batch, then every level-2 entry, then the walks.
+// 4 / NPAL: every RGB load of the batch, then every level-2 entry, then the walks.
 // ----------------------------------------------------------------------------
-constexpr int kA16B = 4;
 #define HQ_ANY16(c) (__builtin_amdgcn_ballot_w64(c) != 0)
 // level-2 cell (64^3) of a pixel in the unit cube; its level-1 cell (16^3) is
 // each coordinate >> 2 (floor(64 x) / 4 = floor(16 x): exact scalings)

@@ -611,15 +611,17 @@ def test_chunked_palettes_match_exhaustive(gpu, filt, K):
 @pytest.mark.parametrize("K,img_u8,mode", [(2048, 1, 1), (4096, 0, 1), (1500, 1, 1), (600, 1, 2), (300, 0, 2),
                                             (8192, 1, 1), (6000, 0, 1)])
 def test_lists16_match_chunked_and_exhaustive(gpu, filt, K, img_u8, mode):
-    """The native 16-bit candidate lists (option lists16, default for 8 and 16
+    """The native 16-bit candidate lists (option lists16, default from 4 to 32
     chunks: one grid over all K colours, hq_lists16.hip) against the per-chunk
     grids (lists16 0) and the exhaustive path (chunked 0): indices bit for bit,
     used flags equal, costs within 1e-6.  Palette 0 is clustered -- every
     colour in a box of side 0.08 around a grey that many pixels sit in, so
     level-2 entries and level-1 lists overflow into their fallbacks (the
     pixel's level-1 list, all K colours) -- palette 1 uniform, palette 2 the
-    uniform one with duplicates across chunks; planar float pixels
-    (img_u8 0) and packed bytes.  Mode 2 takes 2 and 4 chunks too."""
+    uniform one with duplicates across chunks, palette 3 the uniform one
+    stretched to [-0.3, 1.3] (colours outside the unit cube: the level-2
+    lower bound's clamp); planar float pixels (img_u8 0) and packed bytes.
+    Mode 2 takes 2 chunks too."""
     w, h = 320, 200
     R, G, B = o.synthetic_image(w, h, seed=K)
     R[: h // 2] = np.clip(0.45 + 0.06 * (R[: h // 2] - 0.5), 0, 1)  # half the image near the cluster
@@ -634,7 +636,9 @@ def test_lists16_match_chunked_and_exhaustive(gpu, filt, K, img_u8, mode):
     dup = uni.copy()
     for c in range(1, K // 256):
         dup[256 * c + 3] = dup[3]
-    pals = np.stack([clus, uni, dup])
+    far = uni.copy()
+    far[:, :3] = (1.6 * far[:, :3] - 0.3).astype(np.float32)
+    pals = np.stack([clus, uni, dup, far])
     m = hq.ImageManipulation(device=gpu)
     hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
     m.setImage(rgba.reshape(-1), None, w, filt.illum)
@@ -644,11 +648,11 @@ def test_lists16_match_chunked_and_exhaustive(gpu, filt, K, img_u8, mode):
                        ("exh", {"lists16": 1, "chunked": 0})):
         for k, v in opts.items():
             m.setOption(k, v)
-        costs, used = m.computeQuantizationErrorPopulation(pals.reshape(3, -1), 2.0, return_used=True)
-        res[name] = (costs, used, [m.getIndices32(p) for p in range(3)])
+        costs, used = m.computeQuantizationErrorPopulation(pals.reshape(len(pals), -1), 2.0, return_used=True)
+        res[name] = (costs, used, [m.getIndices32(p) for p in range(len(pals))])
     m.close()
     for other in ("chunk", "exh"):
-        for p in range(3):
+        for p in range(len(pals)):
             np.testing.assert_array_equal(res["n16"][2][p], res[other][2][p])
             np.testing.assert_array_equal(res["n16"][1][p], res[other][1][p])
         np.testing.assert_allclose(res["n16"][0], res[other][0], rtol=1e-6)
