@@ -15,7 +15,8 @@
      defined(HQ_ABL_GRID_L1ONLY) || defined(HQ_ABL_TRUNC) || defined(HQ_ABL_NOFILL) ||                \
      defined(HQ_ABL_MFMA1) || defined(HQ_ABL_NOHPASS) || defined(HQ_ABL_NOVSTORE) ||                  \
      defined(HQ_ABL_NOMFMA) || defined(HQ_ABL_NOIDX) || defined(HQ_ABL_NOTAB) ||                      \
-     defined(HQ_ABL_NOLABLD) || defined(HQ_ABL_NOLAB) || defined(HQ_ABL_NORED))
+     defined(HQ_ABL_NOLABLD) || defined(HQ_ABL_NOLAB) || defined(HQ_ABL_NORED) ||                      \
+     defined(HQ_ABL_N16NOL2))
 #error "HQ_ABL_* ablations give wrong results: define HQ_ABLATION_BUILD as well to build one"
 #endif
 

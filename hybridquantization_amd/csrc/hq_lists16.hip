@@ -53,7 +53,7 @@ constexpr int kN16Threads = 1024;
 // SOA: the level-0 candidates as three float planes (12 B per colour: K =
 // 8192 fits beside the lists), else float4 (one ds_read_b128 each; the planes
 // cost K = 4096 1.4 us)
-template <bool SOA>
+template <bool SOA, bool TR>
 __global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
     constexpr int kN16L1Words = SOA ? 256 : 128, kN16L1Cap = kN16L1Words - 1;  // (n16_l1_words)
     // [K] float4 or [3][K] floats, then the colour indices (declared float4: the
@@ -188,9 +188,12 @@ __global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
         }
     }
     __syncthreads();
-    // level 2: wave wv takes parents wv + 16 j, its lane the child; the parent's
-    // list in registers (positions lane and lane + 64), each colour broadcast to
-    // the wave by readlane (no LDS in the loops)
+    // level 2: wave wv takes parents wv + 16 j; each lane writes the entry of
+    // child `lane`.  TR (K > 2048, long parent lists): the bounds formed with
+    // the lanes over the parent's list (transposed); else the lane the child,
+    // the list's colours broadcast by readlane (the transposed form's fixed
+    // cost -- 64 children per slot and a reduction -- is more than short
+    // lists' pairs: K = 1024 grid 34 -> 46 us with it, K = 4096 66 -> 60)
     const float w2 = 1.0f / kN16G2;
     auto rl = [](float x, int i) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), i)); };
     for (int j = 0; j < 4; ++j) {
@@ -205,6 +208,10 @@ __global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
         const int64_t cell2 = (I2 * kN16G2 + J2) * kN16G2 + L2, n2 = kN16G2 * kN16G2 * kN16G2;
         uint16_t* out = a.lvl2 + (a.K <= 4096 ? ((((int64_t)(p >> 1) * n2 + cell2) << 1) + (p & 1))
                                               : (int64_t)p * n2 + cell2) * kN16L2Words;
+#ifdef HQ_ABL_N16NOL2  // timing ablation of the grid: no level-2 lists (every entry overflows)
+        out[0] = kN16Ovf;
+        continue;
+#endif
         if (exh) {
             out[0] = kN16Ovf;
             continue;
@@ -213,52 +220,167 @@ __global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
         const int c1 = __builtin_amdgcn_readfirstlane((int)sl[0]);
         int cnt = 0;
         if (c1 != kN16Ovf) {
-            // the parent's list in registers: position 64 j + lane in slot j
-            constexpr int NSL = (kN16L1Cap + 1) / 64;
-            float4 cs[NSL];
-            float ks[NSL];
+            if constexpr (!TR) {
+                // per child: the lane the child; the parent's list in registers
+                // (position 64 j + lane in slot j), each colour broadcast by readlane
+                constexpr int NSL = (kN16L1Cap + 1) / 64;
+                float4 cs[NSL];
+                float ks[NSL];
 #pragma unroll
-            for (int j = 0; j < NSL; ++j) {
-                const int pj = 64 * j + lane < c1 ? sl[1 + 64 * j + lane] : 0;
-                cs[j] = c0at(pj);
-                ks[j] = (float)s_k0[pj];  // (exact: < 2^24)
-            }
-            // centre form of the bounds (3 VALU per axis): per axis |c - m| + h
-            // and max(|c - m| - h, 0), m the box centre (exact), h = half a cell.
-            // Each is within 2 ulp of the exact term at the terms' sizes here,
-            // which the 1e-5 margin covers with T >= 3 h^2 (a colour at the centre)
-            const float h2 = 0.5f * w2;
-            const float m0 = lo2[0] + h2, m1 = lo2[1] + h2, m2 = lo2[2] + h2;
-            auto bmax = [&](float x, float y, float z) {
-                const float tx = fabsf(x - m0) + h2, ty = fabsf(y - m1) + h2, tz = fabsf(z - m2) + h2;
-                return fmaf(tz, tz, fmaf(ty, ty, tx * tx));
-            };
-            // (the clamp to [0, 1] is the add's clamp bit, not a v_max; a term
-            // above 1 -- a colour outside the unit cube -- only lowers the bound)
-            auto bmin = [&](float x, float y, float z) {
-                const float tx = __builtin_amdgcn_fmed3f(fabsf(x - m0) - h2, 0.f, 1.f),
-                            ty = __builtin_amdgcn_fmed3f(fabsf(y - m1) - h2, 0.f, 1.f),
-                            tz = __builtin_amdgcn_fmed3f(fabsf(z - m2) - h2, 0.f, 1.f);
-                return fmaf(tz, tz, fmaf(ty, ty, tx * tx));
-            };
-            // the least bmax as an unsigned min of the bit patterns (bmax >= +0,
-            // finite): fminf canonicalised the running minimum every iteration
-            uint32_t t2u = 0x7f800000u;
+                for (int j = 0; j < NSL; ++j) {
+                    const int pj = 64 * j + lane < c1 ? sl[1 + 64 * j + lane] : 0;
+                    cs[j] = c0at(pj);
+                    ks[j] = (float)s_k0[pj];  // (exact: < 2^24)
+                }
+                // centre form of the bounds (3 VALU per axis): per axis |c - m| + h
+                // and max(|c - m| - h, 0), m the box centre (exact), h = half a cell.
+                // Each is within 2 ulp of the exact term at the terms' sizes here,
+                // which the 1e-5 margin covers with T >= 3 h^2 (a colour at the centre)
+                const float h2 = 0.5f * w2;
+                const float m0 = lo2[0] + h2, m1 = lo2[1] + h2, m2 = lo2[2] + h2;
+                auto bmax = [&](float x, float y, float z) {
+                    const float tx = fabsf(x - m0) + h2, ty = fabsf(y - m1) + h2, tz = fabsf(z - m2) + h2;
+                    return fmaf(tz, tz, fmaf(ty, ty, tx * tx));
+                };
+                // (the clamp to [0, 1] is the add's clamp bit, not a v_max; a term
+                // above 1 -- a colour outside the unit cube -- only lowers the bound)
+                auto bmin = [&](float x, float y, float z) {
+                    const float tx = __builtin_amdgcn_fmed3f(fabsf(x - m0) - h2, 0.f, 1.f),
+                                ty = __builtin_amdgcn_fmed3f(fabsf(y - m1) - h2, 0.f, 1.f),
+                                tz = __builtin_amdgcn_fmed3f(fabsf(z - m2) - h2, 0.f, 1.f);
+                    return fmaf(tz, tz, fmaf(ty, ty, tx * tx));
+                };
+                // the least bmax as an unsigned min of the bit patterns (bmax >= +0,
+                // finite): fminf canonicalised the running minimum every iteration
+                uint32_t t2u = 0x7f800000u;
 #pragma unroll
-            for (int j = 0; j < NSL; ++j) {
-                const int nj = min(c1 - 64 * j, 64);
-                for (int i = 0; i < nj; ++i)
-                    t2u = min(t2u, __builtin_bit_cast(uint32_t, bmax(rl(cs[j].x, i), rl(cs[j].y, i), rl(cs[j].z, i))));
-            }
-            const float thr2 = __builtin_bit_cast(float, t2u) * HQ_CAND_MARGIN;
+                for (int j = 0; j < NSL; ++j) {
+                    const int nj = min(c1 - 64 * j, 64);
+                    for (int i = 0; i < nj; ++i)
+                        t2u = min(t2u, __builtin_bit_cast(uint32_t, bmax(rl(cs[j].x, i), rl(cs[j].y, i), rl(cs[j].z, i))));
+                }
+                const float thr2 = __builtin_bit_cast(float, t2u) * HQ_CAND_MARGIN;
 #pragma unroll
-            for (int j = 0; j < NSL; ++j) {
-                const int nj = min(c1 - 64 * j, 64);
-                for (int i = 0; i < nj; ++i)
-                    if (bmin(rl(cs[j].x, i), rl(cs[j].y, i), rl(cs[j].z, i)) <= thr2) {
-                        if (cnt < kN16L2Cap) out[1 + cnt] = (uint16_t)rl(ks[j], i);
-                        ++cnt;
+                for (int j = 0; j < NSL; ++j) {
+                    const int nj = min(c1 - 64 * j, 64);
+                    for (int i = 0; i < nj; ++i)
+                        if (bmin(rl(cs[j].x, i), rl(cs[j].y, i), rl(cs[j].z, i)) <= thr2) {
+                            if (cnt < kN16L2Cap) out[1 + cnt] = (uint16_t)rl(ks[j], i);
+                            ++cnt;
+                        }
+                }
+            } else {
+                // Transposed: the lanes take the parent's colours (position 64 j +
+                // lane in slot j) and the 64 children are unrolled.  A child's
+                // bounds are sums of per-axis terms at its 4 x 4 x 4 place in the
+                // parent, so a lane forms 4 terms per axis and slot and one FMA per
+                // child finishes a bound, in the order of the per-child form
+                // (fmaf(tz, tz, fmaf(ty, ty, tx * tx))): the same bits, the same
+                // lists.  Centre form of the terms: per axis |c - m| + h and
+                // max(|c - m| - h, 0), m the child's centre (exact), h half a cell;
+                // each within 2 ulp of the exact term at the sizes here, which the
+                // 1e-5 margin covers with T >= 3 h^2 (a colour at the centre).  The
+                // clamp to [0, 1] is the add's clamp bit (a term above 1 -- a colour
+                // outside the unit cube -- only lowers the bound).
+                constexpr int NSL = (kN16L1Cap + 1) / 64;
+                const float h2 = 0.5f * w2;
+                const int base[3] = {16 * C0i + 4 * (ch >> 4), 16 * C0j + 4 * ((ch >> 2) & 3), 16 * C0k + 4 * (ch & 3)};
+                // slot j's colour (read in each pass: held across both, NSL = 4
+                // spilled)
+                auto colour = [&](int j) { return c0at(64 * j + lane < c1 ? sl[1 + 64 * j + lane] : 0); };
+                auto tmax = [&](float c, int ax, int q) { return fabsf(c - ((float)(base[ax] + q) * w2 + h2)) + h2; };
+                auto tmin = [&](float c, int ax, int q) {
+                    return __builtin_amdgcn_fmed3f(fabsf(c - ((float)(base[ax] + q) * w2 + h2)) - h2, 0.f, 1.f);
+                };
+                // the least bmax per child: lane-partial minima (unsigned min of the
+                // bit patterns: bmax >= +0; a lane past the list gives +inf), then a
+                // transposing reduction that leaves child `lane`'s minimum in T[0]
+                uint32_t T[64];
+#pragma unroll
+                for (int sc = 0; sc < 64; ++sc) T[sc] = 0x7f800000u;
+#pragma unroll
+                for (int j = 0; j < NSL; ++j) {
+                    if (64 * j >= c1) break;
+                    const float4 c = colour(j);
+                    const bool ok = 64 * j + lane < c1;
+                    float x2[4], ty[4], tz[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const float tx = tmax(c.x, 0, q);
+                        x2[q] = tx * tx;
+                        ty[q] = tmax(c.y, 1, q);
+                        tz[q] = ok ? tmax(c.z, 2, q) : INFINITY;
                     }
+#pragma unroll
+                    for (int qa = 0; qa < 4; ++qa)
+#pragma unroll
+                        for (int qb = 0; qb < 4; ++qb) {
+                            const float xy = fmaf(ty[qb], ty[qb], x2[qa]);
+#pragma unroll
+                            for (int qc = 0; qc < 4; ++qc) {
+                                const int sc = 16 * qa + 4 * qb + qc;
+                                T[sc] = min(T[sc], __builtin_bit_cast(uint32_t, fmaf(tz[qc], tz[qc], xy)));
+                            }
+                        }
+                }
+#pragma unroll
+                for (int W = 32; W >= 1; W >>= 1) {
+                    const bool hi = (lane & W) != 0;
+#pragma unroll
+                    for (int sc = 0; sc < W; ++sc) {
+                        const uint32_t send = hi ? T[sc] : T[sc + W], keep = hi ? T[sc + W] : T[sc];
+                        T[sc] = min(keep, (uint32_t)__shfl_xor((int)send, W, 64));
+                    }
+                }
+                const float thr2 = __builtin_bit_cast(float, T[0]) * HQ_CAND_MARGIN;  // child `lane`'s threshold
+                // the candidates: per slot and child a ballot over the colours,
+                // parked in lane `child` of the slot's mask words
+                uint32_t mlo[NSL], mhi[NSL];
+#pragma unroll
+                for (int j = 0; j < NSL; ++j) {
+                    mlo[j] = mhi[j] = 0u;
+                    if (64 * j >= c1) continue;
+                    const float4 c = colour(j);
+                    const bool ok = 64 * j + lane < c1;
+                    float x2[4], ty[4], tz[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const float tx = tmin(c.x, 0, q);
+                        x2[q] = tx * tx;
+                        ty[q] = tmin(c.y, 1, q);
+                        tz[q] = tmin(c.z, 2, q);
+                    }
+#pragma unroll
+                    for (int qa = 0; qa < 4; ++qa)
+#pragma unroll
+                        for (int qb = 0; qb < 4; ++qb) {
+                            const float xy = fmaf(ty[qb], ty[qb], x2[qa]);
+#pragma unroll
+                            for (int qc = 0; qc < 4; ++qc) {
+                                const int sc = 16 * qa + 4 * qb + qc;
+                                const float ts = __builtin_bit_cast(
+                                    float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, thr2), sc));
+                                const uint64_t bal = __ballot(ok && fmaf(tz[qc], tz[qc], xy) <= ts);
+                                mlo[j] = lane == sc ? (uint32_t)bal : mlo[j];
+                                mhi[j] = lane == sc ? (uint32_t)(bal >> 32) : mhi[j];
+                            }
+                        }
+                }
+                // child `lane`'s list: the set bits in ascending position order
+#pragma unroll
+                for (int j = 0; j < NSL; ++j) cnt += __popc(mlo[j]) + __popc(mhi[j]);
+                if (cnt <= kN16L2Cap) {
+                    int n = 0;
+#pragma unroll
+                    for (int j = 0; j < NSL; ++j) {
+                        uint64_t m = ((uint64_t)mhi[j] << 32) | mlo[j];
+                        while (m) {
+                            const int b = __builtin_ctzll(m);
+                            m &= m - 1;
+                            out[1 + n++] = s_k0[sl[1 + 64 * j + b]];
+                        }
+                    }
+                }
             }
         } else {  // the parent list overflowed: every level-0 candidate (broadcast LDS reads)
             float t2 = INFINITY;
@@ -291,13 +413,13 @@ hipError_t launch_lists16_grid(const Lists16Args& a, int P, hipStream_t s) {
     const size_t lds = ((soa ? 3 : 4) * sizeof(float) + sizeof(uint16_t)) * (size_t)a.K +
                        sizeof(uint16_t) * 64 * n16_l1_words(a.K);
     const dim3 grid(kN16G0 * kN16G0 * kN16G0, (unsigned)P);
-    if (soa) {
-        allow_lds16(reinterpret_cast<const void*>(lists16_kernel<true>), lds);
-        HQ_LAUNCH(lists16_kernel<true>, grid, dim3(kN16Threads), lds, s, a);
-    } else {
-        allow_lds16(reinterpret_cast<const void*>(lists16_kernel<false>), lds);
-        HQ_LAUNCH(lists16_kernel<false>, grid, dim3(kN16Threads), lds, s, a);
-    }
+    auto go = [&](auto kern) {
+        allow_lds16(reinterpret_cast<const void*>(kern), lds);
+        HQ_LAUNCH(kern, grid, dim3(kN16Threads), lds, s, a);
+    };
+    if (soa) go(lists16_kernel<true, true>);
+    else if (a.K > 2048) go(lists16_kernel<false, true>);
+    else go(lists16_kernel<false, false>);
     return hipGetLastError();
 }
 
@@ -545,8 +667,9 @@ hipError_t launch_assign16(const AssignArgs& a0, int P, hipStream_t s) {
     return hipGetLastError();
 }
 
-template __global__ void lists16_kernel<true>(Lists16Args);
-template __global__ void lists16_kernel<false>(Lists16Args);
+template __global__ void lists16_kernel<true, true>(Lists16Args);
+template __global__ void lists16_kernel<false, true>(Lists16Args);
+template __global__ void lists16_kernel<false, false>(Lists16Args);
 template __global__ void assign16_kernel<true, 1>(AssignArgs, int);
 template __global__ void assign16_kernel<false, 1>(AssignArgs, int);
 template __global__ void assign16_kernel<true, 2>(AssignArgs, int);
