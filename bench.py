@@ -8,8 +8,12 @@ reduction), the RCCL all-reduce of the partial costs when N > 1, and the
 acceptance step.  value = W*H*P*steps / max-over-ranks wall time (strong
 scaling: the 4096^2 image is row-block sharded over the N GPUs).
 
-Run: python bench.py [--gpus N] [--steps K] [--warmup W]; N > 1 under
-torch.distributed.run (one process per GPU; RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*).
+Run: python bench.py [--gpus N] [--steps K] [--warmup W].  N > 1 runs one
+process per GPU: under torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*
+set; WORLD_SIZE must equal N), or, when WORLD_SIZE is unset, bench.py starts
+the N rank processes itself (launch_ranks: the parent imports neither torch nor
+libhq, so nothing touches the GPU before the ranks exist) and relays rank 0's
+line.
 """
 
 from __future__ import annotations
@@ -207,6 +211,114 @@ def cpu_baseline(args):
                                         "seconds": round(els, 2), "threads": 1}}
 
 
+GPU_MODULES = ("torch", "hybridquantization_amd")
+
+
+def gpu_modules_loaded():
+    """Modules in this process that could touch the GPU (the launcher must have none)."""
+    return sorted(m for m in sys.modules if m.split(".")[0] in GPU_MODULES)
+
+
+def _free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def visible_gpus():
+    """Visible HIP devices, counted in a child process (this one stays GPU-free)."""
+    import subprocess
+
+    r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                       capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        raise RuntimeError(f"bench.py: counting the visible GPUs failed: {r.stderr.strip()[-400:]}")
+    return int(r.stdout.strip().splitlines()[-1])
+
+
+def launch_ranks(n, argv, dry_run=False):
+    """--gpus N > 1 with WORLD_SIZE unset: start N rank processes of this script,
+    one per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N, MASTER_ADDR 127.0.0.1 and
+    a free port), wait for them all, print rank 0's JSON line with a `launcher`
+    record, and return the exit status (non-zero if any rank failed; the other
+    ranks are then stopped).  Nothing here imports torch or libhq."""
+    import subprocess
+    import tempfile
+
+    before = gpu_modules_loaded()
+    if not dry_run:
+        have = visible_gpus()
+        if n > have:
+            print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr, flush=True)
+            return 2
+    port = _free_port()
+    out0 = tempfile.TemporaryFile(mode="w+")
+    procs = []
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                       HQ_BENCH_LAUNCHER=str(os.getpid()))
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                                          stdout=out0 if r == 0 else sys.stderr))
+        rc = 0
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 1
+                    print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                          file=sys.stderr, flush=True)
+                    for q in live:
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    out0.seek(0)
+    lines = [ln for ln in out0.read().splitlines() if ln.startswith("{")]
+    if rc != 0:
+        return rc
+    if len(lines) != 1:
+        print(f"bench.py: rank 0 printed {len(lines)} JSON lines, expected 1", file=sys.stderr, flush=True)
+        return 1
+    line = json.loads(lines[0])
+    line["launcher"] = {"by": "bench.py", "ranks": n, "master": f"127.0.0.1:{port}",
+                        "parent_gpu_modules": before}
+    print(json.dumps(line), flush=True)
+    return 0
+
+
+def dry_run_worker(world, rank):
+    """--dry-run: the rank wiring alone (gloo, no libhq, no GPU).  Rank 0 prints
+    one line with the ranks it saw over the process group."""
+    import torch
+    import torch.distributed as dist
+
+    env = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "world": world, "pid": os.getpid()}
+    if os.environ.get("HQ_DRY_RUN_FAIL_RANK") == str(rank):  # test: one rank dies before the rendezvous
+        raise SystemExit(3)
+    seen = [env]
+    if world > 1:
+        dist.init_process_group("gloo")
+        seen = [None] * world
+        dist.all_gather_object(seen, env)
+        dist.barrier()
+    if rank == 0:
+        print(json.dumps({"metric": "Mpixel*evals/s (SWASA dE cost) at 4096x4096 K=256", "dry_run": True,
+                          "n_gpus": world, "ranks_seen": seen, "torch": torch.__version__}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def full_search(lib, _lib, m, K, P, seed, sa_device, restore):
     """BASELINE config 3 as the plugin runs it: one SWASA search of imax = 5000
     iterations with the default schedule (HQ:197-224), P palettes per
@@ -234,7 +346,9 @@ def full_search(lib, _lib, m, K, P, seed, sa_device, restore):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) of this node; default WORLD_SIZE or 1.  N > 1 with WORLD_SIZE unset: "
+                         "bench.py starts the N rank processes itself")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--size", type=int, default=4096)
@@ -257,16 +371,34 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-full-search", action="store_true",
                     help="skip the imax = 5000 search of BASELINE config 3 (extra keys)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="test the rank wiring only: gloo process group, no libhq, no GPU")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if args.gpus is not None and args.gpus < 1:
+            raise SystemExit(f"bench.py: --gpus {args.gpus}")
+        if args.gpus is not None and args.gpus > 1:  # this process only launches and relays
+            sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.dry_run))
+        world = 1
+    else:
+        world = int(env_world)
+        if args.gpus is not None and args.gpus != world:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one process per GPU")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        dry_run_worker(world, rank)
+        return
     dist = None
     if world > 1:
         import torch
         import torch.distributed as dist
 
+        have = torch.cuda.device_count()
+        if local >= have:
+            raise SystemExit(f"bench.py: rank {rank} needs GPU {local} (LOCAL_RANK) but {have} are visible")
         torch.cuda.set_device(local)
         dist.init_process_group("gloo")  # control plane only; data path is libhq's RCCL comm
 
@@ -298,6 +430,10 @@ def main():
     del R, G, B
     if world > 1:
         hqd.init_comm(m, dist, world, rank)
+    rccl_ranks, rccl_rank = m.commInfo()  # (0, -1): no communicator (one GPU)
+    if world > 1 and (rccl_ranks, rccl_rank) != (world, rank):
+        raise RuntimeError(f"bench.py: RCCL communicator has {rccl_ranks} ranks (rank {rccl_rank}), "
+                           f"expected {world} (rank {rank})")
 
     P = args.population
     # which BASELINE.json config this run's shape is (configs[2] is the default)
@@ -438,6 +574,8 @@ def main():
                              "kernel_avg_ms: HIP events carried by the launches on the context stream over a "
                              "second pass of the same steps, right after the timed one (events idle the GPU "
                              "~5-10 us each, so the timed pass has none)"},
+        "split": "palettes" if psplit else "rows" if world > 1 else "none",
+        "rccl_ranks": rccl_ranks,
         "metric_hbm_roofline_frac": round(value / eval_roof_mpx, 4),
         "kernel_avg_ms": kernel_avg,
         **({"kernel_avg_ms_max_over_ranks": kernel_max} if kernel_max is not None else {}),

@@ -68,6 +68,7 @@ SIGNATURES = {
     "hq_compute_error": (C.c_int, [_ctx, _f, _f, C.c_int64, _f, _d]),
     "hq_comm_unique_id": (C.c_int, [C.POINTER(C.c_ubyte)]),
     "hq_comm_init": (C.c_int, [_ctx, C.c_int, C.c_int, C.POINTER(C.c_ubyte)]),
+    "hq_comm_info": (C.c_int, [_ctx, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "hq_swasa_default_params": (None, [C.POINTER(hq_swasa_params)]),
     "hq_search_create": (C.c_int, [_ctx, C.POINTER(hq_swasa_params), C.c_int, C.c_uint64,
                                    C.POINTER(C.c_void_p)]),

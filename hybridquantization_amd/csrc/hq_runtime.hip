@@ -1524,6 +1524,17 @@ int hq_comm_init(hq_ctx* c, int nranks, int rank, const unsigned char id[128]) {
     return HQ_OK;
 }
 
+int hq_comm_info(hq_ctx* c, int* nranks, int* rank) {
+    if (!c || !nranks || !rank) return HQ_ERR_ARG;
+    *nranks = 0;
+    *rank = -1;
+    if (!c->comm) return HQ_OK;
+    // what the communicator itself reports, not what hq_comm_init was asked for
+    NCCL_TRY(c, ncclCommCount(c->comm, nranks));
+    NCCL_TRY(c, ncclCommUserRank(c->comm, rank));
+    return HQ_OK;
+}
+
 int hq_search_create(hq_ctx* c, const hq_swasa_params* params, int K, uint64_t seed,
                      hq_search** out) {
     if (!c || !params || !out) return HQ_ERR_ARG;

@@ -241,6 +241,14 @@ class ImageManipulation:
         buf = (C.c_ubyte * 128).from_buffer_copy(unique_id)
         check(self._lib.hq_comm_init(ctx, int(nranks), int(rank), buf), ctx)
 
+    def commInfo(self) -> tuple[int, int]:
+        """(ranks, this rank) of the context's RCCL communicator as RCCL reports
+        them; (0, -1) without one."""
+        ctx = self._require()
+        n, r = C.c_int(), C.c_int()
+        check(self._lib.hq_comm_info(ctx, C.byref(n), C.byref(r)), ctx)
+        return n.value, r.value
+
     @staticmethod
     def commUniqueId() -> bytes:
         buf = (C.c_ubyte * 128)()

@@ -152,6 +152,10 @@ int hq_compute_error(hq_ctx *ctx, const float *orig4, const float *quant4, int64
  * Rank 0 calls hq_comm_unique_id and ships the 128 bytes to every rank. */
 int hq_comm_unique_id(unsigned char id[128]);
 int hq_comm_init(hq_ctx *ctx, int nranks, int rank, const unsigned char id[128]);
+/* The ranks of the context's communicator as RCCL reports them (ncclCommCount,
+ * ncclCommUserRank); *nranks = 0 and *rank = -1 without one.  bench.py reports
+ * it next to its own world size. */
+int hq_comm_info(hq_ctx *ctx, int *nranks, int *rank);
 
 /* SWASA parameters (SW:14-28; GUI defaults HQ:192-224). */
 typedef struct hq_swasa_params {

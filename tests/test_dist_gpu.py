@@ -113,3 +113,42 @@ def test_two_process_shards_allreduce_to_full(gpu):
     c = total[:, 0] / (W * H) + 2.0 * np.count_nonzero(total[:, 1:] == 0, axis=1)
     np.testing.assert_allclose(c, costs, rtol=1e-7)
     np.testing.assert_array_equal(total[:, 1:] > 0, used > 0)
+
+
+def _bench(args, timeout=300):
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    return subprocess.run([sys.executable, os.path.join(root, "bench.py"), *args], env=env, cwd=root,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_bench_gpus_1_prints_one_line(gpu):
+    """bench.py --gpus 1 (the driver's BENCH form) stays a single process with
+    today's line, plus the split and the communicator's rank count (none)."""
+    import json
+
+    r = _bench(["--gpus", "1", "--steps", "3", "--warmup", "1", "--size", "256", "--K", "16",
+                "--population", "2", "--no-cpu-baseline", "--no-full-search"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["value"] > 0
+    assert d["split"] == "none" and d["rccl_ranks"] == 0 and "launcher" not in d
+    assert d["roofline"]["kernel_avg_ms"] > 0
+
+
+def test_bench_launcher_refuses_more_gpus_than_visible(gpu):
+    import ctypes
+
+    import hybridquantization_amd as hq
+
+    n = ctypes.c_int()
+    hq.load().hq_device_count(ctypes.byref(n))
+    r = _bench(["--gpus", str(n.value + 1), "--steps", "1", "--size", "256", "--K", "16",
+                "--no-cpu-baseline", "--no-full-search"], timeout=200)
+    assert r.returncode == 2
+    assert f"only {n.value} GPU(s) visible" in r.stderr
