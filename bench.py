@@ -4,7 +4,8 @@ Metric (BASELINE.json): Mpixel*evals/s of the SWASA dE cost at 4096x4096, K=256.
 A "step" is one SWASA iteration of the native search (IM:497-568): neighbour
 generation for P palettes, evaluation of the P candidate costs on the GPU
 (palette prep + exact grid, argmin, S-CIELAB stencil + dE76, fixed-order fp64
-reduction), the RCCL all-reduce of the partial costs when N > 1, and the
+reduction), when N > 1 the RCCL all-gather of every rank's fixed-point
+counter blocks (row blocks) or of the palette split's result rows, and the
 acceptance step.  value = W*H*P*steps / max-over-ranks wall time (strong
 scaling: the 4096^2 image is row-block sharded over the N GPUs).
 
@@ -121,10 +122,12 @@ def use_palette_split(split, P, world):
     return split == "palettes" or (split == "auto" and P >= 8 * world and P % world == 0)
 
 
-def profiled_stages(world):
+def profiled_stages(world, comm=False):
     """hq_profile_get names of one search iteration: the kernels, and at N > 1
-    the collective ("comm": the RCCL all-reduce or all-gather, event-timed)."""
-    return ("sa_step", "grid", "assign", "cost", "finalize") + (("comm",) if world > 1 else ())
+    (or with a one-rank communicator, --shard-comm) the collective ("comm": the
+    RCCL all-gather of the counter blocks or of the palette split's rows,
+    event-timed)."""
+    return ("sa_step", "grid", "assign", "cost", "finalize") + (("comm",) if world > 1 or comm else ())
 
 
 def kernel_profile(prof, world, max_over_ranks=None):
@@ -363,6 +366,9 @@ def main():
     ap.add_argument("--shard-of", type=int, default=0, metavar="N",
                     help="experiment: run rank 0's row block of an N-way split on one GPU, "
                          "no collective (per-rank step time at N GPUs)")
+    ap.add_argument("--shard-comm", action="store_true",
+                    help="with --shard-of: a one-rank RCCL communicator, so each step carries the "
+                         "collective path (the all-gather of the counter blocks)")
     ap.add_argument("--split", choices=["auto", "rows", "palettes"], default="auto",
                     help="N > 1: row-block shards + one all-reduce, or each rank the whole image and P/N "
                          "palettes + one all-gather (SURVEY 8e); auto: palettes when P >= 8 N and N "
@@ -391,6 +397,13 @@ def main():
     if args.dry_run:
         dry_run_worker(world, rank)
         return
+    # The job's stdout carries exactly one JSON line (rank 0's).  Native
+    # libraries print to fd 1 on their own -- RCCL's version banner at
+    # communicator set-up -- so fd 1 goes to stderr for the run and the line is
+    # written to the saved stdout at the end.
+    sys.stdout.flush()
+    line_fd = os.dup(1)
+    os.dup2(2, 1)
     dist = None
     if world > 1:
         import torch
@@ -430,8 +443,10 @@ def main():
     del R, G, B
     if world > 1:
         hqd.init_comm(m, dist, world, rank)
+    elif args.shard_of > 0 and args.shard_comm:
+        m.initComm(1, 0, m.commUniqueId())
     rccl_ranks, rccl_rank = m.commInfo()  # (0, -1): no communicator (one GPU)
-    if world > 1 and (rccl_ranks, rccl_rank) != (world, rank):
+    if (world > 1 or args.shard_comm) and (rccl_ranks, rccl_rank) != (world, rank):
         raise RuntimeError(f"bench.py: RCCL communicator has {rccl_ranks} ranks (rank {rccl_rank}), "
                            f"expected {world} (rank {rank})")
 
@@ -496,7 +511,7 @@ def main():
         elapsed = hqd.max_over_ranks(dist, elapsed)
 
     prof = {}
-    for k in profiled_stages(world):
+    for k in profiled_stages(world, rccl_ranks > 0):
         ms = C.c_double()
         n = C.c_int64()
         lib.hq_profile_get(m.ctx, k.encode(), C.byref(ms), C.byref(n))
@@ -550,7 +565,8 @@ def main():
                    "argmin_grid": args.grid,
                    **({"dpi": args.dpi, "distance_cm": args.distance}
                       if (args.dpi, args.distance) != (72, 45.0) else {}),
-                   **({"shard_of": args.shard_of, "rows": [r0, r1]} if args.shard_of > 0 else {}),
+                   **({"shard_of": args.shard_of, "rows": [r0, r1], "shard_comm": bool(args.shard_comm)}
+                      if args.shard_of > 0 else {}),
                    **({"options": args.opt} if args.opt else {})},
         "roofline": {"bound": "valu", "achieved": round(achieved_tf, 2), "peak": FP32_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4),
@@ -586,8 +602,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)
     m.close()
+    sys.stdout.flush()
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        os.write(line_fd, (json.dumps(out) + "\n").encode())
     if dist is not None:
         dist.destroy_process_group()
 

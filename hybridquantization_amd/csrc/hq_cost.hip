@@ -1994,20 +1994,6 @@ bool trim_window_ok(const float* k1, int H, int HB) {
     return true;
 }
 
-// Dynamic LDS of `bytes` for kernel `fn` (static + dynamic may pass 64 KB): raised once per kernel
-// (each template instance is its own function; the largest size asked so far
-// is kept per function pointer).  False if the runtime refused it.
-static bool allow_dyn_lds(const void* fn, size_t bytes) {
-    static std::mutex mu;
-    static std::unordered_map<const void*, size_t> granted;
-    const std::lock_guard<std::mutex> lock(mu);
-    size_t& g = granted[fn];
-    if (bytes <= g) return true;
-    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess) return false;
-    g = bytes;
-    return true;
-}
-
 template <int HB>
 static size_t taps_bytes() { return 2 * sizeof(CostTaps<HB>); }
 

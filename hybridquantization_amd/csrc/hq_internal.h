@@ -100,13 +100,17 @@ struct SaArgs {
     const uint64_t* jump_A; // LCG jumps: n steps = A_n s + C_n mod 2^48, n = 0 .. 3K*P
     const uint64_t* jump_C;
     PaletteArgs prep;       // outputs of the palette prep of the next candidates
-    // fold (no communicator): the accept step reads the fixed-point sums and the
-    // used bits itself, so no finalize launch sits between the cost kernel and
-    // this step
-    const uint64_t* acc;    // [kAccSlots][P][4] (acc_total)
-    const uint32_t* used_glob;  // [kUsedSlots][used_stride]: [P][8 nch] per slot
+    // fold (no communicator, or a row-block split): the accept step reads the
+    // fixed-point sums and the used bits itself, so no finalize launch sits
+    // between the cost kernel and this step.  Row-block ranks: nranks blocks,
+    // each rank's own, gathered by one RCCL all-gather (integer sums and OR'ed
+    // bits: the same totals in any rank order).
+    const uint64_t* acc;    // [nranks][kAccSlots][P][4] (acc_total), acc_rank_words apart
+    const uint32_t* used_glob;  // [nranks][kUsedSlots][used_stride]: [P][8 nch] per slot
     int used_stride;
     int fold;
+    int nranks;             // rank blocks of acc and used_glob (1 without a communicator)
+    int64_t acc_rank_words;
     double n_total;         // pixels of the whole image
     double keep_threshold;  // SW:59-62 -(tanh(num/den))/2 + 0.5 at the accepted iteration
     float temperature;      // SW:54-57 temperature at the accepted iteration
@@ -195,6 +199,14 @@ struct AssignArgs {
     const uint16_t* l1n = nullptr;
     const uint16_t* l2n = nullptr;
     int kpal = 0;
+    // cell-binned pixels (option assign_bin; packed 8-bit images, K <= 256): the
+    // pixels in level-2 cell order as (position, packed RGB), built once per
+    // image and grid (hq_assign.hip bin_*_kernel); the indices then go out
+    // scattered, into the planes (assign_bin 1) or as one dword of the group's 4
+    // palettes per pixel into idx4 [ceil(P/4)][n_ext] (assign_bin 2), split into
+    // the planes by idx4_split_kernel
+    const uint2* bin = nullptr;
+    uint32_t* idx4 = nullptr;
 };
 
 struct CostArgs {

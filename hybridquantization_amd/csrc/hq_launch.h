@@ -18,6 +18,13 @@ inline unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }
 extern thread_local hipEvent_t t_ev_start, t_ev_stop;
 void set_launch_events(hipEvent_t start, hipEvent_t stop);
 
+// Dynamic LDS of `bytes` for kernel `fn` (static + dynamic may pass 64 KiB, up to
+// the CU's 160 KiB on gfx950): raised once per kernel (each template instance is
+// its own function; the largest size granted so far is kept per function
+// pointer, a refused raise is retried at the next call).  False if the runtime
+// refused it: the launcher then returns an error instead of launching.
+bool allow_dyn_lds(const void* fn, size_t bytes);
+
 #define HQ_LAUNCH(K, G, B, S, STREAM, ...)                                                   \
     do {                                                                                     \
         if (t_ev_start || t_ev_stop)                                                         \

@@ -396,31 +396,19 @@ __global__ __launch_bounds__(kN16Threads) void lists16_kernel(Lists16Args a) {
     }
 }
 
-// Dynamic LDS beyond the default 64 KiB for a kernel (raised once; 160 KiB per CU).
-static void allow_lds16(const void* fn, size_t bytes) {
-    static std::mutex mu;
-    static std::unordered_map<const void*, size_t> raised;
-    std::lock_guard<std::mutex> lk(mu);
-    size_t& r = raised[fn];
-    if (bytes > r) {
-        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-        r = bytes;
-    }
-}
-
 hipError_t launch_lists16_grid(const Lists16Args& a, int P, hipStream_t s) {
     const bool soa = a.K > 4096;
     const size_t lds = ((soa ? 3 : 4) * sizeof(float) + sizeof(uint16_t)) * (size_t)a.K +
                        sizeof(uint16_t) * 64 * n16_l1_words(a.K);
     const dim3 grid(kN16G0 * kN16G0 * kN16G0, (unsigned)P);
     auto go = [&](auto kern) {
-        allow_lds16(reinterpret_cast<const void*>(kern), lds);
+        if (!allow_dyn_lds(reinterpret_cast<const void*>(kern), lds)) return hipErrorInvalidConfiguration;
         HQ_LAUNCH(kern, grid, dim3(kN16Threads), lds, s, a);
+        return hipGetLastError();
     };
-    if (soa) go(lists16_kernel<true, true>);
-    else if (a.K > 2048) go(lists16_kernel<false, true>);
-    else go(lists16_kernel<false, false>);
-    return hipGetLastError();
+    if (soa) return go(lists16_kernel<true, true>);
+    if (a.K > 2048) return go(lists16_kernel<false, true>);
+    return go(lists16_kernel<false, false>);
 }
 
 // ----------------------------------------------------------------------------
@@ -649,9 +637,10 @@ hipError_t launch_assign16(const AssignArgs& a0, int P, hipStream_t s) {
     const int npal = a.K <= 4096 ? 2 : 1;  // two 64 KiB tables fit one workgroup up to K = 4096
     const size_t lds = sizeof(float4) * (size_t)a.K * npal;
     const dim3 grid((unsigned)(a.nblocks * ((P + npal - 1) / npal)));
+    bool ok = true;
     auto go = [&](auto kern) {
-        allow_lds16(reinterpret_cast<const void*>(kern), lds);
-        HQ_LAUNCH(kern, grid, dim3(kN16Threads), lds, s, a, P);
+        ok = allow_dyn_lds(reinterpret_cast<const void*>(kern), lds);
+        if (ok) HQ_LAUNCH(kern, grid, dim3(kN16Threads), lds, s, a, P);
     };
     if (npal == 2) {
         if (a.rgbx) go(assign16_kernel<true, 2>);
@@ -659,6 +648,11 @@ hipError_t launch_assign16(const AssignArgs& a0, int P, hipStream_t s) {
     } else {
         if (a.rgbx) go(assign16_kernel<true, 1>);
         else go(assign16_kernel<false, 1>);
+    }
+    if (!ok) {
+        t_ev_start = ev0;
+        t_ev_stop = ev1;
+        return hipErrorInvalidConfiguration;  // the LDS raise was refused: nothing launched
     }
     t_ev_start = nullptr;
     t_ev_stop = ev1;

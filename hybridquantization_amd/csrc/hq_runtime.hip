@@ -178,6 +178,7 @@ struct hq_ctx {
                            // "palette_split"; SURVEY 8e's split of large populations)
     int slice_ranks = 1, slice_rank = 0;  // test only: the same slice without a communicator
     int slice_lo = 0, slice_n = 0;        // the last evaluation's palettes held on this device
+    int fold_blocks = 1, fold_block = 0;  // test only: rank blocks of the counters without a communicator
     int lists16 = 1;       // native 16-bit candidate lists: 1 = chunked palettes of 4 to 32 chunks, 2 = 2 .. 32
     int chunked = 1;       // 256 < K <= 16384: palettes as 256-colour chunks through the grid and
                            // tiled kernels (option "chunked"; 0 = the exhaustive K > 256 path)
@@ -200,6 +201,7 @@ struct hq_ctx {
     // profiling: start/stop of grid, assign, cost, finalize, [sa_step], the collective
     hipEvent_t ev[kProfEvents] = {};
     int num_cu = 256;
+    size_t lds_optin = 160 * 1024;  // per-workgroup LDS a kernel may opt into (hq_create's query)
 };
 
 struct hq_search {
@@ -215,6 +217,7 @@ struct hq_search {
     int P = 0, ite = 0, st = 0, cd = 0;  // state and candidate buffer parities
     int nch = 1;                         // chunked palettes (256 < K <= 16384): chunks per palette
     bool fold = false;                   // accept steps reduce the partials (no finalize launch)
+    ncclComm_t comm = nullptr;           // the context's communicator at hq_search_create
     float t_acc = 0.f;                   // temperature / threshold of the iteration
     double keep_acc = 0.0;               // whose population awaits acceptance
     DevBuf colors[2], cand[2], err[2], seed[2], best_err[2], best_colors, jA, jC;
@@ -428,10 +431,40 @@ int assign_blocks(const hq_ctx* c, int P) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(nblocks, (c->g.n_ext + chunk - 1) / chunk));
 }
 
+// A row-block split (a communicator, no palette split) keeps one block of
+// counters and used bits per rank in each set, [ranks][...]: every rank fills
+// its own block, and a device-resident search's one all-gather per iteration
+// hands every rank all the blocks, which its accept step folds (no finalize).
+// (test options fold_blocks / fold_block: the same layout without a communicator,
+// this context filling block fold_block and the others staying zero)
+int rank_blocks(const hq_ctx* c) { return c->comm ? (c->psplit ? 1 : c->nranks) : c->fold_blocks; }
+int own_block(const hq_ctx* c) { return c->comm ? (rank_blocks(c) > 1 ? c->rank : 0) : c->fold_block; }
+// A device-resident search folds the partials in its accept step unless the
+// palette split all-gathers finalized rows.
+bool search_folds(const hq_ctx* c) { return !(c->comm && c->psplit); }
+
 // Chunked palettes of 4 to 32 chunks take the native 16-bit lists (option lists16).
+// Their kernels take up to 144 KiB (lists16_kernel at K = 8192) and 128 KiB
+// (assign16_kernel) of dynamic LDS: a device that cannot grant that (less than
+// gfx950's 160 KiB per workgroup) keeps the per-chunk grids.
 bool use_lists16(const hq_ctx* c) {
     const int min_nch = c->lists16 >= 2 ? 2 : kN16MinNch;  // (2: also 2 and 4 chunks)
-    return c->lists16 > 0 && c->G2 > 0 && c->nch_cur >= min_nch && c->nch_cur <= kN16MaxNch;
+    if (!(c->lists16 > 0 && c->G2 > 0 && c->nch_cur >= min_nch && c->nch_cur <= kN16MaxNch)) return false;
+    const size_t K = (size_t)kMaxK * c->nch_cur;
+    const size_t grid_lds = ((K > 4096 ? 3 : 4) * sizeof(float) + sizeof(uint16_t)) * K +
+                            sizeof(uint16_t) * 64 * n16_l1_words((int)K);
+    const size_t assign_lds = sizeof(float4) * K * (K <= 4096 ? 2 : 1);
+    return std::max(grid_lds, assign_lds) <= c->lds_optin;
+}
+
+// The population being enqueued takes the fast tiled cost kernels (else the
+// generic pair, whose [7][n_ext] scratch ensure_population then allocates up
+// front: nothing may allocate while a search run is captured into a graph).
+// Chunked palettes: the 16 x 128 tiles at HB = 10 only.
+bool cost_fast(const hq_ctx* c) {
+    return c->cost_variant == 0 && c->fast_hb > 0 && !c->pal_generic &&
+           (c->nch_cur == 1 || (c->nch_cur <= kMaxNchFast && c->fast_hb == 10 && c->cost_rows == 16 &&
+                                c->cost_tw == 128));
 }
 
 // Ensure population buffers for P palettes of K colours.
@@ -441,7 +474,7 @@ int ensure_population(hq_ctx* c, int P, int K) {
         HIP_TRY(c, c->d_idx16.ensure(sizeof(uint16_t) * (size_t)P * g.idx_pitch + 256));
         if (c->nch_cur > 4) HIP_TRY(c, c->d_dist.ensure(sizeof(float) * (size_t)P * g.idx_pitch));
         if (use_lists16(c)) {
-            HIP_TRY(c, c->d_l1n.ensure(sizeof(uint16_t) * kN16L1WordsMax * (size_t)P * kN16G1 * kN16G1 * kN16G1));
+            HIP_TRY(c, c->d_l1n.ensure(sizeof(uint16_t) * n16_l1_words(K) * (size_t)P * kN16G1 * kN16G1 * kN16G1));
             // (palette pairs interleaved: an odd population's last pair half empty)
             HIP_TRY(c, c->d_l2n.ensure(sizeof(uint16_t) * kN16L2Words * (size_t)(P + 1) / 2 * 2 * kN16G2 * kN16G2 * kN16G2));
         }
@@ -469,16 +502,14 @@ int ensure_population(hq_ctx* c, int P, int K) {
     // bytes past a region's last column (past the buffer on the last palette's
     // last row when idx_pitch has no padding)
     HIP_TRY(c, c->d_idx.ensure((size_t)P * g.idx_pitch + 256));
-    HIP_TRY(c, c->d_used_mask.ensure(2 * sizeof(uint32_t) * kUsedSlots * (size_t)used_stride(P)));
-    HIP_TRY(c, c->d_acc.ensure(2 * sizeof(uint64_t) * acc_words(P)));
+    const size_t rb = (size_t)rank_blocks(c);  // counter / used-bit blocks per set
+    HIP_TRY(c, c->d_used_mask.ensure(2 * rb * sizeof(uint32_t) * kUsedSlots * (size_t)used_stride(P)));
+    HIP_TRY(c, c->d_acc.ensure(2 * rb * sizeof(uint64_t) * acc_words(P)));
     HIP_TRY(c, c->d_out.ensure(sizeof(double) * (size_t)P * (1 + K)));
     if (c->pixel_err) HIP_TRY(c, c->d_pixerr.ensure(sizeof(float) * (size_t)P * std::max<int64_t>(n_own, 1)));
     // the generic path's [7][n_ext] scratch, here rather than at its first launch: an
     // allocation cannot happen while a search run is being captured into a graph
-    const bool fast = c->cost_variant == 0 && c->fast_hb > 0 &&
-                      (c->nch_cur == 1 || (c->nch_cur <= kMaxNchFast && c->fast_hb == 10 && c->cost_rows == 16 &&
-                                           c->cost_tw == 128));
-    if (!fast || K > kMaxK) HIP_TRY(c, c->d_gen_t.ensure(sizeof(float) * 7 * (size_t)g.n_ext + 256));
+    if (!cost_fast(c) || K > kMaxK) HIP_TRY(c, c->d_gen_t.ensure(sizeof(float) * 7 * (size_t)g.n_ext + 256));
     return ensure_pinned(c, sizeof(float) * 4 * (size_t)P * K, sizeof(double) * (size_t)P * (1 + K));
 }
 
@@ -503,9 +534,15 @@ PaletteArgs prep_args(hq_ctx* c, int K) {
 // the grid, assign, cost and finalize launches, carried by the launches
 // themselves (set_launch_events).
 // Counter set `par` of an evaluation of P palettes (P nch sub-palettes Ps).
-uint64_t* acc_set(hq_ctx* c, int par, int P) { return c->d_acc.as<uint64_t>() + (size_t)par * acc_words(P); }
+uint64_t* acc_base(hq_ctx* c, int par, int P) {
+    return c->d_acc.as<uint64_t>() + (size_t)par * rank_blocks(c) * acc_words(P);
+}
+uint32_t* used_base(hq_ctx* c, int par, int Ps) {
+    return c->d_used_mask.as<uint32_t>() + (size_t)par * rank_blocks(c) * kUsedSlots * used_stride(Ps);
+}
+uint64_t* acc_set(hq_ctx* c, int par, int P) { return acc_base(c, par, P) + (size_t)own_block(c) * acc_words(P); }
 uint32_t* used_set(hq_ctx* c, int par, int Ps) {
-    return c->d_used_mask.as<uint32_t>() + (size_t)par * kUsedSlots * used_stride(Ps);
+    return used_base(c, par, Ps) + (size_t)own_block(c) * kUsedSlots * used_stride(Ps);
 }
 
 GridArgs grid_args(hq_ctx* c, int P, int K, int so = 0) {
@@ -710,10 +747,7 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
             1, std::min<int64_t>(std::max(1, c->num_cu / ngr), (g.n_ext + 4095) / 4096));
     }
     const float inv[3] = {1.0f / c->illum[0], 1.0f / c->illum[1], 1.0f / c->illum[2]};
-    // chunked palettes: the 16 x 128 tiles at HB = 10 (else the generic path)
-    const bool fast = c->cost_variant == 0 && c->fast_hb > 0 && !c->pal_generic &&
-                      (nch == 1 || (nch <= kMaxNchFast && c->fast_hb == 10 && c->cost_rows == 16 &&
-                                    c->cost_tw == 128));
+    const bool fast = cost_fast(c);
     // 8-row tiles (cost_mfma_kernel) exist for the 21-tap bucket only
     const int rows = c->fast_hb == 10 ? c->cost_rows : 16;
     const int tw = c->fast_hb == 10 ? c->cost_tw : 128;  // 256-column tiles: HB = 10 only
@@ -764,7 +798,19 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
         // the collective's time (profiling only: an event record between launches
         // idles the GPU a few us, so the timed pass of bench.py records none)
         if (ev) HIP_TRY(c, hipEventRecord(ev[10], s));
-        if (c->psplit) {  // every rank's slice to every rank (in place; one rank: a no-op)
+        if (fold) {
+            // row blocks under a folding search: every rank's counter block and
+            // used-bit block to every rank (in place), one group of two
+            // all-gathers; the accept step sums the integer counters and ORs the
+            // bits of all the blocks itself
+            const size_t na = acc_words(Pl), nu = (size_t)kUsedSlots * used_stride(Ps);
+            NCCL_TRY(c, ncclGroupStart());
+            NCCL_TRY(c, ncclAllGather(acc_set(c, c->acc_par, Pl), acc_base(c, c->acc_par, Pl), na, ncclUint64,
+                                      c->comm, s));
+            NCCL_TRY(c, ncclAllGather(used_set(c, c->acc_par, Ps), used_base(c, c->acc_par, Ps), nu, ncclUint32,
+                                      c->comm, s));
+            NCCL_TRY(c, ncclGroupEnd());
+        } else if (c->psplit) {  // every rank's slice to every rank (in place; one rank: a no-op)
             NCCL_TRY(c, ncclAllGather(c->d_out.as<double>() + (int64_t)lo * (1 + K), c->d_out.p,
                                       (size_t)Pl * (1 + K), ncclFloat64, c->comm, s));
         } else {  // also with one rank (a no-op copy), so that path is exercised on one GPU
@@ -871,11 +917,12 @@ int eval_partial_into_hout(hq_ctx* c, const float* palettes, int P, int K) {
     // them) take the exhaustive K > 256 path instead, which keeps the
     // reference's NaN semantics across all K colours.
     c->nch_cur = c->chunked && fits && c->G2 > 0 && K > kMaxK && K <= kMaxKChunked ? chunk_count(K) : 1;
-    if ((rc = ensure_population(c, P, K))) return rc;
-    if (c->nch_cur > 1) pack_chunks(palettes, P, K, c->nch_cur, c->h_pal);
-    else std::memcpy(c->h_pal, palettes, sizeof(float) * 4 * (size_t)P * K);
-    c->pal_generic = !fits;
-    rc = enqueue_eval(c, P, K);
+    c->pal_generic = !fits;  // (before ensure_population: it sizes the generic path's scratch)
+    if (!(rc = ensure_population(c, P, K))) {
+        if (c->nch_cur > 1) pack_chunks(palettes, P, K, c->nch_cur, c->h_pal);
+        else std::memcpy(c->h_pal, palettes, sizeof(float) * 4 * (size_t)P * K);
+        rc = enqueue_eval(c, P, K);
+    }
     c->pal_generic = false;  // device-resident searches generate clamped palettes
     c->nch_cur = 1;
     return rc;
@@ -926,10 +973,12 @@ SaArgs sa_args(hq_search* s, bool accept, bool init, bool generate, bool random,
     a.generate = generate;
     a.random = random;
     a.convergence = s->prm.convergence;
-    a.acc = acc_set(c, c->acc_par, a.P);
-    a.used_glob = used_set(c, c->acc_par, a.P * s->nch);
+    a.acc = acc_base(c, c->acc_par, a.P);
+    a.used_glob = used_base(c, c->acc_par, a.P * s->nch);
     a.used_stride = used_stride(a.P * s->nch);
     a.fold = s->fold;
+    a.nranks = rank_blocks(c);
+    a.acc_rank_words = (int64_t)acc_words(a.P);
     return a;
 }
 
@@ -964,9 +1013,13 @@ int device_search_create(hq_ctx* c, const hq_swasa_params* params, int K, uint64
     const int P = params->population;
     s->prm = *params;
     s->P = P;
-    // no communicator: nothing has to see the finalized sums, so the accept
-    // step reads the fixed-point sums itself (one launch less per iteration)
-    s->fold = !c->comm;
+    // no communicator, or row blocks: nothing has to see the finalized sums, so
+    // the accept step reads the fixed-point sums itself (one launch less per
+    // iteration; row blocks: one all-gather of every rank's counter blocks in
+    // place of finalize + the all-reduce of P (1 + K) doubles).  The palette
+    // split all-gathers finalized rows.
+    s->fold = search_folds(c);
+    s->comm = c->comm;
     if (c->slice_ranks > 1 && !c->comm)
         return fail(c, HQ_ERR_STATE, "palette slice without a communicator (test option): no search");
     s->pol = new Swasa(*params, seed);
@@ -999,6 +1052,10 @@ int device_search_create(hq_ctx* c, const hq_swasa_params* params, int K, uint64
     const uint64_t s0 = (seed ^ mult) & mask;  // JavaRandom::set_seed
     HIP_TRY(c, hipMemcpy(s->seed[0].p, &s0, sizeof s0, hipMemcpyHostToDevice));
     HIP_TRY(c, hipMemset(s->err[0].p, 0, sizeof(double) * P));
+    if (rank_blocks(c) > 1 && !c->comm) {  // test layout: the blocks no rank fills read zero
+        HIP_TRY(c, hipMemsetAsync(c->d_acc.p, 0, c->d_acc.bytes, c->stream));
+        HIP_TRY(c, hipMemsetAsync(c->d_used_mask.p, 0, c->d_used_mask.bytes, c->stream));
+    }
     for (int i = 0; i < 2; ++i) HIP_TRY(c, hipMemset(s->best_err[i].p, 0, sizeof(double)));
     s->st = s->cd = 0;
     // IM:385-493: random population (SW:40-52), its evaluation, argmin
@@ -1022,8 +1079,9 @@ int device_search_run(hq_search* s, int iterations, int* ran) {
         return fail(c, HQ_ERR_UNSUPPORTED, "CIEDE2000 is unimplemented in the reference (CL:227-230)");
     const NchScope scope(c, s->nch);
     if ((rc = ensure_population(c, s->P, s->K))) return rc;
-    if (s->fold && c->comm)
-        return fail(c, HQ_ERR_STATE, "communicator set after hq_search_create: recreate the search");
+    if (s->comm != c->comm || s->fold != search_folds(c))
+        return fail(c, HQ_ERR_STATE, "communicator or palette split changed after hq_search_create: "
+                                     "recreate the search");
     const bool prof = c->prof;
     if (prof && (rc = ensure_events(s, (size_t)kProfEvents * iterations))) return rc;
     // option sa_graph: the run's kernels go into one hipGraph (stream capture),
@@ -1137,8 +1195,10 @@ int hq_create(int device, int delta_e_type, hq_ctx** out) {
         return HQ_ERR_DEVICE;
     }
     hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) {
         c->num_cu = prop.multiProcessorCount;
+        c->lds_optin = std::max(prop.sharedMemPerBlockOptin, prop.sharedMemPerBlock);
+    }
     for (int ng = 1; ng <= 4; ++ng) c->assign_res[ng] = assign_residency(ng);
     c->assign_res_chunked = assign_residency_chunked();
     for (auto& e : c->ev) (void)hipEventCreate(&e);
@@ -1700,9 +1760,20 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
         // (checked against slice_ranks again at each evaluation: the options may come in either order)
         if (value < 0) return fail(c, HQ_ERR_ARG, "slice_rank must be >= 0");
         c->slice_rank = value;
+    } else if (!std::strcmp(name, "fold_blocks")) {
+        if (value < 1 || value > 64) return fail(c, HQ_ERR_ARG, "fold_blocks in [1, 64]");
+        c->fold_blocks = value;
+        c->fold_block = 0;
+    } else if (!std::strcmp(name, "fold_block")) {
+        if (value < 0 || value >= c->fold_blocks) return fail(c, HQ_ERR_ARG, "fold_block in [0, fold_blocks)");
+        c->fold_block = value;
     } else if (!std::strcmp(name, "lists16")) {
         if (value < 0 || value > 2) return fail(c, HQ_ERR_ARG, "lists16: 0, 1 or 2");
         c->lists16 = (int)value;
+        if (!value) {  // (the lists' 10 MiB per palette are re-allocated when turned on again)
+            c->d_l1n.release();
+            c->d_l2n.release();
+        }
     } else if (!std::strcmp(name, "chunked")) {
         c->chunked = value != 0;
     } else if (!std::strcmp(name, "pixel_err")) {

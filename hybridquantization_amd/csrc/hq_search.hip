@@ -6,6 +6,9 @@
 #include "hq_device.h"
 #include "hq_launch.h"
 
+#include <mutex>
+#include <unordered_map>
+
 namespace hq {
 
 // ----------------------------------------------------------------------------
@@ -169,25 +172,31 @@ __device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared
         for (int j = 0; j < MAXW; ++j) {
             const int e = tid + nt * j;
             if (e < wpp * P) {
-                uint32_t wv[kUsedSlots];
+                // every rank's kUsedSlots copies (row-block ranks: consecutive blocks)
+                for (int r = 0; r < a.nranks; ++r) {
+                    const uint32_t* u = a.used_glob + (int64_t)r * kUsedSlots * a.used_stride + e;
+                    uint32_t wv[kUsedSlots];
 #pragma unroll
-                for (int sl = 0; sl < kUsedSlots; ++sl) wv[sl] = a.used_glob[sl * a.used_stride + e];
+                    for (int sl = 0; sl < kUsedSlots; ++sl) wv[sl] = u[sl * a.used_stride];
 #pragma unroll
-                for (int sl = 0; sl < kUsedSlots; ++sl) fold_word[j] |= wv[sl];
+                    for (int sl = 0; sl < kUsedSlots; ++sl) fold_word[j] |= wv[sl];
+                }
             }
         }
         // palette pp's sum: lanes 16 pp .. 16 pp + 15 load its kAccSlots slot
-        // counters and add them across the lanes (integers: in any order,
-        // acc_total's value)
+        // counters (of every rank) and add them across the lanes (integers: in
+        // any order, acc_total's value)
         static_assert(kAccSlots == 16, "one 16-lane group per palette");
         for (int e0 = 0; e0 < P * kAccSlots; e0 += nt) {
             const int e = e0 + tid, pp = e >> 4, sl = e & 15;
             unsigned long long lo = 0, hi = 0, bad = 0;
             if (e < P * kAccSlots) {
-                const uint64_t* q = a.acc + ((int64_t)sl * acc_pitch(P) + pp) * 4;
-                lo = q[0];
-                hi = q[1];
-                bad = q[2];
+                for (int r = 0; r < a.nranks; ++r) {
+                    const uint64_t* q = a.acc + r * a.acc_rank_words + ((int64_t)sl * acc_pitch(P) + pp) * 4;
+                    lo += q[0];
+                    hi += q[1];
+                    bad += q[2];
+                }
             }
 #pragma unroll
             for (int m = 8; m >= 1; m >>= 1) {
@@ -876,6 +885,17 @@ __global__ __launch_bounds__(1024) void finalize_kernel(FinalizeArgs a) {
 // Launchers
 // ----------------------------------------------------------------------------
 thread_local hipEvent_t t_ev_start = nullptr, t_ev_stop = nullptr;
+
+bool allow_dyn_lds(const void* fn, size_t bytes) {
+    static std::mutex mu;
+    static std::unordered_map<const void*, size_t> granted;
+    const std::lock_guard<std::mutex> lock(mu);
+    size_t& g = granted[fn];
+    if (bytes <= g) return true;
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess) return false;
+    g = bytes;
+    return true;
+}
 void set_launch_events(hipEvent_t start, hipEvent_t stop) {
     t_ev_start = start;
     t_ev_stop = stop;

@@ -133,8 +133,8 @@ def test_bench_gpus_1_prints_one_line(gpu):
     r = _bench(["--gpus", "1", "--steps", "3", "--warmup", "1", "--size", "256", "--K", "16",
                 "--population", "2", "--no-cpu-baseline", "--no-full-search"])
     assert r.returncode == 0, r.stderr[-3000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout  # stdout carries the line and nothing else
     d = json.loads(lines[0])
     assert d["n_gpus"] == 1 and d["steps"] == 3 and d["value"] > 0
     assert d["split"] == "none" and d["rccl_ranks"] == 0 and "launcher" not in d
@@ -152,3 +152,20 @@ def test_bench_launcher_refuses_more_gpus_than_visible(gpu):
                 "--no-cpu-baseline", "--no-full-search"], timeout=200)
     assert r.returncode == 2
     assert f"only {n.value} GPU(s) visible" in r.stderr
+
+
+def test_bench_shard_with_comm_keeps_stdout_to_one_line(gpu):
+    """A shard step with a one-rank RCCL communicator (--shard-comm): RCCL prints
+    its version banner to stdout at communicator set-up; bench.py routes native
+    output to stderr so stdout stays the one JSON line.  The step carries the
+    collective ("comm" timed) and the communicator reports one rank."""
+    import json
+
+    r = _bench(["--steps", "3", "--warmup", "1", "--size", "512", "--K", "16", "--population", "2",
+                "--shard-of", "2", "--shard-comm", "--no-cpu-baseline", "--no-full-search"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["rccl_ranks"] == 1 and d["config"]["shard_comm"] is True
+    assert d["kernel_avg_ms"]["comm"] > 0 and d["kernel_avg_ms"]["finalize"] == 0

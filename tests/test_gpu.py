@@ -984,9 +984,10 @@ def test_device_search_de94_nan_costs(gpu, filt, P):
 
 @pytest.mark.parametrize("split", [0, 1])
 def test_device_search_with_single_rank_comm(gpu, filt, split):
-    """The multi-GPU search loop on one GPU: with libhq's RCCL communicator the
-    all-reduce (split 0: row blocks) or the all-gather (split 1: option
-    palette_split) sits between finalize and sa_step in every iteration; with
+    """The multi-GPU search loop on one GPU: with libhq's RCCL communicator
+    split 0 (row blocks) all-gathers every rank's fixed-point counter and
+    used-bit blocks between the cost kernel and sa_step (no finalize), split 1
+    (option palette_split) all-gathers finalized rows after finalize; with
     one rank the trajectory must be the one without a communicator.  The last
     10 iterations run profiled: the collective is event-timed once per
     iteration ("comm", bench.py's N > 1 line), and only with a communicator."""
@@ -1027,6 +1028,47 @@ def test_device_search_with_single_rank_comm(gpu, filt, split):
     assert res[0][2] == res[1][2] == 40
     assert res[0][1] == res[1][1]
     np.testing.assert_array_equal(res[0][0], res[1][0])
+
+
+@pytest.mark.parametrize("K,P", [(24, 4), (600, 3)])
+def test_device_search_folds_rank_blocks(gpu, filt, K, P):
+    """The row-block layout of the counters (one block of fixed-point sums and
+    used bits per rank, each rank filling its own, the accept step summing and
+    OR'ing all of them after the all-gather) on one context: test options
+    fold_blocks / fold_block put this context's block at position r of R and
+    leave the others zero, as an all-gather of ranks that own no pixels would.
+    The device-resident trajectory must be the one of the plain layout at any
+    (R, r), and a host-driven evaluation (finalize of its own block) too."""
+    import ctypes as C
+    w, h = 80, 72
+    R, G, B = o.synthetic_image(w, h, seed=13)
+    lib = hq.load()
+    pals = np.stack([o.synthetic_palette(K, 30 + p) for p in range(P)]).reshape(P, -1)
+    res = []
+    for nb, b in ((1, 0), (2, 1), (3, 0), (8, 5), (8, 7)):
+        m = hq.ImageManipulation(device=gpu)
+        hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
+        m.setImage(o.inline_rgba(R, G, B).reshape(-1), None, w, filt.illum)
+        m.setOption("fold_blocks", nb)
+        m.setOption("fold_block", b)
+        costs = m.computeQuantizationErrorPopulation(pals, 2.0)
+        sw = hq.SWASA(population=P, imax=25, seed=23, t0=0.05)
+        params = sw.params()
+        handle = C.c_void_p()
+        hq._lib.check(lib.hq_search_create(m.ctx, C.byref(params), K, sw.seed, C.byref(handle)), m.ctx)
+        ran = C.c_int()
+        hq._lib.check(lib.hq_search_run(handle, 25, C.byref(ran)), m.ctx)
+        best = np.zeros(4 * K, np.float32)
+        err = C.c_double()
+        it = C.c_int()
+        hq._lib.check(lib.hq_search_best(handle, hq._lib.fptr(best), C.byref(err), C.byref(it)), m.ctx)
+        lib.hq_search_destroy(handle)
+        m.close()
+        res.append((costs, best, err.value, it.value))
+    for r in res[1:]:
+        np.testing.assert_array_equal(r[0], res[0][0])
+        assert r[2] == res[0][2] and r[3] == res[0][3] == 25
+        np.testing.assert_array_equal(r[1], res[0][1])
 
 
 @pytest.mark.parametrize("K,P,ranks,opts", [(64, 8, 2, {}), (64, 8, 4, {}), (256, 12, 3, {}), (600, 4, 2, {}),
