@@ -1,9 +1,7 @@
 // hq_assign.hip -- per-pixel palette index (CL:179-193 argmin, bit-exact)
 // and used-colour bitmask (CL:193) for a population of palettes, through the
 // exact candidate lists of build_grid (hq_search.hip).
-#include <algorithm>
 #include <type_traits>
-#include <vector>
 
 #include "hq_device.h"
 #include "hq_launch.h"
@@ -309,20 +307,12 @@ __device__ __forceinline__ uint32_t cell_u8(uint32_t v, int lg) {
 // 3 last), each comparing its group's winner with the best so far in the
 // distance scratch; PASS 0 is a single pass (nch <= 4) and the only one that
 // records used bits (nch > 4: used_idx16_kernel from the final indices).
-// BIN (cell-binned pixels, option assign_bin; U8, CMB = 1, PASS = 0): the
-// thread's sequence runs over the pixels in level-2 cell order (AssignArgs::bin:
-// position, packed RGB), so a wave's lanes share one or two cells -- their
-// level-2 lines are one or two L1 lines, their candidate walks as long as those
-// cells' lists, their palette reads LDS broadcasts -- and the indices are stored
-// at each pixel's position: four scattered bytes (BIN 1) or one dword of the
-// group's four indices into idx4 (BIN 2).
-template <int NG, bool U8, int CMB = 1, int PASS = 0, int BIN = 0>
+template <int NG, bool U8, int CMB = 1, int PASS = 0>
 #ifndef HQ_ASSIGN_WAVES
 #define HQ_ASSIGN_WAVES 1
 #endif
 __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(AssignArgs a, int grp0, int ngroups) {
     static_assert(NG % CMB == 0 && (CMB == 4 || PASS == 0), "combine sets inside the group; passes: 4 chunks");
-    static_assert(BIN == 0 || (U8 && CMB == 1 && PASS == 0), "binned pixels: packed 8-bit images, K <= 256");
     // [NG][kMaxK]: a fixed palette stride, so each palette's base folds into the
     // ds_read_b128 offset field and a candidate's address is its byte << 4
     __shared__ __attribute__((aligned(16))) float4 s_pal[NG * kMaxK];
@@ -366,17 +356,11 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
     // PASS >= 2: the best reference distance of the earlier passes, per pixel of
     // the group's palette (loaded with the pixel's RGB)
     const float* dist_in = PASS >= 2 ? a.dist + (int64_t)((4 * grp) >> a.lg_nch) * a.idx_pitch : nullptr;
-    // [NB]: loads in flight, values of pixels being resolved: PASS >= 2 the
-    // distance so far (float bits), BIN the pixel's position
-    uint32_t pdl[3], pdv[3];
-    auto load_rgb = [&](uint32_t q, RawPx<U8>& x, uint32_t& pd) {
+    float pdl[3], pdv[3];  // [NB]: loads in flight, values of pixels being resolved
+    auto load_rgb = [&](uint32_t q, RawPx<U8>& x, float& pd) {
         const uint32_t qc = min(q, qlast);
-        if constexpr (PASS >= 2) pd = __float_as_uint(at(dist_in, qc));
-        if constexpr (BIN) {
-            const uint2 e = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(a.bin) + (qc << 3));
-            pd = e.x;
-            x.v = e.y;
-        } else if constexpr (U8) {
+        if constexpr (PASS >= 2) pd = at(dist_in, qc);
+        if constexpr (U8) {
             x.v = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(a.rgbx) + (qc << 2));
         } else {
             x.r = at(a.R, qc);
@@ -507,23 +491,7 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
             kk[pp] = k1[0];
         }
 #endif
-        if constexpr (BIN) {
-            // a binned pixel's indices at its own position (scattered)
-            const uint32_t pos = pdv[h];
-            if (q < n_ext) {
-                if constexpr (BIN == 2) {
-                    uint32_t v = 0u;
-#pragma unroll
-                    for (int pp = 0; pp < NG; ++pp) v |= (uint32_t)kk[pp] << (8 * pp);
-                    a.idx4[(int64_t)grp * (int64_t)((n_ext + 3u) & ~3u) + pos] = v;
-                } else {
-#pragma unroll
-                    for (int pp = 0; pp < NG; ++pp) idx_base[pp][pos] = (uint8_t)kk[pp];
-                }
-#pragma unroll
-                for (int pp = 0; pp < NG; ++pp) s_usedb[pp][kk[pp]] = 1;
-            }
-        } else if constexpr (CMB == 1) {
+        if constexpr (CMB == 1) {
 #pragma unroll
             for (int pp = 0; pp < NG; ++pp) {
                 const int k = kk[pp];
@@ -555,7 +523,7 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
                 const int64_t pal = (int64_t)((p0 + s0) >> a.lg_nch);
                 if (q < n_ext) {
                     bool win = true;
-                    if constexpr (PASS >= 2) win = best < __uint_as_float(pdv[h]);  // earlier chunks first: strict <
+                    if constexpr (PASS >= 2) win = best < pdv[h];  // earlier chunks first: strict <
                     if (win) __builtin_nontemporal_store(gidx, a.idx16 + pal * a.idx_pitch + q);
                     if constexpr (PASS == 1 || PASS == 2)
                         if (win) a.dist[pal * a.idx_pitch + q] = best;
@@ -647,51 +615,6 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
 }
 
 // ----------------------------------------------------------------------------
-// Cell-binned pixels (option assign_bin): a counting sort of the extended
-// rows' packed pixels by level-2 cell (cell_u8), once per image and grid.
-// The order inside a cell is whatever the atomics give: every pixel is
-// resolved on its own and stored at its own position, so the results do not
-// depend on it.
-// ----------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void bin_count_kernel(const uint32_t* rgbx, int64_t n, int lg, uint32_t* cnt) {
-    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n; q += (int64_t)gridDim.x * 256)
-        atomicAdd(&cnt[cell_u8(rgbx[q], lg)], 1u);
-}
-
-__global__ __launch_bounds__(256) void bin_scatter_kernel(const uint32_t* rgbx, int64_t n, int lg, uint32_t* cursor,
-                                                          uint2* bin) {
-    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n; q += (int64_t)gridDim.x * 256) {
-        const uint32_t v = rgbx[q];
-        const uint32_t j = atomicAdd(&cursor[cell_u8(v, lg)], 1u);
-        bin[j] = make_uint2((uint32_t)q, v);
-    }
-}
-
-// assign_bin 2: the interleaved indices ([group][n_ext] dwords, byte pp =
-// palette 4 group + pp) into the palettes' planes, 4 pixels per thread (one
-// 16-B load, one dword store per palette; the planes' pitch holds the
-// rounded-up tail).
-__global__ __launch_bounds__(256) void idx4_split_kernel(const uint32_t* idx4, uint8_t* idx, int64_t n_ext,
-                                                         int64_t idx_pitch, int P) {
-    const int g = blockIdx.y, npal = min(4, P - 4 * g);
-    const int64_t n4 = (n_ext + 3) / 4;
-    const uint4* src = reinterpret_cast<const uint4*>(idx4 + (int64_t)g * ((n_ext + 3) & ~3ll));
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-        const uint4 v = src[i];
-#pragma unroll
-        for (int pp = 0; pp < 4; ++pp) {
-            if (pp < npal) {
-                // byte pp of each of the 4 dwords -> one dword (v_perm pairs)
-                const uint32_t sel = 0x0c0c0400u + 0x0101u * (uint32_t)pp;  // bytes pp of (lo, hi)
-                const uint32_t lo = __builtin_amdgcn_perm(v.y, v.x, sel);    // (x_pp, y_pp, 0, 0)
-                const uint32_t hi = __builtin_amdgcn_perm(v.w, v.z, sel);    // (z_pp, w_pp, 0, 0)
-                reinterpret_cast<uint32_t*>(idx + (int64_t)(4 * g + pp) * idx_pitch)[i] = lo | (hi << 16);
-            }
-        }
-    }
-}
-
-// ----------------------------------------------------------------------------
 // used_idx16: grid (blocks, P), block 256 (nch > 4 only: the passes leave the
 // used bits to this kernel).  Used bits of palette p from its final 16-bit
 // indices (CL:193): an LDS bitmap per workgroup, OR'ed into used copy
@@ -721,41 +644,6 @@ __global__ __launch_bounds__(256) void used_idx16_kernel(AssignArgs a) {
 // whole groups; nch = 8, 16 run nch / 4 passes (groups j, j + nch / 4, ...),
 // then used_idx16.
 // ----------------------------------------------------------------------------
-// Binned pixels (a.bin, K <= 256): the full groups in one launch, the last
-// group of P mod 4 in a second; assign_bin 2 then splits the interleaved
-// indices into the planes (the profiling events bracket all of it).
-template <int BIN>
-void launch_assign_bin(const AssignArgs& a0, int P, hipStream_t s) {
-    const hipEvent_t ev0 = t_ev_start, ev1 = t_ev_stop;
-    AssignArgs a = a0;
-    a.gstep = 1;
-    const int full = P / 4, rest = P % 4;
-    const bool tail = rest || BIN == 2;
-#define HQ_ASGB(NG, NB, G0, NGR) \
-    HQ_LAUNCH((assign_pipe_kernel<NG, true, 1, 0, BIN>), dim3((unsigned)(NB)), dim3(256), 0, s, a, G0, NGR)
-    if (full > 0) {
-        if (tail) t_ev_stop = nullptr;
-        HQ_ASGB(4, a.nblocks * full, 0, full);
-        t_ev_start = nullptr;
-    }
-    if (rest) t_ev_stop = BIN == 2 ? nullptr : ev1;
-    switch (rest) {
-    case 1: HQ_ASGB(1, a.nblocks, full, 1); break;
-    case 2: HQ_ASGB(2, a.nblocks, full, 1); break;
-    case 3: HQ_ASGB(3, a.nblocks, full, 1); break;
-    default: break;
-    }
-#undef HQ_ASGB
-    if constexpr (BIN == 2) {
-        t_ev_stop = ev1;
-        const unsigned nb = (unsigned)std::min<int64_t>(2048, ((a.n_ext + 3) / 4 + 255) / 256);
-        HQ_LAUNCH(idx4_split_kernel, dim3(nb, (unsigned)((P + 3) / 4)), dim3(256), 0, s, a.idx4, a.idx, a.n_ext,
-                  a.idx_pitch, P);
-    }
-    t_ev_start = ev0;
-    t_ev_stop = ev1;
-}
-
 template <bool U8>
 void launch_assign_t(const AssignArgs& a0, int P, hipStream_t s) {
     const hipEvent_t ev0 = t_ev_start, ev1 = t_ev_stop;
@@ -809,40 +697,9 @@ void launch_used_idx16(const AssignArgs& a, int P, hipStream_t s) {
 }
 
 hipError_t launch_assign(const AssignArgs& a, int P, hipStream_t s) {
-    if (a.bin && a.nch == 1) {
-        if (a.idx4) launch_assign_bin<2>(a, P, s);
-        else launch_assign_bin<1>(a, P, s);
-    } else if (a.rgbx) {
-        launch_assign_t<true>(a, P, s);
-    } else {
-        launch_assign_t<false>(a, P, s);
-    }
+    if (a.rgbx) launch_assign_t<true>(a, P, s);
+    else launch_assign_t<false>(a, P, s);
     return hipGetLastError();
-}
-
-// The cell-binned copy of a packed image's n pixels at grid G2 (bin: n uint2;
-// cnt: G2^3 counters of scratch).  Synchronous (set-up, once per image and grid).
-hipError_t build_pixel_bins(const uint32_t* rgbx, int64_t n, int G2, uint32_t* cnt, uint2* bin, hipStream_t s) {
-    int lg = 0;
-    while ((1 << lg) < G2) ++lg;
-    const size_t ncell = (size_t)G2 * G2 * G2;
-    hipError_t e = hipMemsetAsync(cnt, 0, sizeof(uint32_t) * ncell, s);
-    if (e != hipSuccess) return e;
-    const unsigned nb = (unsigned)std::min<int64_t>(4096, (n + 255) / 256);
-    hipLaunchKernelGGL(bin_count_kernel, dim3(nb), dim3(256), 0, s, rgbx, n, lg, cnt);
-    std::vector<uint32_t> h(ncell);
-    if ((e = hipMemcpyAsync(h.data(), cnt, sizeof(uint32_t) * ncell, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-    uint32_t run = 0;
-    for (size_t c = 0; c < ncell; ++c) {  // exclusive scan: each cell's first slot
-        const uint32_t k = h[c];
-        h[c] = run;
-        run += k;
-    }
-    if ((e = hipMemcpyAsync(cnt, h.data(), sizeof(uint32_t) * ncell, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(bin_scatter_kernel, dim3(nb), dim3(256), 0, s, rgbx, n, lg, cnt, bin);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    return hipStreamSynchronize(s);
 }
 
 // Resident workgroups per CU of assign_pipe_kernel<NG> (the auto size of one
@@ -858,20 +715,6 @@ int assign_residency(int NG) {
     case 2: return std::min(q(assign_pipe_kernel<2, false>), q(assign_pipe_kernel<2, true>));
     case 3: return std::min(q(assign_pipe_kernel<3, false>), q(assign_pipe_kernel<3, true>));
     default: return std::min(q(assign_pipe_kernel<4, false>), q(assign_pipe_kernel<4, true>));
-    }
-}
-
-// The same for the binned forms (option assign_bin, both index layouts).
-int assign_residency_bin(int NG) {
-    auto q = [](auto kern) {
-        int n = 0;
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, 256, 0) == hipSuccess ? n : 0;
-    };
-    switch (NG) {
-    case 1: return std::min(q(assign_pipe_kernel<1, true, 1, 0, 1>), q(assign_pipe_kernel<1, true, 1, 0, 2>));
-    case 2: return std::min(q(assign_pipe_kernel<2, true, 1, 0, 1>), q(assign_pipe_kernel<2, true, 1, 0, 2>));
-    case 3: return std::min(q(assign_pipe_kernel<3, true, 1, 0, 1>), q(assign_pipe_kernel<3, true, 1, 0, 2>));
-    default: return std::min(q(assign_pipe_kernel<4, true, 1, 0, 1>), q(assign_pipe_kernel<4, true, 1, 0, 2>));
     }
 }
 

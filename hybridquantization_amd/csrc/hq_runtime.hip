@@ -31,11 +31,9 @@ hipError_t launch_sa_step(const SaArgs&, hipStream_t);
 void set_launch_events(hipEvent_t start, hipEvent_t stop);
 hipError_t launch_build_grid(const GridArgs&, int P, hipStream_t);
 hipError_t launch_assign(const AssignArgs&, int P, hipStream_t);
-hipError_t build_pixel_bins(const uint32_t* rgbx, int64_t n, int G2, uint32_t* cnt, uint2* bin, hipStream_t s);
 hipError_t launch_lists16_grid(const Lists16Args&, int P, hipStream_t);
 hipError_t launch_assign16(const AssignArgs&, int P, hipStream_t);
 int assign_residency(int NG);
-int assign_residency_bin(int NG);
 int assign_residency_chunked();
 hipError_t launch_cost_chunked(const CostArgs&, int P, int nch, int de, bool trim, hipStream_t);
 void fast_tile_dims(int W, int own_rows, int tile_rows, int tile_w, int* tiles_x, int* ntiles);
@@ -175,7 +173,6 @@ struct hq_ctx {
                                    // thread a grid-stride pixel sequence
     int assign_res[5] = {};   // [NG]
     int assign_res_chunked = 0;  // the chunk-combining forms (NG = 4)
-    int assign_res_bin[5] = {};  // the binned forms (option assign_bin), [NG]
     int psplit = 0;        // with a communicator of N ranks and the whole image on every rank: rank r
                            // evaluates palettes [r P/N, (r+1) P/N), then one all-gather (option
                            // "palette_split"; SURVEY 8e's split of large populations)
@@ -186,10 +183,6 @@ struct hq_ctx {
     int chunked = 1;       // 256 < K <= 16384: palettes as 256-colour chunks through the grid and
                            // tiled kernels (option "chunked"; 0 = the exhaustive K > 256 path)
     int img_u8_path = 1;   // assign reads the packed 8-bit image when there is one (option 'img_u8')
-    int assign_bin = 0;    // assign over cell-binned pixels (K <= 256, packed images): 1 = indices stored
-                           // as scattered bytes, 2 = as interleaved dwords split into the planes after
-    DevBuf d_bin, d_bincnt, d_idx4;  // the binned pixels [n_ext] (position, packed RGB), cell counters
-    int bin_G2 = 0;                  // the grid d_bin was sorted for (0: none / stale)
     int shard_solo = 0;    // experiment: a sharded search without a communicator (per-rank timing)
     int sa_device = 1;     // hq_search_*: 1 = SWASA iterations resident on the device (no host
                            // round trip per iteration), 0 = host-driven (one eval call each)
@@ -369,7 +362,6 @@ int set_image_common(hq_ctx* c, const std::vector<float>& R, const std::vector<f
         flag.release();
         c->img_u8 = not_u8 == 0;
         if (!c->img_u8) c->d_rgbx.release();
-        c->bin_G2 = 0;  // the binned copy follows the image
     }
     if (illum) std::memcpy(c->illum, illum, sizeof c->illum);
     const int own = g.r1 - g.r0;
@@ -422,12 +414,6 @@ int check_geom_args(hq_ctx* c, int w, int h, int r0, int r1) {
 // of workgroups, makes each thread's pixel sequence a grid stride: every thread
 // gets the same number of pixels +-1 (512-row shard 0.1306 -> 0.1261 ms per
 // step vs 4 pixels per chunk at 16 workgroups per CU; 4096^2 unchanged).
-// assign over cell-binned pixels (option assign_bin): packed 8-bit images,
-// K <= 256 (one chunk), the pruned grid.
-bool use_bins(const hq_ctx* c) {
-    return c->assign_bin > 0 && c->img_u8 && c->img_u8_path && c->nch_cur == 1 && c->G2 > 0;
-}
-
 #ifndef HQ_ASSIGN_MINPX
 #define HQ_ASSIGN_MINPX 6
 #endif
@@ -439,7 +425,7 @@ int assign_blocks(const hq_ctx* c, int P) {
     // workgroups, slowed from 43 to 46 us at 8)
     const int64_t chunk = 256 * HQ_ASSIGN_MINPX;
     const int ng = std::min(P, 4);
-    const int res = c->nch_cur > 1 ? c->assign_res_chunked : use_bins(c) ? c->assign_res_bin[ng] : c->assign_res[ng];
+    const int res = c->nch_cur > 1 ? c->assign_res_chunked : c->assign_res[ng];
     const int per_cu = c->assign_blocks_per_cu > 0 ? c->assign_blocks_per_cu : res > 0 ? res : 4;
     const int64_t nblocks = (int64_t)c->num_cu * per_cu;
     return (int)std::max<int64_t>(1, std::min<int64_t>(nblocks, (c->g.n_ext + chunk - 1) / chunk));
@@ -524,17 +510,6 @@ int ensure_population(hq_ctx* c, int P, int K) {
     // the generic path's [7][n_ext] scratch, here rather than at its first launch: an
     // allocation cannot happen while a search run is being captured into a graph
     if (!cost_fast(c) || K > kMaxK) HIP_TRY(c, c->d_gen_t.ensure(sizeof(float) * 7 * (size_t)g.n_ext + 256));
-    if (use_bins(c)) {  // (set-up: once per image and grid, before any capture)
-        if (c->bin_G2 != c->G2) {
-            HIP_TRY(c, c->d_bin.ensure(sizeof(uint2) * (size_t)g.n_ext));
-            HIP_TRY(c, c->d_bincnt.ensure(sizeof(uint32_t) * (size_t)c->G2 * c->G2 * c->G2));
-            HIP_TRY(c, build_pixel_bins(c->d_rgbx.as<uint32_t>(), g.n_ext, c->G2, c->d_bincnt.as<uint32_t>(),
-                                        c->d_bin.as<uint2>(), c->stream));
-            c->bin_G2 = c->G2;
-        }
-        if (c->assign_bin == 2)
-            HIP_TRY(c, c->d_idx4.ensure(sizeof(uint32_t) * (size_t)((P + 3) / 4) * (size_t)((g.n_ext + 3) & ~3ll)));
-    }
     return ensure_pinned(c, sizeof(float) * 4 * (size_t)P * K, sizeof(double) * (size_t)P * (1 + K));
 }
 
@@ -760,10 +735,6 @@ int enqueue_core(hq_ctx* c, int P, int K, const hipEvent_t* ev, bool fold = fals
         aa.dist = nch > 4 ? c->d_dist.as<float>() : nullptr;
         aa.nch = nch;
         while ((1 << aa.lg_nch) < nch) ++aa.lg_nch;
-    }
-    if (use_bins(c) && !n16) {
-        aa.bin = c->d_bin.as<uint2>();
-        aa.idx4 = c->assign_bin == 2 ? c->d_idx4.as<uint32_t>() : nullptr;
     }
     if (n16) {  // one palette of K colours per workgroup (its table in LDS)
         aa.l1n = c->d_l1n.as<uint16_t>();
@@ -1229,7 +1200,6 @@ int hq_create(int device, int delta_e_type, hq_ctx** out) {
         c->lds_optin = std::max(prop.sharedMemPerBlockOptin, prop.sharedMemPerBlock);
     }
     for (int ng = 1; ng <= 4; ++ng) c->assign_res[ng] = assign_residency(ng);
-    for (int ng = 1; ng <= 4; ++ng) c->assign_res_bin[ng] = assign_residency_bin(ng);
     c->assign_res_chunked = assign_residency_chunked();
     for (auto& e : c->ev) (void)hipEventCreate(&e);
     *out = c;
@@ -1244,7 +1214,7 @@ void hq_destroy(hq_ctx* c) {
     for (DevBuf* b : {&c->d_k1, &c->d_k2, &c->d_k3, &c->d_absk3, &c->d_vtaps, &c->d_R, &c->d_G, &c->d_B, &c->d_rgbx,
                       &c->d_labL, &c->d_labA, &c->d_labB, &c->d_pal_in, &c->d_pal, &c->d_opp, &c->d_opp16,
                       &c->d_dup, &c->d_pflags, &c->d_lvl1, &c->d_lvl2, &c->d_idx,
-                      &c->d_used_mask, &c->d_acc, &c->d_out, &c->d_gen_t, &c->d_bin, &c->d_bincnt, &c->d_idx4, &c->d_taps,
+                      &c->d_used_mask, &c->d_acc, &c->d_out, &c->d_gen_t, &c->d_taps,
                       &c->d_vfrag16, &c->d_vfrag16p, &c->d_vfragm, &c->d_htaps, &c->d_idx32, &c->d_used32, &c->d_pixerr, &c->d_idx16, &c->d_dist, &c->d_l1n, &c->d_l2n})
         b->release();
     if (c->h_pal) (void)hipHostFree(c->h_pal);
@@ -1810,9 +1780,6 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
         c->pixel_err = value != 0;
     } else if (!std::strcmp(name, "img_u8")) {
         c->img_u8_path = value != 0;
-    } else if (!std::strcmp(name, "assign_bin")) {
-        if (value < 0 || value > 2) return fail(c, HQ_ERR_ARG, "assign_bin: 0, 1 or 2");
-        c->assign_bin = (int)value;
     } else if (!std::strcmp(name, "assign_blocks_per_cu")) {
         if (value < 0 || value > 64) return fail(c, HQ_ERR_ARG, "assign_blocks_per_cu in [0,64] (0 = auto)");
         c->assign_blocks_per_cu = value;

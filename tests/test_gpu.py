@@ -1655,83 +1655,3 @@ def test_pixel_errors_de94_vs_oracle(gpu, case, variant):
             ref = float(np.mean(ex)) + float(np.count_nonzero(~used)) * 2.0
             assert abs(cost - ref) <= 1e-5 * ref, stats
     m.close()
-
-
-@pytest.mark.parametrize("mode", [1, 2])
-@pytest.mark.parametrize("P,G2", [(1, 32), (3, 32), (4, 32), (6, 16), (4, 64)])
-def test_binned_assign_matches_image_order(gpu, filt, mode, P, G2):
-    """Option assign_bin: the pixels in level-2 cell order (a counting sort of
-    the packed image, once per image and grid), indices stored at each pixel's
-    position as scattered bytes (mode 1) or as one dword of the group's four
-    palettes split into the planes afterwards (mode 2).  Indices, used flags
-    and costs equal the image-order assign bit for bit, and the indices equal
-    the oracle's argmin (CL:179-193), on a 517 x 389 image (odd sizes: a ragged
-    tail) that is half noise and half a narrow cluster (long runs in few
-    cells), with palettes holding pixel colours (exact ties) and duplicates;
-    then a second image on the same context (the bins follow the image)."""
-    w, h = 517, 389
-    R, G, B = o.synthetic_image(w, h, seed=40 + P)
-    R[: h // 2] = np.clip(0.4 + 0.05 * (R[: h // 2] - 0.5), 0, 1)
-    R, G, B = ((np.round(x * 255) / 255).astype(np.float32) for x in (R, G, B))
-    rgba = o.inline_rgba(R, G, B)
-    pals = np.stack([o.synthetic_palette(256, 70 + p) for p in range(P)])
-    pals[0, 10:20, :3] = rgba[3000:3010, :3]
-    pals[-1, 200:210, :3] = rgba[3000:3010, :3]
-    pals[-1, 255] = pals[-1, 17]
-    m = _planar_ctx(gpu, R, G, B, w, h, filt.illum)
-    m.setOption("grid", G2)
-    res = {}
-    for b in (0, mode):
-        m.setOption("assign_bin", b)
-        costs, used = m.computeQuantizationErrorPopulation(pals.reshape(P, -1), 2.0, return_used=True)
-        res[b] = (costs, used, [m.getIndices(p) for p in range(P)])
-    np.testing.assert_array_equal(res[mode][0], res[0][0])
-    np.testing.assert_array_equal(res[mode][1], res[0][1])
-    for p in range(P):
-        np.testing.assert_array_equal(res[mode][2][p], res[0][2][p])
-    for p in (0, P - 1):
-        ref_idx, ref_used = c_oracle.assign(rgba, pals[p], nthreads=_threads())
-        np.testing.assert_array_equal(res[mode][2][p], ref_idx.astype(np.uint8))
-        np.testing.assert_array_equal(res[mode][1][p], ref_used)
-    # a new image on the same context: the binned copy is rebuilt
-    R2, G2_, B2 = o.synthetic_image(w, h, seed=99)
-    hq._lib.check(hq.load().hq_set_image_planar_shard(m.ctx, hq._lib.fptr(R2), hq._lib.fptr(G2_),
-                                                      hq._lib.fptr(B2), w, h, hq._lib.fptr(filt.illum), 0, h),
-                  m.ctx)
-    c2, u2 = m.computeQuantizationErrorPopulation(pals.reshape(P, -1), 2.0, return_used=True)
-    i2 = m.getIndices(0)
-    m.setOption("assign_bin", 0)
-    c0, u0 = m.computeQuantizationErrorPopulation(pals.reshape(P, -1), 2.0, return_used=True)
-    np.testing.assert_array_equal(c2, c0)
-    np.testing.assert_array_equal(u2, u0)
-    np.testing.assert_array_equal(i2, m.getIndices(0))
-    m.close()
-
-
-@pytest.mark.parametrize("mode", [1, 2])
-def test_binned_assign_device_search(gpu, filt, mode):
-    """The device-resident search with binned assign follows the image-order
-    search's trajectory exactly (P = 4, K = 256, shard of rows included)."""
-    import ctypes as C
-    w, h, K, P = 192, 160, 256, 4
-    R, G, B = o.synthetic_image(w, h, seed=5)
-    lib = hq.load()
-    res = []
-    for b in (0, mode):
-        m = _planar_ctx(gpu, R, G, B, w, h, filt.illum)
-        m.setOption("assign_bin", b)
-        sw = hq.SWASA(population=P, imax=20, seed=3, t0=0.05)
-        params = sw.params()
-        handle = C.c_void_p()
-        hq._lib.check(lib.hq_search_create(m.ctx, C.byref(params), K, sw.seed, C.byref(handle)), m.ctx)
-        ran = C.c_int()
-        hq._lib.check(lib.hq_search_run(handle, 20, C.byref(ran)), m.ctx)
-        best = np.zeros(4 * K, np.float32)
-        err = C.c_double()
-        it = C.c_int()
-        hq._lib.check(lib.hq_search_best(handle, hq._lib.fptr(best), C.byref(err), C.byref(it)), m.ctx)
-        lib.hq_search_destroy(handle)
-        m.close()
-        res.append((best, err.value, it.value))
-    assert res[0][1:] == res[1][1:]
-    np.testing.assert_array_equal(res[0][0], res[1][0])
