@@ -199,14 +199,6 @@ struct AssignArgs {
     const uint16_t* l1n = nullptr;
     const uint16_t* l2n = nullptr;
     int kpal = 0;
-    // cell-binned pixels (option assign_bin; packed 8-bit images, K <= 256): the
-    // pixels in level-2 cell order as (position, packed RGB), built once per
-    // image and grid (hq_assign.hip bin_*_kernel); the indices then go out
-    // scattered, into the planes (assign_bin 1) or as one dword of the group's 4
-    // palettes per pixel into idx4 [ceil(P/4)][n_ext] (assign_bin 2), split into
-    // the planes by idx4_split_kernel
-    const uint2* bin = nullptr;
-    uint32_t* idx4 = nullptr;
 };
 
 struct CostArgs {
