@@ -33,6 +33,8 @@ for cfg in "--size 1024 --K 64 --population 1" "--population 1" "" "--size 8192 
 done
 timeout -k 10 200 python bench.py --no-cpu-baseline --shard-of 8 --steps 200 > $E/shard8.json 2> $E/shard8.err
 rc=$?; echo "shard8 rc=$rc"; cut -c1-200 $E/shard8.json; fatal $rc shard8
+timeout -k 10 200 python bench.py --no-cpu-baseline --shard-of 8 --shard-comm --steps 200 > $E/shard8_comm.json 2> $E/shard8_comm.err
+rc=$?; echo "shard8 comm rc=$rc"; cut -c1-200 $E/shard8_comm.json; fatal $rc shard8_comm
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 120 rocprofv3 --pmc $c --kernel-include-regex "cost|assign|build_grid|sa_step|finalize" -f csv -d $E/traffic_$c -o run -- python3 scripts/profile_eval.py --evals 3 > $E/traffic_$c.log 2>&1
   rc=$?; echo "$c rc=$rc"; fatal $rc $c
