@@ -1798,177 +1798,6 @@ template __global__ void gen_hmfma_kernel<uint8_t>(GenArgs, int, int);
 template __global__ void gen_hmfma_kernel<uint16_t>(GenArgs, int, int);
 template __global__ void gen_hmfma_kernel<uint32_t>(GenArgs, int, int);
 
-// gen_fused: the matrix-core generic pair in one kernel (halfSize 25 .. 64),
-// without the [7][n_ext] split planes in HBM.  A workgroup owns a 16 NRB x 32
-// output tile; its window is the tile's rows +- half.  In four sub-passes over
-// the filters of one channel -- (f0, f3) and (f6) on x, (f1, f4) on y, (f2, f5)
-// on z, so each channel's vertical results add up in gen_vmfma's filter order
-// -- it runs gen_hmfma's horizontal MFMAs over the window, 16 rows at a time
-// from a segment of split opponent colours (indices and colours for the next
-// strip in flight during the current one), into one or two window planes in
-// LDS (split dwords, row pitch 36: the vertical B reads of the four lane
-// groups, rows 4 apart, hit distinct banks), then gen_vmfma's vertical MFMAs
-// from those planes into the channel's accumulators.  Every horizontal and
-// vertical product and sum is the two-kernel pair's, in the same order: the
-// per-pixel dE is bit-identical (the tile partial sums group pixels
-// differently).  Wave w owns output blocks (row block p / 2, column block p %
-// 2) for p = w, w + 4, ...
-constexpr int kFuW = 32, kFuPP = 36, kFuMaxSeg = 10;  // (segment values per thread: half <= 64)
-static int fused_seg_pitch(int half) {
-    const int c = kFuW - 16 + 16 * ((16 + 2 * half + 15) / 16);
-    return (c - 8 + 63) / 64 * 64 + 8;  // = 8 mod 64: ds_read_b128's lane groups on distinct banks
-}
-// dwords of LDS: the planes, the segment, the sub-pass's horizontal and vertical taps
-static size_t fused_lds_words(int half, int nrb) {
-    const int S = (16 + 2 * half + 15) / 16, TP = 16 * S + 16;
-    const int pr = 16 * ((16 * nrb + 2 * half + 15) / 16);
-    return 2 * (size_t)pr * kFuPP + 16 * (size_t)fused_seg_pitch(half) + 8 * (size_t)TP;
-}
-template <int DE, typename IT, int NRB>
-__global__ __launch_bounds__(256, 2) void gen_fused_kernel(GenArgs a, int tiles_x, int sp_pitch) {
-    extern __shared__ uint32_t s_fu[];
-    constexpr int TW = kFuW, TH = 16 * NRB, PP = kFuPP, NPAIR = 2 * NRB, PPW = (NPAIR + 3) / 4;
-    __shared__ double s_red[4];
-    const int tid = threadIdx.x, lane = tid & 63, n = lane & 15, g = lane >> 4;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const Geom& gm = a.g;
-    const int half = a.half, S = (16 + 2 * half + 15) / 16, TP = 16 * S + 16;
-    const int NST = (TH + 2 * half + 15) / 16, PR = 16 * NST, SEGC = TW - 16 + 16 * S;
-    const int x0 = (blockIdx.x % tiles_x) * TW, y0 = gm.r0 + (blockIdx.x / tiles_x) * TH;
-    uint32_t* const s_pl = s_fu;                         // [2][PR][PP] window planes
-    uint32_t* const s_seg = s_fu + 2 * PR * PP;          // [16][sp_pitch] segment of one strip
-    uint32_t* const s_tap = s_seg + 16 * sp_pitch;       // [slot][h, v][hi, lo][TP]
-    const IT* idx = static_cast<const IT*>(a.idx);
-    const float* opp = reinterpret_cast<const float*>(a.opp);
-    // window row i -> its extended image row (reflected at the image edges, clamped
-    // to the rows held here; rows past the window feed zero taps only)
-    auto img_row = [&](int i) {
-        int gy = reflect_clamp(y0 - half + i, gm.H);
-        gy = min(max(gy, gm.e0), gm.e1 - 1);
-        return gy - gm.e0;
-    };
-    // this thread's segment elements: row er[m] of the strip, image column ec[m]
-    // and its LDS offset so[m] (-1: past the segment)
-    int er[kFuMaxSeg], ec[kFuMaxSeg], so[kFuMaxSeg];
-#pragma unroll
-    for (int m = 0; m < kFuMaxSeg; ++m) {
-        const int e = min(tid + 256 * m, 16 * SEGC - 1);
-        er[m] = e / SEGC;
-        ec[m] = reflect_clamp(x0 - half + e % SEGC, gm.W);
-        so[m] = tid + 256 * m < 16 * SEGC ? er[m] * sp_pitch + e % SEGC : -1;
-    }
-    uint32_t ixr[kFuMaxSeg];
-    float vr[kFuMaxSeg];
-    auto load_idx = [&](int k) {
-#pragma unroll
-        for (int m = 0; m < kFuMaxSeg; ++m) ixr[m] = (uint32_t)idx[(int64_t)img_row(16 * k + er[m]) * gm.W + ec[m]];
-    };
-    auto load_val = [&](int ch) {
-#pragma unroll
-        for (int m = 0; m < kFuMaxSeg; ++m) vr[m] = opp[4 * (size_t)ixr[m] + ch];
-    };
-    f32x4v D[3][PPW];
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch)
-#pragma unroll
-        for (int q = 0; q < PPW; ++q) D[ch][q] = f32x4v{0.f, 0.f, 0.f, 0.f};
-    // sub-passes: (channel, filters)
-    constexpr int kSpCh[4] = {0, 0, 1, 2}, kSpF0[4] = {0, 6, 1, 2}, kSpF1[4] = {3, -1, 4, 5};
-#pragma unroll
-    for (int sp = 0; sp < 4; ++sp) {
-        const int ch = kSpCh[sp], nf = kSpF1[sp] >= 0 ? 2 : 1;
-        load_idx(0);
-        load_val(ch);
-        if (NST > 1) load_idx(1);
-        __syncthreads();  // the previous sub-pass's vertical reads of the planes and taps are done
-        for (int i = tid; i < 2 * 2 * TP * nf; i += 256) {  // [slot][h, v][hi, lo][TP]
-            const int slot = i / (4 * TP), r = i % (4 * TP), hv = r / (2 * TP), w = r % (2 * TP);
-            const int f = slot ? kSpF1[sp] : kSpF0[sp];
-            s_tap[i] = (hv ? a.vtapd : a.htapd)[f * 2 * TP + w];
-        }
-        const int cb = wv & 1, slot = wv >> 1;
-        for (int k = 0; k < NST; ++k) {
-            if (k) __syncthreads();  // strip k - 1's segment reads are done
-#pragma unroll
-            for (int m = 0; m < kFuMaxSeg; ++m)
-                if (so[m] >= 0) s_seg[so[m]] = split_f16(vr[m]);
-            __syncthreads();
-            if (k + 1 < NST) {  // strip k + 1's colours, strip k + 2's indices, in flight
-                load_val(ch);
-                if (k + 2 < NST) load_idx(k + 2);
-            }
-            if (slot < nf) {  // horizontal: plane row 16 k + n, columns 16 cb + 4 g .. + 3
-                const uint32_t* sb = s_seg + n * sp_pitch + 16 * cb + 4 * g;
-                const uint32_t* th = s_tap + slot * 4 * TP + 4 * g - n + 15;
-                f32x4v d = {0.f, 0.f, 0.f, 0.f};
-                for (int st = 0; st < S; ++st) {
-                    const f16x8 B = __builtin_bit_cast(f16x8, *reinterpret_cast<const u32x4*>(sb + 16 * st));
-                    uint4 ah, al;
-                    ah.x = th[16 * st]; ah.y = th[16 * st + 1]; ah.z = th[16 * st + 2]; ah.w = th[16 * st + 3];
-                    al.x = th[TP + 16 * st]; al.y = th[TP + 16 * st + 1]; al.z = th[TP + 16 * st + 2]; al.w = th[TP + 16 * st + 3];
-                    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, ah), B, d, 0, 0, 0);
-                    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, al), B, d, 0, 0, 0);
-                }
-                *reinterpret_cast<uint4*>(s_pl + (slot * PR + 16 * k + n) * PP + 16 * cb + 4 * g) =
-                    make_uint4(split_f16(d[0] * kVOutScale), split_f16(d[1] * kVOutScale),
-                               split_f16(d[2] * kVOutScale), split_f16(d[3] * kVOutScale));
-            }
-        }
-        __syncthreads();  // the window planes are complete
-        // vertical: the wave's output blocks, filter by filter (gen_vmfma's order)
-#pragma unroll
-        for (int q = 0; q < PPW; ++q) {
-            const int p = wv + 4 * q;
-            if (p < NPAIR) {
-                const int rb = p >> 1, cbv = p & 1;
-                for (int sl = 0; sl < nf; ++sl) {
-                    const uint32_t* pl = s_pl + sl * PR * PP + 16 * cbv + n;
-                    const uint32_t* tv = s_tap + sl * 4 * TP + 2 * TP + 4 * g - n + 15;
-                    f32x4v e = {0.f, 0.f, 0.f, 0.f};
-                    for (int st = 0; st < S; ++st) {
-                        const int r = 16 * rb + 16 * st + 4 * g;
-                        u32x4 b;
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) b[j] = pl[(r + j) * PP];
-                        uint4 ah, al;
-                        ah.x = tv[16 * st]; ah.y = tv[16 * st + 1]; ah.z = tv[16 * st + 2]; ah.w = tv[16 * st + 3];
-                        al.x = tv[TP + 16 * st]; al.y = tv[TP + 16 * st + 1]; al.z = tv[TP + 16 * st + 2]; al.w = tv[TP + 16 * st + 3];
-                        const f16x8 B = __builtin_bit_cast(f16x8, b);
-                        e = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, ah), B, e, 0, 0, 0);
-                        e = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, al), B, e, 0, 0, 0);
-                    }
-                    D[ch][q] += e;
-                }
-            }
-        }
-    }
-    double part = 0.0;
-#pragma unroll
-    for (int q = 0; q < PPW; ++q) {
-        const int p = wv + 4 * q;
-        if (p < NPAIR) {
-            const int rb = p >> 1, cbv = p & 1;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int y = y0 + 16 * rb + 4 * g + i, gx = x0 + 16 * cbv + n;
-                if (gx < gm.W && y < gm.r1) {
-                    // (x 2^-30: the data and tap scales, exactly)
-                    const float3 lf = opp2f_fast(D[0][q][i] * kVOutScale, D[1][q][i] * kVOutScale,
-                                                 D[2][q][i] * kVOutScale, a.m_lab);
-                    const int64_t off = (int64_t)(y - gm.r0) * gm.lab_pitch + gx;
-                    const float ef = delta_e_f<DE>(a.labL[off], a.labA[off], a.labB[off], lf);
-                    if (a.pix_err) a.pix_err[(int64_t)(y - gm.r0) * gm.W + gx] = ef;  // test option: the per-pixel dE
-                    part += (double)ef;
-                }
-            }
-        }
-    }
-    part = wave_sum_to_lane63(part);
-    if ((tid & 63) == 63) s_red[tid >> 6] = part;
-    __syncthreads();
-    if (tid == 0) acc_add(a.acc, a.P, a.p, blockIdx.x, (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]));
-}
-
 // (explicit instantiations: taken only through a generic lambda, the dE94
 // kernels' host handles were left undefined by the host compile)
 template __global__ void gen_vmfma_kernel<0, 1>(GenArgs, int);
@@ -1979,16 +1808,6 @@ template __global__ void gen_vtile2_kernel<0, HQ_VT2_RB>(GenArgs, int);
 template __global__ void gen_vtile2_kernel<1, HQ_VT2_RB>(GenArgs, int);
 template __global__ void gen_vtile_kernel<0>(GenArgs, int);
 template __global__ void gen_vtile_kernel<1>(GenArgs, int);
-#define HQ_FUSED_INST(DE, IT) \
-    template __global__ void gen_fused_kernel<DE, IT, 6>(GenArgs, int, int); \
-    template __global__ void gen_fused_kernel<DE, IT, 4>(GenArgs, int, int);
-HQ_FUSED_INST(0, uint8_t)
-HQ_FUSED_INST(1, uint8_t)
-HQ_FUSED_INST(0, uint16_t)
-HQ_FUSED_INST(1, uint16_t)
-HQ_FUSED_INST(0, uint32_t)
-HQ_FUSED_INST(1, uint32_t)
-#undef HQ_FUSED_INST
 
 // ----------------------------------------------------------------------------
 // Host side: tap tables, MFMA fragments, launchers
@@ -2327,26 +2146,6 @@ hipError_t launch_cost_tiled_generic(const GenArgs& a, int de, int idx_bytes, hi
                        : 256;
         }();
         const int rows = a.g.e1 - a.g.e0;
-        if (a.hmfma && a.htapd && a.fused) {
-            // one kernel, no split planes in HBM: 96-row tiles while two workgroups'
-            // LDS fits a CU, else 64
-            const int nrb = 2 * fused_lds_words(a.half, 6) * sizeof(uint32_t) <= 160 * 1024 ? 6 : 4;
-            const size_t l = sizeof(uint32_t) * fused_lds_words(a.half, nrb);
-            const int tx = (a.g.W + kFuW - 1) / kFuW, ty = (a.g.r1 - a.g.r0 + 16 * nrb - 1) / (16 * nrb);
-            const int spp = fused_seg_pitch(a.half);
-            t_ev_stop = ev1;
-            auto gof = [&](auto kern) {
-                if (!allow_dyn_lds(reinterpret_cast<const void*>(kern), l)) return;
-                HQ_LAUNCH(kern, dim3((unsigned)(tx * ty)), dim3(256), l, s, a, tx, spp);
-            };
-#define HQ_GOF(DE, IT) (nrb == 6 ? gof(gen_fused_kernel<DE, IT, 6>) : gof(gen_fused_kernel<DE, IT, 4>))
-            if (idx_bytes == 4) { if (de == 0) HQ_GOF(0, uint32_t); else HQ_GOF(1, uint32_t); }
-            else if (idx_bytes == 2) { if (de == 0) HQ_GOF(0, uint16_t); else HQ_GOF(1, uint16_t); }
-            else { if (de == 0) HQ_GOF(0, uint8_t); else HQ_GOF(1, uint8_t); }
-#undef HQ_GOF
-            t_ev_start = ev0;
-            return hipGetLastError();
-        }
         if (a.hmfma && a.htapd) {  // both passes on the matrix cores
             const int pitch = hmfma_pitch(a.half), S = (16 + 2 * a.half + 15) / 16;
             const size_t hl = sizeof(uint32_t) * (3 * 16 * (size_t)pitch + (size_t)kNumFilt * 2 * (16 * S + 16));

@@ -278,7 +278,6 @@ struct GenArgs {
     int hmfma = 1;       // with vmfma: the horizontal pass on the matrix cores too (gen_hmfma)
     int shape = 0;       // matrix-core pair's tile shapes: 0 by grid size, 1 the short forms, 2 the tall ones
     const uint32_t* htapd = nullptr;  // its taps, the same layout (k3 signed: the horizontal t3 taps)
-    int fused = 1;       // with vmfma + hmfma: both passes in one kernel (gen_fused, no planes in HBM)
     const float4* htaps = nullptr;  // gen_hrow4: [T][2] (k1.xyz, k3), (k2.xyz, 0) horizontal taps
 };
 

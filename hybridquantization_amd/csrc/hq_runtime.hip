@@ -165,7 +165,6 @@ struct hq_ctx {
     int gen_vtile2 = 1;    // tiled generic path: double-buffered LDS-DMA vertical pass (half <= 64)
     int gen_vmfma = 1;     // tiled generic path: the vertical pass on the matrix cores (half <= 64)
     int gen_hmfma = 1;     // ... and the horizontal pass (gen_hmfma) with it
-    int gen_fused = 1;     // ... both passes in one kernel (gen_fused: no split planes in HBM)
     int gen_shape = 0;     // their tile shapes: 0 by grid size, 1 short, 2 tall (option gen_tile_shape)
     int gen_hrow_no = 4;   // tiled generic path: horizontal outputs per thread (4 or 8)
     int sa_graph = HQ_SA_GRAPH;  // device-resident search: each run's kernels as one hipGraph
@@ -598,7 +597,6 @@ int enqueue_generic_cost(hq_ctx* c, int P, const void* idx_base, int idx_bytes, 
         gn.vmfma = c->gen_vmfma && !c->pal_generic;
         gn.vtapd = c->d_vfragm.bytes ? c->d_vfragm.as<uint32_t>() : nullptr;
         gn.hmfma = c->gen_hmfma;
-        gn.fused = c->gen_fused;
         gn.shape = c->gen_shape;
         gn.htapd = gn.vtapd ? gn.vtapd + vtile_dup_tap_words(c->half) : nullptr;
         gn.htaps = c->d_htaps.as<float4>();
@@ -1743,8 +1741,6 @@ int hq_set_option(hq_ctx* c, const char* name, int value) {
         c->gen_shape = (int)value;
     } else if (!std::strcmp(name, "gen_vtile2")) {
         c->gen_vtile2 = value != 0;
-    } else if (!std::strcmp(name, "gen_fused")) {
-        c->gen_fused = value != 0;
     } else if (!std::strcmp(name, "gen_hrow4")) {
         c->gen_hrow4 = value != 0;
     } else if (!std::strcmp(name, "cost_tw")) {

@@ -1655,41 +1655,3 @@ def test_pixel_errors_de94_vs_oracle(gpu, case, variant):
             ref = float(np.mean(ex)) + float(np.count_nonzero(~used)) * 2.0
             assert abs(cost - ref) <= 1e-5 * ref, stats
     m.close()
-
-
-@pytest.mark.parametrize("dpi,dist,K,shard", [(200, 45.0, 64, False), (250, 50.0, 256, False),
-                                              (300, 50.0, 200, False), (300, 60.0, 48, False),
-                                              (300, 50.0, 64, True), (300, 50.0, 10000, False),
-                                              (250, 50.0, 20000, False)])
-def test_fused_generic_matches_pair(gpu, filt, dpi, dist, K, shard):
-    """gen_fused (option gen_fused, default: both matrix-core passes of the
-    generic path in one kernel, window planes in LDS instead of 7 split planes
-    in HBM) against the two-kernel pair (gen_hmfma + gen_vmfma): every pixel's
-    dE bit for bit -- the same products and sums in the same order -- and the
-    cost to 1e-9 (the tiles group the partial sums differently), at halfSize 30,
-    42, 51, 61 (96- and 64-row tiles), on a ragged 333 x 217 image, a row shard
-    (the window rows clamped to the rows held), and 16- / 32-bit index images
-    (K = 10000: 64 chunks; K = 20000: the exhaustive path)."""
-    w, h = 333, 217
-    R, G, B = o.synthetic_image(w, h, seed=K + dpi)
-    rgba = o.inline_rgba(R, G, B).reshape(-1)
-    pals = np.stack([o.synthetic_palette(K, 300 + p) for p in range(2)])
-    r0, r1 = (60, 170) if shard else (0, h)
-    res = {}
-    for fused in (1, 0):
-        m = hq.ImageManipulation(device=gpu)
-        hq.ScielabProcessor(dpi, dist, hq.Whitepoint.D65, None, m)
-        assert m.halfSize > 24
-        m.setImage(rgba, None, w, filt.illum, row_begin=r0, row_end=r1)
-        m.setOption("pixel_err", 1)
-        m.setOption("gen_fused", fused)
-        part = np.zeros(2 * (1 + K))
-        hq._lib.check(hq.load().hq_eval_population_partial(m.ctx, hq._lib.fptr(pals.reshape(2, -1)), 2, K,
-                                                           hq._lib.dptr(part)), m.ctx)
-        res[fused] = (part.reshape(2, 1 + K), [m.getPixelErrors(p) for p in range(2)])
-        m.close()
-    for p in range(2):
-        np.testing.assert_array_equal(res[1][1][p], res[0][1][p])
-        assert np.all(np.isfinite(res[1][1][p]))
-    np.testing.assert_allclose(res[1][0][:, 0], res[0][0][:, 0], rtol=1e-9)
-    np.testing.assert_array_equal(res[1][0][:, 1:], res[0][0][:, 1:])
