@@ -27,6 +27,9 @@ namespace hq {
 // a fresh slot of its own.  (An all-pairs scan was O(K^2) VALU on one CU:
 // ~5 us per step at K = 256.)
 constexpr int kDupSlots = 2 * kMaxK;
+#ifdef HQ_SA_TIMING
+__device__ uint64_t g_sa_t[4];  // block 0's stamps inside the SA step (diagnostic build)
+#endif
 __device__ __forceinline__ uint32_t dup_hash(float4 c) {
     const uint32_t x = __float_as_uint(c.x == 0.f ? 0.f : c.x);
     const uint32_t y = __float_as_uint(c.y == 0.f ? 0.f : c.y);
@@ -61,6 +64,9 @@ __device__ __forceinline__ bool prep_palette_body(const PaletteArgs& a, int p, f
     else c = make_float4(0.f, 0.f, 0.f, 0.f);
     if (own) s[k] = c;
     __syncthreads();
+#ifdef HQ_SA_TIMING
+    if (tid == 0 && blockIdx.x == 0) g_sa_t[2] = wall_clock64();
+#endif
     // linear RGB (CL:85-87), one component per thread: a colour's three powf
     // run on three threads (12 waves) instead of one after another (4 waves)
     for (int t = tid; t < 3 * a.K; t += blockDim.x) {
@@ -82,6 +88,9 @@ __device__ __forceinline__ bool prep_palette_body(const PaletteArgs& a, int p, f
         atomicMin(&s_min[slot], (uint32_t)k);
     }
     __syncthreads();
+#ifdef HQ_SA_TIMING
+    if (tid == 0 && blockIdx.x == 0) g_sa_t[3] = wall_clock64();
+#endif
     const bool dup = own && s_min[slot] < (uint32_t)k;
     nonfinite = L.nonfinite != 0;
     if (own && write) {
@@ -233,6 +242,9 @@ __device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared
     }
     if (tid < P) s.unused[tid] = 0;
     __syncthreads();
+#ifdef HQ_SA_TIMING
+    if (tid == 0 && blockIdx.x == 0) g_sa_t[0] = wall_clock64();
+#endif
     if (a.accept && a.fold) {
 #pragma unroll
         for (int j = 0; j < MAXW; ++j) {
@@ -273,6 +285,9 @@ __device__ __forceinline__ void sa_accept(const SaArgs& a, bool writer, SaShared
             s.src[tid] = a.init ? tid : -1;
         }
         __syncthreads();
+#ifdef HQ_SA_TIMING
+        if (tid == 0 && blockIdx.x == 0) g_sa_t[1] = wall_clock64();
+#endif
         if (tid == 0) {
             uint64_t seed = s.seed;
             double* cur = s.cur;
@@ -472,8 +487,12 @@ __global__ __launch_bounds__(1024) void sa_step_kernel(SaArgs a) {
 #ifdef HQ_SA_TIMING
     __syncthreads();
     if (threadIdx.x == 0 && p == 0)
-        printf("SA_T %d %d %d %d %d\n", a.accept, (int)(t1 - t0), (int)(t2 - t1), (int)(t3 - t2),
-               (int)(wall_clock64() - t3));
+        printf("SA_T %d %d %d %d %d | loads %d exp %d seq %d\n", a.accept, (int)(t1 - t0), (int)(t2 - t1),
+               (int)(t3 - t2), (int)(wall_clock64() - t3), (int)(g_sa_t[0] - t0), (int)(g_sa_t[1] - g_sa_t[0]),
+               (int)(t1 - g_sa_t[1]));
+    if (threadIdx.x == 0 && p == 0)
+        printf("SA_P fill %d hash %d rest %d\n", (int)(g_sa_t[2] - t3), (int)(g_sa_t[3] - g_sa_t[2]),
+               (int)(wall_clock64() - g_sa_t[3]));
 #endif
 }
 
