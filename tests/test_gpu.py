@@ -1655,3 +1655,28 @@ def test_pixel_errors_de94_vs_oracle(gpu, case, variant):
             ref = float(np.mean(ex)) + float(np.count_nonzero(~used)) * 2.0
             assert abs(cost - ref) <= 1e-5 * ref, stats
     m.close()
+
+
+@pytest.mark.parametrize("w,h", [(10, 10), (11, 37), (37, 11), (129, 17)])
+@pytest.mark.parametrize("K,P", [(1, 1), (2, 5), (3, 2), (255, 3)])
+def test_small_images_and_palettes_vs_oracle(gpu, filt, w, h, K, P):
+    """Edge shapes against the oracle: images down to the stencil's half-width
+    (10 x 10: every pixel's window reflects at both edges, CL:256-263), images
+    smaller than one 16 x 128 tile in either direction, ragged tiles, and
+    palettes of 1, 2, 3 and 255 colours (a one-colour palette: every pixel
+    index 0, no penalty).  Indices and used flags bit-exact, costs within 1e-5."""
+    R, G, B = o.synthetic_image(w, h, seed=w * 131 + h + K)
+    rgba = o.inline_rgba(R, G, B)
+    pals = np.stack([o.synthetic_palette(K, 500 + p) for p in range(P)])
+    m = hq.ImageManipulation(device=gpu)
+    hq.ScielabProcessor(72, 45.0, hq.Whitepoint.D65, None, m)
+    m.setImage(rgba.reshape(-1), None, w, filt.illum)
+    lab = m.getLabRef().reshape(-1, 4)
+    costs, used = m.computeQuantizationErrorPopulation(pals.reshape(P, -1), 2.0, return_used=True)
+    idx = [m.getIndices(p) for p in range(P)]
+    m.close()
+    for p in range(P):
+        ref, parts = c_oracle.eval_palette(rgba, lab, pals[p], filt, w, return_parts=True)
+        np.testing.assert_array_equal(idx[p], parts["idx"].astype(np.uint8))
+        np.testing.assert_array_equal(used[p], parts["used"])
+        assert abs(costs[p] - ref) <= 1e-5 * abs(ref), (p, costs[p], ref)
