@@ -446,7 +446,7 @@ def main():
     elif args.shard_of > 0 and args.shard_comm:
         m.initComm(1, 0, m.commUniqueId())
     rccl_ranks, rccl_rank = m.commInfo()  # (0, -1): no communicator (one GPU)
-    if (world > 1 or args.shard_comm) and (rccl_ranks, rccl_rank) != (world, rank):
+    if (world > 1 or (args.shard_of > 0 and args.shard_comm)) and (rccl_ranks, rccl_rank) != (world, rank):
         raise RuntimeError(f"bench.py: RCCL communicator has {rccl_ranks} ranks (rank {rccl_rank}), "
                            f"expected {world} (rank {rank})")
 
@@ -465,7 +465,8 @@ def main():
     search_line = None
     if not args.no_full_search:
         dev, bdev = full_search(lib, _lib, m, args.K, P, args.seed, 1, sa_device)
-        where = (f"rows [{r0}, {r1}) of an {args.shard_of}-way split, no collective" if args.shard_of > 0
+        where = (f"rows [{r0}, {r1}) of an {args.shard_of}-way split, "
+                 f"{'a one-rank communicator' if args.shard_comm else 'no collective'}" if args.shard_of > 0
                  else f"{world} GPU(s)")
         label = "BASELINE config 3" if shape == (4096, 256, 4) else f"full search ({cfg_name})"
         search_line = {"config": f"{label}: {W}x{H}, K={args.K}, P={P}, imax=5000, "
