@@ -49,10 +49,10 @@ __device__ __noinline__ int argmin_exact_slow(float r, float g, float b, uint4 L
     const uint32_t words[8] = {L0.x, L0.y, L0.z, L0.w, L1.x, L1.y, L1.z, L1.w};
     const int n = all ? K : cnt;
     int bi = all ? 0 : (int)((words[0] >> 8) & 0xff);
-    float best = sqrtf(dist2(r, g, b, s_pal[bi]));
+    float best = ref_dist(r, g, b, s_pal[bi]);
     for (int i = 1; i < n; ++i) {
         const int k = all ? i : (int)((words[(i + 1) >> 2] >> (8 * ((i + 1) & 3))) & 0xff);
-        const float d = sqrtf(dist2(r, g, b, s_pal[k]));
+        const float d = ref_dist(r, g, b, s_pal[k]);
         if (d < best) { best = d; bi = k; }
     }
     return bi;
@@ -110,7 +110,7 @@ __device__ __forceinline__ int argmin_fix(float r, float g, float b, bool s, int
         float bd = INFINITY;
         uint32_t bkey = 0xffffffffu;  // no colour yet
         for (int k = lane; k < K; k += 64) {
-            const float d = sqrtf(dist2(pr, pg, pb, s_pal[k]));
+            const float d = ref_dist(pr, pg, pb, s_pal[k]);
             const bool nan = d != d;
             const float dv = nan ? INFINITY : d;
             const uint32_t key = (nan ? 0x10000u : 0u) | (uint32_t)k;
@@ -129,18 +129,20 @@ __device__ __forceinline__ int argmin_fix(float r, float g, float b, bool s, int
             }
         }
         const int bk = (int)(bkey & 0xffffu);
-        const float d0 = sqrtf(dist2(pr, pg, pb, s_pal[0]));
+        const float d0 = ref_dist(pr, pg, pb, s_pal[0]);
         if (lane == L) result = d0 != d0 ? 0 : bk;
     }
     return result;
 }
 
 // Exact argmin (CL:179-193 semantics) of one pixel against the NG palettes of
-// its group over their level-2 candidate lists.  Candidates are ranked by d2;
-// the reference ranks by sqrtf(d2), which can map two different d2 onto one
-// distance, and then keeps the lower index.  Equal sqrtf values imply
-// |d2a - d2b| < 2^-22 * d2, so lanes whose runner-up d2 lies within 1e-6
-// relative of the best are re-resolved with the reference loop (rare), as are
+// its group over their level-2 candidate lists.  Candidates are ranked by d2
+// (the reference's); the reference ranks by ref_dist (v_sqrt_f32 of d2), which
+// can map two different d2 onto one distance, and then keeps the lower index.
+// Equal distances imply |d2a - d2b| < 2^-21 * d2 (v_sqrt_f32 is monotone and
+// within 1 ulp), so lanes whose runner-up d2 lies within 1e-6 relative of the
+// best (or below 2^-125: near_d2) are re-resolved with the reference loop
+// (rare), as are
 // lanes whose list overflowed the level-2 entry or that have no list.
 // NG > 1 walks the lists in lockstep (HQ_ASSIGN_JOINT): candidate i of every
 // palette in one loop step, NG independent LDS reads and compare chains in
@@ -230,7 +232,7 @@ __device__ __forceinline__ void argmin_group(float r, float g, float b, const L2
             }
         }
 #pragma unroll
-        for (int q = 0; q < NG; ++q) near[q] = second2[q] <= best2[q] * (1.0f + 1e-6f);
+        for (int q = 0; q < NG; ++q) near[q] = near_d2(best2[q], second2[q]);
     }
 #pragma unroll
     for (int q = 0; q < NG; ++q) {
@@ -507,12 +509,12 @@ __global__ __launch_bounds__(256, HQ_ASSIGN_WAVES) void assign_pipe_kernel(Assig
 #pragma unroll
             for (int s0 = 0; s0 < NG; s0 += CMB) {
                 // the chunks' winners in ascending chunk order, by the reference's
-                // distance (sqrtf of the unfused d^2, CL:186): strict <
-                float best = sqrtf(dist2(xr[h], xg[h], xb[h], s_pal[s0 * kMaxK + kk[s0]]));
+                // distance (ref_dist, CL:186): strict <
+                float best = ref_dist(xr[h], xg[h], xb[h], s_pal[s0 * kMaxK + kk[s0]]);
                 int bc = 0, k = kk[s0];
 #pragma unroll
                 for (int c = 1; c < CMB; ++c) {
-                    const float d = sqrtf(dist2(xr[h], xg[h], xb[h], s_pal[(s0 + c) * kMaxK + kk[s0 + c]]));
+                    const float d = ref_dist(xr[h], xg[h], xb[h], s_pal[(s0 + c) * kMaxK + kk[s0 + c]]);
                     const bool lt = d < best;
                     best = lt ? d : best;
                     bc = lt ? c : bc;

@@ -93,10 +93,10 @@ __device__ __forceinline__ float3 opp2lab_ref(float o0, float o1, float o2, cons
     return make_float3(116.0f * fy - 16.0f, 500.0f * (fx - fy), 200.0f * (fy - fz));
 }
 
-// CL:201-231: dE76 (distance) or dE94.  Hardware square root (v_sqrt_f32, ~1 ulp):
+// CL:201-231: dE76 (distance) or dE94.  Hardware square root (v_sqrt_f32, <= 1 ulp):
 // HIP's sqrtf is a correctly rounded ~10-instruction sequence, and the
-// reference's OpenCL distance()/sqrt is itself only ulp-accurate; the cost is
-// compared at 1e-4 relative.  (The argmin keeps sqrtf: its ties are exact.)
+// reference's OpenCL distance()/sqrt on gfx950 is v_sqrt_f32 itself (ref_len
+// below); the cost is compared at 1e-6 relative.
 __device__ __forceinline__ float hw_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 
 template <int DE>
@@ -158,22 +158,58 @@ __device__ __forceinline__ int reflect_only(int j, int n) {
     return j;
 }
 
-// Exact argmin distance ((dx*dx + dy*dy) + dz*dz), never fused: hipcc's default
-// -ffp-contract=fast would otherwise turn it into FMAs (and differently at
-// different call sites), breaking bit-exactness against the oracle.
-__device__ __forceinline__ float dist2(float r, float g, float b, float4 c) {
-#pragma clang fp contract(off)
-    const float dx = r - c.x, dy = g - c.y, dz = b - c.z;
-    return (dx * dx + dy * dy) + dz * dz;
+// The argmin's distance, CL:179-192 `distance(pixel, colour)`, as the
+// reference's own OpenCL build computes it on gfx950 (disassembly of its
+// quantize / quantizeAndConvertToOpp kernels, compiled unmodified into
+// oracle/_ref by oracle/Makefile):
+//   d^2 = fma(dw, dw, fma(dz, dz, fma(dy, dy, dx * dx))),  d = p - c,
+//   d = v_sqrt_f32(d^2) for FLT_MIN <= d^2 < inf (or NaN),
+// and below FLT_MIN (or at +inf) the library's rescaled form: the components
+// times 2^86 (2^-66), the same chain, v_sqrt_f32 with its own ldexp 32 / -16
+// step for a subnormal sum, and back by 2^-86 (2^66).  v_sqrt_f32 is monotone
+// and within 1 ulp, but not correctly rounded (15.1% of the normal floats are 1
+// ulp off: scripts/mb/sqrt_probe.hip, profiles/r06_sqrt_probe.json), so two
+// different d^2 can share one distance, and then the lower index wins (strict
+// <).  The kernels rank by d^2 (dist2_rank: the same chain, so the same
+// value) and re-resolve by ref_len any pixel whose runner-up lies within 1e-6
+// relative of its best d^2 or below 2^-125 (near_d2).
+__device__ __noinline__ float ref_len_scaled(float dx, float dy, float dz, float dw, bool small) {
+    const float s = small ? 0x1p86f : 0x1p-66f;
+    const float x = dx * s, y = dy * s, z = dz * s, w = dw * s;
+    float e = __builtin_fmaf(w, w, __builtin_fmaf(z, z, __builtin_fmaf(y, y, x * x)));
+    const bool den = e < 0x1p-126f;
+    e = __builtin_amdgcn_ldexpf(e, den ? 32 : 0);
+    float r = __builtin_amdgcn_sqrtf(e);
+    r = __builtin_amdgcn_ldexpf(r, den ? -16 : 0);
+    return r * (small ? 0x1p-86f : 0x1p66f);
+}
+__device__ __forceinline__ float ref_len(float dx, float dy, float dz, float dw) {
+    const float d2 = __builtin_fmaf(dw, dw, __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx)));
+    if (__builtin_expect(!(d2 < 0x1p-126f) && d2 != INFINITY, 1)) return __builtin_amdgcn_sqrtf(d2);
+    return ref_len_scaled(dx, dy, dz, dw, d2 < 0x1p-126f);
+}
+// pixel (r, g, b, 0) against colour c (whose .w is 0 on every argmin path:
+// prep_palette / prep_wide clear it, SW:49)
+__device__ __forceinline__ float ref_dist(float r, float g, float b, float4 c) {
+    return ref_len(r - c.x, g - c.y, b - c.z, -c.w);
+}
+// pixel and colour as the reference's float4s (the final quantize, CL:147-170)
+__device__ __forceinline__ float ref_dist4(float4 p, float4 c) {
+    return ref_len(p.x - c.x, p.y - c.y, p.z - c.z, p.w - c.w);
 }
 
-// Ranking distance of the pruned argmin: the same sum with two FMAs.  All three
-// terms are non-negative, so it is within 3 ulp (< 2e-7 relative) of dist2;
-// argmin_from_entry re-resolves with dist2 + sqrtf whenever a runner-up lies
-// within 1e-6 relative, so the winner it returns is the reference's.
+// Ranking distance of the pruned argmin: the reference's d^2 (w = 0).
 __device__ __forceinline__ float dist2_rank(float r, float g, float b, float4 c) {
     const float dx = r - c.x, dy = g - c.y, dz = b - c.z;
     return __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
+}
+
+// A pixel whose ranking by d^2 may differ from the reference's by distance:
+// the runner-up within 1e-6 relative of the best d^2 (v_sqrt_f32 can merge d^2
+// up to ~4 ulp apart), or itself below 2^-125 (the rescaled form's distance
+// is not a function of the underflowed d^2).
+__device__ __forceinline__ bool near_d2(float best2, float second2) {
+    return second2 <= fmaxf(best2 * (1.0f + 1e-6f), 0x1p-125f);
 }
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));

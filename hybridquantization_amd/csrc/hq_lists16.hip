@@ -10,12 +10,12 @@
 //
 // The lists are exact in the sense of build_grid (hq_search.hip): every
 // colour that can be the reference's argmin (CL:179-193: the first minimum of
-// sqrtf(d^2) in ascending index) for some pixel of a cell is listed.  A cell's
+// ref_dist in ascending index) for some pixel of a cell is listed.  A cell's
 // threshold T is the least upper bound of d^2 over the cell among the
 // colours; a colour whose lower bound exceeds T (1 + 1e-5) never wins there.
 // The walk ranks the candidates by d^2 and re-resolves a pixel whose runner-up
-// lies within 1e-6 relative (a possible tie of the reference's sqrtf) by the
-// least (sqrtf(d^2), index) over its list: the reference's first minimum.
+// lies within 1e-6 relative (a possible tie of the reference's distance) by the
+// least (ref_dist, index) over its list: the reference's first minimum.
 // Overflowing level-2 entries fall back to the pixel's level-1 list, an
 // overflowing level-1 list (or a pixel outside the unit cube, or a palette
 // with a non-finite colour) to all K colours, cooperatively by the wave.
@@ -447,7 +447,7 @@ __device__ __noinline__ int argmin16_fix(float r, float g, float b, bool s, int 
         uint32_t bkey = 0xffffffffu;
         for (int j = lane; j < n; j += 64) {
             const int k = list ? (int)list[1 + j] : j;
-            const float d = sqrtf(dist2(pr, pg, pb, s_pal[k]));
+            const float d = ref_dist(pr, pg, pb, s_pal[k]);
             const bool nan = d != d;
             const float dv = nan ? INFINITY : d;
             const uint32_t key = (nan ? 0x10000u : 0u) | (uint32_t)k;
@@ -466,7 +466,7 @@ __device__ __noinline__ int argmin16_fix(float r, float g, float b, bool s, int 
             }
         }
         const int bk = (int)(bkey & 0xffffu);
-        const float d0 = sqrtf(dist2(pr, pg, pb, s_pal[0]));
+        const float d0 = ref_dist(pr, pg, pb, s_pal[0]);
         if (lane == Ln) result = d0 != d0 ? 0 : bk;
     }
     return result;
@@ -579,7 +579,7 @@ __global__ __launch_bounds__(kN16Threads) void assign16_kernel(AssignArgs a, int
             const bool slow = !in_[u] || exh[pq] || c == kN16Ovf || c == 0u;
             const int cnt = slow ? 0 : (int)c;
             // ranked by d^2 (dist2_rank: within 3 ulp of dist2); a runner-up within
-            // 1e-6 relative is a possible sqrtf tie: re-resolved over the list below
+            // 1e-6 relative is a possible distance tie (near_d2): re-resolved over the list below
             float best2 = INFINITY, second2 = INFINITY;
             int bk = 0;
 #pragma unroll
@@ -592,14 +592,14 @@ __global__ __launch_bounds__(kN16Threads) void assign16_kernel(AssignArgs a, int
                 bk = lt ? k : bk;
                 best2 = lt ? d2 : best2;
             }
-            const bool near = !slow && second2 <= best2 * (1.0f + 1e-6f);
+            const bool near = !slow && near_d2(best2, second2);
             if (HQ_ANY16(near)) {
-                if (near) {  // the reference distance over the list: least (sqrtf(d^2), index)
+                if (near) {  // the reference distance over the list: least (ref_dist, index)
                     float bd = INFINITY;
                     int bkk = 0x7fffffff;
                     for (int i = 0; i < cnt; ++i) {
                         const int k = (int)u16_at(E[u][pq], i + 1);
-                        const float d = sqrtf(dist2(r[u], g[u], b[u], sp[k]));
+                        const float d = ref_dist(r[u], g[u], b[u], sp[k]);
                         if (d < bd || (d == bd && k < bkk)) {
                             bd = d;
                             bkk = k;

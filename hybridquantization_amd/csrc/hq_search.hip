@@ -795,10 +795,10 @@ __device__ __forceinline__ void grid_cell_body(const GridArgs& a, int p, int cel
     // f(p) = |p - a|^2 - |p - b|^2 = c . p + |a|^2 - |b|^2 with c = 2 (b - a) is
     // linear, so its minimum over the box is at the corner picked axis by axis.
     // For a pixel p in the box the reference's fp32 d^2 is within ~3e-7
-    // relative of the exact one, and its sqrtf separates two d^2 that differ by
-    // more than 2^-21 relative, so f(p) > 1.1e-6 dmax^2(B, a) makes
-    // sqrtf(d_a) > sqrtf(d_b) strictly: a never wins, not even a tie
-    // (CL:179-192).  The test asks f_min > 1e-5 (dmax^2(B, a) + S), S bounding
+    // relative of the exact one, and its distance (v_sqrt_f32, monotone and
+    // within 1 ulp: ref_len, hq_device.h) separates two d^2 that differ by more
+    // than 2^-20 relative, so f(p) > 1.1e-6 dmax^2(B, a) makes d_a > d_b
+    // strictly: a never wins, not even a tie (CL:179-192).  The test asks f_min > 1e-5 (dmax^2(B, a) + S), S bounding
     // the terms of the fp32 evaluation of f_min (its own rounding is < 1e-6 S).
     // Every reference winner stays listed, so the pruned argmin is unchanged;
     // the lists shrink (uniform noise, K = 256, G2 = 32: mean 2.7 -> 2.05, the

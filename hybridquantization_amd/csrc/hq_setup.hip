@@ -155,11 +155,11 @@ __global__ __launch_bounds__(256) void quantize_kernel(const float4* in, const f
     if (q >= n) return;
     const float4 px = in[q];
     float4 bc = colors[0];
-    float best = sqrtf(dist2(px.x, px.y, px.z, bc));
+    float best = ref_dist4(px, bc);
     int bi = 0;
     for (int i = 1; i < K; ++i) {
         const float4 c = colors[i];
-        const float d = sqrtf(dist2(px.x, px.y, px.z, c));
+        const float d = ref_dist4(px, c);
         if (d < best) { best = d; bc = c; bi = i; }
     }
     out[q] = bc;

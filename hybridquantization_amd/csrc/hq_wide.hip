@@ -27,13 +27,13 @@ __global__ __launch_bounds__(256) void prep_wide_kernel(WideArgs a) {
     if (!(isfinite(c.x) && isfinite(c.y) && isfinite(c.z))) atomicOr(&a.pflags[p], 1);
 }
 
-// The reference loop verbatim (CL:179-192): sqrtf of the unfused d^2, first
+// The reference loop verbatim (CL:179-192): ref_dist (hq_device.h), first
 // minimum in ascending index.
 __device__ __noinline__ uint32_t argmin_wide_slow(float r, float g, float b, const float4* pal, int K) {
-    float best = sqrtf(dist2(r, g, b, pal[0]));
+    float best = ref_dist(r, g, b, pal[0]);
     uint32_t bi = 0;
     for (int k = 1; k < K; ++k) {
-        const float d = sqrtf(dist2(r, g, b, pal[k]));
+        const float d = ref_dist(r, g, b, pal[k]);
         if (d < best) { best = d; bi = (uint32_t)k; }
     }
     return bi;
@@ -43,10 +43,10 @@ __device__ __noinline__ uint32_t argmin_wide_slow(float r, float g, float b, con
 // assign_wide: grid (ceil(n_ext / (256 * kWidePPT)), P), block 256.
 // Each thread ranks kWidePPT pixels against every colour of palette p, chunk by
 // chunk from LDS (a chunk entry is read by all lanes at once: a broadcast).
-// Ranking is by the FMA form of d^2 (within 3 ulp of the reference's unfused
-// d^2) with the runner-up tracked by v_med3; a pixel whose runner-up lies
-// within 1e-6 relative of its best -- where sqrtf could merge the two and the
-// lower index would win (CL:186) -- or that is not finite, or whose palette
+// Ranking is by the reference's d^2 (dist2_rank) with the runner-up tracked
+// by v_med3; a pixel whose runner-up lies within 1e-6 relative of its best (or
+// below 2^-125) -- where its distance could merge the two and the lower index
+// would win (CL:186) -- or that is not finite, or whose palette
 // has a non-finite colour, is re-resolved by the reference loop (the argument
 // of argmin_from_entry, hq_assign.hip).  Used flags: the reference's idempotent
 // store (CL:193), skipped when the flag is already set.
@@ -95,7 +95,7 @@ __global__ __launch_bounds__(256) void assign_wide_kernel(WideArgs a) {
         if (q >= a.n_ext) continue;
         const bool finite = isfinite(r[u]) && isfinite(g[u]) && isfinite(b[u]);
         uint32_t k = bi[u];
-        if (exh || !finite || !(second[u] > best[u] * (1.0f + 1e-6f))) k = argmin_wide_slow(r[u], g[u], b[u], pal, a.K);
+        if (exh || !finite || !(second[u] > fmaxf(best[u] * (1.0f + 1e-6f), 0x1p-125f))) k = argmin_wide_slow(r[u], g[u], b[u], pal, a.K);
         idx[q] = k;
         if (used[k] == 0u) used[k] = 1u;
     }

@@ -2,7 +2,8 @@
 
 The C restatement (hq_oracle.c) is the fast checker for sizes the numpy oracle
 cannot reach in seconds, and the "port" CPU baseline timed by bench.py.
-Parity status: parity unpinned (see oracle/oracle.py header).
+Parity status: pinned against the reference's own OpenCL kernels on the
+MI355X (tests/test_refcl.py; oracle/oracle.py header).
 """
 
 from __future__ import annotations
@@ -46,6 +47,10 @@ def lib():
         L.hqo_xyz_to_scielab_mt.restype = C.c_int
         L.hqo_compute_error.argtypes = [_f, _f, C.c_longlong, _f]
         L.hqo_compute_error.restype = C.c_double
+        L.hqo_ref_len_n.argtypes = [_f, C.c_longlong, _f]
+        L.hqo_set_sqrt.argtypes = [C.c_void_p]
+        L.hqo_set_sqrt.restype = None
+        L.hqo_sqrt_calls.restype = C.c_longlong
         _LIB = L
     return _LIB
 
@@ -117,3 +122,26 @@ def compute_error(orig4, quant4):
     img = np.zeros((n, 4), np.float32)
     e = lib().hqo_compute_error(_p(orig4), _p(quant4), n, _p(img))
     return e, img
+
+
+def ref_len(dx, dy, dz, dw=None):
+    """The argmin distance of hq_oracle.c (ref_len) for arrays of differences."""
+    dx = _c32(dx).ravel()
+    d4 = np.zeros((dx.size, 4), np.float32)
+    d4[:, 0], d4[:, 1], d4[:, 2] = dx, _c32(dy).ravel(), _c32(dz).ravel()
+    if dw is not None:
+        d4[:, 3] = _c32(dw).ravel()
+    out = np.empty(dx.size, np.float32)
+    lib().hqo_ref_len_n(_p(d4), dx.size, _p(out))
+    return out
+
+
+def set_sqrt(fn_ptr):
+    """The argmin distance's square root: the address of a C function float(float)
+    (hw_sqrt.install passes the device's v_sqrt_f32), or None for sqrtf."""
+    lib().hqo_set_sqrt(fn_ptr)
+
+
+def sqrt_calls():
+    """How many times the oracle has called the square root set by set_sqrt."""
+    return int(lib().hqo_sqrt_calls())

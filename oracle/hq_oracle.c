@@ -7,12 +7,13 @@
  * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load it.  The
  * product library (hybridquantization_amd/csrc) never links it.
  *
- * PARITY STATUS: parity unpinned -- the reference ships no tests/golden vectors
- * and cannot run here (no JVM/JavaCL, no OpenCL device); see oracle/oracle.py.
+ * PARITY STATUS: pinned against the reference itself -- its own OpenCL kernels,
+ * compiled unmodified for gfx950 into oracle/_ref and run on the MI355X
+ * (tests/test_refcl.py).  The reference ships no golden vectors.
  *
- * Build: oracle/Makefile  (gcc -O2 -ffp-contract=off: no fma contraction, so the
- * argmin distance is exactly ((dx*dx + dy*dy) + dz*dz) in fp32; explicit fmaf()
- * where the reference's OpenCL calls fma()).
+ * Build: oracle/Makefile  (gcc -O2 -ffp-contract=off: no implicit contraction;
+ * explicit fmaf() where the reference's OpenCL calls fma() or its build
+ * contracts, as in the argmin's d^2 below).
  *
  * Citations (reference tree src/plugins/dbrasseur/hybridquantization/):
  *   CL = OptimizedConvolution.cl, IM = ImageManipulation.java, SW = SWASA.java
@@ -91,17 +92,87 @@ static void parallel_for(int n, int nthreads, range_fn fn, void *arg) {
 }
 
 /* ------------------------------------------------------------------------ */
-/* (a,b) argmin: CL:179-193.  d = sqrtf(((dx*dx + dy*dy) + dz*dz)), strict <. */
+/* (a,b) argmin: CL:179-193, first minimum of distance(pixel, colour), strict <. */
+/* The distance as the reference's own OpenCL build computes it on gfx950    */
+/* (disassembly of its quantize kernels, oracle/_ref):          */
+/*   d2 = fma(dw, dw, fma(dz, dz, fma(dy, dy, dx*dx))), d = SQRT(d2) for      */
+/*   FLT_MIN <= d2 < inf (and NaN); below FLT_MIN (or at inf) the library's  */
+/*   rescaled form (components x 2^86 or x 2^-66, the same chain, SQRT with  */
+/*   its ldexp 32 / -16 step for a subnormal sum, back by 2^-86 or 2^66).    */
+/* SQRT is the device's v_sqrt_f32, which is monotone and within 1 ulp but   */
+/* not correctly rounded (1 ulp off on 15.1% of the normal floats,           */
+/* profiles/r06_sqrt_probe.json): its exact values have no published         */
+/* definition, so the oracle takes it as a parameter (hqo_set_sqrt: the GPU  */
+/* tests pass the device instruction itself, through a test-only helper);   */
+/* without one it is sqrtf, correctly rounded, and the oracle can then split */
+/* a tie the device forms between two d2 a few ulp apart.  The pixel's and   */
+/* colour's .w are taken as 0, as on every evaluation path (SW:49, HQ:279).  */
 /* ------------------------------------------------------------------------ */
+typedef float (*hqo_sqrt_fn)(float);
+static hqo_sqrt_fn g_sqrt = NULL;
+static long long g_sqrt_calls = 0;  /* (not atomic: a diagnostic count) */
+
+void hqo_set_sqrt(hqo_sqrt_fn f) { g_sqrt = f; }
+long long hqo_sqrt_calls(void) { return g_sqrt_calls; }
+
+static inline float dev_sqrt(float x) {
+    if (g_sqrt) { ++g_sqrt_calls; return g_sqrt(x); }
+    return sqrtf(x);
+}
+
+static float ref_len(float dx, float dy, float dz, float dw) {
+    const float d2 = fmaf(dw, dw, fmaf(dz, dz, fmaf(dy, dy, dx * dx)));
+    if (!(d2 < 0x1p-126f) && d2 != INFINITY) return dev_sqrt(d2);
+    const int small = d2 < 0x1p-126f;
+    const float s = small ? 0x1p86f : 0x1p-66f;
+    const float x = dx * s, y = dy * s, z = dz * s, w = dw * s;
+    float e = fmaf(w, w, fmaf(z, z, fmaf(y, y, x * x)));
+    const int den = e < 0x1p-126f;
+    e = ldexpf(e, den ? 32 : 0);
+    float r = dev_sqrt(e);
+    r = ldexpf(r, den ? -16 : 0);
+    return r * (small ? 0x1p-86f : 0x1p66f);
+}
+
+/* ref_len over n (dx, dy, dz, dw) quadruples (the tests compare it with
+ * oracle.py's ref_len). */
+int hqo_ref_len_n(const float *d4, long long n, float *out) {
+    for (long long i = 0; i < n; ++i)
+        out[i] = ref_len(d4[4 * i], d4[4 * i + 1], d4[4 * i + 2], d4[4 * i + 3]);
+    return 0;
+}
+
+static inline float d2_ref(const float *p, const float *c) {
+    const float dx = p[0] - c[0], dy = p[1] - c[1], dz = p[2] - c[2];
+    return fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+}
+
+/* Ranked by d2.  Above FLT_MIN the distance is a monotone function of d2 that
+ * separates any two d2 more than 2^-20 apart (v_sqrt_f32 is within 1 ulp;
+ * the same holds for sqrtf), so only the colours whose d2 lies within 1e-6
+ * relative of the least finite-or-inf d2 m (or below 2^-125, where the
+ * rescaled form takes over) can attain the least distance: the reference's
+ * first minimum is the first of those by distance.  A NaN d2 never wins
+ * unless it is colour 0's (nothing compares below NaN, CL:186). */
 static inline int argmin_px(const float *p, const float *pal4, int K) {
-    float dx = p[0] - pal4[0], dy = p[1] - pal4[1], dz = p[2] - pal4[2];
-    float best = sqrtf((dx * dx + dy * dy) + dz * dz);
+    const float d0 = d2_ref(p, pal4);
+    if (d0 != d0) return 0;
+    float best2 = d0, second2 = INFINITY;
     int bi = 0;
     for (int k = 1; k < K; ++k) {
+        const float d2 = d2_ref(p, pal4 + 4 * k);
+        if (d2 < best2) { second2 = best2; best2 = d2; bi = k; }
+        else if (d2 < second2) second2 = d2;
+    }
+    const float lim = fmaxf(best2 * (1.0f + 1e-6f), 0x1p-125f);
+    if (!(second2 <= lim)) return bi;
+    float best = INFINITY;
+    bi = -1;
+    for (int k = 0; k < K; ++k) {
         const float *c = pal4 + 4 * k;
-        dx = p[0] - c[0]; dy = p[1] - c[1]; dz = p[2] - c[2];
-        float d = sqrtf((dx * dx + dy * dy) + dz * dz);
-        if (d < best) { best = d; bi = k; }
+        if (!(d2_ref(p, c) <= lim)) continue;
+        const float d = ref_len(p[0] - c[0], p[1] - c[1], p[2] - c[2], 0.0f);
+        if (bi < 0 || d < best) { best = d; bi = k; }
     }
     return bi;
 }

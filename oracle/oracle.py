@@ -19,10 +19,10 @@ Citation tags (all under /root/reference/src/plugins/dbrasseur/hybridquantizatio
   SP = ScielabProcessor.java,   SW = SWASA.java,
   CL = OptimizedConvolution.cl
 
-Numerical contract frozen for the integer output (palette index):
-  d2 = ((dx*dx + dy*dy) + dz*dz) in fp32 with no contraction, d = sqrtf(d2)
-  (correctly rounded), winner = first k with d < best (strict, ascending k),
-  following CL:179-192 (``distance`` on float4 with .w = 0).
+Numerical contract for the integer output (palette index), CL:179-192 as the
+reference's own OpenCL build computes ``distance`` on gfx950 (ref_len):
+  d2 = fma(dz, dz, fma(dy, dy, dx*dx)) in fp32, d = v_sqrt_f32(d2) (the rescaled
+  form below FLT_MIN), winner = first k with d < best (strict, ascending k).
 """
 
 from __future__ import annotations
@@ -373,31 +373,94 @@ def srgb_to_scielab(R, G, B, filt: Filters, w: int):
 # Candidate evaluation: steps a-h of SURVEY section 0
 # --------------------------------------------------------------------------
 
+def fma32(a, b, c):
+    """fp32 fma(a, b, c) with one rounding: the product is exact in float64, the
+    sum is carried as a float64 plus its exact error (TwoSum), and a float64 sum
+    that lands exactly on an fp32 midpoint is moved one float64 ulp towards the
+    exact value before the rounding to fp32 (round-to-nearest-even otherwise)."""
+    x = np.asarray(a, np.float64) * np.asarray(b, np.float64)
+    c = np.asarray(c, np.float64)
+    s = x + c
+    bb = s - x
+    err = (x - (s - bb)) + (c - bb)
+    r = s.astype(f32)
+    rd = r.astype(np.float64)
+    other = np.nextafter(r, np.where(rd < s, f32(np.inf), f32(-np.inf))).astype(np.float64)
+    mid = (rd != s) & (s == 0.5 * (rd + other)) & (err != 0)
+    if np.any(mid):
+        s = np.where(mid, np.nextafter(s, s + err), s)
+        r = s.astype(f32)
+    return r
+
+
+_SQRT = None  # the device's square root (set_sqrt); None: correctly rounded
+
+
+def set_sqrt(fn):
+    """The square root of the argmin's distance: a function of an fp32 array
+    (the GPU tests pass v_sqrt_f32 itself through a test-only helper), or None
+    for the correctly rounded one (see ref_len)."""
+    global _SQRT
+    _SQRT = fn
+
+
+def _dev_sqrt(x):
+    x = np.asarray(x, f32)
+    with np.errstate(invalid="ignore"):
+        return np.sqrt(x).astype(f32) if _SQRT is None else np.asarray(_SQRT(x), f32)
+
+
+def ref_len(dx, dy, dz):
+    """CL:179-192 distance() as the reference's OpenCL build computes it on gfx950
+    (disassembly of its quantize kernels, oracle/_ref), w = 0:
+    d2 = fma(dz, dz, fma(dy, dy, dx*dx)); d = sqrt(d2) for FLT_MIN <= d2 < inf
+    (and NaN), else the library's rescaled form (components x 2^86, or x 2^-66
+    at inf, the same chain, sqrt with an ldexp 32 / -16 step for a subnormal
+    sum, and back).  sqrt is the device's v_sqrt_f32 when set_sqrt gave it
+    (monotone, within 1 ulp, 1 ulp off on 15.1% of the normal floats), else
+    correctly rounded."""
+    dx, dy, dz = (np.asarray(v, f32) for v in (dx, dy, dz))
+    with np.errstate(over="ignore", under="ignore", invalid="ignore"):
+        d2 = fma32(dz, dz, fma32(dy, dy, (dx * dx).astype(f32)))
+        small = d2 < f32(2.0 ** -126)
+        big = ~small & (d2 != np.inf)
+        out = np.empty_like(d2)
+        out[big] = _dev_sqrt(d2[big])
+        rest = ~big
+        if np.any(rest):
+            sm = small[rest]
+            sc = np.where(sm, f32(2.0 ** 86), f32(2.0 ** -66)).astype(f32)
+            x, y, z = ((v[rest] * sc).astype(f32) for v in (dx, dy, dz))
+            e = fma32(z, z, fma32(y, y, (x * x).astype(f32)))
+            den = e < f32(2.0 ** -126)
+            e = np.ldexp(e, np.where(den, 32, 0)).astype(f32)
+            r = np.ldexp(_dev_sqrt(e), np.where(den, -16, 0)).astype(f32)
+            out[rest] = (r * np.where(sm, f32(2.0 ** -86), f32(2.0 ** 66))).astype(f32)
+    return out
+
+
 def assign(rgb3, palette4):
-    """CL:172-193 argmin: first k with sqrtf(d2) < best (strict).
+    """CL:172-193 argmin: the first k whose ref_len distance is below the best
+    so far (strict <): a NaN distance never wins unless colour 0's is NaN.
 
     rgb3: [N,3] fp32, palette4: [K,4].  The .w lanes are 0 on both sides in the
     reference (HQ:288 makeinline, SW:49/99), so the w term of ``distance`` is 0.
     Returns (idx int32 [N], used int32 [K]).
     """
-    rgb3 = np.asarray(rgb3, f32)
-    K = palette4.shape[0]
-
-    def dist(k):
-        c = palette4[k]
-        dx = (rgb3[:, 0] - c[0]).astype(f32)
-        dy = (rgb3[:, 1] - c[1]).astype(f32)
-        dz = (rgb3[:, 2] - c[2]).astype(f32)
-        d2 = ((dx * dx + dy * dy) + dz * dz).astype(f32)
-        return np.sqrt(d2).astype(f32)
-
-    best = dist(0)
-    idx = np.zeros(rgb3.shape[0], dtype=np.int32)
-    for k in range(1, K):
-        d = dist(k)
-        m = d < best
-        best = np.where(m, d, best)
-        idx[m] = k
+    rgb3 = np.asarray(rgb3, f32)[:, :3]
+    pal = np.asarray(palette4, f32)[:, :3]
+    K, N = pal.shape[0], rgb3.shape[0]
+    idx = np.zeros(N, dtype=np.int32)
+    step = max(1, (1 << 22) // K)  # pixels per chunk: K x step distances at a time
+    for q0 in range(0, N, step):
+        px = rgb3[q0:q0 + step]
+        d = (px[None, :, :] - pal[:, None, :]).astype(f32)  # [K, n, 3]
+        key = ref_len(d[..., 0].ravel(), d[..., 1].ravel(), d[..., 2].ravel()).reshape(K, -1)
+        nan0 = np.isnan(key[0])
+        key = np.where(np.isnan(key), f32(np.inf), key)
+        ix = np.argmin(key, axis=0).astype(np.int32)  # the first minimum
+        ix[nan0] = 0
+        idx[q0:q0 + step] = ix
     used = np.zeros(K, dtype=np.int32)
     used[np.unique(idx)] = 1
     return idx, used

@@ -41,4 +41,9 @@ def gpu():
     """Skip-free guard: a gpu-marked test run without a device is an error."""
     if not _gpu_available():
         pytest.fail("gpu test requested but no HIP device / libhq.so")
+    # the oracles' argmin distance takes the device's v_sqrt_f32, as the
+    # reference's distance() does on this GPU (oracle/hw_sqrt.py)
+    import hw_sqrt
+
+    hw_sqrt.install()
     return 0

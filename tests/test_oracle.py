@@ -193,3 +193,49 @@ def test_ciede94_f32_statement():
     scaled[:, 1:3] = (lab1[:, 1:3] * k[:, None]).astype(f32)
     assert 0.1 < np.isnan(o.ciede94_f32(lab1, scaled)).mean() < 0.9
     assert (o.ciede94_f32(lab1, lab1) == 0).all()
+
+
+def test_fma32_is_one_rounding():
+    """oracle.fma32 against exact rational arithmetic (Fraction), on random
+    operands and on sums built to land near fp32 midpoints."""
+    from fractions import Fraction
+
+    rng = np.random.default_rng(5)
+    a = rng.standard_normal(3000).astype(np.float32)
+    b = rng.standard_normal(3000).astype(np.float32)
+    c = rng.standard_normal(3000).astype(np.float32)
+    # products whose exact sum sits on or next to a midpoint of the fp32 grid
+    c[:1000] = (-(a[:1000].astype(np.float64) * b[:1000]).astype(np.float32)).astype(np.float32)
+    c[1000:1500] = np.float32(1.0)
+    a[1000:1500] = np.float32(2.0 ** -12) * (1 + rng.integers(0, 8, 500)).astype(np.float32)
+    b[1000:1500] = np.float32(2.0 ** -12) + np.float32(2.0 ** -36) * rng.integers(-4, 5, 500).astype(np.float32)
+    got = o.fma32(a, b, c)
+    for x, y, z, r in zip(a.tolist(), b.tolist(), c.tolist(), got.tolist()):
+        exact = Fraction(x) * Fraction(y) + Fraction(z)
+        lo = np.float32(float(exact))  # nearest double, then fp32: check r is a nearest fp32
+        cand = {float(lo), float(np.nextafter(lo, np.float32(np.inf))), float(np.nextafter(lo, np.float32(-np.inf)))}
+        best = min(cand, key=lambda v: (abs(Fraction(v) - exact), np.float32(v).view(np.uint32) & 1))
+        assert r == best, (x, y, z, r, best)
+
+
+def test_ref_len_numpy_matches_c():
+    """The two oracles' argmin distance (CL:179-192 as compiled for gfx950),
+    correctly rounded sqrt mode: normal, tiny (rescaled x 2^86), subnormal,
+    zero and huge (rescaled x 2^-66) differences."""
+    rng = np.random.default_rng(8)
+    n = 20000
+    d = rng.standard_normal((n, 3)).astype(np.float32)
+    d[:2000] *= np.float32(1e-21)
+    d[2000:3000] *= np.float32(1e-40)
+    d[3000:3100] = 0
+    d[3100:3200] *= np.float32(3e19)
+    d[3200:3300] = np.float32(1.4e-45)
+    a = o.ref_len(d[:, 0], d[:, 1], d[:, 2])
+    c = c_oracle.ref_len(d[:, 0], d[:, 1], d[:, 2])
+    np.testing.assert_array_equal(a.view(np.uint32), c.view(np.uint32))
+    # the rescaled forms are the distance to within a few ulp (normal results;
+    # a subnormal result is on the subnormal grid)
+    ex = np.sqrt(np.sum(d.astype(np.float64) ** 2, axis=1))
+    ok = ex > 2.0 ** -126
+    assert np.max(np.abs(a[ok] - ex[ok]) / ex[ok]) < 1e-6
+    assert np.all(a[ex == 0] == 0) and np.all(np.abs(a[~ok] - ex[~ok]) <= 2.0 ** -149)

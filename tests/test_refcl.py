@@ -1,0 +1,292 @@
+"""Parity against the reference itself: the reference's own OpenCL kernels
+(OptimizedConvolution.cl, compiled unmodified for gfx950 by `make -C oracle
+ref` into oracle/_ref/, run on the MI355X through the ROCm OpenCL runtime by
+oracle/ref_cl_host.c, a restatement of the JavaCL host sequences IM:100-153,
+IM:285-370, IM:450-493 + IM:620-727, IM:770-798) against libhq through the C
+ABI, and against the C oracle that the other tests use as their checker.
+
+Bars: chosen colours (the reference's `quantize`, CL:147-170: its distance()
+argmin with strict <) and used flags bit-exact; costs within 1e-6 relative
+(the north-star bar is 1e-4); per-pixel dE within 3e-4 absolute of the
+reference's error image (CL:201-209; libhq and the oracle each sum the stencil
+in their own fp32 order); LabRef within 2e-4 absolute (IM:285-370).
+"""
+
+import os
+
+import numpy as np
+import pytest
+
+import c_oracle
+import hybridquantization_amd as hq
+import oracle as o
+import ref_cl
+
+pytestmark = pytest.mark.gpu
+
+PIX_ATOL = 3e-4
+
+
+@pytest.fixture(scope="module")
+def filt():
+    return o.design_filters()
+
+
+@pytest.fixture(scope="module")
+def refk(gpu):
+    ref_cl.lib()  # the OpenCL context on the GPU (raises with the runtime's message)
+    return ref_cl
+
+
+def _threads():
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def _ctx(gpu, rgba, lab, w, illum, dpi=72, dist=45.0, **opts):
+    m = hq.ImageManipulation(device=gpu)
+    hq.ScielabProcessor(dpi, dist, hq.Whitepoint.D65, None, m)
+    m.setImage(rgba.reshape(-1), None if lab is None else lab.reshape(-1), w, illum)
+    for k, v in opts.items():
+        m.setOption(k, v)
+    return m
+
+
+@pytest.mark.parametrize("w,h", [(97, 53), (256, 256), (333, 217), (1024, 640)])
+def test_labref_matches_reference_kernels(gpu, refk, filt, w, h):
+    """IM:100 RGBtoXYZ + IM:285 XYZtoScielab on the reference's kernels (filter by
+    filter, the update flag) against libhq's device LabRef and the oracle's."""
+    R, G, B = o.synthetic_image(w, h, seed=w + h)
+    ref = refk.srgb_to_scielab(R, G, B, filt, w)
+    m = _ctx(gpu, o.inline_rgba(R, G, B), None, w, filt.illum)
+    lab = m.getLabRef().reshape(-1, 4)
+    m.close()
+    np.testing.assert_allclose(lab[:, :3], ref[:, :3], atol=2e-4)
+    np.testing.assert_allclose(c_oracle.srgb_to_scielab(R, G, B, filt, w)[:, :3], ref[:, :3], atol=2e-4)
+
+
+@pytest.mark.parametrize("w,h,K,P", [(256, 256, 16, 4), (97, 53, 64, 2), (333, 217, 256, 3), (1024, 512, 256, 2),
+                                     (320, 200, 600, 2), (320, 200, 2048, 1)])
+def test_costs_match_reference_kernels(gpu, refk, filt, w, h, K, P):
+    """computeQuantizationErrorPopulation on the reference's kernels (IM:620-727)
+    against libhq's evaluation and the C oracle's, on the same LabRef (the
+    reference's): costs, used flags, the per-pixel dE of palette 0, and the
+    chosen colours (the reference's quantize kernel) -- at C1 (256^2, K = 16, P =
+    4), K = 256 on ragged images, and chunked palettes (K = 600, 2048)."""
+    R, G, B = o.synthetic_image(w, h, seed=3 * w + K)
+    rgba = o.inline_rgba(R, G, B)
+    lab = refk.srgb_to_scielab(R, G, B, filt, w)
+    pals = np.stack([o.synthetic_palette(K, 40 + p) for p in range(P)])
+    rc, ru, re = refk.eval_population(rgba, lab, w, pals, filt, return_err=True)
+    m = _ctx(gpu, rgba, lab, w, filt.illum, pixel_err=1)
+    costs, used = m.computeQuantizationErrorPopulation(pals.reshape(P, -1), 2.0, return_used=True)
+    idx = [m.getIndices32(p) for p in range(P)]
+    pe0 = m.getPixelErrors(0)
+    m.close()
+    np.testing.assert_allclose(costs, rc, rtol=1e-6)
+    np.testing.assert_array_equal(used > 0, ru != 0)
+    assert np.abs(pe0 - re[0]).max() <= PIX_ATOL
+    for p in range(P):
+        q, qu = refk.quantize(rgba, pals[p])
+        np.testing.assert_array_equal(pals[p][idx[p]], q)
+        np.testing.assert_array_equal(qu != 0, ru[p] != 0)
+    oc, parts = c_oracle.eval_palette(rgba, lab, pals[0], filt, w, nthreads=_threads(), return_parts=True)
+    assert abs(oc - rc[0]) <= 1e-6 * rc[0]
+    assert np.abs(parts["err"] - re[0]).max() <= PIX_ATOL
+
+
+@pytest.mark.parametrize("dpi,dist", [(96, 60.0), (150, 30.0), (300, 50.0)])
+def test_viewing_geometries_match_reference_kernels(gpu, refk, dpi, dist):
+    """Other viewing geometries (HQ:229-231): halfSize 19 and 15 (the tiled
+    kernel's larger tap buckets) and 51 (the generic matrix-core pair)."""
+    f = o.design_filters(dpi, dist)
+    w, h, K, P = 301, 173, 64, 2
+    R, G, B = o.synthetic_image(w, h, seed=dpi)
+    rgba = o.inline_rgba(R, G, B)
+    lab = refk.srgb_to_scielab(R, G, B, f, w)
+    pals = np.stack([o.synthetic_palette(K, 60 + p) for p in range(P)])
+    rc, ru, re = refk.eval_population(rgba, lab, w, pals, f, return_err=True)
+    m = _ctx(gpu, rgba, None, w, f.illum, dpi=dpi, dist=dist, pixel_err=1)
+    np.testing.assert_allclose(m.getLabRef().reshape(-1, 4)[:, :3], lab[:, :3], atol=2e-4)
+    m.close()
+    m = _ctx(gpu, rgba, lab, w, f.illum, dpi=dpi, dist=dist, pixel_err=1)
+    costs, used = m.computeQuantizationErrorPopulation(pals.reshape(P, -1), 2.0, return_used=True)
+    pe = [m.getPixelErrors(p) for p in range(P)]
+    m.close()
+    np.testing.assert_allclose(costs, rc, rtol=1e-6)
+    np.testing.assert_array_equal(used > 0, ru != 0)
+    for p in range(P):
+        assert np.abs(pe[p] - re[p]).max() <= PIX_ATOL
+
+
+def _adversarial(G2=32):
+    """Pixels on the level-2 cell faces i/G2 and one ulp either side; palettes:
+    0 colours on faces and corners, 1 colour pairs mirrored across a face (exact
+    ties), 2 colour pairs one ulp apart, 3 exact duplicates and colours equal to
+    pixels."""
+    rng = np.random.default_rng(77)
+    w, h = 128, 96
+    n = w * h
+    faces = (np.arange(G2 + 1) / G2).astype(np.float32)
+    vals = np.concatenate([faces, np.nextafter(faces[:-1], np.float32(2)), np.nextafter(faces[1:], np.float32(-1))])
+    px = np.zeros((n, 4), np.float32)
+    px[:, :3] = rng.choice(vals, size=(n, 3))
+    K = 256
+    pals = np.zeros((4, K, 4), np.float32)
+    pals[0, :, :3] = rng.choice(faces, size=(K, 3))
+    for i in range(K // 2):
+        ax = i % 3
+        f = faces[rng.integers(1, G2)]
+        d = np.float32(rng.integers(1, 8)) / np.float32(4 * G2)
+        base = rng.choice(faces, 3)
+        a, b = base.copy(), base.copy()
+        a[ax], b[ax] = f - d, f + d
+        pals[1, 2 * i, :3], pals[1, 2 * i + 1, :3] = np.clip(a, 0, 1), np.clip(b, 0, 1)
+        on = base.copy()
+        on[ax] = f
+        px[i, :3] = on
+    c = rng.random((K // 2, 3), dtype=np.float32)
+    pals[2, 0::2, :3] = c
+    pals[2, 1::2, :3] = np.nextafter(c, np.float32(2))
+    pals[3, :, :3] = (rng.integers(0, 256, (K, 3)) / 255.0).astype(np.float32)
+    pals[3, 200:210] = pals[3, 3]
+    pals[3, 100:110, :3] = px[500:510, :3]
+    pals[3, 240:250, :3] = px[500:510, :3]
+    return px, pals, w
+
+
+def test_adversarial_argmin_matches_reference_kernels(gpu, refk, filt):
+    """The argmin's decision boundaries on the reference's own distance()
+    (CL:179-192, compiled for gfx950: fma-chain d^2, v_sqrt_f32): pixels on
+    level-2 cell faces and one ulp either side, mirrored pairs (exact ties: the
+    lower index wins), one-ulp pairs (ties that v_sqrt_f32 forms between
+    different d^2), duplicates, pixel-equal colours and pixels one subnormal
+    ulp from a colour (the rescaled form).  libhq's chosen colours (pruned grid
+    and exhaustive) equal the reference quantize kernel's bit for bit, and the
+    used flags too."""
+    px, pals, w = _adversarial()
+    for g in (32, 0):
+        m = _ctx(gpu, px, np.zeros_like(px), w, filt.illum, grid=g)
+        _, used = m.computeQuantizationErrorPopulation(pals.reshape(4, -1), 2.0, return_used=True)
+        idx = [m.getIndices(p) for p in range(4)]
+        m.close()
+        for p in range(4):
+            q, qu = refk.quantize(px, pals[p])
+            np.testing.assert_array_equal(pals[p][idx[p]], q, err_msg=f"grid {g} palette {p}")
+            np.testing.assert_array_equal(used[p] > 0, qu != 0, err_msg=f"grid {g} palette {p}")
+
+
+def test_oracles_match_reference_argmin(gpu, refk):
+    """The two oracles' argmin (hq_oracle.c and oracle.py, with the device's
+    v_sqrt_f32 installed by the gpu fixture) against the reference's quantize
+    kernel on the adversarial palettes: identical choices.  With the correctly
+    rounded sqrt instead, the oracles split some of the ties v_sqrt_f32 forms."""
+    import hw_sqrt
+
+    px, pals, _ = _adversarial()
+    calls0 = c_oracle.sqrt_calls()
+    for p in range(4):
+        q, _ = refk.quantize(px, pals[p])
+        ci, _ = c_oracle.assign(px, pals[p])
+        ni, _ = o.assign(px[:, :3], pals[p])
+        np.testing.assert_array_equal(pals[p][ci], q, err_msg=f"C oracle, palette {p}")
+        np.testing.assert_array_equal(pals[p][ni], q, err_msg=f"numpy oracle, palette {p}")
+    assert c_oracle.sqrt_calls() > calls0  # the near ties went through v_sqrt_f32
+    hw_sqrt.uninstall()
+    try:
+        diff = sum(int(np.any(pals[p][c_oracle.assign(px, pals[p])[0]] != refk.quantize(px, pals[p])[0], axis=1).sum())
+                   for p in range(4))
+    finally:
+        hw_sqrt.install()
+    assert diff > 0
+
+
+def test_hw_sqrt_monotone_within_one_ulp(gpu):
+    """The properties the argmin's re-resolution window rests on: v_sqrt_f32 is
+    monotone and within 1 ulp of the correctly rounded root (a stride-61 sample
+    of the normal floats plus runs of consecutive ones; the exhaustive count is
+    in profiles/r06_sqrt_probe.json), and not correctly rounded (0x00806001)."""
+    import hw_sqrt
+
+    bits = np.concatenate([np.arange(0x00800000, 0x7F800000, 61, dtype=np.uint32),
+                           np.arange(0x3F800000, 0x3F800000 + 200000, dtype=np.uint32),
+                           np.arange(0x00806001, 0x00806001 + 4096, dtype=np.uint32)])
+    x = bits.view(np.float32)
+    y = hw_sqrt.sqrt_n(x)
+    cr = np.sqrt(x.astype(np.float64)).astype(np.float32)  # double sqrt rounded to fp32: correctly rounded
+    ulps = np.abs(y.view(np.int32).astype(np.int64) - cr.view(np.int32).astype(np.int64))
+    assert ulps.max() <= 1
+    assert 0.05 < np.mean(ulps) < 0.3
+    order = np.argsort(bits, kind="stable")
+    assert np.all(np.diff(y[order]) >= 0)
+    assert y[bits == 0x00806001][0].view(np.uint32) == 0x20002FF7
+
+
+def test_config3_4096_matches_reference_kernels(gpu, refk, filt):
+    """BASELINE config 3's shape (4096^2, K = 256) through the reference's kernels:
+    LabRef, two palettes' costs and used flags, and palette 0's chosen colour for
+    every one of the 16.8 M pixels."""
+    w = h = 4096
+    R, G, B = o.synthetic_image(w, h, seed=1)
+    rgba = o.inline_rgba(R, G, B)
+    lab = refk.srgb_to_scielab(R, G, B, filt, w)
+    pals = np.stack([o.synthetic_palette(256, 2 + p) for p in range(2)])
+    rc, ru = refk.eval_population(rgba, lab, w, pals, filt)
+    m = _ctx(gpu, rgba, None, w, filt.illum)
+    np.testing.assert_allclose(m.getLabRef().reshape(-1, 4)[:, :3], lab[:, :3], atol=2e-4)
+    m.close()
+    m = _ctx(gpu, rgba, lab, w, filt.illum)
+    costs, used = m.computeQuantizationErrorPopulation(pals.reshape(2, -1), 2.0, return_used=True)
+    idx0 = m.getIndices(0)
+    m.close()
+    np.testing.assert_allclose(costs, rc, rtol=1e-6)
+    np.testing.assert_array_equal(used > 0, ru != 0)
+    q, _ = refk.quantize(rgba, pals[0])
+    np.testing.assert_array_equal(pals[0][idx0], q)
+
+
+def test_reference_kernels_timed_against_libhq(gpu, refk, filt):
+    """The reference's own population evaluation on this MI355X (its five kernels per
+    member, IM:620-727) beside libhq's, at BASELINE config 3 (4096^2, K = 256, P = 4):
+    the same work, the same inputs.  libhq's population (one call through the C ABI,
+    costs read back) must take less time than the reference's kernels alone.  With
+    HQ_REFCL_TIMING_OUT set, the numbers are written there as JSON."""
+    import json
+    import time
+
+    w = h = 4096
+    P, K = 4, 256
+    R, G, B = o.synthetic_image(w, h, seed=1)
+    rgba = o.inline_rgba(R, G, B)
+    lab = refk.srgb_to_scielab(R, G, B, filt, w)
+    pals = np.stack([o.synthetic_palette(K, 2 + p) for p in range(P)])
+    ref = refk.time_population(rgba, lab, w, pals, filt, reps=3)
+    ref_kernels_ms = P * sum(ref["kernel_ms"].values())
+    m = _ctx(gpu, rgba, lab, w, filt.illum)
+    flat = pals.reshape(P, -1)
+    m.computeQuantizationErrorPopulation(flat, 2.0)
+    reps = 20
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        m.computeQuantizationErrorPopulation(flat, 2.0)
+    hq_ms = 1e3 * (time.perf_counter() - t0) / reps
+    m.close()
+    px_evals = w * h * P
+    out = {
+        "config": {"workload": "C3 population evaluation", "size": w, "K": K, "P": P, "halfSize": 10},
+        "reference_opencl_on_mi355x": {
+            "wall_ms_per_population": ref["wall_ms"],
+            "kernel_ms_per_member": ref["kernel_ms"],
+            "kernels_ms_per_population": ref_kernels_ms,
+            "mpx_evals_per_s_kernels": px_evals / ref_kernels_ms / 1e3,
+            "mpx_evals_per_s_wall": px_evals / ref["wall_ms"] / 1e3,
+        },
+        "libhq": {"ms_per_population": hq_ms, "mpx_evals_per_s": px_evals / hq_ms / 1e3},
+        "speedup_vs_reference_kernels": ref_kernels_ms / hq_ms,
+        "speedup_vs_reference_wall": ref["wall_ms"] / hq_ms,
+    }
+    path = os.environ.get("HQ_REFCL_TIMING_OUT")
+    if path:
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+    print(json.dumps(out))
+    assert hq_ms < ref_kernels_ms, out
