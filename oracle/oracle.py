@@ -5,14 +5,16 @@ the *checker* for the HIP path.  Only ``tests/``, ``__graft_entry__.smoke()`` an
 ``bench.py``'s ``cpu_baseline`` leg may import it.  The product
 (``hybridquantization_amd``) never imports anything under ``oracle/``.
 
-PARITY STATUS: **parity unpinned.**  The reference (Helios77760/HybridQuantization,
-Java + JavaCL/OpenCL) ships no tests, no golden vectors and no fixtures, and it
-cannot be run in this container (no JVM, no Icy/EzPlug/JavaCL jars, OpenCL
-platform with 0 devices).  The oracle is pinned only by
-(a) line-by-line restatement of the cited reference code, (b) self-consistency
-checks of the reference's own constants (tests/test_oracle.py), and (c) the
-agreement of two independent restatements (this numpy file and
-``oracle/hq_oracle.c``).
+PARITY STATUS: **pinned against the reference itself.**  The reference
+(Helios77760/HybridQuantization, Java + JavaCL/OpenCL) ships no tests, golden
+vectors or fixtures, and its Java host cannot run here (no JVM, no
+Icy/EzPlug/JavaCL jars).  Its per-pixel kernels, one
+OpenCL C file, are compiled unmodified for gfx950 (oracle/Makefile, into
+oracle/_ref/) and run on the MI355X by oracle/ref_cl_host.c, a restatement of
+its JavaCL host sequence; tests/test_refcl.py (GPU) checks this oracle and
+libhq against them.  Further pins: line-by-line restatement,
+self-consistency of the reference's constants (tests/test_oracle.py), and the
+agreement of two independent restatements (this file and oracle/hq_oracle.c).
 
 Citation tags (all under /root/reference/src/plugins/dbrasseur/hybridquantization/):
   HQ = HybridQuantization.java, IM = ImageManipulation.java,

@@ -1,11 +1,13 @@
 """Generate the golden fixtures under tests/golden/ from the CPU oracle.
 
 Provenance: the reference (Java + JavaCL) holds no tests, fixtures or golden
-vectors and cannot run in this container, so every expected
-value here comes from the oracle's restatement of the reference semantics
-(oracle/oracle.py, cross-checked against oracle/hq_oracle.c) -- "parity
-unpinned".  The only externally pinned values are the java.util.Random
-known answers in kat_java_random.json (published outputs of the JDK class).
+vectors and its Java host cannot run in this container, so every
+expected value here comes from the oracle's restatement of the reference
+semantics (oracle/oracle.py, cross-checked against oracle/hq_oracle.c), with
+the correctly rounded square root (oracle.ref_len).  The oracle is pinned
+against the reference's own OpenCL kernels on the MI355X by tests/test_refcl.py
+(GPU); the java.util.Random known answers in kat_java_random.json are published
+outputs of the JDK class.
 
 Run:  python tests/golden/make_golden.py
 """

@@ -2,8 +2,9 @@
 agreement of the two independent restatements (numpy and C).
 
 Parity status: the reference ships no vectors, so the fixtures
-are oracle-generated (tests/golden/make_golden.py) -- "parity unpinned" except
-for the java.util.Random known answers.
+are oracle-generated (tests/golden/make_golden.py); the oracle itself is pinned
+against the reference's own OpenCL kernels run on the MI355X (tests/test_refcl.py,
+GPU) and, here, by the java.util.Random known answers.
 """
 
 import json
