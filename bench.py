@@ -199,6 +199,7 @@ def cpu_baseline(args):
         va, na, ela = rate(args.size, args.K, usable, args.cpu_seconds, 64)
         all_cores = {"measured": True, "value": round(va, 3), "threads": usable, "evals": na,
                      "seconds": round(ela, 2)}
+    ref_gpu = reference_kernels_on_gpu(args)
     return {"value": round(v, 3), "unit": "Mpixel*evals/s", "cores": threads, "kind": "port",
             "nproc": os.cpu_count(), "usable_cpus": usable, "cpu_share": share or None,
             "cpu_model": _cpu_model(),
@@ -211,7 +212,41 @@ def cpu_baseline(args):
                             "threads": threads},
             "all_cores": all_cores,
             "single_thread_1024_k256": {"value": round(st, 3), "evals": ns,
-                                        "seconds": round(els, 2), "threads": 1}}
+                                        "seconds": round(els, 2), "threads": 1},
+            "reference_kernels_on_this_gpu": ref_gpu}
+
+
+def reference_kernels_on_gpu(args, reps=3):
+    """The reference's own population evaluation on this GPU, same shape: its
+    OpenCL kernels (OptimizedConvolution.cl, compiled unmodified for gfx950 into
+    oracle/_ref by `make -C oracle ref`) driven in the order of its JavaCL host
+    code (IM:620-727, oracle/ref_cl_host.c).  Part of the baseline leg, after
+    the timed region; never fails the run (a missing build or runtime is
+    reported).  The LabRef input is zeros: the reference's work does not depend
+    on its values."""
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as o
+        import ref_cl  # the reference's kernels (baseline only)
+
+        R, G, B = synthetic_planes(args.size, args.size, seed=args.seed)
+        rgba = o.inline_rgba(R.ravel(), G.ravel(), B.ravel())
+        del R, G, B
+        pals = np.stack([o.synthetic_palette(args.K, 2 + p) for p in range(args.population)])
+        t = ref_cl.time_population(rgba, np.zeros_like(rgba), args.size, pals, o.design_filters(args.dpi, args.distance),
+                                   reps=reps)
+        px_evals = args.size * args.size * args.population
+        kern_ms = args.population * sum(t["kernel_ms"].values())
+        return {"value": round(px_evals / kern_ms / 1e3, 2), "unit": "Mpixel*evals/s",
+                "wall_value": round(px_evals / t["wall_ms"] / 1e3, 2),
+                "kernel_ms_per_population": round(kern_ms, 4), "wall_ms_per_population": round(t["wall_ms"], 3),
+                "kernel_ms_per_member": {k: round(v, 4) for k, v in t["kernel_ms"].items()},
+                "reps": reps, "kind": "reference",
+                "sample": f"{args.size}x{args.size}, K={args.K}, P={args.population}: the reference's five kernels "
+                          "per member (value: their device time) and its host sequence with the error-image "
+                          "reads and host means (wall_value)"}
+    except Exception as e:  # noqa: BLE001 -- a baseline, never the run's outcome
+        return {"value": None, "error": f"{type(e).__name__}: {e}"}
 
 
 GPU_MODULES = ("torch", "hybridquantization_amd")
@@ -602,6 +637,9 @@ def main():
         out["full_search_c3"] = search_line
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)
+        ref = out["cpu_baseline"].get("reference_kernels_on_this_gpu") or {}
+        if ref.get("value"):  # this line's value over the reference's own kernels on this GPU
+            ref["libhq_over_reference"] = round(value / ref["value"], 2)
     m.close()
     sys.stdout.flush()
     if rank == 0:

@@ -1,7 +1,7 @@
 // hq_device.h -- device helpers shared by the gfx950 kernels of libhq:
-// colour constants and conversions (CL:77-145), the frozen argmin distance
-// (CL:179-193), dE (CL:201-226), wave reductions and the XCD-aware grid
-// relabelling.  Included by every .hip translation unit of the library.
+// colour constants and conversions (CL:77-145), the argmin distance as the
+// reference computes it on gfx950 (CL:179-193), dE (CL:201-226), wave
+// reductions and the XCD-aware grid relabelling.  Included by every .hip translation unit of the library.
 #pragma once
 
 // HQ_ABL_* switches are timing ablations: they drop work and give wrong

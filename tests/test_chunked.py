@@ -3,8 +3,8 @@ assign_pipe_kernel with CMB > 1; hq_runtime.hip pack_chunks):
 
 a palette of K colours becomes nch = 2, 4, 8 or 16 sub-palettes of 256
 (colours 256 c .. 256 c + 255; past K, copies of colour 0).  Each chunk's
-winner is that chunk's own reference argmin (CL:179-193: sqrtf of the unfused
-fp32 d^2, first minimum in ascending index), and the winners are compared in
+winner is that chunk's own reference argmin (CL:179-193: the reference's
+distance, oracle.ref_len; first minimum in ascending index), and the winners are compared in
 ascending chunk order by the same distance with a strict <, nch / 4 chunks at a
 time when nch > 4 (the passes keep the best distance so far).  The result must
 be the reference argmin over all K colours, for palettes with exact ties across
@@ -47,9 +47,9 @@ def chunked_argmin(px, pal):
 
 
 def ref_dist_at(px, pal, idx):
-    """sqrtf(((dx*dx + dy*dy) + dz*dz)) in fp32, unfused (CL:186 as the oracle has it)."""
+    """The reference's distance (CL:186 as compiled for gfx950: oracle.ref_len)."""
     d = (px[:, :3] - pal[idx, :3]).astype(f32)
-    return np.sqrt(((d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2]).astype(f32)).astype(f32)
+    return o.ref_len(d[:, 0], d[:, 1], d[:, 2])
 
 
 @pytest.mark.parametrize("K", [257, 300, 512, 600, 1000, 1500, 2048, 4096])

@@ -7,8 +7,8 @@
 - for lists still longer than an 8-B level-2 entry holds (7), the same test
   against every other listed colour (build_grid's prune_long_lists).
 
-Each is checked against the reference's own argmin (CL:179-192: sqrtf of the
-unfused fp32 d^2, first minimum in ascending index) over dense pixel sets
+Each is checked against the reference's own argmin (CL:179-192: its distance
+as compiled for gfx950, oracle.ref_len; first minimum in ascending index) over dense pixel sets
 inside the box -- every u8/255 value of the box, its corners and faces, and
 points one ulp inside -- for random and adversarial palettes: a colour the
 tests drop never wins, ties included.  No GPU needed.
@@ -70,10 +70,9 @@ def box_pixels(lo, hi, rng):
 
 
 def ref_argmin(px, pal):
-    """CL:179-192 over all colours: sqrtf of the unfused fp32 d^2, strict <."""
-    d = np.sqrt(((px[:, None, 0] - pal[None, :, 0]) ** 2 + (px[:, None, 1] - pal[None, :, 1]) ** 2) +
-                (px[:, None, 2] - pal[None, :, 2]) ** 2, dtype=np.float32)
-    return np.argmin(d, axis=1)  # first minimum
+    """CL:179-192 over all colours: the reference's distance on gfx950
+    (oracle.ref_len: fma-chain d^2, its square root), first minimum."""
+    return o.assign(px, pal)[0]
 
 
 def check_palette(pal, G2, rng, cells=60, long_cap=7):
