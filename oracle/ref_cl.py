@@ -18,7 +18,8 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 REF_DIR = os.path.join(_HERE, "_ref")
 LIB_PATH = os.path.join(REF_DIR, "libhq_refcl.so")
-BIN_PATH = os.path.join(REF_DIR, "optimized_convolution.gfx950.co")
+BIN_PATH = os.path.join(REF_DIR, "optimized_convolution.gfx950.co")  # -DCIE76 (IM:63, HQ:96)
+BIN_PATHS = {"cie76": BIN_PATH, "cie94": os.path.join(REF_DIR, "optimized_convolution.cie94.gfx950.co")}
 _LIB = None
 
 _f = C.POINTER(C.c_float)
@@ -43,6 +44,14 @@ def lib():
             raise RuntimeError("reference OpenCL kernels: " + lb.hqref_error().decode())
         _LIB = lb
     return _LIB
+
+
+def use(variant):
+    """Run the -DCIE76 ("cie76", the default) or the -DCIE94 ("cie94") build of the
+    reference's kernels from now on (IM:63: the dE type is a build option)."""
+    L = lib()
+    if L.hqref_init(BIN_PATHS[variant].encode()) != 0:
+        raise RuntimeError("reference OpenCL kernels: " + L.hqref_error().decode())
 
 
 def _check(rc):

@@ -41,6 +41,7 @@ static cl_context g_ctx;
 static cl_command_queue g_q;
 static cl_program g_prog;
 static cl_device_id g_dev;
+static char g_bin[1024];  /* the binary g_prog was built from */
 static char g_err[512];
 
 static int fail(const char *fmt, ...) {
@@ -53,9 +54,36 @@ static int fail(const char *fmt, ...) {
 
 const char *hqref_error(void) { return g_err; }
 
-/* The first GPU device of the first platform that has one. */
+/* The context and in-order queue on the first GPU device of the first
+ * platform that has one (once). */
+static int init_context(void) {
+    if (g_ctx) return 0;
+    cl_uint np = 0;
+    cl_platform_id plats[8];
+    if (clGetPlatformIDs(8, plats, &np) != CL_SUCCESS || np == 0) return fail("no OpenCL platform");
+    cl_int e = CL_DEVICE_NOT_FOUND;
+    for (cl_uint i = 0; i < np && e != CL_SUCCESS; ++i) {
+        cl_uint nd = 0;
+        e = clGetDeviceIDs(plats[i], CL_DEVICE_TYPE_GPU, 1, &g_dev, &nd);
+        if (e == CL_SUCCESS && nd == 0) e = CL_DEVICE_NOT_FOUND;
+    }
+    if (e != CL_SUCCESS) return fail("no OpenCL GPU device (%d)", e);
+    cl_context ctx = clCreateContext(NULL, 1, &g_dev, NULL, NULL, &e);
+    if (e != CL_SUCCESS) return fail("clCreateContext %d", e);
+    g_q = clCreateCommandQueue(ctx, g_dev, 0, &e);  /* in-order, as JavaCL's default queue (IM:59) */
+    if (e != CL_SUCCESS) {
+        clReleaseContext(ctx);
+        return fail("clCreateCommandQueue %d", e);
+    }
+    g_ctx = ctx;
+    return 0;
+}
+
+/* The program from binary_path; a different binary than the current one
+ * replaces it (the -DCIE76 and -DCIE94 builds). */
 int hqref_init(const char *binary_path) {
-    if (g_prog) return 0;
+    if (g_prog && strcmp(binary_path, g_bin) == 0) return 0;
+    if (init_context()) return -1;
     FILE *f = fopen(binary_path, "rb");
     if (!f) return fail("cannot open %s", binary_path);
     fseek(f, 0, SEEK_END);
@@ -68,49 +96,26 @@ int hqref_init(const char *binary_path) {
         return fail("cannot read %s", binary_path);
     }
     fclose(f);
-    cl_uint np = 0;
-    cl_platform_id plats[8];
-    if (clGetPlatformIDs(8, plats, &np) != CL_SUCCESS || np == 0) {
-        free(bin);
-        return fail("no OpenCL platform");
-    }
-    cl_int e = CL_DEVICE_NOT_FOUND;
-    for (cl_uint i = 0; i < np && e != CL_SUCCESS; ++i) {
-        cl_uint nd = 0;
-        e = clGetDeviceIDs(plats[i], CL_DEVICE_TYPE_GPU, 1, &g_dev, &nd);
-        if (e == CL_SUCCESS && nd == 0) e = CL_DEVICE_NOT_FOUND;
-    }
-    if (e != CL_SUCCESS) {
-        free(bin);
-        return fail("no OpenCL GPU device (%d)", e);
-    }
-    g_ctx = clCreateContext(NULL, 1, &g_dev, NULL, NULL, &e);
-    if (e != CL_SUCCESS) {
-        free(bin);
-        return fail("clCreateContext %d", e);
-    }
-    g_q = clCreateCommandQueue(g_ctx, g_dev, 0, &e);  /* in-order, as JavaCL's default queue (IM:59) */
-    if (e != CL_SUCCESS) {
-        free(bin);
-        return fail("clCreateCommandQueue %d", e);
+    if (g_prog) {
+        clReleaseProgram(g_prog);
+        g_prog = NULL;
+        g_bin[0] = 0;
     }
     const unsigned char *bp = bin;
     const size_t bl = (size_t)len;
-    cl_int st = 0;
-    g_prog = clCreateProgramWithBinary(g_ctx, 1, &g_dev, &bl, &bp, &st, &e);
+    cl_int st = 0, e = 0;
+    cl_program prog = clCreateProgramWithBinary(g_ctx, 1, &g_dev, &bl, &bp, &st, &e);
     free(bin);
-    if (e != CL_SUCCESS || st != CL_SUCCESS) {
-        g_prog = NULL;
-        return fail("clCreateProgramWithBinary %d / %d", e, st);
-    }
-    e = clBuildProgram(g_prog, 1, &g_dev, "", NULL, NULL);
+    if (e != CL_SUCCESS || st != CL_SUCCESS) return fail("clCreateProgramWithBinary %d / %d", e, st);
+    e = clBuildProgram(prog, 1, &g_dev, "", NULL, NULL);
     if (e != CL_SUCCESS) {
         char log[256] = {0};
-        clGetProgramBuildInfo(g_prog, g_dev, CL_PROGRAM_BUILD_LOG, sizeof log - 1, log, NULL);
-        clReleaseProgram(g_prog);
-        g_prog = NULL;
+        clGetProgramBuildInfo(prog, g_dev, CL_PROGRAM_BUILD_LOG, sizeof log - 1, log, NULL);
+        clReleaseProgram(prog);
         return fail("clBuildProgram %d: %s", e, log);
     }
+    g_prog = prog;
+    snprintf(g_bin, sizeof g_bin, "%s", binary_path);
     return 0;
 }
 

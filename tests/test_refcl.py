@@ -290,3 +290,49 @@ def test_reference_kernels_timed_against_libhq(gpu, refk, filt):
             json.dump(out, f, indent=1)
     print(json.dumps(out))
     assert hq_ms < ref_kernels_ms, out
+
+
+@pytest.mark.parametrize("w,h,dpi,dist", [(256, 256, 72, 45.0), (193, 131, 96, 60.0)])
+def test_de94_matches_reference_kernels(gpu, refk, w, h, dpi, dist):
+    """dE94 (CL:217-226) against the reference's -DCIE94 build (IM:63): per pixel
+    and per palette.  Its dH = sqrt(fma(da, da, db db) - dC dC) has no clamp,
+    so a pixel whose hue difference is within rounding of 0 is NaN, and which
+    pixels those are depends on the last bits of each side's Lab: a NaN pixel on
+    either side must have a float64 dH^2 within rounding of 0; every other pixel
+    agrees within 3e-4; a cost is NaN exactly when one of its pixels is; used
+    flags bit-exact."""
+    from test_gpu import _de94_exact, exact_pixel_err
+
+    f = o.design_filters(dpi, dist)
+    R, G, B = o.synthetic_image(w, h, seed=w + dpi)
+    rgba = o.inline_rgba(R, G, B)
+    lab = refk.srgb_to_scielab(R, G, B, f, w)
+    pals = np.stack([o.synthetic_palette(64, 70 + p) for p in range(2)])
+    refk.use("cie94")
+    try:
+        rc, ru, re = refk.eval_population(rgba, lab, w, pals, f, return_err=True)
+    finally:
+        refk.use("cie76")
+    m = hq.ImageManipulation(hq.deltaETypes.CIE94, device=gpu)
+    hq.ScielabProcessor(dpi, dist, hq.Whitepoint.D65, None, m)
+    m.setOption("pixel_err", 1)
+    m.setImage(rgba.reshape(-1), lab.reshape(-1), w, f.illum)
+    costs, used = m.computeQuantizationErrorPopulation(pals.reshape(2, -1), 2.0, return_used=True)
+    errs = [m.getPixelErrors(p) for p in range(2)]
+    idxs = [m.getIndices(p) for p in range(2)]
+    m.close()
+    np.testing.assert_array_equal(used > 0, ru != 0)
+    n_nan = 0
+    for p in range(2):
+        err, ref = errs[p], re[p]
+        _, dH2, dab2 = _de94_exact(lab, exact_pixel_err(idxs[p], pals[p], lab, f, w, h, lab_only=True))
+        near0 = np.abs(dH2) <= 1e-3 * (np.sqrt(dab2) + 1.0)
+        nan_g, nan_r = np.isnan(err), np.isnan(ref)
+        assert near0[nan_g].all() and near0[nan_r].all()
+        ok = ~(nan_g | nan_r)
+        assert np.abs(err[ok] - ref[ok]).max() <= PIX_ATOL
+        assert np.isnan(costs[p]) == bool(nan_g.any()) and np.isnan(rc[p]) == bool(nan_r.any())
+        if not (nan_g.any() or nan_r.any()):
+            assert abs(costs[p] - rc[p]) <= 1e-6 * rc[p]
+        n_nan += int(nan_g.sum() + nan_r.sum())
+    print(f"dE94 {w}x{h} {dpi}/{dist}: NaN pixels (libhq + reference) {n_nan}")
