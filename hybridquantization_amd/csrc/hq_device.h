@@ -173,7 +173,7 @@ __device__ __forceinline__ int reflect_only(int j, int n) {
 // <).  The kernels rank by d^2 (dist2_rank: the same chain, so the same
 // value) and re-resolve by ref_len any pixel whose runner-up lies within 1e-6
 // relative of its best d^2 or below 2^-125 (near_d2).
-__device__ __noinline__ float ref_len_scaled(float dx, float dy, float dz, float dw, bool small) {
+__device__ __forceinline__ float ref_len_scaled(float dx, float dy, float dz, float dw, bool small) {
     const float s = small ? 0x1p86f : 0x1p-66f;
     const float x = dx * s, y = dy * s, z = dz * s, w = dw * s;
     float e = __builtin_fmaf(w, w, __builtin_fmaf(z, z, __builtin_fmaf(y, y, x * x)));
@@ -209,7 +209,7 @@ __device__ __forceinline__ float dist2_rank(float r, float g, float b, float4 c)
 // up to ~4 ulp apart), or itself below 2^-125 (the rescaled form's distance
 // is not a function of the underflowed d^2).
 __device__ __forceinline__ bool near_d2(float best2, float second2) {
-    return second2 <= fmaxf(best2 * (1.0f + 1e-6f), 0x1p-125f);
+    return second2 <= __builtin_fmaf(best2, 1.0f + 1e-6f, 0x1p-125f);  // (one v_fma, as the plain bound's v_mul)
 }
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));

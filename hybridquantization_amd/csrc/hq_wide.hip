@@ -95,7 +95,7 @@ __global__ __launch_bounds__(256) void assign_wide_kernel(WideArgs a) {
         if (q >= a.n_ext) continue;
         const bool finite = isfinite(r[u]) && isfinite(g[u]) && isfinite(b[u]);
         uint32_t k = bi[u];
-        if (exh || !finite || !(second[u] > fmaxf(best[u] * (1.0f + 1e-6f), 0x1p-125f))) k = argmin_wide_slow(r[u], g[u], b[u], pal, a.K);
+        if (exh || !finite || !(second[u] > __builtin_fmaf(best[u], 1.0f + 1e-6f, 0x1p-125f))) k = argmin_wide_slow(r[u], g[u], b[u], pal, a.K);
         idx[q] = k;
         if (used[k] == 0u) used[k] = 1u;
     }
