@@ -141,3 +141,19 @@ def time_population(rgba4, lab4, w, pals, filt, reps=3):
     _check(lib().hqref_time_population(_p(rgba4), _p(lab4), w, h, _p(pals), P, K, _p(k1), _p(k2), _p(k3), _p(a3),
                                        T, _p(il), int(reps), C.byref(wall), _p(kern, _d)))
     return {"wall_ms": wall.value, "kernel_ms": dict(zip(KERNELS, kern.tolist()))}
+
+
+def compute_error(orig4, quant4, errorImage=None):
+    """IM:858-894 computeError: the CIEDE kernel per pixel, then the host's error
+    image ((255 - e)^2 / 255^2 in channels 0-2, computed in float as Java does)
+    and mean (one sequential double sum)."""
+    orig4, quant4 = _c32(orig4).reshape(-1, 4), _c32(quant4).reshape(-1, 4)
+    n = orig4.shape[0]
+    err = np.zeros(n, np.float32)
+    _check(lib().hqref_compute_error(_p(orig4), _p(quant4), n, _p(err)))
+    if errorImage is not None:
+        v = ((np.float32(255) - err) * (np.float32(255) - err) / np.float32(255 * 255)).astype(np.float32)
+        img = errorImage.reshape(-1, 4)
+        img[:, 0] = img[:, 1] = img[:, 2] = v
+    s = float(np.cumsum(err, dtype=np.float64)[-1]) if n else 0.0  # sequential, as the Java loop
+    return s / n, err

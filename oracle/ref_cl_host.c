@@ -20,6 +20,7 @@
  *                            the mean of the error image, IM:736-768, here one
  *                            sequential double sum, plus delta * #unused, SW:74-82)
  *  - hqref_quantize          IM:770-798  (quantize, CL:147-170)
+ *  - hqref_compute_error     IM:858-884  (CIEDE on two Lab images, CL:201-231)
  * Filters: k1_4 = filters4[0], k2_4 = filters4[1], k3_4 = filters4[2],
  * absk3_4 = absfilters4 (float4 per tap, IM:800-841), k3 = filter3, absk3 =
  * absfilter3 (scalar per tap).  Work sizes: one work item per pixel, local size
@@ -374,5 +375,23 @@ out:
     free(uh);
     free(zero);
     free(ev);
+    return rc;
+}
+
+/* IM:858-884: the CIEDE kernel (CL:201-231) on two inline Lab images; err = the
+ * per-pixel dE it writes (the host's error-image transform and mean, IM:886-893,
+ * are the caller's). */
+int hqref_compute_error(const float *orig4, const float *quant4, int n, float *err) {
+    int rc = 0;
+    cl_int e;
+    cl_mem a = buf(16 * (size_t)n, orig4, &e), b = buf(16 * (size_t)n, quant4, &e), o = buf(4 * (size_t)n, NULL, &e);
+    cl_kernel k = kern("CIEDE", &e);
+    if (e != CL_SUCCESS) { rc = fail("computeError setup %d", e); goto out; }
+    CHK(ARG(k, 0, a)); CHK(ARG(k, 1, b)); CHK(ARG(k, 2, o));
+    if ((rc = run1d(k, (size_t)n))) goto out;
+    CHK(clEnqueueReadBuffer(g_q, o, CL_TRUE, 0, 4 * (size_t)n, err, 0, NULL, NULL));
+out:
+    if (k) clReleaseKernel(k);
+    clReleaseMemObject(a); clReleaseMemObject(b); clReleaseMemObject(o);
     return rc;
 }

@@ -336,3 +336,34 @@ def test_de94_matches_reference_kernels(gpu, refk, w, h, dpi, dist):
             assert abs(costs[p] - rc[p]) <= 1e-6 * rc[p]
         n_nan += int(nan_g.sum() + nan_r.sum())
     print(f"dE94 {w}x{h} {dpi}/{dist}: NaN pixels (libhq + reference) {n_nan}")
+
+
+def test_quantize_and_compute_error_match_reference_kernels(gpu, refk, filt):
+    """The plugin's last two calls (HQ:93-137): quantize (IM:770-798, CL:147-170)
+    with pixels and colours whose .w is not 0 -- the reference's distance() then
+    takes the w term too, and the chosen colour is copied whole -- and
+    computeError (IM:858-894: CIEDE between the original's and the quantized
+    image's S-CIELAB, the host's error image and mean).  Chosen colours and used
+    flags bit-exact; the mean within 1e-6 relative, the error image within 1e-5."""
+    w, h, K = 211, 157, 64
+    rng = np.random.default_rng(31)
+    R, G, B = o.synthetic_image(w, h, seed=5)
+    rgba = o.inline_rgba(R, G, B)
+    rgba[:, 3] = rng.random(w * h, dtype=np.float32)
+    pal = o.synthetic_palette(K, 9)
+    pal[:, 3] = rng.random(K, dtype=np.float32)
+    m = hq.ImageManipulation(device=gpu)
+    q = m.quantize(rgba.reshape(-1), pal.reshape(-1)).reshape(-1, 4)
+    used = m.lastUsedColors.copy()
+    rq, ru = refk.quantize(rgba, pal)
+    np.testing.assert_array_equal(q, rq)
+    np.testing.assert_array_equal(used != 0, ru != 0)
+    lab0 = refk.srgb_to_scielab(R, G, B, filt, w)
+    lab1 = refk.srgb_to_scielab(rq[:, 0], rq[:, 1], rq[:, 2], filt, w)
+    img = np.zeros(4 * w * h, np.float32)
+    mean = m.computeError(lab0.reshape(-1), lab1.reshape(-1), img)
+    m.close()
+    rimg = np.zeros(4 * w * h, np.float32)
+    rmean, _ = refk.compute_error(lab0, lab1, rimg)
+    assert abs(mean - rmean) <= 1e-6 * rmean
+    np.testing.assert_allclose(img.reshape(-1, 4)[:, :3], rimg.reshape(-1, 4)[:, :3], rtol=0, atol=1e-5)
