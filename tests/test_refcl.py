@@ -367,3 +367,31 @@ def test_quantize_and_compute_error_match_reference_kernels(gpu, refk, filt):
     rmean, _ = refk.compute_error(lab0, lab1, rimg)
     assert abs(mean - rmean) <= 1e-6 * rmean
     np.testing.assert_allclose(img.reshape(-1, 4)[:, :3], rimg.reshape(-1, 4)[:, :3], rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("w,h,K,P,imax,seed,t0", [(96, 64, 16, 3, 40, 77, 0.5), (128, 96, 32, 4, 150, 5, 0.05)])
+def test_search_on_reference_kernels_matches_device_search(gpu, refk, filt, w, h, K, P, imax, seed, t0):
+    """The plugin's whole search (IM:383-591 with SW:14-116, restated by
+    oracle.find_best_quantization and checked bit for bit against libhq's native
+    driver by tests/test_capi.py) with every population evaluated by the
+    reference's own kernels (IM:620-727) on the MI355X, against libhq's
+    device-resident search (sa_step_kernel) on its own costs: the same best
+    palette and error -- the costs agree to ~1e-7, so every acceptance
+    decision is the same unless one lands within that of its threshold."""
+    R, G, B = o.synthetic_image(w, h, seed=8)
+    rgba = o.inline_rgba(R, G, B)
+    lab = refk.srgb_to_scielab(R, G, B, filt, w)
+
+    def ref_eval(ps):
+        return list(refk.eval_population(rgba, lab, w, np.stack(ps), filt)[0])
+
+    osw = o.Swasa(o.SwasaParams(population=P, imax=imax, t0=t0), seed)
+    ob, oe = o.find_best_quantization(ref_eval, K, osw)
+    m = _ctx(gpu, rgba, lab, w, filt.illum)
+    m.setOption("sa_device", 1)
+    sw = hq.SWASA(population=P, imax=imax, seed=seed, t0=t0)
+    best = m.findBestQuantization(rgba.reshape(-1), lab.reshape(-1), w, K, sw, None, None, filt.illum)
+    err = m.bestError
+    m.close()
+    assert abs(err - oe) <= 1e-6 * oe
+    np.testing.assert_array_equal(np.asarray(best, np.float32).reshape(K, 4), ob)
