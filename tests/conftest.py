@@ -42,8 +42,15 @@ def gpu():
     if not _gpu_available():
         pytest.fail("gpu test requested but no HIP device / libhq.so")
     # the oracles' argmin distance takes the device's v_sqrt_f32, as the
-    # reference's distance() does on this GPU (oracle/hw_sqrt.py)
+    # reference's distance() does on this GPU (oracle/hw_sqrt.py; built by
+    # build() with the oracle).  Without the helper the oracles keep the
+    # correctly rounded root, and the tests that need the device's fail.
+    import warnings
+
     import hw_sqrt
 
-    hw_sqrt.install()
+    try:
+        hw_sqrt.install()
+    except OSError as e:
+        warnings.warn(f"oracle/libhq_hwsqrt.so not loadable ({e}): the oracles' argmin uses sqrtf")
     return 0
