@@ -216,37 +216,55 @@ def cpu_baseline(args):
             "reference_kernels_on_this_gpu": ref_gpu}
 
 
-def reference_kernels_on_gpu(args, reps=3):
+def reference_kernels_on_gpu(args, reps=3, timeout=180):
     """The reference's own population evaluation on this GPU, same shape: its
     OpenCL kernels (OptimizedConvolution.cl, compiled unmodified for gfx950 into
     oracle/_ref by `make -C oracle ref`) driven in the order of its JavaCL host
     code (IM:620-727, oracle/ref_cl_host.c).  Part of the baseline leg, after
-    the timed region; never fails the run (a missing build or runtime is
-    reported).  The LabRef input is zeros: the reference's work does not depend
-    on its values."""
-    try:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle as o
-        import ref_cl  # the reference's kernels (baseline only)
+    the timed region, in a child process under a time limit (an OpenCL runtime
+    that misbehaves can neither hang nor fail the run: its error is reported).
+    The LabRef input is zeros: the reference's work does not depend on its
+    values."""
+    import subprocess
 
-        R, G, B = synthetic_planes(args.size, args.size, seed=args.seed)
-        rgba = o.inline_rgba(R.ravel(), G.ravel(), B.ravel())
-        del R, G, B
-        pals = np.stack([o.synthetic_palette(args.K, 2 + p) for p in range(args.population)])
-        t = ref_cl.time_population(rgba, np.zeros_like(rgba), args.size, pals, o.design_filters(args.dpi, args.distance),
-                                   reps=reps)
-        px_evals = args.size * args.size * args.population
-        kern_ms = args.population * sum(t["kernel_ms"].values())
-        return {"value": round(px_evals / kern_ms / 1e3, 2), "unit": "Mpixel*evals/s",
-                "wall_value": round(px_evals / t["wall_ms"] / 1e3, 2),
-                "kernel_ms_per_population": round(kern_ms, 4), "wall_ms_per_population": round(t["wall_ms"], 3),
-                "kernel_ms_per_member": {k: round(v, 4) for k, v in t["kernel_ms"].items()},
-                "reps": reps, "kind": "reference",
-                "sample": f"{args.size}x{args.size}, K={args.K}, P={args.population}: the reference's five kernels "
-                          "per member (value: their device time) and its host sequence with the error-image "
-                          "reads and host means (wall_value)"}
+    cmd = [sys.executable, os.path.abspath(__file__), "--ref-kernels-child",
+           json.dumps({"size": args.size, "K": args.K, "P": args.population, "seed": args.seed,
+                       "dpi": args.dpi, "distance": args.distance, "reps": reps})]
+    try:
+        res = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+        lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+        if res.returncode != 0 or not lines:
+            return {"value": None, "error": f"exit {res.returncode}: {res.stderr.strip()[-300:]}"}
+        return json.loads(lines[-1])
+    except subprocess.TimeoutExpired:
+        return {"value": None, "error": f"timed out after {timeout} s"}
     except Exception as e:  # noqa: BLE001 -- a baseline, never the run's outcome
         return {"value": None, "error": f"{type(e).__name__}: {e}"}
+
+
+def _ref_kernels_child(spec):
+    """Child of reference_kernels_on_gpu: prints one JSON object."""
+    c = json.loads(spec)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as o
+    import ref_cl  # the reference's kernels (baseline only)
+
+    R, G, B = synthetic_planes(c["size"], c["size"], seed=c["seed"])
+    rgba = o.inline_rgba(R.ravel(), G.ravel(), B.ravel())
+    del R, G, B
+    pals = np.stack([o.synthetic_palette(c["K"], 2 + p) for p in range(c["P"])])
+    t = ref_cl.time_population(rgba, np.zeros_like(rgba), c["size"], pals, o.design_filters(c["dpi"], c["distance"]),
+                               reps=c["reps"])
+    px_evals = c["size"] * c["size"] * c["P"]
+    kern_ms = c["P"] * sum(t["kernel_ms"].values())
+    print(json.dumps({"value": round(px_evals / kern_ms / 1e3, 2), "unit": "Mpixel*evals/s",
+                      "wall_value": round(px_evals / t["wall_ms"] / 1e3, 2),
+                      "kernel_ms_per_population": round(kern_ms, 4), "wall_ms_per_population": round(t["wall_ms"], 3),
+                      "kernel_ms_per_member": {k: round(v, 4) for k, v in t["kernel_ms"].items()},
+                      "reps": c["reps"], "kind": "reference",
+                      "sample": f"{c['size']}x{c['size']}, K={c['K']}, P={c['P']}: the reference's five kernels per "
+                                "member (value: their device time) and its host sequence with the error-image reads "
+                                "and host means (wall_value)"}))
 
 
 GPU_MODULES = ("torch", "hybridquantization_amd")
@@ -383,6 +401,9 @@ def full_search(lib, _lib, m, K, P, seed, sa_device, restore):
 
 
 def main():
+    if len(sys.argv) == 3 and sys.argv[1] == "--ref-kernels-child":
+        _ref_kernels_child(sys.argv[2])
+        return
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
                     help="GPUs (ranks) of this node; default WORLD_SIZE or 1.  N > 1 with WORLD_SIZE unset: "

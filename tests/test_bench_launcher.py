@@ -69,3 +69,17 @@ def test_launcher_module_has_no_gpu_imports():
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert r.stdout.strip() == "[]"
+
+
+def test_reference_baseline_never_fails_the_run():
+    """bench.py's timing of the reference's own kernels runs in a child process
+    under a time limit; without a GPU (or without the build) it reports an
+    error in the line instead of raising."""
+    import argparse
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    args = argparse.Namespace(size=64, K=16, population=2, seed=1, dpi=72, distance=45.0)
+    out = bench.reference_kernels_on_gpu(args, reps=1, timeout=120)
+    assert out["value"] is None and out["error"]
