@@ -665,6 +665,21 @@ __device__ __forceinline__ void drop_positions(uint32_t (&w)[4], int& n, uint32_
     }
 }
 
+#ifdef HQ_GRID_TIMING
+// diagnostic build: per workgroup start, end, the phase ends (level-1 list,
+// pass 1, pass 2, dominance, long lists; wall_clock64 ticks) and the level-1
+// list length | long-list count << 16
+constexpr int kGridStamps = 65536;
+__device__ unsigned long long g_grid_t[kGridStamps][8];
+#define HQ_GT_STAMP(i, v)                                                                   \
+    do {                                                                                    \
+        if (threadIdx.x == 0 && blockIdx.y * gridDim.x + blockIdx.x < (unsigned)kGridStamps) \
+            g_grid_t[blockIdx.y * gridDim.x + blockIdx.x][i] = (v);                         \
+    } while (0)
+#else
+#define HQ_GT_STAMP(i, v) ((void)0)
+#endif
+
 // LDS of one level-1 cell's grid work.
 struct GridLds {
     float4 col[kMaxK];
@@ -717,6 +732,7 @@ __device__ __forceinline__ void grid_cell_body(const GridArgs& a, int p, int cel
     const int total = exh ? 0 : s_wcount[0] + s_wcount[1] + s_wcount[2] + s_wcount[3];
     if (cand) s_list[base + __popcll(bal & ((1ull << lane) - 1ull))] = (uint8_t)tid;
     __syncthreads();
+    HQ_GT_STAMP(2, wall_clock64());
 
     uint8_t* l1 = a.lvl1 + (int64_t)p * a.lvl1_pitch + (int64_t)cell * 32;
     const bool ovf1 = exh || total > kL1Cap;
@@ -757,6 +773,7 @@ __device__ __forceinline__ void grid_cell_body(const GridArgs& a, int p, int cel
     const float thr = t2 * HQ_CAND_MARGIN;
     const int bstar = total > 0 ? (int)s_list[t2pos] : 0;
     __syncthreads();
+    HQ_GT_STAMP(3, wall_clock64());
     axis_terms<false>(s_ax, s_col, s_list, total, ci, cj, ck, inv2);
     __syncthreads();
     // pass 2, 32 positions at a time: candidate mask, ranks in list order
@@ -789,6 +806,7 @@ __device__ __forceinline__ void grid_cell_body(const GridArgs& a, int p, int cel
         w[k] |= (uint32_t)__shfl_xor((int)w[k], 1, 64);
         w[k] |= (uint32_t)__shfl_xor((int)w[k], 2, 64);
     }
+    HQ_GT_STAMP(4, wall_clock64());
     // Dominance pruning (exact).  Candidate a of the child's list is dropped
     // when b* -- the colour attaining T2, the child's nearest in the worst
     // case -- is nearer than a to EVERY point of the child box by a margin:
@@ -812,6 +830,7 @@ __device__ __forceinline__ void grid_cell_body(const GridArgs& a, int p, int cel
         const float bhi[3] = {blo[0] + inv2, blo[1] + inv2, blo[2] + inv2};
         prune_dominated(w, n, s_col, bstar, blo, bhi, q);
     }
+    HQ_GT_STAMP(5, wall_clock64());
     if constexpr (kL2Cap < kL2Build) {
         const bool lng = !exh && n > kL2Cap && n <= kL2Build;  // quad-uniform
         int slot = 0;
@@ -825,12 +844,14 @@ __device__ __forceinline__ void grid_cell_body(const GridArgs& a, int p, int cel
         }
         __syncthreads();
         const int nl = s_long.count;
+        HQ_GT_STAMP(7, (unsigned long long)total | ((unsigned long long)nl << 16));
         if (nl > 0) {  // workgroup-uniform
             prune_long_lists(s_long, s_col, nl, ci, cj, ck, inv2);
             __syncthreads();
             slot = __shfl(slot, (int)(threadIdx.x & 60), 64);
             if (lng) drop_positions(w, n, s_long.drop[slot]);
         }
+        HQ_GT_STAMP(6, wall_clock64());
     }
 #endif
     if (q == 0) {
@@ -846,10 +867,6 @@ __device__ __forceinline__ void grid_cell_body(const GridArgs& a, int p, int cel
     }
 }
 
-#ifdef HQ_GRID_TIMING
-constexpr int kGridStamps = 65536;
-__device__ unsigned long long g_grid_t[kGridStamps][2];  // per workgroup: start, end (wall_clock64 ticks)
-#endif
 
 __global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
     const int p = blockIdx.y, tid = threadIdx.x;
@@ -871,10 +888,8 @@ __global__ __launch_bounds__(256) void build_grid_kernel(GridArgs a) {
     grid_cell_body(a, p, blockIdx.x, c, valid, exh, L);
 #ifdef HQ_GRID_TIMING
     __syncthreads();
-    if (tid == 0 && p * (int)gridDim.x + (int)blockIdx.x < kGridStamps) {
-        g_grid_t[p * gridDim.x + blockIdx.x][0] = t_start;
-        g_grid_t[p * gridDim.x + blockIdx.x][1] = wall_clock64();
-    }
+    HQ_GT_STAMP(0, t_start);
+    HQ_GT_STAMP(1, wall_clock64());
 #endif
 }
 // ----------------------------------------------------------------------------
@@ -946,6 +961,6 @@ hipError_t launch_finalize(const FinalizeArgs& a, int P, hipStream_t s) {
 // diagnostic build only: the last build_grid launch's workgroup stamps
 extern "C" int hq_debug_grid_stamps(unsigned long long* out, int n) {
     n = n < hq::kGridStamps ? n : hq::kGridStamps;
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(hq::g_grid_t), sizeof(unsigned long long) * 2 * (size_t)n);
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(hq::g_grid_t), sizeof(unsigned long long) * 8 * (size_t)n);
 }
 #endif

@@ -27,12 +27,12 @@ if len(sys.argv) > 1 and sys.argv[1] == "run":
         m.computeQuantizationErrorPopulation(pal.reshape(4, -1), 2.0)
     import ctypes as C
     n = 4 * 512
-    buf = np.zeros((n, 2), np.uint64)
+    buf = np.zeros((n, 8), np.uint64)
     lib.hq_debug_grid_stamps.argtypes = [C.c_void_p, C.c_int]
     lib.hq_debug_grid_stamps(buf.ctypes.data, n)
     m.close()
     for i, r in enumerate(buf):
-        print("GRID_T %d %d %d %d" % (i // 512, i % 512, int(r[0]), int(r[1])))
+        print("GRID_T %d %d %s" % (i // 512, i % 512, " ".join(str(int(x)) for x in r)))
     sys.exit(0)
 res = subprocess.run([sys.executable, __file__, "run"], capture_output=True, text=True, timeout=300)
 last = [l.split() for l in res.stdout.splitlines() if l.startswith("GRID_T")]
@@ -47,3 +47,23 @@ print(f"{len(last)} workgroups; start spread {starts[-1]:.2f} us (50% by {starts
       f"end {max((e - t0) / 100.0 for e in en):.2f} us")
 print("duration us: min %.2f med %.2f p90 %.2f max %.2f" % (durs[0], durs[len(durs) // 2],
                                                            durs[int(len(durs) * 0.9)], durs[-1]))
+# phases (stamps 2..6: level-1 list, pass 1, pass 2, dominance, long lists) of the
+# slowest 5% of workgroups against the median ones, and their level-1 list lengths
+rows = []
+for x in last:
+    v = [int(t) for t in x[3:11]]
+    if len(v) < 8 or v[6] == 0:
+        continue
+    ph = [(v[2] - v[0]) / 100.0, (v[3] - v[2]) / 100.0, (v[4] - v[3]) / 100.0, (v[5] - v[4]) / 100.0,
+          (v[6] - v[5]) / 100.0, (v[1] - v[6]) / 100.0]
+    rows.append(((v[1] - v[0]) / 100.0, ph, v[7] & 0xFFFF, v[7] >> 16))
+rows.sort(key=lambda r: r[0])
+if rows:
+    def summ(sel, name):
+        import statistics as st
+        print(f"{name} ({len(sel)} wg): dur {st.mean(r[0] for r in sel):.2f} us; phases l1/pass1/pass2/dom/long/tail "
+              + " ".join(f"{st.mean(r[1][k] for r in sel):.2f}" for k in range(6))
+              + f"; level-1 list {st.mean(r[2] for r in sel):.1f}; long lists {st.mean(r[3] for r in sel):.2f}")
+    n = len(rows)
+    summ(rows[int(n * 0.45):int(n * 0.55)], "median")
+    summ(rows[int(n * 0.95):], "slowest 5%")
