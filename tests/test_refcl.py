@@ -71,13 +71,18 @@ def test_labref_matches_reference_kernels(gpu, refk, filt, w, h):
 
 
 @pytest.mark.parametrize("w,h,K,P", [(256, 256, 16, 4), (97, 53, 64, 2), (333, 217, 256, 3), (1024, 512, 256, 2),
-                                     (320, 200, 600, 2), (320, 200, 2048, 1)])
+                                     (320, 200, 600, 2), (320, 200, 2048, 1), (128, 96, 4096, 2),
+                                     (96, 64, 20000, 1), (10, 10, 16, 2), (11, 37, 5, 3), (64, 48, 1, 2),
+                                     (64, 48, 2, 2)])
 def test_costs_match_reference_kernels(gpu, refk, filt, w, h, K, P):
     """computeQuantizationErrorPopulation on the reference's kernels (IM:620-727)
     against libhq's evaluation and the C oracle's, on the same LabRef (the
     reference's): costs, used flags, the per-pixel dE of palette 0, and the
     chosen colours (the reference's quantize kernel) -- at C1 (256^2, K = 16, P =
-    4), K = 256 on ragged images, and chunked palettes (K = 600, 2048)."""
+    4), K = 256 on ragged images, chunked palettes (K = 600, 2048), native 16-bit
+    lists (K = 4096), the exhaustive 32-bit path (K = 20000 > 16384), images as
+    small as the stencil's half-width (10 x 10, 11 x 37: reflection at both
+    edges of every row and column), and K = 1, 2, 5."""
     R, G, B = o.synthetic_image(w, h, seed=3 * w + K)
     rgba = o.inline_rgba(R, G, B)
     lab = refk.srgb_to_scielab(R, G, B, filt, w)
