@@ -105,10 +105,17 @@ def test_costs_match_reference_kernels(gpu, refk, filt, w, h, K, P):
     assert np.abs(parts["err"] - re[0]).max() <= PIX_ATOL
 
 
-@pytest.mark.parametrize("dpi,dist", [(96, 60.0), (150, 30.0), (300, 50.0)])
+@pytest.mark.parametrize("dpi,dist", [(96, 60.0), (150, 30.0), (200, 30.0), (72, 30.0), (300, 50.0), (300, 100.0)])
 def test_viewing_geometries_match_reference_kernels(gpu, refk, dpi, dist):
-    """Other viewing geometries (HQ:229-231): halfSize 19 and 15 (the tiled
-    kernel's larger tap buckets) and 51 (the generic matrix-core pair)."""
+    """Other viewing geometries (HQ:229-231): halfSize 19, 15, 20 and 7 (the
+    tiled kernel's 19-, 15-, 24- and 10-tap buckets), 51 (the generic
+    matrix-core pair) and 102 (205 taps: the generic fp32 pair).  Up to 103
+    taps the costs agree within 1e-6 and every pixel within 3e-4; at 205 taps
+    two fp32 orders of each pixel's 2 x 205-tap sums drift further apart, so
+    the costs are held to 1e-5 and to a float64 evaluation of the same inputs:
+    libhq no further from it than the reference (x 1.5)."""
+    from test_gpu import exact_pixel_err
+
     f = o.design_filters(dpi, dist)
     w, h, K, P = 301, 173, 64, 2
     R, G, B = o.synthetic_image(w, h, seed=dpi)
@@ -122,11 +129,22 @@ def test_viewing_geometries_match_reference_kernels(gpu, refk, dpi, dist):
     m = _ctx(gpu, rgba, lab, w, f.illum, dpi=dpi, dist=dist, pixel_err=1)
     costs, used = m.computeQuantizationErrorPopulation(pals.reshape(P, -1), 2.0, return_used=True)
     pe = [m.getPixelErrors(p) for p in range(P)]
+    idx = [m.getIndices(p) for p in range(P)]
     m.close()
-    np.testing.assert_allclose(costs, rc, rtol=1e-6)
     np.testing.assert_array_equal(used > 0, ru != 0)
+    if f.half <= 64:
+        np.testing.assert_allclose(costs, rc, rtol=1e-6)
+        for p in range(P):
+            assert np.abs(pe[p] - re[p]).max() <= PIX_ATOL
+        return
+    np.testing.assert_allclose(costs, rc, rtol=1e-5)
     for p in range(P):
-        assert np.abs(pe[p] - re[p]).max() <= PIX_ATOL
+        ex = exact_pixel_err(idx[p], pals[p], lab, f, w, h)
+        assert np.abs(pe[p] - re[p]).max() <= 10 * PIX_ATOL
+        d_hq, d_ref = abs(float(np.mean(pe[p], dtype=np.float64)) - float(np.mean(ex))), \
+            abs(float(np.mean(re[p], dtype=np.float64)) - float(np.mean(ex)))
+        print(f"{dpi}/{dist} palette {p}: |mean - float64| libhq {d_hq:.3g} reference {d_ref:.3g}")
+        assert d_hq <= 1.5 * d_ref + 1e-7
 
 
 def _adversarial(G2=32):
