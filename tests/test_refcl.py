@@ -273,27 +273,30 @@ def test_config3_4096_matches_reference_kernels(gpu, refk, filt):
     np.testing.assert_array_equal(pals[0][idx0], q)
 
 
-def test_reference_kernels_timed_against_libhq(gpu, refk, filt):
+@pytest.mark.parametrize("name,size,K,P,dpi,dist", [("C3", 4096, 256, 4, 72, 45.0), ("C1", 256, 16, 4, 72, 45.0),
+                                                     ("C2", 1024, 64, 1, 72, 45.0), ("C5", 4096, 256, 64, 72, 45.0),
+                                                     ("C3 at 96 dpi / 60 cm", 4096, 256, 4, 96, 60.0)])
+def test_reference_kernels_timed_against_libhq(gpu, refk, name, size, K, P, dpi, dist):
     """The reference's own population evaluation on this MI355X (its five kernels per
-    member, IM:620-727) beside libhq's, at BASELINE config 3 (4096^2, K = 256, P = 4):
-    the same work, the same inputs.  libhq's population (one call through the C ABI,
-    costs read back) must take less time than the reference's kernels alone.  With
-    HQ_REFCL_TIMING_OUT set, the numbers are written there as JSON."""
+    member, IM:620-727) beside libhq's, at the BASELINE configs' shapes: the same
+    work, the same inputs.  libhq's population (one call through the C ABI, costs
+    read back) must take less time than the reference's kernels alone.  With
+    HQ_REFCL_TIMING_OUT set, one JSON line per config is appended there."""
     import json
     import time
 
-    w = h = 4096
-    P, K = 4, 256
+    filt = o.design_filters(dpi, dist)
+    w = h = size
     R, G, B = o.synthetic_image(w, h, seed=1)
     rgba = o.inline_rgba(R, G, B)
     lab = refk.srgb_to_scielab(R, G, B, filt, w)
     pals = np.stack([o.synthetic_palette(K, 2 + p) for p in range(P)])
-    ref = refk.time_population(rgba, lab, w, pals, filt, reps=3)
+    ref = refk.time_population(rgba, lab, w, pals, filt, reps=2 if P > 8 else 3)
     ref_kernels_ms = P * sum(ref["kernel_ms"].values())
-    m = _ctx(gpu, rgba, lab, w, filt.illum)
+    m = _ctx(gpu, rgba, lab, w, filt.illum, dpi=dpi, dist=dist)
     flat = pals.reshape(P, -1)
     m.computeQuantizationErrorPopulation(flat, 2.0)
-    reps = 20
+    reps = 5 if P > 8 else 20
     t0 = time.perf_counter()
     for _ in range(reps):
         m.computeQuantizationErrorPopulation(flat, 2.0)
@@ -301,7 +304,8 @@ def test_reference_kernels_timed_against_libhq(gpu, refk, filt):
     m.close()
     px_evals = w * h * P
     out = {
-        "config": {"workload": "C3 population evaluation", "size": w, "K": K, "P": P, "halfSize": 10},
+        "config": {"workload": f"{name} population evaluation", "size": w, "K": K, "P": P, "dpi": dpi,
+                   "distance_cm": dist, "halfSize": filt.half},
         "reference_opencl_on_mi355x": {
             "wall_ms_per_population": ref["wall_ms"],
             "kernel_ms_per_member": ref["kernel_ms"],
@@ -309,14 +313,15 @@ def test_reference_kernels_timed_against_libhq(gpu, refk, filt):
             "mpx_evals_per_s_kernels": px_evals / ref_kernels_ms / 1e3,
             "mpx_evals_per_s_wall": px_evals / ref["wall_ms"] / 1e3,
         },
-        "libhq": {"ms_per_population": hq_ms, "mpx_evals_per_s": px_evals / hq_ms / 1e3},
+        "libhq": {"ms_per_population": hq_ms, "mpx_evals_per_s": px_evals / hq_ms / 1e3,
+                  "note": "one hq_eval_population call through the C ABI, costs read back (host API)"},
         "speedup_vs_reference_kernels": ref_kernels_ms / hq_ms,
         "speedup_vs_reference_wall": ref["wall_ms"] / hq_ms,
     }
     path = os.environ.get("HQ_REFCL_TIMING_OUT")
     if path:
-        with open(path, "w") as f:
-            json.dump(out, f, indent=1)
+        with open(path, "a") as f:
+            f.write(json.dumps(out) + "\n")
     print(json.dumps(out))
     assert hq_ms < ref_kernels_ms, out
 
