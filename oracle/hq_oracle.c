@@ -110,13 +110,16 @@ static void parallel_for(int n, int nthreads, range_fn fn, void *arg) {
 /* ------------------------------------------------------------------------ */
 typedef float (*hqo_sqrt_fn)(float);
 static hqo_sqrt_fn g_sqrt = NULL;
-static long long g_sqrt_calls = 0;  /* (not atomic: a diagnostic count) */
+static long long g_sqrt_calls = 0;  /* calls of g_sqrt (the worker threads add atomically) */
 
 void hqo_set_sqrt(hqo_sqrt_fn f) { g_sqrt = f; }
-long long hqo_sqrt_calls(void) { return g_sqrt_calls; }
+long long hqo_sqrt_calls(void) { return __atomic_load_n(&g_sqrt_calls, __ATOMIC_RELAXED); }
 
 static inline float dev_sqrt(float x) {
-    if (g_sqrt) { ++g_sqrt_calls; return g_sqrt(x); }
+    if (g_sqrt) {
+        __atomic_fetch_add(&g_sqrt_calls, 1, __ATOMIC_RELAXED);
+        return g_sqrt(x);
+    }
     return sqrtf(x);
 }
 

@@ -121,12 +121,26 @@ int hqref_init(const char *binary_path) {
 }
 
 /* ---- small helpers ---- */
+/* Buffer and kernel creation keep the first error in *e (sticky: a later
+ * success does not hide an earlier failure; *e starts at CL_SUCCESS). */
 static cl_mem buf(size_t bytes, const void *src, cl_int *e) {
-    return clCreateBuffer(g_ctx, CL_MEM_READ_WRITE | (src ? CL_MEM_COPY_HOST_PTR : 0), bytes ? bytes : 4,
-                          (void *)src, e);
+    cl_int r = CL_SUCCESS;
+    cl_mem m = clCreateBuffer(g_ctx, CL_MEM_READ_WRITE | (src ? CL_MEM_COPY_HOST_PTR : 0), bytes ? bytes : 4,
+                              (void *)src, &r);
+    if (*e == CL_SUCCESS) *e = r;
+    return r == CL_SUCCESS ? m : NULL;
 }
 
-static cl_kernel kern(const char *name, cl_int *e) { return clCreateKernel(g_prog, name, e); }
+static cl_kernel kern(const char *name, cl_int *e) {
+    cl_int r = CL_SUCCESS;
+    cl_kernel k = clCreateKernel(g_prog, name, &r);
+    if (*e == CL_SUCCESS) *e = r;
+    return r == CL_SUCCESS ? k : NULL;
+}
+
+static void release_mem(cl_mem m) {
+    if (m) clReleaseMemObject(m);
+}
 
 static int run1d(cl_kernel k, size_t n) {
     const cl_int e = clEnqueueNDRangeKernel(g_q, k, 1, NULL, &n, NULL, 0, NULL, NULL);
@@ -142,7 +156,7 @@ static int run1d(cl_kernel k, size_t n) {
 /* IM:100-153: planar R, G, B -> inline XYZ (CL:79-90). */
 int hqref_rgb_to_xyz(const float *R, const float *G, const float *B, int n, float *xyz4) {
     int rc = 0;
-    cl_int e;
+    cl_int e = CL_SUCCESS;
     cl_mem r = buf(4 * (size_t)n, R, &e), g = buf(4 * (size_t)n, G, &e), b = buf(4 * (size_t)n, B, &e),
            o = buf(16 * (size_t)n, NULL, &e);
     cl_kernel k = kern("RGB2XYZ", &e);
@@ -152,7 +166,7 @@ int hqref_rgb_to_xyz(const float *R, const float *G, const float *B, int n, floa
     CHK(clEnqueueReadBuffer(g_q, o, CL_TRUE, 0, 16 * (size_t)n, xyz4, 0, NULL, NULL));
 out:
     if (k) clReleaseKernel(k);
-    clReleaseMemObject(r); clReleaseMemObject(g); clReleaseMemObject(b); clReleaseMemObject(o);
+    release_mem(r); release_mem(g); release_mem(b); release_mem(o);
     return rc;
 }
 
@@ -160,7 +174,7 @@ out:
 int hqref_xyz_to_scielab(const float *xyz4, int w, int h, const float *k1_4, const float *k2_4,
                          const float *k3_4, const float *absk3_4, int taps, const float *illum, float *lab4) {
     int rc = 0;
-    cl_int e;
+    cl_int e = CL_SUCCESS;
     const size_t n = (size_t)w * h, fb = 16 * (size_t)taps;
     const int half = (4 * taps) / 8;  /* IM:299 filters4[0].length / 8 */
     cl_mem in = buf(16 * n, xyz4, &e), opp = buf(16 * n, NULL, &e), conv = buf(16 * n, NULL, &e),
@@ -193,9 +207,9 @@ out:
     if (c4) clReleaseKernel(c4);
     if (c1) clReleaseKernel(c1);
     if (kl) clReleaseKernel(kl);
-    clReleaseMemObject(in); clReleaseMemObject(opp); clReleaseMemObject(conv); clReleaseMemObject(tmp);
-    clReleaseMemObject(lab); clReleaseMemObject(f1); clReleaseMemObject(f2); clReleaseMemObject(f3);
-    clReleaseMemObject(fa);
+    release_mem(in); release_mem(opp); release_mem(conv); release_mem(tmp);
+    release_mem(lab); release_mem(f1); release_mem(f2); release_mem(f3);
+    release_mem(fa);
     return rc;
 }
 
@@ -206,7 +220,7 @@ int hqref_eval_population(const float *rgba4, const float *lab4, int w, int h, c
                           const float *k1_4, const float *k2_4, const float *k3, const float *absk3, int taps,
                           const float *illum, float delta, double *costs, int32_t *used, float *err) {
     int rc = 0;
-    cl_int e;
+    cl_int e = CL_SUCCESS;
     const size_t n = (size_t)w * h;
     const int half = (4 * taps) / 8;  /* IM:408 */
     float *errh = (float *)malloc(4 * n);
@@ -264,7 +278,7 @@ out:
 /* IM:770-798: the chosen colour of every pixel (CL:147-170) and the used flags. */
 int hqref_quantize(const float *rgba4, int n, const float *pal4, int K, float *out4, int32_t *used) {
     int rc = 0;
-    cl_int e;
+    cl_int e = CL_SUCCESS;
     int32_t *uh = (int32_t *)calloc((size_t)K, 4);
     cl_mem in = buf(16 * (size_t)n, rgba4, &e), col = buf(16 * (size_t)K, pal4, &e),
            u = buf(4 * (size_t)K, uh, &e), o = buf(16 * (size_t)n, NULL, &e);
@@ -276,7 +290,7 @@ int hqref_quantize(const float *rgba4, int n, const float *pal4, int K, float *o
     CHK(clEnqueueReadBuffer(g_q, u, CL_TRUE, 0, 4 * (size_t)K, used ? used : uh, 0, NULL, NULL));
 out:
     if (k) clReleaseKernel(k);
-    clReleaseMemObject(in); clReleaseMemObject(col); clReleaseMemObject(u); clReleaseMemObject(o);
+    release_mem(in); release_mem(col); release_mem(u); release_mem(o);
     free(uh);
     return rc;
 }
@@ -301,7 +315,7 @@ int hqref_time_population(const float *rgba4, const float *lab4, int w, int h, c
                           const float *k1_4, const float *k2_4, const float *k3, const float *absk3, int taps,
                           const float *illum, int reps, double *wall_ms, double *kern_ms) {
     int rc = 0;
-    cl_int e;
+    cl_int e = CL_SUCCESS;
     const size_t n = (size_t)w * h;
     const int half = (4 * taps) / 8;
     cl_command_queue q = clCreateCommandQueue(g_ctx, g_dev, CL_QUEUE_PROFILING_ENABLE, &e);
@@ -383,7 +397,7 @@ out:
  * are the caller's). */
 int hqref_compute_error(const float *orig4, const float *quant4, int n, float *err) {
     int rc = 0;
-    cl_int e;
+    cl_int e = CL_SUCCESS;
     cl_mem a = buf(16 * (size_t)n, orig4, &e), b = buf(16 * (size_t)n, quant4, &e), o = buf(4 * (size_t)n, NULL, &e);
     cl_kernel k = kern("CIEDE", &e);
     if (e != CL_SUCCESS) { rc = fail("computeError setup %d", e); goto out; }
@@ -392,6 +406,6 @@ int hqref_compute_error(const float *orig4, const float *quant4, int n, float *e
     CHK(clEnqueueReadBuffer(g_q, o, CL_TRUE, 0, 4 * (size_t)n, err, 0, NULL, NULL));
 out:
     if (k) clReleaseKernel(k);
-    clReleaseMemObject(a); clReleaseMemObject(b); clReleaseMemObject(o);
+    release_mem(a); release_mem(b); release_mem(o);
     return rc;
 }

@@ -429,3 +429,37 @@ def test_search_on_reference_kernels_matches_device_search(gpu, refk, filt, w, h
     m.close()
     assert abs(err - oe) <= 1e-6 * oe
     np.testing.assert_array_equal(np.asarray(best, np.float32).reshape(K, 4), ob)
+
+
+def test_compute_error_de94_matches_reference_kernels(gpu, refk, filt):
+    """computeError (IM:858-894) with dE94: the reference's -DCIE94 CIEDE kernel
+    against libhq's.  Its unclamped dH (CL:222) is NaN where the hue difference
+    is within rounding of 0; the two sides may disagree on which of those
+    pixels turn NaN (last bits), so: the finite pixels agree within 1e-4, and
+    NaN pixels are rare on both sides (< 2e-3) and the mean is NaN exactly when
+    a pixel is."""
+    w, h, K = 160, 120, 32
+    R, G, B = o.synthetic_image(w, h, seed=12)
+    rgba = o.inline_rgba(R, G, B)
+    pal = o.synthetic_palette(K, 13)
+    rq, _ = refk.quantize(rgba, pal)
+    lab0 = refk.srgb_to_scielab(R, G, B, filt, w)
+    lab1 = refk.srgb_to_scielab(rq[:, 0], rq[:, 1], rq[:, 2], filt, w)
+    refk.use("cie94")
+    try:
+        rmean, rerr = refk.compute_error(lab0, lab1)
+    finally:
+        refk.use("cie76")
+    m = hq.ImageManipulation(hq.deltaETypes.CIE94, device=gpu)
+    img = np.zeros(4 * w * h, np.float32)
+    mean = m.computeError(lab0.reshape(-1), lab1.reshape(-1), img)
+    m.close()
+    e = np.float32(255) - np.sqrt(img.reshape(-1, 4)[:, 0].astype(np.float64) * (255.0 * 255.0))  # back from (255 - e)^2 / 255^2
+    nan_r = np.isnan(rerr)
+    nan_g = np.isnan(img.reshape(-1, 4)[:, 0])
+    assert nan_r.mean() < 2e-3 and nan_g.mean() < 2e-3
+    ok = ~(nan_r | nan_g)
+    assert np.abs(e[ok] - rerr[ok]).max() <= 1e-3
+    assert np.isnan(mean) == bool(nan_g.any()) and np.isnan(rmean) == bool(nan_r.any())
+    if not (nan_g.any() or nan_r.any()):
+        assert abs(mean - rmean) <= 1e-6 * rmean
